@@ -1,0 +1,201 @@
+"""ctypes binding of the C-ABI in include/dbindex_hip.h (libdbindex_hip.so).
+
+This is the Python twin of the JNI shim described in INTEGRATION.md: every
+symbol is bound with its exact C signature.  There is no fallback path — if
+the in-tree HIP library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+from .params import DbiParams
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdbindex_hip.so")
+
+DBI_OK, DBI_E_INVALID, DBI_E_OOM, DBI_E_HIP, DBI_E_RCCL, DBI_E_STATE = 0, -1, -2, -3, -4, -5
+FILTER_INCLUDE, FILTER_SKIP, FILTER_SKIP_PROTEIN_START = 0, 1, 2
+ERROR_NAMES = {-1: "DBI_E_INVALID", -2: "DBI_E_OOM", -3: "DBI_E_HIP", -4: "DBI_E_RCCL", -5: "DBI_E_STATE"}
+
+
+class DBIndexStoreException(Exception):
+    """Mirror of edu.scripps.yates.utilities.fasta.dbindex.DBIndexStoreException:
+    every non-zero status of the C-ABI is raised, never swallowed."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class DbiStats(ctypes.Structure):
+    _fields_ = [
+        ("n_residues", c_uint64), ("n_proteins", c_uint64), ("n_total", c_uint64),
+        ("n_dropped", c_uint64), ("n_kept", c_uint64), ("n_unique", c_uint64),
+        ("n_keys", c_uint64), ("n_bins", c_uint64), ("n_big_bins", c_uint64),
+        ("device_bytes", c_uint64), ("build_ms", c_double), ("digest_ms", c_double),
+    ]
+
+
+class DbiQueryResult(ctypes.Structure):
+    _fields_ = [("nq", c_uint64), ("n_hits", c_uint64), ("row_ptr", POINTER(c_uint64)),
+                ("ids", POINTER(c_uint64))]
+
+
+class DbiDeviceIndex(ctypes.Structure):
+    _fields_ = [("mass", c_void_p), ("prot_id", c_void_p), ("offset", c_void_p), ("length", c_void_p),
+                ("occ_off", c_void_p), ("occ_prot", c_void_p), ("n_unique", c_uint64),
+                ("n_kept", c_uint64)]
+
+
+class DbiSeqList(ctypes.Structure):
+    _fields_ = [
+        ("n", c_uint64), ("mass", POINTER(c_double)), ("seq_off", POINTER(c_uint64)),
+        ("seq_chars", c_void_p), ("res_left", c_void_p), ("res_right", c_void_p),
+        ("prot_off", POINTER(c_uint64)), ("prot_ids", POINTER(c_uint32)),
+        ("offset", POINTER(c_uint32)), ("length", POINTER(c_uint32)), ("unique_id", POINTER(c_uint64)),
+    ]
+
+
+# (name, restype, argtypes) for every exported symbol of include/dbindex_hip.h
+P = c_void_p
+SIGNATURES = [
+    ("dbi_params_default", None, [POINTER(DbiParams), c_int32, c_int32]),
+    ("dbi_open", c_int, [POINTER(DbiParams), c_int, POINTER(c_void_p)]),
+    ("dbi_close", None, [P]),
+    ("dbi_build", c_int, [P, P, c_uint64, P, c_uint64]),
+    ("dbi_build_device", c_int, [P, P, c_uint64, P, c_uint64, P]),
+    ("dbi_build_occurrences", c_int, [P, P, c_uint64, P, c_uint64, P, P, P, P, c_uint64, c_uint64]),
+    ("dbi_stats_get", c_int, [P, POINTER(DbiStats)]),
+    ("dbi_query", c_int, [P, P, P, c_uint64, P, P]),
+    ("dbi_query_device", c_int, [P, P, P, c_uint64, P, P, P]),
+    ("dbi_query_csr", c_int, [P, P, P, c_uint64, POINTER(POINTER(DbiQueryResult))]),
+    ("dbi_query_result_free", None, [POINTER(DbiQueryResult)]),
+    ("dbi_peptides", c_int, [P, P, c_uint64, P, P, P, P, P, P]),
+    ("dbi_occurrences", c_int, [P, c_uint64, c_uint64, P]),
+    ("dbi_export", c_int, [P, P, P, P, P, P, P]),
+    ("dbi_entry_keys", c_int, [P, P, c_uint64, POINTER(c_uint64)]),
+    ("dbi_device_view", c_int, [P, POINTER(DbiDeviceIndex)]),
+    ("dbi_stage_times", c_int, [P, P, P, P, c_uint64, POINTER(c_uint64)]),
+    ("dbi_store_create", c_int, [POINTER(DbiParams), c_int, POINTER(c_void_p)]),
+    ("dbi_store_close", None, [P]),
+    ("dbi_store_set_device_digest", c_int, [P, c_int]),
+    ("dbi_store_init", c_int, [P, c_char_p]),
+    ("dbi_store_start_add_seq", c_int, [P]),
+    ("dbi_store_stop_add_seq", c_int, [P]),
+    ("dbi_store_index_exists", c_int, [P, POINTER(c_int)]),
+    ("dbi_store_add_protein_def", c_int, [P, c_int64, c_char_p, c_char_p, c_uint64, POINTER(c_int64)]),
+    ("dbi_store_filter_sequence", c_int, [P, c_double, c_char_p, c_uint64, POINTER(c_int)]),
+    ("dbi_store_add_sequence", c_int, [P, c_double, c_int32, c_int32, c_int64]),
+    ("dbi_store_get_number_sequences", c_int, [P, POINTER(c_int64)]),
+    ("dbi_store_get_total_seq_count", c_int, [P, POINTER(c_int64)]),
+    ("dbi_store_get_entry_keys", c_int, [P, P, c_uint64, POINTER(c_uint64)]),
+    ("dbi_store_engine", c_void_p, [P]),
+    ("dbi_store_get_sequences", c_int, [P, c_double, c_double, POINTER(POINTER(DbiSeqList))]),
+    ("dbi_store_get_sequences_ranges", c_int, [P, P, P, c_uint64, POINTER(POINTER(DbiSeqList))]),
+    ("dbi_seq_list_free", None, [POINTER(DbiSeqList)]),
+    ("dbi_store_protein_count", c_int, [P, POINTER(c_uint64)]),
+    ("dbi_store_protein_def", c_int, [P, c_uint64, POINTER(c_char_p), POINTER(c_uint64)]),
+    ("dbi_store_protein_sequence", c_int, [P, c_uint64, POINTER(c_void_p), POINTER(c_uint64)]),
+    ("dbi_dev_alloc", c_int, [c_int, c_uint64, POINTER(c_void_p)]),
+    ("dbi_dev_free", c_int, [c_int, P]),
+    ("dbi_dev_copy_h2d", c_int, [c_int, P, P, c_uint64]),
+    ("dbi_dev_copy_d2h", c_int, [c_int, P, P, c_uint64]),
+    ("dbi_dev_synchronize", c_int, [c_int]),
+    ("dbi_last_error", c_char_p, []),
+    ("dbi_abi_version", c_int, []),
+    ("dbi_device_count", c_int, [POINTER(c_int)]),
+]
+
+_lib = None
+
+
+def lib():
+    """Loads the in-tree HIP library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -m dbindex_amd.build` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    m = lib().dbi_last_error()
+    return m.decode(errors="replace") if m else ""
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise DBIndexStoreException(rc, last_error())
+
+
+def default_params(max_missed: int = 2, semi: bool = False) -> DbiParams:
+    p = DbiParams()
+    lib().dbi_params_default(ctypes.byref(p), max_missed, 1 if semi else 0)
+    return p
+
+
+def device_count() -> int:
+    n = c_int(0)
+    lib().dbi_device_count(ctypes.byref(n))
+    return n.value
+
+
+class DeviceBuffer:
+    """HBM allocation owned through the engine's own HIP runtime.
+
+    (PyTorch-ROCm ships a separate libamdhip64; mixing two HIP runtimes in one
+    process is order-dependent, so device-resident inputs for the engine are
+    allocated here rather than as torch tensors.)"""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.device = device
+        self.nbytes = int(nbytes)
+        p = c_void_p()
+        check(lib().dbi_dev_alloc(device, self.nbytes, ctypes.byref(p)))
+        self.ptr = p.value or 0
+
+    @classmethod
+    def from_numpy(cls, a, device: int = 0) -> "DeviceBuffer":
+        import numpy as np
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes, device)
+        b.upload(a)
+        return b
+
+    def upload(self, a) -> None:
+        import numpy as np
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        check(lib().dbi_dev_copy_h2d(self.device, c_void_p(self.ptr), a.ctypes.data_as(c_void_p), a.nbytes))
+
+    def download(self, dtype, count: int):
+        import numpy as np
+        out = np.empty(count, dtype=dtype)
+        assert out.nbytes <= self.nbytes
+        check(lib().dbi_dev_copy_d2h(self.device, out.ctypes.data_as(c_void_p), c_void_p(self.ptr), out.nbytes))
+        return out
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().dbi_dev_free(self.device, c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def synchronize(device: int = 0) -> None:
+    check(lib().dbi_dev_synchronize(device))

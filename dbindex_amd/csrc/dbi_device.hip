@@ -1,0 +1,1252 @@
+// dbi_device.hip — CDNA4 (gfx950) kernels of the peptide-index build and the
+// mass-window query.  Written for 64-wide wavefronts; compiled with
+// -ffp-contract=off so the fp64 mass accumulation is the plain sequential
+// left-to-right sum of DBIndexer.cutSeq (DBIndexer.java:265-308), i.e.
+// bit-identical to the reference's masses.
+//
+// Build pipeline (one stream):
+//   1. k_digest<COUNT>  — per 2048-start tile: residues + residue tables staged in
+//                          LDS, cleavage-site starts compacted with wave ballots,
+//                          one walk per site (cutSeq inner loop), per-tile count.
+//   2. scan of tile counts (insertion-order output offsets).
+//   3. k_digest<EMIT>   — same walk, block scan, 16-B records in insertion order.
+//   4. radix partition of records by mass bin (stable LSD passes, 8-bit digits).
+//   5. k_bin_sort       — per bin, bitonic sort by mass bits in LDS; equal-mass
+//                          runs grouped by peptide string (first appearance first),
+//                          unique-peptide heads flagged  (IndexMerge.getMergedData).
+//   6. scan of per-bin unique counts, k_finalize writes the unique table + the
+//                          occurrence CSR (protein ids, insertion order).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "dbi_internal.h"
+
+namespace dbi {
+
+// ---------------------------------------------------------------------------
+// wave / block primitives (wave = 64 lanes)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned lane_id() { return threadIdx.x & 63u; }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const unsigned l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if ((int)lane_id() >= d) v += o;
+    }
+    return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Block-wide exclusive scan of one value per thread.  s_tmp: >= NT/64 + 1 slots.
+template <int NT, typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* s_tmp, T& total) {
+    constexpr int NW = NT / 64;
+    const int w = threadIdx.x >> 6;
+    T inc = wave_incl_scan(v);
+    if (lane_id() == 63) s_tmp[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T acc = 0;
+        for (int i = 0; i < NW; ++i) {
+            T t = s_tmp[i];
+            s_tmp[i] = acc;
+            acc += t;
+        }
+        s_tmp[NW] = acc;
+    }
+    __syncthreads();
+    T r = inc - v + s_tmp[w];
+    total = s_tmp[NW];
+    __syncthreads();
+    return r;
+}
+
+template <int NT, typename T>
+__device__ __forceinline__ T block_sum(T v, T* s_tmp) {
+    T tot;
+    block_excl_scan<NT, T>(v, s_tmp, tot);
+    return tot;
+}
+
+__device__ __forceinline__ uint32_t bin_of(double m, const BinMap& bm) {
+    double x = (m - bm.lo) * bm.scale;
+    if (!(x > 0.0)) return 0u;
+    if (x >= (double)(bm.nbins - 1)) return bm.nbins - 1;
+    return (uint32_t)x;
+}
+
+__device__ __forceinline__ uint64_t dbits(double m) { return (uint64_t)__double_as_longlong(m); }
+
+// ---------------------------------------------------------------------------
+// 1/3. digest: DBIndexer.cutSeq (:237-405) + SQLiteMult.filterSequence/addSequence
+// ---------------------------------------------------------------------------
+constexpr int WIN_PRE = 16;  // residues staged before the tile (N-terminal context)
+constexpr int WIN = WIN_PRE + DIGEST_TILE + DIGEST_HALO;
+constexpr int STARTS_PER_THREAD = DIGEST_TILE / DIGEST_THREADS;
+constexpr int PLIST_CAP = WIN + 2;
+
+struct DigestSmem {
+    double mass[256];
+    uint16_t win[WIN];          // residue | residue-class flags << 8, for the staged window
+    uint8_t flags[256];
+    uint8_t pstart[DIGEST_TILE];
+    uint32_t plist[PLIST_CAP];  // protein offsets overlapping the window
+    uint16_t cand[DIGEST_TILE]; // compacted candidate starts (tile-local), in order
+    uint32_t tmp[DIGEST_THREADS / 64 + 1];
+};
+
+// largest p in [lo, hi) with poff[p] <= x   (poff ascending)
+__device__ __forceinline__ uint32_t find_le(const uint32_t* poff, uint32_t lo, uint32_t hi, uint32_t x) {
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (poff[mid] <= x) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// protein containing residue g, narrowed by the per-tile table
+__device__ __forceinline__ uint32_t find_pid(const uint32_t* __restrict__ poff, const uint32_t* __restrict__ tile_pf,
+                                             uint32_t n_prot, uint32_t ntiles, uint32_t g) {
+    const uint32_t t = g / (uint32_t)DIGEST_TILE;
+    const uint32_t lo = tile_pf[t];
+    const uint32_t hi = min(tile_pf[min(t + 1, ntiles)] + 1, n_prot);
+    return find_le(poff, lo, max(hi, lo + 1), g);
+}
+
+// tile_pf[t] = protein containing residue min(t*TILE, R-1), t in [0, ntiles]
+__global__ void k_tile_proteins(const uint32_t* __restrict__ poff, uint32_t n_prot, uint32_t n_res, uint32_t ntiles,
+                                uint32_t* __restrict__ tile_pf) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint32_t x = min(t * (uint32_t)DIGEST_TILE, n_res - 1);
+    tile_pf[t] = find_le(poff, 0, n_prot, x);
+}
+
+hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res, uint32_t* d_tile_pf,
+                                hipStream_t s) {
+    if (n_res == 0 || n_prot == 0) return hipSuccess;
+    const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
+    hipLaunchKernelGGL(k_tile_proteins, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
+                       d_tile_pf);
+    return hipGetLastError();
+}
+
+struct WalkOut {
+    uint32_t kept;
+    uint32_t dropped;
+    bool overflow;  // the LDS window ended before the walk did: redo it from HBM
+};
+
+// One start: the cutSeq inner loop (:256-397) in branch-light form.
+//   SEMI  : checkCleavage = N_ok || C_ok (else N_ok && C_ok; full-mode
+//           candidates are N_ok by construction, so cut == C_ok)
+//   MAND  : getMandatoryInternalAAs() != null (break + filterSequence path)
+//   GLOBAL: residues come from HBM instead of the LDS window (rare: walks
+//           that run past the halo, e.g. through zero-mass residues)
+// Identical decisions to the literal loop: the mass is the same sequential
+// fp64 sum, the loop exits exactly where the reference breaks, and since
+// m <= maxMH and m >= minMH hold at every emit the non-mandatory
+// filterSequence is always INCLUDE.
+template <bool EMIT, bool SEMI, bool MAND, bool GLOBAL>
+__device__ __forceinline__ WalkOut walk_start(const DevParams& dp, const DigestSmem& sm,
+                                              const uint8_t* __restrict__ g_res, uint32_t w0, uint32_t wlim,
+                                              uint32_t s, uint32_t ps, uint32_t pe, bool n_ok,
+                                              Rec* __restrict__ out, Counters* ctr) {
+    WalkOut r{0u, 0u, false};
+    double m = dp.m0;                 // precMass after H2O+H+, cTerm, nTerm (:265-271)
+    int mc = -1;                      // intMisCleavageCount (:280)
+    bool mand_excl = false;           // a mandatory residue in [s, e-1]
+    if (!(m <= dp.max_mh)) return r;  // while condition before the first residue (:284)
+    (void)ps;
+    auto load = [&](uint32_t g) -> uint32_t {
+        if (GLOBAL) {
+            const uint8_t c = g_res[g];
+            return (uint32_t)c | ((uint32_t)sm.flags[c] << 8);
+        }
+        return sm.win[g - w0];
+    };
+    uint32_t e = s;
+    uint32_t cur = load(e);
+    uint32_t kept = 0, dropped = 0;
+    for (;;) {
+        const uint32_t c = cur & 0xFFu;
+        const uint32_t fl = cur >> 8;
+        m = m + sm.mass[c];                                   // :306-308
+        mc += (int)(fl & F_CLEAVE);                           // :314-316
+        const bool last = (e + 1 == pe);
+        uint32_t nxt;
+        if (GLOBAL) {
+            nxt = last ? 0u : load(e + 1);
+        } else {
+            // clamped read: past the window only matters when !last (overflow exit below)
+            nxt = sm.win[min(e + 1, wlim - 1) - w0];
+            if (!last && e + 1 >= wlim) { r.overflow = true; return r; }
+        }
+        const bool c_ok = last | (((fl & F_CLEAVE) != 0) & (((nxt >> 8) & F_NOCUT) == 0));
+        const bool cut = SEMI ? (n_ok | c_ok) : c_ok;         // checkCleavage (:318)
+        const bool brk = cut & ((mc > dp.max_missed) | (m > dp.max_mh));          // :322-329
+        const uint32_t pep = e - s + 1;
+        bool emit = cut & !brk & ((int)pep >= dp.min_len) & (m >= dp.min_mh);   // :331
+        bool mbrk = false;
+        if (MAND) {
+            mbrk = emit & !(mand_excl | ((fl & F_MAND) != 0));  // :334-344 (break, not continue)
+            emit = emit & !mbrk & (!dp.mand_filter | mand_excl); // filterSequence (:247-263)
+            mand_excl = mand_excl | ((fl & F_MAND) != 0);
+        }
+        const bool drop = emit & (m >= dp.drop_mass);         // bucket > NUM_BUCKETS-1 (:282-288)
+        const bool keep = emit & !drop;
+        if (EMIT && keep) {
+            Rec rec;
+            rec.mass = m;
+            rec.gstart = s;
+            rec.len = (uint16_t)pep;
+            rec.flags = 0;
+            if (pep > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
+            out[kept] = rec;
+        }
+        kept += keep;
+        dropped += drop;
+        if (brk | mbrk | last | !(m <= dp.max_mh)) break;     // breaks + while condition (:284)
+        ++e;
+        cur = nxt;
+    }
+    r.kept = kept;
+    r.dropped = dropped;
+    return r;
+}
+
+template <bool EMIT, bool SEMI, bool MAND>
+__device__ __forceinline__ WalkOut walk(const DevParams& dp, const DigestSmem& sm, const uint8_t* __restrict__ g_res,
+                                        uint32_t w0, uint32_t wlim, uint32_t s, uint32_t ps, uint32_t pe, bool n_ok,
+                                        Rec* __restrict__ out, Counters* ctr) {
+    WalkOut w = walk_start<EMIT, SEMI, MAND, false>(dp, sm, g_res, w0, wlim, s, ps, pe, n_ok, out, ctr);
+    if (w.overflow) w = walk_start<EMIT, SEMI, MAND, true>(dp, sm, g_res, w0, wlim, s, ps, pe, n_ok, out, ctr);
+    return w;
+}
+
+// COUNT: per-thread kept counts -> d_thr, per-tile totals -> d_blk.
+// EMIT : d_blk holds the exclusive per-tile offsets; a block scan of the
+//        per-thread counts places each thread's contiguous run of candidates:
+//        thread order == start order, so records land in insertion order.
+template <bool EMIT, bool SEMI, bool MAND>
+__global__ void __launch_bounds__(DIGEST_THREADS)
+k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
+         const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
+         uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, uint32_t* __restrict__ d_blk,
+         uint32_t* __restrict__ d_thr, Rec* __restrict__ d_out, Counters* __restrict__ d_ctr) {
+    __shared__ DigestSmem sm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t ntiles = gridDim.x;
+    const uint32_t t0 = blockIdx.x * (uint32_t)DIGEST_TILE;
+    const uint32_t t_end = min(t0 + (uint32_t)DIGEST_TILE, n_res);
+    const uint32_t w0 = t0 >= (uint32_t)WIN_PRE ? t0 - WIN_PRE : 0u;
+    const uint32_t w_end = min(w0 + (uint32_t)WIN, n_res);
+
+    // residue tables -> LDS
+    sm.mass[tid] = d_mass_tab[tid];
+    sm.flags[tid] = d_flags[tid];
+    for (uint32_t i = tid; i < (uint32_t)DIGEST_TILE; i += DIGEST_THREADS) sm.pstart[i] = 0;
+    // proteins overlapping [t0, w_end): [pf, pl] narrowed by the tile table
+    const uint32_t pf = d_tile_pf[blockIdx.x];
+    const uint32_t pl = find_le(d_poff, pf, min(d_tile_pf[min(blockIdx.x + 2, ntiles)] + 1, n_prot), w_end - 1);
+    const uint32_t np_all = pl - pf + 2;
+    const uint32_t np = np_all <= (uint32_t)PLIST_CAP ? np_all : 0u;
+    __syncthreads();
+    // residue window -> LDS as (residue | flags << 8), 16 residues per load when aligned
+    {
+        const uint32_t nbytes = w_end - w0;
+        const uintptr_t base = (uintptr_t)(d_res + w0);
+        if ((base & 15u) == 0) {
+            const uint32_t nvec = nbytes >> 4;
+            for (uint32_t i = tid; i < nvec; i += DIGEST_THREADS) {
+                const uint4 v = reinterpret_cast<const uint4*>(d_res + w0)[i];
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const uint32_t c = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                    sm.win[i * 16 + k] = (uint16_t)(c | ((uint32_t)sm.flags[c] << 8));
+                }
+            }
+            for (uint32_t i = (nvec << 4) + tid; i < nbytes; i += DIGEST_THREADS) {
+                const uint32_t c = d_res[w0 + i];
+                sm.win[i] = (uint16_t)(c | ((uint32_t)sm.flags[c] << 8));
+            }
+        } else {
+            for (uint32_t i = tid; i < nbytes; i += DIGEST_THREADS) {
+                const uint32_t c = d_res[w0 + i];
+                sm.win[i] = (uint16_t)(c | ((uint32_t)sm.flags[c] << 8));
+            }
+        }
+    }
+    for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
+        const uint32_t o = d_poff[pf + i];
+        if (np) sm.plist[i] = o;
+        if (o >= t0 && o < t_end) sm.pstart[o - t0] = 1;  // protein N-terminus in the tile
+    }
+    __syncthreads();
+
+    // N_ok(s): protein N-term, or a site after a cleave residue not before a nocut one
+    auto n_ok_at = [&](uint32_t i) -> bool {
+        const uint32_t s = t0 + i;
+        return sm.pstart[i] ||
+               (((sm.win[s - 1 - w0] >> 8) & F_CLEAVE) && !((sm.win[s - w0] >> 8) & F_NOCUT));
+    };
+    // cleavage-site compaction: thread t owns starts [t*SPT, t*SPT+SPT) in order
+    uint32_t mybits = 0, mycnt = 0;
+#pragma unroll
+    for (int k = 0; k < STARTS_PER_THREAD; ++k) {
+        const uint32_t i = tid * STARTS_PER_THREAD + k;
+        const bool ok = (t0 + i < t_end) && (SEMI || n_ok_at(i));
+        if (ok) { mybits |= 1u << k; ++mycnt; }
+    }
+    uint32_t ncand;
+    uint32_t pos = block_excl_scan<DIGEST_THREADS, uint32_t>(mycnt, sm.tmp, ncand);
+#pragma unroll
+    for (int k = 0; k < STARTS_PER_THREAD; ++k)
+        if (mybits & (1u << k)) sm.cand[pos++] = (uint16_t)(tid * STARTS_PER_THREAD + k);
+    __syncthreads();
+
+    // thread t walks candidates [jb, je): a contiguous, balanced share
+    const uint32_t q = ncand / DIGEST_THREADS, rr = ncand % DIGEST_THREADS;
+    const uint32_t jb = tid * q + min(tid, rr);
+    const uint32_t je = jb + q + (tid < rr ? 1u : 0u);
+
+    auto site = [&](uint32_t j, uint32_t& s, uint32_t& ps, uint32_t& pe, bool& n_ok) {
+        const uint32_t i = sm.cand[j];
+        s = t0 + i;
+        if (np) {
+            const uint32_t k = find_le(sm.plist, 0, np - 1, s);
+            ps = sm.plist[k];
+            pe = sm.plist[k + 1];
+        } else {
+            const uint32_t p = find_le(d_poff, pf, pl + 1, s);
+            ps = d_poff[p];
+            pe = d_poff[p + 1];
+        }
+        n_ok = SEMI ? n_ok_at(i) : true;
+    };
+
+    if (!EMIT) {
+        uint32_t kept = 0, dropped = 0;
+        for (uint32_t j = jb; j < je; ++j) {
+            uint32_t s, ps, pe;
+            bool n_ok;
+            site(j, s, ps, pe, n_ok);
+            const WalkOut w = walk<false, SEMI, MAND>(dp, sm, d_res, w0, w_end, s, ps, pe, n_ok, nullptr, d_ctr);
+            kept += w.kept;
+            dropped += w.dropped;
+        }
+        d_thr[blockIdx.x * DIGEST_THREADS + tid] = kept;
+        const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
+        const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
+        if (tid == 0) {
+            d_blk[blockIdx.x] = tk;
+            if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
+        }
+        return;
+    }
+
+    uint32_t tot;
+    const uint32_t my = d_thr[blockIdx.x * DIGEST_THREADS + tid];
+    Rec* out = d_out + d_blk[blockIdx.x] + block_excl_scan<DIGEST_THREADS, uint32_t>(my, sm.tmp, tot);
+    for (uint32_t j = jb; j < je; ++j) {
+        uint32_t s, ps, pe;
+        bool n_ok;
+        site(j, s, ps, pe, n_ok);
+        out += walk<true, SEMI, MAND>(dp, sm, d_res, w0, w_end, s, ps, pe, n_ok, out, d_ctr).kept;
+    }
+}
+
+template <bool EMIT>
+static hipError_t launch_digest(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                                const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                                const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr, Rec* d_out,
+                                Counters* d_ctr, hipStream_t s) {
+    const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
+    if (nblk == 0) return hipSuccess;
+#define DBI_DIGEST(SEMI, MAND)                                                                              \
+    hipLaunchKernelGGL((k_digest<EMIT, SEMI, MAND>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
+                       d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_out, d_ctr)
+    if (dp.semi) {
+        if (dp.mand_mode) DBI_DIGEST(true, true); else DBI_DIGEST(true, false);
+    } else {
+        if (dp.mand_mode) DBI_DIGEST(false, true); else DBI_DIGEST(false, false);
+    }
+#undef DBI_DIGEST
+    return hipGetLastError();
+}
+
+hipError_t launch_digest_count(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                               const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
+                               uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr,
+                               Counters* d_ctr, hipStream_t s) {
+    return launch_digest<false>(dp, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr,
+                                nullptr, d_ctr, s);
+}
+
+hipError_t launch_digest_emit(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                              const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
+                              uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk_off, uint32_t* d_thr,
+                              Rec* d_out, Counters* d_ctr, hipStream_t s) {
+    return launch_digest<true>(dp, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk_off, d_thr,
+                               d_out, d_ctr, s);
+}
+
+// ---------------------------------------------------------------------------
+// 2. exclusive scan of u32 (reduce -> single-block scan of block sums -> downsweep)
+// ---------------------------------------------------------------------------
+constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_ITEMS = 4;
+constexpr uint64_t SCAN_CHUNK = (uint64_t)SCAN_THREADS * SCAN_ITEMS;
+
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ sums) {
+    __shared__ uint32_t tmp[SCAN_THREADS / 64 + 1];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK;
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * SCAN_THREADS + threadIdx.x;
+        if (i < n) v += in[i];
+    }
+    const uint32_t t = block_sum<SCAN_THREADS, uint32_t>(v, tmp);
+    if (threadIdx.x == 0) sums[blockIdx.x] = t;
+}
+
+// single block: exclusive scan of n values in place-able, u64 carry, total -> *d_total
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan_single(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t n,
+              unsigned long long* __restrict__ d_total) {
+    __shared__ unsigned long long tmp[SCAN_THREADS / 64 + 1];
+    unsigned long long carry = 0;
+    for (uint64_t base = 0; base < n; base += SCAN_CHUNK) {
+        uint32_t v[SCAN_ITEMS];
+        unsigned long long loc = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            const uint64_t i = base + (uint64_t)threadIdx.x * SCAN_ITEMS + k;
+            v[k] = i < n ? in[i] : 0u;
+            loc += v[k];
+        }
+        unsigned long long tot;
+        unsigned long long run = block_excl_scan<SCAN_THREADS, unsigned long long>(loc, tmp, tot);
+        run += carry;
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            const uint64_t i = base + (uint64_t)threadIdx.x * SCAN_ITEMS + k;
+            if (i < n) out[i] = (uint32_t)run;
+            run += v[k];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0 && d_total) *d_total = carry;
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t n,
+            const uint32_t* __restrict__ block_off) {
+    __shared__ uint32_t tmp[SCAN_THREADS / 64 + 1];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK;
+    uint32_t v[SCAN_ITEMS];
+    uint32_t loc = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)threadIdx.x * SCAN_ITEMS + k;
+        v[k] = i < n ? in[i] : 0u;
+        loc += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan<SCAN_THREADS, uint32_t>(loc, tmp, tot) + block_off[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)threadIdx.x * SCAN_ITEMS + k;
+        if (i < n) out[i] = run;
+        run += v[k];
+    }
+}
+
+size_t scan_u32_tmp_elems(uint64_t n) { return (size_t)((n + SCAN_CHUNK - 1) / SCAN_CHUNK) + 1; }
+
+hipError_t launch_scan_u32(const uint32_t* d_in, uint32_t* d_out, uint64_t n, uint32_t* d_block_tmp,
+                           uint64_t tmp_elems, unsigned long long* d_total, hipStream_t s) {
+    if (n <= SCAN_CHUNK * 4) {
+        hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(SCAN_THREADS), 0, s, d_in, d_out, n, d_total);
+        return hipGetLastError();
+    }
+    const uint64_t nb = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
+    if (tmp_elems < nb) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, n, d_block_tmp);
+    hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(SCAN_THREADS), 0, s, d_block_tmp, d_block_tmp, nb, d_total);
+    hipLaunchKernelGGL(k_scan_down, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, d_out, n, d_block_tmp);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// 4. stable LSD radix pass over the mass-bin id (digit = (bin >> shift) & mask)
+// ---------------------------------------------------------------------------
+constexpr uint32_t RADIX_CHUNK = RADIX_THREADS * RADIX_ITEMS;
+constexpr int RADIX_D = 1 << RADIX_BITS;
+constexpr int RADIX_NW = RADIX_THREADS / 64;
+
+size_t radix_hist_elems(uint32_t n, int bits) {
+    const uint64_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    return (size_t)g * (size_t)(1u << bits);
+}
+
+__global__ void __launch_bounds__(RADIX_THREADS)
+k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int bits,
+             uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[RADIX_D];
+    const uint32_t D = 1u << bits, mask = D - 1;
+    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) h[d] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * RADIX_CHUNK;
+#pragma unroll 4
+    for (int k = 0; k < RADIX_ITEMS; ++k) {
+        const uint32_t i = base + k * RADIX_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&h[(bin_of(in[i].mass, bm) >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) hist[(size_t)d * gridDim.x + blockIdx.x] = h[d];
+}
+
+__global__ void __launch_bounds__(RADIX_THREADS)
+k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, BinMap bm, int shift,
+                int bits, const uint32_t* __restrict__ offs) {
+    __shared__ uint32_t wcount[RADIX_NW][RADIX_D];
+    const uint32_t D = 1u << bits, mask = D - 1;
+    const uint32_t tid = threadIdx.x;
+    const int w = tid >> 6;
+    // this thread owns the running offsets of digits tid and tid + RADIX_THREADS
+    uint32_t running0 = tid < D ? offs[(size_t)tid * gridDim.x + blockIdx.x] : 0u;
+    uint32_t running1 = tid + RADIX_THREADS < D ? offs[(size_t)(tid + RADIX_THREADS) * gridDim.x + blockIdx.x] : 0u;
+    const uint32_t base = blockIdx.x * RADIX_CHUNK;
+    for (int k = 0; k < RADIX_ITEMS; ++k) {
+        const uint32_t i = base + k * RADIX_THREADS + tid;
+        const bool valid = i < n;
+        Rec r;
+        uint32_t d = 0;
+        if (valid) {
+            r = in[i];
+            d = (bin_of(r.mass, bm) >> shift) & mask;
+        }
+        // peers: lanes of this wave holding the same digit
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < bits; ++b) {
+            const uint64_t bal = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? bal : ~bal;
+        }
+        for (uint32_t x = tid; x < (uint32_t)(RADIX_NW * RADIX_D); x += RADIX_THREADS)
+            (&wcount[0][0])[x] = 0;
+        __syncthreads();
+        const uint32_t rank = __popcll(peers & lanemask_lt());
+        if (valid && rank == 0) wcount[w][d] = __popcll(peers);
+        __syncthreads();
+        if (tid < D) {
+            uint32_t acc = running0;
+#pragma unroll
+            for (int ww = 0; ww < RADIX_NW; ++ww) {
+                const uint32_t t = wcount[ww][tid];
+                wcount[ww][tid] = acc;
+                acc += t;
+            }
+            running0 = acc;
+        }
+        if (tid + RADIX_THREADS < D) {
+            const uint32_t dd = tid + RADIX_THREADS;
+            uint32_t acc = running1;
+#pragma unroll
+            for (int ww = 0; ww < RADIX_NW; ++ww) {
+                const uint32_t t = wcount[ww][dd];
+                wcount[ww][dd] = acc;
+                acc += t;
+            }
+            running1 = acc;
+        }
+        __syncthreads();
+        if (valid) out[wcount[w][d] + rank] = r;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, uint32_t* d_hist,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    hipLaunchKernelGGL(k_radix_hist, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, bm, shift, bits, d_hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
+                                const uint32_t* d_hist, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    hipLaunchKernelGGL(k_radix_scatter, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, bm, shift, bits,
+                       d_hist);
+    return hipGetLastError();
+}
+
+uint64_t radix_blocks(uint32_t n) { return (n + RADIX_CHUNK - 1) / RADIX_CHUNK; }
+
+// bin_start[b] = first record of bin b (records sorted by bin), bin_start[nbins] = n
+__global__ void k_bin_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap bm,
+                             uint32_t* __restrict__ bin_start) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t b = bin_of(recs[i].mass, bm);
+    const int64_t bp = i ? (int64_t)bin_of(recs[i - 1].mass, bm) : -1;
+    for (int64_t j = bp + 1; j <= (int64_t)b; ++j) bin_start[j] = i;
+    if (i == n - 1)
+        for (uint32_t j = b + 1; j <= bm.nbins; ++j) bin_start[j] = n;
+}
+
+hipError_t launch_bin_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t* d_bin_start,
+                             hipStream_t s) {
+    if (n == 0) {
+        return hipMemsetAsync(d_bin_start, 0, sizeof(uint32_t) * ((size_t)bm.nbins + 1), s);
+    }
+    hipLaunchKernelGGL(k_bin_bounds, dim3((n + 255) / 256), dim3(256), 0, s, d_recs, n, bm, d_bin_start);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// 5. chunk sort + group by peptide string (IndexMerge.getMergedData :620-719)
+// ---------------------------------------------------------------------------
+// A chunk is a run of whole mass bins: chunk c = records [B(c*T), B((c+1)*T))
+// with B(x) = start of the first bin starting at or after x.  Bins never
+// straddle chunks, so sorting a chunk by mass equals sorting its bins, and
+// chunk sizes stay near T whatever the mass-density skew.
+constexpr uint32_t HASH_GROUP = 16;
+
+// 64-bit FNV-1a over the peptide's residue bytes: the tie-break key between
+// different peptides of bit-identical mass (pinned order).
+// Loads are issued HASH_GROUP at a time so one latency covers a typical peptide.
+__device__ __forceinline__ unsigned long long pep_hash(const uint8_t* __restrict__ res, uint32_t g, uint32_t len) {
+    unsigned long long h = 14695981039346656037ull;
+    for (uint32_t k0 = 0; k0 < len; k0 += HASH_GROUP) {
+        uint32_t b[HASH_GROUP];
+#pragma unroll
+        for (uint32_t j = 0; j < HASH_GROUP; ++j) b[j] = (k0 + j < len) ? res[g + k0 + j] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < HASH_GROUP; ++j) {
+            if (k0 + j < len) {
+                h ^= b[j];
+                h *= 1099511628211ull;
+            }
+        }
+    }
+    return h;
+}
+
+__device__ __forceinline__ bool seq_equal(const uint8_t* __restrict__ res, const Rec& a, const Rec& b) {
+    if (a.len != b.len) return false;
+    if (a.gstart == b.gstart) return true;
+    const uint32_t len = a.len;
+    for (uint32_t k0 = 0; k0 < len; k0 += HASH_GROUP) {
+        uint32_t x[HASH_GROUP], y[HASH_GROUP];
+#pragma unroll
+        for (uint32_t j = 0; j < HASH_GROUP; ++j) {
+            x[j] = (k0 + j < len) ? res[a.gstart + k0 + j] : 0u;
+            y[j] = (k0 + j < len) ? res[b.gstart + k0 + j] : 0u;
+        }
+        bool eq = true;
+#pragma unroll
+        for (uint32_t j = 0; j < HASH_GROUP; ++j) eq &= (x[j] == y[j]);
+        if (!eq) return false;
+    }
+    return true;
+}
+
+// Bitonic sort of (key, hsh, idx) triples, ascending; NT threads.
+template <int NT>
+__device__ void bitonic_sort3(unsigned long long* key, unsigned long long* hsh, uint32_t* k2, uint32_t P2) {
+    for (uint32_t k = 2; k <= P2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P2; i += NT) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long a = key[i], b = key[ixj];
+                    const unsigned long long ha = hsh[i], hb = hsh[ixj];
+                    const uint32_t ai = k2[i], bi = k2[ixj];
+                    const bool gt = (a > b) || (a == b && (ha > hb || (ha == hb && ai > bi)));
+                    const bool asc = (i & k) == 0;
+                    if (asc ? gt : !gt) {
+                        key[i] = b; key[ixj] = a;
+                        hsh[i] = hb; hsh[ixj] = ha;
+                        k2[i] = bi; k2[ixj] = ai;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// One chunk of n records (in: global, insertion order inside every bin).
+// Sorted order = (mass, FNV-1a hash of the string, insertion idx); equal
+// (mass, hash) neighbours are string-verified; a true 64-bit collision falls
+// back to grouping equal-(mass, hash) runs by first appearance.
+// STAGE: copy the records into rec[] (LDS) first; otherwise rec == in (global).
+// key/hsh/k2/k3 are P2-sized scratch; s_u32 >= NT/64+1 slots.
+template <int NT, bool STAGE>
+__device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __restrict__ out, uint32_t n,
+                                  const uint8_t* __restrict__ res, unsigned long long* key, unsigned long long* hsh,
+                                  uint32_t* k2, uint32_t* k3, uint32_t* s_u32, unsigned long long* s_flag) {
+    uint32_t P2 = 1;
+    while (P2 < n) P2 <<= 1;
+    for (uint32_t i = threadIdx.x; i < P2; i += NT) {
+        if (i < n) {
+            const Rec r = in[i];
+            if (STAGE) rec[i] = r;
+            key[i] = dbits(r.mass);
+            hsh[i] = pep_hash(res, r.gstart, r.len);
+        } else {
+            key[i] = ~0ull;  // padding sorts last
+            hsh[i] = ~0ull;
+        }
+        k2[i] = i;  // local idx = insertion order
+    }
+    if (threadIdx.x == 0) *s_flag = 0;
+    __syncthreads();
+    bitonic_sort3<NT>(key, hsh, k2, P2);
+
+    // verify equal (mass, hash) neighbours are the same string
+    for (uint32_t i = threadIdx.x + 1; i < n; i += NT) {
+        if (key[i] == key[i - 1] && hsh[i] == hsh[i - 1]) {
+            if (!seq_equal(res, rec[k2[i]], rec[k2[i - 1]])) atomicOr(s_flag, 1ull);
+        }
+    }
+    __syncthreads();
+    if (*s_flag != 0) {
+        // k3[i] = first position of the equal-(mass, hash) run containing i
+        // (block max-scan of head positions; thread t owns [t*E, t*E+E))
+        const uint32_t E = (n + NT - 1) / NT;
+        const uint32_t lo = min(threadIdx.x * E, n), hi = min(lo + E, n);
+        uint32_t last = 0;
+        bool has = false;
+        for (uint32_t i = lo; i < hi; ++i) {
+            if (i == 0 || key[i] != key[i - 1] || hsh[i] != hsh[i - 1]) { last = i; has = true; }
+            k3[i] = last;
+        }
+        const int w = threadIdx.x >> 6;
+        uint32_t inc = has ? last : 0u;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(inc, d, 64);
+            if ((int)lane_id() >= d) inc = max(inc, o);
+        }
+        if (lane_id() == 63) s_u32[w] = inc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int i = 0; i < NT / 64; ++i) {
+                const uint32_t t = s_u32[i];
+                s_u32[i] = acc;
+                acc = max(acc, t);
+            }
+        }
+        __syncthreads();
+        uint32_t excl = __shfl_up(inc, 1, 64);
+        if (lane_id() == 0) excl = 0;
+        excl = max(excl, s_u32[w]);
+        for (uint32_t i = lo; i < hi; ++i) {
+            if (i == 0 || key[i] != key[i - 1] || hsh[i] != hsh[i - 1]) break;
+            k3[i] = excl;
+        }
+        __syncthreads();
+        // leader = smallest-idx element of the run with the same string; re-key
+        // as (run start, leader, idx) and sort again
+        for (uint32_t i = threadIdx.x; i < n; i += NT) {
+            const uint32_t rs = k3[i];
+            uint32_t leader = k2[rs];
+            if (rs != i) {
+                const Rec me = rec[k2[i]];
+                if (!seq_equal(res, me, rec[k2[rs]])) {
+                    leader = k2[i];
+                    for (uint32_t r = rs + 1; r < i; ++r)
+                        if (seq_equal(res, me, rec[k2[r]])) { leader = k2[r]; break; }
+                }
+            }
+            // nobody reads key/hsh any more in this phase: re-key in place
+            hsh[i] = ((unsigned long long)rs << 32) | leader;
+            key[i] = 0;
+        }
+        __syncthreads();
+        bitonic_sort3<NT>(key, hsh, k2, P2);  // -> (run start, leader, idx); padding keeps ~0
+    }
+
+    // unique-peptide heads + write the chunk in final order
+    uint32_t myheads = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += NT) {
+        const bool head = (i == 0) || key[i] != key[i - 1] || hsh[i] != hsh[i - 1];
+        Rec r = rec[k2[i]];
+        r.flags = head ? 1 : 0;
+        out[i] = r;
+        myheads += head;
+    }
+    return myheads;
+}
+
+// chunk c = records [chunk_lo[c], chunk_lo[c+1]) = bins [chunk_bin[c], chunk_bin[c+1]);
+// chunk_lo[c] = start of the first bin starting at or after c*T (one thread per chunk)
+__global__ void k_chunk_bounds(const uint32_t* __restrict__ bin_start, uint32_t nbins, uint32_t n, uint32_t T,
+                               uint32_t nchunks, uint32_t* __restrict__ chunk_lo, uint32_t* __restrict__ chunk_bin) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > nchunks) return;
+    const uint32_t x = c == nchunks ? n : min(c * T, n);
+    uint32_t lo = 0, hi = nbins;  // lower_bound over bin_start[0..nbins] (bin_start[nbins] == n)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (bin_start[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    chunk_bin[c] = lo;
+    chunk_lo[c] = bin_start[lo];
+}
+
+hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint32_t n, uint32_t T, uint32_t nchunks,
+                               uint32_t* d_chunk_lo, uint32_t* d_chunk_bin, hipStream_t s) {
+    hipLaunchKernelGGL(k_chunk_bounds, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_bin_start, nbins, n, T,
+                       nchunks, d_chunk_lo, d_chunk_bin);
+    return hipGetLastError();
+}
+
+// Per chunk: keys + peptide hashes into LDS, then every fine bin is rank-sorted
+// by one wave (rank = #elements of the bin ordered before, by (mass bits,
+// FNV-1a hash, insertion idx); broadcast LDS reads, no block barriers).  Equal
+// (mass, hash) neighbours are string-verified; a chunk with a true hash
+// collision, a bin above RANK_MAX or more than CAP records goes to the
+// global-memory path (k_big_chunks), which groups by first appearance.
+constexpr uint32_t RANK_MAX = 2048;
+
+template <int NT, int CAP>
+__global__ void __launch_bounds__(NT)
+k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
+             const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, uint32_t* __restrict__ big_list,
+             Counters* __restrict__ ctr, uint32_t ablate) {
+    __shared__ unsigned long long key[CAP];
+    __shared__ unsigned long long hsh[CAP];
+    __shared__ uint32_t binid[CAP];
+    __shared__ uint16_t perm[CAP];
+    __shared__ uint16_t run_start[CAP + 1];
+    __shared__ uint32_t s_u32[NT / 64 + 1];
+    __shared__ uint32_t s_bad;
+    constexpr uint32_t NW = NT / 64;
+    const uint32_t c = blockIdx.x;
+    const uint32_t a = chunk_lo[c];
+    const uint32_t m = chunk_lo[c + 1] - a;
+    if (m == 0) {
+        if (threadIdx.x == 0) ucount[c] = 0;
+        return;
+    }
+    if (m > (uint32_t)CAP) {
+        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
+        return;
+    }
+    if (threadIdx.x == 0) s_bad = 0;
+    for (uint32_t i = threadIdx.x; i < m; i += NT) {
+        const Rec r = in[a + i];
+        key[i] = dbits(r.mass);
+        binid[i] = bin_of(r.mass, bm);
+        hsh[i] = (ablate & 1) ? 0ull : pep_hash(res, r.gstart, r.len);
+    }
+    __syncthreads();
+    // runs of equal bin id (records are grouped by bin): compact the run starts
+    {
+        constexpr uint32_t E = CAP / NT;
+        const uint32_t lo = threadIdx.x * E;
+        uint32_t flags = 0, cnt = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint32_t i = lo + k;
+            const bool h = i < m && (i == 0 || binid[i] != binid[i - 1]);
+            flags |= (uint32_t)h << k;
+            cnt += h;
+        }
+        uint32_t nruns;
+        uint32_t pos = block_excl_scan<NT, uint32_t>(cnt, s_u32, nruns);
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k)
+            if (flags & (1u << k)) run_start[pos++] = (uint16_t)(lo + k);
+        if (threadIdx.x == 0) {
+            run_start[nruns] = (uint16_t)m;
+            s_u32[NW] = nruns;
+        }
+    }
+    __syncthreads();
+    const uint32_t nruns = s_u32[NW];
+    // rank sort inside every run (= fine bin): one wave per run, broadcast LDS reads
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (uint32_t r = w; r < nruns; r += NW) {
+        const uint32_t lo = run_start[r], hi = run_start[r + 1];
+        const uint32_t nb = hi - lo;
+        if (nb == 1) {
+            if (lane == 0) perm[lo] = (uint16_t)lo;
+            continue;
+        }
+        if (nb > RANK_MAX) {
+            if (lane == 0) s_bad = 1;
+            continue;
+        }
+        if (ablate & 2) {
+            for (uint32_t i = lo + lane; i < hi; i += 64) perm[i] = (uint16_t)i;
+            continue;
+        }
+        for (uint32_t base = lo; base < hi; base += 64) {
+            const uint32_t i = base + lane;
+            const bool act = i < hi;
+            const unsigned long long ki = act ? key[i] : 0, hi_ = act ? hsh[i] : 0;
+            uint32_t rank = 0;
+            for (uint32_t j = lo; j < hi; ++j) {
+                const unsigned long long kj = key[j], hj = hsh[j];
+                rank += (kj < ki) | ((kj == ki) & ((hj < hi_) | ((hj == hi_) & (j < i))));
+            }
+            if (act) perm[lo + rank] = (uint16_t)i;
+        }
+    }
+    __syncthreads();
+    // verify equal (mass, hash) neighbours are the same string (else: collision)
+    uint32_t myheads = 0;
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        const uint32_t i = perm[p];
+        bool head = true;
+        if (p > 0) {
+            const uint32_t ip = perm[p - 1];
+            if (key[i] == key[ip] && hsh[i] == hsh[ip]) {
+                head = false;
+                if (!(ablate & 4) && !seq_equal(res, in[a + i], in[a + ip])) s_bad = 1;
+            }
+        }
+        myheads += head;
+    }
+    __syncthreads();
+    if (s_bad) {  // 64-bit hash collision or oversized run: the global-memory path redoes the chunk
+        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
+        return;
+    }
+    for (uint32_t p = threadIdx.x; p < m && !(ablate & 8); p += NT) {
+        const uint32_t i = perm[p];
+        const bool head = p == 0 || key[i] != key[perm[p - 1]] || hsh[i] != hsh[perm[p - 1]];
+        Rec r = in[a + i];
+        r.flags = head ? 1 : 0;
+        out[a + p] = r;
+    }
+    const uint32_t tot = block_sum<NT, uint32_t>(myheads, s_u32);
+    if (threadIdx.x == 0) ucount[c] = tot;
+}
+
+hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
+                             uint32_t nchunks, const uint8_t* d_res, uint32_t* d_ucount, uint32_t* d_big_list,
+                             Counters* d_ctr, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    static const uint32_t ablate = getenv("DBI_ABLATE") ? (uint32_t)atoi(getenv("DBI_ABLATE")) : 0u;
+    hipLaunchKernelGGL((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
+                       d_out, bm, d_chunk_lo, d_res, d_ucount, d_big_list, d_ctr, ablate);
+    return hipGetLastError();
+}
+
+// chunks above the LDS capacity (runs of very frequent peptides): same body,
+// scratch in a global workspace (region [4a, 4a+4m) of each array)
+__global__ void __launch_bounds__(BIG_THREADS)
+k_big_chunks(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
+             const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, const uint32_t* __restrict__ big_list,
+             unsigned long long* ws_key, uint32_t* ws_k2, Counters* __restrict__ ctr) {
+    __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
+    __shared__ unsigned long long s_flag;
+    const uint32_t nbig = ctr->n_big;
+    for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {
+        const uint32_t c = big_list[j];
+        const uint32_t a = chunk_lo[c];
+        const uint32_t m = chunk_lo[c + 1] - a;
+        unsigned long long* key = ws_key + 4ull * a;   // [4a, 4a+2m): key, [4a+2m, 4a+4m): hash
+        unsigned long long* hsh = key + 2ull * m;
+        uint32_t* k2 = ws_k2 + 4ull * a;               // [4a, 4a+2m): idx, [4a+2m, 4a+3m): runs
+        uint32_t* k3 = k2 + 2ull * m;
+        const uint32_t h = process_chunk<BIG_THREADS, false>(in + a, const_cast<Rec*>(in + a), out + a, m, res, key,
+                                                              hsh, k2, k3, s_u32, &s_flag);
+        const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
+        if (threadIdx.x == 0) ucount[c] = tot;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
+                             uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t max_blocks,
+                             unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr, hipStream_t s) {
+    if (max_blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_big_chunks, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res,
+                       d_ucount, d_big_list, d_ws_key, d_ws_k2, d_ctr);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// 6. finalize: unique table + occurrence CSR (per chunk)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
+           const uint32_t* __restrict__ poff, uint32_t n_prot, const uint32_t* __restrict__ tile_pf,
+           uint32_t ntiles, double* __restrict__ umass, uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff,
+           uint32_t* __restrict__ ulen, uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid) {
+    __shared__ uint32_t tmp[256 / 64 + 1];
+    const uint32_t c = blockIdx.x;
+    const uint32_t a = chunk_lo[c];
+    const uint32_t n = chunk_lo[c + 1] - a;
+    uint32_t run = ubase[c];
+    for (uint32_t t = 0; t < n; t += 256) {
+        const uint32_t i = t + threadIdx.x;
+        Rec r;
+        uint32_t head = 0;
+        if (i < n) {
+            r = recs[a + i];
+            head = r.flags & 1u;
+        }
+        uint32_t tot;
+        const uint32_t u = run + block_excl_scan<256, uint32_t>(head, tmp, tot);
+        if (i < n) {
+            const uint32_t p = find_pid(poff, tile_pf, n_prot, ntiles, r.gstart);
+            occ_pid[a + i] = p;
+            if (head) {
+                umass[u] = r.mass;
+                upid[u] = p;
+                uoff[u] = r.gstart - poff[p];
+                ulen[u] = r.len;
+                occ_off[u] = a + i;
+            }
+        }
+        run += tot;
+    }
+}
+
+hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
+                           const uint32_t* d_poff, uint32_t n_prot, const uint32_t* d_tile_pf, uint32_t n_res,
+                           double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
+                           uint32_t* d_occ_off, uint32_t* d_occ_pid, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
+    hipLaunchKernelGGL(k_finalize, dim3(nchunks), dim3(256), 0, s, d_recs, d_chunk_lo, d_ubase, d_poff, n_prot,
+                       d_tile_pf, ntiles, d_umass, d_upid, d_uoff, d_ulen, d_occ_off, d_occ_pid);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// distinct mass keys (int)(mass*factor) over the mass-sorted unique table;
+// U is read from the device counters (no host round trip), grid sized by n_upper.
+__global__ void k_count_keys(const double* __restrict__ umass, int32_t factor, uint32_t* __restrict__ flags,
+                             Counters* __restrict__ ctr) {
+    __shared__ uint32_t tmp[256 / 64 + 1];
+    const uint32_t n = (uint32_t)ctr->n_unique;
+    uint32_t f = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int32_t k = java_d2i(umass[i] * (double)factor);
+        const uint32_t fi = (i == 0) || (java_d2i(umass[i - 1] * (double)factor) != k);
+        if (flags) flags[i] = fi;
+        f += fi;
+    }
+    const uint32_t t = block_sum<256, uint32_t>(f, tmp);
+    // one add per block into one of 8 shards (no single-word contention)
+    if (threadIdx.x == 0 && t) atomicAdd(&ctr->n_keys_shard[blockIdx.x & 7], (unsigned long long)t);
+}
+
+hipError_t launch_count_keys(const double* d_umass, uint32_t n_upper, int32_t factor, uint32_t* d_flags,
+                             Counters* d_ctr, hipStream_t s) {
+    if (n_upper == 0) return hipSuccess;
+    const uint32_t g = min((n_upper + 255) / 256, 1024u);
+    hipLaunchKernelGGL(k_count_keys, dim3(g), dim3(256), 0, s, d_umass, factor, d_flags, d_ctr);
+    return hipGetLastError();
+}
+
+// occ_off[U] = n_kept (U from the device counters)
+__global__ void k_write_tail(uint32_t* __restrict__ occ_off, uint32_t n_kept, const Counters* __restrict__ ctr) {
+    if (threadIdx.x == 0) occ_off[ctr->n_unique] = n_kept;
+}
+
+hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s) {
+    hipLaunchKernelGGL(k_write_tail, dim3(1), dim3(64), 0, s, d_occ_off, n_kept, d_ctr);
+    return hipGetLastError();
+}
+
+// gather per-unique data for arbitrary ids (dbi_peptides)
+__global__ void k_gather(const uint64_t* __restrict__ ids, uint64_t n, const double* __restrict__ umass,
+                         const uint32_t* __restrict__ upid, const uint32_t* __restrict__ uoff,
+                         const uint32_t* __restrict__ ulen, const uint32_t* __restrict__ occ_off,
+                         double* __restrict__ o_mass, uint32_t* __restrict__ o_pid, uint32_t* __restrict__ o_off,
+                         uint32_t* __restrict__ o_len, uint64_t* __restrict__ o_b, uint64_t* __restrict__ o_e) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t u = ids[i];
+    o_mass[i] = umass[u];
+    o_pid[i] = upid[u];
+    o_off[i] = uoff[u];
+    o_len[i] = ulen[u];
+    o_b[i] = occ_off[u];
+    o_e[i] = occ_off[u + 1];
+}
+
+hipError_t launch_gather(const uint64_t* d_ids, uint64_t n, const double* d_umass, const uint32_t* d_upid,
+                         const uint32_t* d_uoff, const uint32_t* d_ulen, const uint32_t* d_occ_off,
+                         double* o_mass, uint32_t* o_pid, uint32_t* o_off, uint32_t* o_len, uint64_t* o_b,
+                         uint64_t* o_e, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_ids, n, d_umass, d_upid,
+                       d_uoff, d_ulen, d_occ_off, o_mass, o_pid, o_off, o_len, o_b, o_e);
+    return hipGetLastError();
+}
+
+__global__ void k_write_keys(const double* __restrict__ umass, uint32_t n, int32_t factor,
+                             const uint32_t* __restrict__ pos, int32_t* __restrict__ keys) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int32_t k = java_d2i(umass[i] * (double)factor);
+    if (i == 0 || java_d2i(umass[i - 1] * (double)factor) != k) keys[pos[i]] = k;
+}
+
+hipError_t launch_write_keys(const double* d_umass, uint32_t n_unique, int32_t factor, const uint32_t* d_pos,
+                             int32_t* d_keys, hipStream_t s) {
+    if (n_unique == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_write_keys, dim3((n_unique + 255) / 256), dim3(256), 0, s, d_umass, n_unique, factor,
+                       d_pos, d_keys);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// query: getSequences(m, tol) (SQLiteMult:315-350 + IndexMerge:146-217,386-481)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lower_bound_d(const double* __restrict__ a, uint32_t n, double x) {
+    uint32_t lo = 0, hi = n;  // first i with a[i] >= x
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ uint32_t upper_bound_d(const double* __restrict__ a, uint32_t n, double x) {
+    uint32_t lo = 0, hi = n;  // first i with a[i] > x
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+// first i with key(a[i]) > k   (key monotone in mass)
+__device__ __forceinline__ uint32_t key_upper(const double* __restrict__ a, uint32_t n, int32_t factor, int32_t k) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (java_d2i(a[mid] * (double)factor) <= k) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_query(DevParams dp, int32_t factor, const double* __restrict__ umass, uint32_t nu,
+                        const double* __restrict__ qm, const double* __restrict__ qt, uint64_t nq,
+                        uint64_t* __restrict__ first, uint64_t* __restrict__ count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const double precMass = qm[i], tol = qt[i];
+    double lo = precMass - tol;
+    if (lo < 0) lo = 0;
+    const double hi = precMass + tol;
+    const int b0 = java_d2i(lo) / dp.br, b1 = java_d2i(hi) / dp.br;
+    uint64_t f = 0, c = 0;
+    if (!(b0 > dp.nb - 1 || b1 > dp.nb - 1)) {
+        if (lo != lo || hi != hi) {
+            // NaN bounds: rows BETWEEN (int)NaN=0 AND 0, and no mass test rejects
+            // (comparisons with NaN are false) -> every unique with key 0.
+            c = key_upper(umass, nu, factor, 0);
+        } else {
+            const uint32_t a = lower_bound_d(umass, nu, lo);
+            const uint32_t e = upper_bound_d(umass, nu, hi);
+            if (e > a) { f = a; c = e - a; }
+        }
+    }
+    first[i] = f;
+    count[i] = c;
+}
+
+hipError_t launch_query(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,
+                        const double* d_qmass, const double* d_qtol, uint64_t nq, uint64_t* d_first,
+                        uint64_t* d_count, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_query, dim3((uint32_t)((nq + 255) / 256)), dim3(256), 0, s, dp, factor, d_umass,
+                       n_unique, d_qmass, d_qtol, nq, d_first, d_count);
+    return hipGetLastError();
+}
+
+// unique-id range [out[0], out[1]) of keys in [klo, khi]
+__global__ void k_key_range(const double* __restrict__ umass, uint32_t nu, int32_t factor, int32_t klo,
+                            int32_t khi, uint64_t* out) {
+    if (threadIdx.x != 0) return;
+    out[0] = klo == (-2147483647 - 1) ? 0u : key_upper(umass, nu, factor, klo - 1);
+    out[1] = key_upper(umass, nu, factor, khi);
+}
+
+hipError_t launch_key_range(const double* d_umass, uint32_t n_unique, int32_t factor, int32_t klo,
+                            int32_t khi, uint64_t* d_out2, hipStream_t s) {
+    hipLaunchKernelGGL(k_key_range, dim3(1), dim3(64), 0, s, d_umass, n_unique, factor, klo, khi, d_out2);
+    return hipGetLastError();
+}
+
+__global__ void k_expand_csr(const uint64_t* __restrict__ first, const uint64_t* __restrict__ count,
+                             const uint64_t* __restrict__ row, uint64_t nq, uint64_t* __restrict__ ids) {
+    const uint64_t q = blockIdx.x;
+    if (q >= nq) return;
+    const uint64_t f = first[q], c = count[q], o = row[q];
+    for (uint64_t k = threadIdx.x; k < c; k += blockDim.x) ids[o + k] = f + k;
+}
+
+hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
+                             uint64_t nq, uint64_t* d_ids, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_expand_csr, dim3((uint32_t)nq), dim3(64), 0, s, d_first, d_count, d_row, nq, d_ids);
+    return hipGetLastError();
+}
+
+// host-supplied occurrences -> records (DBIndexStore.addSequence path)
+__global__ void k_occ_to_recs(const double* __restrict__ mass, const uint32_t* __restrict__ pid,
+                              const uint32_t* __restrict__ off, const uint32_t* __restrict__ len,
+                              const uint32_t* __restrict__ poff, uint64_t n, Rec* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Rec r;
+    r.mass = mass[i];
+    r.gstart = poff[pid[i]] + off[i];
+    r.len = (uint16_t)len[i];
+    r.flags = 0;
+    out[i] = r;
+}
+
+hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const uint32_t* d_off,
+                              const uint32_t* d_len, const uint32_t* d_poff, uint64_t n, Rec* d_out,
+                              hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_occ_to_recs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_mass, d_pid, d_off,
+                       d_len, d_poff, n, d_out);
+    return hipGetLastError();
+}
+
+__global__ void k_off64_to_32(const uint64_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)in[i];
+}
+
+hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_off64_to_32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, d_out, n);
+    return hipGetLastError();
+}
+
+}  // namespace dbi

@@ -1,0 +1,833 @@
+// dbi_engine.hip — host orchestration of the device build and queries behind
+// the batch C-ABI (include/dbindex_hip.h).  One engine = one HIP device, one
+// stream, an HBM-resident index and a workspace that grows but never shrinks
+// (steady-state rebuilds allocate nothing).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dbi_internal.h"
+
+namespace dbi {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    g_err = std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ") in " + what;
+    return e == hipErrorOutOfMemory ? DBI_E_OOM : DBI_E_HIP;
+}
+
+// Growable device buffer.
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;  // elements
+    int ensure(size_t n) {
+        if (n <= cap && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1);
+        hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            return hip_fail(e, "hipMalloc");
+        }
+        cap = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    size_t bytes() const { return cap * sizeof(T); }
+};
+
+}  // namespace dbi
+
+using namespace dbi;
+
+struct dbi_handle {
+    dbi_params params;
+    DevParams dp;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+
+    DevBuf<double> mass_tab;
+    DevBuf<uint8_t> flags_tab;
+    DevBuf<Counters> ctr;
+
+    // inputs (owned copies for host builds)
+    DevBuf<uint8_t> res;
+    DevBuf<uint64_t> poff64;
+    DevBuf<uint32_t> poff;
+    const uint8_t* d_res = nullptr;  // residues the index refers to
+    uint64_t n_res = 0, n_prot = 0;
+
+    // workspace
+    DevBuf<uint32_t> blk;       // digest tile counts / offsets
+    DevBuf<uint32_t> thr;       // digest per-thread counts
+    DevBuf<uint32_t> tile_pf;   // first protein of every digest tile (+1)
+    DevBuf<uint32_t> scan_tmp;
+    DevBuf<Rec> recA, recB;
+    DevBuf<uint32_t> hist;
+    DevBuf<uint32_t> bin_start, ucount, big_list, chunk_lo, chunk_bin;
+    DevBuf<unsigned long long> ws_key;
+    DevBuf<uint32_t> ws_k2;
+
+    // index
+    DevBuf<double> umass;
+    DevBuf<uint32_t> upid, uoff, ulen, occ_off, occ_pid, key_flags;
+    bool built = false;
+
+    // host-input occurrences (addSequence path)
+    DevBuf<double> o_mass;
+    DevBuf<uint32_t> o_pid, o_off, o_len;
+
+    // query scratch
+    DevBuf<double> q_mass, q_tol;
+    DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
+    DevBuf<double> g_mass;
+    DevBuf<uint32_t> g_pid, g_off, g_len;
+    DevBuf<uint64_t> g_b, g_e;
+
+    dbi_stats stats{};
+    Counters hc{};
+    uint64_t n_total_extra = 0;
+
+    // per-launch HIP events on the engine stream (dbi_stage_times)
+    struct Stage {
+        const char* name;
+        int eb, ee;                     // event pool slots
+        double cR, cN, cU, cP, cB;      // algorithmic bytes = cR*R + cN*N + cU*U + cP*P + cB*nbins
+        double ms, bytes;
+    };
+    static constexpr int MAX_STAGES = 48;
+    hipEvent_t evpool[2 * MAX_STAGES] = {};
+    Stage stages[MAX_STAGES];
+    int nstage = 0;
+};
+
+namespace {
+
+int check_params(const dbi_params* p) {
+    if (!p) return set_error(DBI_E_INVALID, "params is NULL");
+    if (p->index_factor <= 0 || p->index_factor > MAX_PRECURSOR_INT)
+        return set_error(DBI_E_INVALID, "index_factor must be in [1, 8000] (BUCKET_MASS_RANGE = 8000/index_factor)");
+    if (!(p->min_mh >= 0.0)) return set_error(DBI_E_INVALID, "min precursor mass must be >= 0");
+    if (!(p->max_mh == p->max_mh)) return set_error(DBI_E_INVALID, "max precursor mass is NaN");
+    if (p->mass_group_factor <= 0) return set_error(DBI_E_INVALID, "mass_group_factor must be > 0");
+    for (int c = 0; c < 256; ++c)
+        if (!(p->mass[c] >= 0.0) || std::isinf(p->mass[c]))
+            return set_error(DBI_E_INVALID, "residue masses must be finite and >= 0");
+    return 0;
+}
+
+DevParams make_dev_params(const dbi_params& p) {
+    DevParams d{};
+    d.min_mh = p.min_mh;
+    d.max_mh = p.max_mh;
+    // DBIndexer.java:265-271: precMass = 0; (+= H2O_PROTON); += cTerm; += nTerm
+    volatile double m = 0;
+    if (p.add_h2o_proton) m = m + p.h2o_proton;
+    m = m + p.cterm;
+    m = m + p.nterm;
+    d.m0 = m;
+    d.max_missed = p.max_missed;
+    d.min_len = p.min_len;
+    d.nb = p.index_factor;
+    d.br = MAX_PRECURSOR_INT / p.index_factor;
+    d.mand_mode = p.mandatory_mode ? 1 : 0;
+    d.mand_filter = (p.mandatory_mode && p.mandatory_count > 0) ? 1 : 0;
+    d.semi = p.semi ? 1 : 0;
+    d.drop_mass = (double)(d.nb * d.br);
+    return d;
+}
+
+uint32_t choose_nbins(uint64_t n) {
+    uint64_t want = n / BIN_AVG;  // fine mass bins; chunks group them to ~CHUNK_T records
+    uint32_t b = 1;
+    while (b < want && b < (1u << 24)) b <<= 1;
+    return b;
+}
+
+int log2_ceil(uint32_t x) {
+    int r = 0;
+    while ((1ull << r) < x) ++r;
+    return r;
+}
+
+int read_counters(dbi_handle* h) {
+    DBI_HIP(hipMemcpyAsync(&h->hc, h->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, h->stream));
+    DBI_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+struct Bytes {
+    double cR = 0, cN = 0, cU = 0, cP = 0, cB = 0;
+};
+
+int stage_begin(dbi_handle* h, const char* name, Bytes b) {
+    if (h->nstage >= dbi_handle::MAX_STAGES) return -1;
+    const int i = h->nstage++;
+    auto& st = h->stages[i];
+    st.name = name;
+    st.eb = 2 * i;
+    st.ee = 2 * i + 1;
+    st.cR = b.cR; st.cN = b.cN; st.cU = b.cU; st.cP = b.cP; st.cB = b.cB;
+    st.ms = 0;
+    st.bytes = 0;
+    (void)hipEventRecord(h->evpool[st.eb], h->stream);
+    return i;
+}
+
+void stage_end(dbi_handle* h, int i) {
+    if (i >= 0) (void)hipEventRecord(h->evpool[h->stages[i].ee], h->stream);
+}
+
+#define STAGE(h, NAME, BYTES, EXPR)               \
+    do {                                          \
+        const int _si = stage_begin(h, NAME, BYTES); \
+        DBI_HIP(EXPR);                            \
+        stage_end(h, _si);                        \
+    } while (0)
+
+Bytes by(double cR, double cN, double cU, double cP, double cB) {
+    Bytes b;
+    b.cR = cR; b.cN = cN; b.cU = cU; b.cP = cP; b.cB = cB;
+    return b;
+}
+
+// Steps 4-6 over n records in recA: partition by mass bin, per-bin sort +
+// dedup, finalize.  lo/hi bound every record mass.
+int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
+    hipStream_t s = h->stream;
+    int rc;
+    const uint32_t n32 = (uint32_t)n;
+    const uint32_t nbins = choose_nbins(n);
+    BinMap bm;
+    bm.lo = lo;
+    bm.nbins = nbins;
+    bm.scale = (hi > lo) ? (double)nbins / (hi - lo) : 0.0;
+    const int total_bits = log2_ceil(nbins);
+    const int passes = (total_bits + RADIX_BITS - 1) / RADIX_BITS;
+    const int bits_per = passes ? (total_bits + passes - 1) / passes : 0;
+    const size_t hist_elems = passes ? radix_hist_elems(n32, bits_per) : 1;
+
+    // every allocation before the first launch of this stage: a reallocation
+    // must never free a buffer that queued kernels still use
+    const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + CHUNK_T - 1) / CHUNK_T, 1);
+    const size_t scan_need = std::max(scan_u32_tmp_elems(hist_elems), scan_u32_tmp_elems(nchunks));
+    if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_need, h->scan_tmp.cap)))) return rc;
+    if ((rc = h->recB.ensure(n)) || (rc = h->hist.ensure(hist_elems)) ||
+        (rc = h->bin_start.ensure((size_t)nbins + 1)) || (rc = h->ucount.ensure(nchunks)) ||
+        (rc = h->chunk_lo.ensure((size_t)nchunks + 1)) || (rc = h->chunk_bin.ensure((size_t)nchunks + 1)) || (rc = h->big_list.ensure(nchunks)) ||
+        (rc = h->ws_key.ensure(4 * n)) || (rc = h->ws_k2.ensure(4 * n)) ||
+        (rc = h->umass.ensure(n)) || (rc = h->upid.ensure(n)) || (rc = h->uoff.ensure(n)) ||
+        (rc = h->ulen.ensure(n)) || (rc = h->occ_off.ensure(n + 1)) || (rc = h->occ_pid.ensure(n)) ||
+        (rc = h->key_flags.ensure(n)))
+        return rc;
+
+    // stable LSD passes over the bin id
+    Rec* src = h->recA.p;
+    Rec* dst = h->recB.p;
+    int shift = 0;
+    for (int ps = 0; ps < passes; ++ps) {
+        const int bits = std::min(bits_per, total_bits - shift);
+        const double hbytes = 8.0 * (double)radix_blocks(n32) * (double)(1u << bits);  // hist write + scan
+        // hist reads the 8-B mass of every record; scatter moves 16 B in + 16 B out
+        STAGE(h, "radix_hist", by(0, 8, 0, 0, 0), launch_radix_hist(src, n32, bm, shift, bits, h->hist.p, s));
+        STAGE(h, "radix_scan", by(0, 0, 0, 0, 0),
+              launch_scan_u32(h->hist.p, h->hist.p, (uint64_t)radix_blocks(n32) << bits, h->scan_tmp.p,
+                              h->scan_tmp.cap, nullptr, s));
+        h->stages[h->nstage - 1].cB = hbytes / std::max<double>(nbins, 1.0);
+        STAGE(h, "radix_scatter", by(0, 32, 0, 0, 0), launch_radix_scatter(src, dst, n32, bm, shift, bits, h->hist.p, s));
+        std::swap(src, dst);
+        shift += bits;
+    }
+    // src: records grouped by bin, insertion order inside each bin
+    STAGE(h, "bin_bounds", by(0, 8, 0, 0, 4), launch_bin_bounds(src, n32, bm, h->bin_start.p, s));
+    // chunk sort: 16 B in + 16 B out per record (+ the residues of every peptide for its hash)
+    STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
+          launch_chunk_bounds(h->bin_start.p, nbins, n32, CHUNK_T, nchunks, h->chunk_lo.p, h->chunk_bin.p, s));
+    STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
+          launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->ucount.p, h->big_list.p, h->ctr.p, s));
+    STAGE(h, "big_chunks", by(0, 0, 0, 0, 0),
+          launch_big_chunks(src, dst, h->chunk_lo.p, h->d_res, h->ucount.p, h->big_list.p,
+                            std::min<uint32_t>(nchunks, 256u), h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
+    // unique offsets per chunk
+    STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
+          launch_scan_u32(h->ucount.p, h->ucount.p, nchunks, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_unique, s));
+    // finalize: 16 B record in, 4 B occurrence protein id out, 24 B per unique out
+    STAGE(h, "finalize", by(0, 20, 24, 0, 0),
+          launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->poff.p, (uint32_t)h->n_prot, h->tile_pf.p,
+                          (uint32_t)h->n_res, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p, h->occ_off.p,
+                          h->occ_pid.p, s));
+    DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s));
+    STAGE(h, "count_keys", by(0, 0, 12, 0, 0),
+          launch_count_keys(h->umass.p, n32, h->params.mass_group_factor, h->key_flags.p, h->ctr.p, s));
+    h->stats.n_bins = nbins;
+    return 0;
+}
+
+int finish_build(dbi_handle* h) {
+    DBI_HIP(hipEventRecord(h->ev1, h->stream));
+    int rc = read_counters(h);
+    if (rc) return rc;
+    if (h->hc.err & ERR_LEN_OVERFLOW) return set_error(DBI_E_INVALID, "peptide longer than 65535 residues");
+    float ms = 0, ms_d = 0;
+    DBI_HIP(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    DBI_HIP(hipEventElapsedTime(&ms_d, h->ev0, h->ev2));
+    dbi_stats& st = h->stats;
+    st.n_residues = h->n_res;
+    st.n_proteins = h->n_prot;
+    st.n_kept = h->hc.n_kept;
+    st.n_dropped = h->hc.n_dropped + h->n_total_extra;
+    st.n_total = st.n_kept + st.n_dropped;
+    st.n_unique = h->hc.n_unique;
+    st.n_keys = h->hc.n_keys;
+    for (int i = 0; i < 8; ++i) st.n_keys += h->hc.n_keys_shard[i];
+    st.n_big_bins = h->hc.n_big;
+    st.build_ms = ms;
+    st.digest_ms = ms_d;
+    for (int i = 0; i < h->nstage; ++i) {
+        auto& sg = h->stages[i];
+        float t = 0;
+        if (hipEventElapsedTime(&t, h->evpool[sg.eb], h->evpool[sg.ee]) != hipSuccess) t = 0;
+        sg.ms = t;
+        sg.bytes = sg.cR * (double)h->n_res + sg.cN * (double)st.n_kept + sg.cU * (double)st.n_unique +
+                   sg.cP * (double)(h->n_prot + 1) + sg.cB * (double)st.n_bins;
+    }
+    size_t bytes = 0;
+    bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
+    bytes += h->thr.bytes() + h->tile_pf.bytes() + h->chunk_lo.bytes();
+    bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->bin_start.bytes() + h->ucount.bytes();
+    bytes += h->big_list.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
+    bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes() + h->key_flags.bytes();
+    st.device_bytes = bytes;
+    h->built = true;
+    return 0;
+}
+
+// per-tile first-protein table (digest tiles + protein-id lookups in finalize)
+int prepare_tiles(dbi_handle* h) {
+    const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
+    int rc;
+    if ((rc = h->tile_pf.ensure((size_t)ntiles + 2))) return rc;
+    STAGE(h, "tile_proteins", by(0, 0, 0, 0, 0),
+          launch_tile_proteins(h->poff.p, (uint32_t)h->n_prot, (uint32_t)h->n_res, h->tile_pf.p, h->stream));
+    return 0;
+}
+
+// Device digest build over residues at d_res (n_res) with u32 offsets in h->poff.
+int build_digest(dbi_handle* h) {
+    hipStream_t s = h->stream;
+    int rc;
+    const uint64_t R = h->n_res;
+    const uint32_t nblk = (uint32_t)((R + DIGEST_TILE - 1) / DIGEST_TILE);
+    if ((rc = h->blk.ensure(std::max<uint32_t>(nblk, 1))) || (rc = h->thr.ensure((size_t)nblk * DIGEST_THREADS + 1)))
+        return rc;
+    if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(nblk), h->scan_tmp.cap)))) return rc;
+    if ((rc = prepare_tiles(h))) return rc;
+    // digest reads every residue once (+ the protein offset table)
+    STAGE(h, "digest_count", by(1, 0, 0, 4, 0),
+          launch_digest_count(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
+                              (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->ctr.p, s));
+    STAGE(h, "digest_scan", by(0, 0, 0, 0, 0),
+          launch_scan_u32(h->blk.p, h->blk.p, nblk, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_kept, s));
+    if ((rc = read_counters(h))) return rc;
+    const uint64_t n = h->hc.n_kept;
+    if (n >= (1ull << 32) - 1)
+        return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences on one device: shard the FASTA");
+    if ((rc = h->recA.ensure(n))) return rc;
+    // digest emit: residues in, one 16-B record per kept occurrence out
+    STAGE(h, "digest_emit", by(1, 16, 0, 4, 0),
+          launch_digest_emit(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
+                             (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->recA.p, h->ctr.p, s));
+    DBI_HIP(hipEventRecord(h->ev2, s));
+    return build_tail(h, n, h->params.min_mh, h->params.max_mh);
+}
+
+int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
+    if (n_res >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_res must be < 2^32-1 per device: shard the FASTA");
+    if (n_prot >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_prot must be < 2^32-1");
+    DBI_HIP(hipSetDevice(h->device));
+    h->built = false;
+    h->n_res = n_res;
+    h->n_prot = n_prot;
+    h->n_total_extra = 0;
+    std::memset(&h->stats, 0, sizeof(h->stats));
+    h->nstage = 0;
+    DBI_HIP(hipEventRecord(h->ev0, h->stream));
+    DBI_HIP(hipMemsetAsync(h->ctr.p, 0, sizeof(Counters), h->stream));
+    return 0;
+}
+
+int check_offsets_host(const uint64_t* off, uint64_t n_res, uint64_t n_prot) {
+    if (off[0] != 0) return set_error(DBI_E_INVALID, "prot_off[0] must be 0");
+    if (off[n_prot] != n_res) return set_error(DBI_E_INVALID, "prot_off[n_prot] must equal n_res");
+    for (uint64_t i = 0; i < n_prot; ++i)
+        if (off[i + 1] < off[i]) return set_error(DBI_E_INVALID, "prot_off must be non-decreasing");
+    return 0;
+}
+
+int check_residues_host(const uint8_t* res, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i)
+        if (res[i] == '[') return set_error(DBI_E_INVALID, "inline '[formula]' PTMs are not supported (DBIndexer.java:288-303)");
+    return 0;
+}
+
+int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off, uint64_t n_prot) {
+    int rc;
+    if ((rc = h->res.ensure(n_res + 16))) return rc;
+    if ((rc = h->poff.ensure(n_prot + 1))) return rc;
+    std::vector<uint32_t> off32(n_prot + 1);
+    for (uint64_t i = 0; i <= n_prot; ++i) off32[i] = (uint32_t)prot_off[i];
+    if (n_res) DBI_HIP(hipMemcpyAsync(h->res.p, residues, n_res, hipMemcpyHostToDevice, h->stream));
+    DBI_HIP(hipMemcpyAsync(h->poff.p, off32.data(), sizeof(uint32_t) * (n_prot + 1), hipMemcpyHostToDevice, h->stream));
+    DBI_HIP(hipStreamSynchronize(h->stream));  // off32 is a stack vector
+    h->d_res = h->res.p;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dbi_last_error(void) { return g_err.c_str(); }
+
+int dbi_dev_alloc(int device, uint64_t bytes, void** out) {
+    if (!out) return set_error(DBI_E_INVALID, "NULL argument");
+    DBI_HIP(hipSetDevice(device));
+    DBI_HIP(hipMalloc(out, std::max<uint64_t>(bytes, 1)));
+    return 0;
+}
+
+int dbi_dev_free(int device, void* p) {
+    DBI_HIP(hipSetDevice(device));
+    if (p) DBI_HIP(hipFree(p));
+    return 0;
+}
+
+int dbi_dev_copy_h2d(int device, void* dst, const void* src, uint64_t bytes) {
+    DBI_HIP(hipSetDevice(device));
+    if (bytes) DBI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int dbi_dev_copy_d2h(int device, void* dst, const void* src, uint64_t bytes) {
+    DBI_HIP(hipSetDevice(device));
+    if (bytes) DBI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int dbi_dev_synchronize(int device) {
+    DBI_HIP(hipSetDevice(device));
+    DBI_HIP(hipDeviceSynchronize());
+    return 0;
+}
+int dbi_abi_version(void) { return DBI_ABI_VERSION; }
+
+int dbi_device_count(int* out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return 0;
+}
+
+void dbi_params_default(dbi_params* p, int32_t max_missed, int32_t semi) {
+    std::memset(p, 0, sizeof(*p));
+    // pinned monoisotopic residue masses (Unimod), see dbindex_amd/params.py
+    static const struct { char c; double m; } tab[] = {
+        {'G', 57.021464},  {'A', 71.037114},  {'S', 87.032028},  {'P', 97.052764},  {'V', 99.068414},
+        {'T', 101.047679}, {'C', 103.009185}, {'L', 113.084064}, {'I', 113.084064}, {'N', 114.042927},
+        {'D', 115.026943}, {'Q', 128.058578}, {'K', 128.094963}, {'E', 129.042593}, {'M', 131.040485},
+        {'H', 137.058912}, {'F', 147.068414}, {'R', 156.101111}, {'Y', 163.063329}, {'W', 186.079313},
+        {'U', 150.953636}, {'O', 237.147727},
+    };
+    for (const auto& t : tab) p->mass[(unsigned char)t.c] = t.m;
+    p->min_mh = 500.0;    // default_min_precursor_mass (dbindex.properties:9)
+    p->max_mh = 6000.0;   // default_max_precursor_mass (dbindex.properties:8)
+    p->h2o_proton = 18.0105646863 + 1.00727646688;
+    p->cleave[(unsigned char)'K'] = 1;  // default_enzyme_residues=KR (dbindex.properties:12)
+    p->cleave[(unsigned char)'R'] = 1;
+    p->max_missed = max_missed;
+    p->semi = semi;
+    p->add_h2o_proton = 1;
+    p->min_len = 6;
+    p->mass_group_factor = 10000;
+    p->index_factor = 8;
+}
+
+int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
+    if (!out) return set_error(DBI_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int rc = check_params(params);
+    if (rc) return rc;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) return set_error(DBI_E_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return set_error(DBI_E_INVALID, "device ordinal out of range");
+    DBI_HIP(hipSetDevice(device));
+    dbi_handle* h = new dbi_handle();
+    h->params = *params;
+    h->dp = make_dev_params(*params);
+    h->device = device;
+    auto fail = [&](int code) {
+        dbi_close(h);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(set_error(DBI_E_HIP, "hipStreamCreate failed"));
+    if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+        hipEventCreate(&h->ev2) != hipSuccess)
+        return fail(set_error(DBI_E_HIP, "hipEventCreate failed"));
+    for (auto& ev : h->evpool)
+        if (hipEventCreate(&ev) != hipSuccess) return fail(set_error(DBI_E_HIP, "hipEventCreate failed"));
+    if ((rc = h->mass_tab.ensure(256)) || (rc = h->flags_tab.ensure(256)) || (rc = h->ctr.ensure(1)))
+        return fail(rc);
+    uint8_t fl[256];
+    for (int c = 0; c < 256; ++c)
+        fl[c] = (params->cleave[c] ? F_CLEAVE : 0) | (params->nocut[c] ? F_NOCUT : 0) |
+                (params->mandatory[c] ? F_MAND : 0);
+    if (hipMemcpy(h->mass_tab.p, params->mass, sizeof(double) * 256, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->flags_tab.p, fl, 256, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(h->ctr.p, 0, sizeof(Counters)) != hipSuccess)
+        return fail(set_error(DBI_E_HIP, "parameter upload failed"));
+    *out = h;
+    return 0;
+}
+
+void dbi_close(dbi_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
+    h->res.release(); h->poff64.release(); h->poff.release(); h->blk.release(); h->scan_tmp.release();
+    h->thr.release(); h->tile_pf.release(); h->chunk_lo.release(); h->chunk_bin.release();
+    h->recA.release(); h->recB.release(); h->hist.release(); h->bin_start.release(); h->ucount.release();
+    h->big_list.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
+    h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release(); h->key_flags.release();
+    h->o_mass.release(); h->o_pid.release(); h->o_off.release(); h->o_len.release();
+    h->q_mass.release(); h->q_tol.release(); h->q_first.release(); h->q_count.release(); h->q_row.release();
+    h->q_ids.release(); h->g_mass.release(); h->g_pid.release(); h->g_off.release(); h->g_len.release();
+    h->g_b.release(); h->g_e.release();
+    for (auto& ev : h->evpool)
+        if (ev) (void)hipEventDestroy(ev);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->ev2) (void)hipEventDestroy(h->ev2);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int dbi_build(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off, uint64_t n_prot) {
+    if (!h || (!residues && n_res) || !prot_off) return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = check_offsets_host(prot_off, n_res, n_prot))) return rc;
+    if ((rc = check_residues_host(residues, n_res))) return rc;
+    if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
+    DBI_HIP(hipEventRecord(h->ev0, h->stream));  // device time excludes the H2D copy
+    if ((rc = build_digest(h))) return rc;
+    return finish_build(h);
+}
+
+int dbi_build_device(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, const uint64_t* d_prot_off,
+                     uint64_t n_prot, void* stream) {
+    if (!h || (!d_residues && n_res) || !d_prot_off) return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    hipStream_t user = (hipStream_t)stream;
+    if (user) {
+        // order the engine stream after the caller's producer work
+        hipEvent_t ev;
+        DBI_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        DBI_HIP(hipEventRecord(ev, user));
+        DBI_HIP(hipStreamWaitEvent(h->stream, ev, 0));
+        DBI_HIP(hipEventDestroy(ev));
+    }
+    if ((rc = h->poff.ensure(n_prot + 1))) return rc;
+    DBI_HIP(launch_off64_to_32(d_prot_off, h->poff.p, n_prot + 1, h->stream));
+    h->d_res = d_residues;
+    if ((rc = build_digest(h))) return rc;
+    return finish_build(h);
+}
+
+int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off,
+                          uint64_t n_prot, const double* mass, const uint32_t* prot_id, const uint32_t* offset,
+                          const uint32_t* length, uint64_t n_occ, uint64_t n_dropped_extra) {
+    if (!h || (!residues && n_res) || !prot_off || (n_occ && (!mass || !prot_id || !offset || !length)))
+        return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = check_offsets_host(prot_off, n_res, n_prot))) return rc;
+    if (n_occ >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "too many occurrences for one device");
+    double lo = 0, hi = 0;
+    for (uint64_t i = 0; i < n_occ; ++i) {
+        if (!(mass[i] >= 0.0) || std::isinf(mass[i])) return set_error(DBI_E_INVALID, "occurrence mass must be finite and >= 0");
+        if (prot_id[i] >= n_prot) return set_error(DBI_E_INVALID, "occurrence protein id out of range");
+        const uint64_t plen = prot_off[prot_id[i] + 1] - prot_off[prot_id[i]];
+        if ((uint64_t)offset[i] + length[i] > plen || length[i] == 0 || length[i] > 0xFFFFu)
+            return set_error(DBI_E_INVALID, "occurrence offset/length outside its protein");
+        if (i == 0 || mass[i] < lo) lo = mass[i];
+        if (i == 0 || mass[i] > hi) hi = mass[i];
+    }
+    if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
+    DBI_HIP(hipEventRecord(h->ev0, h->stream));
+    if ((rc = h->o_mass.ensure(n_occ)) || (rc = h->o_pid.ensure(n_occ)) || (rc = h->o_off.ensure(n_occ)) ||
+        (rc = h->o_len.ensure(n_occ)) || (rc = h->recA.ensure(n_occ)))
+        return rc;
+    if (n_occ) {
+        DBI_HIP(hipMemcpyAsync(h->o_mass.p, mass, 8 * n_occ, hipMemcpyHostToDevice, h->stream));
+        DBI_HIP(hipMemcpyAsync(h->o_pid.p, prot_id, 4 * n_occ, hipMemcpyHostToDevice, h->stream));
+        DBI_HIP(hipMemcpyAsync(h->o_off.p, offset, 4 * n_occ, hipMemcpyHostToDevice, h->stream));
+        DBI_HIP(hipMemcpyAsync(h->o_len.p, length, 4 * n_occ, hipMemcpyHostToDevice, h->stream));
+    }
+    DBI_HIP(launch_occ_to_recs(h->o_mass.p, h->o_pid.p, h->o_off.p, h->o_len.p, h->poff.p, n_occ, h->recA.p,
+                               h->stream));
+    // n_kept known on the host: seed the device counter
+    Counters c0{};
+    c0.n_kept = n_occ;
+    DBI_HIP(hipMemcpyAsync(h->ctr.p, &c0, sizeof(Counters), hipMemcpyHostToDevice, h->stream));
+    DBI_HIP(hipStreamSynchronize(h->stream));
+    DBI_HIP(hipEventRecord(h->ev2, h->stream));
+    h->n_total_extra = n_dropped_extra;
+    if ((rc = prepare_tiles(h))) return rc;
+    if ((rc = build_tail(h, n_occ, lo, hi))) return rc;
+    return finish_build(h);
+}
+
+int dbi_stats_get(dbi_handle* h, dbi_stats* out) {
+    if (!h || !out) return set_error(DBI_E_INVALID, "NULL argument");
+    *out = h->stats;
+    return 0;
+}
+
+int dbi_query_device(dbi_handle* h, const double* d_mass, const double* d_tol, uint64_t nq, uint64_t* d_first,
+                     uint64_t* d_count, void* stream) {
+    if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    DBI_HIP(hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    DBI_HIP(launch_query(h->dp, h->params.mass_group_factor, h->umass.p, (uint32_t)h->stats.n_unique, d_mass,
+                         d_tol, nq, d_first, d_count, s));
+    return 0;
+}
+
+int dbi_query(dbi_handle* h, const double* mass, const double* tol, uint64_t nq, uint64_t* first, uint64_t* count) {
+    if (!h || (nq && (!mass || !tol || !first || !count))) return set_error(DBI_E_INVALID, "NULL argument");
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    if (nq == 0) return 0;
+    DBI_HIP(hipSetDevice(h->device));
+    int rc;
+    if ((rc = h->q_mass.ensure(nq)) || (rc = h->q_tol.ensure(nq)) || (rc = h->q_first.ensure(nq)) ||
+        (rc = h->q_count.ensure(nq)))
+        return rc;
+    DBI_HIP(hipMemcpyAsync(h->q_mass.p, mass, 8 * nq, hipMemcpyHostToDevice, h->stream));
+    DBI_HIP(hipMemcpyAsync(h->q_tol.p, tol, 8 * nq, hipMemcpyHostToDevice, h->stream));
+    if ((rc = dbi_query_device(h, h->q_mass.p, h->q_tol.p, nq, h->q_first.p, h->q_count.p, h->stream))) return rc;
+    DBI_HIP(hipMemcpyAsync(first, h->q_first.p, 8 * nq, hipMemcpyDeviceToHost, h->stream));
+    DBI_HIP(hipMemcpyAsync(count, h->q_count.p, 8 * nq, hipMemcpyDeviceToHost, h->stream));
+    DBI_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int dbi_query_csr(dbi_handle* h, const double* mass, const double* tol, uint64_t nq, dbi_query_result** out) {
+    if (!out) return set_error(DBI_E_INVALID, "NULL argument");
+    *out = nullptr;
+    std::vector<uint64_t> first(nq), count(nq);
+    int rc = dbi_query(h, mass, tol, nq, first.data(), count.data());
+    if (rc) return rc;
+    dbi_query_result* r = (dbi_query_result*)std::calloc(1, sizeof(dbi_query_result));
+    if (!r) return set_error(DBI_E_OOM, "calloc");
+    r->nq = nq;
+    r->row_ptr = (uint64_t*)std::malloc(8 * (nq + 1));
+    uint64_t tot = 0;
+    for (uint64_t i = 0; i < nq; ++i) {
+        r->row_ptr[i] = tot;
+        tot += count[i];
+    }
+    r->row_ptr[nq] = tot;
+    r->n_hits = tot;
+    r->ids = (uint64_t*)std::malloc(8 * std::max<uint64_t>(tot, 1));
+    if (!r->row_ptr || !r->ids) {
+        dbi_query_result_free(r);
+        return set_error(DBI_E_OOM, "malloc");
+    }
+    if (tot) {
+        if ((rc = h->q_row.ensure(nq + 1)) || (rc = h->q_ids.ensure(tot))) {
+            dbi_query_result_free(r);
+            return rc;
+        }
+        hipError_t e = hipMemcpyAsync(h->q_row.p, r->row_ptr, 8 * (nq + 1), hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = launch_expand_csr(h->q_first.p, h->q_count.p, h->q_row.p, nq, h->q_ids.p, h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(r->ids, h->q_ids.p, 8 * tot, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) {
+            dbi_query_result_free(r);
+            return hip_fail(e, "dbi_query_csr");
+        }
+    }
+    *out = r;
+    return 0;
+}
+
+void dbi_query_result_free(dbi_query_result* r) {
+    if (!r) return;
+    std::free(r->row_ptr);
+    std::free(r->ids);
+    std::free(r);
+}
+
+int dbi_peptides(dbi_handle* h, const uint64_t* ids, uint64_t n, double* mass, uint32_t* prot_id, uint32_t* offset,
+                 uint32_t* length, uint64_t* occ_begin, uint64_t* occ_end) {
+    if (!h || (n && !ids)) return set_error(DBI_E_INVALID, "NULL argument");
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    if (n == 0) return 0;
+    for (uint64_t i = 0; i < n; ++i)
+        if (ids[i] >= h->stats.n_unique) return set_error(DBI_E_INVALID, "peptide id out of range");
+    DBI_HIP(hipSetDevice(h->device));
+    int rc;
+    if ((rc = h->q_ids.ensure(n)) || (rc = h->g_mass.ensure(n)) || (rc = h->g_pid.ensure(n)) ||
+        (rc = h->g_off.ensure(n)) || (rc = h->g_len.ensure(n)) || (rc = h->g_b.ensure(n)) || (rc = h->g_e.ensure(n)))
+        return rc;
+    hipStream_t s = h->stream;
+    DBI_HIP(hipMemcpyAsync(h->q_ids.p, ids, 8 * n, hipMemcpyHostToDevice, s));
+    DBI_HIP(launch_gather(h->q_ids.p, n, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p, h->occ_off.p, h->g_mass.p,
+                          h->g_pid.p, h->g_off.p, h->g_len.p, h->g_b.p, h->g_e.p, s));
+    if (mass) DBI_HIP(hipMemcpyAsync(mass, h->g_mass.p, 8 * n, hipMemcpyDeviceToHost, s));
+    if (prot_id) DBI_HIP(hipMemcpyAsync(prot_id, h->g_pid.p, 4 * n, hipMemcpyDeviceToHost, s));
+    if (offset) DBI_HIP(hipMemcpyAsync(offset, h->g_off.p, 4 * n, hipMemcpyDeviceToHost, s));
+    if (length) DBI_HIP(hipMemcpyAsync(length, h->g_len.p, 4 * n, hipMemcpyDeviceToHost, s));
+    if (occ_begin) DBI_HIP(hipMemcpyAsync(occ_begin, h->g_b.p, 8 * n, hipMemcpyDeviceToHost, s));
+    if (occ_end) DBI_HIP(hipMemcpyAsync(occ_end, h->g_e.p, 8 * n, hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+int dbi_occurrences(dbi_handle* h, uint64_t begin, uint64_t end, uint32_t* prot_id) {
+    if (!h || !prot_id) return set_error(DBI_E_INVALID, "NULL argument");
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    if (begin > end || end > h->stats.n_kept) return set_error(DBI_E_INVALID, "occurrence range out of bounds");
+    if (end == begin) return 0;
+    DBI_HIP(hipSetDevice(h->device));
+    DBI_HIP(hipMemcpyAsync(prot_id, h->occ_pid.p + begin, 4 * (end - begin), hipMemcpyDeviceToHost, h->stream));
+    DBI_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int dbi_export(dbi_handle* h, double* mass, uint32_t* prot_id, uint32_t* offset, uint32_t* length, uint64_t* occ_off,
+               uint32_t* occ_prot) {
+    if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    DBI_HIP(hipSetDevice(h->device));
+    const uint64_t U = h->stats.n_unique, K = h->stats.n_kept;
+    hipStream_t s = h->stream;
+    std::vector<uint32_t> oo;
+    if (mass && U) DBI_HIP(hipMemcpyAsync(mass, h->umass.p, 8 * U, hipMemcpyDeviceToHost, s));
+    if (prot_id && U) DBI_HIP(hipMemcpyAsync(prot_id, h->upid.p, 4 * U, hipMemcpyDeviceToHost, s));
+    if (offset && U) DBI_HIP(hipMemcpyAsync(offset, h->uoff.p, 4 * U, hipMemcpyDeviceToHost, s));
+    if (length && U) DBI_HIP(hipMemcpyAsync(length, h->ulen.p, 4 * U, hipMemcpyDeviceToHost, s));
+    if (occ_off) {
+        oo.resize(U + 1);
+        DBI_HIP(hipMemcpyAsync(oo.data(), h->occ_off.p, 4 * (U + 1), hipMemcpyDeviceToHost, s));
+    }
+    if (occ_prot && K) DBI_HIP(hipMemcpyAsync(occ_prot, h->occ_pid.p, 4 * K, hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    if (occ_off)
+        for (uint64_t i = 0; i <= U; ++i) occ_off[i] = oo[i];
+    return 0;
+}
+
+int dbi_entry_keys(dbi_handle* h, int32_t* keys, uint64_t cap, uint64_t* n) {
+    if (!h || !n) return set_error(DBI_E_INVALID, "NULL argument");
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    *n = h->stats.n_keys;
+    if (!keys) return 0;
+    if (cap < h->stats.n_keys) return set_error(DBI_E_INVALID, "keys buffer too small");
+    const uint64_t U = h->stats.n_unique;
+    if (U == 0) return 0;
+    DBI_HIP(hipSetDevice(h->device));
+    DevBuf<uint32_t> pos;
+    DevBuf<int32_t> dk;
+    int rc;
+    if ((rc = pos.ensure(U)) || (rc = dk.ensure(h->stats.n_keys))) {
+        pos.release();
+        dk.release();
+        return rc;
+    }
+    if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(U), h->scan_tmp.cap)))) return rc;
+    hipError_t e = launch_scan_u32(h->key_flags.p, pos.p, U, h->scan_tmp.p, h->scan_tmp.cap, nullptr, h->stream);
+    if (e == hipSuccess)
+        e = launch_write_keys(h->umass.p, (uint32_t)U, h->params.mass_group_factor, pos.p, dk.p, h->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(keys, dk.p, 4 * h->stats.n_keys, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    pos.release();
+    dk.release();
+    if (e != hipSuccess) return hip_fail(e, "dbi_entry_keys");
+    return 0;
+}
+
+int dbi_stage_times(dbi_handle* h, const char** names, double* ms, double* bytes, uint64_t cap, uint64_t* n) {
+    if (!h || !n) return set_error(DBI_E_INVALID, "NULL argument");
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    *n = (uint64_t)h->nstage;
+    for (int i = 0; i < h->nstage && (uint64_t)i < cap; ++i) {
+        if (names) names[i] = h->stages[i].name;
+        if (ms) ms[i] = h->stages[i].ms;
+        if (bytes) bytes[i] = h->stages[i].bytes;
+    }
+    return 0;
+}
+
+int dbi_device_view(dbi_handle* h, dbi_device_index* out) {
+    if (!h || !out) return set_error(DBI_E_INVALID, "NULL argument");
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    out->mass = h->umass.p;
+    out->prot_id = h->upid.p;
+    out->offset = h->uoff.p;
+    out->length = h->ulen.p;
+    out->occ_off = h->occ_off.p;
+    out->occ_prot = h->occ_pid.p;
+    out->n_unique = h->stats.n_unique;
+    out->n_kept = h->stats.n_kept;
+    return 0;
+}
+
+}  // extern "C"
+
+// ---- internal accessors used by the store mirror (dbi_store.cpp) ----------------
+namespace dbi {
+int engine_key_range(dbi_handle* h, int32_t klo, int32_t khi, uint64_t* b, uint64_t* e) {
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    DBI_HIP(hipSetDevice(h->device));
+    int rc;
+    if ((rc = h->q_first.ensure(2))) return rc;
+    DBI_HIP(launch_key_range(h->umass.p, (uint32_t)h->stats.n_unique, h->params.mass_group_factor, klo, khi,
+                             h->q_first.p, h->stream));
+    uint64_t r[2];
+    DBI_HIP(hipMemcpyAsync(r, h->q_first.p, 16, hipMemcpyDeviceToHost, h->stream));
+    DBI_HIP(hipStreamSynchronize(h->stream));
+    *b = r[0];
+    *e = r[1];
+    return 0;
+}
+bool engine_built(const dbi_handle* h) { return h && h->built; }
+const dbi_params& engine_params(const dbi_handle* h) { return h->params; }
+}  // namespace dbi

@@ -1,0 +1,155 @@
+// dbi_internal.h — shared between the device kernels (dbi_device.hip) and the
+// host orchestration (dbi_engine.hip, dbi_store.cpp).  Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/dbindex_hip.h"
+
+namespace dbi {
+
+// Occurrence record as it moves through the build: 16 B, HBM-aligned.
+//   mass   : MH+ (fp64, bit-identical to the reference's sequential sum)
+//   gstart : global residue position of the first residue (protein offset + start)
+//   len    : peptide length (curSeqI, DBIndexer.java:309,388)
+//   flags  : bit0 = first occurrence of its unique peptide (set by the bin sort)
+struct alignas(16) Rec {
+    double mass;
+    uint32_t gstart;
+    uint16_t len;
+    uint16_t flags;
+};
+static_assert(sizeof(Rec) == 16, "Rec must be 16 bytes");
+
+constexpr int MAX_PRECURSOR_INT = 8000;  // (int) Constants.MAX_PRECURSOR_MASS
+
+// Residue class bits, one byte per char, staged in LDS by the digest kernels.
+constexpr uint8_t F_CLEAVE = 1;
+constexpr uint8_t F_NOCUT = 2;
+constexpr uint8_t F_MAND = 4;
+
+// Device-side copy of the parameters the kernels need (kernel argument).
+struct DevParams {
+    double min_mh, max_mh;
+    double m0;                // ((0 + H2O_PROTON) + cTerm) + nTerm, Java order
+    int32_t max_missed;
+    int32_t min_len;
+    int32_t nb;               // NUM_BUCKETS
+    int32_t br;               // BUCKET_MASS_RANGE
+    int32_t mand_mode;        // 0 null, 1 non-null
+    int32_t mand_filter;      // mand_mode && count > 0 (filterSequence path)
+    int32_t semi;
+    double drop_mass;         // bucket > NUM_BUCKETS-1  <=>  (int)m >= nb*br  <=>  m >= nb*br
+};
+
+// Device counters block (one per engine), read back once per build.
+struct Counters {
+    unsigned long long n_kept;     // occurrences stored
+    unsigned long long n_dropped;  // bucket > NUM_BUCKETS-1
+    unsigned long long n_unique;
+    unsigned long long n_keys;
+    unsigned long long n_keys_shard[8];  // per-XCD-group partial key counts (summed on readback)
+    unsigned int n_big;            // bins above the LDS capacity
+    unsigned int err;              // device error bits
+    unsigned int pad[2];
+};
+constexpr unsigned ERR_LEN_OVERFLOW = 1;  // peptide longer than 65535 residues
+
+// Tunables
+constexpr int DIGEST_THREADS = 256;
+constexpr int DIGEST_TILE = 2048;   // starts per digest block
+constexpr int DIGEST_HALO = 256;    // residues staged past the tile
+constexpr int RADIX_BITS = 9;        // max digit width (512 buckets)
+constexpr int RADIX_THREADS = 256;
+constexpr int RADIX_ITEMS = 16;     // records per thread per radix block
+constexpr int CHUNK_THREADS = 256;
+constexpr int CHUNK_CAP = 2048;     // records per chunk sorted in LDS
+constexpr int CHUNK_T = 1024;       // target chunk size (whole mass bins, ~T..T+maxbin)
+constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
+constexpr int BIG_THREADS = 1024;
+
+// ---- launchers (dbi_device.hip) -------------------------------------------------
+// All return hipError_t of the launch.
+hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res, uint32_t* d_tile_pf,
+                                hipStream_t s);
+hipError_t launch_digest_count(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                               const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
+                               uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr,
+                               Counters* d_ctr, hipStream_t s);
+hipError_t launch_digest_emit(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                              const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
+                              uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk_off, uint32_t* d_thr,
+                              Rec* d_out, Counters* d_ctr, hipStream_t s);
+// exclusive scan of n u32 values into out (may alias), total written to *d_total
+hipError_t launch_scan_u32(const uint32_t* d_in, uint32_t* d_out, uint64_t n, uint32_t* d_block_tmp,
+                           uint64_t tmp_elems, unsigned long long* d_total, hipStream_t s);
+size_t scan_u32_tmp_elems(uint64_t n);
+
+struct BinMap {
+    double lo;
+    double scale;     // nbins / (hi - lo)
+    uint32_t nbins;
+};
+hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, uint32_t* d_hist,
+                             hipStream_t s);
+hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
+                                const uint32_t* d_hist, hipStream_t s);
+uint64_t radix_blocks(uint32_t n);
+size_t radix_hist_elems(uint32_t n, int bits);
+hipError_t launch_bin_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t* d_bin_start,
+                             hipStream_t s);
+hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint32_t n, uint32_t T, uint32_t nchunks,
+                               uint32_t* d_chunk_lo, uint32_t* d_chunk_bin, hipStream_t s);
+hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
+                             uint32_t nchunks, const uint8_t* d_res, uint32_t* d_ucount, uint32_t* d_big_list,
+                             Counters* d_ctr, hipStream_t s);
+hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
+                             uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t max_blocks,
+                             unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr, hipStream_t s);
+hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
+                           const uint32_t* d_poff, uint32_t n_prot, const uint32_t* d_tile_pf, uint32_t n_res,
+                           double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
+                           uint32_t* d_occ_off, uint32_t* d_occ_pid, hipStream_t s);
+hipError_t launch_count_keys(const double* d_umass, uint32_t n_upper, int32_t factor,
+                             uint32_t* d_flags, Counters* d_ctr, hipStream_t s);
+hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s);
+hipError_t launch_gather(const uint64_t* d_ids, uint64_t n, const double* d_umass, const uint32_t* d_upid,
+                         const uint32_t* d_uoff, const uint32_t* d_ulen, const uint32_t* d_occ_off,
+                         double* o_mass, uint32_t* o_pid, uint32_t* o_off, uint32_t* o_len, uint64_t* o_b,
+                         uint64_t* o_e, hipStream_t s);
+hipError_t launch_write_keys(const double* d_umass, uint32_t n_unique, int32_t factor,
+                             const uint32_t* d_pos, int32_t* d_keys, hipStream_t s);
+hipError_t launch_query(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,
+                        const double* d_qmass, const double* d_qtol, uint64_t nq,
+                        uint64_t* d_first, uint64_t* d_count, hipStream_t s);
+hipError_t launch_key_range(const double* d_umass, uint32_t n_unique, int32_t factor, int32_t klo,
+                            int32_t khi, uint64_t* d_out2, hipStream_t s);
+hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const uint32_t* d_off,
+                              const uint32_t* d_len, const uint32_t* d_poff, uint64_t n, Rec* d_out,
+                              hipStream_t s);
+hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s);
+hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
+                             uint64_t nq, uint64_t* d_ids, hipStream_t s);
+
+// ---- error plumbing (dbi_engine.hip) ------------------------------------------------
+int set_error(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+// Java (int) cast of a double (JLS 5.1.3), host+device.
+__host__ __device__ inline int32_t java_d2i(double d) {
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return 2147483647;
+    if (d <= -2147483648.0) return (-2147483647 - 1);
+    return (int32_t)d;
+}
+
+}  // namespace dbi
+
+#define DBI_HIP(expr)                                          \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) return ::dbi::hip_fail(_e, #expr); \
+    } while (0)

@@ -1,0 +1,181 @@
+"""Batch engine: the device-resident peptide index behind the C-ABI
+(``dbi_open`` / ``dbi_build*`` / ``dbi_query*`` / ``dbi_peptides`` ...).
+
+Inputs are numpy arrays (copied to HBM) or device pointers (``build_device`` /
+``query_device``, e.g. from ``torch.Tensor.data_ptr()`` on a ROCm tensor), so
+the timed path can start with residues already resident in HBM.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _native
+from ._native import DbiDeviceIndex, DbiQueryResult, DbiStats, check
+from .fasta import PackedProteins
+from .params import DBIndexSearchParams, DbiParams
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+@dataclass
+class BuildStats:
+    n_residues: int
+    n_proteins: int
+    n_total: int      # totalSeqCount: peptides indexed (incl. bucket-dropped)
+    n_dropped: int
+    n_kept: int
+    n_unique: int
+    n_keys: int       # getNumberSequences(): distinct mass-key rows
+    n_bins: int
+    n_big_bins: int
+    device_bytes: int
+    build_ms: float
+    digest_ms: float
+
+
+class Engine:
+    def __init__(self, params, device: int = 0):
+        if isinstance(params, DBIndexSearchParams):
+            params = params.to_c()
+        assert isinstance(params, DbiParams)
+        self.cparams = params
+        self.device = device
+        h = ctypes.c_void_p()
+        check(_native.lib().dbi_open(ctypes.byref(params), device, ctypes.byref(h)))
+        self.h = h
+        self._keep = None
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            _native.lib().dbi_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- build ---------------------------------------------------------------
+    def build(self, proteins: PackedProteins) -> BuildStats:
+        res = np.ascontiguousarray(proteins.residues, dtype=np.uint8)
+        off = np.ascontiguousarray(proteins.offsets, dtype=np.uint64)
+        check(_native.lib().dbi_build(self.h, _p(res), res.shape[0], _p(off), off.shape[0] - 1))
+        return self.stats()
+
+    def build_device(self, d_residues: int, n_res: int, d_offsets: int, n_prot: int,
+                     stream: int = 0) -> BuildStats:
+        check(_native.lib().dbi_build_device(self.h, ctypes.c_void_p(d_residues), n_res,
+                                             ctypes.c_void_p(d_offsets), n_prot,
+                                             ctypes.c_void_p(stream) if stream else None))
+        return self.stats()
+
+    def build_occurrences(self, proteins: PackedProteins, mass, prot_id, offset, length,
+                          n_dropped_extra: int = 0) -> BuildStats:
+        res = np.ascontiguousarray(proteins.residues, dtype=np.uint8)
+        off = np.ascontiguousarray(proteins.offsets, dtype=np.uint64)
+        m = np.ascontiguousarray(mass, np.float64)
+        pid = np.ascontiguousarray(prot_id, np.uint32)
+        o = np.ascontiguousarray(offset, np.uint32)
+        ln = np.ascontiguousarray(length, np.uint32)
+        check(_native.lib().dbi_build_occurrences(self.h, _p(res), res.shape[0], _p(off), off.shape[0] - 1,
+                                                  _p(m), _p(pid), _p(o), _p(ln), m.shape[0], n_dropped_extra))
+        return self.stats()
+
+    def stats(self) -> BuildStats:
+        st = DbiStats()
+        check(_native.lib().dbi_stats_get(self.h, ctypes.byref(st)))
+        return BuildStats(*[getattr(st, f) for f, _ in DbiStats._fields_])
+
+    # -- queries -------------------------------------------------------------
+    def query(self, mass, tol) -> Tuple[np.ndarray, np.ndarray]:
+        """(first, count) per query: ids first..first+count-1 of the mass-sorted
+        unique table (getSequences(m, tol) semantics)."""
+        m = np.ascontiguousarray(np.atleast_1d(mass), np.float64)
+        t = np.ascontiguousarray(np.broadcast_to(np.atleast_1d(tol), m.shape), np.float64)
+        first = np.zeros(m.shape[0], np.uint64)
+        count = np.zeros(m.shape[0], np.uint64)
+        check(_native.lib().dbi_query(self.h, _p(m), _p(t), m.shape[0], _p(first), _p(count)))
+        return first, count
+
+    def query_device(self, d_mass: int, d_tol: int, nq: int, d_first: int, d_count: int,
+                     stream: int = 0) -> None:
+        check(_native.lib().dbi_query_device(self.h, ctypes.c_void_p(d_mass), ctypes.c_void_p(d_tol), nq,
+                                             ctypes.c_void_p(d_first), ctypes.c_void_p(d_count),
+                                             ctypes.c_void_p(stream) if stream else None))
+
+    def query_csr(self, mass, tol) -> Tuple[np.ndarray, np.ndarray]:
+        m = np.ascontiguousarray(np.atleast_1d(mass), np.float64)
+        t = np.ascontiguousarray(np.broadcast_to(np.atleast_1d(tol), m.shape), np.float64)
+        r = ctypes.POINTER(DbiQueryResult)()
+        check(_native.lib().dbi_query_csr(self.h, _p(m), _p(t), m.shape[0], ctypes.byref(r)))
+        try:
+            nq, nh = r.contents.nq, r.contents.n_hits
+            row = np.ctypeslib.as_array(r.contents.row_ptr, shape=(nq + 1,)).copy()
+            ids = np.ctypeslib.as_array(r.contents.ids, shape=(max(nh, 1),))[:nh].copy()
+        finally:
+            _native.lib().dbi_query_result_free(r)
+        return row, ids
+
+    def peptides(self, ids):
+        ids = np.ascontiguousarray(np.atleast_1d(ids), np.uint64)
+        n = ids.shape[0]
+        out = dict(mass=np.zeros(n, np.float64), prot_id=np.zeros(n, np.uint32),
+                   offset=np.zeros(n, np.uint32), length=np.zeros(n, np.uint32),
+                   occ_begin=np.zeros(n, np.uint64), occ_end=np.zeros(n, np.uint64))
+        check(_native.lib().dbi_peptides(self.h, _p(ids), n, _p(out["mass"]), _p(out["prot_id"]),
+                                         _p(out["offset"]), _p(out["length"]), _p(out["occ_begin"]),
+                                         _p(out["occ_end"])))
+        return out
+
+    def occurrences(self, begin: int, end: int) -> np.ndarray:
+        out = np.zeros(max(end - begin, 0), np.uint32)
+        check(_native.lib().dbi_occurrences(self.h, begin, end, _p(out)))
+        return out
+
+    def export(self):
+        st = self.stats()
+        U, K = st.n_unique, st.n_kept
+        out = dict(mass=np.zeros(U, np.float64), prot_id=np.zeros(U, np.uint32),
+                   offset=np.zeros(U, np.uint32), length=np.zeros(U, np.uint32),
+                   occ_off=np.zeros(U + 1, np.uint64), occ_prot=np.zeros(K, np.uint32))
+        check(_native.lib().dbi_export(self.h, _p(out["mass"]), _p(out["prot_id"]), _p(out["offset"]),
+                                       _p(out["length"]), _p(out["occ_off"]), _p(out["occ_prot"])))
+        return out
+
+    def entry_keys(self) -> np.ndarray:
+        n = ctypes.c_uint64()
+        check(_native.lib().dbi_entry_keys(self.h, None, 0, ctypes.byref(n)))
+        keys = np.zeros(n.value, np.int32)
+        check(_native.lib().dbi_entry_keys(self.h, _p(keys), n.value, ctypes.byref(n)))
+        return keys
+
+    def stage_times(self):
+        """[(kernel, ms, algorithmic bytes)] of the last build, from HIP events
+        recorded on the engine stream around every launch."""
+        n = ctypes.c_uint64()
+        check(_native.lib().dbi_stage_times(self.h, None, None, None, 0, ctypes.byref(n)))
+        k = n.value
+        names = (ctypes.c_char_p * max(k, 1))()
+        ms = np.zeros(max(k, 1), np.float64)
+        by = np.zeros(max(k, 1), np.float64)
+        check(_native.lib().dbi_stage_times(self.h, ctypes.cast(names, ctypes.c_void_p), _p(ms), _p(by), k,
+                                            ctypes.byref(n)))
+        return [(names[i].decode(), float(ms[i]), float(by[i])) for i in range(k)]
+
+    def device_view(self) -> DbiDeviceIndex:
+        v = DbiDeviceIndex()
+        check(_native.lib().dbi_device_view(self.h, ctypes.byref(v)))
+        return v

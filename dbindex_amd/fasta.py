@@ -1,0 +1,170 @@
+"""FASTA input for the index build: a packed-protein container, a UniProt-style
+FASTA reader/writer, and the seeded synthetic generator of SURVEY.md §8(d).
+
+Protein numbering follows the reference: protein id = 0-based position in FASTA
+order (``DBIndexer.java:251,418``; ``ProteinCache.addProtein``
+``ProteinCache.java:84-95``; ``DBIndexStoreSQLiteMult.addProteinDef`` returns
+``num`` ``:446-450``).  The reference rejects FASTA without UniProt accessions
+(``DBIndexer.java:560-565``), so synthetic headers are UniProt style.
+"""
+from __future__ import annotations
+
+import hashlib
+import io
+from dataclasses import dataclass, field
+from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+# SwissProt residue frequencies (percent), SURVEY.md §8(d)
+AA_FREQ = {
+    "A": 8.25, "R": 5.53, "N": 4.06, "D": 5.45, "C": 1.37, "Q": 3.93, "E": 6.75,
+    "G": 7.07, "H": 2.27, "I": 5.96, "L": 9.66, "K": 5.84, "M": 2.42, "F": 3.86,
+    "P": 4.70, "S": 6.56, "T": 5.34, "W": 1.08, "Y": 2.92, "V": 6.87,
+}
+
+# Named synthetic configurations (BASELINE.json configs; seeds per SURVEY.md §8(d))
+CONFIGS = {
+    "1k": dict(n_proteins=1000, seed=1),
+    "human": dict(n_proteins=20000, seed=2),
+    "swissprot": dict(n_proteins=560000, seed=3),
+}
+
+
+@dataclass
+class PackedProteins:
+    """Proteins packed for HBM: ``residues`` (u8, all sequences concatenated in
+    FASTA order) + ``offsets`` (u64, P+1 entries) + the FASTA definitions."""
+
+    residues: np.ndarray
+    offsets: np.ndarray
+    defs: List[str] = field(default_factory=list)
+
+    @property
+    def n_proteins(self) -> int:
+        return int(self.offsets.shape[0] - 1)
+
+    @property
+    def n_residues(self) -> int:
+        return int(self.residues.shape[0])
+
+    def sequence(self, i: int) -> str:
+        a, b = int(self.offsets[i]), int(self.offsets[i + 1])
+        return self.residues[a:b].tobytes().decode("ascii")
+
+    def sequences(self) -> List[str]:
+        return [self.sequence(i) for i in range(self.n_proteins)]
+
+    def sha256(self) -> str:
+        h = hashlib.sha256()
+        h.update(np.ascontiguousarray(self.residues).tobytes())
+        h.update(np.ascontiguousarray(self.offsets, dtype=np.uint64).tobytes())
+        return h.hexdigest()
+
+    def slice(self, p0: int, p1: int) -> "PackedProteins":
+        """Proteins [p0, p1) as a new container (offsets rebased to 0)."""
+        a, b = int(self.offsets[p0]), int(self.offsets[p1])
+        offs = (self.offsets[p0: p1 + 1] - np.uint64(a)).astype(np.uint64)
+        defs = self.defs[p0:p1] if self.defs else []
+        return PackedProteins(self.residues[a:b].copy(), offs, defs)
+
+    @staticmethod
+    def from_sequences(seqs: Sequence[str], defs: Optional[Sequence[str]] = None) -> "PackedProteins":
+        lens = np.array([len(s) for s in seqs], dtype=np.uint64)
+        offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        res = np.frombuffer("".join(seqs).encode("ascii"), dtype=np.uint8).copy()
+        return PackedProteins(res, offs, list(defs) if defs is not None else [])
+
+
+def uniprot_header(i: int) -> str:
+    return (f"sp|S{i:07d}|SYN{i}_HUMAN Synthetic {i} OS=Homo sapiens OX=9606 "
+            f"GN=SYN{i} PE=1 SV=1")
+
+
+def synthetic(n_proteins: int, seed: int, copy_frac: float = 0.10,
+              len_mu: float = float(np.log(300.0)), len_sigma: float = 0.6,
+              len_min: int = 30, len_max: int = 35000, with_defs: bool = True) -> PackedProteins:
+    """Seeded synthetic proteome: 20 canonical residues i.i.d.
+    at SwissProt frequencies, lognormal lengths clipped to [30, 35000], and 10 %
+    of proteins overwritten with a random 50-300 aa segment of an earlier
+    protein (shared peptides exercise the dedup of IndexMerge.getMergedData)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lens = np.clip(np.rint(rng.lognormal(len_mu, len_sigma, n_proteins)), len_min, len_max)
+    lens = lens.astype(np.uint64)
+    offs = np.zeros(n_proteins + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    total = int(offs[-1])
+    letters = np.frombuffer("".join(AA_FREQ.keys()).encode("ascii"), dtype=np.uint8)
+    probs = np.array(list(AA_FREQ.values()), dtype=np.float64)
+    probs /= probs.sum()
+    res = letters[rng.choice(len(letters), size=total, p=probs)]
+    # shared segments: protein i copies [s, s+L) of an earlier protein j
+    donors = np.nonzero(rng.random(n_proteins) < copy_frac)[0]
+    for i in donors:
+        if i == 0:
+            continue
+        j = int(rng.integers(0, i))
+        seg = int(rng.integers(50, 301))
+        li, lj = int(lens[i]), int(lens[j])
+        seg = min(seg, li, lj)
+        sj = int(rng.integers(0, lj - seg + 1))
+        si = int(rng.integers(0, li - seg + 1))
+        a, b = int(offs[i]) + si, int(offs[j]) + sj
+        res[a: a + seg] = res[b: b + seg]
+    defs = [uniprot_header(i) for i in range(n_proteins)] if with_defs else []
+    return PackedProteins(res, offs, defs)
+
+
+def config(name: str, **kw) -> PackedProteins:
+    c = dict(CONFIGS[name])
+    c.update(kw)
+    return synthetic(**c)
+
+
+# ----------------------------------------------------------------------------
+# FASTA text I/O
+# ----------------------------------------------------------------------------
+def write_fasta(pp: PackedProteins, fh: io.TextIOBase, width: int = 60) -> None:
+    for i in range(pp.n_proteins):
+        d = pp.defs[i] if pp.defs else uniprot_header(i)
+        fh.write(">" + d + "\n")
+        s = pp.sequence(i)
+        for k in range(0, len(s), width):
+            fh.write(s[k: k + width] + "\n")
+
+
+def iter_fasta(lines: Iterable[str]) -> Iterator[Tuple[str, str]]:
+    """Yields (definition, sequence) in file order; definition without '>'.
+    Sequence lines are concatenated with whitespace stripped."""
+    d: Optional[str] = None
+    parts: List[str] = []
+    for line in lines:
+        if line.startswith(">"):
+            if d is not None:
+                yield d, "".join(parts)
+            d = line[1:].rstrip("\r\n")
+            parts = []
+        elif d is not None:
+            parts.append("".join(line.split()))
+    if d is not None:
+        yield d, "".join(parts)
+
+
+def read_fasta(path: str) -> PackedProteins:
+    defs, seqs = [], []
+    with open(path, "r") as fh:
+        for d, s in iter_fasta(fh):
+            defs.append(d)
+            seqs.append(s)
+    return PackedProteins.from_sequences(seqs, defs)
+
+
+def uniprot_accession(definition: str) -> Optional[str]:
+    """Accession of a UniProt-style header ``db|ACC|NAME ...`` (the reference's
+    FastaReader.getACCsFromFasta requirement, DBIndexer.java:560-565)."""
+    head = definition.split(" ", 1)[0]
+    parts = head.split("|")
+    if len(parts) >= 3 and parts[0] in ("sp", "tr") and parts[1]:
+        return parts[1]
+    return None

@@ -1,0 +1,135 @@
+"""``DBIndexer`` mirror with the ``DBIndexerHip`` digestion hook.
+
+Reference: ``/root/reference/src/main/java/edu/scripps/yates/dbindex/DBIndexer.java``.
+The drop-in overrides the protected ``cutSeq(String, String)`` (``:237``) so it
+only registers the protein with the store (``addProteinDef(++protNum, ...)``,
+``:251``); the whole digestion loop (``:256-397``) then runs on the GPU when
+the store finalises (``stopAddSeq``, ``:666``).  The query-side logic that
+lives in ``DBIndexer`` (ppm probe loop ``:787-844``, exact-mass protein lookup
+``:925-947``, parent masses ``:979-992``) is mirrored here unchanged, on top of
+the store's ``getSequences``.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional, Set, Tuple, Union
+
+from .fasta import PackedProteins, iter_fasta, uniprot_accession
+from .params import DBIndexSearchParams, calculate_mass, tolerance_in_dalton
+from .store import DBIndexStoreHip, IndexedProtein, IndexedSequence, MassRange
+
+PRECISION = 0.000001  # Constants.java:50
+
+
+class DBIndexerException(Exception):
+    pass
+
+
+class IndexerMode:
+    INDEX = "INDEX"
+    SEARCH_INDEXED = "SEARCH_INDEXED"
+
+
+class DBIndexer:
+    """``DBIndexerHip extends DBIndexer``: device digestion behind the same API."""
+
+    def __init__(self, sparam: DBIndexSearchParams, mode: str = IndexerMode.INDEX,
+                 indexStore: Optional[DBIndexStoreHip] = None, device: int = 0,
+                 database_name: str = "synthetic.fasta"):
+        self.sparam = sparam
+        self.mode = mode
+        self.indexStore = indexStore if indexStore is not None else DBIndexStoreHip(sparam, device)
+        self.indexStore.setDeviceDigest(True)
+        self.protNum = -1
+        self.inited = False
+        self.database_name = database_name
+
+    # DBIndexer.init (:412-451)
+    def init(self) -> None:
+        if self.inited:
+            raise RuntimeError("Already inited")
+        self.protNum = -1
+        self.indexStore.init(self.database_name + "_dbindex_hip")
+        self.inited = True
+
+    # DBIndexerHip.cutSeq: only hand the protein to the store (DBIndexer.java:251)
+    def cutSeq(self, protAccession: str, protSeq: str) -> None:
+        if "[" in protSeq:
+            raise DBIndexerException("inline [formula] PTMs are not supported (DBIndexer.java:288-303)")
+        self.protNum += 1
+        self.indexStore.addProteinDef(self.protNum, protAccession, protSeq)
+
+    # DBIndexer.run (:508-684), INDEX mode
+    def run(self, fasta: Union[PackedProteins, str, Iterable[Tuple[str, str]]]) -> None:
+        if not self.inited:
+            raise RuntimeError("Not initialized.")
+        if self.indexStore.indexExists():
+            return  # "Found existing index, skipping indexing." (:522-527)
+        items = _fasta_items(fasta)
+        if not any(uniprot_accession(d) for d, _ in items):
+            raise DBIndexerException("Reading FASTA file was not able to extract any single Uniprot "
+                                     "protein accession.")  # :560-565
+        self.indexStore.startAddSeq()
+        try:
+            for d, s in items:
+                self.cutSeq(d, s)
+        finally:
+            self.indexStore.stopAddSeq()
+
+    # --- queries (DBIndexer.java:762-871) -------------------------------------
+    def getSequencesUsingDaltonTolerance(self, precursorMass: float, massToleranceInDa: float):
+        return self.indexStore.getSequences(precursorMass, massToleranceInDa)
+
+    def getSequencesUsingPPMTolerance(self, precursorMass: float, massToleranceInPPM: float):
+        massTolerance = tolerance_in_dalton(precursorMass, massToleranceInPPM)
+        sequences = self.indexStore.getSequences(precursorMass, massTolerance)
+        seen = {s.getSequence() for s in sequences}
+        upperBound = precursorMass + massTolerance
+        while True:  # upper-bound probe loop (:808-839)
+            massTolerance2 = tolerance_in_dalton(upperBound, massToleranceInPPM)
+            lowerBoundOfUpperBoundMass = upperBound - massTolerance2
+            if lowerBoundOfUpperBoundMass < precursorMass:
+                sequences2 = self.indexStore.getSequences(upperBound, 0.0)
+                if not sequences2:
+                    break
+                for s2 in sequences2:
+                    if s2.getSequence() not in seen:
+                        sequences.append(s2)
+                        seen.add(s2.getSequence())
+            else:
+                break
+            newupperBound = upperBound + PRECISION
+            if newupperBound == upperBound:
+                break
+            upperBound = newupperBound
+        return sequences
+
+    def getSequences(self, massRanges: List[MassRange]):
+        return self.indexStore.getSequences(massRanges)
+
+    def getProteins(self, seq: Union[IndexedSequence, str]):
+        if isinstance(seq, IndexedSequence):
+            return self.indexStore.getProteins(seq)
+        # getProteins(String) (:925-947): exact-mass lookup then string equality
+        mass = calculate_mass(seq, self.sparam)
+        ret: Set[IndexedProtein] = set()
+        for s in self.getSequencesUsingDaltonTolerance(mass, 0.0):
+            if s.getSequence() == seq:
+                ret.update(self.indexStore.getProteins(s))
+        return ret
+
+    def getNumParentMasses(self) -> int:
+        return self.indexStore.getNumberSequences()
+
+    def getParentMasses(self) -> List[float]:
+        return [k * 1.0 / self.sparam.mass_group_factor for k in self.indexStore.getEntryKeys()]
+
+
+def _fasta_items(fasta) -> List[Tuple[str, str]]:
+    if isinstance(fasta, PackedProteins):
+        from .fasta import uniprot_header
+        return [(fasta.defs[i] if fasta.defs else uniprot_header(i), fasta.sequence(i))
+                for i in range(fasta.n_proteins)]
+    if isinstance(fasta, str):
+        with open(fasta) as fh:
+            return list(iter_fasta(fh))
+    return list(fasta)

@@ -1,0 +1,280 @@
+"""``DBIndexStoreHip`` — Python face of the dbi_store_* C-ABI, method-for-method
+the ``DBIndexStore`` interface of the reference
+(``/root/reference/src/main/java/edu/scripps/yates/dbindex/DBIndexStore.java:19-194``)
+with the semantics of ``DBIndexStoreSQLiteMult`` (the store ``DBIndexer`` builds).
+
+It is what a JNI ``DBIndexStoreHip implements DBIndexStore`` does on the Java
+side: each Java method is one C call; non-zero statuses become
+``DBIndexStoreException``.  The value types below mirror the external
+``IndexedSequence`` / ``IndexedProtein`` / ``ResidueInfo`` / ``MassRange``
+classes of ``edu.scripps.yates.utilities`` (not vendored).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Iterator, List, Optional, Sequence
+
+import numpy as np
+
+from . import _native
+from ._native import DbiSeqList, DBIndexStoreException, check
+from .params import DBIndexSearchParams, DbiParams
+
+FilterResult_INCLUDE = _native.FILTER_INCLUDE
+FilterResult_SKIP = _native.FILTER_SKIP
+FilterResult_SKIP_PROTEIN_START = _native.FILTER_SKIP_PROTEIN_START
+
+
+@dataclass
+class ResidueInfo:
+    resLeft: str
+    resRight: str
+
+
+@dataclass
+class IndexedSequence:
+    """``new IndexedSequence(0, seqMass, peptideSequence, "", "")`` +
+    ``setProteinIds`` + ``setResidues`` (IndexMerge.java:459-470)."""
+
+    mass: float
+    sequence: str
+    proteinIds: List[int]
+    residues: ResidueInfo
+    sequenceOffset: int
+    sequenceLen: int
+    uniqueId: int = -1
+
+    def getSequence(self) -> str:
+        return self.sequence
+
+    def getMass(self) -> float:
+        return self.mass
+
+    def getProteinIds(self) -> List[int]:
+        return self.proteinIds
+
+    def getResLeft(self) -> str:
+        return self.residues.resLeft
+
+    def getResRight(self) -> str:
+        return self.residues.resRight
+
+    def getSequenceOffset(self) -> int:
+        return self.sequenceOffset
+
+    def getSequenceLen(self) -> int:
+        return self.sequenceLen
+
+
+@dataclass(frozen=True)
+class IndexedProtein:
+    accession: str
+    id: int
+
+    def getAccession(self) -> str:
+        return self.accession
+
+    def getId(self) -> int:
+        return self.id
+
+
+@dataclass
+class MassRange:
+    precMass: float
+    tolerance: float
+
+    def getPrecMass(self) -> float:
+        return self.precMass
+
+    def getTolerance(self) -> float:
+        return self.tolerance
+
+
+def _seq_list(ptr) -> List[IndexedSequence]:
+    l = ptr.contents
+    n = l.n
+    out: List[IndexedSequence] = []
+    if n == 0:
+        return out
+    seq_off = np.ctypeslib.as_array(l.seq_off, shape=(n + 1,))
+    chars = ctypes.string_at(l.seq_chars, int(seq_off[n])).decode("ascii")
+    left = ctypes.string_at(l.res_left, 3 * n).decode("ascii")
+    right = ctypes.string_at(l.res_right, 3 * n).decode("ascii")
+    prot_off = np.ctypeslib.as_array(l.prot_off, shape=(n + 1,))
+    nprot = int(prot_off[n])
+    prot_ids = np.ctypeslib.as_array(l.prot_ids, shape=(max(nprot, 1),))[:nprot]
+    mass = np.ctypeslib.as_array(l.mass, shape=(n,))
+    off = np.ctypeslib.as_array(l.offset, shape=(n,))
+    ln = np.ctypeslib.as_array(l.length, shape=(n,))
+    uid = np.ctypeslib.as_array(l.unique_id, shape=(n,))
+    for i in range(n):
+        out.append(IndexedSequence(
+            mass=float(mass[i]), sequence=chars[seq_off[i]:seq_off[i + 1]],
+            proteinIds=[int(x) for x in prot_ids[prot_off[i]:prot_off[i + 1]]],
+            residues=ResidueInfo(left[3 * i:3 * i + 3], right[3 * i:3 * i + 3]),
+            sequenceOffset=int(off[i]), sequenceLen=int(ln[i]), uniqueId=int(uid[i])))
+    return out
+
+
+class DBIndexStoreHip:
+    """``implements DBIndexStore`` on the MI355X engine."""
+
+    def __init__(self, sparam, device: int = 0, device_digest: bool = False):
+        if isinstance(sparam, DBIndexSearchParams):
+            self.sparam = sparam
+            cp = sparam.to_c()
+        else:
+            self.sparam = None
+            cp = sparam
+        assert isinstance(cp, DbiParams)
+        self._cp = cp
+        s = ctypes.c_void_p()
+        check(_native.lib().dbi_store_create(ctypes.byref(cp), device, ctypes.byref(s)))
+        self.s = s
+        if device_digest:
+            self.setDeviceDigest(True)
+
+    def close(self) -> None:
+        if getattr(self, "s", None):
+            _native.lib().dbi_store_close(self.s)
+            self.s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- DBIndexerHip hook ----------------------------------------------------
+    def setDeviceDigest(self, on: bool) -> None:
+        check(_native.lib().dbi_store_set_device_digest(self.s, 1 if on else 0))
+
+    # --- DBIndexStore ---------------------------------------------------------
+    def lastBuffertoDatabase(self) -> None:
+        raise NotImplementedError("Not supported yet.")  # DBIndexStoreSQLiteByte.java:720-730
+
+    def init(self, databaseID: Optional[str]) -> None:
+        check(_native.lib().dbi_store_init(self.s, (databaseID or "").encode()))
+
+    def startAddSeq(self) -> None:
+        check(_native.lib().dbi_store_start_add_seq(self.s))
+
+    def stopAddSeq(self) -> None:
+        check(_native.lib().dbi_store_stop_add_seq(self.s))
+
+    def indexExists(self) -> bool:
+        v = ctypes.c_int()
+        check(_native.lib().dbi_store_index_exists(self.s, ctypes.byref(v)))
+        return bool(v.value)
+
+    def filterSequence(self, precMass: float, sequence: str) -> int:
+        b = sequence.encode("ascii")
+        v = ctypes.c_int()
+        check(_native.lib().dbi_store_filter_sequence(self.s, precMass, b, len(b), ctypes.byref(v)))
+        return v.value
+
+    def addSequence(self, precMass: float, sequenceOffset: int, sequenceLen: int, sequence=None,
+                    resLeft=None, resRight=None, proteinId: int = 0) -> None:
+        check(_native.lib().dbi_store_add_sequence(self.s, precMass, sequenceOffset, sequenceLen, proteinId))
+
+    def getSequences(self, precMass, tolerance=None) -> List[IndexedSequence]:
+        """``getSequences(double, double)`` or ``getSequences(List<MassRange>)``."""
+        L = _native.lib()
+        r = ctypes.POINTER(DbiSeqList)()
+        if tolerance is None:
+            ranges: Sequence[MassRange] = precMass
+            m = np.ascontiguousarray([x.getPrecMass() for x in ranges], np.float64)
+            t = np.ascontiguousarray([x.getTolerance() for x in ranges], np.float64)
+            check(L.dbi_store_get_sequences_ranges(self.s, m.ctypes.data_as(ctypes.c_void_p),
+                                                   t.ctypes.data_as(ctypes.c_void_p), m.shape[0],
+                                                   ctypes.byref(r)))
+        else:
+            check(L.dbi_store_get_sequences(self.s, float(precMass), float(tolerance), ctypes.byref(r)))
+        try:
+            return _seq_list(r)
+        finally:
+            L.dbi_seq_list_free(r)
+
+    def getSequencesIterator(self, ranges: Sequence[MassRange]) -> Iterator[IndexedSequence]:
+        return iter(self.getSequences(ranges))
+
+    def addProteinDef(self, num: int, accession: str, protSequence: str) -> int:
+        b = protSequence.encode("ascii")
+        out = ctypes.c_int64()
+        check(_native.lib().dbi_store_add_protein_def(self.s, num, accession.encode(), b, len(b),
+                                                      ctypes.byref(out)))
+        return out.value
+
+    def setProteinCache(self, proteinCache) -> None:
+        # the store keeps its own ProteinCache, filled by addProteinDef
+        self.proteinCache = proteinCache
+
+    def supportsProteinCache(self) -> bool:
+        return True
+
+    def getProteins(self, sequence: IndexedSequence) -> List[IndexedProtein]:
+        return [IndexedProtein(self.getProteinDef(pid), pid) for pid in sequence.getProteinIds()]
+
+    def getNumberSequences(self) -> int:
+        v = ctypes.c_int64()
+        check(_native.lib().dbi_store_get_number_sequences(self.s, ctypes.byref(v)))
+        return v.value
+
+    def getTotalSeqCount(self) -> int:
+        v = ctypes.c_int64()
+        check(_native.lib().dbi_store_get_total_seq_count(self.s, ctypes.byref(v)))
+        return v.value
+
+    def getResidues(self, peptideSequence: IndexedSequence, protein: IndexedProtein) -> ResidueInfo:
+        """SQLiteMult.getResidues (:294-312) -> Util.getResidues (Util.java:130-162)."""
+        prot = self.getProteinSequence(protein.getId())
+        off = peptideSequence.getSequenceOffset()
+        if off is None or off < 0:
+            off = prot.find(peptideSequence.getSequence())
+        if off == -1:
+            raise RuntimeError("Could not get subsequence, unexpected error")
+        return get_residues(off, peptideSequence.getSequenceLen(), prot)
+
+    def getEntryKeys(self) -> List[int]:
+        L = _native.lib()
+        n = ctypes.c_uint64()
+        check(L.dbi_store_get_entry_keys(self.s, None, 0, ctypes.byref(n)))
+        keys = np.zeros(n.value, np.int32)
+        if n.value:
+            check(L.dbi_store_get_entry_keys(self.s, keys.ctypes.data_as(ctypes.c_void_p), n.value,
+                                             ctypes.byref(n)))
+        return [int(k) for k in keys]
+
+    # --- ProteinCache accessors ----------------------------------------------
+    def getNumberProteins(self) -> int:
+        v = ctypes.c_uint64()
+        check(_native.lib().dbi_store_protein_count(self.s, ctypes.byref(v)))
+        return v.value
+
+    def getProteinDef(self, pid: int) -> str:
+        p = ctypes.c_char_p()
+        n = ctypes.c_uint64()
+        check(_native.lib().dbi_store_protein_def(self.s, pid, ctypes.byref(p), ctypes.byref(n)))
+        return ctypes.string_at(p, n.value).decode()
+
+    def getProteinSequence(self, pid: int) -> str:
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        check(_native.lib().dbi_store_protein_sequence(self.s, pid, ctypes.byref(p), ctypes.byref(n)))
+        return ctypes.string_at(p, n.value).decode("ascii") if n.value else ""
+
+    def engine_handle(self):
+        return _native.lib().dbi_store_engine(self.s)
+
+
+def get_residues(offset: int, length: int, prot: str) -> ResidueInfo:
+    """Util.getResidues (Util.java:130-162), incl. the right-flank quirk
+    ``min(3, protLen - end - 1)``."""
+    n = len(prot)
+    left_i = offset - 3 if offset >= 3 else 0
+    left = prot[left_i:left_i + min(3, offset)]
+    end = offset + length
+    right_len = min(3, n - end - 1)
+    right = prot[end:end + right_len] if (end < n and right_len > 0) else ""
+    return ResidueInfo("-" * (3 - len(left)) + left, right + "-" * (3 - len(right)))

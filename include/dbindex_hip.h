@@ -1,0 +1,282 @@
+/*
+ * dbindex_hip.h — C-ABI of the MI355X-native peptide-index engine.
+ *
+ * This is the drop-in boundary for dbIndex's digestion + index + mass-lookup
+ * hot path.  A JNI shim binds these symbols one-for-one to
+ * the Java extension points of the reference:
+ *
+ *   DBIndexStore            /root/reference/src/main/java/edu/scripps/yates/dbindex/DBIndexStore.java:19-194
+ *   DBIndexStoreSQLiteMult  (the store the reference builds)   DBIndexStoreSQLiteMult.java:23-637
+ *   DBIndexer.cutSeq        (digestion loop, run on device)    DBIndexer.java:237-405
+ *
+ * Two layers are exported:
+ *   - dbi_store_*  : one function per DBIndexStore method (init, startAddSeq,
+ *                    addProteinDef, filterSequence, addSequence, stopAddSeq,
+ *                    indexExists, getSequences(m,tol), getSequences(List),
+ *                    getNumberSequences, getEntryKeys, getProteins, ...).
+ *   - dbi_*        : the batch engine underneath (build from a packed residue
+ *                    array, batched mass-window queries, peptide gathers),
+ *                    usable on host buffers or on buffers already in HBM.
+ *
+ * Conventions: plain C types only, no torch types.  Every function returns an
+ * int status: 0 = OK, negative = error class (DBI_E_*); the message of the
+ * last error on the calling thread is in dbi_last_error().  Nothing is
+ * swallowed (unlike DBIndexer.cutSeq, DBIndexer.java:398-403).
+ * Library-allocated results are freed by the caller with the matching *_free.
+ */
+#ifndef DBINDEX_HIP_H
+#define DBINDEX_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DBI_OK 0
+#define DBI_E_INVALID (-1) /* invalid argument / unsupported input     */
+#define DBI_E_OOM (-2)     /* host or device allocation failed          */
+#define DBI_E_HIP (-3)     /* HIP runtime error (kernel launch, copy)   */
+#define DBI_E_RCCL (-4)    /* collective error (sharded build)          */
+#define DBI_E_STATE (-5)   /* call not valid in the current state       */
+
+#define DBI_ABI_VERSION 1
+
+/* DBIndexStore.FilterResult (DBIndexStore.java:22-24) */
+#define DBI_FILTER_INCLUDE 0
+#define DBI_FILTER_SKIP 1
+#define DBI_FILTER_SKIP_PROTEIN_START 2
+
+/*
+ * Flat parameter block: the handful of DBIndexSearchParams / AssignMass /
+ * Enzyme values the hot loop reads.
+ * The Java side fills mass[] from AssignMass.getMass(char) for every char,
+ * cleave[] from the Enzyme residues and nocut[] from getEnzymeNocutResidues(),
+ * so residue arithmetic and the cleavage sets are identical by construction.
+ */
+typedef struct dbi_params {
+    double min_mh;       /* getMinPrecursorMass()          DBIndexer.java:331        */
+    double max_mh;       /* getMaxPrecursorMass()          DBIndexer.java:284,325    */
+    double h2o_proton;   /* AssignMass.H2O_PROTON          DBIndexer.java:269        */
+    double cterm;        /* AssignMass.getcTerm()          DBIndexer.java:270        */
+    double nterm;        /* AssignMass.getnTerm()          DBIndexer.java:271        */
+    double mass[256];    /* AssignMass.getMass(char)       DBIndexer.java:306        */
+    uint8_t cleave[256]; /* Enzyme.isEnzyme(char)          DBIndexer.java:314        */
+    uint8_t nocut[256];  /* getEnzymeNocutResidues()       DBIndexer.java:318-319    */
+    uint8_t mandatory[256]; /* getMandatoryInternalAAs()   DBIndexer.java:334-344    */
+    int32_t max_missed;        /* getMaxMissedCleavages()  DBIndexer.java:246,322    */
+    int32_t semi;              /* isSemiCleavage()  (Enzyme semi flag)               */
+    int32_t add_h2o_proton;    /* isH2OPlusProtonAdded()   DBIndexer.java:268        */
+    int32_t min_len;           /* Constants.MIN_PEP_LENGTH = 6   Constants.java:10    */
+    int32_t mass_group_factor; /* getMassGroupFactor() = 10000  DBIndexStoreSQLiteByte.java:187 */
+    int32_t index_factor;      /* getIndexFactor() = NUM_BUCKETS  DBIndexStoreSQLiteMult.java:55 */
+    int32_t mandatory_mode;    /* 0: getMandatoryInternalAAs()==null, 1: non-null    */
+    int32_t mandatory_count;   /* its length (filterSequence tests length>0)         */
+    int32_t reserved[8];
+} dbi_params;
+
+/* Fills *p with the reference defaults (dbindex.properties:6-22 + Constants):
+ * trypsin "KR", empty nocut, mc=max_missed, 500..6000 Da, H2O+H+ added,
+ * factor 10000, index_factor 8, min length 6, pinned monoisotopic table. */
+void dbi_params_default(dbi_params* p, int32_t max_missed, int32_t semi);
+
+/* ------------------------------------------------------------------------ */
+/* Batch engine                                                             */
+/* ------------------------------------------------------------------------ */
+typedef struct dbi_handle dbi_handle;
+
+typedef struct dbi_stats {
+    uint64_t n_residues;     /* R                                                  */
+    uint64_t n_proteins;     /* P                                                  */
+    uint64_t n_total;        /* N: occurrences passing all filters = totalSeqCount */
+                             /*    (DBIndexStoreSQLiteMult.java:277)               */
+    uint64_t n_dropped;      /* of N, bucket > NUM_BUCKETS-1 (SQLiteMult:283-288)  */
+    uint64_t n_kept;         /* N - n_dropped: occurrences stored in the index     */
+    uint64_t n_unique;       /* U: unique peptide sequences (IndexMerge:620-719)   */
+    uint64_t n_keys;         /* distinct mass-key rows = getNumberSequences()      */
+    uint64_t n_bins;         /* device mass bins used by the build                 */
+    uint64_t n_big_bins;     /* bins sorted by the large-bin path                  */
+    uint64_t device_bytes;   /* HBM held by the index + workspace                  */
+    double build_ms;         /* device time of the last build (HIP events)         */
+    double digest_ms;        /* of which: digest count + emit kernels              */
+} dbi_stats;
+
+/* Opens an engine on HIP device `device` (ordinal as seen by this process). */
+int dbi_open(const dbi_params* params, int device, dbi_handle** out);
+void dbi_close(dbi_handle* h);
+
+/* Build the index from a packed FASTA: residues[0..n_res) = all protein
+ * sequences concatenated in FASTA order, prot_off[0..n_prot] = start offsets
+ * (prot_off[0]=0, prot_off[n_prot]=n_res).  Protein id = 0-based position
+ * (DBIndexer.java:251,418 + DBIndexStoreSQLiteMult.addProteinDef:446-450).
+ * Host pointers; copied to HBM.  Replaces any previous index of the handle. */
+int dbi_build(dbi_handle* h, const uint8_t* residues, uint64_t n_res,
+              const uint64_t* prot_off, uint64_t n_prot);
+
+/* Same, with residues / offsets already resident in HBM (device pointers),
+ * work ordered on `stream` (a hipStream_t, NULL = default stream). */
+int dbi_build_device(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res,
+                     const uint64_t* d_prot_off, uint64_t n_prot, void* stream);
+
+/* Build from externally supplied occurrences (DBIndexStore.addSequence path):
+ * mass / protein id / offset-in-protein / length per occurrence, in insertion
+ * order, over the protein residues given as above.  Dedup + sort + query are
+ * identical to the device-digest build. */
+int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res,
+                          const uint64_t* prot_off, uint64_t n_prot,
+                          const double* mass, const uint32_t* prot_id,
+                          const uint32_t* offset, const uint32_t* length,
+                          uint64_t n_occ, uint64_t n_dropped_extra);
+
+int dbi_stats_get(dbi_handle* h, dbi_stats* out);
+
+/* Batched single-range mass-window queries, getSequences(m, tol) semantics
+ * (DBIndexStoreSQLiteMult.java:315-350 + IndexMerge.java:146-217,386-481):
+ * for query i, the unique peptides with lo<=mass<=hi, lo=max(0,m-tol),
+ * hi=m+tol, empty when a bucket of lo or hi exceeds NUM_BUCKETS-1.
+ * Results are contiguous in the mass-sorted unique table: ids
+ * first[i] .. first[i]+count[i]-1, ascending mass.  Host arrays. */
+int dbi_query(dbi_handle* h, const double* mass, const double* tol, uint64_t nq,
+              uint64_t* first, uint64_t* count);
+
+/* Same on device arrays (stream = hipStream_t or NULL). */
+int dbi_query_device(dbi_handle* h, const double* d_mass, const double* d_tol, uint64_t nq,
+                     uint64_t* d_first, uint64_t* d_count, void* stream);
+
+/* Materialised CSR form of a query batch: row_ptr[nq+1] and ids[] (H ids). */
+typedef struct dbi_query_result {
+    uint64_t nq;
+    uint64_t n_hits;
+    uint64_t* row_ptr; /* nq+1 */
+    uint64_t* ids;     /* n_hits, unique-peptide ids */
+} dbi_query_result;
+int dbi_query_csr(dbi_handle* h, const double* mass, const double* tol, uint64_t nq,
+                  dbi_query_result** out);
+void dbi_query_result_free(dbi_query_result* r);
+
+/* Gather per-unique-peptide data for ids[0..n): mass, representative
+ * (first-occurrence) protein id + offset + length (IndexMerge.java:671-675),
+ * and the occurrence range [occ_begin, occ_end) into dbi_occurrences().
+ * Any output pointer may be NULL. */
+int dbi_peptides(dbi_handle* h, const uint64_t* ids, uint64_t n, double* mass,
+                 uint32_t* prot_id, uint32_t* offset, uint32_t* length,
+                 uint64_t* occ_begin, uint64_t* occ_end);
+
+/* Protein ids of occurrences [begin, end) (insertion order, duplicates kept,
+ * IndexMerge.java:676-681). */
+int dbi_occurrences(dbi_handle* h, uint64_t begin, uint64_t end, uint32_t* prot_id);
+
+/* Copy the whole index to host (any pointer may be NULL):
+ * mass[U], prot_id[U], offset[U], length[U], occ_off[U+1], occ_prot[n_kept]. */
+int dbi_export(dbi_handle* h, double* mass, uint32_t* prot_id, uint32_t* offset,
+               uint32_t* length, uint64_t* occ_off, uint32_t* occ_prot);
+
+/* Distinct mass keys (int)(mass*factor), ascending = getEntryKeys()
+ * (DBIndexStoreSQLiteByte.java:693-716 summed over buckets).  keys may be
+ * NULL to query the count only. */
+int dbi_entry_keys(dbi_handle* h, int32_t* keys, uint64_t cap, uint64_t* n);
+
+/* Device pointers of the resident index (for in-HBM consumers / bench).
+ * d_mass[U] f64 ascending; others as dbi_export. */
+typedef struct dbi_device_index {
+    const double* mass;
+    const uint32_t* prot_id;
+    const uint32_t* offset;
+    const uint32_t* length;
+    const uint32_t* occ_off;   /* U+1 */
+    const uint32_t* occ_prot;  /* n_kept */
+    uint64_t n_unique;
+    uint64_t n_kept;
+} dbi_device_index;
+int dbi_device_view(dbi_handle* h, dbi_device_index* out);
+
+/* Per-kernel device times of the last build, from HIP events recorded on the
+ * engine stream around every launch (always on; a few us per build).
+ * names[i] are static strings ("digest_count", "digest_emit", "radix_hist",
+ * "radix_scatter", "bin_sort", ...); bytes[i] = algorithmic HBM bytes of that
+ * launch.  Arrays may be NULL to query *n. */
+int dbi_stage_times(dbi_handle* h, const char** names, double* ms, double* bytes, uint64_t cap,
+                    uint64_t* n);
+
+/* ------------------------------------------------------------------------ */
+/* DBIndexStore mirror                                                      */
+/* ------------------------------------------------------------------------ */
+typedef struct dbi_store dbi_store;
+
+/* new DBIndexStoreSQLiteMult(sparam, inMemory) (DBIndexStoreSQLiteMult.java:47-64) */
+int dbi_store_create(const dbi_params* params, int device, dbi_store** out);
+void dbi_store_close(dbi_store* s);
+
+/* Device digestion switch (the DBIndexerHip hook): when on, stopAddSeq runs
+ * the cutSeq loop on the GPU over every protein given to addProteinDef, and
+ * filterSequence answers SKIP_PROTEIN_START so a stock DBIndexer.cutSeq bails
+ * out of every start (DBIndexer.java:351-354).  When off (default), the store
+ * indexes exactly the occurrences passed to addSequence, like the reference. */
+int dbi_store_set_device_digest(dbi_store* s, int on);
+
+int dbi_store_init(dbi_store* s, const char* database_id);              /* init(String)      */
+int dbi_store_start_add_seq(dbi_store* s);                              /* startAddSeq()     */
+int dbi_store_stop_add_seq(dbi_store* s);                               /* stopAddSeq()      */
+int dbi_store_index_exists(dbi_store* s, int* out);                     /* indexExists()     */
+/* addProteinDef(long num, String def, String seq): returns num (SQLiteMult:446-450) */
+int dbi_store_add_protein_def(dbi_store* s, int64_t num, const char* def, const char* seq,
+                              uint64_t seq_len, int64_t* out_id);
+/* filterSequence(double, String) (DBIndexStoreSQLiteMult.java:245-268) */
+int dbi_store_filter_sequence(dbi_store* s, double mass, const char* seq, uint64_t seq_len,
+                              int* out_result);
+/* addSequence(double, int, int, String, String, String, long) (SQLiteMult:271-291) */
+int dbi_store_add_sequence(dbi_store* s, double mass, int32_t offset, int32_t length,
+                           int64_t protein_id);
+int dbi_store_get_number_sequences(dbi_store* s, int64_t* out);         /* getNumberSequences */
+int dbi_store_get_total_seq_count(dbi_store* s, int64_t* out);          /* totalSeqCount      */
+int dbi_store_get_entry_keys(dbi_store* s, int32_t* keys, uint64_t cap, uint64_t* n);
+dbi_handle* dbi_store_engine(dbi_store* s);                             /* batch engine view  */
+
+/* A materialised List<IndexedSequence> (IndexMerge.parseAddPeptideInfo:386-481). */
+typedef struct dbi_seq_list {
+    uint64_t n;
+    double* mass;          /* n                                              */
+    uint64_t* seq_off;     /* n+1: sequence i = seq_chars[seq_off[i]..seq_off[i+1]) */
+    char* seq_chars;
+    char* res_left;        /* n*3: Util.getResidues left flank (Util.java:130-162)  */
+    char* res_right;       /* n*3: right flank, '-' padded                   */
+    uint64_t* prot_off;    /* n+1: protein ids of i = prot_ids[prot_off[i]..)       */
+    uint32_t* prot_ids;
+    uint32_t* offset;      /* n: representative offset  (IndexedSequence offset)    */
+    uint32_t* length;      /* n                                              */
+    uint64_t* unique_id;   /* n: id in the mass-sorted unique table          */
+} dbi_seq_list;
+
+/* getSequences(double precMass, double tolerance) */
+int dbi_store_get_sequences(dbi_store* s, double mass, double tol, dbi_seq_list** out);
+/* getSequences(List<MassRange>) (DBIndexStoreSQLiteMult.java:353-430) */
+int dbi_store_get_sequences_ranges(dbi_store* s, const double* mass, const double* tol,
+                                   uint64_t n_ranges, dbi_seq_list** out);
+void dbi_seq_list_free(dbi_seq_list* l);
+
+/* ProteinCache accessors (ProteinCache.java:60-127) */
+int dbi_store_protein_count(dbi_store* s, uint64_t* out);
+int dbi_store_protein_def(dbi_store* s, uint64_t id, const char** def, uint64_t* len);
+int dbi_store_protein_sequence(dbi_store* s, uint64_t id, const char** seq, uint64_t* len);
+
+/* ------------------------------------------------------------------------ */
+/* Device memory helpers (so host code needs no other HIP runtime binding)  */
+/* ------------------------------------------------------------------------ */
+int dbi_dev_alloc(int device, uint64_t bytes, void** out);
+int dbi_dev_free(int device, void* p);
+int dbi_dev_copy_h2d(int device, void* dst, const void* src, uint64_t bytes);
+int dbi_dev_copy_d2h(int device, void* dst, const void* src, uint64_t bytes);
+int dbi_dev_synchronize(int device);
+
+/* ------------------------------------------------------------------------ */
+/* Misc                                                                     */
+/* ------------------------------------------------------------------------ */
+const char* dbi_last_error(void); /* thread-local; "" when no error */
+int dbi_abi_version(void);
+int dbi_device_count(int* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DBINDEX_HIP_H */

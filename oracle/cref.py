@@ -1,0 +1,201 @@
+"""oracle/cref.py — TEST INFRASTRUCTURE ONLY: ctypes view of oracle/cpu_ref.cpp.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  The product path (dbindex_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libdbi_oracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P, U8, U32, U64, D = (ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8),
+                              ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64),
+                              ctypes.POINTER(ctypes.c_double))
+        L.oref_digest.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, P, P, ctypes.c_uint64, U64]
+        L.oref_build.argtypes = [P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+        L.oref_build_occurrences.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, P,
+                                             ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+        L.oref_free.argtypes = [P]
+        for f in ("oref_n_total", "oref_n_dropped", "oref_n_unique", "oref_n_kept", "oref_n_keys"):
+            getattr(L, f).argtypes = [P]
+            getattr(L, f).restype = ctypes.c_uint64
+        L.oref_build_seconds.argtypes = [P]
+        L.oref_build_seconds.restype = ctypes.c_double
+        L.oref_entry_keys.argtypes = [P, P]
+        L.oref_unique.argtypes = [P, P, P, P, P, P, P]
+        L.oref_query.argtypes = [P, ctypes.c_double, ctypes.c_double, P, ctypes.c_uint64, U64]
+        L.oref_query_ranges.argtypes = [P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, U64]
+        L.oref_calculate_mass.argtypes = [P, P, ctypes.c_uint64]
+        L.oref_calculate_mass.restype = ctypes.c_double
+        L.oref_tolerance_in_dalton.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.oref_tolerance_in_dalton.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+@dataclass
+class Digest:
+    mass: np.ndarray
+    pid: np.ndarray
+    offset: np.ndarray
+    length: np.ndarray
+    dropped: np.ndarray
+
+
+def digest(cparams, residues: np.ndarray, offsets: np.ndarray) -> Digest:
+    L = lib()
+    residues = np.ascontiguousarray(residues, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = ctypes.c_uint64()
+    P = offsets.shape[0] - 1
+    L.oref_digest(ctypes.byref(cparams), _ptr(residues), _ptr(offsets), P,
+                  None, None, None, None, None, 0, ctypes.byref(n))
+    k = n.value
+    out = Digest(np.zeros(k, np.float64), np.zeros(k, np.uint32), np.zeros(k, np.uint32),
+                 np.zeros(k, np.uint32), np.zeros(k, np.uint8))
+    if k:
+        rc = L.oref_digest(ctypes.byref(cparams), _ptr(residues), _ptr(offsets), P,
+                           _ptr(out.mass), _ptr(out.pid), _ptr(out.offset), _ptr(out.length),
+                           _ptr(out.dropped), k, ctypes.byref(n))
+        assert rc == 0
+    return out
+
+
+class Index:
+    """The oracle's store: buckets -> rows -> merged peptides."""
+
+    def __init__(self, cparams, residues: np.ndarray, offsets: np.ndarray, occurrences=None):
+        L = lib()
+        self._keep = (np.ascontiguousarray(residues, dtype=np.uint8),
+                      np.ascontiguousarray(offsets, dtype=np.uint64))
+        self.params = cparams
+        h = ctypes.c_void_p()
+        P = offsets.shape[0] - 1
+        if occurrences is None:
+            rc = L.oref_build(ctypes.byref(cparams), _ptr(self._keep[0]), _ptr(self._keep[1]),
+                              P, ctypes.byref(h))
+        else:
+            m, pid, off, ln = (np.ascontiguousarray(occurrences[0], np.float64),
+                               np.ascontiguousarray(occurrences[1], np.uint32),
+                               np.ascontiguousarray(occurrences[2], np.uint32),
+                               np.ascontiguousarray(occurrences[3], np.uint32))
+            rc = L.oref_build_occurrences(ctypes.byref(cparams), _ptr(self._keep[0]),
+                                          _ptr(self._keep[1]), P, _ptr(m), _ptr(pid), _ptr(off),
+                                          _ptr(ln), m.shape[0], ctypes.byref(h))
+        if rc != 0:
+            raise ValueError(f"oref_build failed: {rc}")
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oref_free(self.h)
+            self.h = None
+
+    @property
+    def build_seconds(self) -> float:
+        return lib().oref_build_seconds(self.h)
+
+    @property
+    def n_total(self) -> int:
+        return lib().oref_n_total(self.h)
+
+    @property
+    def n_dropped(self) -> int:
+        return lib().oref_n_dropped(self.h)
+
+    @property
+    def n_kept(self) -> int:
+        return lib().oref_n_kept(self.h)
+
+    @property
+    def n_unique(self) -> int:
+        return lib().oref_n_unique(self.h)
+
+    @property
+    def n_keys(self) -> int:
+        return lib().oref_n_keys(self.h)
+
+    def entry_keys(self) -> np.ndarray:
+        k = np.zeros(self.n_keys, np.int32)
+        lib().oref_entry_keys(self.h, _ptr(k))
+        return k
+
+    def unique(self):
+        U, K = self.n_unique, self.n_kept
+        mass = np.zeros(U, np.float64)
+        pid = np.zeros(U, np.uint32)
+        off = np.zeros(U, np.uint32)
+        ln = np.zeros(U, np.uint32)
+        occ_off = np.zeros(U + 1, np.uint64)
+        occ_pid = np.zeros(K, np.uint32)
+        lib().oref_unique(self.h, _ptr(mass), _ptr(pid), _ptr(off), _ptr(ln), _ptr(occ_off),
+                          _ptr(occ_pid))
+        return dict(mass=mass, prot_id=pid, offset=off, length=ln, occ_off=occ_off,
+                    occ_prot=occ_pid)
+
+    def query(self, mass: float, tol: float) -> np.ndarray:
+        L = lib()
+        n = ctypes.c_uint64()
+        L.oref_query(self.h, mass, tol, None, 0, ctypes.byref(n))
+        ids = np.zeros(n.value, np.uint64)
+        if n.value:
+            L.oref_query(self.h, mass, tol, _ptr(ids), n.value, ctypes.byref(n))
+        return ids
+
+    def query_ranges(self, masses, tols) -> np.ndarray:
+        L = lib()
+        m = np.ascontiguousarray(masses, np.float64)
+        t = np.ascontiguousarray(tols, np.float64)
+        n = ctypes.c_uint64()
+        L.oref_query_ranges(self.h, _ptr(m), _ptr(t), m.shape[0], None, 0, ctypes.byref(n))
+        ids = np.zeros(n.value, np.uint64)
+        if n.value:
+            L.oref_query_ranges(self.h, _ptr(m), _ptr(t), m.shape[0], _ptr(ids), n.value,
+                                ctypes.byref(n))
+        return ids
+
+    def query_batch(self, masses, tols):
+        """(first, count) per query, as the engine reports them (contiguous ranges)."""
+        first = np.zeros(len(masses), np.uint64)
+        count = np.zeros(len(masses), np.uint64)
+        for i, (m, t) in enumerate(zip(masses, tols)):
+            ids = self.query(float(m), float(t))
+            count[i] = ids.shape[0]
+            if ids.shape[0]:
+                first[i] = ids[0]
+                assert np.all(np.diff(ids.astype(np.int64)) == 1), "non-contiguous oracle result"
+        return first, count
+
+
+def calculate_mass(cparams, seq: str) -> float:
+    b = np.frombuffer(seq.encode("ascii"), dtype=np.uint8).copy()
+    return lib().oref_calculate_mass(ctypes.byref(cparams), _ptr(b), b.shape[0])
+
+
+def tolerance_in_dalton(mass: float, ppm: float) -> float:
+    return lib().oref_tolerance_in_dalton(mass, ppm)

@@ -1,0 +1,229 @@
+"""GPU parity: the HIP engine (through the C-ABI) vs the oracle on the same
+seeded inputs.  Bar: bit-exact for every count, index, id and mass.
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from dbindex_amd import fasta
+from dbindex_amd.params import DBIndexSearchParams, calculate_mass
+from oracle import cref
+from tests.helpers import assert_index_equal, assert_queries_equal, query_masses
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def Engine():
+    from dbindex_amd.engine import Engine
+    from dbindex_amd import _native
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    return Engine
+
+
+def _check(Engine, prm, pp, ctx, nq=2000):
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    with Engine(cp) as eng:
+        eng.build(pp)
+        assert_index_equal(eng, oix, ctx)
+        m, t = query_masses(oix, nq)
+        assert_queries_equal(eng, oix, m, t, ctx)
+    return oix
+
+
+KAT_PROTEINS = [
+    "MKWVTFISLLLLFSSAYSRGVFRRDTHKSEIAHRFKDLGEEHFKGLVLIAFSQYLQQCPFDEHVK",  # albumin head
+    "PEPTIDEKAAAAAAKPEPTLDEKGGGGGGR",   # I/L isobaric pair inside one protein
+    "AAAAAAKPAAAAAAKRPPPPPPRAAAAAAAAA",  # KP / RP (nocut) and a C-terminal non-K/R end
+    "PEPTIDEKAAAAAAKPEPTIDEKPEPTIDEK",  # duplicate peptide twice in one protein
+    "GGGGGGK",                          # exactly length 7
+    "GGGGK",                            # shorter than MIN_PEP_LENGTH
+    "",                                 # empty protein
+    "K",
+    "WWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWWK",  # heavy: crosses maxMH
+]
+
+
+def kat_pack(extra=()):
+    seqs = list(KAT_PROTEINS) + list(extra)
+    return fasta.PackedProteins.from_sequences(seqs, [fasta.uniprot_header(i) for i in range(len(seqs))])
+
+
+@pytest.mark.parametrize("name,prm", [
+    ("tryp0", DBIndexSearchParams.trypsin(0)),
+    ("tryp2", DBIndexSearchParams.trypsin(2)),
+    ("tryp2_nocutP", DBIndexSearchParams.trypsin(2, enzyme_nocut_residues="P")),
+    ("semi2", DBIndexSearchParams.semi_tryptic(2)),
+    ("nonspec", DBIndexSearchParams.non_specific(50)),
+    ("mand_K", DBIndexSearchParams.trypsin(2, mandatory_internal_aas="K")),
+    ("mand_empty", DBIndexSearchParams.trypsin(2, mandatory_internal_aas="")),
+    ("no_h2o", DBIndexSearchParams.trypsin(1, h2o_plus_proton_added=False, min_precursor_mass=100.0)),
+    ("terms", DBIndexSearchParams.trypsin(1, cterm=17.0265491, nterm=42.010565)),
+])
+def test_kat_proteins(Engine, name, prm):
+    _check(Engine, prm, kat_pack(), name, nq=500)
+
+
+@pytest.mark.parametrize("name,prm,nprot", [
+    ("1k_tryp0", DBIndexSearchParams.trypsin(0), 1000),
+    ("1k_tryp2", DBIndexSearchParams.trypsin(2), 1000),
+    ("1k_semi2", DBIndexSearchParams.semi_tryptic(2), 1000),
+    ("100_nonspec", DBIndexSearchParams.non_specific(50), 100),
+])
+def test_synthetic(Engine, name, prm, nprot):
+    pp = fasta.config("1k") if nprot == 1000 else fasta.config("1k").slice(0, nprot)
+    _check(Engine, prm, pp, name)
+
+
+@pytest.mark.parametrize("index_factor,maxmh,nprot", [(7, 7999.9, 1000), (3000, 7999.0, 300)])
+def test_bucket_drop(Engine, index_factor, maxmh, nprot):
+    """BUCKET_MASS_RANGE = 8000 / index_factor (integer division): peptides whose
+    bucket exceeds NUM_BUCKETS-1 count in totalSeqCount but are not stored
+    (SQLiteMult:277-288); queries touching such buckets return nothing."""
+    prm = DBIndexSearchParams.trypsin(4, index_factor=index_factor, max_precursor_mass=maxmh)
+    pp = fasta.config("1k").slice(0, nprot)
+    oix = _check(Engine, prm, pp, f"drop-{index_factor}")
+    assert oix.n_dropped > 0
+
+
+def test_big_bins_and_duplicates(Engine):
+    """3000 copies of one protein: every peptide repeats 3000x, bins exceed the
+    LDS capacity and take the large-bin path; protein-id lists keep order."""
+    base = fasta.config("1k").sequence(5)
+    seqs = [base] * 3000 + [fasta.config("1k").sequence(i) for i in range(6, 40)]
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    with Engine(cp) as eng:
+        st = eng.build(pp)
+        assert st.n_big_bins > 0
+        assert_index_equal(eng, oix, "bigbins")
+
+
+def test_isobaric_runs(Engine):
+    """I/L swaps give bit-identical masses: equal-mass runs holding several
+    peptide strings must group by string, first appearance first."""
+    rng = np.random.default_rng(11)
+    core = "".join(rng.choice(list("ACDEFGHMNPQSTVWY"), 12))
+    seqs = []
+    for i in range(400):
+        pep = core[:4] + ("I" if rng.random() < 0.5 else "L") + core[5:8] + ("I" if rng.random() < 0.5 else "L") + core[9:]
+        seqs.append("MK" + pep + "K" + "".join(rng.choice(list("ACDEFGHMNPQSTVWY"), 20)) + "R")
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    _check(Engine, DBIndexSearchParams.trypsin(1), pp, "isobaric")
+
+
+def test_zero_mass_long_walks(Engine):
+    """Residues with mass 0 (unknown letters) let a walk run past the LDS halo."""
+    prm = DBIndexSearchParams.trypsin(2)
+    prm.residue_mass["X"] = 0.0
+    seqs = ["AK" + "X" * 700 + "GGGGGGGK" + "X" * 300 + "R", "MKR" + "X" * 5000 + "K"]
+    pp = fasta.PackedProteins.from_sequences(seqs + [fasta.config("1k").sequence(1)])
+    _check(Engine, prm, pp, "zero-mass")
+
+
+def test_empty_inputs(Engine):
+    prm = DBIndexSearchParams.trypsin(2)
+    with Engine(prm) as eng:
+        st = eng.build(fasta.PackedProteins.from_sequences([]))
+        assert st.n_total == 0 and st.n_unique == 0 and st.n_keys == 0
+        f, c = eng.query([1000.0, 2000.0], [0.1, 0.1])
+        assert c.sum() == 0
+        st = eng.build(fasta.PackedProteins.from_sequences(["", "GGK", ""]))
+        assert st.n_total == 0
+
+
+def test_edge_queries(Engine):
+    prm = DBIndexSearchParams.trypsin(2)
+    pp = fasta.config("1k").slice(0, 200)
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    u = oix.unique()["mass"]
+    qs = [(u[0], 0.0), (u[-1], 0.0), (u[len(u) // 2], 0.0), (999.995, 0.01), (1000.0, 0.0),
+          (7999.0, 2.0), (8000.0, 0.0), (3.0, 10.0), (0.0, 0.0), (-5.0, 1.0), (600.0, 1e9),
+          (float("nan"), 1.0), (1500.0, float("nan")), (1500.0, -1.0), (u[10], 1e-12),
+          (2000.0, float("inf"))]
+    m = np.array([q[0] for q in qs])
+    t = np.array([q[1] for q in qs])
+    with Engine(cp) as eng:
+        eng.build(pp)
+        assert_queries_equal(eng, oix, m, t, "edge")
+
+
+def test_exact_mass_lookup(Engine):
+    """getProteins(String): IndexUtil.calculateMass + window [m, m] must find
+    every indexed peptide (bit-identical masses)."""
+    prm = DBIndexSearchParams.trypsin(2)
+    pp = fasta.config("1k").slice(0, 300)
+    with Engine(prm) as eng:
+        eng.build(pp)
+        g = eng.export()
+        idx = np.linspace(0, g["mass"].shape[0] - 1, 400).astype(np.int64)
+        seqs = [pp.sequence(int(g["prot_id"][i]))[int(g["offset"][i]):int(g["offset"][i]) + int(g["length"][i])]
+                for i in idx]
+        masses = np.array([calculate_mass(s, prm) for s in seqs])
+        assert np.array_equal(masses.view(np.uint64), g["mass"][idx].view(np.uint64))
+        first, count = eng.query(masses, np.zeros_like(masses))
+        assert np.all(count >= 1)
+        assert np.all((first <= idx) & (idx < first + count))
+
+
+def test_rebuild_reuses_workspace(Engine):
+    prm = DBIndexSearchParams.trypsin(2)
+    big = fasta.config("1k")
+    small = big.slice(0, 50)
+    cp = prm.to_c()
+    with Engine(cp) as eng:
+        eng.build(big)
+        eng.build(small)
+        assert_index_equal(eng, cref.Index(cp, small.residues, small.offsets), "rebuild-small")
+        eng.build(big)
+        assert_index_equal(eng, cref.Index(cp, big.residues, big.offsets), "rebuild-big")
+
+
+def test_build_device_pointers(Engine):
+    """Residues already resident in HBM (dbi_build_device / dbi_query_device)."""
+    from dbindex_amd._native import DeviceBuffer, synchronize
+    prm = DBIndexSearchParams.trypsin(2)
+    pp = fasta.config("1k")
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    d_res = DeviceBuffer.from_numpy(pp.residues)
+    d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64))
+    with Engine(cp) as eng:
+        eng.build_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins)
+        assert_index_equal(eng, oix, "device-ptr")
+        m, t = query_masses(oix, 1000)
+        dm, dt = DeviceBuffer.from_numpy(m), DeviceBuffer.from_numpy(t)
+        df, dc = DeviceBuffer(8 * 1000), DeviceBuffer(8 * 1000)
+        eng.query_device(dm.ptr, dt.ptr, 1000, df.ptr, dc.ptr)
+        synchronize()
+        f, c = eng.query(m, t)
+        assert np.array_equal(df.download(np.uint64, 1000), f)
+        assert np.array_equal(dc.download(np.uint64, 1000), c)
+
+
+def test_query_csr_and_peptides(Engine):
+    prm = DBIndexSearchParams.trypsin(2)
+    pp = fasta.config("1k").slice(0, 300)
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    m, t = query_masses(oix, 300)
+    with Engine(cp) as eng:
+        eng.build(pp)
+        row, ids = eng.query_csr(m, t)
+        for i in range(300):
+            exp = oix.query(float(m[i]), float(t[i]))
+            assert np.array_equal(ids[row[i]:row[i + 1]], exp)
+        o = oix.unique()
+        sel = np.unique(ids)[:200]
+        pep = eng.peptides(sel)
+        assert np.array_equal(pep["mass"], o["mass"][sel])
+        assert np.array_equal(pep["prot_id"], o["prot_id"][sel])
+        assert np.array_equal(pep["occ_begin"], o["occ_off"][sel])
+        assert np.array_equal(pep["occ_end"], o["occ_off"][sel + 1])

@@ -1,0 +1,205 @@
+"""CPU tests of the oracle (no GPU): hand-derived known-answer tests, the two
+independent restatements (C++ cpu_ref / Python pyref) agreeing bit-exactly,
+and the committed golden fixtures.
+
+Reference semantics under test (paths relative to
+/root/reference/src/main/java/edu/scripps/yates/dbindex/): DBIndexer.cutSeq
+:237-405, DBIndexStoreSQLiteMult :215-350, DBIndexStoreSQLiteByteIndexMerge
+:146-217,386-481,620-719, Util.getResidues :130-162, IndexUtil :197-240.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from dbindex_amd import fasta
+from dbindex_amd.params import DBIndexSearchParams, calculate_mass, tolerance_in_dalton
+from oracle import cref, pyref
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def digest_set(prm, seqs):
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    d = cref.digest(prm.to_c(), pp.residues, pp.offsets)
+    return [(int(p), int(o), int(l)) for p, o, l in zip(d.pid, d.offset, d.length)], d
+
+
+# ---------------------------------------------------------------- KATs
+def test_kat_trypsin_mc0_and_mc2():
+    seq = "AAAAAAKGGGGGGRCCCCCC"
+    got, d = digest_set(DBIndexSearchParams.trypsin(0), [seq])
+    # AAAAAAK, GGGGGGR, GGGGGGRCCCCCC (internal R, C-terminal end: mc = 0), CCCCCC
+    assert got == [(0, 0, 7), (0, 7, 7), (0, 7, 13), (0, 14, 6)]
+    for (p, o, l), m in zip(got, d.mass):
+        assert m == calculate_mass(seq[o:o + l], DBIndexSearchParams())  # bit-identical sequential sum
+    got2, _ = digest_set(DBIndexSearchParams.trypsin(2), [seq])
+    assert got2 == [(0, 0, 7), (0, 0, 14), (0, 0, 20), (0, 7, 7), (0, 7, 13), (0, 14, 6)]
+    assert got2 == sorted(got2)
+
+
+def test_kat_cterm_quirk_allows_maxmc_plus_one():
+    """mc counts K/R *including* the last residue, minus 1 (mc starts at -1):
+    a peptide ending at the protein C-terminus with a non-K/R residue may hold
+    maxMC+1 internal K/R (DBIndexer.java:280,314-316)."""
+    seq = "WWWWWWKWWWWWWW"  # one internal K, C-terminal end not K/R
+    got, _ = digest_set(DBIndexSearchParams.trypsin(0), [seq])
+    assert (0, 0, 14) in got  # mc = 1 - 1 = 0 at the C-terminus although K is internal
+    assert (0, 0, 7) in got and (0, 7, 7) in got
+
+
+def test_kat_nocut_counts_missed_cleavage():
+    """With nocut P, K before P is not a site but still counts as a missed
+    cleavage (quirk ii): no peptide from start 0 at maxMC 0."""
+    seq = "AAAAAAKPAAAAAAR"
+    got0, _ = digest_set(DBIndexSearchParams.trypsin(0, enzyme_nocut_residues="P"), [seq])
+    assert got0 == []
+    got1, _ = digest_set(DBIndexSearchParams.trypsin(1, enzyme_nocut_residues="P"), [seq])
+    assert got1 == [(0, 0, 15)]
+    # empty nocut (the default): KP cleaves
+    got_def, _ = digest_set(DBIndexSearchParams.trypsin(0), [seq])
+    assert got_def == [(0, 0, 7), (0, 7, 8)]
+
+
+def test_kat_min_length_and_mass_bounds():
+    prm = DBIndexSearchParams.trypsin(0)
+    got, _ = digest_set(prm, ["WWWWK" + "WWWWWK"])  # lengths 5 and 6
+    assert got == [(0, 5, 6)]
+    pep = "WWWWWK"
+    m = calculate_mass(pep, prm)
+    # MH+ exactly at minMH / maxMH is included (>= / <=)
+    for lo, hi, exp in [(m, 6000.0, True), (500.0, m, True), (np.nextafter(m, 1e9), 6000.0, False),
+                        (500.0, np.nextafter(m, 0), False)]:
+        p2 = DBIndexSearchParams.trypsin(0, min_precursor_mass=float(lo), max_precursor_mass=float(hi))
+        g, _ = digest_set(p2, ["WWWWK" + pep])
+        assert (g == [(0, 5, 6)]) == exp, (lo, hi)
+
+
+def test_kat_semi_and_nonspecific():
+    seq = "MAAAAAAAKGG"
+    semi, _ = digest_set(DBIndexSearchParams.semi_tryptic(0, min_precursor_mass=100.0), [seq])
+    # N-terminal (start 0) prefixes of length >= 6, and C-anchored suffixes ending at K or C-term
+    assert (0, 0, 6) in semi and (0, 0, 9) in semi and (0, 3, 6) in semi and (0, 5, 6) in semi
+    ns, _ = digest_set(DBIndexSearchParams.non_specific(8, min_precursor_mass=100.0), [seq])
+    assert all(6 <= l <= 8 for _, _, l in ns)
+    assert len(ns) == sum(1 for s in range(len(seq)) for l in range(6, 9) if s + l <= len(seq))
+
+
+def test_kat_duplicates_keep_protein_ids_and_order():
+    """Same peptide twice in protein 0 and once in protein 1: one unique entry,
+    proteinIds [0, 0, 1] in insertion order, first occurrence as representative
+    (IndexMerge.java:656-681)."""
+    seqs = ["PEPTIDEKPEPTIDEK", "GGKPEPTIDEK"]
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    ix = cref.Index(DBIndexSearchParams.trypsin(0, min_precursor_mass=300.0).to_c(), pp.residues, pp.offsets)
+    u = ix.unique()
+    i = int(np.nonzero((u["length"] == 8) & (u["prot_id"] == 0) & (u["offset"] == 0))[0][0])
+    assert list(u["occ_prot"][u["occ_off"][i]:u["occ_off"][i + 1]]) == [0, 0, 1]
+
+
+def test_kat_isobaric_pair_two_entries():
+    seqs = ["PEPTIDEK", "PEPTLDEK"]
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    ix = cref.Index(DBIndexSearchParams.trypsin(0, min_precursor_mass=300.0).to_c(), pp.residues, pp.offsets)
+    u = ix.unique()
+    assert ix.n_unique == 2 and u["mass"][0] == u["mass"][1]
+    # pinned tie order: FNV-1a hash of the string
+    order = sorted(seqs, key=pyref.fnv1a64)
+    assert [seqs[p] for p in u["prot_id"]] == order
+
+
+def test_kat_query_bucket_edges():
+    """Bucket = (int)mass / (8000/index_factor): a window straddling 1000 Da at
+    index_factor 8 spans two buckets; hi >= 8000 -> empty; lo < 0 clamps
+    (DBIndexStoreSQLiteMult.java:315-350)."""
+    pp = fasta.config("1k").slice(0, 200)
+    prm = DBIndexSearchParams.trypsin(2)
+    ix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    st = pyref.build(prm, pp.sequences())
+    u = ix.unique()["mass"]
+    for m, t in [(1000.0, 0.5), (7999.0, 1.5), (3.0, 10.0), (float(u[5]), 0.0), (2500.0, 2500.0)]:
+        ids = list(ix.query(m, t))
+        assert ids == st.get_sequences(m, t)
+        lo, hi = max(0.0, m - t), m + t
+        if int(hi) // 1000 > 7:
+            assert ids == []
+        else:
+            assert ids == [i for i in range(u.shape[0]) if lo <= u[i] <= hi]
+
+
+def test_kat_multirange_reproduces_reference_row_selection():
+    """getSequences(List<MassRange>) with >1 range binds Da-valued bounds to the
+    integer key column (IndexMerge.java:300-312): realistic peptides are never
+    returned; a single range delegates to getSequences(m, tol)."""
+    pp = fasta.config("1k").slice(0, 100)
+    ix = cref.Index(DBIndexSearchParams.trypsin(2).to_c(), pp.residues, pp.offsets)
+    u = ix.unique()["mass"]
+    assert list(ix.query_ranges([u[3]], [0.01])) == list(ix.query(float(u[3]), 0.01))
+    assert list(ix.query_ranges([u[3], u[100]], [0.01, 0.01])) == []
+
+
+def test_kat_residue_flanks_quirk():
+    prot = "ABCDEFGHIJ"
+    assert pyref.get_residues(0, 3, prot) == ("---", "DEF")
+    assert pyref.get_residues(4, 3, prot) == ("BCD", "HIJ"[:2] + "-")  # min(3, 10-7-1) = 2
+    assert pyref.get_residues(7, 2, prot) == ("EFG", "---")             # min(3, 10-9-1) = 0
+    assert pyref.get_residues(7, 3, prot) == ("EFG", "---")
+
+
+def test_java_int_and_tolerance():
+    assert pyref.java_int(float("nan")) == 0
+    assert pyref.java_int(1e12) == 2147483647 and pyref.java_int(-1e12) == -2147483648
+    assert pyref.java_int(-2.7) == -2 and pyref.java_int(2.7) == 2
+    for m, ppm in [(1000.0, 20.0), (2345.678, 5.0), (6000.0, 50.0)]:
+        assert cref.tolerance_in_dalton(m, ppm) == tolerance_in_dalton(m, ppm)
+
+
+# ---------------------------------------------------------------- twins
+@pytest.mark.parametrize("name,prm,n", [
+    ("tryp0", DBIndexSearchParams.trypsin(0), 60),
+    ("tryp2_nocutP", DBIndexSearchParams.trypsin(2, enzyme_nocut_residues="P"), 60),
+    ("semi1", DBIndexSearchParams.semi_tryptic(1), 25),
+    ("nonspec", DBIndexSearchParams.non_specific(20), 8),
+    ("mandK", DBIndexSearchParams.trypsin(2, mandatory_internal_aas="K"), 60),
+    ("drop", DBIndexSearchParams.trypsin(4, index_factor=3000, max_precursor_mass=7999.0), 40),
+])
+def test_twin_restatements_agree(name, prm, n):
+    pp = fasta.config("1k").slice(0, n)
+    seqs = pp.sequences()
+    d = cref.digest(prm.to_c(), pp.residues, pp.offsets)
+    py = pyref.digest(prm, seqs)
+    assert len(py) == d.mass.shape[0]
+    assert np.array_equal(np.array([x[0] for x in py], np.float64).view(np.uint64), d.mass.view(np.uint64))
+    assert [x[1:4] for x in py] == list(zip(d.pid.tolist(), d.offset.tolist(), d.length.tolist()))
+    assert [bool(x[4]) for x in py] == [bool(v) for v in d.dropped]
+    ix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    st = pyref.build(prm, seqs)
+    u = ix.unique()
+    assert len(st.flat) == ix.n_unique
+    assert np.array_equal(np.array([g[0] for g in st.flat], np.float64).view(np.uint64), u["mass"].view(np.uint64))
+    assert st.number_sequences() == ix.n_keys and st.entry_keys() == list(ix.entry_keys())
+
+
+# ---------------------------------------------------------------- golden
+@pytest.mark.parametrize("fname,prm,nprot", [
+    ("golden_1k_tryp0.npz", DBIndexSearchParams.trypsin(0), 1000),
+    ("golden_1k_tryp2.npz", DBIndexSearchParams.trypsin(2), 300),
+])
+def test_oracle_matches_golden(fname, prm, nprot):
+    g = np.load(os.path.join(GOLDEN, fname))
+    pp = fasta.config("1k") if nprot == 1000 else fasta.config("1k").slice(0, nprot)
+    assert bytes(g["residues_sha256"]).decode() == pp.sha256(), "synthetic generator drifted"
+    d = cref.digest(prm.to_c(), pp.residues, pp.offsets)
+    assert np.array_equal(d.mass.view(np.uint64), g["occ_mass"].view(np.uint64))
+    assert np.array_equal(d.pid, g["occ_pid"]) and np.array_equal(d.offset, g["occ_offset"])
+    assert np.array_equal(d.length, g["occ_length"].astype(np.uint32))
+    ix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    u = ix.unique()
+    assert ix.n_total == int(g["n_total"][0]) and ix.n_keys == int(g["n_keys"][0])
+    assert np.array_equal(u["mass"].view(np.uint64), g["u_mass"].view(np.uint64))
+    assert np.array_equal(u["occ_off"], g["u_occ_off"].astype(np.uint64))
+    assert np.array_equal(u["occ_prot"], g["u_occ_prot"])
+    first, count = ix.query_batch(g["q_mass"][:300], g["q_tol"][:300])
+    assert np.array_equal(first, g["q_first"][:300]) and np.array_equal(count, g["q_count"][:300])

@@ -1,0 +1,45 @@
+#!/bin/bash
+# tools/gpu_round.sh TAG [what...] — one GPU-box session: parity tests, bench,
+# rocprofv3 kernel trace + stats, HBM counter passes.  Every GPU step has its
+# own time limit; the script stops at the first failure.
+#   what: tests bench prof pmc smoke (default: tests bench prof)
+set -u -o pipefail
+TAG=${1:-r}
+shift || true
+WHAT=${*:-tests bench prof}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+step() {  # name timeout cmd...
+    local name=$1 to=$2
+    shift 2
+    echo "== $name"
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name exit $rc"
+    tail -5 "$OUT/$name.log"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+}
+for w in $WHAT; do
+    case $w in
+    tests) step tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps 20 --warmup 3
+           cp "$OUT/bench.log" "$OUT/bench.json" ;;
+    bench_sp) step bench_sp 900 python bench.py --config swissprot --steps 5 --warmup 2 ;;
+    prof)  export TMPDIR=/tmp
+           step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
+                -- python3 bench.py --steps 10 --warmup 2 --queries 0 --no-cpu-baseline ;;
+    pmc)   export TMPDIR=/tmp
+           step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
+                -- python3 bench.py --steps 3 --warmup 1 --queries 0 --no-cpu-baseline
+           step pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
+                -- python3 bench.py --steps 3 --warmup 1 --queries 0 --no-cpu-baseline ;;
+    pmc_sq) export TMPDIR=/tmp
+           step pmc_sq 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
+                --output-format csv -d "$OUT/pmc_sq" -o run \
+                -- python3 bench.py --steps 3 --warmup 1 --queries 0 --no-cpu-baseline ;;
+    esac
+done
+echo ALLDONE
