@@ -77,6 +77,7 @@ SIGNATURES = [
     ("dbi_export", c_int, [P, P, P, P, P, P, P]),
     ("dbi_entry_keys", c_int, [P, P, c_uint64, POINTER(c_uint64)]),
     ("dbi_device_view", c_int, [P, POINTER(DbiDeviceIndex)]),
+    ("dbi_set_timing", c_int, [P, c_int, c_char_p]),
     ("dbi_stage_times", c_int, [P, P, P, P, c_uint64, POINTER(c_uint64)]),
     ("dbi_store_create", c_int, [POINTER(DbiParams), c_int, POINTER(c_void_p)]),
     ("dbi_store_close", None, [P]),

@@ -18,7 +18,7 @@ LIB = os.path.join(HERE, "libdbindex_hip.so")
 SOURCES = ["dbi_device.hip", "dbi_engine.hip", "dbi_store.cpp"]
 ARCH = os.environ.get("DBI_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
-         "-Wno-unused-result", f"--offload-arch={ARCH}"]
+         "-Wno-unused-result", "-Wshadow", f"--offload-arch={ARCH}"]
 
 
 def hipcc() -> str:
@@ -59,7 +59,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         out, _ = p.communicate()
         if p.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n{out.decode(errors='replace')}")
-        if verbose and out:
+        if out:  # warnings are never silent
             print(out.decode(errors="replace"), file=sys.stderr)
     tmp = LIB + ".tmp"
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]

@@ -141,7 +141,7 @@ hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_
                                 hipStream_t s) {
     if (n_res == 0 || n_prot == 0) return hipSuccess;
     const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
-    hipLaunchKernelGGL(k_tile_proteins, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
+    DBI_LAUNCH(k_tile_proteins, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
                        d_tile_pf);
     return hipGetLastError();
 }
@@ -380,7 +380,7 @@ static hipError_t launch_digest(const DevParams& dp, const double* d_mass_tab, c
     const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     if (nblk == 0) return hipSuccess;
 #define DBI_DIGEST(SEMI, MAND)                                                                              \
-    hipLaunchKernelGGL((k_digest<EMIT, SEMI, MAND>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
+    DBI_LAUNCH((k_digest<EMIT, SEMI, MAND>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
                        d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_out, d_ctr)
     if (dp.semi) {
         if (dp.mand_mode) DBI_DIGEST(true, true); else DBI_DIGEST(true, false);
@@ -485,14 +485,14 @@ size_t scan_u32_tmp_elems(uint64_t n) { return (size_t)((n + SCAN_CHUNK - 1) / S
 hipError_t launch_scan_u32(const uint32_t* d_in, uint32_t* d_out, uint64_t n, uint32_t* d_block_tmp,
                            uint64_t tmp_elems, unsigned long long* d_total, hipStream_t s) {
     if (n <= SCAN_CHUNK * 4) {
-        hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(SCAN_THREADS), 0, s, d_in, d_out, n, d_total);
+        DBI_LAUNCH(k_scan_single, dim3(1), dim3(SCAN_THREADS), 0, s, d_in, d_out, n, d_total);
         return hipGetLastError();
     }
     const uint64_t nb = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
     if (tmp_elems < nb) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, n, d_block_tmp);
-    hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(SCAN_THREADS), 0, s, d_block_tmp, d_block_tmp, nb, d_total);
-    hipLaunchKernelGGL(k_scan_down, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, d_out, n, d_block_tmp);
+    DBI_LAUNCH(k_scan_reduce, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, n, d_block_tmp);
+    DBI_LAUNCH(k_scan_single, dim3(1), dim3(SCAN_THREADS), 0, s, d_block_tmp, d_block_tmp, nb, d_total);
+    DBI_LAUNCH(k_scan_down, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, d_out, n, d_block_tmp);
     return hipGetLastError();
 }
 
@@ -588,7 +588,7 @@ hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int 
                              hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
-    hipLaunchKernelGGL(k_radix_hist, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, bm, shift, bits, d_hist);
+    DBI_LAUNCH(k_radix_hist, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, bm, shift, bits, d_hist);
     return hipGetLastError();
 }
 
@@ -596,7 +596,7 @@ hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const B
                                 const uint32_t* d_hist, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
-    hipLaunchKernelGGL(k_radix_scatter, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, bm, shift, bits,
+    DBI_LAUNCH(k_radix_scatter, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, bm, shift, bits,
                        d_hist);
     return hipGetLastError();
 }
@@ -620,7 +620,7 @@ hipError_t launch_bin_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, ui
     if (n == 0) {
         return hipMemsetAsync(d_bin_start, 0, sizeof(uint32_t) * ((size_t)bm.nbins + 1), s);
     }
-    hipLaunchKernelGGL(k_bin_bounds, dim3((n + 255) / 256), dim3(256), 0, s, d_recs, n, bm, d_bin_start);
+    DBI_LAUNCH(k_bin_bounds, dim3((n + 255) / 256), dim3(256), 0, s, d_recs, n, bm, d_bin_start);
     return hipGetLastError();
 }
 
@@ -820,7 +820,7 @@ __global__ void k_chunk_bounds(const uint32_t* __restrict__ bin_start, uint32_t 
 
 hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint32_t n, uint32_t T, uint32_t nchunks,
                                uint32_t* d_chunk_lo, uint32_t* d_chunk_bin, hipStream_t s) {
-    hipLaunchKernelGGL(k_chunk_bounds, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_bin_start, nbins, n, T,
+    DBI_LAUNCH(k_chunk_bounds, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_bin_start, nbins, n, T,
                        nchunks, d_chunk_lo, d_chunk_bin);
     return hipGetLastError();
 }
@@ -837,7 +837,7 @@ template <int NT, int CAP>
 __global__ void __launch_bounds__(NT)
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
              const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, uint32_t* __restrict__ big_list,
-             Counters* __restrict__ ctr, uint32_t ablate) {
+             Counters* __restrict__ ctr) {
     __shared__ unsigned long long key[CAP];
     __shared__ unsigned long long hsh[CAP];
     __shared__ uint32_t binid[CAP];
@@ -862,7 +862,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         const Rec r = in[a + i];
         key[i] = dbits(r.mass);
         binid[i] = bin_of(r.mass, bm);
-        hsh[i] = (ablate & 1) ? 0ull : pep_hash(res, r.gstart, r.len);
+        hsh[i] = pep_hash(res, r.gstart, r.len);
     }
     __syncthreads();
     // runs of equal bin id (records are grouped by bin): compact the run starts
@@ -902,10 +902,6 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
             if (lane == 0) s_bad = 1;
             continue;
         }
-        if (ablate & 2) {
-            for (uint32_t i = lo + lane; i < hi; i += 64) perm[i] = (uint16_t)i;
-            continue;
-        }
         for (uint32_t base = lo; base < hi; base += 64) {
             const uint32_t i = base + lane;
             const bool act = i < hi;
@@ -928,7 +924,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
             const uint32_t ip = perm[p - 1];
             if (key[i] == key[ip] && hsh[i] == hsh[ip]) {
                 head = false;
-                if (!(ablate & 4) && !seq_equal(res, in[a + i], in[a + ip])) s_bad = 1;
+                if (!seq_equal(res, in[a + i], in[a + ip])) s_bad = 1;
             }
         }
         myheads += head;
@@ -938,7 +934,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
         return;
     }
-    for (uint32_t p = threadIdx.x; p < m && !(ablate & 8); p += NT) {
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
         const uint32_t i = perm[p];
         const bool head = p == 0 || key[i] != key[perm[p - 1]] || hsh[i] != hsh[perm[p - 1]];
         Rec r = in[a + i];
@@ -953,9 +949,8 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
                              uint32_t nchunks, const uint8_t* d_res, uint32_t* d_ucount, uint32_t* d_big_list,
                              Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    static const uint32_t ablate = getenv("DBI_ABLATE") ? (uint32_t)atoi(getenv("DBI_ABLATE")) : 0u;
-    hipLaunchKernelGGL((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
-                       d_out, bm, d_chunk_lo, d_res, d_ucount, d_big_list, d_ctr, ablate);
+    DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
+                       d_out, bm, d_chunk_lo, d_res, d_ucount, d_big_list, d_ctr);
     return hipGetLastError();
 }
 
@@ -988,7 +983,7 @@ hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chun
                              uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t max_blocks,
                              unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr, hipStream_t s) {
     if (max_blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_big_chunks, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res,
+    DBI_LAUNCH(k_big_chunks, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res,
                        d_ucount, d_big_list, d_ws_key, d_ws_k2, d_ctr);
     return hipGetLastError();
 }
@@ -1037,7 +1032,7 @@ hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32
                            uint32_t* d_occ_off, uint32_t* d_occ_pid, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
-    hipLaunchKernelGGL(k_finalize, dim3(nchunks), dim3(256), 0, s, d_recs, d_chunk_lo, d_ubase, d_poff, n_prot,
+    DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(256), 0, s, d_recs, d_chunk_lo, d_ubase, d_poff, n_prot,
                        d_tile_pf, ntiles, d_umass, d_upid, d_uoff, d_ulen, d_occ_off, d_occ_pid);
     return hipGetLastError();
 }
@@ -1065,7 +1060,7 @@ hipError_t launch_count_keys(const double* d_umass, uint32_t n_upper, int32_t fa
                              Counters* d_ctr, hipStream_t s) {
     if (n_upper == 0) return hipSuccess;
     const uint32_t g = min((n_upper + 255) / 256, 1024u);
-    hipLaunchKernelGGL(k_count_keys, dim3(g), dim3(256), 0, s, d_umass, factor, d_flags, d_ctr);
+    DBI_LAUNCH(k_count_keys, dim3(g), dim3(256), 0, s, d_umass, factor, d_flags, d_ctr);
     return hipGetLastError();
 }
 
@@ -1075,7 +1070,7 @@ __global__ void k_write_tail(uint32_t* __restrict__ occ_off, uint32_t n_kept, co
 }
 
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s) {
-    hipLaunchKernelGGL(k_write_tail, dim3(1), dim3(64), 0, s, d_occ_off, n_kept, d_ctr);
+    DBI_LAUNCH(k_write_tail, dim3(1), dim3(64), 0, s, d_occ_off, n_kept, d_ctr);
     return hipGetLastError();
 }
 
@@ -1101,7 +1096,7 @@ hipError_t launch_gather(const uint64_t* d_ids, uint64_t n, const double* d_umas
                          double* o_mass, uint32_t* o_pid, uint32_t* o_off, uint32_t* o_len, uint64_t* o_b,
                          uint64_t* o_e, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gather, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_ids, n, d_umass, d_upid,
+    DBI_LAUNCH(k_gather, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_ids, n, d_umass, d_upid,
                        d_uoff, d_ulen, d_occ_off, o_mass, o_pid, o_off, o_len, o_b, o_e);
     return hipGetLastError();
 }
@@ -1117,7 +1112,7 @@ __global__ void k_write_keys(const double* __restrict__ umass, uint32_t n, int32
 hipError_t launch_write_keys(const double* d_umass, uint32_t n_unique, int32_t factor, const uint32_t* d_pos,
                              int32_t* d_keys, hipStream_t s) {
     if (n_unique == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_write_keys, dim3((n_unique + 255) / 256), dim3(256), 0, s, d_umass, n_unique, factor,
+    DBI_LAUNCH(k_write_keys, dim3((n_unique + 255) / 256), dim3(256), 0, s, d_umass, n_unique, factor,
                        d_pos, d_keys);
     return hipGetLastError();
 }
@@ -1181,7 +1176,7 @@ hipError_t launch_query(const DevParams& dp, int32_t factor, const double* d_uma
                         const double* d_qmass, const double* d_qtol, uint64_t nq, uint64_t* d_first,
                         uint64_t* d_count, hipStream_t s) {
     if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_query, dim3((uint32_t)((nq + 255) / 256)), dim3(256), 0, s, dp, factor, d_umass,
+    DBI_LAUNCH(k_query, dim3((uint32_t)((nq + 255) / 256)), dim3(256), 0, s, dp, factor, d_umass,
                        n_unique, d_qmass, d_qtol, nq, d_first, d_count);
     return hipGetLastError();
 }
@@ -1196,7 +1191,7 @@ __global__ void k_key_range(const double* __restrict__ umass, uint32_t nu, int32
 
 hipError_t launch_key_range(const double* d_umass, uint32_t n_unique, int32_t factor, int32_t klo,
                             int32_t khi, uint64_t* d_out2, hipStream_t s) {
-    hipLaunchKernelGGL(k_key_range, dim3(1), dim3(64), 0, s, d_umass, n_unique, factor, klo, khi, d_out2);
+    DBI_LAUNCH(k_key_range, dim3(1), dim3(64), 0, s, d_umass, n_unique, factor, klo, khi, d_out2);
     return hipGetLastError();
 }
 
@@ -1211,7 +1206,7 @@ __global__ void k_expand_csr(const uint64_t* __restrict__ first, const uint64_t*
 hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
                              uint64_t nq, uint64_t* d_ids, hipStream_t s) {
     if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_expand_csr, dim3((uint32_t)nq), dim3(64), 0, s, d_first, d_count, d_row, nq, d_ids);
+    DBI_LAUNCH(k_expand_csr, dim3((uint32_t)nq), dim3(64), 0, s, d_first, d_count, d_row, nq, d_ids);
     return hipGetLastError();
 }
 
@@ -1233,7 +1228,7 @@ hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const
                               const uint32_t* d_len, const uint32_t* d_poff, uint64_t n, Rec* d_out,
                               hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_occ_to_recs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_mass, d_pid, d_off,
+    DBI_LAUNCH(k_occ_to_recs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_mass, d_pid, d_off,
                        d_len, d_poff, n, d_out);
     return hipGetLastError();
 }
@@ -1245,7 +1240,7 @@ __global__ void k_off64_to_32(const uint64_t* __restrict__ in, uint32_t* __restr
 
 hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_off64_to_32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, d_out, n);
+    DBI_LAUNCH(k_off64_to_32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, d_out, n);
     return hipGetLastError();
 }
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -59,12 +60,18 @@ struct DevBuf {
 
 using namespace dbi;
 
+namespace dbi {
+thread_local LaunchEvents t_launch_ev;
+}
+
 struct dbi_handle {
     dbi_params params;
     DevParams dp;
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    bool timing = true;                  // per-stage kernel-attached events (dbi_set_timing)
+    std::string timing_only;             // "" = every stage
+    std::chrono::steady_clock::time_point t0;
 
     DevBuf<double> mass_tab;
     DevBuf<uint8_t> flags_tab;
@@ -114,6 +121,7 @@ struct dbi_handle {
         int eb, ee;                     // event pool slots
         double cR, cN, cU, cP, cB;      // algorithmic bytes = cR*R + cN*N + cU*U + cP*P + cB*nbins
         double ms, bytes;
+        bool launched;
     };
     static constexpr int MAX_STAGES = 48;
     hipEvent_t evpool[2 * MAX_STAGES] = {};
@@ -190,19 +198,26 @@ int stage_begin(dbi_handle* h, const char* name, Bytes b) {
     st.cR = b.cR; st.cN = b.cN; st.cU = b.cU; st.cP = b.cP; st.cB = b.cB;
     st.ms = 0;
     st.bytes = 0;
-    (void)hipEventRecord(h->evpool[st.eb], h->stream);
+    st.launched = false;
+    if (h->timing && (h->timing_only.empty() || h->timing_only == name))
+        t_launch_ev = LaunchEvents{h->evpool[st.eb], h->evpool[st.ee]};
+    else
+        t_launch_ev = LaunchEvents{};
     return i;
 }
 
 void stage_end(dbi_handle* h, int i) {
-    if (i >= 0) (void)hipEventRecord(h->evpool[h->stages[i].ee], h->stream);
+    // the first launch of the stage consumed `start`: otherwise nothing ran
+    if (i >= 0) h->stages[i].launched = t_launch_ev.stop != nullptr && t_launch_ev.start == nullptr;
+    t_launch_ev = LaunchEvents{};
 }
 
-#define STAGE(h, NAME, BYTES, EXPR)               \
-    do {                                          \
+#define STAGE(h, NAME, BYTES, EXPR)                  \
+    do {                                             \
         const int _si = stage_begin(h, NAME, BYTES); \
-        DBI_HIP(EXPR);                            \
-        stage_end(h, _si);                        \
+        const hipError_t _stage_err = (EXPR);        \
+        stage_end(h, _si);                           \
+        DBI_HIP(_stage_err);                         \
     } while (0)
 
 Bytes by(double cR, double cN, double cU, double cP, double cB) {
@@ -284,13 +299,10 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
 }
 
 int finish_build(dbi_handle* h) {
-    DBI_HIP(hipEventRecord(h->ev1, h->stream));
     int rc = read_counters(h);
     if (rc) return rc;
     if (h->hc.err & ERR_LEN_OVERFLOW) return set_error(DBI_E_INVALID, "peptide longer than 65535 residues");
-    float ms = 0, ms_d = 0;
-    DBI_HIP(hipEventElapsedTime(&ms, h->ev0, h->ev1));
-    DBI_HIP(hipEventElapsedTime(&ms_d, h->ev0, h->ev2));
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h->t0).count();
     dbi_stats& st = h->stats;
     st.n_residues = h->n_res;
     st.n_proteins = h->n_prot;
@@ -302,12 +314,13 @@ int finish_build(dbi_handle* h) {
     for (int i = 0; i < 8; ++i) st.n_keys += h->hc.n_keys_shard[i];
     st.n_big_bins = h->hc.n_big;
     st.build_ms = ms;
-    st.digest_ms = ms_d;
+    st.digest_ms = 0;
     for (int i = 0; i < h->nstage; ++i) {
         auto& sg = h->stages[i];
         float t = 0;
-        if (hipEventElapsedTime(&t, h->evpool[sg.eb], h->evpool[sg.ee]) != hipSuccess) t = 0;
+        if (!sg.launched || hipEventElapsedTime(&t, h->evpool[sg.eb], h->evpool[sg.ee]) != hipSuccess) t = 0;
         sg.ms = t;
+        if (std::strncmp(sg.name, "digest", 6) == 0) st.digest_ms += t;
         sg.bytes = sg.cR * (double)h->n_res + sg.cN * (double)st.n_kept + sg.cU * (double)st.n_unique +
                    sg.cP * (double)(h->n_prot + 1) + sg.cB * (double)st.n_bins;
     }
@@ -357,7 +370,6 @@ int build_digest(dbi_handle* h) {
     STAGE(h, "digest_emit", by(1, 16, 0, 4, 0),
           launch_digest_emit(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
                              (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->recA.p, h->ctr.p, s));
-    DBI_HIP(hipEventRecord(h->ev2, s));
     return build_tail(h, n, h->params.min_mh, h->params.max_mh);
 }
 
@@ -371,7 +383,7 @@ int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
     h->n_total_extra = 0;
     std::memset(&h->stats, 0, sizeof(h->stats));
     h->nstage = 0;
-    DBI_HIP(hipEventRecord(h->ev0, h->stream));
+    h->t0 = std::chrono::steady_clock::now();
     DBI_HIP(hipMemsetAsync(h->ctr.p, 0, sizeof(Counters), h->stream));
     return 0;
 }
@@ -493,9 +505,6 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     };
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(set_error(DBI_E_HIP, "hipStreamCreate failed"));
-    if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
-        hipEventCreate(&h->ev2) != hipSuccess)
-        return fail(set_error(DBI_E_HIP, "hipEventCreate failed"));
     for (auto& ev : h->evpool)
         if (hipEventCreate(&ev) != hipSuccess) return fail(set_error(DBI_E_HIP, "hipEventCreate failed"));
     if ((rc = h->mass_tab.ensure(256)) || (rc = h->flags_tab.ensure(256)) || (rc = h->ctr.ensure(1)))
@@ -528,9 +537,6 @@ void dbi_close(dbi_handle* h) {
     h->g_b.release(); h->g_e.release();
     for (auto& ev : h->evpool)
         if (ev) (void)hipEventDestroy(ev);
-    if (h->ev0) (void)hipEventDestroy(h->ev0);
-    if (h->ev1) (void)hipEventDestroy(h->ev1);
-    if (h->ev2) (void)hipEventDestroy(h->ev2);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -542,7 +548,6 @@ int dbi_build(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint
     if ((rc = check_residues_host(residues, n_res))) return rc;
     if ((rc = begin_build(h, n_res, n_prot))) return rc;
     if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
-    DBI_HIP(hipEventRecord(h->ev0, h->stream));  // device time excludes the H2D copy
     if ((rc = build_digest(h))) return rc;
     return finish_build(h);
 }
@@ -588,7 +593,6 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
     }
     if ((rc = begin_build(h, n_res, n_prot))) return rc;
     if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
-    DBI_HIP(hipEventRecord(h->ev0, h->stream));
     if ((rc = h->o_mass.ensure(n_occ)) || (rc = h->o_pid.ensure(n_occ)) || (rc = h->o_off.ensure(n_occ)) ||
         (rc = h->o_len.ensure(n_occ)) || (rc = h->recA.ensure(n_occ)))
         return rc;
@@ -605,7 +609,6 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
     c0.n_kept = n_occ;
     DBI_HIP(hipMemcpyAsync(h->ctr.p, &c0, sizeof(Counters), hipMemcpyHostToDevice, h->stream));
     DBI_HIP(hipStreamSynchronize(h->stream));
-    DBI_HIP(hipEventRecord(h->ev2, h->stream));
     h->n_total_extra = n_dropped_extra;
     if ((rc = prepare_tiles(h))) return rc;
     if ((rc = build_tail(h, n_occ, lo, hi))) return rc;
@@ -781,6 +784,13 @@ int dbi_entry_keys(dbi_handle* h, int32_t* keys, uint64_t cap, uint64_t* n) {
     pos.release();
     dk.release();
     if (e != hipSuccess) return hip_fail(e, "dbi_entry_keys");
+    return 0;
+}
+
+int dbi_set_timing(dbi_handle* h, int on, const char* only) {
+    if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    h->timing = on != 0;
+    h->timing_only = only ? only : "";
     return 0;
 }
 

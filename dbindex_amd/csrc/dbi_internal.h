@@ -2,6 +2,7 @@
 // host orchestration (dbi_engine.hip, dbi_store.cpp).  Not part of the C-ABI.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -134,6 +135,18 @@ hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n,
 hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
                              uint64_t nq, uint64_t* d_ids, hipStream_t s);
 
+// ---- per-stage timing ----------------------------------------------------------
+// Events of the stage being launched, attached to the dispatch packets
+// themselves (hipExtLaunchKernelGGL): timing adds no marker packets, hence no
+// idle gaps, between kernels.  `start` is consumed by the first launch of the
+// stage; every launch re-records `stop`, so it ends up at the stage's last
+// kernel.  Both null = untimed.
+struct LaunchEvents {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+};
+extern thread_local LaunchEvents t_launch_ev;
+
 // ---- error plumbing (dbi_engine.hip) ------------------------------------------------
 int set_error(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
@@ -147,6 +160,13 @@ __host__ __device__ inline int32_t java_d2i(double d) {
 }
 
 }  // namespace dbi
+
+#define DBI_LAUNCH(KERNEL, GRID, BLOCK, SHMEM, STREAM, ...)                                                  \
+    do {                                                                                                   \
+        hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, SHMEM, STREAM, ::dbi::t_launch_ev.start,                \
+                              ::dbi::t_launch_ev.stop, 0u, __VA_ARGS__);                                   \
+        ::dbi::t_launch_ev.start = nullptr;                                                                \
+    } while (0)
 
 #define DBI_HIP(expr)                                          \
     do {                                                       \

@@ -162,9 +162,14 @@ class Engine:
         check(_native.lib().dbi_entry_keys(self.h, _p(keys), n.value, ctypes.byref(n)))
         return keys
 
+    def set_timing(self, on: bool, only: str = "") -> None:
+        """Per-kernel HIP events carried by the dispatch packets (default: every
+        stage); ``only`` restricts them to the stages of that name."""
+        check(_native.lib().dbi_set_timing(self.h, 1 if on else 0, only.encode()))
+
     def stage_times(self):
-        """[(kernel, ms, algorithmic bytes)] of the last build, from HIP events
-        recorded on the engine stream around every launch."""
+        """[(kernel, ms, algorithmic bytes)] of the last build, from the HIP
+        events carried by each kernel's dispatch packet (0 ms if untimed)."""
         n = ctypes.c_uint64()
         check(_native.lib().dbi_stage_times(self.h, None, None, None, 0, ctypes.byref(n)))
         k = n.value

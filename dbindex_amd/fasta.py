@@ -22,6 +22,7 @@ AA_FREQ = {
     "G": 7.07, "H": 2.27, "I": 5.96, "L": 9.66, "K": 5.84, "M": 2.42, "F": 3.86,
     "P": 4.70, "S": 6.56, "T": 5.34, "W": 1.08, "Y": 2.92, "V": 6.87,
 }
+CANONICAL = "".join(AA_FREQ)
 
 # Named synthetic configurations (BASELINE.json configs; seeds per SURVEY.md §8(d))
 CONFIGS = {

@@ -28,8 +28,17 @@ FilterResult_SKIP_PROTEIN_START = _native.FILTER_SKIP_PROTEIN_START
 
 @dataclass
 class ResidueInfo:
+    """``edu.scripps.yates.utilities.fasta.dbindex.ResidueInfo`` (external):
+    the 3-residue left/right flanks, padded with '-'."""
+
     resLeft: str
     resRight: str
+
+    def getResLeft(self) -> str:
+        return self.resLeft
+
+    def getResRight(self) -> str:
+        return self.resRight
 
 
 @dataclass

@@ -191,11 +191,17 @@ typedef struct dbi_device_index {
 } dbi_device_index;
 int dbi_device_view(dbi_handle* h, dbi_device_index* out);
 
-/* Per-kernel device times of the last build, from HIP events recorded on the
- * engine stream around every launch (always on; a few us per build).
- * names[i] are static strings ("digest_count", "digest_emit", "radix_hist",
- * "radix_scatter", "bin_sort", ...); bytes[i] = algorithmic HBM bytes of that
- * launch.  Arrays may be NULL to query *n. */
+/* Per-kernel device times of the last build.  With timing on (the default)
+ * every launch carries HIP start/stop events in its own dispatch packet
+ * (hipExtLaunchKernelGGL on the engine stream), so timing inserts no marker
+ * packets and no idle gaps between kernels.  names[i] are static strings
+ * ("digest_count", "digest_emit", "radix_scatter", "chunk_sort", ...);
+ * ms[i] = 0 for a stage that launched nothing or with timing off;
+ * bytes[i] = algorithmic HBM bytes of that launch.
+ * Arrays may be NULL to query *n. */
+/* on = 0: no events (wall clock only); on = 1: time every stage, or only the
+ * stages named `only` (NULL or "" = all) — each timed stage costs a few us. */
+int dbi_set_timing(dbi_handle* h, int on, const char* only);
 int dbi_stage_times(dbi_handle* h, const char** names, double* ms, double* bytes, uint64_t cap,
                     uint64_t* n);
 

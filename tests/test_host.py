@@ -1,0 +1,171 @@
+"""CPU tests (no GPU): the C-ABI library loads and exports every symbol of
+include/dbindex_hip.h, parameter packing, the DBIndexStore mirror's host-side
+state machine and filters, the indexer's host checks, and the synthetic
+FASTA generator / reader.  Nothing here launches a kernel.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from dbindex_amd import _native, fasta
+from dbindex_amd.indexer import DBIndexer, DBIndexerException
+from dbindex_amd.params import DBIndexSearchParams, DbiParams, MONO_RESIDUE_MASS
+from dbindex_amd.store import DBIndexStoreHip, get_residues
+from oracle import pyref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dbindex_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_ \*]*?\b(dbi_[a-z0-9_]+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _native.lib()
+    names = header_functions()
+    assert len(names) >= 40
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    bound = {n for n, _, _ in _native.SIGNATURES}
+    assert set(names) == bound, (set(names) ^ bound)
+
+
+def test_abi_version_and_errors():
+    L = _native.lib()
+    assert L.dbi_abi_version() >= 1
+    s = ctypes.c_void_p()
+    bad = DBIndexSearchParams(index_factor=0).to_c()
+    assert L.dbi_store_create(ctypes.byref(bad), 0, ctypes.byref(s)) == _native.DBI_E_INVALID
+    assert b"index_factor" in L.dbi_last_error()
+
+
+@pytest.mark.parametrize("mc,semi", [(0, 0), (2, 0), (2, 1)])
+def test_params_default_matches_python(mc, semi):
+    c = DbiParams()
+    _native.lib().dbi_params_default(ctypes.byref(c), mc, semi)
+    py = (DBIndexSearchParams.semi_tryptic(mc) if semi else DBIndexSearchParams.trypsin(mc)).to_c()
+    assert bytes(c) == bytes(py)
+
+
+def test_mass_table_literals():
+    # monoisotopic residue masses pinned in DESIGN.md (AssignMass is absent from the reference)
+    assert MONO_RESIDUE_MASS["G"] == 57.021464
+    assert MONO_RESIDUE_MASS["W"] == 186.079313
+    assert MONO_RESIDUE_MASS["K"] == 128.094963
+    assert len([k for k in MONO_RESIDUE_MASS if k in fasta.CANONICAL]) == 20
+    assert MONO_RESIDUE_MASS["I"] == MONO_RESIDUE_MASS["L"]
+
+
+# ------------------------------------------------------------- store (host)
+def test_store_state_machine_messages():
+    st = DBIndexStoreHip(DBIndexSearchParams.trypsin(2))
+    with pytest.raises(_native.DBIndexStoreException, match="not initialized"):
+        st.startAddSeq()
+    with pytest.raises(_native.DBIndexStoreException, match="Index path is missing"):
+        st.init("")
+    st.init("x.fasta_dbindex")
+    with pytest.raises(_native.DBIndexStoreException, match="Already intialized"):
+        st.init("x.fasta_dbindex")
+    with pytest.raises(_native.DBIndexStoreException, match="Not in transaction"):
+        st.stopAddSeq()
+    st.startAddSeq()
+    with pytest.raises(_native.DBIndexStoreException, match="In transaction already"):
+        st.startAddSeq()
+    assert not st.indexExists() and st.getNumberSequences() == 0 and st.getEntryKeys() == []
+    st.close()
+
+
+def test_store_filter_sequence_matches_reference_rule():
+    for prm in [DBIndexSearchParams.trypsin(2), DBIndexSearchParams.trypsin(2, mandatory_internal_aas="CK")]:
+        st = DBIndexStoreHip(prm)
+        for m, seq in [(499.99, "AAAAAK"), (500.0, "AAAAAK"), (6000.0, "ACAAAK"), (6000.01, "ACAAAK"),
+                       (800.0, "AAAAAC"), (800.0, "KAAAAA"), (800.0, "AAAAAA")]:
+            assert st.filterSequence(m, seq) == pyref.filter_sequence(prm, m, seq), (m, seq)
+        st.close()
+    st = DBIndexStoreHip(DBIndexSearchParams.trypsin(2), device_digest=True)
+    assert st.filterSequence(800.0, "AAAAAK") == _native.FILTER_SKIP_PROTEIN_START
+    st.close()
+
+
+def test_store_add_sequence_validation_and_drop_count():
+    prm = DBIndexSearchParams.trypsin(2, index_factor=8)
+    st = DBIndexStoreHip(prm)
+    st.init("db")
+    st.startAddSeq()
+    assert st.addProteinDef(0, "sp|P1|A\tB", "PEPTIDEKAAAAAAK") == 0
+    assert st.getProteinDef(0) == "sp|P1|A B"  # ProteinCache.addProtein tab -> space
+    assert st.getProteinSequence(0) == "PEPTIDEKAAAAAAK" and st.getNumberProteins() == 1
+    with pytest.raises(_native.DBIndexStoreException, match="protein numbers"):
+        st.addProteinDef(5, "x", "AAA")
+    st.addSequence(927.45, 0, 8, proteinId=0)
+    st.addSequence(8000.5, 0, 8, proteinId=0)  # bucket 8 > NUM_BUCKETS-1: dropped, still counted
+    assert st.getTotalSeqCount() == 2
+    with pytest.raises(_native.DBIndexStoreException, match="outside its protein"):
+        st.addSequence(927.45, 10, 8, proteinId=0)
+    with pytest.raises(_native.DBIndexStoreException, match="addProteinDef"):
+        st.addSequence(927.45, 0, 8, proteinId=3)
+    st.close()
+
+
+def test_get_residues_twins():
+    prot = "MKWVTFISLLLLFSSAYSRGVFRR"
+    for off in range(0, len(prot) - 6):
+        for ln in (6, 7, 9):
+            if off + ln > len(prot):
+                continue
+            r = get_residues(off, ln, prot)
+            assert (r.getResLeft(), r.getResRight()) == pyref.get_residues(off, ln, prot)
+
+
+# ------------------------------------------------------------- indexer (host)
+def test_indexer_host_checks():
+    prm = DBIndexSearchParams.trypsin(2)
+    ix = DBIndexer(prm)
+    with pytest.raises(RuntimeError, match="Not initialized"):
+        ix.run([("sp|P1|X", "PEPTIDEK")])
+    ix.init()
+    with pytest.raises(RuntimeError, match="Already inited"):
+        ix.init()
+    with pytest.raises(DBIndexerException, match="Uniprot"):
+        ix.run([("no accession here", "PEPTIDEK")])
+    with pytest.raises(DBIndexerException, match="formula"):
+        ix.cutSeq("sp|P1|X", "PEP[C2H2]TIDEK")
+
+
+# ------------------------------------------------------------- FASTA
+def test_synthetic_deterministic_and_canonical():
+    a = fasta.config("1k")
+    b = fasta.config("1k")
+    assert a.sha256() == b.sha256() and a.n_proteins == 1000
+    lens = np.diff(a.offsets)
+    assert lens.min() >= 30 and lens.max() <= 35000
+    assert set(np.unique(a.residues).tobytes().decode()) <= set(fasta.CANONICAL)
+    assert all(fasta.uniprot_accession(d) for d in a.defs[:50])
+    assert fasta.config("human").n_proteins == 20000
+
+
+def test_fasta_write_read_roundtrip(tmp_path):
+    pp = fasta.config("1k").slice(0, 40)
+    path = tmp_path / "syn.fasta"
+    with open(path, "w") as fh:
+        fasta.write_fasta(pp, fh)
+    text = path.read_text()
+    assert all(len(l) <= 60 for l in text.splitlines() if not l.startswith(">"))
+    back = fasta.read_fasta(str(path))
+    assert back.sha256() == pp.sha256() and back.defs == pp.defs
+
+
+def test_slice_and_from_sequences():
+    pp = fasta.config("1k")
+    s = pp.slice(10, 20)
+    assert s.sequences() == pp.sequences()[10:20]
+    t = fasta.PackedProteins.from_sequences(s.sequences())
+    assert np.array_equal(t.residues, s.residues) and np.array_equal(t.offsets, s.offsets)

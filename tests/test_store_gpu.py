@@ -1,0 +1,164 @@
+"""GPU parity of the Java-API mirror (DBIndexer / DBIndexStore over the C-ABI
+``dbi_store_*``) against the oracle: every field of every IndexedSequence a
+query returns (sequence, mass bits, proteinIds in order, flanks, offset,
+length), the store counters, entry keys / parent masses, ppm and multi-range
+queries, getProteins(String), and the golden fixtures.
+
+Reference flows: DBIndexer.run/cutSeq (DBIndexer.java:237-405,508-684),
+DBIndexStoreSQLiteMult (:245-350), IndexMerge.getSequences/parseAddPeptideInfo
+(:146-217,386-481), Util.getResidues (:130-162).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from dbindex_amd import fasta
+from dbindex_amd.indexer import DBIndexer
+from dbindex_amd.params import DBIndexSearchParams, calculate_mass, tolerance_in_dalton
+from dbindex_amd.store import DBIndexStoreHip, MassRange
+from oracle import cref, pyref
+from tests.helpers import query_masses
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from dbindex_amd import _native
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+
+
+def expected(oix, seqs, ids):
+    u = oix.unique()
+    out = []
+    for i in ids:
+        pids = [int(x) for x in u["occ_prot"][u["occ_off"][i]:u["occ_off"][i + 1]]]
+        p0, off, ln = int(u["prot_id"][i]), int(u["offset"][i]), int(u["length"][i])
+        assert pids[0] == p0
+        left, right = pyref.get_residues(off, ln, seqs[p0])
+        out.append((seqs[p0][off:off + ln], float(u["mass"][i]), pids, left, right, off, ln))
+    return out
+
+
+def got(lst):
+    return [(s.getSequence(), s.getMass(), list(s.getProteinIds()), s.getResLeft(), s.getResRight(),
+             s.getSequenceOffset(), s.getSequenceLen()) for s in lst]
+
+
+def same(a, b):
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert x[0] == y[0] and np.float64(x[1]).view(np.uint64) == np.float64(y[1]).view(np.uint64)
+        assert x[2:] == y[2:], (x, y)
+
+
+def _indexer(prm, pp):
+    ix = DBIndexer(prm)
+    ix.init()
+    ix.run(pp)
+    return ix
+
+
+@pytest.mark.parametrize("name,prm,nprot", [
+    ("tryp2", DBIndexSearchParams.trypsin(2), 150),
+    ("semi1", DBIndexSearchParams.semi_tryptic(1), 40),
+    ("tryp1_if6", DBIndexSearchParams.trypsin(1, index_factor=6, enzyme_nocut_residues="P"), 150),
+])
+def test_indexer_device_digest(name, prm, nprot):
+    pp = fasta.config("1k").slice(0, nprot)
+    seqs = pp.sequences()
+    oix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    ix = _indexer(prm, pp)
+    st = ix.indexStore
+    assert st.indexExists()
+    assert st.getTotalSeqCount() == oix.n_total
+    assert st.getNumberSequences() == oix.n_keys == ix.getNumParentMasses()
+    keys = list(oix.entry_keys())
+    assert st.getEntryKeys() == keys
+    assert ix.getParentMasses() == [k * 1.0 / prm.mass_group_factor for k in keys]
+    m, t = query_masses(oix, 150, seed=11)
+    for mi, ti in zip(m, t):
+        same(got(ix.getSequencesUsingDaltonTolerance(float(mi), float(ti))),
+             expected(oix, seqs, oix.query(float(mi), float(ti))))
+
+
+def test_store_host_digest_flow():
+    """The reference's own flow: cutSeq -> filterSequence -> addSequence per
+    peptide (the oracle's cutSeq drives the store), then stopAddSeq builds."""
+    prm = DBIndexSearchParams.trypsin(2, index_factor=3000, max_precursor_mass=7999.0)
+    pp = fasta.config("1k").slice(0, 120)
+    seqs = pp.sequences()
+    oix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    st = DBIndexStoreHip(prm)
+    st.init("synthetic.fasta_dbindex")
+    st.startAddSeq()
+    for i, s in enumerate(seqs):
+        assert st.addProteinDef(i, pp.defs[i], s) == i
+    for (mass, pid, off, ln, _dropped) in pyref.digest(prm, seqs):
+        assert st.filterSequence(mass, seqs[pid][off:off + ln]) == 0
+        st.addSequence(mass, off, ln, proteinId=pid)
+    st.stopAddSeq()
+    assert oix.n_dropped > 0
+    assert st.getTotalSeqCount() == oix.n_total
+    assert st.getNumberSequences() == oix.n_keys and st.getEntryKeys() == list(oix.entry_keys())
+    m, t = query_masses(oix, 100, seed=3)
+    for mi, ti in zip(m, t):
+        same(got(st.getSequences(float(mi), float(ti))), expected(oix, seqs, oix.query(float(mi), float(ti))))
+    st.close()
+
+
+def test_ppm_multirange_and_proteins():
+    prm = DBIndexSearchParams.trypsin(2)
+    pp = fasta.config("1k").slice(0, 200)
+    seqs = pp.sequences()
+    oix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    ix = _indexer(prm, pp)
+    u = oix.unique()
+    for i in range(0, oix.n_unique, max(1, oix.n_unique // 60)):
+        mi = float(u["mass"][i])
+        tol = tolerance_in_dalton(mi, 10.0)
+        res = got(ix.getSequencesUsingPPMTolerance(mi, 10.0))
+        base = expected(oix, seqs, oix.query(mi, tol))
+        # the ppm path = the Dalton window plus the upper-bound probe loop (DBIndexer.java:787-844)
+        assert [r[0] for r in res[:len(base)]] == [b[0] for b in base]
+        assert len({r[0] for r in res}) == len(res)
+        # single range delegates to getSequences(m, tol); >1 range reproduces the key-column binding
+        same(got(ix.getSequences([MassRange(mi, 0.02)])), expected(oix, seqs, oix.query(mi, 0.02)))
+        j = (i * 7 + 3) % oix.n_unique
+        mj = float(u["mass"][j])
+        same(got(ix.getSequences([MassRange(mi, 0.02), MassRange(mj, 0.5)])),
+             expected(oix, seqs, oix.query_ranges([mi, mj], [0.02, 0.5])))
+        # getProteins(String): exact-mass lookup + string equality (DBIndexer.java:925-947)
+        pep = seqs[int(u["prot_id"][i])][int(u["offset"][i]):int(u["offset"][i]) + int(u["length"][i])]
+        assert calculate_mass(pep, prm) == mi
+        pids = {int(x) for x in u["occ_prot"][u["occ_off"][i]:u["occ_off"][i + 1]]}
+        assert {p.getId() for p in ix.getProteins(pep)} == pids
+
+
+@pytest.mark.parametrize("fname,prm,nprot", [
+    ("golden_1k_tryp0.npz", DBIndexSearchParams.trypsin(0), 1000),
+    ("golden_1k_tryp2.npz", DBIndexSearchParams.trypsin(2), 300),
+])
+def test_engine_matches_golden(fname, prm, nprot):
+    from dbindex_amd.engine import Engine
+    g = np.load(os.path.join(GOLDEN, fname))
+    pp = fasta.config("1k") if nprot == 1000 else fasta.config("1k").slice(0, nprot)
+    assert bytes(g["residues_sha256"]).decode() == pp.sha256()
+    with Engine(prm.to_c()) as eng:
+        eng.build(pp)
+        st = eng.stats()
+        assert st.n_total == int(g["n_total"][0]) and st.n_keys == int(g["n_keys"][0])
+        ex = eng.export()
+        assert np.array_equal(ex["mass"].view(np.uint64), g["u_mass"].view(np.uint64))
+        for k, gk in [("prot_id", "u_pid"), ("offset", "u_offset"), ("length", "u_length"),
+                      ("occ_off", "u_occ_off"), ("occ_prot", "u_occ_prot")]:
+            assert np.array_equal(ex[k].astype(np.uint64), g[gk].astype(np.uint64)), k
+        assert np.array_equal(eng.entry_keys().astype(np.int64), g["entry_keys"].astype(np.int64))
+        first, count = eng.query(g["q_mass"], g["q_tol"])
+        assert np.array_equal(first.astype(np.uint64), g["q_first"].astype(np.uint64))
+        assert np.array_equal(count.astype(np.uint64), g["q_count"].astype(np.uint64))
