@@ -183,10 +183,12 @@ __device__ __forceinline__ WalkOut walk_start(const DevParams& dp, const DigestS
     uint32_t e = s;
     uint32_t cur = load(e);
     uint32_t kept = 0, dropped = 0;
+    uint32_t hsh = FNV32_OFFSET;      // peptide_tag of [s, e] (EMIT only)
     for (;;) {
         const uint32_t c = cur & 0xFFu;
         const uint32_t fl = cur >> 8;
         m = m + sm.mass[c];                                   // :306-308
+        if (EMIT) hsh = fnv32_step(hsh, c);
         mc += (int)(fl & F_CLEAVE);                           // :314-316
         const bool last = (e + 1 == pe);
         uint32_t nxt;
@@ -215,7 +217,7 @@ __device__ __forceinline__ WalkOut walk_start(const DevParams& dp, const DigestS
             rec.mass = m;
             rec.gstart = s;
             rec.len = (uint16_t)pep;
-            rec.flags = 0;
+            rec.tag = fold_tag(hsh);
             if (pep > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
             out[kept] = rec;
         }
@@ -631,27 +633,7 @@ hipError_t launch_bin_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, ui
 // with B(x) = start of the first bin starting at or after x.  Bins never
 // straddle chunks, so sorting a chunk by mass equals sorting its bins, and
 // chunk sizes stay near T whatever the mass-density skew.
-constexpr uint32_t HASH_GROUP = 16;
-
-// 64-bit FNV-1a over the peptide's residue bytes: the tie-break key between
-// different peptides of bit-identical mass (pinned order).
-// Loads are issued HASH_GROUP at a time so one latency covers a typical peptide.
-__device__ __forceinline__ unsigned long long pep_hash(const uint8_t* __restrict__ res, uint32_t g, uint32_t len) {
-    unsigned long long h = 14695981039346656037ull;
-    for (uint32_t k0 = 0; k0 < len; k0 += HASH_GROUP) {
-        uint32_t b[HASH_GROUP];
-#pragma unroll
-        for (uint32_t j = 0; j < HASH_GROUP; ++j) b[j] = (k0 + j < len) ? res[g + k0 + j] : 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < HASH_GROUP; ++j) {
-            if (k0 + j < len) {
-                h ^= b[j];
-                h *= 1099511628211ull;
-            }
-        }
-    }
-    return h;
-}
+constexpr uint32_t HASH_GROUP = 16;  // residues compared per batch of loads
 
 __device__ __forceinline__ bool seq_equal(const uint8_t* __restrict__ res, const Rec& a, const Rec& b) {
     if (a.len != b.len) return false;
@@ -714,7 +696,7 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __r
             const Rec r = in[i];
             if (STAGE) rec[i] = r;
             key[i] = dbits(r.mass);
-            hsh[i] = pep_hash(res, r.gstart, r.len);
+            hsh[i] = r.tag;
         } else {
             key[i] = ~0ull;  // padding sorts last
             hsh[i] = ~0ull;
@@ -795,7 +777,7 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __r
     for (uint32_t i = threadIdx.x; i < n; i += NT) {
         const bool head = (i == 0) || key[i] != key[i - 1] || hsh[i] != hsh[i - 1];
         Rec r = rec[k2[i]];
-        r.flags = head ? 1 : 0;
+        r.tag = head ? 1 : 0;
         out[i] = r;
         myheads += head;
     }
@@ -825,27 +807,28 @@ hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint
     return hipGetLastError();
 }
 
-// Per chunk: keys + peptide hashes into LDS, then every fine bin is rank-sorted
-// by one wave (rank = #elements of the bin ordered before, by (mass bits,
-// FNV-1a hash, insertion idx); broadcast LDS reads, no block barriers).  Equal
-// (mass, hash) neighbours are string-verified; a chunk with a true hash
-// collision, a bin above RANK_MAX or more than CAP records goes to the
-// global-memory path (k_big_chunks), which groups by first appearance.
-constexpr uint32_t RANK_MAX = 2048;
-
+// Per chunk (<= CAP records, whole fine mass bins, insertion order inside every
+// bin): every record is ranked inside its bin by (mass bits, peptide tag, local
+// index) — one lane per record, the bin's members read from LDS — which is the
+// pinned unique order.  Equal (mass, tag) neighbours must be the
+// same string (string-verified from HBM); a chunk where they are not (a 16-bit
+// tag collision between isobaric peptides) or with more than CAP records goes
+// to the global-memory path (k_big_chunks), which groups by first appearance.
+// LDS: 8+4+4+2 B per record = 36 KiB at CAP 2048 -> 4 blocks per CU.
 template <int NT, int CAP>
 __global__ void __launch_bounds__(NT)
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
              const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, uint32_t* __restrict__ big_list,
              Counters* __restrict__ ctr) {
-    __shared__ unsigned long long key[CAP];
-    __shared__ unsigned long long hsh[CAP];
-    __shared__ uint32_t binid[CAP];
-    __shared__ uint16_t perm[CAP];
-    __shared__ uint16_t run_start[CAP + 1];
-    __shared__ uint32_t s_u32[NT / 64 + 1];
-    __shared__ uint32_t s_bad;
+    static_assert(CAP <= 65535 && CAP % NT == 0, "16-bit local indices");
     constexpr uint32_t NW = NT / 64;
+    constexpr uint32_t E = CAP / NT;  // records per thread in the run-detection pass
+    __shared__ unsigned long long key[CAP];  // mass bits (positive doubles order as integers)
+    __shared__ uint32_t sec[CAP];            // tag << 16 | local index
+    __shared__ uint32_t aux[CAP];            // bin id -> run bounds lo | hi << 16
+    __shared__ uint16_t perm[CAP];           // run starts -> sorted position -> local index
+    __shared__ uint32_t s_u32[NW + 1];
+    __shared__ uint32_t s_bad;
     const uint32_t c = blockIdx.x;
     const uint32_t a = chunk_lo[c];
     const uint32_t m = chunk_lo[c + 1] - a;
@@ -861,68 +844,67 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
     for (uint32_t i = threadIdx.x; i < m; i += NT) {
         const Rec r = in[a + i];
         key[i] = dbits(r.mass);
-        binid[i] = bin_of(r.mass, bm);
-        hsh[i] = pep_hash(res, r.gstart, r.len);
+        sec[i] = ((uint32_t)r.tag << 16) | i;
+        aux[i] = bin_of(r.mass, bm);
     }
     __syncthreads();
-    // runs of equal bin id (records are grouped by bin): compact the run starts
+    // runs of equal bin id: thread t owns records [t*E, t*E+E); run index of
+    // each record kept in registers, run starts compacted into perm[]
+    const uint32_t lo0 = threadIdx.x * E;
+    uint32_t runof[E];
+    uint32_t nruns;
     {
-        constexpr uint32_t E = CAP / NT;
-        const uint32_t lo = threadIdx.x * E;
         uint32_t flags = 0, cnt = 0;
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) {
-            const uint32_t i = lo + k;
-            const bool h = i < m && (i == 0 || binid[i] != binid[i - 1]);
+            const uint32_t i = lo0 + k;
+            const bool h = i < m && (i == 0 || aux[i] != aux[i - 1]);
             flags |= (uint32_t)h << k;
             cnt += h;
         }
-        uint32_t nruns;
         uint32_t pos = block_excl_scan<NT, uint32_t>(cnt, s_u32, nruns);
 #pragma unroll
-        for (uint32_t k = 0; k < E; ++k)
-            if (flags & (1u << k)) run_start[pos++] = (uint16_t)(lo + k);
-        if (threadIdx.x == 0) {
-            run_start[nruns] = (uint16_t)m;
-            s_u32[NW] = nruns;
+        for (uint32_t k = 0; k < E; ++k) {
+            if (flags & (1u << k)) perm[pos++] = (uint16_t)(lo0 + k);
+            runof[k] = pos - 1;
         }
     }
     __syncthreads();
-    const uint32_t nruns = s_u32[NW];
-    // rank sort inside every run (= fine bin): one wave per run, broadcast LDS reads
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-    for (uint32_t r = w; r < nruns; r += NW) {
-        const uint32_t lo = run_start[r], hi = run_start[r + 1];
-        const uint32_t nb = hi - lo;
-        if (nb == 1) {
-            if (lane == 0) perm[lo] = (uint16_t)lo;
-            continue;
-        }
-        if (nb > RANK_MAX) {
-            if (lane == 0) s_bad = 1;
-            continue;
-        }
-        for (uint32_t base = lo; base < hi; base += 64) {
-            const uint32_t i = base + lane;
-            const bool act = i < hi;
-            const unsigned long long ki = act ? key[i] : 0, hi_ = act ? hsh[i] : 0;
-            uint32_t rank = 0;
-            for (uint32_t j = lo; j < hi; ++j) {
-                const unsigned long long kj = key[j], hj = hsh[j];
-                rank += (kj < ki) | ((kj == ki) & ((hj < hi_) | ((hj == hi_) & (j < i))));
-            }
-            if (act) perm[lo + rank] = (uint16_t)i;
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint32_t i = lo0 + k;
+        if (i < m) {
+            const uint32_t r = runof[k];
+            const uint32_t rlo = perm[r];
+            const uint32_t rhi = r + 1 < nruns ? perm[r + 1] : m;
+            aux[i] = rlo | (rhi << 16);
         }
     }
     __syncthreads();
-    // verify equal (mass, hash) neighbours are the same string (else: collision)
+    // rank inside the run: lanes of a wave walk their own runs (the wave
+    // iterates max run length of its 64 records); all reads hit LDS
+    for (uint32_t i = threadIdx.x; i < m; i += NT) {
+        const uint32_t b = aux[i];
+        const uint32_t rlo = b & 0xFFFFu, rhi = b >> 16;
+        const unsigned long long ki = key[i];
+        const uint32_t si = sec[i];
+        uint32_t rank = 0;
+#pragma unroll 4
+        for (uint32_t j = rlo; j < rhi; ++j) {
+            const unsigned long long kj = key[j];
+            rank += (kj < ki) | ((kj == ki) & (sec[j] < si));
+        }
+        perm[rlo + rank] = (uint16_t)i;
+    }
+    __syncthreads();
+    // unique heads; equal (mass, tag) neighbours are verified to be one string
     uint32_t myheads = 0;
     for (uint32_t p = threadIdx.x; p < m; p += NT) {
         const uint32_t i = perm[p];
         bool head = true;
         if (p > 0) {
             const uint32_t ip = perm[p - 1];
-            if (key[i] == key[ip] && hsh[i] == hsh[ip]) {
+            if (key[i] == key[ip] && (sec[i] >> 16) == (sec[ip] >> 16)) {
                 head = false;
                 if (!seq_equal(res, in[a + i], in[a + ip])) s_bad = 1;
             }
@@ -930,15 +912,50 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         myheads += head;
     }
     __syncthreads();
-    if (s_bad) {  // 64-bit hash collision or oversized run: the global-memory path redoes the chunk
-        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
+    if (s_bad) {
+        // a 16-bit tag collision between different isobaric peptides (rare,
+        // block-uniform): inside every equal-(mass, tag) group [gs, ge) the
+        // order becomes (first appearance of the string, local index).
+        // aux[p] = gs << 16 | leader, leader = local index of the string's
+        // first occurrence (positions of a group are in local-index order).
+        for (uint32_t p = threadIdx.x; p < m; p += NT) {
+            const uint32_t i = perm[p];
+            uint32_t gs = p;
+            while (gs > 0 && key[perm[gs - 1]] == key[i] && (sec[perm[gs - 1]] >> 16) == (sec[i] >> 16)) --gs;
+            uint32_t lead = i;
+            for (uint32_t q = gs; q < p; ++q) {
+                if (seq_equal(res, in[a + perm[q]], in[a + i])) {
+                    lead = perm[q];
+                    break;
+                }
+            }
+            aux[p] = (gs << 16) | lead;
+        }
+        __syncthreads();
+        uint32_t nheads = 0;
+        for (uint32_t p = threadIdx.x; p < m; p += NT) {
+            const uint32_t i = perm[p];
+            const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
+            uint32_t np = gs;
+            for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
+                const uint32_t lq = aux[q] & 0xFFFFu;
+                np += (lq < lead) | ((lq == lead) & (q < p));
+            }
+            Rec r = in[a + i];
+            r.tag = lead == i ? 1 : 0;
+            out[a + np] = r;
+            nheads += lead == i;
+        }
+        const uint32_t tot = block_sum<NT, uint32_t>(nheads, s_u32);
+        if (threadIdx.x == 0) ucount[c] = tot;
         return;
     }
     for (uint32_t p = threadIdx.x; p < m; p += NT) {
         const uint32_t i = perm[p];
-        const bool head = p == 0 || key[i] != key[perm[p - 1]] || hsh[i] != hsh[perm[p - 1]];
+        const uint32_t ip = p > 0 ? perm[p - 1] : i;
+        const bool head = p == 0 || key[i] != key[ip] || (sec[i] >> 16) != (sec[ip] >> 16);
         Rec r = in[a + i];
-        r.flags = head ? 1 : 0;
+        r.tag = head ? 1 : 0;
         out[a + p] = r;
     }
     const uint32_t tot = block_sum<NT, uint32_t>(myheads, s_u32);
@@ -1007,7 +1024,7 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
         uint32_t head = 0;
         if (i < n) {
             r = recs[a + i];
-            head = r.flags & 1u;
+            head = r.tag & 1u;
         }
         uint32_t tot;
         const uint32_t u = run + block_excl_scan<256, uint32_t>(head, tmp, tot);
@@ -1213,23 +1230,26 @@ hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, c
 // host-supplied occurrences -> records (DBIndexStore.addSequence path)
 __global__ void k_occ_to_recs(const double* __restrict__ mass, const uint32_t* __restrict__ pid,
                               const uint32_t* __restrict__ off, const uint32_t* __restrict__ len,
-                              const uint32_t* __restrict__ poff, uint64_t n, Rec* __restrict__ out) {
+                              const uint32_t* __restrict__ poff, const uint8_t* __restrict__ res, uint64_t n,
+                              Rec* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Rec r;
     r.mass = mass[i];
     r.gstart = poff[pid[i]] + off[i];
     r.len = (uint16_t)len[i];
-    r.flags = 0;
+    uint32_t h = FNV32_OFFSET;
+    for (uint32_t k = 0; k < r.len; ++k) h = fnv32_step(h, res[r.gstart + k]);
+    r.tag = fold_tag(h);
     out[i] = r;
 }
 
 hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const uint32_t* d_off,
-                              const uint32_t* d_len, const uint32_t* d_poff, uint64_t n, Rec* d_out,
-                              hipStream_t s) {
+                              const uint32_t* d_len, const uint32_t* d_poff, const uint8_t* d_res, uint64_t n,
+                              Rec* d_out, hipStream_t s) {
     if (n == 0) return hipSuccess;
     DBI_LAUNCH(k_occ_to_recs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_mass, d_pid, d_off,
-                       d_len, d_poff, n, d_out);
+                       d_len, d_poff, d_res, n, d_out);
     return hipGetLastError();
 }
 

@@ -602,7 +602,7 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
         DBI_HIP(hipMemcpyAsync(h->o_off.p, offset, 4 * n_occ, hipMemcpyHostToDevice, h->stream));
         DBI_HIP(hipMemcpyAsync(h->o_len.p, length, 4 * n_occ, hipMemcpyHostToDevice, h->stream));
     }
-    DBI_HIP(launch_occ_to_recs(h->o_mass.p, h->o_pid.p, h->o_off.p, h->o_len.p, h->poff.p, n_occ, h->recA.p,
+    DBI_HIP(launch_occ_to_recs(h->o_mass.p, h->o_pid.p, h->o_off.p, h->o_len.p, h->poff.p, h->d_res, n_occ, h->recA.p,
                                h->stream));
     // n_kept known on the host: seed the device counter
     Counters c0{};

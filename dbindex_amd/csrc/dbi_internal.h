@@ -16,14 +16,23 @@ namespace dbi {
 //   mass   : MH+ (fp64, bit-identical to the reference's sequential sum)
 //   gstart : global residue position of the first residue (protein offset + start)
 //   len    : peptide length (curSeqI, DBIndexer.java:309,388)
-//   flags  : bit0 = first occurrence of its unique peptide (set by the bin sort)
+//   tag    : digest -> chunk sort: peptide_tag() of the string (tie-break key);
+//            chunk sort -> finalize: 1 = first occurrence of its unique peptide
 struct alignas(16) Rec {
     double mass;
     uint32_t gstart;
     uint16_t len;
-    uint16_t flags;
+    uint16_t tag;
 };
 static_assert(sizeof(Rec) == 16, "Rec must be 16 bytes");
+
+// Pinned order of different peptides with bit-identical mass:
+// (16-bit tag, first appearance), tag = 32-bit FNV-1a of the residue string
+// xor-folded to 16 bits.  The digest walk extends it one residue at a time.
+constexpr uint32_t FNV32_OFFSET = 2166136261u;
+constexpr uint32_t FNV32_PRIME = 16777619u;
+__host__ __device__ inline uint32_t fnv32_step(uint32_t h, uint32_t c) { return (h ^ c) * FNV32_PRIME; }
+__host__ __device__ inline uint16_t fold_tag(uint32_t h) { return (uint16_t)((h >> 16) ^ (h & 0xFFFFu)); }
 
 constexpr int MAX_PRECURSOR_INT = 8000;  // (int) Constants.MAX_PRECURSOR_MASS
 
@@ -129,8 +138,8 @@ hipError_t launch_query(const DevParams& dp, int32_t factor, const double* d_uma
 hipError_t launch_key_range(const double* d_umass, uint32_t n_unique, int32_t factor, int32_t klo,
                             int32_t khi, uint64_t* d_out2, hipStream_t s);
 hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const uint32_t* d_off,
-                              const uint32_t* d_len, const uint32_t* d_poff, uint64_t n, Rec* d_out,
-                              hipStream_t s);
+                              const uint32_t* d_len, const uint32_t* d_poff, const uint8_t* d_res, uint64_t n,
+                              Rec* d_out, hipStream_t s);
 hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s);
 hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
                              uint64_t nq, uint64_t* d_ids, hipStream_t s);

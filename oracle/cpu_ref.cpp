@@ -176,31 +176,32 @@ std::string pep_string(const oref_index* ix, uint32_t pid, uint32_t off, uint32_
     return std::string((const char*)s, len);
 }
 
-// 64-bit FNV-1a of the peptide string: pinned tie-break between different
-// peptides of bit-identical mass (semantics A7).
-uint64_t fnv1a64(const std::string& s) {
-    uint64_t h = 14695981039346656037ull;
+// Pinned tie-break between different peptides of bit-identical mass
+// (semantics A7): the 32-bit FNV-1a of the peptide string folded
+// to 16 bits, then first appearance.
+uint16_t peptide_tag(const std::string& s) {
+    uint32_t h = 2166136261u;
     for (unsigned char c : s) {
         h ^= c;
-        h *= 1099511628211ull;
+        h *= 16777619u;
     }
-    return h;
+    return (uint16_t)((h >> 16) ^ (h & 0xFFFFu));
 }
 
 // DBIndexStoreSQLiteByteIndexMerge.getMergedData (:620-719).  The reference
 // groups through a THashMap (iteration order unspecified) and then stable-sorts
 // by mass (IndexedSeqMerged.compareTo); we pin the order of equal-mass groups to
-// (FNV-1a hash of the string, first appearance) (semantics A7).
+// (16-bit FNV-1a tag of the string, first appearance) (semantics A7).
 void merge_row(const oref_index* ix, Row& row) {
     std::unordered_map<std::string, size_t> where;
     std::vector<Merged> groups;
-    std::vector<uint64_t> ghash;
+    std::vector<uint16_t> gtag;
     where.reserve(row.recs.size() * 2);
     for (const Occ& r : row.recs) {
         std::string pep = pep_string(ix, r.pid, r.offset, r.length);
         auto it = where.find(pep);
         if (it == where.end()) {
-            ghash.push_back(fnv1a64(pep));
+            gtag.push_back(peptide_tag(pep));
             where.emplace(std::move(pep), groups.size());
             // first occurrence keeps mass/offset/length; its protein id is first
             groups.push_back(Merged{r.mass, r.offset, r.length, {r.pid}, 0});
@@ -209,12 +210,12 @@ void merge_row(const oref_index* ix, Row& row) {
         }
     }
     // Collections.sort(sortedMerged) — stable, by mass (IndexedSeqMerged.compareTo),
-    // ties pinned to (hash, first appearance)
+    // ties pinned to (tag, first appearance)
     std::vector<size_t> ord(groups.size());
     for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
     std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
         if (groups[a].mass != groups[b].mass) return groups[a].mass < groups[b].mass;
-        return ghash[a] < ghash[b];
+        return gtag[a] < gtag[b];
     });
     row.merged.clear();
     row.merged.reserve(groups.size());

@@ -14,7 +14,7 @@ sources (paths relative to /root/reference/src/main/java/edu/scripps/yates/dbind
 
 Only for small inputs (pure-Python loops).  Agreement with the C++ oracle is
 bit-exact (masses compared as float64 bit patterns).  Ties between different
-peptides of identical mass inside one row are ordered by (64-bit FNV-1a hash of
+peptides of identical mass inside one row are ordered by (16-bit FNV-1a tag of
 the string, first appearance): the reference's THashMap order is unspecified,
 so this project pins it (DESIGN.md semantics A7).
 """
@@ -125,13 +125,14 @@ def digest(params, proteins: Sequence[str]) -> list:
     return out
 
 
-def fnv1a64(s: str) -> int:
-    """64-bit FNV-1a of the peptide string (pinned tie-break)."""
-    h = 14695981039346656037
+def peptide_tag(s: str) -> int:
+    """Pinned tie-break between different peptides of bit-identical mass
+    (DESIGN.md A7): 32-bit FNV-1a of the string folded to 16 bits."""
+    h = 2166136261
     for ch in s.encode("ascii"):
         h ^= ch
-        h = (h * 1099511628211) & 0xFFFFFFFFFFFFFFFF
-    return h
+        h = (h * 16777619) & 0xFFFFFFFF
+    return (h >> 16) ^ (h & 0xFFFF)
 
 
 def get_residues(offset: int, length: int, prot: str) -> Tuple[str, str]:
@@ -177,8 +178,8 @@ class Store:
                         groups[pep] = [mass, off, ln, [pid]]
                     else:
                         groups[pep][3].append(pid)
-                # stable sort by mass; equal masses by (FNV-1a hash, first appearance)
-                merged = [groups[k] for k in sorted(groups, key=lambda k: (groups[k][0], fnv1a64(k)))]
+                # stable sort by mass; equal masses by (16-bit tag, first appearance)
+                merged = [groups[k] for k in sorted(groups, key=lambda k: (groups[k][0], peptide_tag(k)))]
                 self.buckets[b][key] = merged
         self.flat = []
         for b in range(self.nb):

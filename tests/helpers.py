@@ -47,3 +47,31 @@ def assert_queries_equal(eng, oix, masses, tols, ctx: str = "") -> None:
     bad = np.nonzero((count != oc) | ((count > 0) & (first != of)))[0]
     assert bad.shape[0] == 0, (ctx, "query mismatch", bad[:5], masses[bad[:5]], first[bad[:5]], of[bad[:5]],
                                count[bad[:5]], oc[bad[:5]])
+
+
+def tag_collision_proteins():
+    """Proteins whose tryptic peptides include isobaric permutations with
+    bit-identical fp64 MH+ AND equal 16-bit tag (pairs and a triple), repeated
+    in mixed order, so the equal-(mass, tag) groups hold different strings and
+    the pinned first-appearance order is exercised."""
+    import collections
+    import itertools
+
+    from dbindex_amd.params import DBIndexSearchParams, calculate_mass
+    from oracle.pyref import peptide_tag
+
+    prm = DBIndexSearchParams.trypsin(0)
+    groups = collections.defaultdict(list)
+    for perm in itertools.permutations("ACDEFGHM"):
+        s = "".join(perm) + "K"
+        groups[(np.float64(calculate_mass(s, prm)).view(np.uint64).item(), peptide_tag(s))].append(s)
+    pairs = [v for v in groups.values() if len(v) == 2][:40]
+    triples = [v for v in groups.values() if len(v) >= 3][:10]
+    prots = []
+    for a, b in pairs:
+        prots.append(b + a + "WWWWWWK" + b)
+        prots.append(a + a + b + "GGGGGGGR" + a)
+    for t in triples:
+        prots.append(t[2] + t[0] + t[1] + t[0])
+        prots.append(t[1] * 5 + t[2])
+    return prots

@@ -11,7 +11,7 @@ import pytest
 from dbindex_amd import fasta
 from dbindex_amd.params import DBIndexSearchParams, calculate_mass
 from oracle import cref
-from tests.helpers import assert_index_equal, assert_queries_equal, query_masses
+from tests.helpers import assert_index_equal, assert_queries_equal, query_masses, tag_collision_proteins
 
 pytestmark = pytest.mark.gpu
 
@@ -227,3 +227,14 @@ def test_query_csr_and_peptides(Engine):
         assert np.array_equal(pep["prot_id"], o["prot_id"][sel])
         assert np.array_equal(pep["occ_begin"], o["occ_off"][sel])
         assert np.array_equal(pep["occ_end"], o["occ_off"][sel + 1])
+
+
+@pytest.mark.parametrize("copies", [1, 40])
+def test_tag_collisions(Engine, copies):
+    """Equal (mass, 16-bit tag) groups holding different strings: regrouped by
+    first appearance inside the LDS chunk sort (and, with 40 copies of every
+    protein, inside big duplicate runs)."""
+    seqs = tag_collision_proteins() * copies
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    _check(Engine, DBIndexSearchParams.trypsin(0), pp, f"collisions x{copies}", nq=500)
+    _check(Engine, DBIndexSearchParams.trypsin(2), pp, f"collisions mc2 x{copies}", nq=500)

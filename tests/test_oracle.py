@@ -105,8 +105,8 @@ def test_kat_isobaric_pair_two_entries():
     ix = cref.Index(DBIndexSearchParams.trypsin(0, min_precursor_mass=300.0).to_c(), pp.residues, pp.offsets)
     u = ix.unique()
     assert ix.n_unique == 2 and u["mass"][0] == u["mass"][1]
-    # pinned tie order: FNV-1a hash of the string
-    order = sorted(seqs, key=pyref.fnv1a64)
+    # pinned tie order: 16-bit FNV-1a tag of the string, then first appearance
+    order = sorted(seqs, key=pyref.peptide_tag)
     assert [seqs[p] for p in u["prot_id"]] == order
 
 
@@ -180,6 +180,23 @@ def test_twin_restatements_agree(name, prm, n):
     assert len(st.flat) == ix.n_unique
     assert np.array_equal(np.array([g[0] for g in st.flat], np.float64).view(np.uint64), u["mass"].view(np.uint64))
     assert st.number_sequences() == ix.n_keys and st.entry_keys() == list(ix.entry_keys())
+
+
+def test_twin_tag_collisions():
+    from tests.helpers import tag_collision_proteins
+    seqs = tag_collision_proteins()
+    prm = DBIndexSearchParams.trypsin(0)
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    ix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    st = pyref.build(prm, seqs)
+    u = ix.unique()
+    assert len(st.flat) == ix.n_unique
+    got = [seqs[int(p)][int(o):int(o) + int(l)] for p, o, l in zip(u["prot_id"], u["offset"], u["length"])]
+    exp = [seqs[g[3][0]][g[1]:g[1] + g[2]] for g in st.flat]
+    assert got == exp
+    # equal (mass, tag) groups with different strings exist
+    keys = [(float(m), pyref.peptide_tag(g)) for m, g in zip(u["mass"], got)]
+    assert any(keys[i] == keys[i + 1] for i in range(len(keys) - 1))
 
 
 # ---------------------------------------------------------------- golden
