@@ -962,6 +962,170 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
     if (threadIdx.x == 0) ucount[c] = tot;
 }
 
+// One chunk of m <= CAP records sorted in LDS by (mass bits, tag, local index)
+// with a bitonic network (cost independent of how the masses cluster), then
+// unique heads flagged as in k_chunk_sort.  key/sec/aux: CAP entries each.
+// Returns this thread's head count.
+template <int NT, int CAP>
+__device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m,
+                                  const uint8_t* __restrict__ res, unsigned long long* key, uint32_t* sec,
+                                  uint32_t* aux, uint32_t* s_u32, uint32_t* s_bad) {
+    uint32_t P2 = 2;
+    while (P2 < m) P2 <<= 1;
+    if (threadIdx.x == 0) *s_bad = 0;
+    for (uint32_t i = threadIdx.x; i < P2; i += NT) {
+        if (i < m) {
+            const Rec r = in[i];
+            key[i] = dbits(r.mass);
+            sec[i] = ((uint32_t)r.tag << 16) | i;
+        } else {
+            key[i] = ~0ull;  // padding sorts last
+            sec[i] = ~0u;
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= P2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < (P2 >> 1); t += NT) {
+                const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                const uint32_t l = i | j;
+                const unsigned long long ki = key[i], kl = key[l];
+                const uint32_t si = sec[i], sl = sec[l];
+                const bool gt = (ki > kl) | ((ki == kl) & (si > sl));
+                if (gt == ((i & k) == 0)) {
+                    key[i] = kl; key[l] = ki;
+                    sec[i] = sl; sec[l] = si;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // heads; equal (mass, tag) neighbours must be one string
+    uint32_t heads = 0;
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        bool head = true;
+        if (p > 0 && key[p] == key[p - 1] && (sec[p] >> 16) == (sec[p - 1] >> 16)) {
+            head = false;
+            if (!seq_equal(res, in[sec[p] & 0xFFFFu], in[sec[p - 1] & 0xFFFFu])) *s_bad = 1;
+        }
+        aux[p] = head ? p : 0u;
+        heads += head;
+    }
+    __syncthreads();
+    if (*s_bad == 0) {
+        for (uint32_t p = threadIdx.x; p < m; p += NT) {
+            Rec r = in[sec[p] & 0xFFFFu];
+            r.tag = aux[p] == p ? 1 : 0;  // p == 0 is always a head
+            out[p] = r;
+        }
+        return heads;
+    }
+    // 16-bit tag collision (rare, block-uniform): group start gs(p) = max head
+    // position <= p (block max-scan over contiguous per-thread ranges), then
+    // the group is regrouped by first appearance of each string as in k_chunk_sort
+    {
+        const uint32_t E = (m + NT - 1) / NT;
+        const uint32_t lo = min(threadIdx.x * E, m), hi = min(lo + E, m);
+        uint32_t run = 0;
+        for (uint32_t p = lo; p < hi; ++p) run = max(run, aux[p]);
+        const uint32_t w = threadIdx.x >> 6;
+        uint32_t inc = run;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(inc, d, 64);
+            if ((int)lane_id() >= d) inc = max(inc, o);
+        }
+        if (lane_id() == 63) s_u32[w] = inc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int q = 0; q < NT / 64; ++q) {
+                const uint32_t t = s_u32[q];
+                s_u32[q] = acc;
+                acc = max(acc, t);
+            }
+        }
+        __syncthreads();
+        uint32_t excl = __shfl_up(inc, 1, 64);
+        if (lane_id() == 0) excl = 0;
+        uint32_t cur = max(excl, s_u32[w]);
+        for (uint32_t p = lo; p < hi; ++p) {
+            cur = max(cur, aux[p]);
+            aux[p] = cur;  // group start of p
+        }
+    }
+    __syncthreads();
+    // leader = local index of the first occurrence of p's string in its group;
+    // keep the group start in the high half (local indices < 65536)
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        const uint32_t gs = aux[p] & 0xFFFFu;
+        const uint32_t i = sec[p] & 0xFFFFu;
+        uint32_t lead = i;
+        for (uint32_t q = gs; q < p; ++q) {
+            if (seq_equal(res, in[sec[q] & 0xFFFFu], in[i])) {
+                lead = sec[q] & 0xFFFFu;
+                break;
+            }
+        }
+        aux[p] = (gs << 16) | lead;
+    }
+    __syncthreads();
+    heads = 0;
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        const uint32_t i = sec[p] & 0xFFFFu;
+        const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
+        uint32_t np = gs;
+        for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
+            const uint32_t lq = aux[q] & 0xFFFFu;
+            np += (lq < lead) | ((lq == lead) & (q < p));
+        }
+        Rec r = in[i];
+        r.tag = lead == i ? 1 : 0;
+        out[np] = r;
+        heads += lead == i;
+    }
+    return heads;
+}
+
+// chunks of (CHUNK_CAP, BIG_CAP] records (bins of very frequent masses at
+// SwissProt scale): 1024 threads, 128 KiB LDS, one block per CU; larger
+// chunks go on to the global-memory path.
+__global__ void __launch_bounds__(BIG_THREADS)
+k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
+                 const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount,
+                 const uint32_t* __restrict__ big_list, uint32_t* __restrict__ giant_list,
+                 Counters* __restrict__ ctr) {
+    static_assert(BIG_CAP <= 65536, "16-bit local indices");
+    __shared__ unsigned long long key[BIG_CAP];
+    __shared__ uint32_t sec[BIG_CAP];
+    __shared__ uint32_t aux[BIG_CAP];
+    __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
+    __shared__ uint32_t s_bad;
+    const uint32_t nbig = ctr->n_big;
+    for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {
+        const uint32_t c = big_list[j];
+        const uint32_t a = chunk_lo[c];
+        const uint32_t m = chunk_lo[c + 1] - a;
+        if (m > (uint32_t)BIG_CAP) {
+            if (threadIdx.x == 0) giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
+            continue;
+        }
+        const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, res, key, sec, aux, s_u32, &s_bad);
+        const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
+        if (threadIdx.x == 0) ucount[c] = tot;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
+                                 uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t* d_giant_list,
+                                 uint32_t max_blocks, Counters* d_ctr, hipStream_t s) {
+    if (max_blocks == 0) return hipSuccess;
+    DBI_LAUNCH(k_chunk_sort_big, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res,
+               d_ucount, d_big_list, d_giant_list, d_ctr);
+    return hipGetLastError();
+}
+
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, uint32_t* d_ucount, uint32_t* d_big_list,
                              Counters* d_ctr, hipStream_t s) {
@@ -979,7 +1143,7 @@ k_big_chunks(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* 
              unsigned long long* ws_key, uint32_t* ws_k2, Counters* __restrict__ ctr) {
     __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
     __shared__ unsigned long long s_flag;
-    const uint32_t nbig = ctr->n_big;
+    const uint32_t nbig = ctr->n_giant;
     for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {
         const uint32_t c = big_list[j];
         const uint32_t a = chunk_lo[c];

@@ -91,7 +91,7 @@ struct dbi_handle {
     DevBuf<uint32_t> scan_tmp;
     DevBuf<Rec> recA, recB;
     DevBuf<uint32_t> hist;
-    DevBuf<uint32_t> bin_start, ucount, big_list, chunk_lo, chunk_bin;
+    DevBuf<uint32_t> bin_start, ucount, big_list, giant_list, chunk_lo, chunk_bin;
     DevBuf<unsigned long long> ws_key;
     DevBuf<uint32_t> ws_k2;
 
@@ -250,6 +250,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
     if ((rc = h->recB.ensure(n)) || (rc = h->hist.ensure(hist_elems)) ||
         (rc = h->bin_start.ensure((size_t)nbins + 1)) || (rc = h->ucount.ensure(nchunks)) ||
         (rc = h->chunk_lo.ensure((size_t)nchunks + 1)) || (rc = h->chunk_bin.ensure((size_t)nchunks + 1)) || (rc = h->big_list.ensure(nchunks)) ||
+        (rc = h->giant_list.ensure(nchunks)) ||
         (rc = h->ws_key.ensure(4 * n)) || (rc = h->ws_k2.ensure(4 * n)) ||
         (rc = h->umass.ensure(n)) || (rc = h->upid.ensure(n)) || (rc = h->uoff.ensure(n)) ||
         (rc = h->ulen.ensure(n)) || (rc = h->occ_off.ensure(n + 1)) || (rc = h->occ_pid.ensure(n)) ||
@@ -280,8 +281,11 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
           launch_chunk_bounds(h->bin_start.p, nbins, n32, CHUNK_T, nchunks, h->chunk_lo.p, h->chunk_bin.p, s));
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->ucount.p, h->big_list.p, h->ctr.p, s));
-    STAGE(h, "big_chunks", by(0, 0, 0, 0, 0),
-          launch_big_chunks(src, dst, h->chunk_lo.p, h->d_res, h->ucount.p, h->big_list.p,
+    STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
+          launch_chunk_sort_big(src, dst, h->chunk_lo.p, h->d_res, h->ucount.p, h->big_list.p, h->giant_list.p,
+                                std::min<uint32_t>(nchunks, 256u), h->ctr.p, s));
+    STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
+          launch_big_chunks(src, dst, h->chunk_lo.p, h->d_res, h->ucount.p, h->giant_list.p,
                             std::min<uint32_t>(nchunks, 256u), h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
     // unique offsets per chunk
     STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
@@ -312,7 +316,7 @@ int finish_build(dbi_handle* h) {
     st.n_unique = h->hc.n_unique;
     st.n_keys = h->hc.n_keys;
     for (int i = 0; i < 8; ++i) st.n_keys += h->hc.n_keys_shard[i];
-    st.n_big_bins = h->hc.n_big;
+    st.n_big_bins = h->hc.n_big;  // chunks above CHUNK_CAP (of which n_giant above BIG_CAP)
     st.build_ms = ms;
     st.digest_ms = 0;
     for (int i = 0; i < h->nstage; ++i) {
@@ -328,7 +332,7 @@ int finish_build(dbi_handle* h) {
     bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
     bytes += h->thr.bytes() + h->tile_pf.bytes() + h->chunk_lo.bytes();
     bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->bin_start.bytes() + h->ucount.bytes();
-    bytes += h->big_list.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
+    bytes += h->big_list.bytes() + h->giant_list.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
     bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes() + h->key_flags.bytes();
     st.device_bytes = bytes;
     h->built = true;
@@ -529,7 +533,7 @@ void dbi_close(dbi_handle* h) {
     h->res.release(); h->poff64.release(); h->poff.release(); h->blk.release(); h->scan_tmp.release();
     h->thr.release(); h->tile_pf.release(); h->chunk_lo.release(); h->chunk_bin.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->bin_start.release(); h->ucount.release();
-    h->big_list.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
+    h->big_list.release(); h->giant_list.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
     h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release(); h->key_flags.release();
     h->o_mass.release(); h->o_pid.release(); h->o_off.release(); h->o_len.release();
     h->q_mass.release(); h->q_tol.release(); h->q_first.release(); h->q_count.release(); h->q_row.release();

@@ -62,9 +62,10 @@ struct Counters {
     unsigned long long n_unique;
     unsigned long long n_keys;
     unsigned long long n_keys_shard[8];  // per-XCD-group partial key counts (summed on readback)
-    unsigned int n_big;            // bins above the LDS capacity
+    unsigned int n_big;            // chunks above CHUNK_CAP (sorted by the 1024-thread LDS kernel)
     unsigned int err;              // device error bits
-    unsigned int pad[2];
+    unsigned int n_giant;          // chunks above BIG_CAP (global-memory path)
+    unsigned int pad;
 };
 constexpr unsigned ERR_LEN_OVERFLOW = 1;  // peptide longer than 65535 residues
 
@@ -80,6 +81,7 @@ constexpr int CHUNK_CAP = 2048;     // records per chunk sorted in LDS
 constexpr int CHUNK_T = 1024;       // target chunk size (whole mass bins, ~T..T+maxbin)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
 constexpr int BIG_THREADS = 1024;
+constexpr int BIG_CAP = 8192;       // records per oversize chunk sorted in LDS (1 block per CU)
 
 // ---- launchers (dbi_device.hip) -------------------------------------------------
 // All return hipError_t of the launch.
@@ -116,8 +118,13 @@ hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, uint32_t* d_ucount, uint32_t* d_big_list,
                              Counters* d_ctr, hipStream_t s);
+// chunks of (CHUNK_CAP, BIG_CAP] records listed in d_big_list: LDS bitonic, 1024 threads
+hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
+                                 uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t* d_giant_list,
+                                 uint32_t max_blocks, Counters* d_ctr, hipStream_t s);
+// chunks above BIG_CAP listed in d_giant_list: global-memory scratch
 hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                             uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t max_blocks,
+                             uint32_t* d_ucount, const uint32_t* d_giant_list, uint32_t max_blocks,
                              unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr, hipStream_t s);
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            const uint32_t* d_poff, uint32_t n_prot, const uint32_t* d_tile_pf, uint32_t n_res,

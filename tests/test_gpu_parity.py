@@ -91,18 +91,20 @@ def test_bucket_drop(Engine, index_factor, maxmh, nprot):
     assert oix.n_dropped > 0
 
 
-def test_big_bins_and_duplicates(Engine):
-    """3000 copies of one protein: every peptide repeats 3000x, bins exceed the
-    LDS capacity and take the large-bin path; protein-id lists keep order."""
+@pytest.mark.parametrize("copies", [3000, 9000])
+def test_big_bins_and_duplicates(Engine, copies):
+    """Thousands of copies of one protein: every peptide repeats `copies`
+    times, so chunks exceed CHUNK_CAP (3000: 1024-thread LDS bitonic path) or
+    BIG_CAP (9000: global-memory path); protein-id lists keep insertion order."""
     base = fasta.config("1k").sequence(5)
-    seqs = [base] * 3000 + [fasta.config("1k").sequence(i) for i in range(6, 40)]
+    seqs = [base] * copies + [fasta.config("1k").sequence(i) for i in range(6, 40)]
     pp = fasta.PackedProteins.from_sequences(seqs)
     cp = DBIndexSearchParams.trypsin(2).to_c()
     oix = cref.Index(cp, pp.residues, pp.offsets)
     with Engine(cp) as eng:
         st = eng.build(pp)
         assert st.n_big_bins > 0
-        assert_index_equal(eng, oix, "bigbins")
+        assert_index_equal(eng, oix, f"bigbins x{copies}")
 
 
 def test_isobaric_runs(Engine):
@@ -229,11 +231,11 @@ def test_query_csr_and_peptides(Engine):
         assert np.array_equal(pep["occ_end"], o["occ_off"][sel + 1])
 
 
-@pytest.mark.parametrize("copies", [1, 40])
+@pytest.mark.parametrize("copies", [1, 40, 300])
 def test_tag_collisions(Engine, copies):
     """Equal (mass, 16-bit tag) groups holding different strings: regrouped by
-    first appearance inside the LDS chunk sort (and, with 40 copies of every
-    protein, inside big duplicate runs)."""
+    first appearance inside the LDS chunk sort (40 copies: big duplicate runs;
+    300 copies: equal-mass bins above CHUNK_CAP, the 1024-thread path)."""
     seqs = tag_collision_proteins() * copies
     pp = fasta.PackedProteins.from_sequences(seqs)
     _check(Engine, DBIndexSearchParams.trypsin(0), pp, f"collisions x{copies}", nq=500)
