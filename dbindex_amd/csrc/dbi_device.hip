@@ -83,6 +83,19 @@ __device__ __forceinline__ T block_sum(T v, T* s_tmp) {
     return tot;
 }
 
+// Block-wide max (all threads get it).  s_tmp: >= NT/64 + 1 slots.
+template <int NT>
+__device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* s_tmp) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+    if (lane_id() == 0) s_tmp[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t r = 0;
+    for (int i = 0; i < NT / 64; ++i) r = max(r, s_tmp[i]);
+    __syncthreads();
+    return r;
+}
+
 __device__ __forceinline__ uint32_t bin_of(double m, const BinMap& bm) {
     double x = (m - bm.lo) * bm.scale;
     if (!(x > 0.0)) return 0u;
@@ -807,161 +820,6 @@ hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint
     return hipGetLastError();
 }
 
-// Per chunk (<= CAP records, whole fine mass bins, insertion order inside every
-// bin): every record is ranked inside its bin by (mass bits, peptide tag, local
-// index) — one lane per record, the bin's members read from LDS — which is the
-// pinned unique order (DESIGN.md A7).  Equal (mass, tag) neighbours must be the
-// same string (string-verified from HBM); a chunk where they are not (a 16-bit
-// tag collision between isobaric peptides) or with more than CAP records goes
-// to the global-memory path (k_big_chunks), which groups by first appearance.
-// LDS: 8+4+4+2 B per record = 36 KiB at CAP 2048 -> 4 blocks per CU.
-template <int NT, int CAP>
-__global__ void __launch_bounds__(NT)
-k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
-             const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, uint32_t* __restrict__ big_list,
-             Counters* __restrict__ ctr) {
-    static_assert(CAP <= 65535 && CAP % NT == 0, "16-bit local indices");
-    constexpr uint32_t NW = NT / 64;
-    constexpr uint32_t E = CAP / NT;  // records per thread in the run-detection pass
-    __shared__ unsigned long long key[CAP];  // mass bits (positive doubles order as integers)
-    __shared__ uint32_t sec[CAP];            // tag << 16 | local index
-    __shared__ uint32_t aux[CAP];            // bin id -> run bounds lo | hi << 16
-    __shared__ uint16_t perm[CAP];           // run starts -> sorted position -> local index
-    __shared__ uint32_t s_u32[NW + 1];
-    __shared__ uint32_t s_bad;
-    const uint32_t c = blockIdx.x;
-    const uint32_t a = chunk_lo[c];
-    const uint32_t m = chunk_lo[c + 1] - a;
-    if (m == 0) {
-        if (threadIdx.x == 0) ucount[c] = 0;
-        return;
-    }
-    if (m > (uint32_t)CAP) {
-        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
-        return;
-    }
-    if (threadIdx.x == 0) s_bad = 0;
-    for (uint32_t i = threadIdx.x; i < m; i += NT) {
-        const Rec r = in[a + i];
-        key[i] = dbits(r.mass);
-        sec[i] = ((uint32_t)r.tag << 16) | i;
-        aux[i] = bin_of(r.mass, bm);
-    }
-    __syncthreads();
-    // runs of equal bin id: thread t owns records [t*E, t*E+E); run index of
-    // each record kept in registers, run starts compacted into perm[]
-    const uint32_t lo0 = threadIdx.x * E;
-    uint32_t runof[E];
-    uint32_t nruns;
-    {
-        uint32_t flags = 0, cnt = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < E; ++k) {
-            const uint32_t i = lo0 + k;
-            const bool h = i < m && (i == 0 || aux[i] != aux[i - 1]);
-            flags |= (uint32_t)h << k;
-            cnt += h;
-        }
-        uint32_t pos = block_excl_scan<NT, uint32_t>(cnt, s_u32, nruns);
-#pragma unroll
-        for (uint32_t k = 0; k < E; ++k) {
-            if (flags & (1u << k)) perm[pos++] = (uint16_t)(lo0 + k);
-            runof[k] = pos - 1;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < E; ++k) {
-        const uint32_t i = lo0 + k;
-        if (i < m) {
-            const uint32_t r = runof[k];
-            const uint32_t rlo = perm[r];
-            const uint32_t rhi = r + 1 < nruns ? perm[r + 1] : m;
-            aux[i] = rlo | (rhi << 16);
-        }
-    }
-    __syncthreads();
-    // rank inside the run: lanes of a wave walk their own runs (the wave
-    // iterates max run length of its 64 records); all reads hit LDS
-    for (uint32_t i = threadIdx.x; i < m; i += NT) {
-        const uint32_t b = aux[i];
-        const uint32_t rlo = b & 0xFFFFu, rhi = b >> 16;
-        const unsigned long long ki = key[i];
-        const uint32_t si = sec[i];
-        uint32_t rank = 0;
-#pragma unroll 4
-        for (uint32_t j = rlo; j < rhi; ++j) {
-            const unsigned long long kj = key[j];
-            rank += (kj < ki) | ((kj == ki) & (sec[j] < si));
-        }
-        perm[rlo + rank] = (uint16_t)i;
-    }
-    __syncthreads();
-    // unique heads; equal (mass, tag) neighbours are verified to be one string
-    uint32_t myheads = 0;
-    for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        const uint32_t i = perm[p];
-        bool head = true;
-        if (p > 0) {
-            const uint32_t ip = perm[p - 1];
-            if (key[i] == key[ip] && (sec[i] >> 16) == (sec[ip] >> 16)) {
-                head = false;
-                if (!seq_equal(res, in[a + i], in[a + ip])) s_bad = 1;
-            }
-        }
-        myheads += head;
-    }
-    __syncthreads();
-    if (s_bad) {
-        // a 16-bit tag collision between different isobaric peptides (rare,
-        // block-uniform): inside every equal-(mass, tag) group [gs, ge) the
-        // order becomes (first appearance of the string, local index).
-        // aux[p] = gs << 16 | leader, leader = local index of the string's
-        // first occurrence (positions of a group are in local-index order).
-        for (uint32_t p = threadIdx.x; p < m; p += NT) {
-            const uint32_t i = perm[p];
-            uint32_t gs = p;
-            while (gs > 0 && key[perm[gs - 1]] == key[i] && (sec[perm[gs - 1]] >> 16) == (sec[i] >> 16)) --gs;
-            uint32_t lead = i;
-            for (uint32_t q = gs; q < p; ++q) {
-                if (seq_equal(res, in[a + perm[q]], in[a + i])) {
-                    lead = perm[q];
-                    break;
-                }
-            }
-            aux[p] = (gs << 16) | lead;
-        }
-        __syncthreads();
-        uint32_t nheads = 0;
-        for (uint32_t p = threadIdx.x; p < m; p += NT) {
-            const uint32_t i = perm[p];
-            const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
-            uint32_t np = gs;
-            for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
-                const uint32_t lq = aux[q] & 0xFFFFu;
-                np += (lq < lead) | ((lq == lead) & (q < p));
-            }
-            Rec r = in[a + i];
-            r.tag = lead == i ? 1 : 0;
-            out[a + np] = r;
-            nheads += lead == i;
-        }
-        const uint32_t tot = block_sum<NT, uint32_t>(nheads, s_u32);
-        if (threadIdx.x == 0) ucount[c] = tot;
-        return;
-    }
-    for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        const uint32_t i = perm[p];
-        const uint32_t ip = p > 0 ? perm[p - 1] : i;
-        const bool head = p == 0 || key[i] != key[ip] || (sec[i] >> 16) != (sec[ip] >> 16);
-        Rec r = in[a + i];
-        r.tag = head ? 1 : 0;
-        out[a + p] = r;
-    }
-    const uint32_t tot = block_sum<NT, uint32_t>(myheads, s_u32);
-    if (threadIdx.x == 0) ucount[c] = tot;
-}
-
 // One chunk of m <= CAP records sorted in LDS by (mass bits, tag, local index)
 // with a bitonic network (cost independent of how the masses cluster), then
 // unique heads flagged as in k_chunk_sort.  key/sec/aux: CAP entries each.
@@ -1085,6 +943,172 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
         heads += lead == i;
     }
     return heads;
+}
+
+// Per chunk (<= CAP records, whole fine mass bins, insertion order inside every
+// bin): every record is ranked inside its bin by (mass bits, peptide tag, local
+// index) — one lane per record, the bin's members read from LDS — which is the
+// pinned unique order (DESIGN.md A7).  Equal (mass, tag) neighbours must be the
+// same string (string-verified from HBM); a chunk where they are not (a 16-bit
+// tag collision between isobaric peptides) or with more than CAP records goes
+// to the global-memory path (k_big_chunks), which groups by first appearance.
+// LDS: 8+4+4+2 B per record = 36 KiB at CAP 2048 -> 4 blocks per CU.
+constexpr uint32_t RANK_MAX_RUN = 128;  // largest fine bin ranked per lane; above: bitonic
+
+template <int NT, int CAP>
+__global__ void __launch_bounds__(NT)
+k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
+             const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, uint32_t* __restrict__ big_list,
+             Counters* __restrict__ ctr) {
+    static_assert(CAP <= 65535 && CAP % NT == 0, "16-bit local indices");
+    constexpr uint32_t NW = NT / 64;
+    constexpr uint32_t E = CAP / NT;  // records per thread in the run-detection pass
+    __shared__ unsigned long long key[CAP];  // mass bits (positive doubles order as integers)
+    __shared__ uint32_t sec[CAP];            // tag << 16 | local index
+    __shared__ uint32_t aux[CAP];            // bin id -> run bounds lo | hi << 16
+    __shared__ uint16_t perm[CAP];           // run starts -> sorted position -> local index
+    __shared__ uint32_t s_u32[NW + 1];
+    __shared__ uint32_t s_bad;
+    const uint32_t c = blockIdx.x;
+    const uint32_t a = chunk_lo[c];
+    const uint32_t m = chunk_lo[c + 1] - a;
+    if (m == 0) {
+        if (threadIdx.x == 0) ucount[c] = 0;
+        return;
+    }
+    if (m > (uint32_t)CAP) {
+        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
+        return;
+    }
+    if (threadIdx.x == 0) s_bad = 0;
+    for (uint32_t i = threadIdx.x; i < m; i += NT) {
+        const Rec r = in[a + i];
+        key[i] = dbits(r.mass);
+        sec[i] = ((uint32_t)r.tag << 16) | i;
+        aux[i] = bin_of(r.mass, bm);
+    }
+    __syncthreads();
+    // runs of equal bin id: thread t owns records [t*E, t*E+E); run index of
+    // each record kept in registers, run starts compacted into perm[]
+    const uint32_t lo0 = threadIdx.x * E;
+    uint32_t runof[E];
+    uint32_t nruns;
+    {
+        uint32_t flags = 0, cnt = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint32_t i = lo0 + k;
+            const bool h = i < m && (i == 0 || aux[i] != aux[i - 1]);
+            flags |= (uint32_t)h << k;
+            cnt += h;
+        }
+        uint32_t pos = block_excl_scan<NT, uint32_t>(cnt, s_u32, nruns);
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            if (flags & (1u << k)) perm[pos++] = (uint16_t)(lo0 + k);
+            runof[k] = pos - 1;
+        }
+    }
+    __syncthreads();
+    uint32_t maxrun = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint32_t i = lo0 + k;
+        if (i < m) {
+            const uint32_t r = runof[k];
+            const uint32_t rlo = perm[r];
+            const uint32_t rhi = r + 1 < nruns ? perm[r + 1] : m;
+            aux[i] = rlo | (rhi << 16);
+            maxrun = max(maxrun, rhi - rlo);
+        }
+    }
+    // a bin of many records (equal-mass spikes at SwissProt scale) makes the
+    // per-bin rank quadratic: sort such a chunk with the bitonic network instead
+    if (block_max<NT>(maxrun, s_u32) > RANK_MAX_RUN) {
+        const uint32_t h = bitonic_chunk<NT, CAP>(in + a, out + a, m, res, key, sec, aux, s_u32, &s_bad);
+        const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
+        if (threadIdx.x == 0) ucount[c] = tot;
+        return;
+    }
+    // rank inside the run: lanes of a wave walk their own runs (the wave
+    // iterates max run length of its 64 records); all reads hit LDS
+    for (uint32_t i = threadIdx.x; i < m; i += NT) {
+        const uint32_t b = aux[i];
+        const uint32_t rlo = b & 0xFFFFu, rhi = b >> 16;
+        const unsigned long long ki = key[i];
+        const uint32_t si = sec[i];
+        uint32_t rank = 0;
+#pragma unroll 4
+        for (uint32_t j = rlo; j < rhi; ++j) {
+            const unsigned long long kj = key[j];
+            rank += (kj < ki) | ((kj == ki) & (sec[j] < si));
+        }
+        perm[rlo + rank] = (uint16_t)i;
+    }
+    __syncthreads();
+    // unique heads; equal (mass, tag) neighbours are verified to be one string
+    uint32_t myheads = 0;
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        const uint32_t i = perm[p];
+        bool head = true;
+        if (p > 0) {
+            const uint32_t ip = perm[p - 1];
+            if (key[i] == key[ip] && (sec[i] >> 16) == (sec[ip] >> 16)) {
+                head = false;
+                if (!seq_equal(res, in[a + i], in[a + ip])) s_bad = 1;
+            }
+        }
+        myheads += head;
+    }
+    __syncthreads();
+    if (s_bad) {
+        // a 16-bit tag collision between different isobaric peptides (rare,
+        // block-uniform): inside every equal-(mass, tag) group [gs, ge) the
+        // order becomes (first appearance of the string, local index).
+        // aux[p] = gs << 16 | leader, leader = local index of the string's
+        // first occurrence (positions of a group are in local-index order).
+        for (uint32_t p = threadIdx.x; p < m; p += NT) {
+            const uint32_t i = perm[p];
+            uint32_t gs = p;
+            while (gs > 0 && key[perm[gs - 1]] == key[i] && (sec[perm[gs - 1]] >> 16) == (sec[i] >> 16)) --gs;
+            uint32_t lead = i;
+            for (uint32_t q = gs; q < p; ++q) {
+                if (seq_equal(res, in[a + perm[q]], in[a + i])) {
+                    lead = perm[q];
+                    break;
+                }
+            }
+            aux[p] = (gs << 16) | lead;
+        }
+        __syncthreads();
+        uint32_t nheads = 0;
+        for (uint32_t p = threadIdx.x; p < m; p += NT) {
+            const uint32_t i = perm[p];
+            const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
+            uint32_t np = gs;
+            for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
+                const uint32_t lq = aux[q] & 0xFFFFu;
+                np += (lq < lead) | ((lq == lead) & (q < p));
+            }
+            Rec r = in[a + i];
+            r.tag = lead == i ? 1 : 0;
+            out[a + np] = r;
+            nheads += lead == i;
+        }
+        const uint32_t tot = block_sum<NT, uint32_t>(nheads, s_u32);
+        if (threadIdx.x == 0) ucount[c] = tot;
+        return;
+    }
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        const uint32_t i = perm[p];
+        const uint32_t ip = p > 0 ? perm[p - 1] : i;
+        const bool head = p == 0 || key[i] != key[ip] || (sec[i] >> 16) != (sec[ip] >> 16);
+        Rec r = in[a + i];
+        r.tag = head ? 1 : 0;
+        out[a + p] = r;
+    }
+    const uint32_t tot = block_sum<NT, uint32_t>(myheads, s_u32);
+    if (threadIdx.x == 0) ucount[c] = tot;
 }
 
 // chunks of (CHUNK_CAP, BIG_CAP] records (bins of very frequent masses at
