@@ -3,13 +3,14 @@
 
 Step = one full index build (digest -> mass bins -> per-bin sort + dedup ->
 unique table + occurrence CSR) over one synthetic proteome already resident in
-HBM.  Workload at N=1: BASELINE.json configs[1], "UniProt human (~20k proteins),
-trypsin, 2 missed cleavages, 1xMI355X" as a seeded synthetic proteome
-(seed 2).  N>1 (torchrun, one rank per GPU): every rank builds
-its own protein shard of the same size (seed 2+rank) -> weak scaling, no
-data-path collective.
+HBM.  Default workload at N=1: the SwissProt-scale FASTA the metric is quoted
+on (BASELINE.json configs[2] "SwissProt (~560k proteins), trypsin, 2 missed
+cleavages", which fits one MI355X) as a seeded synthetic proteome (SURVEY.md
+§8(d), seed 3).  --config human is configs[1] (20k proteins, seed 2).
+N>1 (torchrun, one rank per GPU): every rank builds its own protein shard of
+the same size (seed + 1000*rank) -> weak scaling, no data-path collective.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config human|1k|swissprot]
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config swissprot|human|1k]
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -58,7 +59,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="human", choices=sorted(WORKLOADS))
+    ap.add_argument("--config", default="swissprot", choices=sorted(WORKLOADS))
     ap.add_argument("--queries", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -161,6 +162,18 @@ def main() -> None:
         out.sort(key=lambda k: -k["ms_per_build"])
         return out
 
+    def pmc_traffic(stage):
+        """HBM bytes per launch of `stage` from the newest committed rocprofv3
+        PMC summary of this workload (profiles/<round>_<config>_summary.json,
+        tools/prof_summary.py: 2 x FETCH_SIZE + WRITE_SIZE), or (None, None)."""
+        import glob
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{args.config}_summary.json")))
+        for f in reversed(files):
+            st = json.load(open(f)).get("stages", {}).get(stage, {})
+            if "traffic_bytes" in st:
+                return st["traffic_bytes"], os.path.relpath(f, ROOT)
+        return None, None
+
     kernels = kernel_table(warm_acc, max(max(args.warmup, 1) - 1, 1))
     timed = kernel_table(stage_acc, args.steps)
     dom = timed[0] if timed else None
@@ -207,6 +220,7 @@ def main() -> None:
                           f"workload ({oix.n_total} peptides, {t1:.1f}s); host CPU: {cpu_model()}",
                    seconds=t1)
 
+    traffic, traffic_src = pmc_traffic(dom["kernel"]) if dom else (None, None)
     if rank == 0:
         out = {
             "metric": BASELINE_METRIC,
@@ -239,7 +253,8 @@ def main() -> None:
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": dom["gbps"] / HBM_PEAK_GBPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": dom["alg_bytes"],
                 "avg_launch_ms": dom["avg_ms"],
             },

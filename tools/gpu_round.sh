@@ -2,7 +2,7 @@
 # tools/gpu_round.sh TAG [what...] — one GPU-box session: parity tests, bench,
 # rocprofv3 kernel trace + stats, HBM counter passes.  Every GPU step has its
 # own time limit; the script stops at the first failure.
-#   what: tests bench prof pmc smoke (default: tests bench prof)
+#   what: tests smoke bench bench_h prof pmc pmc_sq (default: tests bench prof)
 set -u -o pipefail
 TAG=${1:-r}
 shift || true
@@ -27,7 +27,7 @@ for w in $WHAT; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3
            cp "$OUT/bench.log" "$OUT/bench.json" ;;
-    bench_sp) step bench_sp 900 python bench.py --config swissprot --steps 5 --warmup 2 ;;
+    bench_h) step bench_h 600 python bench.py --config human --steps 20 --warmup 3 ;;
     prof)  export TMPDIR=/tmp
            step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
                 -- python3 bench.py --steps 10 --warmup 2 --queries 0 --no-cpu-baseline ;;
