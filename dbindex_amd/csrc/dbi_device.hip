@@ -83,19 +83,6 @@ __device__ __forceinline__ T block_sum(T v, T* s_tmp) {
     return tot;
 }
 
-// Block-wide max (all threads get it).  s_tmp: >= NT/64 + 1 slots.
-template <int NT>
-__device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* s_tmp) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
-    if (lane_id() == 0) s_tmp[threadIdx.x >> 6] = v;
-    __syncthreads();
-    uint32_t r = 0;
-    for (int i = 0; i < NT / 64; ++i) r = max(r, s_tmp[i]);
-    __syncthreads();
-    return r;
-}
-
 __device__ __forceinline__ uint32_t bin_of(double m, const BinMap& bm) {
     double x = (m - bm.lo) * bm.scale;
     if (!(x > 0.0)) return 0u;
@@ -646,23 +633,40 @@ hipError_t launch_bin_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, ui
 // with B(x) = start of the first bin starting at or after x.  Bins never
 // straddle chunks, so sorting a chunk by mass equals sorting its bins, and
 // chunk sizes stay near T whatever the mass-density skew.
-constexpr uint32_t HASH_GROUP = 16;  // residues compared per batch of loads
-
+// Same peptide string?  (The tie-break tag is 16 bits: equal (mass, tag) is
+// not proof.)  16 residues per round: the 5 dwords covering them in each
+// string are loaded together (addresses clamped to the string's last dword,
+// so nothing past the string is read) and realigned with v_alignbyte — one
+// memory round trip per 16 residues.  A residue buffer that is not 4-B aligned
+// is read from the dword holding its first byte.
 __device__ __forceinline__ bool seq_equal(const uint8_t* __restrict__ res, const Rec& a, const Rec& b) {
     if (a.len != b.len) return false;
     if (a.gstart == b.gstart) return true;
     const uint32_t len = a.len;
-    for (uint32_t k0 = 0; k0 < len; k0 += HASH_GROUP) {
-        uint32_t x[HASH_GROUP], y[HASH_GROUP];
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(res) & 3u);
+    const uint32_t* __restrict__ w = reinterpret_cast<const uint32_t*>(res - mis);
+    const uint64_t ga = (uint64_t)a.gstart + mis, gb = (uint64_t)b.gstart + mis;
+    const uint64_t last_a = (ga + len - 1) >> 2, last_b = (gb + len - 1) >> 2;
+    for (uint32_t k0 = 0; k0 < len; k0 += 16) {
+        const uint64_t ia = (ga + k0) >> 2, ib = (gb + k0) >> 2;
+        uint32_t wa[5], wb[5];
 #pragma unroll
-        for (uint32_t j = 0; j < HASH_GROUP; ++j) {
-            x[j] = (k0 + j < len) ? res[a.gstart + k0 + j] : 0u;
-            y[j] = (k0 + j < len) ? res[b.gstart + k0 + j] : 0u;
+        for (uint32_t j = 0; j < 5; ++j) {
+            wa[j] = w[min(ia + j, last_a)];
+            wb[j] = w[min(ib + j, last_b)];
         }
-        bool eq = true;
+        const uint32_t sa = (uint32_t)((ga + k0) & 3u), sb = (uint32_t)((gb + k0) & 3u);
+        uint32_t diff = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < HASH_GROUP; ++j) eq &= (x[j] == y[j]);
-        if (!eq) return false;
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t k = k0 + 4 * j;
+            const uint32_t x = __builtin_amdgcn_alignbyte(wa[j + 1], wa[j], sa);
+            const uint32_t y = __builtin_amdgcn_alignbyte(wb[j + 1], wb[j], sb);
+            const uint32_t rem = k < len ? len - k : 0u;
+            const uint32_t mask = rem >= 4 ? ~0u : ((1u << (8 * rem)) - 1u);
+            diff |= (x ^ y) & mask;
+        }
+        if (diff) return false;
     }
     return true;
 }
@@ -820,6 +824,11 @@ hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint
     return hipGetLastError();
 }
 
+template <int NT>
+__device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m,
+                                  const uint8_t* __restrict__ res, const unsigned long long* key, const uint32_t* sec,
+                                  uint32_t* aux, uint16_t* pairs, uint32_t* s_u32, uint32_t* s_bad);
+
 // One chunk of m <= CAP records sorted in LDS by (mass bits, tag, local index)
 // with a bitonic network (cost independent of how the masses cluster), then
 // unique heads flagged as in k_chunk_sort.  key/sec/aux: CAP entries each.
@@ -827,10 +836,9 @@ hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint
 template <int NT, int CAP>
 __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m,
                                   const uint8_t* __restrict__ res, unsigned long long* key, uint32_t* sec,
-                                  uint32_t* aux, uint32_t* s_u32, uint32_t* s_bad) {
+                                  uint32_t* aux, uint16_t* pairs, uint32_t* s_u32, uint32_t* s_bad) {
     uint32_t P2 = 2;
     while (P2 < m) P2 <<= 1;
-    if (threadIdx.x == 0) *s_bad = 0;
     for (uint32_t i = threadIdx.x; i < P2; i += NT) {
         if (i < m) {
             const Rec r = in[i];
@@ -858,23 +866,62 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
             __syncthreads();
         }
     }
-    // heads; equal (mass, tag) neighbours must be one string
+    return finish_sorted<NT>(in, out, m, res, key, sec, aux, pairs, s_u32, s_bad);
+}
+
+// Chunk in sorted order in LDS (key = mass bits, sec = tag << 16 | local index):
+// flag unique heads, string-verify equal (mass, tag) neighbours, regroup a
+// 16-bit tag collision by first appearance, write the records in final order
+// (tag field = head flag).  aux: scratch.  Returns this thread's head count.
+template <int NT>
+__device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m,
+                                  const uint8_t* __restrict__ res, const unsigned long long* key, const uint32_t* sec,
+                                  uint32_t* aux, uint16_t* pairs, uint32_t* s_u32, uint32_t* s_bad) {
+    if (threadIdx.x == 0) {
+        *s_bad = 0;
+        s_u32[NT / 64] = 0;  // number of equal (mass, tag) neighbour pairs
+    }
+    __syncthreads();
     uint32_t heads = 0;
     for (uint32_t p = threadIdx.x; p < m; p += NT) {
         bool head = true;
         if (p > 0 && key[p] == key[p - 1] && (sec[p] >> 16) == (sec[p - 1] >> 16)) {
             head = false;
-            if (!seq_equal(res, in[sec[p] & 0xFFFFu], in[sec[p - 1] & 0xFFFFu])) *s_bad = 1;
+            pairs[atomicAdd(&s_u32[NT / 64], 1u)] = (uint16_t)p;
         }
         aux[p] = head ? p : 0u;
         heads += head;
     }
     __syncthreads();
+    // string-verify every pair in one parallel round (each check is a chain
+    // of HBM loads: never serialise them per thread)
+    const uint32_t npairs = s_u32[NT / 64];
+    for (uint32_t q = threadIdx.x; q < npairs; q += NT) {
+        const uint32_t p = pairs[q];
+        if (!seq_equal(res, in[sec[p] & 0xFFFFu], in[sec[p - 1] & 0xFFFFu])) *s_bad = 1;
+    }
+    __syncthreads();
     if (*s_bad == 0) {
-        for (uint32_t p = threadIdx.x; p < m; p += NT) {
-            Rec r = in[sec[p] & 0xFFFFu];
-            r.tag = aux[p] == p ? 1 : 0;  // p == 0 is always a head
-            out[p] = r;
+        // records in final order; OUT_BATCH gathers in flight per thread
+        constexpr uint32_t OUT_BATCH = 8;
+        const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
+        uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
+        for (uint32_t p0 = 0; p0 < m; p0 += OUT_BATCH * NT) {
+            uint4 rv[OUT_BATCH];
+#pragma unroll
+            for (uint32_t k = 0; k < OUT_BATCH; ++k) {
+                const uint32_t p = p0 + threadIdx.x + k * NT;
+                rv[k] = p < m ? in4[sec[p] & 0xFFFFu] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < OUT_BATCH; ++k) {
+                const uint32_t p = p0 + threadIdx.x + k * NT;
+                if (p < m) {
+                    uint4 r = rv[k];
+                    r.w = (r.w & 0xFFFFu) | ((aux[p] == p ? 1u : 0u) << 16);  // tag := head (p == 0 always)
+                    out4[p] = r;
+                }
+            }
         }
         return heads;
     }
@@ -945,15 +992,81 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
     return heads;
 }
 
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void cmp_swap(unsigned long long* key, uint32_t* sec, uint32_t x, uint32_t y) {
+    const unsigned long long kx = key[x], ky = key[y];
+    const uint32_t sx = sec[x], sy = sec[y];
+    if ((kx > ky) | ((kx == ky) & (sx > sy))) {
+        key[x] = ky; key[y] = kx;
+        sec[x] = sy; sec[y] = sx;
+    }
+}
+
+// One wave sorts key/sec[lo, lo+L) in place, ascending, with the all-ascending
+// ("flip + half-cleaner") bitonic network over the next power of two: every
+// comparator puts the smaller value at the lower index, so the virtual +inf
+// padding never moves and comparators that reach past L are simply skipped.
+__device__ void wave_bitonic(unsigned long long* key, uint32_t* sec, uint32_t lo, uint32_t L) {
+    uint32_t P2 = 2;
+    while (P2 < L) P2 <<= 1;
+    const uint32_t lane = lane_id();
+    for (uint32_t k = 2; k <= P2; k <<= 1) {
+        const uint32_t half = k >> 1;
+        for (uint32_t t = lane; t < (P2 >> 1); t += 64) {
+            const uint32_t base = (t / half) * k, off = t & (half - 1);
+            const uint32_t l = base + k - 1 - off;
+            if (l < L) cmp_swap(key, sec, lo + base + off, lo + l);
+        }
+        wave_sync();
+        for (uint32_t j = half >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = lane; t < (P2 >> 1); t += 64) {
+                const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                if (i + j < L) cmp_swap(key, sec, lo + i, lo + i + j);
+            }
+            wave_sync();
+        }
+    }
+}
+
+// The same network with the whole block (bins too big for one wave).
+template <int NT>
+__device__ void block_bitonic(unsigned long long* key, uint32_t* sec, uint32_t lo, uint32_t L) {
+    uint32_t P2 = 2;
+    while (P2 < L) P2 <<= 1;
+    for (uint32_t k = 2; k <= P2; k <<= 1) {
+        const uint32_t half = k >> 1;
+        for (uint32_t t = threadIdx.x; t < (P2 >> 1); t += NT) {
+            const uint32_t base = (t / half) * k, off = t & (half - 1);
+            const uint32_t l = base + k - 1 - off;
+            if (l < L) cmp_swap(key, sec, lo + base + off, lo + l);
+        }
+        __syncthreads();
+        for (uint32_t j = half >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < (P2 >> 1); t += NT) {
+                const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                if (i + j < L) cmp_swap(key, sec, lo + i, lo + i + j);
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // Per chunk (<= CAP records, whole fine mass bins, insertion order inside every
-// bin): every record is ranked inside its bin by (mass bits, peptide tag, local
-// index) — one lane per record, the bin's members read from LDS — which is the
-// pinned unique order.  Equal (mass, tag) neighbours must be the
-// same string (string-verified from HBM); a chunk where they are not (a 16-bit
-// tag collision between isobaric peptides) or with more than CAP records goes
-// to the global-memory path (k_big_chunks), which groups by first appearance.
-// LDS: 8+4+4+2 B per record = 36 KiB at CAP 2048 -> 4 blocks per CU.
-constexpr uint32_t RANK_MAX_RUN = 128;  // largest fine bin ranked per lane; above: bitonic
+// bin): sort every bin by (mass bits, peptide tag, local index) — the pinned
+// unique order — then finish_sorted().  Bins of <= RANK_MAX_RUN
+// records: one lane per record counts the bin members ordered before it (all
+// LDS reads, no barriers); bigger bins (equal-mass spikes at SwissProt scale):
+// one wave each sorts the bin in place with wave_bitonic.  A chunk above CAP
+// goes to k_chunk_sort_big.  LDS: 8+4+4+2 B per record = 36 KiB at CAP 2048
+// -> 4 blocks per CU.
+constexpr uint32_t RANK_MAX_RUN = 64;
+constexpr uint32_t WAVE_SORT_MAX = 256;
+constexpr uint32_t MAX_BIG_RUNS = 64;
 
 template <int NT, int CAP>
 __global__ void __launch_bounds__(NT)
@@ -961,14 +1074,16 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
              const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, uint32_t* __restrict__ big_list,
              Counters* __restrict__ ctr) {
     static_assert(CAP <= 65535 && CAP % NT == 0, "16-bit local indices");
+    static_assert(CAP / (RANK_MAX_RUN + 1) <= MAX_BIG_RUNS, "big-run list");
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t E = CAP / NT;  // records per thread in the run-detection pass
     __shared__ unsigned long long key[CAP];  // mass bits (positive doubles order as integers)
     __shared__ uint32_t sec[CAP];            // tag << 16 | local index
-    __shared__ uint32_t aux[CAP];            // bin id -> run bounds lo | hi << 16
+    __shared__ uint32_t aux[CAP];            // bin id -> run bounds lo | hi << 16 -> scratch
     __shared__ uint16_t perm[CAP];           // run starts -> sorted position -> local index
+    __shared__ uint32_t s_big[MAX_BIG_RUNS];  // runs above RANK_MAX_RUN: lo | hi << 16
     __shared__ uint32_t s_u32[NW + 1];
-    __shared__ uint32_t s_bad;
+    __shared__ uint32_t s_nbig, s_bad;
     const uint32_t c = blockIdx.x;
     const uint32_t a = chunk_lo[c];
     const uint32_t m = chunk_lo[c + 1] - a;
@@ -980,21 +1095,36 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
         return;
     }
-    if (threadIdx.x == 0) s_bad = 0;
-    for (uint32_t i = threadIdx.x; i < m; i += NT) {
-        const Rec r = in[a + i];
-        key[i] = dbits(r.mass);
-        sec[i] = ((uint32_t)r.tag << 16) | i;
-        aux[i] = bin_of(r.mass, bm);
+    if (threadIdx.x == 0) s_nbig = 0;
+    {
+        // all E loads in flight before the first use (Rec as 4 dwords:
+        // mass lo, mass hi, gstart, len | tag << 16)
+        const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in + a);
+        uint4 rv[E];
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint32_t i = threadIdx.x + k * NT;
+            rv[k] = i < m ? in4[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint32_t i = threadIdx.x + k * NT;
+            if (i < m) {
+                const double mass = __hiloint2double((int)rv[k].y, (int)rv[k].x);
+                key[i] = dbits(mass);
+                sec[i] = (rv[k].w & 0xFFFF0000u) | i;
+                aux[i] = bin_of(mass, bm);
+            }
+        }
     }
     __syncthreads();
     // runs of equal bin id: thread t owns records [t*E, t*E+E); run index of
     // each record kept in registers, run starts compacted into perm[]
     const uint32_t lo0 = threadIdx.x * E;
     uint32_t runof[E];
-    uint32_t nruns;
+    uint32_t flags = 0, nruns;
     {
-        uint32_t flags = 0, cnt = 0;
+        uint32_t cnt = 0;
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) {
             const uint32_t i = lo0 + k;
@@ -1010,7 +1140,6 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         }
     }
     __syncthreads();
-    uint32_t maxrun = 0;
 #pragma unroll
     for (uint32_t k = 0; k < E; ++k) {
         const uint32_t i = lo0 + k;
@@ -1019,22 +1148,15 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
             const uint32_t rlo = perm[r];
             const uint32_t rhi = r + 1 < nruns ? perm[r + 1] : m;
             aux[i] = rlo | (rhi << 16);
-            maxrun = max(maxrun, rhi - rlo);
+            if ((flags & (1u << k)) && rhi - rlo > RANK_MAX_RUN) s_big[atomicAdd(&s_nbig, 1u)] = rlo | (rhi << 16);
         }
     }
-    // a bin of many records (equal-mass spikes at SwissProt scale) makes the
-    // per-bin rank quadratic: sort such a chunk with the bitonic network instead
-    if (block_max<NT>(maxrun, s_u32) > RANK_MAX_RUN) {
-        const uint32_t h = bitonic_chunk<NT, CAP>(in + a, out + a, m, res, key, sec, aux, s_u32, &s_bad);
-        const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
-        if (threadIdx.x == 0) ucount[c] = tot;
-        return;
-    }
-    // rank inside the run: lanes of a wave walk their own runs (the wave
-    // iterates max run length of its 64 records); all reads hit LDS
+    __syncthreads();
+    // small bins: rank inside the bin, one lane per record
     for (uint32_t i = threadIdx.x; i < m; i += NT) {
         const uint32_t b = aux[i];
         const uint32_t rlo = b & 0xFFFFu, rhi = b >> 16;
+        if (rhi - rlo > RANK_MAX_RUN) continue;
         const unsigned long long ki = key[i];
         const uint32_t si = sec[i];
         uint32_t rank = 0;
@@ -1045,69 +1167,46 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         }
         perm[rlo + rank] = (uint16_t)i;
     }
-    __syncthreads();
-    // unique heads; equal (mass, tag) neighbours are verified to be one string
-    uint32_t myheads = 0;
-    for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        const uint32_t i = perm[p];
-        bool head = true;
-        if (p > 0) {
-            const uint32_t ip = perm[p - 1];
-            if (key[i] == key[ip] && (sec[i] >> 16) == (sec[ip] >> 16)) {
-                head = false;
-                if (!seq_equal(res, in[a + i], in[a + ip])) s_bad = 1;
-            }
-        }
-        myheads += head;
+    // big bins, sorted in place (disjoint from the small bins): up to
+    // WAVE_SORT_MAX records one wave each, above that the whole block
+    const uint32_t nbig = s_nbig;
+    for (uint32_t r = threadIdx.x >> 6; r < nbig; r += NW) {
+        const uint32_t b = s_big[r];
+        const uint32_t L = (b >> 16) - (b & 0xFFFFu);
+        if (L <= WAVE_SORT_MAX) wave_bitonic(key, sec, b & 0xFFFFu, L);
     }
     __syncthreads();
-    if (s_bad) {
-        // a 16-bit tag collision between different isobaric peptides (rare,
-        // block-uniform): inside every equal-(mass, tag) group [gs, ge) the
-        // order becomes (first appearance of the string, local index).
-        // aux[p] = gs << 16 | leader, leader = local index of the string's
-        // first occurrence (positions of a group are in local-index order).
-        for (uint32_t p = threadIdx.x; p < m; p += NT) {
-            const uint32_t i = perm[p];
-            uint32_t gs = p;
-            while (gs > 0 && key[perm[gs - 1]] == key[i] && (sec[perm[gs - 1]] >> 16) == (sec[i] >> 16)) --gs;
-            uint32_t lead = i;
-            for (uint32_t q = gs; q < p; ++q) {
-                if (seq_equal(res, in[a + perm[q]], in[a + i])) {
-                    lead = perm[q];
-                    break;
-                }
-            }
-            aux[p] = (gs << 16) | lead;
-        }
-        __syncthreads();
-        uint32_t nheads = 0;
-        for (uint32_t p = threadIdx.x; p < m; p += NT) {
-            const uint32_t i = perm[p];
-            const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
-            uint32_t np = gs;
-            for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
-                const uint32_t lq = aux[q] & 0xFFFFu;
-                np += (lq < lead) | ((lq == lead) & (q < p));
-            }
-            Rec r = in[a + i];
-            r.tag = lead == i ? 1 : 0;
-            out[a + np] = r;
-            nheads += lead == i;
-        }
-        const uint32_t tot = block_sum<NT, uint32_t>(nheads, s_u32);
-        if (threadIdx.x == 0) ucount[c] = tot;
-        return;
+    for (uint32_t r = 0; r < nbig; ++r) {
+        const uint32_t b = s_big[r];
+        const uint32_t L = (b >> 16) - (b & 0xFFFFu);
+        if (L > WAVE_SORT_MAX) block_bitonic<NT>(key, sec, b & 0xFFFFu, L);
     }
-    for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        const uint32_t i = perm[p];
-        const uint32_t ip = p > 0 ? perm[p - 1] : i;
-        const bool head = p == 0 || key[i] != key[ip] || (sec[i] >> 16) != (sec[ip] >> 16);
-        Rec r = in[a + i];
-        r.tag = head ? 1 : 0;
-        out[a + p] = r;
+    // whole chunk into sorted order: small bins gather through perm, big bins
+    // are already in place (registers first, then one barrier, then store)
+    unsigned long long kv[E];
+    uint32_t sv[E];
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint32_t p = lo0 + k;
+        if (p < m) {
+            const uint32_t b = aux[p];
+            const uint32_t src = ((b >> 16) - (b & 0xFFFFu) > RANK_MAX_RUN) ? p : perm[p];
+            kv[k] = key[src];
+            sv[k] = sec[src];
+        }
     }
-    const uint32_t tot = block_sum<NT, uint32_t>(myheads, s_u32);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint32_t p = lo0 + k;
+        if (p < m) {
+            key[p] = kv[k];
+            sec[p] = sv[k];
+        }
+    }
+    __syncthreads();
+    const uint32_t h = finish_sorted<NT>(in + a, out + a, m, res, key, sec, aux, perm, s_u32, &s_bad);
+    const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
     if (threadIdx.x == 0) ucount[c] = tot;
 }
 
@@ -1123,6 +1222,7 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
     __shared__ unsigned long long key[BIG_CAP];
     __shared__ uint32_t sec[BIG_CAP];
     __shared__ uint32_t aux[BIG_CAP];
+    __shared__ uint16_t pairs[BIG_CAP];
     __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
     __shared__ uint32_t s_bad;
     const uint32_t nbig = ctr->n_big;
@@ -1134,7 +1234,8 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
             if (threadIdx.x == 0) giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
             continue;
         }
-        const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, res, key, sec, aux, s_u32, &s_bad);
+        const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, res, key, sec, aux, pairs, s_u32,
+                                                               &s_bad);
         const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
         if (threadIdx.x == 0) ucount[c] = tot;
         __syncthreads();
@@ -1196,49 +1297,117 @@ hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chun
 // ---------------------------------------------------------------------------
 // 6. finalize: unique table + occurrence CSR (per chunk)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
+// ptile[t] = {p, poff[p], poff[p+1], 0} for the protein p holding residue
+// t << PID_TILE_SHIFT (one thread per protein writes the tiles whose first
+// residue it holds; empty proteins none)
+__global__ void k_pid_tiles(const uint32_t* __restrict__ poff, uint32_t n_prot, uint4* __restrict__ ptile) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_prot) return;
+    constexpr uint32_t M = (1u << PID_TILE_SHIFT) - 1;
+    const uint32_t lo = poff[p], hi = poff[p + 1];
+    const uint32_t t_hi = (hi + M) >> PID_TILE_SHIFT;
+    for (uint32_t t = (lo + M) >> PID_TILE_SHIFT; t < t_hi; ++t) ptile[t] = make_uint4(p, lo, hi, 0);
+}
+
+hipError_t launch_pid_tiles(const uint32_t* d_poff, uint32_t n_prot, uint4* d_ptile, hipStream_t s) {
+    if (n_prot == 0) return hipSuccess;
+    DBI_LAUNCH(k_pid_tiles, dim3((n_prot + 255) / 256), dim3(256), 0, s, d_poff, n_prot, d_ptile);
+    return hipGetLastError();
+}
+
+// Per chunk: protein id of every occurrence (occurrence CSR, insertion order
+// inside each unique peptide) and the unique table at the head records.
+// A round covers FIN_ITEMS * FIN_THREADS records, k-major (record
+// t0 + k*NT + tid), so every load/store instruction is coalesced and all loads
+// of a round (records, tile table, protein offsets) are in flight together;
+// unique slots come from per-(k, wave) ballot counts.
+constexpr uint32_t FIN_THREADS = 256;
+constexpr uint32_t FIN_ITEMS = 8;
+
+__global__ void __launch_bounds__(FIN_THREADS)
 k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
-           const uint32_t* __restrict__ poff, uint32_t n_prot, const uint32_t* __restrict__ tile_pf,
-           uint32_t ntiles, double* __restrict__ umass, uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff,
-           uint32_t* __restrict__ ulen, uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid) {
-    __shared__ uint32_t tmp[256 / 64 + 1];
+           const uint32_t* __restrict__ poff, const uint4* __restrict__ ptile, double* __restrict__ umass,
+           uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff, uint32_t* __restrict__ ulen,
+           uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid) {
+    constexpr uint32_t NW = FIN_THREADS / 64;
+    __shared__ uint32_t wc[FIN_ITEMS * NW];  // heads per (round item k, wave), then exclusive bases
+    __shared__ uint32_t s_tot;
     const uint32_t c = blockIdx.x;
     const uint32_t a = chunk_lo[c];
     const uint32_t n = chunk_lo[c + 1] - a;
+    const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(recs + a);
+    const uint32_t w = threadIdx.x >> 6;
     uint32_t run = ubase[c];
-    for (uint32_t t = 0; t < n; t += 256) {
-        const uint32_t i = t + threadIdx.x;
-        Rec r;
-        uint32_t head = 0;
-        if (i < n) {
-            r = recs[a + i];
-            head = r.tag & 1u;
+    for (uint32_t t0 = 0; t0 < n; t0 += FIN_THREADS * FIN_ITEMS) {
+        uint4 rv[FIN_ITEMS];
+        uint4 pt[FIN_ITEMS];  // {protein, its first residue, one past its last}
+        uint32_t lpre[FIN_ITEMS];
+#pragma unroll
+        for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
+            const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
+            rv[k] = i < n ? r4[i] : make_uint4(0, 0, 0, 0);  // tag field (w >> 16) = head flag
         }
-        uint32_t tot;
-        const uint32_t u = run + block_excl_scan<256, uint32_t>(head, tmp, tot);
-        if (i < n) {
-            const uint32_t p = find_pid(poff, tile_pf, n_prot, ntiles, r.gstart);
-            occ_pid[a + i] = p;
-            if (head) {
-                umass[u] = r.mass;
-                upid[u] = p;
-                uoff[u] = r.gstart - poff[p];
-                ulen[u] = r.len;
-                occ_off[u] = a + i;
+#pragma unroll
+        for (uint32_t k = 0; k < FIN_ITEMS; ++k) pt[k] = ptile[rv[k].z >> PID_TILE_SHIFT];
+        // a protein starts between the tile start and the peptide: next protein
+#pragma unroll
+        for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
+            if (rv[k].z >= pt[k].z) {
+                pt[k].x += 1;
+                pt[k].y = pt[k].z;
+                pt[k].z = poff[pt[k].x + 1];
             }
         }
-        run += tot;
+#pragma unroll
+        for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
+            const uint64_t bal = __ballot((rv[k].w >> 16) != 0);
+            lpre[k] = (uint32_t)__popcll(bal & lanemask_lt());
+            if (lane_id() == 0) wc[k * NW + w] = (uint32_t)__popcll(bal);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (uint32_t q = 0; q < FIN_ITEMS * NW; ++q) {
+                const uint32_t t = wc[q];
+                wc[q] = acc;
+                acc += t;
+            }
+            s_tot = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
+            const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
+            if (i < n) {
+                const uint32_t g = rv[k].z;
+                while (pt[k].z <= g) {  // several protein starts in one tile (short/empty proteins)
+                    pt[k].x += 1;
+                    pt[k].y = pt[k].z;
+                    pt[k].z = poff[pt[k].x + 1];
+                }
+                occ_pid[a + i] = pt[k].x;
+                if (rv[k].w >> 16) {
+                    const uint32_t u = run + wc[k * NW + w] + lpre[k];
+                    umass[u] = __hiloint2double((int)rv[k].y, (int)rv[k].x);
+                    upid[u] = pt[k].x;
+                    uoff[u] = g - pt[k].y;
+                    ulen[u] = rv[k].w & 0xFFFFu;
+                    occ_off[u] = a + i;
+                }
+            }
+        }
+        run += s_tot;
+        __syncthreads();  // wc / s_tot reused next round
     }
 }
 
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
-                           const uint32_t* d_poff, uint32_t n_prot, const uint32_t* d_tile_pf, uint32_t n_res,
-                           double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
-                           uint32_t* d_occ_off, uint32_t* d_occ_pid, hipStream_t s) {
+                           const uint32_t* d_poff, const uint4* d_ptile, double* d_umass, uint32_t* d_upid,
+                           uint32_t* d_uoff, uint32_t* d_ulen, uint32_t* d_occ_off, uint32_t* d_occ_pid,
+                           hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
-    DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(256), 0, s, d_recs, d_chunk_lo, d_ubase, d_poff, n_prot,
-                       d_tile_pf, ntiles, d_umass, d_upid, d_uoff, d_ulen, d_occ_off, d_occ_pid);
+    DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(FIN_THREADS), 0, s, d_recs, d_chunk_lo, d_ubase, d_poff, d_ptile,
+               d_umass, d_upid, d_uoff, d_ulen, d_occ_off, d_occ_pid);
     return hipGetLastError();
 }
 

@@ -88,6 +88,7 @@ struct dbi_handle {
     DevBuf<uint32_t> blk;       // digest tile counts / offsets
     DevBuf<uint32_t> thr;       // digest per-thread counts
     DevBuf<uint32_t> tile_pf;   // first protein of every digest tile (+1)
+    DevBuf<uint4> ptile;        // {protein, start, end} of every 256th residue (finalize)
     DevBuf<uint32_t> scan_tmp;
     DevBuf<Rec> recA, recB;
     DevBuf<uint32_t> hist;
@@ -292,9 +293,8 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
           launch_scan_u32(h->ucount.p, h->ucount.p, nchunks, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_unique, s));
     // finalize: 16 B record in, 4 B occurrence protein id out, 24 B per unique out
     STAGE(h, "finalize", by(0, 20, 24, 0, 0),
-          launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->poff.p, (uint32_t)h->n_prot, h->tile_pf.p,
-                          (uint32_t)h->n_res, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p, h->occ_off.p,
-                          h->occ_pid.p, s));
+          launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->poff.p, h->ptile.p, h->umass.p, h->upid.p,
+                          h->uoff.p, h->ulen.p, h->occ_off.p, h->occ_pid.p, s));
     DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s));
     STAGE(h, "count_keys", by(0, 0, 12, 0, 0),
           launch_count_keys(h->umass.p, n32, h->params.mass_group_factor, h->key_flags.p, h->ctr.p, s));
@@ -330,7 +330,7 @@ int finish_build(dbi_handle* h) {
     }
     size_t bytes = 0;
     bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
-    bytes += h->thr.bytes() + h->tile_pf.bytes() + h->chunk_lo.bytes();
+    bytes += h->thr.bytes() + h->tile_pf.bytes() + h->ptile.bytes() + h->chunk_lo.bytes();
     bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->bin_start.bytes() + h->ucount.bytes();
     bytes += h->big_list.bytes() + h->giant_list.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
     bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes() + h->key_flags.bytes();
@@ -344,8 +344,10 @@ int prepare_tiles(dbi_handle* h) {
     const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
     int rc;
     if ((rc = h->tile_pf.ensure((size_t)ntiles + 2))) return rc;
+    if ((rc = h->ptile.ensure((size_t)(h->n_res >> PID_TILE_SHIFT) + 1))) return rc;
     STAGE(h, "tile_proteins", by(0, 0, 0, 0, 0),
           launch_tile_proteins(h->poff.p, (uint32_t)h->n_prot, (uint32_t)h->n_res, h->tile_pf.p, h->stream));
+    STAGE(h, "pid_tiles", by(0.0625, 0, 0, 8, 0), launch_pid_tiles(h->poff.p, (uint32_t)h->n_prot, h->ptile.p, h->stream));
     return 0;
 }
 
@@ -531,7 +533,7 @@ void dbi_close(dbi_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
     h->res.release(); h->poff64.release(); h->poff.release(); h->blk.release(); h->scan_tmp.release();
-    h->thr.release(); h->tile_pf.release(); h->chunk_lo.release(); h->chunk_bin.release();
+    h->thr.release(); h->tile_pf.release(); h->ptile.release(); h->chunk_lo.release(); h->chunk_bin.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->bin_start.release(); h->ucount.release();
     h->big_list.release(); h->giant_list.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
     h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release(); h->key_flags.release();

@@ -80,6 +80,7 @@ constexpr int CHUNK_THREADS = 256;
 constexpr int CHUNK_CAP = 2048;     // records per chunk sorted in LDS
 constexpr int CHUNK_T = 1024;       // target chunk size (whole mass bins, ~T..T+maxbin)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
+constexpr int PID_TILE_SHIFT = 8;   // finalize's residue -> protein table: one entry per 256 residues
 constexpr int BIG_THREADS = 1024;
 constexpr int BIG_CAP = 8192;       // records per oversize chunk sorted in LDS (1 block per CU)
 
@@ -126,10 +127,13 @@ hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_
 hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
                              uint32_t* d_ucount, const uint32_t* d_giant_list, uint32_t max_blocks,
                              unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr, hipStream_t s);
+// ptile[t] = {p, poff[p], poff[p+1], 0}, p = protein holding residue t << PID_TILE_SHIFT
+// ((R >> PID_TILE_SHIFT) + 1 entries)
+hipError_t launch_pid_tiles(const uint32_t* d_poff, uint32_t n_prot, uint4* d_ptile, hipStream_t s);
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
-                           const uint32_t* d_poff, uint32_t n_prot, const uint32_t* d_tile_pf, uint32_t n_res,
-                           double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
-                           uint32_t* d_occ_off, uint32_t* d_occ_pid, hipStream_t s);
+                           const uint32_t* d_poff, const uint4* d_ptile, double* d_umass, uint32_t* d_upid,
+                           uint32_t* d_uoff, uint32_t* d_ulen, uint32_t* d_occ_off, uint32_t* d_occ_pid,
+                           hipStream_t s);
 hipError_t launch_count_keys(const double* d_umass, uint32_t n_upper, int32_t factor,
                              uint32_t* d_flags, Counters* d_ctr, hipStream_t s);
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s);
