@@ -35,6 +35,14 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// Orders this wave's LDS accesses before / after (a wave executes its LDS
+// instructions in order; this keeps the compiler from reordering them).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
 #pragma unroll
@@ -510,79 +518,100 @@ size_t radix_hist_elems(uint32_t n, int bits) {
     return (size_t)g * (size_t)(1u << bits);
 }
 
+// Digit of record r for this pass, and the wave's peers holding the same digit.
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits) {
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < bits; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    return peers;
+}
+
+// Wave w of a block owns the contiguous records [base + w*RADIX_ITEMS*64,
+// +RADIX_ITEMS*64), item k = lanes' records k*64 + lane: per-wave digit counts
+// accumulate in input order, so ranks are stable with no block barrier inside
+// the item loop.
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int bits,
              uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[RADIX_D];
+    __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
     const uint32_t D = 1u << bits, mask = D - 1;
-    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) h[d] = 0;
-    __syncthreads();
-    const uint32_t base = blockIdx.x * RADIX_CHUNK;
-#pragma unroll 4
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
+    wave_sync();
+    const uint32_t base = blockIdx.x * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
+    double mv[RADIX_ITEMS];
+#pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
-        const uint32_t i = base + k * RADIX_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&h[(bin_of(in[i].mass, bm) >> shift) & mask], 1u);
+        const uint32_t i = base + k * 64 + lane;
+        mv[k] = i < n ? in[i].mass : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < RADIX_ITEMS; ++k) {
+        const uint32_t i = base + k * 64 + lane;
+        const uint32_t d = (bin_of(mv[k], bm) >> shift) & mask;
+        const uint64_t peers = digit_peers(d, i < n, bits);
+        if (i < n && __popcll(peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
+        wave_sync();
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) hist[(size_t)d * gridDim.x + blockIdx.x] = h[d];
+    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int ww = 0; ww < RADIX_NW; ++ww) t += cnt[ww][d];
+        hist[(size_t)d * gridDim.x + blockIdx.x] = t;
+    }
 }
 
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, BinMap bm, int shift,
                 int bits, const uint32_t* __restrict__ offs) {
-    __shared__ uint32_t wcount[RADIX_NW][RADIX_D];
+    __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
     const uint32_t D = 1u << bits, mask = D - 1;
-    const uint32_t tid = threadIdx.x;
-    const int w = tid >> 6;
-    // this thread owns the running offsets of digits tid and tid + RADIX_THREADS
-    uint32_t running0 = tid < D ? offs[(size_t)tid * gridDim.x + blockIdx.x] : 0u;
-    uint32_t running1 = tid + RADIX_THREADS < D ? offs[(size_t)(tid + RADIX_THREADS) * gridDim.x + blockIdx.x] : 0u;
-    const uint32_t base = blockIdx.x * RADIX_CHUNK;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
+    wave_sync();
+    const uint32_t base = blockIdx.x * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
+    const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
+    uint4 rv[RADIX_ITEMS];
+#pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
-        const uint32_t i = base + k * RADIX_THREADS + tid;
-        const bool valid = i < n;
-        Rec r;
-        uint32_t d = 0;
-        if (valid) {
-            r = in[i];
-            d = (bin_of(r.mass, bm) >> shift) & mask;
-        }
-        // peers: lanes of this wave holding the same digit
-        uint64_t peers = __ballot(valid);
-        for (int b = 0; b < bits; ++b) {
-            const uint64_t bal = __ballot((d >> b) & 1u);
-            peers &= ((d >> b) & 1u) ? bal : ~bal;
-        }
-        for (uint32_t x = tid; x < (uint32_t)(RADIX_NW * RADIX_D); x += RADIX_THREADS)
-            (&wcount[0][0])[x] = 0;
-        __syncthreads();
-        const uint32_t rank = __popcll(peers & lanemask_lt());
-        if (valid && rank == 0) wcount[w][d] = __popcll(peers);
-        __syncthreads();
-        if (tid < D) {
-            uint32_t acc = running0;
+        const uint32_t i = base + k * 64 + lane;
+        rv[k] = i < n ? in4[i] : make_uint4(0, 0, 0, 0);
+    }
+    // rank of every record among the wave's earlier records of its digit
+    uint32_t dg[RADIX_ITEMS], pos[RADIX_ITEMS];
 #pragma unroll
-            for (int ww = 0; ww < RADIX_NW; ++ww) {
-                const uint32_t t = wcount[ww][tid];
-                wcount[ww][tid] = acc;
-                acc += t;
-            }
-            running0 = acc;
-        }
-        if (tid + RADIX_THREADS < D) {
-            const uint32_t dd = tid + RADIX_THREADS;
-            uint32_t acc = running1;
+    for (int k = 0; k < RADIX_ITEMS; ++k) {
+        const uint32_t i = base + k * 64 + lane;
+        const uint32_t d = (bin_of(__hiloint2double((int)rv[k].y, (int)rv[k].x), bm) >> shift) & mask;
+        const uint64_t peers = digit_peers(d, i < n, bits);
+        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+        const uint32_t before = cnt[w][d];
+        wave_sync();
+        if (i < n && rank == 0) cnt[w][d] = before + (uint32_t)__popcll(peers);
+        wave_sync();
+        dg[k] = d;
+        pos[k] = before + rank;
+    }
+    __syncthreads();
+    // per digit: global offset of this block, then the waves in order
+    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) {
+        uint32_t acc = offs[(size_t)d * gridDim.x + blockIdx.x];
 #pragma unroll
-            for (int ww = 0; ww < RADIX_NW; ++ww) {
-                const uint32_t t = wcount[ww][dd];
-                wcount[ww][dd] = acc;
-                acc += t;
-            }
-            running1 = acc;
+        for (int ww = 0; ww < RADIX_NW; ++ww) {
+            const uint32_t t = cnt[ww][d];
+            cnt[ww][d] = acc;
+            acc += t;
         }
-        __syncthreads();
-        if (valid) out[wcount[w][d] + rank] = r;
-        __syncthreads();
+    }
+    __syncthreads();
+    uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
+#pragma unroll
+    for (int k = 0; k < RADIX_ITEMS; ++k) {
+        const uint32_t i = base + k * 64 + lane;
+        if (i < n) out4[cnt[w][dg[k]] + pos[k]] = rv[k];
     }
 }
 
@@ -990,12 +1019,6 @@ __device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ 
         heads += lead == i;
     }
     return heads;
-}
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ void cmp_swap(unsigned long long* key, uint32_t* sec, uint32_t x, uint32_t y) {
