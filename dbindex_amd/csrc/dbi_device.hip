@@ -110,9 +110,9 @@ constexpr int PLIST_CAP = WIN + 2;
 
 struct DigestSmem {
     double mass[256];
-    uint16_t win[WIN];          // residue | residue-class flags << 8, for the staged window
+    uint16_t win[WIN];          // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST)
     uint8_t flags[256];
-    uint8_t pstart[DIGEST_TILE];
+    uint8_t pbit[WIN + 1];      // 1 = a protein starts at this window position (incl. one past the window)
     uint32_t plist[PLIST_CAP];  // protein offsets overlapping the window
     uint16_t cand[DIGEST_TILE]; // compacted candidate starts (tile-local), in order
     uint32_t tmp[DIGEST_THREADS / 64 + 1];
@@ -125,15 +125,6 @@ __device__ __forceinline__ uint32_t find_le(const uint32_t* poff, uint32_t lo, u
         if (poff[mid] <= x) lo = mid; else hi = mid;
     }
     return lo;
-}
-
-// protein containing residue g, narrowed by the per-tile table
-__device__ __forceinline__ uint32_t find_pid(const uint32_t* __restrict__ poff, const uint32_t* __restrict__ tile_pf,
-                                             uint32_t n_prot, uint32_t ntiles, uint32_t g) {
-    const uint32_t t = g / (uint32_t)DIGEST_TILE;
-    const uint32_t lo = tile_pf[t];
-    const uint32_t hi = min(tile_pf[min(t + 1, ntiles)] + 1, n_prot);
-    return find_le(poff, lo, max(hi, lo + 1), g);
 }
 
 // tile_pf[t] = protein containing residue min(t*TILE, R-1), t in [0, ntiles]
@@ -150,7 +141,7 @@ hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_
     if (n_res == 0 || n_prot == 0) return hipSuccess;
     const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     DBI_LAUNCH(k_tile_proteins, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
-                       d_tile_pf);
+               d_tile_pf);
     return hipGetLastError();
 }
 
@@ -160,93 +151,126 @@ struct WalkOut {
     bool overflow;  // the LDS window ended before the walk did: redo it from HBM
 };
 
-// One start: the cutSeq inner loop (:256-397) in branch-light form.
-//   SEMI  : checkCleavage = N_ok || C_ok (else N_ok && C_ok; full-mode
-//           candidates are N_ok by construction, so cut == C_ok)
+// One start s: the cutSeq inner loop (DBIndexer.java:256-397) in branch-light
+// form over the staged window.  Per residue step: the window entry, the mass
+// lookup, one fp64 add and three fp64 compares; the cleavage decision
+// checkCleavage(:318) and the protein end are precomputed window flags:
+//   F_CUT  = last residue of the protein, or cleave(seq[e]) && !nocut(seq[e+1])
+//   F_LAST = last residue of the protein
+//   SEMI  : checkCleavage = N_ok || C_ok (full mode: candidates are N_ok by
+//           construction, so cut == C_ok == F_CUT)
 //   MAND  : getMandatoryInternalAAs() != null (break + filterSequence path)
-//   GLOBAL: residues come from HBM instead of the LDS window (rare: walks
-//           that run past the halo, e.g. through zero-mass residues)
 // Identical decisions to the literal loop: the mass is the same sequential
-// fp64 sum, the loop exits exactly where the reference breaks, and since
-// m <= maxMH and m >= minMH hold at every emit the non-mandatory
-// filterSequence is always INCLUDE.
-template <bool EMIT, bool SEMI, bool MAND, bool GLOBAL>
-__device__ __forceinline__ WalkOut walk_start(const DevParams& dp, const DigestSmem& sm,
-                                              const uint8_t* __restrict__ g_res, uint32_t w0, uint32_t wlim,
-                                              uint32_t s, uint32_t ps, uint32_t pe, bool n_ok,
-                                              Rec* __restrict__ out, Counters* ctr) {
+// fp64 sum; once m > maxMH the reference stops (a break at a cut, the while
+// condition elsewhere); m <= maxMH and m >= minMH hold at every emit, so the
+// non-mandatory filterSequence is always INCLUDE.
+template <bool EMIT, bool SEMI, bool MAND>
+__device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSmem& sm, uint32_t w0, uint32_t wlim,
+                                            uint32_t s, bool n_ok, Rec* __restrict__ out, Counters* ctr) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;                 // precMass after H2O+H+, cTerm, nTerm (:265-271)
+    if (!(m <= dp.max_mh)) return r;  // while condition before the first residue (:284)
     int mc = -1;                      // intMisCleavageCount (:280)
     bool mand_excl = false;           // a mandatory residue in [s, e-1]
-    if (!(m <= dp.max_mh)) return r;  // while condition before the first residue (:284)
-    (void)ps;
-    auto load = [&](uint32_t g) -> uint32_t {
-        if (GLOBAL) {
-            const uint8_t c = g_res[g];
-            return (uint32_t)c | ((uint32_t)sm.flags[c] << 8);
-        }
-        return sm.win[g - w0];
-    };
-    uint32_t e = s;
-    uint32_t cur = load(e);
-    uint32_t kept = 0, dropped = 0;
+    const uint32_t e_min = s + (uint32_t)dp.min_len - 1;  // pepSize >= MIN_PEP_LENGTH (:331)
+    const bool can_drop = dp.drop_mass <= dp.max_mh;     // uniform
     uint32_t hsh = FNV32_OFFSET;      // peptide_tag of [s, e] (EMIT only)
+    uint32_t kept = 0, dropped = 0;
+    uint32_t e = s;
+    uint32_t cur = sm.win[e - w0];
+    bool ovf;
+    // single exit at the bottom: the window overflow is one more predicate
     for (;;) {
+        // next window entry first: its LDS latency overlaps this step
+        const uint32_t nxt = sm.win[min(e + 1, wlim - 1) - w0];
         const uint32_t c = cur & 0xFFu;
         const uint32_t fl = cur >> 8;
         m = m + sm.mass[c];                                   // :306-308
-        if (EMIT) hsh = fnv32_step(hsh, c);
         mc += (int)(fl & F_CLEAVE);                           // :314-316
-        const bool last = (e + 1 == pe);
-        uint32_t nxt;
-        if (GLOBAL) {
-            nxt = last ? 0u : load(e + 1);
-        } else {
-            // clamped read: past the window only matters when !last (overflow exit below)
-            nxt = sm.win[min(e + 1, wlim - 1) - w0];
-            if (!last && e + 1 >= wlim) { r.overflow = true; return r; }
-        }
-        const bool c_ok = last | (((fl & F_CLEAVE) != 0) & (((nxt >> 8) & F_NOCUT) == 0));
-        const bool cut = SEMI ? (n_ok | c_ok) : c_ok;         // checkCleavage (:318)
-        const bool brk = cut & ((mc > dp.max_missed) | (m > dp.max_mh));          // :322-329
-        const uint32_t pep = e - s + 1;
-        bool emit = cut & !brk & ((int)pep >= dp.min_len) & (m >= dp.min_mh);   // :331
+        if (EMIT) hsh = fnv32_step(hsh, c);
+        const bool last = (fl & F_LAST) != 0;
+        ovf = !last & (e + 1 >= wlim);  // F_CUT of the window's last entry is unknown: redo from HBM
+        const bool cut = SEMI ? (n_ok | ((fl & F_CUT) != 0)) : ((fl & F_CUT) != 0);  // checkCleavage (:318)
+        const bool over = m > dp.max_mh;
+        const bool brk = cut & ((mc > dp.max_missed) | over);                    // :322-329
+        bool emit = cut & !brk & !ovf & (e >= e_min) & (m >= dp.min_mh);         // :331
         bool mbrk = false;
         if (MAND) {
             mbrk = emit & !(mand_excl | ((fl & F_MAND) != 0));  // :334-344 (break, not continue)
             emit = emit & !mbrk & (!dp.mand_filter | mand_excl); // filterSequence (:247-263)
             mand_excl = mand_excl | ((fl & F_MAND) != 0);
         }
-        const bool drop = emit & (m >= dp.drop_mass);         // bucket > NUM_BUCKETS-1 (:282-288)
+        const bool drop = can_drop & emit & (m >= dp.drop_mass);  // bucket > NUM_BUCKETS-1 (:282-288)
         const bool keep = emit & !drop;
         if (EMIT && keep) {
             Rec rec;
             rec.mass = m;
             rec.gstart = s;
-            rec.len = (uint16_t)pep;
+            rec.len = (uint16_t)(e - s + 1);
             rec.tag = fold_tag(hsh);
-            if (pep > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
+            if (e - s + 1 > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
             out[kept] = rec;
         }
         kept += keep;
         dropped += drop;
-        if (brk | mbrk | last | !(m <= dp.max_mh)) break;     // breaks + while condition (:284)
+        if (brk | mbrk | last | over | ovf) break;            // breaks + while condition (:284)
         ++e;
         cur = nxt;
     }
     r.kept = kept;
     r.dropped = dropped;
+    r.overflow = ovf;
     return r;
 }
 
+// The same loop reading residues from HBM (walks that run past the staged
+// window, e.g. through zero-mass residues): flags from the residue tables,
+// the cut from the next residue and the protein end pe.
 template <bool EMIT, bool SEMI, bool MAND>
-__device__ __forceinline__ WalkOut walk(const DevParams& dp, const DigestSmem& sm, const uint8_t* __restrict__ g_res,
-                                        uint32_t w0, uint32_t wlim, uint32_t s, uint32_t ps, uint32_t pe, bool n_ok,
-                                        Rec* __restrict__ out, Counters* ctr) {
-    WalkOut w = walk_start<EMIT, SEMI, MAND, false>(dp, sm, g_res, w0, wlim, s, ps, pe, n_ok, out, ctr);
-    if (w.overflow) w = walk_start<EMIT, SEMI, MAND, true>(dp, sm, g_res, w0, wlim, s, ps, pe, n_ok, out, ctr);
-    return w;
+__device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const uint8_t* __restrict__ g_res,
+                               uint32_t s, uint32_t pe, bool n_ok, Rec* __restrict__ out, Counters* ctr) {
+    WalkOut r{0u, 0u, false};
+    double m = dp.m0;
+    if (!(m <= dp.max_mh)) return r;
+    int mc = -1;
+    bool mand_excl = false;
+    uint32_t hsh = FNV32_OFFSET;
+    uint32_t kept = 0, dropped = 0;
+    for (uint32_t e = s; e < pe; ++e) {
+        const uint32_t c = g_res[e];
+        const uint32_t fl = sm.flags[c];
+        m = m + sm.mass[c];
+        mc += (int)(fl & F_CLEAVE);
+        if (EMIT) hsh = fnv32_step(hsh, c);
+        const bool last = e + 1 == pe;
+        const bool c_ok = last || ((fl & F_CLEAVE) && !(sm.flags[g_res[e + 1]] & F_NOCUT));
+        const bool cut = SEMI ? (n_ok || c_ok) : c_ok;
+        const bool over = m > dp.max_mh;
+        const bool brk = cut && (mc > dp.max_missed || over);
+        bool emit = cut && !brk && (int)(e - s + 1) >= dp.min_len && m >= dp.min_mh;
+        bool mbrk = false;
+        if (MAND) {
+            mbrk = emit && !(mand_excl || (fl & F_MAND));
+            emit = emit && !mbrk && (!dp.mand_filter || mand_excl);
+            mand_excl = mand_excl || (fl & F_MAND);
+        }
+        const bool drop = emit && m >= dp.drop_mass;
+        if (EMIT && emit && !drop) {
+            Rec rec;
+            rec.mass = m;
+            rec.gstart = s;
+            rec.len = (uint16_t)(e - s + 1);
+            rec.tag = fold_tag(hsh);
+            if (e - s + 1 > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
+            out[kept] = rec;
+        }
+        kept += emit && !drop;
+        dropped += drop;
+        if (brk || mbrk || last || over) break;
+    }
+    r.kept = kept;
+    r.dropped = dropped;
+    return r;
 }
 
 // COUNT: per-thread kept counts -> d_thr, per-tile totals -> d_blk.
@@ -266,12 +290,13 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     const uint32_t t_end = min(t0 + (uint32_t)DIGEST_TILE, n_res);
     const uint32_t w0 = t0 >= (uint32_t)WIN_PRE ? t0 - WIN_PRE : 0u;
     const uint32_t w_end = min(w0 + (uint32_t)WIN, n_res);
+    const uint32_t nbytes = w_end - w0;
 
     // residue tables -> LDS
     sm.mass[tid] = d_mass_tab[tid];
     sm.flags[tid] = d_flags[tid];
-    for (uint32_t i = tid; i < (uint32_t)DIGEST_TILE; i += DIGEST_THREADS) sm.pstart[i] = 0;
-    // proteins overlapping [t0, w_end): [pf, pl] narrowed by the tile table
+    for (uint32_t i = tid; i <= (uint32_t)WIN; i += DIGEST_THREADS) sm.pbit[i] = 0;
+    // proteins overlapping [t0, w_end]: [pf, pl] narrowed by the tile table
     const uint32_t pf = d_tile_pf[blockIdx.x];
     const uint32_t pl = find_le(d_poff, pf, min(d_tile_pf[min(blockIdx.x + 2, ntiles)] + 1, n_prot), w_end - 1);
     const uint32_t np_all = pl - pf + 2;
@@ -279,7 +304,6 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     __syncthreads();
     // residue window -> LDS as (residue | flags << 8), 16 residues per load when aligned
     {
-        const uint32_t nbytes = w_end - w0;
         const uintptr_t base = (uintptr_t)(d_res + w0);
         if ((base & 15u) == 0) {
             const uint32_t nvec = nbytes >> 4;
@@ -306,15 +330,39 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
         const uint32_t o = d_poff[pf + i];
         if (np) sm.plist[i] = o;
-        if (o >= t0 && o < t_end) sm.pstart[o - t0] = 1;  // protein N-terminus in the tile
+        if (o >= w0 && o <= w_end) sm.pbit[o - w0] = 1;  // protein starts (and the end of the last one)
+    }
+    __syncthreads();
+    // cleavage-cut and protein-end flags of every window position.  At the
+    // window's last position (w_end < R) the next residue is unknown; a walk
+    // that reaches it without a protein end overflows to walk_global first.
+    {
+        uint32_t cf[(WIN + DIGEST_THREADS - 1) / DIGEST_THREADS];
+#pragma unroll
+        for (uint32_t k = 0; k < (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS; ++k) {
+            const uint32_t i = tid + k * DIGEST_THREADS;
+            cf[k] = 0;
+            if (i < nbytes) {
+                const uint32_t fl = sm.win[i] >> 8;
+                const uint32_t last = sm.pbit[i + 1];
+                const bool nocut_next = i + 1 < nbytes && ((sm.win[i + 1] >> 8) & F_NOCUT);
+                const bool cut = last || ((fl & F_CLEAVE) && !nocut_next);
+                cf[k] = (cut ? F_CUT : 0u) | (last ? F_LAST : 0u);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS; ++k) {
+            const uint32_t i = tid + k * DIGEST_THREADS;
+            if (i < nbytes) sm.win[i] |= (uint16_t)(cf[k] << 8);
+        }
     }
     __syncthreads();
 
-    // N_ok(s): protein N-term, or a site after a cleave residue not before a nocut one
+    // N_ok(s): protein N-terminus, or the previous position is a cut
     auto n_ok_at = [&](uint32_t i) -> bool {
-        const uint32_t s = t0 + i;
-        return sm.pstart[i] ||
-               (((sm.win[s - 1 - w0] >> 8) & F_CLEAVE) && !((sm.win[s - w0] >> 8) & F_NOCUT));
+        const uint32_t p = t0 + i - w0;
+        return sm.pbit[p] || (p > 0 && ((sm.win[p - 1] >> 8) & F_CUT));
     };
     // cleavage-site compaction: thread t owns starts [t*SPT, t*SPT+SPT) in order
     uint32_t mybits = 0, mycnt = 0;
@@ -336,28 +384,28 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     const uint32_t jb = tid * q + min(tid, rr);
     const uint32_t je = jb + q + (tid < rr ? 1u : 0u);
 
-    auto site = [&](uint32_t j, uint32_t& s, uint32_t& ps, uint32_t& pe, bool& n_ok) {
+    // one candidate: LDS walk, or the HBM walk when it outruns the window
+    auto walk = [&](uint32_t j, Rec* o) -> WalkOut {
         const uint32_t i = sm.cand[j];
-        s = t0 + i;
-        if (np) {
-            const uint32_t k = find_le(sm.plist, 0, np - 1, s);
-            ps = sm.plist[k];
-            pe = sm.plist[k + 1];
-        } else {
-            const uint32_t p = find_le(d_poff, pf, pl + 1, s);
-            ps = d_poff[p];
-            pe = d_poff[p + 1];
+        const uint32_t s = t0 + i;
+        const bool n_ok = SEMI ? n_ok_at(i) : true;
+        WalkOut w = walk_lds<EMIT, SEMI, MAND>(dp, sm, w0, w_end, s, n_ok, o, d_ctr);
+        if (w.overflow) {
+            uint32_t pe;
+            if (np) {
+                pe = sm.plist[find_le(sm.plist, 0, np - 1, s) + 1];
+            } else {
+                pe = d_poff[find_le(d_poff, pf, pl + 1, s) + 1];
+            }
+            w = walk_global<EMIT, SEMI, MAND>(dp, sm, d_res, s, pe, n_ok, o, d_ctr);
         }
-        n_ok = SEMI ? n_ok_at(i) : true;
+        return w;
     };
 
     if (!EMIT) {
         uint32_t kept = 0, dropped = 0;
         for (uint32_t j = jb; j < je; ++j) {
-            uint32_t s, ps, pe;
-            bool n_ok;
-            site(j, s, ps, pe, n_ok);
-            const WalkOut w = walk<false, SEMI, MAND>(dp, sm, d_res, w0, w_end, s, ps, pe, n_ok, nullptr, d_ctr);
+            const WalkOut w = walk(j, nullptr);
             kept += w.kept;
             dropped += w.dropped;
         }
@@ -374,12 +422,7 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     uint32_t tot;
     const uint32_t my = d_thr[blockIdx.x * DIGEST_THREADS + tid];
     Rec* out = d_out + d_blk[blockIdx.x] + block_excl_scan<DIGEST_THREADS, uint32_t>(my, sm.tmp, tot);
-    for (uint32_t j = jb; j < je; ++j) {
-        uint32_t s, ps, pe;
-        bool n_ok;
-        site(j, s, ps, pe, n_ok);
-        out += walk<true, SEMI, MAND>(dp, sm, d_res, w0, w_end, s, ps, pe, n_ok, out, d_ctr).kept;
-    }
+    for (uint32_t j = jb; j < je; ++j) out += walk(j, out).kept;
 }
 
 template <bool EMIT>

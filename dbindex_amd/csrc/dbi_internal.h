@@ -40,6 +40,8 @@ constexpr int MAX_PRECURSOR_INT = 8000;  // (int) Constants.MAX_PRECURSOR_MASS
 constexpr uint8_t F_CLEAVE = 1;
 constexpr uint8_t F_NOCUT = 2;
 constexpr uint8_t F_MAND = 4;
+constexpr uint8_t F_CUT = 8;    // window only: checkCleavage C-side ok at this residue (or protein end)
+constexpr uint8_t F_LAST = 16;  // window only: last residue of its protein
 
 // Device-side copy of the parameters the kernels need (kernel argument).
 struct DevParams {
