@@ -677,27 +677,6 @@ hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const B
 
 uint64_t radix_blocks(uint32_t n) { return (n + RADIX_CHUNK - 1) / RADIX_CHUNK; }
 
-// bin_start[b] = first record of bin b (records sorted by bin), bin_start[nbins] = n
-__global__ void k_bin_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap bm,
-                             uint32_t* __restrict__ bin_start) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t b = bin_of(recs[i].mass, bm);
-    const int64_t bp = i ? (int64_t)bin_of(recs[i - 1].mass, bm) : -1;
-    for (int64_t j = bp + 1; j <= (int64_t)b; ++j) bin_start[j] = i;
-    if (i == n - 1)
-        for (uint32_t j = b + 1; j <= bm.nbins; ++j) bin_start[j] = n;
-}
-
-hipError_t launch_bin_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t* d_bin_start,
-                             hipStream_t s) {
-    if (n == 0) {
-        return hipMemsetAsync(d_bin_start, 0, sizeof(uint32_t) * ((size_t)bm.nbins + 1), s);
-    }
-    DBI_LAUNCH(k_bin_bounds, dim3((n + 255) / 256), dim3(256), 0, s, d_recs, n, bm, d_bin_start);
-    return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------
 // 5. chunk sort + group by peptide string (IndexMerge.getMergedData :620-719)
 // ---------------------------------------------------------------------------
@@ -873,26 +852,38 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __r
     return myheads;
 }
 
-// chunk c = records [chunk_lo[c], chunk_lo[c+1]) = bins [chunk_bin[c], chunk_bin[c+1]);
-// chunk_lo[c] = start of the first bin starting at or after c*T (one thread per chunk)
-__global__ void k_chunk_bounds(const uint32_t* __restrict__ bin_start, uint32_t nbins, uint32_t n, uint32_t T,
-                               uint32_t nchunks, uint32_t* __restrict__ chunk_lo, uint32_t* __restrict__ chunk_bin) {
+// chunk c = records [chunk_lo[c], chunk_lo[c+1]): chunk_lo[c] = the first bin
+// start at or after c*T, found on the bin-sorted records themselves (one
+// thread per chunk: galloping, then binary search for the end of the bin that
+// straddles c*T — a few loads for ordinary bins, log steps for mass spikes).
+__global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap bm, uint32_t T, uint32_t nchunks,
+                               uint32_t* __restrict__ chunk_lo) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c > nchunks) return;
     const uint32_t x = c == nchunks ? n : min(c * T, n);
-    uint32_t lo = 0, hi = nbins;  // lower_bound over bin_start[0..nbins] (bin_start[nbins] == n)
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (bin_start[mid] < x) lo = mid + 1; else hi = mid;
+    if (x == 0 || x == n) {
+        chunk_lo[c] = x;
+        return;
     }
-    chunk_bin[c] = lo;
-    chunk_lo[c] = bin_start[lo];
+    const uint32_t b = bin_of(recs[x - 1].mass, bm);
+    // first i >= x with bin(i) > b (bins are non-decreasing); lo: known <= b
+    uint32_t lo = x - 1, step = 1, hi = x;
+    while (hi < n && bin_of(recs[hi].mass, bm) <= b) {
+        lo = hi;
+        step <<= 1;
+        hi = min(x - 1 + step, n);
+    }
+    while (hi - lo > 1) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (bin_of(recs[mid].mass, bm) <= b) lo = mid; else hi = mid;
+    }
+    chunk_lo[c] = hi;
 }
 
-hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint32_t n, uint32_t T, uint32_t nchunks,
-                               uint32_t* d_chunk_lo, uint32_t* d_chunk_bin, hipStream_t s) {
-    DBI_LAUNCH(k_chunk_bounds, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_bin_start, nbins, n, T,
-                       nchunks, d_chunk_lo, d_chunk_bin);
+hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,
+                               uint32_t* d_chunk_lo, hipStream_t s) {
+    DBI_LAUNCH(k_chunk_bounds, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_recs, n, bm, T, nchunks,
+               d_chunk_lo);
     return hipGetLastError();
 }
 
@@ -1388,13 +1379,14 @@ hipError_t launch_pid_tiles(const uint32_t* d_poff, uint32_t n_prot, uint4* d_pt
 // of a round (records, tile table, protein offsets) are in flight together;
 // unique slots come from per-(k, wave) ballot counts.
 constexpr uint32_t FIN_THREADS = 256;
-constexpr uint32_t FIN_ITEMS = 8;
+constexpr uint32_t FIN_ITEMS = 4;  // one round = 1024 records ~ one chunk
 
 __global__ void __launch_bounds__(FIN_THREADS)
 k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
            const uint32_t* __restrict__ poff, const uint4* __restrict__ ptile, double* __restrict__ umass,
            uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff, uint32_t* __restrict__ ulen,
-           uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid) {
+           uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid, int32_t factor,
+           Counters* __restrict__ ctr) {
     constexpr uint32_t NW = FIN_THREADS / 64;
     __shared__ uint32_t wc[FIN_ITEMS * NW];  // heads per (round item k, wave), then exclusive bases
     __shared__ uint32_t s_tot;
@@ -1404,6 +1396,7 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
     const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(recs + a);
     const uint32_t w = threadIdx.x >> 6;
     uint32_t run = ubase[c];
+    uint32_t nkeys = 0;  // heads whose mass key differs from the previous unique's (SQLiteByte rows)
     for (uint32_t t0 = 0; t0 < n; t0 += FIN_THREADS * FIN_ITEMS) {
         uint4 rv[FIN_ITEMS];
         uint4 pt[FIN_ITEMS];  // {protein, its first residue, one past its last}
@@ -1412,6 +1405,13 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
             const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
             rv[k] = i < n ? r4[i] : make_uint4(0, 0, 0, 0);  // tag field (w >> 16) = head flag
+        }
+        // mass of the record before each one (= the previous unique's mass at a head)
+        double prevm[FIN_ITEMS];
+#pragma unroll
+        for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
+            const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
+            prevm[k] = (i < n && a + i > 0 && (rv[k].w >> 16)) ? recs[a + i - 1].mass : 0.0;
         }
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) pt[k] = ptile[rv[k].z >> PID_TILE_SHIFT];
@@ -1454,7 +1454,9 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
                 occ_pid[a + i] = pt[k].x;
                 if (rv[k].w >> 16) {
                     const uint32_t u = run + wc[k * NW + w] + lpre[k];
-                    umass[u] = __hiloint2double((int)rv[k].y, (int)rv[k].x);
+                    const double mu = __hiloint2double((int)rv[k].y, (int)rv[k].x);
+                    nkeys += (a + i == 0) || java_d2i(mu * (double)factor) != java_d2i(prevm[k] * (double)factor);
+                    umass[u] = mu;
                     upid[u] = pt[k].x;
                     uoff[u] = g - pt[k].y;
                     ulen[u] = rv[k].w & 0xFFFFu;
@@ -1465,42 +1467,35 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
         run += s_tot;
         __syncthreads();  // wc / s_tot reused next round
     }
+    const uint32_t t = block_sum<FIN_THREADS, uint32_t>(nkeys, wc);
+    // one add per block into one of 8 shards (no single-word contention)
+    if (threadIdx.x == 0 && t) atomicAdd(&ctr->n_keys_shard[blockIdx.x & 7], (unsigned long long)t);
 }
 
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            const uint32_t* d_poff, const uint4* d_ptile, double* d_umass, uint32_t* d_upid,
                            uint32_t* d_uoff, uint32_t* d_ulen, uint32_t* d_occ_off, uint32_t* d_occ_pid,
-                           hipStream_t s) {
+                           int32_t factor, Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(FIN_THREADS), 0, s, d_recs, d_chunk_lo, d_ubase, d_poff, d_ptile,
-               d_umass, d_upid, d_uoff, d_ulen, d_occ_off, d_occ_pid);
+               d_umass, d_upid, d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, d_ctr);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// distinct mass keys (int)(mass*factor) over the mass-sorted unique table;
-// U is read from the device counters (no host round trip), grid sized by n_upper.
-__global__ void k_count_keys(const double* __restrict__ umass, int32_t factor, uint32_t* __restrict__ flags,
-                             Counters* __restrict__ ctr) {
-    __shared__ uint32_t tmp[256 / 64 + 1];
-    const uint32_t n = (uint32_t)ctr->n_unique;
-    uint32_t f = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        const int32_t k = java_d2i(umass[i] * (double)factor);
-        const uint32_t fi = (i == 0) || (java_d2i(umass[i - 1] * (double)factor) != k);
-        if (flags) flags[i] = fi;
-        f += fi;
-    }
-    const uint32_t t = block_sum<256, uint32_t>(f, tmp);
-    // one add per block into one of 8 shards (no single-word contention)
-    if (threadIdx.x == 0 && t) atomicAdd(&ctr->n_keys_shard[blockIdx.x & 7], (unsigned long long)t);
+// flags[i] = 1 where the mass key (int)(mass*factor) of unique i differs from
+// unique i-1's (dbi_entry_keys; the count itself comes from k_finalize)
+__global__ void k_key_flags(const double* __restrict__ umass, uint32_t n, int32_t factor,
+                            uint32_t* __restrict__ flags) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    flags[i] = (i == 0) || (java_d2i(umass[i - 1] * (double)factor) != java_d2i(umass[i] * (double)factor));
 }
 
-hipError_t launch_count_keys(const double* d_umass, uint32_t n_upper, int32_t factor, uint32_t* d_flags,
-                             Counters* d_ctr, hipStream_t s) {
-    if (n_upper == 0) return hipSuccess;
-    const uint32_t g = min((n_upper + 255) / 256, 1024u);
-    DBI_LAUNCH(k_count_keys, dim3(g), dim3(256), 0, s, d_umass, factor, d_flags, d_ctr);
+hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t factor, uint32_t* d_flags,
+                            hipStream_t s) {
+    if (n_unique == 0) return hipSuccess;
+    DBI_LAUNCH(k_key_flags, dim3((n_unique + 255) / 256), dim3(256), 0, s, d_umass, n_unique, factor, d_flags);
     return hipGetLastError();
 }
 

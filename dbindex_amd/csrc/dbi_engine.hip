@@ -92,13 +92,13 @@ struct dbi_handle {
     DevBuf<uint32_t> scan_tmp;
     DevBuf<Rec> recA, recB;
     DevBuf<uint32_t> hist;
-    DevBuf<uint32_t> bin_start, ucount, big_list, giant_list, chunk_lo, chunk_bin;
+    DevBuf<uint32_t> ucount, big_list, giant_list, chunk_lo;
     DevBuf<unsigned long long> ws_key;
     DevBuf<uint32_t> ws_k2;
 
     // index
     DevBuf<double> umass;
-    DevBuf<uint32_t> upid, uoff, ulen, occ_off, occ_pid, key_flags;
+    DevBuf<uint32_t> upid, uoff, ulen, occ_off, occ_pid;
     bool built = false;
 
     // host-input occurrences (addSequence path)
@@ -249,13 +249,12 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
     const size_t scan_need = std::max(scan_u32_tmp_elems(hist_elems), scan_u32_tmp_elems(nchunks));
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_need, h->scan_tmp.cap)))) return rc;
     if ((rc = h->recB.ensure(n)) || (rc = h->hist.ensure(hist_elems)) ||
-        (rc = h->bin_start.ensure((size_t)nbins + 1)) || (rc = h->ucount.ensure(nchunks)) ||
-        (rc = h->chunk_lo.ensure((size_t)nchunks + 1)) || (rc = h->chunk_bin.ensure((size_t)nchunks + 1)) || (rc = h->big_list.ensure(nchunks)) ||
+        (rc = h->ucount.ensure(nchunks)) || (rc = h->chunk_lo.ensure((size_t)nchunks + 1)) ||
+        (rc = h->big_list.ensure(nchunks)) ||
         (rc = h->giant_list.ensure(nchunks)) ||
         (rc = h->ws_key.ensure(4 * n)) || (rc = h->ws_k2.ensure(4 * n)) ||
         (rc = h->umass.ensure(n)) || (rc = h->upid.ensure(n)) || (rc = h->uoff.ensure(n)) ||
-        (rc = h->ulen.ensure(n)) || (rc = h->occ_off.ensure(n + 1)) || (rc = h->occ_pid.ensure(n)) ||
-        (rc = h->key_flags.ensure(n)))
+        (rc = h->ulen.ensure(n)) || (rc = h->occ_off.ensure(n + 1)) || (rc = h->occ_pid.ensure(n)))
         return rc;
 
     // stable LSD passes over the bin id
@@ -276,10 +275,9 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
         shift += bits;
     }
     // src: records grouped by bin, insertion order inside each bin
-    STAGE(h, "bin_bounds", by(0, 8, 0, 0, 4), launch_bin_bounds(src, n32, bm, h->bin_start.p, s));
     // chunk sort: 16 B in + 16 B out per record (+ the residues of every peptide for its hash)
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
-          launch_chunk_bounds(h->bin_start.p, nbins, n32, CHUNK_T, nchunks, h->chunk_lo.p, h->chunk_bin.p, s));
+          launch_chunk_bounds(src, n32, bm, CHUNK_T, nchunks, h->chunk_lo.p, s));
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->ucount.p, h->big_list.p, h->ctr.p, s));
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
@@ -294,10 +292,8 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
     // finalize: 16 B record in, 4 B occurrence protein id out, 24 B per unique out
     STAGE(h, "finalize", by(0, 20, 24, 0, 0),
           launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->poff.p, h->ptile.p, h->umass.p, h->upid.p,
-                          h->uoff.p, h->ulen.p, h->occ_off.p, h->occ_pid.p, s));
+                          h->uoff.p, h->ulen.p, h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor, h->ctr.p, s));
     DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s));
-    STAGE(h, "count_keys", by(0, 0, 12, 0, 0),
-          launch_count_keys(h->umass.p, n32, h->params.mass_group_factor, h->key_flags.p, h->ctr.p, s));
     h->stats.n_bins = nbins;
     return 0;
 }
@@ -331,9 +327,9 @@ int finish_build(dbi_handle* h) {
     size_t bytes = 0;
     bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
     bytes += h->thr.bytes() + h->tile_pf.bytes() + h->ptile.bytes() + h->chunk_lo.bytes();
-    bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->bin_start.bytes() + h->ucount.bytes();
+    bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->ucount.bytes();
     bytes += h->big_list.bytes() + h->giant_list.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
-    bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes() + h->key_flags.bytes();
+    bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes();
     st.device_bytes = bytes;
     h->built = true;
     return 0;
@@ -533,10 +529,10 @@ void dbi_close(dbi_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
     h->res.release(); h->poff64.release(); h->poff.release(); h->blk.release(); h->scan_tmp.release();
-    h->thr.release(); h->tile_pf.release(); h->ptile.release(); h->chunk_lo.release(); h->chunk_bin.release();
-    h->recA.release(); h->recB.release(); h->hist.release(); h->bin_start.release(); h->ucount.release();
+    h->thr.release(); h->tile_pf.release(); h->ptile.release(); h->chunk_lo.release();
+    h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
     h->big_list.release(); h->giant_list.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
-    h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release(); h->key_flags.release();
+    h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release();
     h->o_mass.release(); h->o_pid.release(); h->o_off.release(); h->o_len.release();
     h->q_mass.release(); h->q_tol.release(); h->q_first.release(); h->q_count.release(); h->q_row.release();
     h->q_ids.release(); h->g_mass.release(); h->g_pid.release(); h->g_off.release(); h->g_len.release();
@@ -772,21 +768,25 @@ int dbi_entry_keys(dbi_handle* h, int32_t* keys, uint64_t cap, uint64_t* n) {
     const uint64_t U = h->stats.n_unique;
     if (U == 0) return 0;
     DBI_HIP(hipSetDevice(h->device));
-    DevBuf<uint32_t> pos;
+    DevBuf<uint32_t> flags, pos;
     DevBuf<int32_t> dk;
     int rc;
-    if ((rc = pos.ensure(U)) || (rc = dk.ensure(h->stats.n_keys))) {
+    if ((rc = flags.ensure(U)) || (rc = pos.ensure(U)) || (rc = dk.ensure(h->stats.n_keys))) {
+        flags.release();
         pos.release();
         dk.release();
         return rc;
     }
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(U), h->scan_tmp.cap)))) return rc;
-    hipError_t e = launch_scan_u32(h->key_flags.p, pos.p, U, h->scan_tmp.p, h->scan_tmp.cap, nullptr, h->stream);
+    hipError_t e = launch_key_flags(h->umass.p, (uint32_t)U, h->params.mass_group_factor, flags.p, h->stream);
+    if (e == hipSuccess)
+        e = launch_scan_u32(flags.p, pos.p, U, h->scan_tmp.p, h->scan_tmp.cap, nullptr, h->stream);
     if (e == hipSuccess)
         e = launch_write_keys(h->umass.p, (uint32_t)U, h->params.mass_group_factor, pos.p, dk.p, h->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(keys, dk.p, 4 * h->stats.n_keys, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    flags.release();
     pos.release();
     dk.release();
     if (e != hipSuccess) return hip_fail(e, "dbi_entry_keys");

@@ -114,10 +114,9 @@ hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const B
                                 const uint32_t* d_hist, hipStream_t s);
 uint64_t radix_blocks(uint32_t n);
 size_t radix_hist_elems(uint32_t n, int bits);
-hipError_t launch_bin_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t* d_bin_start,
-                             hipStream_t s);
-hipError_t launch_chunk_bounds(const uint32_t* d_bin_start, uint32_t nbins, uint32_t n, uint32_t T, uint32_t nchunks,
-                               uint32_t* d_chunk_lo, uint32_t* d_chunk_bin, hipStream_t s);
+// chunk_lo[c] = first bin start at or after c*T in the bin-sorted records (nchunks+1 entries)
+hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,
+                               uint32_t* d_chunk_lo, hipStream_t s);
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, uint32_t* d_ucount, uint32_t* d_big_list,
                              Counters* d_ctr, hipStream_t s);
@@ -135,9 +134,9 @@ hipError_t launch_pid_tiles(const uint32_t* d_poff, uint32_t n_prot, uint4* d_pt
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            const uint32_t* d_poff, const uint4* d_ptile, double* d_umass, uint32_t* d_upid,
                            uint32_t* d_uoff, uint32_t* d_ulen, uint32_t* d_occ_off, uint32_t* d_occ_pid,
-                           hipStream_t s);
-hipError_t launch_count_keys(const double* d_umass, uint32_t n_upper, int32_t factor,
-                             uint32_t* d_flags, Counters* d_ctr, hipStream_t s);
+                           int32_t factor, Counters* d_ctr, hipStream_t s);
+hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t factor, uint32_t* d_flags,
+                            hipStream_t s);
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s);
 hipError_t launch_gather(const uint64_t* d_ids, uint64_t n, const double* d_umass, const uint32_t* d_upid,
                          const uint32_t* d_uoff, const uint32_t* d_ulen, const uint32_t* d_occ_off,
