@@ -78,7 +78,7 @@ constexpr int DIGEST_HALO = 256;    // residues staged past the tile
 constexpr int RADIX_BITS = 9;        // max digit width (512 buckets)
 constexpr int RADIX_THREADS = 256;
 constexpr int RADIX_ITEMS = 16;     // records per thread per radix block
-constexpr int CHUNK_THREADS = 256;
+constexpr int CHUNK_THREADS = 512;
 constexpr int CHUNK_CAP = 2048;     // records per chunk sorted in LDS
 constexpr int CHUNK_T = 1024;       // target chunk size (whole mass bins, ~T..T+maxbin)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
