@@ -106,14 +106,12 @@ __device__ __forceinline__ uint64_t dbits(double m) { return (uint64_t)__double_
 constexpr int WIN_PRE = 16;  // residues staged before the tile (N-terminal context)
 constexpr int WIN = WIN_PRE + DIGEST_TILE + DIGEST_HALO;
 constexpr int STARTS_PER_THREAD = DIGEST_TILE / DIGEST_THREADS;
-constexpr int PLIST_CAP = WIN + 2;
 
 struct DigestSmem {
     double mass[256];
     uint16_t win[WIN];          // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST)
     uint8_t flags[256];
     uint8_t pbit[WIN + 1];      // 1 = a protein starts at this window position (incl. one past the window)
-    uint32_t plist[PLIST_CAP];  // protein offsets overlapping the window
     uint16_t cand[DIGEST_TILE]; // compacted candidate starts (tile-local), in order
     uint32_t tmp[DIGEST_THREADS / 64 + 1];
 };
@@ -166,7 +164,8 @@ struct WalkOut {
 // non-mandatory filterSequence is always INCLUDE.
 template <bool EMIT, bool SEMI, bool MAND>
 __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSmem& sm, uint32_t w0, uint32_t wlim,
-                                            uint32_t s, bool n_ok, Rec* __restrict__ out, Counters* ctr) {
+                                            uint32_t s, bool n_ok, Rec* __restrict__ out, const Rec* out_end,
+                                            Counters* ctr) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;                 // precMass after H2O+H+, cTerm, nTerm (:265-271)
     if (!(m <= dp.max_mh)) return r;  // while condition before the first residue (:284)
@@ -209,7 +208,7 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
             rec.len = (uint16_t)(e - s + 1);
             rec.tag = fold_tag(hsh);
             if (e - s + 1 > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
-            out[kept] = rec;
+            if (out + kept < out_end) out[kept] = rec;
         }
         kept += keep;
         dropped += drop;
@@ -228,7 +227,8 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
 // the cut from the next residue and the protein end pe.
 template <bool EMIT, bool SEMI, bool MAND>
 __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const uint8_t* __restrict__ g_res,
-                               uint32_t s, uint32_t pe, bool n_ok, Rec* __restrict__ out, Counters* ctr) {
+                               uint32_t s, uint32_t pe, bool n_ok, Rec* __restrict__ out, const Rec* out_end,
+                               Counters* ctr) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;
     if (!(m <= dp.max_mh)) return r;
@@ -262,7 +262,7 @@ __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const 
             rec.len = (uint16_t)(e - s + 1);
             rec.tag = fold_tag(hsh);
             if (e - s + 1 > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
-            out[kept] = rec;
+            if (out + kept < out_end) out[kept] = rec;
         }
         kept += emit && !drop;
         dropped += drop;
@@ -273,34 +273,42 @@ __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const 
     return r;
 }
 
-// COUNT: per-thread kept counts -> d_thr, per-tile totals -> d_blk.
-// EMIT : d_blk holds the exclusive per-tile offsets; a block scan of the
-//        per-thread counts places each thread's contiguous run of candidates:
-//        thread order == start order, so records land in insertion order.
-template <bool EMIT, bool SEMI, bool MAND>
-__global__ void __launch_bounds__(DIGEST_THREADS)
-k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
-         const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
-         uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, uint32_t* __restrict__ d_blk,
-         uint32_t* __restrict__ d_thr, Rec* __restrict__ d_out, Counters* __restrict__ d_ctr) {
-    __shared__ DigestSmem sm;
+// One digest tile: starts [t0, t_end), staged window [w0, w_end), proteins [pf, pl].
+struct TileCtx {
+    uint32_t t0, t_end, w0, w_end, nbytes, pf, pl;
+};
+
+// N_ok(s) for tile position i: protein N-terminus, or the previous position is a cut
+__device__ __forceinline__ bool n_ok_at(const DigestSmem& sm, const TileCtx& tc, uint32_t i) {
+    const uint32_t p = tc.t0 + i - tc.w0;
+    return sm.pbit[p] || (p > 0 && ((sm.win[p - 1] >> 8) & F_CUT));
+}
+
+// Stage the tile's window (residues + class flags + cut / protein-end flags)
+// and the residue tables in LDS, and compact the candidate starts (every start
+// in SEMI mode, else the N_ok ones) into sm.cand.  Returns the candidate count.
+template <bool SEMI>
+__device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, const double* __restrict__ d_mass_tab,
+                                   const uint8_t* __restrict__ d_flags, const uint8_t* __restrict__ d_res,
+                                   const uint32_t* __restrict__ d_poff, uint32_t n_prot, uint32_t n_res,
+                                   const uint32_t* __restrict__ d_tile_pf) {
     const uint32_t tid = threadIdx.x;
     const uint32_t ntiles = gridDim.x;
-    const uint32_t t0 = blockIdx.x * (uint32_t)DIGEST_TILE;
-    const uint32_t t_end = min(t0 + (uint32_t)DIGEST_TILE, n_res);
-    const uint32_t w0 = t0 >= (uint32_t)WIN_PRE ? t0 - WIN_PRE : 0u;
-    const uint32_t w_end = min(w0 + (uint32_t)WIN, n_res);
-    const uint32_t nbytes = w_end - w0;
+    tc.t0 = tile * (uint32_t)DIGEST_TILE;
+    tc.t_end = min(tc.t0 + (uint32_t)DIGEST_TILE, n_res);
+    tc.w0 = tc.t0 >= (uint32_t)WIN_PRE ? tc.t0 - WIN_PRE : 0u;
+    tc.w_end = min(tc.w0 + (uint32_t)WIN, n_res);
+    tc.nbytes = tc.w_end - tc.w0;
+    const uint32_t w0 = tc.w0, w_end = tc.w_end, nbytes = tc.nbytes;
 
     // residue tables -> LDS
     sm.mass[tid] = d_mass_tab[tid];
     sm.flags[tid] = d_flags[tid];
     for (uint32_t i = tid; i <= (uint32_t)WIN; i += DIGEST_THREADS) sm.pbit[i] = 0;
     // proteins overlapping [t0, w_end]: [pf, pl] narrowed by the tile table
-    const uint32_t pf = d_tile_pf[blockIdx.x];
-    const uint32_t pl = find_le(d_poff, pf, min(d_tile_pf[min(blockIdx.x + 2, ntiles)] + 1, n_prot), w_end - 1);
-    const uint32_t np_all = pl - pf + 2;
-    const uint32_t np = np_all <= (uint32_t)PLIST_CAP ? np_all : 0u;
+    tc.pf = d_tile_pf[tile];
+    tc.pl = find_le(d_poff, tc.pf, min(d_tile_pf[min(tile + 2, ntiles)] + 1, n_prot), w_end - 1);
+    const uint32_t np_all = tc.pl - tc.pf + 2;
     __syncthreads();
     // residue window -> LDS as (residue | flags << 8), 16 residues per load when aligned
     {
@@ -328,8 +336,7 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
         }
     }
     for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
-        const uint32_t o = d_poff[pf + i];
-        if (np) sm.plist[i] = o;
+        const uint32_t o = d_poff[tc.pf + i];
         if (o >= w0 && o <= w_end) sm.pbit[o - w0] = 1;  // protein starts (and the end of the last one)
     }
     __syncthreads();
@@ -337,9 +344,10 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     // window's last position (w_end < R) the next residue is unknown; a walk
     // that reaches it without a protein end overflows to walk_global first.
     {
-        uint32_t cf[(WIN + DIGEST_THREADS - 1) / DIGEST_THREADS];
+        constexpr uint32_t K = (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS;
+        uint32_t cf[K];
 #pragma unroll
-        for (uint32_t k = 0; k < (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS; ++k) {
+        for (uint32_t k = 0; k < K; ++k) {
             const uint32_t i = tid + k * DIGEST_THREADS;
             cf[k] = 0;
             if (i < nbytes) {
@@ -352,24 +360,18 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
         }
         __syncthreads();
 #pragma unroll
-        for (uint32_t k = 0; k < (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS; ++k) {
+        for (uint32_t k = 0; k < K; ++k) {
             const uint32_t i = tid + k * DIGEST_THREADS;
             if (i < nbytes) sm.win[i] |= (uint16_t)(cf[k] << 8);
         }
     }
     __syncthreads();
-
-    // N_ok(s): protein N-terminus, or the previous position is a cut
-    auto n_ok_at = [&](uint32_t i) -> bool {
-        const uint32_t p = t0 + i - w0;
-        return sm.pbit[p] || (p > 0 && ((sm.win[p - 1] >> 8) & F_CUT));
-    };
     // cleavage-site compaction: thread t owns starts [t*SPT, t*SPT+SPT) in order
     uint32_t mybits = 0, mycnt = 0;
 #pragma unroll
     for (int k = 0; k < STARTS_PER_THREAD; ++k) {
         const uint32_t i = tid * STARTS_PER_THREAD + k;
-        const bool ok = (t0 + i < t_end) && (SEMI || n_ok_at(i));
+        const bool ok = (tc.t0 + i < tc.t_end) && (SEMI || n_ok_at(sm, tc, i));
         if (ok) { mybits |= 1u << k; ++mycnt; }
     }
     uint32_t ncand;
@@ -378,51 +380,339 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     for (int k = 0; k < STARTS_PER_THREAD; ++k)
         if (mybits & (1u << k)) sm.cand[pos++] = (uint16_t)(tid * STARTS_PER_THREAD + k);
     __syncthreads();
+    return ncand;
+}
 
-    // thread t walks candidates [jb, je): a contiguous, balanced share
+// One candidate: LDS walk, or the HBM walk when it outruns the window
+template <bool EMIT, bool SEMI, bool MAND>
+__device__ __forceinline__ WalkOut walk_candidate(const DevParams& dp, const DigestSmem& sm, const TileCtx& tc,
+                                                  const uint8_t* __restrict__ d_res,
+                                                  const uint32_t* __restrict__ d_poff, uint32_t j,
+                                                  Rec* __restrict__ o, const Rec* o_end, Counters* ctr) {
+    const uint32_t i = sm.cand[j];
+    const uint32_t s = tc.t0 + i;
+    const bool n_ok = SEMI ? n_ok_at(sm, tc, i) : true;
+    WalkOut w = walk_lds<EMIT, SEMI, MAND>(dp, sm, tc.w0, tc.w_end, s, n_ok, o, o_end, ctr);
+    if (w.overflow) {
+        const uint32_t pe = d_poff[find_le(d_poff, tc.pf, tc.pl + 1, s) + 1];
+        w = walk_global<EMIT, SEMI, MAND>(dp, sm, d_res, s, pe, n_ok, o, o_end, ctr);
+    }
+    return w;
+}
+
+// thread t walks candidates [jb, je): a contiguous, balanced share (thread
+// order == start order, so EMIT writes land in insertion order)
+__device__ __forceinline__ void thread_share(uint32_t ncand, uint32_t& jb, uint32_t& je) {
     const uint32_t q = ncand / DIGEST_THREADS, rr = ncand % DIGEST_THREADS;
-    const uint32_t jb = tid * q + min(tid, rr);
-    const uint32_t je = jb + q + (tid < rr ? 1u : 0u);
+    jb = threadIdx.x * q + min(threadIdx.x, rr);
+    je = jb + q + (threadIdx.x < rr ? 1u : 0u);
+}
 
-    // one candidate: LDS walk, or the HBM walk when it outruns the window
-    auto walk = [&](uint32_t j, Rec* o) -> WalkOut {
-        const uint32_t i = sm.cand[j];
-        const uint32_t s = t0 + i;
-        const bool n_ok = SEMI ? n_ok_at(i) : true;
-        WalkOut w = walk_lds<EMIT, SEMI, MAND>(dp, sm, w0, w_end, s, n_ok, o, d_ctr);
-        if (w.overflow) {
-            uint32_t pe;
-            if (np) {
-                pe = sm.plist[find_le(sm.plist, 0, np - 1, s) + 1];
-            } else {
-                pe = d_poff[find_le(d_poff, pf, pl + 1, s) + 1];
-            }
-            w = walk_global<EMIT, SEMI, MAND>(dp, sm, d_res, s, pe, n_ok, o, d_ctr);
-        }
-        return w;
-    };
+// per-thread kept counts -> d_thr, per-tile totals -> d_blk, dropped -> counter
+__device__ __forceinline__ void publish_counts(DigestSmem& sm, uint32_t kept, uint32_t dropped,
+                                               uint32_t* __restrict__ d_blk, uint32_t* __restrict__ d_thr,
+                                               Counters* __restrict__ d_ctr) {
+    d_thr[blockIdx.x * DIGEST_THREADS + threadIdx.x] = kept;
+    const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
+    const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
+    if (threadIdx.x == 0) {
+        d_blk[blockIdx.x] = tk;
+        if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
+    }
+}
 
+// COUNT: per-thread kept counts -> d_thr, per-tile totals -> d_blk.
+// EMIT : d_blk holds the exclusive per-tile offsets; a block scan of the
+//        per-thread counts places each thread's contiguous run of candidates:
+//        thread order == start order, so records land in insertion order.
+template <bool EMIT, bool SEMI, bool MAND>
+__global__ void __launch_bounds__(DIGEST_THREADS)
+k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
+         const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
+         uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, uint32_t* __restrict__ d_blk,
+         uint32_t* __restrict__ d_thr, Rec* __restrict__ d_out, Counters* __restrict__ d_ctr) {
+    __shared__ DigestSmem sm;
+    TileCtx tc;
+    const uint32_t ncand = digest_prepare<SEMI>(sm, tc, blockIdx.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
+                                                d_tile_pf);
+    uint32_t jb, je;
+    thread_share(ncand, jb, je);
     if (!EMIT) {
         uint32_t kept = 0, dropped = 0;
         for (uint32_t j = jb; j < je; ++j) {
-            const WalkOut w = walk(j, nullptr);
+            const WalkOut w = walk_candidate<false, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr, d_ctr);
             kept += w.kept;
             dropped += w.dropped;
         }
-        d_thr[blockIdx.x * DIGEST_THREADS + tid] = kept;
-        const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
-        const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
-        if (tid == 0) {
-            d_blk[blockIdx.x] = tk;
-            if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
-        }
+        publish_counts(sm, kept, dropped, d_blk, d_thr, d_ctr);
         return;
     }
-
     uint32_t tot;
-    const uint32_t my = d_thr[blockIdx.x * DIGEST_THREADS + tid];
+    const uint32_t my = d_thr[blockIdx.x * DIGEST_THREADS + threadIdx.x];
     Rec* out = d_out + d_blk[blockIdx.x] + block_excl_scan<DIGEST_THREADS, uint32_t>(my, sm.tmp, tot);
-    for (uint32_t j = jb; j < je; ++j) out += walk(j, out).kept;
+    const Rec* out_end = reinterpret_cast<const Rec*>(~(uintptr_t)0 & ~(uintptr_t)15);  // sized from the count pass
+    for (uint32_t j = jb; j < je; ++j)
+        out += walk_candidate<true, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, out, out_end, d_ctr).kept;
+}
+
+
+// ---------------------------------------------------------------------------
+// COUNT for full-enzyme digestion without mandatory residues: decisions only
+// happen at cuts (checkCleavage is C_ok; the mass only grows), so a start
+// steps cut to cut: window-local fp64 prefix sums give the mass, prefix
+// counts of cleave residues give intMisCleavageCount, a next-cut table the
+// next cut.  ~4 steps per start instead of ~30 residues.  A start whose
+// approximate mass comes within CUT_EPS Da of minMH / maxMH / the bucket-drop
+// mass, or that would leave the window, is recounted by the exact walk, so the
+// counts equal the emit pass's exactly.  (Prefix error over a 2320-residue
+// window < 3e-7 Da; CUT_EPS = 1e-5.)
+// ---------------------------------------------------------------------------
+constexpr double CUT_EPS = 1e-4;  // > 2 x the fixed-point rounding of the prefix tables (7.6e-6 Da each)
+constexpr uint16_t NO_CUT = 0xFFFFu;
+constexpr uint32_t PM_BLOCK = 64;  // positions per fp64 prefix base
+
+// Window prefix tables for cut stepping.  Mass prefix of positions [0, i]:
+// base[i / 64] (fp64, prefix before the 64-position block) + off[i] / 2^16 Da
+// (fixed point; within a block < 64 residues x 1024 Da, DevParams::cut_count).
+struct CutSmem {
+    double base[WIN / PM_BLOCK + 1];
+    uint32_t off[WIN];
+    uint16_t ccl[WIN];    // cleave residues in [0, i]
+    uint16_t ncut[WIN];   // first cut position >= i (the last position only if a protein ends there)
+    uint16_t first[DIGEST_THREADS];
+};
+
+__device__ __forceinline__ double cut_prefix(const CutSmem& cs, uint32_t i) {
+    return cs.base[i / PM_BLOCK] + (double)cs.off[i] * (1.0 / 65536.0);
+}
+
+struct CutCount {
+    uint32_t kept, dropped;
+    bool exact;  // false: recount with the residue walk
+};
+
+__device__ __forceinline__ CutCount count_by_cuts(const DevParams& dp, const DigestSmem& sm, const CutSmem& cs,
+                                                  uint32_t nbytes, uint32_t ps) {
+    CutCount r{0u, 0u, true};
+    if (!(dp.m0 <= dp.max_mh)) return r;
+    const double pb = ps > 0 ? cut_prefix(cs, ps - 1) : 0.0;
+    const int cb = ps > 0 ? (int)cs.ccl[ps - 1] : 0;
+    const bool can_drop = dp.drop_mass <= dp.max_mh;
+    uint32_t e = cs.ncut[ps];
+    for (;;) {
+        if (e == NO_CUT) {
+            // no cut before the window ends: only fine if the mass passes maxMH first
+            const double m_end = dp.m0 + (cut_prefix(cs, nbytes - 1) - pb);
+            r.exact = m_end > dp.max_mh + CUT_EPS;
+            return r;
+        }
+        const double m = dp.m0 + (cut_prefix(cs, e) - pb);
+        if (fabs(m - dp.max_mh) <= CUT_EPS) { r.exact = false; return r; }
+        const int mc = (int)cs.ccl[e] - cb - 1;
+        if (mc > dp.max_missed || m > dp.max_mh) return r;  // break (:322-329)
+        if ((int)(e - ps + 1) >= dp.min_len) {
+            if (fabs(m - dp.min_mh) <= CUT_EPS || (can_drop && fabs(m - dp.drop_mass) <= CUT_EPS)) {
+                r.exact = false;
+                return r;
+            }
+            if (m >= dp.min_mh) {
+                const bool drop = can_drop && m >= dp.drop_mass;
+                r.kept += !drop;
+                r.dropped += drop;
+            }
+        }
+        if ((sm.win[e] >> 8) & F_LAST) return r;
+        e = e + 1 < nbytes ? cs.ncut[e + 1] : NO_CUT;
+    }
+}
+
+// Build the cut tables from the staged window (all threads; ends with a barrier).
+__device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nbytes, double* s_dtmp) {
+    constexpr uint32_t E = (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS;
+    const uint32_t lo = threadIdx.x * E;
+    double msum = 0.0;
+    uint32_t csum = 0;
+    uint32_t fc = NO_CUT;  // first cut in my range
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint32_t i = lo + k;
+        if (i < nbytes) {
+            const uint32_t w = sm.win[i];
+            msum += sm.mass[w & 0xFFu];
+            csum += (w >> 8) & F_CLEAVE;
+            const bool cut = ((w >> 8) & F_CUT) && (i + 1 < nbytes || ((w >> 8) & F_LAST));
+            if (cut && fc == NO_CUT) fc = i;
+        }
+    }
+    double dtot;
+    uint32_t ctot;
+    double mrun = block_excl_scan<DIGEST_THREADS, double>(msum, s_dtmp, dtot);
+    uint32_t crun = block_excl_scan<DIGEST_THREADS, uint32_t>(csum, reinterpret_cast<uint32_t*>(s_dtmp), ctot);
+    cs.first[threadIdx.x] = (uint16_t)fc;
+    if (threadIdx.x == 0) cs.base[0] = 0.0;
+    double pm[E];
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint32_t i = lo + k;
+        pm[k] = 0.0;
+        if (i < nbytes) {
+            const uint32_t w = sm.win[i];
+            mrun += sm.mass[w & 0xFFu];
+            crun += (w >> 8) & F_CLEAVE;
+            pm[k] = mrun;
+            cs.ccl[i] = (uint16_t)crun;
+            if (i % PM_BLOCK == PM_BLOCK - 1) cs.base[i / PM_BLOCK + 1] = mrun;
+        }
+    }
+    __syncthreads();
+    uint32_t nxt = NO_CUT;  // first cut after my range
+    for (uint32_t t = threadIdx.x + 1; t < DIGEST_THREADS && nxt == NO_CUT; ++t) nxt = cs.first[t];
+#pragma unroll
+    for (int k = (int)E - 1; k >= 0; --k) {
+        const uint32_t i = lo + (uint32_t)k;
+        if (i < nbytes) {
+            cs.off[i] = (uint32_t)__double2ll_rn((pm[k] - cs.base[i / PM_BLOCK]) * 65536.0);
+            const uint32_t w = sm.win[i];
+            const bool cut = ((w >> 8) & F_CUT) && (i + 1 < nbytes || ((w >> 8) & F_LAST));
+            if (cut) nxt = i;
+            cs.ncut[i] = (uint16_t)nxt;
+        }
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(DIGEST_THREADS)
+k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
+                    const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
+                    uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, uint32_t* __restrict__ d_blk,
+                    uint32_t* __restrict__ d_thr, Counters* __restrict__ d_ctr) {
+    __shared__ DigestSmem sm;
+    __shared__ CutSmem cs;
+    __shared__ double s_dtmp[DIGEST_THREADS / 64 + 1];
+    TileCtx tc;
+    const uint32_t ncand = digest_prepare<false>(sm, tc, blockIdx.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
+                                                 d_tile_pf);
+    build_cut_tables(sm, cs, tc.nbytes, s_dtmp);
+    uint32_t jb, je;
+    thread_share(ncand, jb, je);
+    uint32_t kept = 0, dropped = 0;
+    for (uint32_t j = jb; j < je; ++j) {
+        CutCount r = count_by_cuts(dp, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0);
+        if (!r.exact) {
+            const WalkOut w = walk_candidate<false, false, false>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr, d_ctr);
+            r.kept = w.kept;
+            r.dropped = w.dropped;
+        }
+        kept += r.kept;
+        dropped += r.dropped;
+    }
+    publish_counts(sm, kept, dropped, d_blk, d_thr, d_ctr);
+}
+
+// ---------------------------------------------------------------------------
+// Fused COUNT + EMIT (one staging of the window): count the tile's kept
+// records, publish the tile total, find the tile's output offset by a
+// decoupled look-back over earlier tiles (tiles numbered by an atomic ticket
+// in dispatch order, so every predecessor is running or done), then walk again
+// and emit.  Status word per tile: epoch (16 b) | state (2 b) | value (46 b),
+// state 1 = tile total, 2 = inclusive prefix; agent-scope atomics.
+// ---------------------------------------------------------------------------
+constexpr unsigned long long ST_AGG = 1ull, ST_PREFIX = 2ull;
+
+__device__ __forceinline__ unsigned long long st_pack(uint32_t epoch, unsigned long long state,
+                                                      unsigned long long v) {
+    return ((unsigned long long)epoch << 48) | (state << 46) | v;
+}
+
+template <bool SEMI, bool MAND>
+__global__ void __launch_bounds__(DIGEST_THREADS)
+k_digest_fused(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
+               const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
+               uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, unsigned long long* __restrict__ status,
+               uint32_t epoch, Rec* __restrict__ d_out, uint32_t cap, Counters* __restrict__ d_ctr) {
+    __shared__ DigestSmem sm;
+    __shared__ uint32_t s_tile;
+    __shared__ unsigned long long s_base;
+    if (threadIdx.x == 0) s_tile = atomicAdd(&d_ctr->tile_ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    TileCtx tc;
+    const uint32_t ncand = digest_prepare<SEMI>(sm, tc, tile, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
+                                                d_tile_pf);
+    uint32_t jb, je;
+    thread_share(ncand, jb, je);
+    // count (exact walk: the cut-stepping tables would cost this kernel its
+    // occupancy, and its emit walk is issue-bound)
+    uint32_t kept = 0, dropped = 0;
+    for (uint32_t j = jb; j < je; ++j) {
+        const WalkOut w = walk_candidate<false, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr, d_ctr);
+        kept += w.kept;
+        dropped += w.dropped;
+    }
+    uint32_t total;
+    const uint32_t mine = block_excl_scan<DIGEST_THREADS, uint32_t>(kept, sm.tmp, total);
+    const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
+    if (threadIdx.x < 64) {
+        // wave 0: publish, then look back 64 tiles at a time
+        if (threadIdx.x == 0) {
+            if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
+            __hip_atomic_store(&status[tile], st_pack(epoch, tile == 0 ? ST_PREFIX : ST_AGG, total),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        unsigned long long excl = 0;
+        int64_t t = (int64_t)tile - 1;
+        const uint32_t lane = lane_id();
+        while (t >= 0) {
+            const int64_t q = t - (int64_t)lane;
+            unsigned long long v = 0;
+            bool ready = true;
+            if (q >= 0) {
+                v = __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ready = (uint32_t)(v >> 48) == epoch && ((v >> 46) & 3ull) != 0;
+            }
+            const uint64_t pref = __ballot(q >= 0 && ready && ((v >> 46) & 3ull) == ST_PREFIX);
+            const uint64_t notready = __ballot(!ready);
+            // lanes up to (and including) the nearest prefix, all ready -> sum them
+            const uint32_t upto = pref ? (uint32_t)__ffsll((long long)pref) - 1 : 64u;  // nearest prefix lane
+            const uint64_t need = upto >= 63 ? ~0ull : ((2ull << upto) - 1);
+            if (notready & need) continue;  // a predecessor has not published yet: poll again
+            const unsigned long long val = (lane <= upto && q >= 0) ? (v & ((1ull << 46) - 1)) : 0ull;
+            excl += wave_sum(val);
+            if (pref) break;
+            t -= 64;
+        }
+        if (threadIdx.x == 0) {
+            if (tile != 0)
+                __hip_atomic_store(&status[tile], st_pack(epoch, ST_PREFIX, excl + total), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (tile == gridDim.x - 1) d_ctr->n_kept = excl + total;
+            s_base = excl;
+        }
+    }
+    __syncthreads();
+    const unsigned long long base = s_base + mine;
+    Rec* out = d_out + base;
+    const Rec* out_end = d_out + cap;
+    for (uint32_t j = jb; j < je; ++j)
+        out += walk_candidate<true, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, out, out_end, d_ctr).kept;
+}
+
+hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                               const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                               const uint32_t* d_tile_pf, unsigned long long* d_status, uint32_t epoch,
+                               Rec* d_out, uint32_t cap, Counters* d_ctr, hipStream_t s) {
+    const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
+    if (nblk == 0) return hipSuccess;
+#define DBI_FUSED(SEMI, MAND)                                                                              \
+    DBI_LAUNCH((k_digest_fused<SEMI, MAND>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, \
+               d_res, d_poff, n_prot, n_res, d_tile_pf, d_status, epoch, d_out, cap, d_ctr)
+    if (dp.semi) {
+        if (dp.mand_mode) DBI_FUSED(true, true); else DBI_FUSED(true, false);
+    } else {
+        if (dp.mand_mode) DBI_FUSED(false, true); else DBI_FUSED(false, false);
+    }
+#undef DBI_FUSED
+    return hipGetLastError();
 }
 
 template <bool EMIT>
@@ -435,6 +725,11 @@ static hipError_t launch_digest(const DevParams& dp, const double* d_mass_tab, c
 #define DBI_DIGEST(SEMI, MAND)                                                                              \
     DBI_LAUNCH((k_digest<EMIT, SEMI, MAND>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
                        d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_out, d_ctr)
+    if (!EMIT && !dp.semi && !dp.mand_mode && dp.cut_count) {
+        DBI_LAUNCH(k_digest_count_cuts, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
+                   d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr);
+        return hipGetLastError();
+    }
     if (dp.semi) {
         if (dp.mand_mode) DBI_DIGEST(true, true); else DBI_DIGEST(true, false);
     } else {

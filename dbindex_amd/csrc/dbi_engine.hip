@@ -86,6 +86,8 @@ struct dbi_handle {
 
     // workspace
     DevBuf<uint32_t> blk;       // digest tile counts / offsets
+    DevBuf<unsigned long long> status;  // fused digest: per-tile look-back words
+    uint32_t epoch = 0;                 // tag of the current fused launch in `status`
     DevBuf<uint32_t> thr;       // digest per-thread counts
     DevBuf<uint32_t> tile_pf;   // first protein of every digest tile (+1)
     DevBuf<uint4> ptile;        // {protein, start, end} of every 256th residue (finalize)
@@ -163,6 +165,9 @@ DevParams make_dev_params(const dbi_params& p) {
     d.mand_filter = (p.mandatory_mode && p.mandatory_count > 0) ? 1 : 0;
     d.semi = p.semi ? 1 : 0;
     d.drop_mass = (double)(d.nb * d.br);
+    double mmax = 0.0;
+    for (int c = 0; c < 256; ++c) mmax = std::max(mmax, p.mass[c]);
+    d.cut_count = (!p.semi && !p.mandatory_mode && mmax < 1024.0) ? 1 : 0;  // fixed-point prefix tables fit u32
     return d;
 }
 
@@ -357,21 +362,47 @@ int build_digest(dbi_handle* h) {
         return rc;
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(nblk), h->scan_tmp.cap)))) return rc;
     if ((rc = prepare_tiles(h))) return rc;
-    // digest reads every residue once (+ the protein offset table)
-    STAGE(h, "digest_count", by(1, 0, 0, 4, 0),
-          launch_digest_count(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
-                              (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->ctr.p, s));
-    STAGE(h, "digest_scan", by(0, 0, 0, 0, 0),
-          launch_scan_u32(h->blk.p, h->blk.p, nblk, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_kept, s));
-    if ((rc = read_counters(h))) return rc;
-    const uint64_t n = h->hc.n_kept;
-    if (n >= (1ull << 32) - 1)
-        return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences on one device: shard the FASTA");
-    if ((rc = h->recA.ensure(n))) return rc;
-    // digest emit: residues in, one 16-B record per kept occurrence out
-    STAGE(h, "digest_emit", by(1, 16, 0, 4, 0),
-          launch_digest_emit(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
-                             (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->recA.p, h->ctr.p, s));
+    uint64_t n;
+    if (h->recA.cap >= 1024) {
+        // warm: one fused pass into the capacity of the previous build; the
+        // exact total comes back with the counters, and a short buffer is
+        // grown and the pass run again
+        if ((rc = h->status.ensure(nblk))) return rc;
+        for (int attempt = 0;; ++attempt) {
+            if (++h->epoch >= 0xFFFFu) {
+                DBI_HIP(hipMemsetAsync(h->status.p, 0, sizeof(unsigned long long) * h->status.cap, s));
+                h->epoch = 1;
+            }
+            const uint32_t cap = (uint32_t)std::min<size_t>(h->recA.cap, 0xFFFFFFFFull);
+            STAGE(h, "digest", by(1, 16, 0, 4, 0),
+                  launch_digest_fused(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
+                                      (uint32_t)R, h->tile_pf.p, h->status.p, h->epoch, h->recA.p, cap, h->ctr.p, s));
+            if ((rc = read_counters(h))) return rc;
+            n = h->hc.n_kept;
+            if (n >= (1ull << 32) - 1)
+                return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences on one device: shard the FASTA");
+            if (n <= cap) break;
+            if (attempt > 0) return set_error(DBI_E_STATE, "digest output grew between identical passes");
+            if ((rc = h->recA.ensure(n + n / 8))) return rc;
+            DBI_HIP(hipMemsetAsync(h->ctr.p, 0, sizeof(Counters), s));
+        }
+    } else {
+        // cold: count, scan, size the output, emit
+        STAGE(h, "digest_count", by(1, 0, 0, 4, 0),
+              launch_digest_count(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
+                                  (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->ctr.p, s));
+        STAGE(h, "digest_scan", by(0, 0, 0, 0, 0),
+              launch_scan_u32(h->blk.p, h->blk.p, nblk, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_kept, s));
+        if ((rc = read_counters(h))) return rc;
+        n = h->hc.n_kept;
+        if (n >= (1ull << 32) - 1)
+            return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences on one device: shard the FASTA");
+        if ((rc = h->recA.ensure(n))) return rc;
+        // digest emit: residues in, one 16-B record per kept occurrence out
+        STAGE(h, "digest_emit", by(1, 16, 0, 4, 0),
+              launch_digest_emit(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
+                                 (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->recA.p, h->ctr.p, s));
+    }
     return build_tail(h, n, h->params.min_mh, h->params.max_mh);
 }
 
@@ -529,6 +560,7 @@ void dbi_close(dbi_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
     h->res.release(); h->poff64.release(); h->poff.release(); h->blk.release(); h->scan_tmp.release();
+    h->status.release();
     h->thr.release(); h->tile_pf.release(); h->ptile.release(); h->chunk_lo.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
     h->big_list.release(); h->giant_list.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();

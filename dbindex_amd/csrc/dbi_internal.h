@@ -55,6 +55,7 @@ struct DevParams {
     int32_t mand_filter;      // mand_mode && count > 0 (filterSequence path)
     int32_t semi;
     double drop_mass;         // bucket > NUM_BUCKETS-1  <=>  (int)m >= nb*br  <=>  m >= nb*br
+    int32_t cut_count;        // count by cut stepping (full enzyme, no mandatory AAs, residue masses < 1024 Da)
 };
 
 // Device counters block (one per engine), read back once per build.
@@ -67,7 +68,7 @@ struct Counters {
     unsigned int n_big;            // chunks above CHUNK_CAP (sorted by the 1024-thread LDS kernel)
     unsigned int err;              // device error bits
     unsigned int n_giant;          // chunks above BIG_CAP (global-memory path)
-    unsigned int pad;
+    unsigned int tile_ticket;      // k_digest_fused: tiles in dispatch order
 };
 constexpr unsigned ERR_LEN_OVERFLOW = 1;  // peptide longer than 65535 residues
 
@@ -94,6 +95,14 @@ hipError_t launch_digest_count(const DevParams& dp, const double* d_mass_tab, co
                                const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
                                uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr,
                                Counters* d_ctr, hipStream_t s);
+// One pass: count, decoupled look-back for the tile's output offset, emit.
+// Records past `cap` are not written (the exact total still lands in
+// ctr->n_kept: the caller grows the buffer and runs it again).  status:
+// ntiles words tagged with `epoch` (never 0; reset the words when it wraps).
+hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                               const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                               const uint32_t* d_tile_pf, unsigned long long* d_status, uint32_t epoch,
+                               Rec* d_out, uint32_t cap, Counters* d_ctr, hipStream_t s);
 hipError_t launch_digest_emit(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                               const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
                               uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk_off, uint32_t* d_thr,

@@ -26,13 +26,17 @@ def Engine():
 
 
 def _check(Engine, prm, pp, ctx, nq=2000):
+    """Build twice on one engine: the first build counts then emits (cold),
+    the second runs the fused single-pass digest into the first build's
+    capacity (warm).  Both must equal the oracle."""
     cp = prm.to_c()
     oix = cref.Index(cp, pp.residues, pp.offsets)
+    m, t = query_masses(oix, nq)
     with Engine(cp) as eng:
-        eng.build(pp)
-        assert_index_equal(eng, oix, ctx)
-        m, t = query_masses(oix, nq)
-        assert_queries_equal(eng, oix, m, t, ctx)
+        for phase in ("cold", "warm"):
+            eng.build(pp)
+            assert_index_equal(eng, oix, f"{ctx} [{phase}]")
+            assert_queries_equal(eng, oix, m, t, f"{ctx} [{phase}]")
     return oix
 
 
@@ -176,6 +180,9 @@ def test_exact_mass_lookup(Engine):
 
 
 def test_rebuild_reuses_workspace(Engine):
+    """Workspace reuse across inputs, including a fused (warm) build whose
+    output outgrows the previous capacity: the pass is re-run into a grown
+    buffer."""
     prm = DBIndexSearchParams.trypsin(2)
     big = fasta.config("1k")
     small = big.slice(0, 50)
@@ -186,6 +193,12 @@ def test_rebuild_reuses_workspace(Engine):
         assert_index_equal(eng, cref.Index(cp, small.residues, small.offsets), "rebuild-small")
         eng.build(big)
         assert_index_equal(eng, cref.Index(cp, big.residues, big.offsets), "rebuild-big")
+    with Engine(cp) as eng:
+        eng.build(big.slice(0, 120))      # cold: capacity ~ 120 proteins
+        eng.build(big)                    # warm, capacity short -> grown and re-run
+        assert_index_equal(eng, cref.Index(cp, big.residues, big.offsets), "outgrow")
+        eng.build(big)
+        assert_index_equal(eng, cref.Index(cp, big.residues, big.offsets), "outgrow-again")
 
 
 def test_build_device_pointers(Engine):
@@ -240,3 +253,15 @@ def test_tag_collisions(Engine, copies):
     pp = fasta.PackedProteins.from_sequences(seqs)
     _check(Engine, DBIndexSearchParams.trypsin(0), pp, f"collisions x{copies}", nq=500)
     _check(Engine, DBIndexSearchParams.trypsin(2), pp, f"collisions mc2 x{copies}", nq=500)
+
+
+def test_thresholds_on_exact_peptide_masses(Engine):
+    """minMH / maxMH set exactly to indexed peptide masses: inclusive bounds
+    (DBIndexer.java:284,331) decided on the bit-exact sequential sum, also in
+    the cut-stepping count pass (near-threshold starts are recounted exactly)."""
+    pp = fasta.config("1k").slice(0, 150)
+    d = cref.digest(DBIndexSearchParams.trypsin(2).to_c(), pp.residues, pp.offsets)
+    m = np.sort(d.mass)
+    for lo, hi in [(m[100], m[-100]), (m[7], m[8]), (np.nextafter(m[50], 0), np.nextafter(m[-50], 1e9))]:
+        prm = DBIndexSearchParams.trypsin(2, min_precursor_mass=float(lo), max_precursor_mass=float(hi))
+        _check(Engine, prm, pp, f"thresholds {lo} {hi}", nq=300)
