@@ -100,6 +100,11 @@ __device__ __forceinline__ uint32_t bin_of(double m, const BinMap& bm) {
 
 __device__ __forceinline__ uint64_t dbits(double m) { return (uint64_t)__double_as_longlong(m); }
 
+// a Rec loaded as 4 dwords: x,y = q0, z,w = q1
+__device__ __forceinline__ uint64_t u4_q0(const uint4& r) { return ((uint64_t)r.y << 32) | r.x; }
+__device__ __forceinline__ uint64_t u4_q1(const uint4& r) { return ((uint64_t)r.w << 32) | r.z; }
+__device__ __forceinline__ double u4_mass(const uint4& r) { return q0_mass(u4_q0(r)); }
+
 // ---------------------------------------------------------------------------
 // 1/3. digest: DBIndexer.cutSeq (:237-405) + SQLiteMult.filterSequence/addSequence
 // ---------------------------------------------------------------------------
@@ -107,8 +112,11 @@ constexpr int WIN_PRE = 16;  // residues staged before the tile (N-terminal cont
 constexpr int WIN = WIN_PRE + DIGEST_TILE + DIGEST_HALO;
 constexpr int STARTS_PER_THREAD = DIGEST_TILE / DIGEST_THREADS;
 
+constexpr uint32_t PST_CAP = 512;  // protein starts of a tile kept in LDS (else searched in HBM)
+
 struct DigestSmem {
     double mass[256];
+    uint32_t pst[PST_CAP];      // poff[pf .. pl+1] (protein of a start: binary search)
     uint16_t win[WIN];          // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST)
     uint8_t flags[256];
     uint8_t pbit[WIN + 1];      // 1 = a protein starts at this window position (incl. one past the window)
@@ -125,21 +133,36 @@ __device__ __forceinline__ uint32_t find_le(const uint32_t* poff, uint32_t lo, u
     return lo;
 }
 
-// tile_pf[t] = protein containing residue min(t*TILE, R-1), t in [0, ntiles]
+// tile_pf[t] = protein containing residue min(t*TILE, R-1), t in [0, ntiles];
+// threads < n_prot also fold their protein's length into ctr->max_plen
 __global__ void k_tile_proteins(const uint32_t* __restrict__ poff, uint32_t n_prot, uint32_t n_res, uint32_t ntiles,
-                                uint32_t* __restrict__ tile_pf) {
+                                uint32_t* __restrict__ tile_pf, Counters* __restrict__ ctr) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    const uint32_t x = min(t * (uint32_t)DIGEST_TILE, n_res - 1);
-    tile_pf[t] = find_le(poff, 0, n_prot, x);
+    if (t <= ntiles) {
+        const uint32_t x = min(t * (uint32_t)DIGEST_TILE, n_res - 1);
+        tile_pf[t] = find_le(poff, 0, n_prot, x);
+    }
+    // block max, then one atomic per block that can still raise the value
+    __shared__ uint32_t s_max[4];
+    uint32_t len = t < n_prot ? poff[t + 1] - poff[t] : 0u;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) len = max(len, (uint32_t)__shfl_xor((int)len, d, 64));
+    if (lane_id() == 0) s_max[threadIdx.x >> 6] = len;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t m = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+        if (m > __hip_atomic_load(&ctr->max_plen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMax(&ctr->max_plen, m);
+    }
 }
 
 hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res, uint32_t* d_tile_pf,
-                                hipStream_t s) {
+                                Counters* d_ctr, hipStream_t s) {
     if (n_res == 0 || n_prot == 0) return hipSuccess;
     const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
-    DBI_LAUNCH(k_tile_proteins, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
-               d_tile_pf);
+    const uint32_t nthr = max(ntiles + 1, n_prot);
+    DBI_LAUNCH(k_tile_proteins, dim3((nthr + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
+               d_tile_pf, d_ctr);
     return hipGetLastError();
 }
 
@@ -164,8 +187,8 @@ struct WalkOut {
 // non-mandatory filterSequence is always INCLUDE.
 template <bool EMIT, bool SEMI, bool MAND>
 __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSmem& sm, uint32_t w0, uint32_t wlim,
-                                            uint32_t s, bool n_ok, Rec* __restrict__ out, const Rec* out_end,
-                                            Counters* ctr) {
+                                            uint32_t s, bool n_ok, uint64_t loc, Rec* __restrict__ out,
+                                            const Rec* out_end) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;                 // precMass after H2O+H+, cTerm, nTerm (:265-271)
     if (!(m <= dp.max_mh)) return r;  // while condition before the first residue (:284)
@@ -202,12 +225,10 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
         const bool drop = can_drop & emit & (m >= dp.drop_mass);  // bucket > NUM_BUCKETS-1 (:282-288)
         const bool keep = emit & !drop;
         if (EMIT && keep) {
+            const uint32_t tag = fold_tag(hsh);
             Rec rec;
-            rec.mass = m;
-            rec.gstart = s;
-            rec.len = (uint16_t)(e - s + 1);
-            rec.tag = fold_tag(hsh);
-            if (e - s + 1 > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
+            rec.q0 = rec_q0(m, tag);
+            rec.q1 = rec_q1(tag, loc, e - s + 1);
             if (out + kept < out_end) out[kept] = rec;
         }
         kept += keep;
@@ -227,8 +248,8 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
 // the cut from the next residue and the protein end pe.
 template <bool EMIT, bool SEMI, bool MAND>
 __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const uint8_t* __restrict__ g_res,
-                               uint32_t s, uint32_t pe, bool n_ok, Rec* __restrict__ out, const Rec* out_end,
-                               Counters* ctr) {
+                               uint32_t s, uint32_t pe, bool n_ok, uint64_t loc, Rec* __restrict__ out,
+                               const Rec* out_end) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;
     if (!(m <= dp.max_mh)) return r;
@@ -256,12 +277,10 @@ __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const 
         }
         const bool drop = emit && m >= dp.drop_mass;
         if (EMIT && emit && !drop) {
+            const uint32_t tag = fold_tag(hsh);
             Rec rec;
-            rec.mass = m;
-            rec.gstart = s;
-            rec.len = (uint16_t)(e - s + 1);
-            rec.tag = fold_tag(hsh);
-            if (e - s + 1 > 0xFFFFu) atomicOr(&ctr->err, ERR_LEN_OVERFLOW);
+            rec.q0 = rec_q0(m, tag);
+            rec.q1 = rec_q1(tag, loc, e - s + 1);
             if (out + kept < out_end) out[kept] = rec;
         }
         kept += emit && !drop;
@@ -276,6 +295,8 @@ __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const 
 // One digest tile: starts [t0, t_end), staged window [w0, w_end), proteins [pf, pl].
 struct TileCtx {
     uint32_t t0, t_end, w0, w_end, nbytes, pf, pl;
+    uint32_t npst;  // entries of sm.pst (0: the tile's protein starts did not fit)
+    uint32_t w;     // record field width (EMIT)
 };
 
 // N_ok(s) for tile position i: protein N-terminus, or the previous position is a cut
@@ -335,9 +356,11 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, c
             }
         }
     }
+    tc.npst = np_all <= PST_CAP ? np_all : 0u;
     for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
         const uint32_t o = d_poff[tc.pf + i];
         if (o >= w0 && o <= w_end) sm.pbit[o - w0] = 1;  // protein starts (and the end of the last one)
+        if (i < PST_CAP) sm.pst[i] = o;
     }
     __syncthreads();
     // cleavage-cut and protein-end flags of every window position.  At the
@@ -383,19 +406,43 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, c
     return ncand;
 }
 
+// Protein of start s in the tile: largest p in [pf, pl] with poff[p] <= s
+// (LDS copy of the tile's offsets; HBM when they did not fit), and its start.
+__device__ __forceinline__ uint32_t tile_protein(const DigestSmem& sm, const TileCtx& tc,
+                                                 const uint32_t* __restrict__ d_poff, uint32_t s, uint32_t& pstart) {
+    if (tc.npst) {
+        uint32_t lo = 0, hi = tc.npst - 1;  // pst[hi] = poff[pl+1] > s
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sm.pst[mid] <= s) lo = mid; else hi = mid;
+        }
+        pstart = sm.pst[lo];
+        return tc.pf + lo;
+    }
+    const uint32_t p = find_le(d_poff, tc.pf, tc.pl + 1, s);
+    pstart = d_poff[p];
+    return p;
+}
+
 // One candidate: LDS walk, or the HBM walk when it outruns the window
 template <bool EMIT, bool SEMI, bool MAND>
 __device__ __forceinline__ WalkOut walk_candidate(const DevParams& dp, const DigestSmem& sm, const TileCtx& tc,
                                                   const uint8_t* __restrict__ d_res,
                                                   const uint32_t* __restrict__ d_poff, uint32_t j,
-                                                  Rec* __restrict__ o, const Rec* o_end, Counters* ctr) {
+                                                  Rec* __restrict__ o, const Rec* o_end) {
     const uint32_t i = sm.cand[j];
     const uint32_t s = tc.t0 + i;
     const bool n_ok = SEMI ? n_ok_at(sm, tc, i) : true;
-    WalkOut w = walk_lds<EMIT, SEMI, MAND>(dp, sm, tc.w0, tc.w_end, s, n_ok, o, o_end, ctr);
+    uint64_t loc = 0;
+    if (EMIT) {
+        uint32_t pstart;
+        const uint32_t p = tile_protein(sm, tc, d_poff, s, pstart);
+        loc = rec_loc(p, s - pstart, tc.w);
+    }
+    WalkOut w = walk_lds<EMIT, SEMI, MAND>(dp, sm, tc.w0, tc.w_end, s, n_ok, loc, o, o_end);
     if (w.overflow) {
         const uint32_t pe = d_poff[find_le(d_poff, tc.pf, tc.pl + 1, s) + 1];
-        w = walk_global<EMIT, SEMI, MAND>(dp, sm, d_res, s, pe, n_ok, o, o_end, ctr);
+        w = walk_global<EMIT, SEMI, MAND>(dp, sm, d_res, s, pe, n_ok, loc, o, o_end);
     }
     return w;
 }
@@ -440,19 +487,21 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     if (!EMIT) {
         uint32_t kept = 0, dropped = 0;
         for (uint32_t j = jb; j < je; ++j) {
-            const WalkOut w = walk_candidate<false, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr, d_ctr);
+            const WalkOut w = walk_candidate<false, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr);
             kept += w.kept;
             dropped += w.dropped;
         }
         publish_counts(sm, kept, dropped, d_blk, d_thr, d_ctr);
         return;
     }
+    tc.w = rec_width(d_ctr->max_plen);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && !rec_layout_ok(tc.w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
     uint32_t tot;
     const uint32_t my = d_thr[blockIdx.x * DIGEST_THREADS + threadIdx.x];
     Rec* out = d_out + d_blk[blockIdx.x] + block_excl_scan<DIGEST_THREADS, uint32_t>(my, sm.tmp, tot);
     const Rec* out_end = reinterpret_cast<const Rec*>(~(uintptr_t)0 & ~(uintptr_t)15);  // sized from the count pass
     for (uint32_t j = jb; j < je; ++j)
-        out += walk_candidate<true, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, out, out_end, d_ctr).kept;
+        out += walk_candidate<true, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, out, out_end).kept;
 }
 
 
@@ -599,7 +648,7 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     for (uint32_t j = jb; j < je; ++j) {
         CutCount r = count_by_cuts(dp, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0);
         if (!r.exact) {
-            const WalkOut w = walk_candidate<false, false, false>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr, d_ctr);
+            const WalkOut w = walk_candidate<false, false, false>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr);
             r.kept = w.kept;
             r.dropped = w.dropped;
         }
@@ -645,7 +694,7 @@ k_digest_fused(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_
     // occupancy, and its emit walk is issue-bound)
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
-        const WalkOut w = walk_candidate<false, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr, d_ctr);
+        const WalkOut w = walk_candidate<false, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr);
         kept += w.kept;
         dropped += w.dropped;
     }
@@ -690,11 +739,13 @@ k_digest_fused(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_
         }
     }
     __syncthreads();
+    tc.w = rec_width(d_ctr->max_plen);
+    if (tile == 0 && threadIdx.x == 0 && !rec_layout_ok(tc.w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
     const unsigned long long base = s_base + mine;
     Rec* out = d_out + base;
     const Rec* out_end = d_out + cap;
     for (uint32_t j = jb; j < je; ++j)
-        out += walk_candidate<true, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, out, out_end, d_ctr).kept;
+        out += walk_candidate<true, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, out, out_end).kept;
 }
 
 hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
@@ -883,7 +934,7 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int b
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
-        mv[k] = i < n ? in[i].mass : 0.0;
+        mv[k] = i < n ? q0_mass(in[i].q0) : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
@@ -923,7 +974,7 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, B
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
-        const uint32_t d = (bin_of(__hiloint2double((int)rv[k].y, (int)rv[k].x), bm) >> shift) & mask;
+        const uint32_t d = (bin_of(u4_mass(rv[k]), bm) >> shift) & mask;
         const uint64_t peers = digit_peers(d, i < n, bits);
         const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t before = cnt[w][d];
@@ -985,13 +1036,12 @@ uint64_t radix_blocks(uint32_t n) { return (n + RADIX_CHUNK - 1) / RADIX_CHUNK; 
 // so nothing past the string is read) and realigned with v_alignbyte — one
 // memory round trip per 16 residues.  A residue buffer that is not 4-B aligned
 // is read from the dword holding its first byte.
-__device__ __forceinline__ bool seq_equal(const uint8_t* __restrict__ res, const Rec& a, const Rec& b) {
-    if (a.len != b.len) return false;
-    if (a.gstart == b.gstart) return true;
-    const uint32_t len = a.len;
+__device__ __forceinline__ bool seq_equal_at(const uint8_t* __restrict__ res, uint32_t g_a, uint32_t g_b,
+                                             uint32_t len) {
+    if (g_a == g_b) return true;
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(res) & 3u);
     const uint32_t* __restrict__ w = reinterpret_cast<const uint32_t*>(res - mis);
-    const uint64_t ga = (uint64_t)a.gstart + mis, gb = (uint64_t)b.gstart + mis;
+    const uint64_t ga = (uint64_t)g_a + mis, gb = (uint64_t)g_b + mis;
     const uint64_t last_a = (ga + len - 1) >> 2, last_b = (gb + len - 1) >> 2;
     for (uint32_t k0 = 0; k0 < len; k0 += 16) {
         const uint64_t ia = (ga + k0) >> 2, ib = (gb + k0) >> 2;
@@ -1015,6 +1065,26 @@ __device__ __forceinline__ bool seq_equal(const uint8_t* __restrict__ res, const
         if (diff) return false;
     }
     return true;
+}
+
+// Where a record's peptide sits in the residue buffer (poff[pid] + off), and its length.
+struct RecLoc {
+    const uint8_t* res;
+    const uint32_t* poff;
+    uint32_t w;
+    __device__ __forceinline__ uint32_t gstart(uint64_t q1) const { return poff[q1_pid(q1, w)] + q1_off(q1, w); }
+    __device__ __forceinline__ bool same(const Rec& a, const Rec& b) const {
+        const uint32_t la = q1_len(a.q1, w);
+        if (la != q1_len(b.q1, w)) return false;
+        if ((a.q1 & 0x00FFFFFFFFFFFFFFull) == (b.q1 & 0x00FFFFFFFFFFFFFFull)) return true;
+        return seq_equal_at(res, gstart(a.q1), gstart(b.q1), la);
+    }
+};
+
+// record with the head flag in place of the tag (chunk sort -> finalize)
+__device__ __forceinline__ Rec with_head(Rec r, bool head) {
+    r.q0 = (r.q0 & ~0xFFull) | (head ? 1ull : 0ull);
+    return r;
 }
 
 // Bitonic sort of (key, hsh, idx) triples, ascending; NT threads.
@@ -1050,7 +1120,7 @@ __device__ void bitonic_sort3(unsigned long long* key, unsigned long long* hsh, 
 // key/hsh/k2/k3 are P2-sized scratch; s_u32 >= NT/64+1 slots.
 template <int NT, bool STAGE>
 __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __restrict__ out, uint32_t n,
-                                  const uint8_t* __restrict__ res, unsigned long long* key, unsigned long long* hsh,
+                                  const RecLoc& rl, unsigned long long* key, unsigned long long* hsh,
                                   uint32_t* k2, uint32_t* k3, uint32_t* s_u32, unsigned long long* s_flag) {
     uint32_t P2 = 1;
     while (P2 < n) P2 <<= 1;
@@ -1058,8 +1128,8 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __r
         if (i < n) {
             const Rec r = in[i];
             if (STAGE) rec[i] = r;
-            key[i] = dbits(r.mass);
-            hsh[i] = r.tag;
+            key[i] = r.q0;        // mass, tag >> 8
+            hsh[i] = r.q1 >> 56;  // tag & 0xFF
         } else {
             key[i] = ~0ull;  // padding sorts last
             hsh[i] = ~0ull;
@@ -1073,7 +1143,7 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __r
     // verify equal (mass, hash) neighbours are the same string
     for (uint32_t i = threadIdx.x + 1; i < n; i += NT) {
         if (key[i] == key[i - 1] && hsh[i] == hsh[i - 1]) {
-            if (!seq_equal(res, rec[k2[i]], rec[k2[i - 1]])) atomicOr(s_flag, 1ull);
+            if (!rl.same(rec[k2[i]], rec[k2[i - 1]])) atomicOr(s_flag, 1ull);
         }
     }
     __syncthreads();
@@ -1121,10 +1191,10 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __r
             uint32_t leader = k2[rs];
             if (rs != i) {
                 const Rec me = rec[k2[i]];
-                if (!seq_equal(res, me, rec[k2[rs]])) {
+                if (!rl.same(me, rec[k2[rs]])) {
                     leader = k2[i];
                     for (uint32_t r = rs + 1; r < i; ++r)
-                        if (seq_equal(res, me, rec[k2[r]])) { leader = k2[r]; break; }
+                        if (rl.same(me, rec[k2[r]])) { leader = k2[r]; break; }
                 }
             }
             // nobody reads key/hsh any more in this phase: re-key in place
@@ -1139,9 +1209,7 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __r
     uint32_t myheads = 0;
     for (uint32_t i = threadIdx.x; i < n; i += NT) {
         const bool head = (i == 0) || key[i] != key[i - 1] || hsh[i] != hsh[i - 1];
-        Rec r = rec[k2[i]];
-        r.tag = head ? 1 : 0;
-        out[i] = r;
+        out[i] = with_head(rec[k2[i]], head);
         myheads += head;
     }
     return myheads;
@@ -1160,17 +1228,17 @@ __global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap 
         chunk_lo[c] = x;
         return;
     }
-    const uint32_t b = bin_of(recs[x - 1].mass, bm);
+    const uint32_t b = bin_of(q0_mass(recs[x - 1].q0), bm);
     // first i >= x with bin(i) > b (bins are non-decreasing); lo: known <= b
     uint32_t lo = x - 1, step = 1, hi = x;
-    while (hi < n && bin_of(recs[hi].mass, bm) <= b) {
+    while (hi < n && bin_of(q0_mass(recs[hi].q0), bm) <= b) {
         lo = hi;
         step <<= 1;
         hi = min(x - 1 + step, n);
     }
     while (hi - lo > 1) {
         const uint32_t mid = lo + ((hi - lo) >> 1);
-        if (bin_of(recs[mid].mass, bm) <= b) lo = mid; else hi = mid;
+        if (bin_of(q0_mass(recs[mid].q0), bm) <= b) lo = mid; else hi = mid;
     }
     chunk_lo[c] = hi;
 }
@@ -1183,9 +1251,9 @@ hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, 
 }
 
 template <int NT>
-__device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m,
-                                  const uint8_t* __restrict__ res, const unsigned long long* key, const uint32_t* sec,
-                                  uint32_t* aux, uint16_t* pairs, uint32_t* s_u32, uint32_t* s_bad);
+__device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const RecLoc& rl,
+                                  const unsigned long long* key, const uint32_t* sec, uint32_t* aux, uint16_t* pairs,
+                                  uint32_t* s_u32, uint32_t* s_bad);
 
 // One chunk of m <= CAP records sorted in LDS by (mass bits, tag, local index)
 // with a bitonic network (cost independent of how the masses cluster), then
@@ -1193,15 +1261,15 @@ __device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ 
 // Returns this thread's head count.
 template <int NT, int CAP>
 __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m,
-                                  const uint8_t* __restrict__ res, unsigned long long* key, uint32_t* sec,
+                                  const RecLoc& rl, unsigned long long* key, uint32_t* sec,
                                   uint32_t* aux, uint16_t* pairs, uint32_t* s_u32, uint32_t* s_bad) {
     uint32_t P2 = 2;
     while (P2 < m) P2 <<= 1;
     for (uint32_t i = threadIdx.x; i < P2; i += NT) {
         if (i < m) {
             const Rec r = in[i];
-            key[i] = dbits(r.mass);
-            sec[i] = ((uint32_t)r.tag << 16) | i;
+            key[i] = r.q0;                                 // mass, tag >> 8
+            sec[i] = ((uint32_t)(r.q1 >> 56) << 16) | i;  // tag & 0xFF, local index
         } else {
             key[i] = ~0ull;  // padding sorts last
             sec[i] = ~0u;
@@ -1224,7 +1292,7 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
             __syncthreads();
         }
     }
-    return finish_sorted<NT>(in, out, m, res, key, sec, aux, pairs, s_u32, s_bad);
+    return finish_sorted<NT>(in, out, m, rl, key, sec, aux, pairs, s_u32, s_bad);
 }
 
 // Chunk in sorted order in LDS (key = mass bits, sec = tag << 16 | local index):
@@ -1232,9 +1300,9 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
 // 16-bit tag collision by first appearance, write the records in final order
 // (tag field = head flag).  aux: scratch.  Returns this thread's head count.
 template <int NT>
-__device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m,
-                                  const uint8_t* __restrict__ res, const unsigned long long* key, const uint32_t* sec,
-                                  uint32_t* aux, uint16_t* pairs, uint32_t* s_u32, uint32_t* s_bad) {
+__device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const RecLoc& rl,
+                                  const unsigned long long* key, const uint32_t* sec, uint32_t* aux, uint16_t* pairs,
+                                  uint32_t* s_u32, uint32_t* s_bad) {
     if (threadIdx.x == 0) {
         *s_bad = 0;
         s_u32[NT / 64] = 0;  // number of equal (mass, tag) neighbour pairs
@@ -1256,7 +1324,7 @@ __device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ 
     const uint32_t npairs = s_u32[NT / 64];
     for (uint32_t q = threadIdx.x; q < npairs; q += NT) {
         const uint32_t p = pairs[q];
-        if (!seq_equal(res, in[sec[p] & 0xFFFFu], in[sec[p - 1] & 0xFFFFu])) *s_bad = 1;
+        if (!rl.same(in[sec[p] & 0xFFFFu], in[sec[p - 1] & 0xFFFFu])) *s_bad = 1;
     }
     __syncthreads();
     if (*s_bad == 0) {
@@ -1276,7 +1344,7 @@ __device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ 
                 const uint32_t p = p0 + threadIdx.x + k * NT;
                 if (p < m) {
                     uint4 r = rv[k];
-                    r.w = (r.w & 0xFFFFu) | ((aux[p] == p ? 1u : 0u) << 16);  // tag := head (p == 0 always)
+                    r.x = (r.x & ~0xFFu) | (aux[p] == p ? 1u : 0u);  // tag byte := head (p == 0 always)
                     out4[p] = r;
                 }
             }
@@ -1325,7 +1393,7 @@ __device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ 
         const uint32_t i = sec[p] & 0xFFFFu;
         uint32_t lead = i;
         for (uint32_t q = gs; q < p; ++q) {
-            if (seq_equal(res, in[sec[q] & 0xFFFFu], in[i])) {
+            if (rl.same(in[sec[q] & 0xFFFFu], in[i])) {
                 lead = sec[q] & 0xFFFFu;
                 break;
             }
@@ -1342,9 +1410,7 @@ __device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ 
             const uint32_t lq = aux[q] & 0xFFFFu;
             np += (lq < lead) | ((lq == lead) & (q < p));
         }
-        Rec r = in[i];
-        r.tag = lead == i ? 1 : 0;
-        out[np] = r;
+        out[np] = with_head(in[i], lead == i);
         heads += lead == i;
     }
     return heads;
@@ -1423,8 +1489,8 @@ constexpr uint32_t MAX_BIG_RUNS = 64;
 template <int NT, int CAP>
 __global__ void __launch_bounds__(NT)
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
-             const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, uint32_t* __restrict__ big_list,
-             Counters* __restrict__ ctr) {
+             const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
+             uint32_t* __restrict__ big_list, Counters* __restrict__ ctr) {
     static_assert(CAP <= 65535 && CAP % NT == 0, "16-bit local indices");
     static_assert(CAP / (RANK_MAX_RUN + 1) <= MAX_BIG_RUNS, "big-run list");
     constexpr uint32_t NW = NT / 64;
@@ -1449,8 +1515,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
     }
     if (threadIdx.x == 0) s_nbig = 0;
     {
-        // all E loads in flight before the first use (Rec as 4 dwords:
-        // mass lo, mass hi, gstart, len | tag << 16)
+        // all E loads in flight before the first use (Rec as 4 dwords: q0, q1)
         const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in + a);
         uint4 rv[E];
 #pragma unroll
@@ -1462,10 +1527,9 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         for (uint32_t k = 0; k < E; ++k) {
             const uint32_t i = threadIdx.x + k * NT;
             if (i < m) {
-                const double mass = __hiloint2double((int)rv[k].y, (int)rv[k].x);
-                key[i] = dbits(mass);
-                sec[i] = (rv[k].w & 0xFFFF0000u) | i;
-                aux[i] = bin_of(mass, bm);
+                key[i] = u4_q0(rv[k]);                  // mass, tag >> 8
+                sec[i] = ((rv[k].w >> 24) << 16) | i;   // tag & 0xFF, local index
+                aux[i] = bin_of(u4_mass(rv[k]), bm);
             }
         }
     }
@@ -1557,7 +1621,8 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         }
     }
     __syncthreads();
-    const uint32_t h = finish_sorted<NT>(in + a, out + a, m, res, key, sec, aux, perm, s_u32, &s_bad);
+    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
+    const uint32_t h = finish_sorted<NT>(in + a, out + a, m, rl, key, sec, aux, perm, s_u32, &s_bad);
     const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
     if (threadIdx.x == 0) ucount[c] = tot;
 }
@@ -1567,7 +1632,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
 // chunks go on to the global-memory path.
 __global__ void __launch_bounds__(BIG_THREADS)
 k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
-                 const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount,
+                 const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
                  const uint32_t* __restrict__ big_list, uint32_t* __restrict__ giant_list,
                  Counters* __restrict__ ctr) {
     static_assert(BIG_CAP <= 65536, "16-bit local indices");
@@ -1578,6 +1643,7 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
     __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
     __shared__ uint32_t s_bad;
     const uint32_t nbig = ctr->n_big;
+    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {
         const uint32_t c = big_list[j];
         const uint32_t a = chunk_lo[c];
@@ -1586,7 +1652,7 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
             if (threadIdx.x == 0) giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
             continue;
         }
-        const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, res, key, sec, aux, pairs, s_u32,
+        const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, rl, key, sec, aux, pairs, s_u32,
                                                                &s_bad);
         const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
         if (threadIdx.x == 0) ucount[c] = tot;
@@ -1595,20 +1661,20 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
 }
 
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                                 uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t* d_giant_list,
-                                 uint32_t max_blocks, Counters* d_ctr, hipStream_t s) {
+                                 const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list,
+                                 uint32_t* d_giant_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s) {
     if (max_blocks == 0) return hipSuccess;
-    DBI_LAUNCH(k_chunk_sort_big, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res,
+    DBI_LAUNCH(k_chunk_sort_big, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res, d_poff,
                d_ucount, d_big_list, d_giant_list, d_ctr);
     return hipGetLastError();
 }
 
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
-                             uint32_t nchunks, const uint8_t* d_res, uint32_t* d_ucount, uint32_t* d_big_list,
-                             Counters* d_ctr, hipStream_t s) {
+                             uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
+                             uint32_t* d_big_list, Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
-                       d_out, bm, d_chunk_lo, d_res, d_ucount, d_big_list, d_ctr);
+                       d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_ctr);
     return hipGetLastError();
 }
 
@@ -1616,11 +1682,13 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
 // scratch in a global workspace (region [4a, 4a+4m) of each array)
 __global__ void __launch_bounds__(BIG_THREADS)
 k_big_chunks(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
-             const uint8_t* __restrict__ res, uint32_t* __restrict__ ucount, const uint32_t* __restrict__ big_list,
+             const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
+             const uint32_t* __restrict__ big_list,
              unsigned long long* ws_key, uint32_t* ws_k2, Counters* __restrict__ ctr) {
     __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
     __shared__ unsigned long long s_flag;
     const uint32_t nbig = ctr->n_giant;
+    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {
         const uint32_t c = big_list[j];
         const uint32_t a = chunk_lo[c];
@@ -1629,7 +1697,7 @@ k_big_chunks(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* 
         unsigned long long* hsh = key + 2ull * m;
         uint32_t* k2 = ws_k2 + 4ull * a;               // [4a, 4a+2m): idx, [4a+2m, 4a+3m): runs
         uint32_t* k3 = k2 + 2ull * m;
-        const uint32_t h = process_chunk<BIG_THREADS, false>(in + a, const_cast<Rec*>(in + a), out + a, m, res, key,
+        const uint32_t h = process_chunk<BIG_THREADS, false>(in + a, const_cast<Rec*>(in + a), out + a, m, rl, key,
                                                               hsh, k2, k3, s_u32, &s_flag);
         const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
         if (threadIdx.x == 0) ucount[c] = tot;
@@ -1638,10 +1706,11 @@ k_big_chunks(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* 
 }
 
 hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                             uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t max_blocks,
-                             unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr, hipStream_t s) {
+                             const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list,
+                             uint32_t max_blocks, unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr,
+                             hipStream_t s) {
     if (max_blocks == 0) return hipSuccess;
-    DBI_LAUNCH(k_big_chunks, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res,
+    DBI_LAUNCH(k_big_chunks, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res, d_poff,
                        d_ucount, d_big_list, d_ws_key, d_ws_k2, d_ctr);
     return hipGetLastError();
 }
@@ -1649,79 +1718,49 @@ hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chun
 // ---------------------------------------------------------------------------
 // 6. finalize: unique table + occurrence CSR (per chunk)
 // ---------------------------------------------------------------------------
-// ptile[t] = {p, poff[p], poff[p+1], 0} for the protein p holding residue
-// t << PID_TILE_SHIFT (one thread per protein writes the tiles whose first
-// residue it holds; empty proteins none)
-__global__ void k_pid_tiles(const uint32_t* __restrict__ poff, uint32_t n_prot, uint4* __restrict__ ptile) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_prot) return;
-    constexpr uint32_t M = (1u << PID_TILE_SHIFT) - 1;
-    const uint32_t lo = poff[p], hi = poff[p + 1];
-    const uint32_t t_hi = (hi + M) >> PID_TILE_SHIFT;
-    for (uint32_t t = (lo + M) >> PID_TILE_SHIFT; t < t_hi; ++t) ptile[t] = make_uint4(p, lo, hi, 0);
-}
-
-hipError_t launch_pid_tiles(const uint32_t* d_poff, uint32_t n_prot, uint4* d_ptile, hipStream_t s) {
-    if (n_prot == 0) return hipSuccess;
-    DBI_LAUNCH(k_pid_tiles, dim3((n_prot + 255) / 256), dim3(256), 0, s, d_poff, n_prot, d_ptile);
-    return hipGetLastError();
-}
-
 // Per chunk: protein id of every occurrence (occurrence CSR, insertion order
 // inside each unique peptide) and the unique table at the head records.
 // A round covers FIN_ITEMS * FIN_THREADS records, k-major (record
 // t0 + k*NT + tid), so every load/store instruction is coalesced and all loads
-// of a round (records, tile table, protein offsets) are in flight together;
-// unique slots come from per-(k, wave) ballot counts.
+// of a round are in flight together; unique slots come from per-(k, wave)
+// ballot counts.  Protein id, offset and length come out of the record itself.
 constexpr uint32_t FIN_THREADS = 256;
 constexpr uint32_t FIN_ITEMS = 4;  // one round = 1024 records ~ one chunk
 
 __global__ void __launch_bounds__(FIN_THREADS)
 k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
-           const uint32_t* __restrict__ poff, const uint4* __restrict__ ptile, double* __restrict__ umass,
-           uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff, uint32_t* __restrict__ ulen,
-           uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid, int32_t factor,
-           Counters* __restrict__ ctr) {
+           double* __restrict__ umass, uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff,
+           uint32_t* __restrict__ ulen, uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid,
+           int32_t factor, Counters* __restrict__ ctr) {
     constexpr uint32_t NW = FIN_THREADS / 64;
     __shared__ uint32_t wc[FIN_ITEMS * NW];  // heads per (round item k, wave), then exclusive bases
     __shared__ uint32_t s_tot;
     const uint32_t c = blockIdx.x;
     const uint32_t a = chunk_lo[c];
     const uint32_t n = chunk_lo[c + 1] - a;
+    const uint32_t W = rec_width(ctr->max_plen);
     const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(recs + a);
     const uint32_t w = threadIdx.x >> 6;
     uint32_t run = ubase[c];
     uint32_t nkeys = 0;  // heads whose mass key differs from the previous unique's (SQLiteByte rows)
     for (uint32_t t0 = 0; t0 < n; t0 += FIN_THREADS * FIN_ITEMS) {
         uint4 rv[FIN_ITEMS];
-        uint4 pt[FIN_ITEMS];  // {protein, its first residue, one past its last}
         uint32_t lpre[FIN_ITEMS];
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
             const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
-            rv[k] = i < n ? r4[i] : make_uint4(0, 0, 0, 0);  // tag field (w >> 16) = head flag
+            rv[k] = i < n ? r4[i] : make_uint4(0, 0, 0, 0);  // low byte of q0 = head flag
         }
-        // mass of the record before each one (= the previous unique's mass at a head)
+        // mass of the record before each head (= the previous unique's mass)
         double prevm[FIN_ITEMS];
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
             const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
-            prevm[k] = (i < n && a + i > 0 && (rv[k].w >> 16)) ? recs[a + i - 1].mass : 0.0;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < FIN_ITEMS; ++k) pt[k] = ptile[rv[k].z >> PID_TILE_SHIFT];
-        // a protein starts between the tile start and the peptide: next protein
-#pragma unroll
-        for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
-            if (rv[k].z >= pt[k].z) {
-                pt[k].x += 1;
-                pt[k].y = pt[k].z;
-                pt[k].z = poff[pt[k].x + 1];
-            }
+            prevm[k] = (i < n && a + i > 0 && (rv[k].x & 0xFFu)) ? q0_mass(recs[a + i - 1].q0) : 0.0;
         }
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
-            const uint64_t bal = __ballot((rv[k].w >> 16) != 0);
+            const uint64_t bal = __ballot((rv[k].x & 0xFFu) != 0);
             lpre[k] = (uint32_t)__popcll(bal & lanemask_lt());
             if (lane_id() == 0) wc[k * NW + w] = (uint32_t)__popcll(bal);
         }
@@ -1740,21 +1779,17 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
             const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
             if (i < n) {
-                const uint32_t g = rv[k].z;
-                while (pt[k].z <= g) {  // several protein starts in one tile (short/empty proteins)
-                    pt[k].x += 1;
-                    pt[k].y = pt[k].z;
-                    pt[k].z = poff[pt[k].x + 1];
-                }
-                occ_pid[a + i] = pt[k].x;
-                if (rv[k].w >> 16) {
+                const uint64_t q1 = u4_q1(rv[k]);
+                const uint32_t pid = q1_pid(q1, W);
+                occ_pid[a + i] = pid;
+                if (rv[k].x & 0xFFu) {
                     const uint32_t u = run + wc[k * NW + w] + lpre[k];
-                    const double mu = __hiloint2double((int)rv[k].y, (int)rv[k].x);
+                    const double mu = u4_mass(rv[k]);
                     nkeys += (a + i == 0) || java_d2i(mu * (double)factor) != java_d2i(prevm[k] * (double)factor);
                     umass[u] = mu;
-                    upid[u] = pt[k].x;
-                    uoff[u] = g - pt[k].y;
-                    ulen[u] = rv[k].w & 0xFFFFu;
+                    upid[u] = pid;
+                    uoff[u] = q1_off(q1, W);
+                    ulen[u] = q1_len(q1, W);
                     occ_off[u] = a + i;
                 }
             }
@@ -1768,12 +1803,11 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
 }
 
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
-                           const uint32_t* d_poff, const uint4* d_ptile, double* d_umass, uint32_t* d_upid,
-                           uint32_t* d_uoff, uint32_t* d_ulen, uint32_t* d_occ_off, uint32_t* d_occ_pid,
-                           int32_t factor, Counters* d_ctr, hipStream_t s) {
+                           double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
+                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(FIN_THREADS), 0, s, d_recs, d_chunk_lo, d_ubase, d_poff, d_ptile,
-               d_umass, d_upid, d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, d_ctr);
+    DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(FIN_THREADS), 0, s, d_recs, d_chunk_lo, d_ubase, d_umass, d_upid,
+               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, d_ctr);
     return hipGetLastError();
 }
 
@@ -1940,29 +1974,33 @@ hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, c
     return hipGetLastError();
 }
 
-// host-supplied occurrences -> records (DBIndexStore.addSequence path)
+// host-supplied occurrences -> records (DBIndexStore.addSequence path; the
+// host checked 1 <= mass < 65536 and that every occurrence lies in its protein)
 __global__ void k_occ_to_recs(const double* __restrict__ mass, const uint32_t* __restrict__ pid,
                               const uint32_t* __restrict__ off, const uint32_t* __restrict__ len,
                               const uint32_t* __restrict__ poff, const uint8_t* __restrict__ res, uint64_t n,
-                              Rec* __restrict__ out) {
+                              uint64_t n_prot, Rec* __restrict__ out, Counters* __restrict__ ctr) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t W = rec_width(ctr->max_plen);
+    if (i == 0 && !rec_layout_ok(W, n_prot)) atomicOr(&ctr->err, ERR_LAYOUT);
     if (i >= n) return;
-    Rec r;
-    r.mass = mass[i];
-    r.gstart = poff[pid[i]] + off[i];
-    r.len = (uint16_t)len[i];
+    const uint32_t p = pid[i], o = off[i], l = len[i];
+    const uint8_t* __restrict__ g = res + poff[p] + o;
     uint32_t h = FNV32_OFFSET;
-    for (uint32_t k = 0; k < r.len; ++k) h = fnv32_step(h, res[r.gstart + k]);
-    r.tag = fold_tag(h);
+    for (uint32_t k = 0; k < l; ++k) h = fnv32_step(h, g[k]);
+    const uint32_t tag = fold_tag(h);
+    Rec r;
+    r.q0 = rec_q0(mass[i], tag);
+    r.q1 = rec_q1(tag, rec_loc(p, o, W), l);
     out[i] = r;
 }
 
 hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const uint32_t* d_off,
                               const uint32_t* d_len, const uint32_t* d_poff, const uint8_t* d_res, uint64_t n,
-                              Rec* d_out, hipStream_t s) {
+                              uint64_t n_prot, Rec* d_out, Counters* d_ctr, hipStream_t s) {
     if (n == 0) return hipSuccess;
     DBI_LAUNCH(k_occ_to_recs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_mass, d_pid, d_off,
-                       d_len, d_poff, d_res, n, d_out);
+                       d_len, d_poff, d_res, n, n_prot, d_out, d_ctr);
     return hipGetLastError();
 }
 

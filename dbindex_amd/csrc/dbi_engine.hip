@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -90,7 +91,6 @@ struct dbi_handle {
     uint32_t epoch = 0;                 // tag of the current fused launch in `status`
     DevBuf<uint32_t> thr;       // digest per-thread counts
     DevBuf<uint32_t> tile_pf;   // first protein of every digest tile (+1)
-    DevBuf<uint4> ptile;        // {protein, start, end} of every 256th residue (finalize)
     DevBuf<uint32_t> scan_tmp;
     DevBuf<Rec> recA, recB;
     DevBuf<uint32_t> hist;
@@ -144,6 +144,15 @@ int check_params(const dbi_params* p) {
     for (int c = 0; c < 256; ++c)
         if (!(p->mass[c] >= 0.0) || std::isinf(p->mass[c]))
             return set_error(DBI_E_INVALID, "residue masses must be finite and >= 0");
+    return 0;
+}
+
+// every kept mass is >= max(minMH, m0) (residue masses are >= 0): the 16-B
+// record encodes masses in [1, 65536) Da exactly (Rec)
+int check_mass_floor(const dbi_params* p, double m0) {
+    if (!(std::max(p->min_mh, m0) >= 1.0))
+        return set_error(DBI_E_INVALID, "peptide masses below 1 Da are not supported (min precursor mass and "
+                                        "H2O + proton + termini both < 1)");
     return 0;
 }
 
@@ -284,20 +293,21 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
           launch_chunk_bounds(src, n32, bm, CHUNK_T, nchunks, h->chunk_lo.p, s));
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
-          launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->ucount.p, h->big_list.p, h->ctr.p, s));
+          launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->poff.p, h->ucount.p, h->big_list.p,
+                            h->ctr.p, s));
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
-          launch_chunk_sort_big(src, dst, h->chunk_lo.p, h->d_res, h->ucount.p, h->big_list.p, h->giant_list.p,
-                                std::min<uint32_t>(nchunks, 256u), h->ctr.p, s));
+          launch_chunk_sort_big(src, dst, h->chunk_lo.p, h->d_res, h->poff.p, h->ucount.p, h->big_list.p,
+                                h->giant_list.p, std::min<uint32_t>(nchunks, 256u), h->ctr.p, s));
     STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
-          launch_big_chunks(src, dst, h->chunk_lo.p, h->d_res, h->ucount.p, h->giant_list.p,
+          launch_big_chunks(src, dst, h->chunk_lo.p, h->d_res, h->poff.p, h->ucount.p, h->giant_list.p,
                             std::min<uint32_t>(nchunks, 256u), h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
     // unique offsets per chunk
     STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
           launch_scan_u32(h->ucount.p, h->ucount.p, nchunks, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_unique, s));
     // finalize: 16 B record in, 4 B occurrence protein id out, 24 B per unique out
     STAGE(h, "finalize", by(0, 20, 24, 0, 0),
-          launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->poff.p, h->ptile.p, h->umass.p, h->upid.p,
-                          h->uoff.p, h->ulen.p, h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor, h->ctr.p, s));
+          launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p,
+                          h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor, h->ctr.p, s));
     DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s));
     h->stats.n_bins = nbins;
     return 0;
@@ -306,7 +316,9 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
 int finish_build(dbi_handle* h) {
     int rc = read_counters(h);
     if (rc) return rc;
-    if (h->hc.err & ERR_LEN_OVERFLOW) return set_error(DBI_E_INVALID, "peptide longer than 65535 residues");
+    if (h->hc.err & ERR_LAYOUT)
+        return set_error(DBI_E_INVALID, "2 x bits(longest protein) + bits(protein count) exceeds the 56 bits of the "
+                                        "16-B occurrence record: shard the FASTA");
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h->t0).count();
     dbi_stats& st = h->stats;
     st.n_residues = h->n_res;
@@ -331,7 +343,7 @@ int finish_build(dbi_handle* h) {
     }
     size_t bytes = 0;
     bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
-    bytes += h->thr.bytes() + h->tile_pf.bytes() + h->ptile.bytes() + h->chunk_lo.bytes();
+    bytes += h->thr.bytes() + h->tile_pf.bytes() + h->chunk_lo.bytes();
     bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->ucount.bytes();
     bytes += h->big_list.bytes() + h->giant_list.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
     bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes();
@@ -340,15 +352,14 @@ int finish_build(dbi_handle* h) {
     return 0;
 }
 
-// per-tile first-protein table (digest tiles + protein-id lookups in finalize)
+// per-tile first-protein table (digest tiles) + the longest protein (record layout)
 int prepare_tiles(dbi_handle* h) {
     const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
     int rc;
     if ((rc = h->tile_pf.ensure((size_t)ntiles + 2))) return rc;
-    if ((rc = h->ptile.ensure((size_t)(h->n_res >> PID_TILE_SHIFT) + 1))) return rc;
-    STAGE(h, "tile_proteins", by(0, 0, 0, 0, 0),
-          launch_tile_proteins(h->poff.p, (uint32_t)h->n_prot, (uint32_t)h->n_res, h->tile_pf.p, h->stream));
-    STAGE(h, "pid_tiles", by(0.0625, 0, 0, 8, 0), launch_pid_tiles(h->poff.p, (uint32_t)h->n_prot, h->ptile.p, h->stream));
+    STAGE(h, "tile_proteins", by(0, 0, 0, 4, 0),
+          launch_tile_proteins(h->poff.p, (uint32_t)h->n_prot, (uint32_t)h->n_res, h->tile_pf.p, h->ctr.p,
+                               h->stream));
     return 0;
 }
 
@@ -384,7 +395,8 @@ int build_digest(dbi_handle* h) {
             if (n <= cap) break;
             if (attempt > 0) return set_error(DBI_E_STATE, "digest output grew between identical passes");
             if ((rc = h->recA.ensure(n + n / 8))) return rc;
-            DBI_HIP(hipMemsetAsync(h->ctr.p, 0, sizeof(Counters), s));
+            // counters back to zero, except the record layout (max_plen) set by prepare_tiles
+            DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
         }
     } else {
         // cold: count, scan, size the output, emit
@@ -523,6 +535,7 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     *out = nullptr;
     int rc = check_params(params);
     if (rc) return rc;
+    if ((rc = check_mass_floor(params, make_dev_params(*params).m0))) return rc;
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev == 0) return set_error(DBI_E_HIP, "no HIP device available");
@@ -561,7 +574,7 @@ void dbi_close(dbi_handle* h) {
     h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
     h->res.release(); h->poff64.release(); h->poff.release(); h->blk.release(); h->scan_tmp.release();
     h->status.release();
-    h->thr.release(); h->tile_pf.release(); h->ptile.release(); h->chunk_lo.release();
+    h->thr.release(); h->tile_pf.release(); h->chunk_lo.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
     h->big_list.release(); h->giant_list.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
     h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release();
@@ -617,10 +630,11 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
     if (n_occ >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "too many occurrences for one device");
     double lo = 0, hi = 0;
     for (uint64_t i = 0; i < n_occ; ++i) {
-        if (!(mass[i] >= 0.0) || std::isinf(mass[i])) return set_error(DBI_E_INVALID, "occurrence mass must be finite and >= 0");
+        if (!(mass[i] >= 1.0 && mass[i] < 65536.0))
+            return set_error(DBI_E_INVALID, "occurrence mass must be in [1, 65536) Da");
         if (prot_id[i] >= n_prot) return set_error(DBI_E_INVALID, "occurrence protein id out of range");
         const uint64_t plen = prot_off[prot_id[i] + 1] - prot_off[prot_id[i]];
-        if ((uint64_t)offset[i] + length[i] > plen || length[i] == 0 || length[i] > 0xFFFFu)
+        if ((uint64_t)offset[i] + length[i] > plen || length[i] == 0)
             return set_error(DBI_E_INVALID, "occurrence offset/length outside its protein");
         if (i == 0 || mass[i] < lo) lo = mass[i];
         if (i == 0 || mass[i] > hi) hi = mass[i];
@@ -636,15 +650,14 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
         DBI_HIP(hipMemcpyAsync(h->o_off.p, offset, 4 * n_occ, hipMemcpyHostToDevice, h->stream));
         DBI_HIP(hipMemcpyAsync(h->o_len.p, length, 4 * n_occ, hipMemcpyHostToDevice, h->stream));
     }
-    DBI_HIP(launch_occ_to_recs(h->o_mass.p, h->o_pid.p, h->o_off.p, h->o_len.p, h->poff.p, h->d_res, n_occ, h->recA.p,
-                               h->stream));
+    if ((rc = prepare_tiles(h))) return rc;  // record layout first
+    DBI_HIP(launch_occ_to_recs(h->o_mass.p, h->o_pid.p, h->o_off.p, h->o_len.p, h->poff.p, h->d_res, n_occ, n_prot,
+                               h->recA.p, h->ctr.p, h->stream));
     // n_kept known on the host: seed the device counter
-    Counters c0{};
-    c0.n_kept = n_occ;
-    DBI_HIP(hipMemcpyAsync(h->ctr.p, &c0, sizeof(Counters), hipMemcpyHostToDevice, h->stream));
+    const unsigned long long kept = n_occ;
+    DBI_HIP(hipMemcpyAsync(&h->ctr.p->n_kept, &kept, sizeof(kept), hipMemcpyHostToDevice, h->stream));
     DBI_HIP(hipStreamSynchronize(h->stream));
     h->n_total_extra = n_dropped_extra;
-    if ((rc = prepare_tiles(h))) return rc;
     if ((rc = build_tail(h, n_occ, lo, hi))) return rc;
     return finish_build(h);
 }

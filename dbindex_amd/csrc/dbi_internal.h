@@ -12,19 +12,61 @@
 
 namespace dbi {
 
-// Occurrence record as it moves through the build: 16 B, HBM-aligned.
-//   mass   : MH+ (fp64, bit-identical to the reference's sequential sum)
-//   gstart : global residue position of the first residue (protein offset + start)
-//   len    : peptide length (curSeqI, DBIndexer.java:309,388)
-//   tag    : digest -> chunk sort: peptide_tag() of the string (tie-break key);
-//            chunk sort -> finalize: 1 = first occurrence of its unique peptide
+// Occurrence record as it moves through the build: 16 B, two u64 words.
+//   q0 = enc(mass) << 8 | tag >> 8
+//   q1 = (tag & 0xFF) << 56 | pid << 2W | off << W | len
+// enc(m) = bits(m) - bits(1.0): exact and order-preserving for 1 <= m < 65536
+// Da (every kept mass: >= max(minMH, m0) >= 1 is checked at dbi_open, and
+// < NUM_BUCKETS * BUCKET_MASS_RANGE <= 8000).  W = bits(longest protein), read
+// by every kernel from Counters::max_plen, so off < plen and len <= plen
+// always fit; pid gets 56 - 2W bits (ERR_LAYOUT otherwise).  Ordering records
+// by q0 then (q1 >> 56) is ordering by (mass, peptide tag); pid/off locate
+// the occurrence directly, so nothing downstream looks proteins up.
+//   tag : digest -> chunk sort: peptide_tag() of the string (tie-break key);
+//         chunk sort -> finalize: the low byte of q0 = 1 for the first
+//         occurrence of its unique peptide, else 0
 struct alignas(16) Rec {
-    double mass;
-    uint32_t gstart;
-    uint16_t len;
-    uint16_t tag;
+    uint64_t q0;
+    uint64_t q1;
 };
 static_assert(sizeof(Rec) == 16, "Rec must be 16 bytes");
+
+constexpr uint64_t MASS_BIAS = 0x3FF0000000000000ull;  // bits(1.0)
+__host__ __device__ inline uint64_t rec_q0(double m, uint32_t tag) {
+    uint64_t b;
+    __builtin_memcpy(&b, &m, 8);
+    return ((b - MASS_BIAS) << 8) | (tag >> 8);
+}
+__host__ __device__ inline double q0_mass(uint64_t q0) {
+    const uint64_t b = (q0 >> 8) + MASS_BIAS;
+    double m;
+    __builtin_memcpy(&m, &b, 8);
+    return m;
+}
+// pid << 2W | off << W (the per-start part of q1)
+__host__ __device__ inline uint64_t rec_loc(uint32_t pid, uint32_t off, uint32_t w) {
+    return ((uint64_t)pid << (2 * w)) | ((uint64_t)off << w);
+}
+__host__ __device__ inline uint64_t rec_q1(uint32_t tag, uint64_t loc, uint32_t len) {
+    return ((uint64_t)(tag & 0xFFu) << 56) | loc | len;
+}
+__host__ __device__ inline uint32_t q1_len(uint64_t q1, uint32_t w) { return (uint32_t)(q1 & ((1ull << w) - 1)); }
+__host__ __device__ inline uint32_t q1_off(uint64_t q1, uint32_t w) {
+    return (uint32_t)((q1 >> w) & ((1ull << w) - 1));
+}
+__host__ __device__ inline uint32_t q1_pid(uint64_t q1, uint32_t w) {
+    return (uint32_t)((q1 >> (2 * w)) & ((1ull << (56 - 2 * w)) - 1));
+}
+// field width W from the longest protein (>= 1)
+__host__ __device__ inline uint32_t rec_width(uint32_t max_plen) {
+    uint32_t w = 1;
+    while (w < 32 && (max_plen >> w) != 0) ++w;
+    return w;
+}
+// pid of every protein fits in 56 - 2W bits
+__host__ __device__ inline bool rec_layout_ok(uint32_t w, uint64_t n_prot) {
+    return 2 * w < 56 && (n_prot == 0 || ((n_prot - 1) >> (56 - 2 * w)) == 0);
+}
 
 // Pinned order of different peptides with bit-identical mass:
 // (16-bit tag, first appearance), tag = 32-bit FNV-1a of the residue string
@@ -69,8 +111,11 @@ struct Counters {
     unsigned int err;              // device error bits
     unsigned int n_giant;          // chunks above BIG_CAP (global-memory path)
     unsigned int tile_ticket;      // k_digest_fused: tiles in dispatch order
+    // read by every block of every kernel: its own cache line, away from the
+    // atomics above (sharing the tile ticket's line cost the digest 30%)
+    alignas(256) unsigned int max_plen;  // longest protein (k_tile_proteins): the record field width
 };
-constexpr unsigned ERR_LEN_OVERFLOW = 1;  // peptide longer than 65535 residues
+constexpr unsigned ERR_LAYOUT = 1;  // 2*bits(longest protein) + bits(proteins) > 56
 
 // Tunables
 constexpr int DIGEST_THREADS = 256;
@@ -83,14 +128,15 @@ constexpr int CHUNK_THREADS = 512;
 constexpr int CHUNK_CAP = 2048;     // records per chunk sorted in LDS
 constexpr int CHUNK_T = 1024;       // target chunk size (whole mass bins, ~T..T+maxbin)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
-constexpr int PID_TILE_SHIFT = 8;   // finalize's residue -> protein table: one entry per 256 residues
 constexpr int BIG_THREADS = 1024;
 constexpr int BIG_CAP = 8192;       // records per oversize chunk sorted in LDS (1 block per CU)
 
 // ---- launchers (dbi_device.hip) -------------------------------------------------
 // All return hipError_t of the launch.
+// tile_pf[t] = protein holding residue min(t*DIGEST_TILE, R-1); ctr->max_plen
+// = longest protein (the record field width, see Rec)
 hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res, uint32_t* d_tile_pf,
-                                hipStream_t s);
+                                Counters* d_ctr, hipStream_t s);
 hipError_t launch_digest_count(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
                                uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr,
@@ -127,23 +173,19 @@ size_t radix_hist_elems(uint32_t n, int bits);
 hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,
                                uint32_t* d_chunk_lo, hipStream_t s);
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
-                             uint32_t nchunks, const uint8_t* d_res, uint32_t* d_ucount, uint32_t* d_big_list,
-                             Counters* d_ctr, hipStream_t s);
+                             uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
+                             uint32_t* d_big_list, Counters* d_ctr, hipStream_t s);
 // chunks of (CHUNK_CAP, BIG_CAP] records listed in d_big_list: LDS bitonic, 1024 threads
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                                 uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t* d_giant_list,
+                                 const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t* d_giant_list,
                                  uint32_t max_blocks, Counters* d_ctr, hipStream_t s);
 // chunks above BIG_CAP listed in d_giant_list: global-memory scratch
 hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                             uint32_t* d_ucount, const uint32_t* d_giant_list, uint32_t max_blocks,
+                             const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_giant_list, uint32_t max_blocks,
                              unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr, hipStream_t s);
-// ptile[t] = {p, poff[p], poff[p+1], 0}, p = protein holding residue t << PID_TILE_SHIFT
-// ((R >> PID_TILE_SHIFT) + 1 entries)
-hipError_t launch_pid_tiles(const uint32_t* d_poff, uint32_t n_prot, uint4* d_ptile, hipStream_t s);
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
-                           const uint32_t* d_poff, const uint4* d_ptile, double* d_umass, uint32_t* d_upid,
-                           uint32_t* d_uoff, uint32_t* d_ulen, uint32_t* d_occ_off, uint32_t* d_occ_pid,
-                           int32_t factor, Counters* d_ctr, hipStream_t s);
+                           double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
+                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, Counters* d_ctr, hipStream_t s);
 hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t factor, uint32_t* d_flags,
                             hipStream_t s);
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s);
@@ -160,7 +202,7 @@ hipError_t launch_key_range(const double* d_umass, uint32_t n_unique, int32_t fa
                             int32_t khi, uint64_t* d_out2, hipStream_t s);
 hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const uint32_t* d_off,
                               const uint32_t* d_len, const uint32_t* d_poff, const uint8_t* d_res, uint64_t n,
-                              Rec* d_out, hipStream_t s);
+                              uint64_t n_prot, Rec* d_out, Counters* d_ctr, hipStream_t s);
 hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s);
 hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
                              uint64_t nq, uint64_t* d_ids, hipStream_t s);

@@ -22,17 +22,18 @@ import sys
 # rocprof kernel name prefix -> bench/engine stage name
 STAGES = [
     ("dbi::k_tile_proteins", "tile_proteins"),
+    ("void dbi::k_digest_fused<", "digest"),
+    ("dbi::k_digest_count_cuts", "digest_count"),
     ("void dbi::k_digest<false", "digest_count"),
     ("void dbi::k_digest<true", "digest_emit"),
     ("dbi::k_radix_hist", "radix_hist"),
     ("dbi::k_radix_scatter", "radix_scatter"),
-    ("dbi::k_bin_bounds", "bin_bounds"),
     ("dbi::k_chunk_bounds", "chunk_bounds"),
     ("void dbi::k_chunk_sort<", "chunk_sort"),
     ("dbi::k_chunk_sort_big", "chunk_sort_big"),
     ("dbi::k_big_chunks", "chunk_sort_giant"),
     ("dbi::k_finalize", "finalize"),
-    ("dbi::k_count_keys", "count_keys"),
+    ("dbi::k_key_flags", "key_flags"),
     ("dbi::k_write_tail", "write_tail"),
     ("dbi::k_scan", "scan"),
     ("dbi::k_off64_to_32", "off64_to_32"),
