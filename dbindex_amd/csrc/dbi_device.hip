@@ -673,6 +673,42 @@ __device__ __forceinline__ unsigned long long st_pack(uint32_t epoch, unsigned l
     return ((unsigned long long)epoch << 48) | (state << 46) | v;
 }
 
+// Wave 0 of tile `tile`: publish the tile's total, look back 64 tiles at a
+// time for the exclusive prefix (returned to every lane), publish the
+// inclusive prefix.
+__device__ unsigned long long tile_lookback(unsigned long long* __restrict__ status, uint32_t tile, uint32_t epoch,
+                                            unsigned long long total) {
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&status[tile], st_pack(epoch, tile == 0 ? ST_PREFIX : ST_AGG, total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long excl = 0;
+    int64_t t = (int64_t)tile - 1;
+    const uint32_t lane = lane_id();
+    while (t >= 0) {
+        const int64_t q = t - (int64_t)lane;
+        unsigned long long v = 0;
+        bool ready = true;
+        if (q >= 0) {
+            v = __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ready = (uint32_t)(v >> 48) == epoch && ((v >> 46) & 3ull) != 0;
+        }
+        const uint64_t pref = __ballot(q >= 0 && ready && ((v >> 46) & 3ull) == ST_PREFIX);
+        const uint64_t notready = __ballot(!ready);
+        // lanes up to (and including) the nearest prefix, all ready -> sum them
+        const uint32_t upto = pref ? (uint32_t)__ffsll((long long)pref) - 1 : 64u;  // nearest prefix lane
+        const uint64_t need = upto >= 63 ? ~0ull : ((2ull << upto) - 1);
+        if (notready & need) continue;  // a predecessor has not published yet: poll again
+        const unsigned long long val = (lane <= upto && q >= 0) ? (v & ((1ull << 46) - 1)) : 0ull;
+        excl += wave_sum(val);
+        if (pref) break;
+        t -= 64;
+    }
+    if (threadIdx.x == 0 && tile != 0)
+        __hip_atomic_store(&status[tile], st_pack(epoch, ST_PREFIX, excl + total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 template <bool SEMI, bool MAND>
 __global__ void __launch_bounds__(DIGEST_THREADS)
 k_digest_fused(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
@@ -702,38 +738,9 @@ k_digest_fused(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_
     const uint32_t mine = block_excl_scan<DIGEST_THREADS, uint32_t>(kept, sm.tmp, total);
     const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
     if (threadIdx.x < 64) {
-        // wave 0: publish, then look back 64 tiles at a time
+        const unsigned long long excl = tile_lookback(status, tile, epoch, total);
         if (threadIdx.x == 0) {
             if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
-            __hip_atomic_store(&status[tile], st_pack(epoch, tile == 0 ? ST_PREFIX : ST_AGG, total),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        unsigned long long excl = 0;
-        int64_t t = (int64_t)tile - 1;
-        const uint32_t lane = lane_id();
-        while (t >= 0) {
-            const int64_t q = t - (int64_t)lane;
-            unsigned long long v = 0;
-            bool ready = true;
-            if (q >= 0) {
-                v = __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ready = (uint32_t)(v >> 48) == epoch && ((v >> 46) & 3ull) != 0;
-            }
-            const uint64_t pref = __ballot(q >= 0 && ready && ((v >> 46) & 3ull) == ST_PREFIX);
-            const uint64_t notready = __ballot(!ready);
-            // lanes up to (and including) the nearest prefix, all ready -> sum them
-            const uint32_t upto = pref ? (uint32_t)__ffsll((long long)pref) - 1 : 64u;  // nearest prefix lane
-            const uint64_t need = upto >= 63 ? ~0ull : ((2ull << upto) - 1);
-            if (notready & need) continue;  // a predecessor has not published yet: poll again
-            const unsigned long long val = (lane <= upto && q >= 0) ? (v & ((1ull << 46) - 1)) : 0ull;
-            excl += wave_sum(val);
-            if (pref) break;
-            t -= 64;
-        }
-        if (threadIdx.x == 0) {
-            if (tile != 0)
-                __hip_atomic_store(&status[tile], st_pack(epoch, ST_PREFIX, excl + total), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
             if (tile == gridDim.x - 1) d_ctr->n_kept = excl + total;
             s_base = excl;
         }
@@ -763,6 +770,67 @@ hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, co
         if (dp.mand_mode) DBI_FUSED(false, true); else DBI_FUSED(false, false);
     }
 #undef DBI_FUSED
+    return hipGetLastError();
+}
+
+// One walk per start (see launch_digest_bounded): reservation look-back right
+// after compaction, then emit into the thread's own slots.
+__global__ void __launch_bounds__(DIGEST_THREADS)
+k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
+                 const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
+                 uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, unsigned long long* __restrict__ status,
+                 uint32_t epoch, Rec* __restrict__ d_out, uint64_t cap, Counters* __restrict__ d_ctr) {
+    __shared__ DigestSmem sm;
+    __shared__ uint32_t s_tile;
+    __shared__ unsigned long long s_base;
+    if (threadIdx.x == 0) s_tile = atomicAdd(&d_ctr->tile_ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    TileCtx tc;
+    const uint32_t ncand = digest_prepare<false>(sm, tc, tile, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
+                                                 d_tile_pf);
+    const uint32_t B = (uint32_t)dp.max_missed + 2u;  // records per start, at most
+    if (threadIdx.x < 64) {
+        const unsigned long long excl = tile_lookback(status, tile, epoch, (unsigned long long)ncand * B);
+        if (threadIdx.x == 0) {
+            if (tile == gridDim.x - 1) d_ctr->n_slots = excl + (unsigned long long)ncand * B;
+            s_base = excl;
+        }
+    }
+    __syncthreads();
+    const unsigned long long base = s_base;
+    if (base + (unsigned long long)ncand * B > cap) return;  // too small: the caller grows it and runs again
+    tc.w = rec_width(d_ctr->max_plen);
+    if (tile == 0 && threadIdx.x == 0 && !rec_layout_ok(tc.w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
+    uint32_t jb, je;
+    thread_share(ncand, jb, je);
+    Rec* __restrict__ o = d_out + base + (unsigned long long)jb * B;
+    const uint32_t lim = (je - jb) * B;
+    uint32_t kept = 0, dropped = 0;
+    for (uint32_t j = jb; j < je; ++j) {
+        const WalkOut w = walk_candidate<true, false, false>(dp, sm, tc, d_res, d_poff, j, o + kept, o + lim);
+        kept += w.kept;
+        dropped += w.dropped;
+    }
+    const Rec sent{REC_SENTINEL, REC_SENTINEL};
+    for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
+    const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
+    const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
+    if (threadIdx.x == 0) {
+        if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
+        if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
+    }
+}
+
+hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                                 const uint32_t* d_tile_pf, unsigned long long* d_status, uint32_t epoch,
+                                 Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s) {
+    const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
+    if (nblk == 0) return hipSuccess;
+    if (dp.semi || dp.mand_mode) return hipErrorInvalidValue;
+    DBI_LAUNCH(k_digest_bounded, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res, d_poff,
+               n_prot, n_res, d_tile_pf, d_status, epoch, d_out, cap, d_ctr);
     return hipGetLastError();
 }
 
@@ -921,6 +989,7 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits
 // +RADIX_ITEMS*64), item k = lanes' records k*64 + lane: per-wave digit counts
 // accumulate in input order, so ranks are stable with no block barrier inside
 // the item loop.
+template <bool SPARSE>
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int bits,
              uint32_t* __restrict__ hist) {
@@ -930,18 +999,19 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int b
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
     wave_sync();
     const uint32_t base = blockIdx.x * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
-    double mv[RADIX_ITEMS];
+    uint64_t qv[RADIX_ITEMS];
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
-        mv[k] = i < n ? q0_mass(in[i].q0) : 0.0;
+        qv[k] = i < n ? in[i].q0 : REC_SENTINEL;
     }
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
-        const uint32_t d = (bin_of(mv[k], bm) >> shift) & mask;
-        const uint64_t peers = digit_peers(d, i < n, bits);
-        if (i < n && __popcll(peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
+        const bool valid = i < n && (!SPARSE || qv[k] != REC_SENTINEL);
+        const uint32_t d = (bin_of(q0_mass(qv[k]), bm) >> shift) & mask;
+        const uint64_t peers = digit_peers(d, valid, bits);
+        if (valid && __popcll(peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
         wave_sync();
     }
     __syncthreads();
@@ -953,6 +1023,7 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int b
     }
 }
 
+template <bool SPARSE>
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, BinMap bm, int shift,
                 int bits, const uint32_t* __restrict__ offs) {
@@ -971,15 +1042,18 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, B
     }
     // rank of every record among the wave's earlier records of its digit
     uint32_t dg[RADIX_ITEMS], pos[RADIX_ITEMS];
+    uint32_t vmask = 0;
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
+        const bool valid = i < n && (!SPARSE || (rv[k].x & rv[k].y) != 0xFFFFFFFFu);
+        vmask |= (uint32_t)valid << k;
         const uint32_t d = (bin_of(u4_mass(rv[k]), bm) >> shift) & mask;
-        const uint64_t peers = digit_peers(d, i < n, bits);
+        const uint64_t peers = digit_peers(d, valid, bits);
         const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t before = cnt[w][d];
         wave_sync();
-        if (i < n && rank == 0) cnt[w][d] = before + (uint32_t)__popcll(peers);
+        if (valid && rank == 0) cnt[w][d] = before + (uint32_t)__popcll(peers);
         wave_sync();
         dg[k] = d;
         pos[k] = before + rank;
@@ -998,26 +1072,31 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, B
     __syncthreads();
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
 #pragma unroll
-    for (int k = 0; k < RADIX_ITEMS; ++k) {
-        const uint32_t i = base + k * 64 + lane;
-        if (i < n) out4[cnt[w][dg[k]] + pos[k]] = rv[k];
-    }
+    for (int k = 0; k < RADIX_ITEMS; ++k)
+        if (vmask & (1u << k)) out4[cnt[w][dg[k]] + pos[k]] = rv[k];
 }
 
-hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, uint32_t* d_hist,
-                             hipStream_t s) {
+hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,
+                             uint32_t* d_hist, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
-    DBI_LAUNCH(k_radix_hist, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, bm, shift, bits, d_hist);
+    if (sparse)
+        DBI_LAUNCH(k_radix_hist<true>, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, bm, shift, bits, d_hist);
+    else
+        DBI_LAUNCH(k_radix_hist<false>, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, bm, shift, bits, d_hist);
     return hipGetLastError();
 }
 
 hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
-                                const uint32_t* d_hist, hipStream_t s) {
+                                bool sparse, const uint32_t* d_hist, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
-    DBI_LAUNCH(k_radix_scatter, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, bm, shift, bits,
-                       d_hist);
+    if (sparse)
+        DBI_LAUNCH(k_radix_scatter<true>, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, bm, shift, bits,
+                   d_hist);
+    else
+        DBI_LAUNCH(k_radix_scatter<false>, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, bm, shift, bits,
+                   d_hist);
     return hipGetLastError();
 }
 
@@ -1112,50 +1191,47 @@ __device__ void bitonic_sort3(unsigned long long* key, unsigned long long* hsh, 
     }
 }
 
-// One chunk of n records (in: global, insertion order inside every bin).
-// Sorted order = (mass, FNV-1a hash of the string, insertion idx); equal
-// (mass, hash) neighbours are string-verified; a true 64-bit collision falls
-// back to grouping equal-(mass, hash) runs by first appearance.
-// STAGE: copy the records into rec[] (LDS) first; otherwise rec == in (global).
+// One chunk of n records above the LDS capacity, scratch in global memory.
+// Sorted order = the record key (q0, q1) = (mass, tag, first appearance);
+// equal (mass, tag) neighbours are string-verified; a 16-bit tag collision
+// regroups its run by string, strings in first-appearance order.
 // key/hsh/k2/k3 are P2-sized scratch; s_u32 >= NT/64+1 slots.
-template <int NT, bool STAGE>
-__device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __restrict__ out, uint32_t n,
-                                  const RecLoc& rl, unsigned long long* key, unsigned long long* hsh,
-                                  uint32_t* k2, uint32_t* k3, uint32_t* s_u32, unsigned long long* s_flag) {
+template <int NT>
+__device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, const RecLoc& rl,
+                                  unsigned long long* key, unsigned long long* hsh, uint32_t* k2, uint32_t* k3,
+                                  uint32_t* s_u32, unsigned long long* s_flag) {
     uint32_t P2 = 1;
     while (P2 < n) P2 <<= 1;
     for (uint32_t i = threadIdx.x; i < P2; i += NT) {
         if (i < n) {
             const Rec r = in[i];
-            if (STAGE) rec[i] = r;
-            key[i] = r.q0;        // mass, tag >> 8
-            hsh[i] = r.q1 >> 56;  // tag & 0xFF
+            key[i] = r.q0;
+            hsh[i] = r.q1;
         } else {
             key[i] = ~0ull;  // padding sorts last
             hsh[i] = ~0ull;
         }
-        k2[i] = i;  // local idx = insertion order
+        k2[i] = i;
     }
     if (threadIdx.x == 0) *s_flag = 0;
     __syncthreads();
     bitonic_sort3<NT>(key, hsh, k2, P2);
+    auto same_tag = [&](uint32_t i) { return key[i] == key[i - 1] && (hsh[i] >> 56) == (hsh[i - 1] >> 56); };
+    auto rec_at = [&](uint32_t i) { return Rec{key[i], hsh[i]}; };
 
-    // verify equal (mass, hash) neighbours are the same string
-    for (uint32_t i = threadIdx.x + 1; i < n; i += NT) {
-        if (key[i] == key[i - 1] && hsh[i] == hsh[i - 1]) {
-            if (!rl.same(rec[k2[i]], rec[k2[i - 1]])) atomicOr(s_flag, 1ull);
-        }
-    }
+    for (uint32_t i = threadIdx.x + 1; i < n; i += NT)
+        if (same_tag(i) && !rl.same(rec_at(i), rec_at(i - 1))) atomicOr(s_flag, 1ull);
     __syncthreads();
-    if (*s_flag != 0) {
-        // k3[i] = first position of the equal-(mass, hash) run containing i
+    const bool regroup = *s_flag != 0;
+    if (regroup) {
+        // k3[i] = first position of the equal-(mass, tag) run containing i
         // (block max-scan of head positions; thread t owns [t*E, t*E+E))
         const uint32_t E = (n + NT - 1) / NT;
         const uint32_t lo = min(threadIdx.x * E, n), hi = min(lo + E, n);
         uint32_t last = 0;
         bool has = false;
         for (uint32_t i = lo; i < hi; ++i) {
-            if (i == 0 || key[i] != key[i - 1] || hsh[i] != hsh[i - 1]) { last = i; has = true; }
+            if (i == 0 || !same_tag(i)) { last = i; has = true; }
             k3[i] = last;
         }
         const int w = threadIdx.x >> 6;
@@ -1180,36 +1256,32 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* rec, Rec* __r
         if (lane_id() == 0) excl = 0;
         excl = max(excl, s_u32[w]);
         for (uint32_t i = lo; i < hi; ++i) {
-            if (i == 0 || key[i] != key[i - 1] || hsh[i] != hsh[i - 1]) break;
+            if (i == 0 || !same_tag(i)) break;
             k3[i] = excl;
         }
         __syncthreads();
-        // leader = smallest-idx element of the run with the same string; re-key
-        // as (run start, leader, idx) and sort again
+        // leader = first position of i's string in its run (positions in a run
+        // follow first appearance; runs are disjoint ascending ranges, so the
+        // leader position alone orders runs, then strings inside a run)
         for (uint32_t i = threadIdx.x; i < n; i += NT) {
             const uint32_t rs = k3[i];
-            uint32_t leader = k2[rs];
-            if (rs != i) {
-                const Rec me = rec[k2[i]];
-                if (!rl.same(me, rec[k2[rs]])) {
-                    leader = k2[i];
-                    for (uint32_t r = rs + 1; r < i; ++r)
-                        if (rl.same(me, rec[k2[r]])) { leader = k2[r]; break; }
-                }
-            }
-            // nobody reads key/hsh any more in this phase: re-key in place
-            hsh[i] = ((unsigned long long)rs << 32) | leader;
-            key[i] = 0;
+            uint32_t leader = i;
+            const Rec me = rec_at(i);
+            for (uint32_t r = rs; r < i; ++r)
+                if (rl.same(me, rec_at(r))) { leader = r; break; }
+            k3[i] = leader;
         }
         __syncthreads();
-        bitonic_sort3<NT>(key, hsh, k2, P2);  // -> (run start, leader, idx); padding keeps ~0
+        for (uint32_t i = threadIdx.x; i < n; i += NT) key[i] = k3[i];
+        __syncthreads();
+        bitonic_sort3<NT>(key, hsh, k2, P2);  // -> (leader, occurrence); padding keeps ~0
     }
 
     // unique-peptide heads + write the chunk in final order
     uint32_t myheads = 0;
     for (uint32_t i = threadIdx.x; i < n; i += NT) {
-        const bool head = (i == 0) || key[i] != key[i - 1] || hsh[i] != hsh[i - 1];
-        out[i] = with_head(rec[k2[i]], head);
+        const bool head = (i == 0) || (regroup ? key[i] != key[i - 1] : !same_tag(i));
+        out[i] = with_head(in[k2[i]], head);
         myheads += head;
     }
     return myheads;
@@ -1250,186 +1322,25 @@ hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, 
     return hipGetLastError();
 }
 
-template <int NT>
-__device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const RecLoc& rl,
-                                  const unsigned long long* key, const uint32_t* sec, uint32_t* aux, uint16_t* pairs,
-                                  uint32_t* s_u32, uint32_t* s_bad);
-
-// One chunk of m <= CAP records sorted in LDS by (mass bits, tag, local index)
-// with a bitonic network (cost independent of how the masses cluster), then
-// unique heads flagged as in k_chunk_sort.  key/sec/aux: CAP entries each.
-// Returns this thread's head count.
-template <int NT, int CAP>
-__device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m,
-                                  const RecLoc& rl, unsigned long long* key, uint32_t* sec,
-                                  uint32_t* aux, uint16_t* pairs, uint32_t* s_u32, uint32_t* s_bad) {
-    uint32_t P2 = 2;
-    while (P2 < m) P2 <<= 1;
-    for (uint32_t i = threadIdx.x; i < P2; i += NT) {
-        if (i < m) {
-            const Rec r = in[i];
-            key[i] = r.q0;                                 // mass, tag >> 8
-            sec[i] = ((uint32_t)(r.q1 >> 56) << 16) | i;  // tag & 0xFF, local index
-        } else {
-            key[i] = ~0ull;  // padding sorts last
-            sec[i] = ~0u;
-        }
-    }
-    __syncthreads();
-    for (uint32_t k = 2; k <= P2; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < (P2 >> 1); t += NT) {
-                const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
-                const uint32_t l = i | j;
-                const unsigned long long ki = key[i], kl = key[l];
-                const uint32_t si = sec[i], sl = sec[l];
-                const bool gt = (ki > kl) | ((ki == kl) & (si > sl));
-                if (gt == ((i & k) == 0)) {
-                    key[i] = kl; key[l] = ki;
-                    sec[i] = sl; sec[l] = si;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    return finish_sorted<NT>(in, out, m, rl, key, sec, aux, pairs, s_u32, s_bad);
+// ---- LDS chunk sort over 128-bit keys (k0, k1) = (q0, q1) --------------------
+__device__ __forceinline__ bool key_lt(unsigned long long a0, unsigned long long a1, unsigned long long b0,
+                                       unsigned long long b1) {
+    return (a0 < b0) | ((a0 == b0) & (a1 < b1));
 }
 
-// Chunk in sorted order in LDS (key = mass bits, sec = tag << 16 | local index):
-// flag unique heads, string-verify equal (mass, tag) neighbours, regroup a
-// 16-bit tag collision by first appearance, write the records in final order
-// (tag field = head flag).  aux: scratch.  Returns this thread's head count.
-template <int NT>
-__device__ uint32_t finish_sorted(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const RecLoc& rl,
-                                  const unsigned long long* key, const uint32_t* sec, uint32_t* aux, uint16_t* pairs,
-                                  uint32_t* s_u32, uint32_t* s_bad) {
-    if (threadIdx.x == 0) {
-        *s_bad = 0;
-        s_u32[NT / 64] = 0;  // number of equal (mass, tag) neighbour pairs
-    }
-    __syncthreads();
-    uint32_t heads = 0;
-    for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        bool head = true;
-        if (p > 0 && key[p] == key[p - 1] && (sec[p] >> 16) == (sec[p - 1] >> 16)) {
-            head = false;
-            pairs[atomicAdd(&s_u32[NT / 64], 1u)] = (uint16_t)p;
-        }
-        aux[p] = head ? p : 0u;
-        heads += head;
-    }
-    __syncthreads();
-    // string-verify every pair in one parallel round (each check is a chain
-    // of HBM loads: never serialise them per thread)
-    const uint32_t npairs = s_u32[NT / 64];
-    for (uint32_t q = threadIdx.x; q < npairs; q += NT) {
-        const uint32_t p = pairs[q];
-        if (!rl.same(in[sec[p] & 0xFFFFu], in[sec[p - 1] & 0xFFFFu])) *s_bad = 1;
-    }
-    __syncthreads();
-    if (*s_bad == 0) {
-        // records in final order; OUT_BATCH gathers in flight per thread
-        constexpr uint32_t OUT_BATCH = 8;
-        const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
-        uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
-        for (uint32_t p0 = 0; p0 < m; p0 += OUT_BATCH * NT) {
-            uint4 rv[OUT_BATCH];
-#pragma unroll
-            for (uint32_t k = 0; k < OUT_BATCH; ++k) {
-                const uint32_t p = p0 + threadIdx.x + k * NT;
-                rv[k] = p < m ? in4[sec[p] & 0xFFFFu] : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < OUT_BATCH; ++k) {
-                const uint32_t p = p0 + threadIdx.x + k * NT;
-                if (p < m) {
-                    uint4 r = rv[k];
-                    r.x = (r.x & ~0xFFu) | (aux[p] == p ? 1u : 0u);  // tag byte := head (p == 0 always)
-                    out4[p] = r;
-                }
-            }
-        }
-        return heads;
-    }
-    // 16-bit tag collision (rare, block-uniform): group start gs(p) = max head
-    // position <= p (block max-scan over contiguous per-thread ranges), then
-    // the group is regrouped by first appearance of each string as in k_chunk_sort
-    {
-        const uint32_t E = (m + NT - 1) / NT;
-        const uint32_t lo = min(threadIdx.x * E, m), hi = min(lo + E, m);
-        uint32_t run = 0;
-        for (uint32_t p = lo; p < hi; ++p) run = max(run, aux[p]);
-        const uint32_t w = threadIdx.x >> 6;
-        uint32_t inc = run;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(inc, d, 64);
-            if ((int)lane_id() >= d) inc = max(inc, o);
-        }
-        if (lane_id() == 63) s_u32[w] = inc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (int q = 0; q < NT / 64; ++q) {
-                const uint32_t t = s_u32[q];
-                s_u32[q] = acc;
-                acc = max(acc, t);
-            }
-        }
-        __syncthreads();
-        uint32_t excl = __shfl_up(inc, 1, 64);
-        if (lane_id() == 0) excl = 0;
-        uint32_t cur = max(excl, s_u32[w]);
-        for (uint32_t p = lo; p < hi; ++p) {
-            cur = max(cur, aux[p]);
-            aux[p] = cur;  // group start of p
-        }
-    }
-    __syncthreads();
-    // leader = local index of the first occurrence of p's string in its group;
-    // keep the group start in the high half (local indices < 65536)
-    for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        const uint32_t gs = aux[p] & 0xFFFFu;
-        const uint32_t i = sec[p] & 0xFFFFu;
-        uint32_t lead = i;
-        for (uint32_t q = gs; q < p; ++q) {
-            if (rl.same(in[sec[q] & 0xFFFFu], in[i])) {
-                lead = sec[q] & 0xFFFFu;
-                break;
-            }
-        }
-        aux[p] = (gs << 16) | lead;
-    }
-    __syncthreads();
-    heads = 0;
-    for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        const uint32_t i = sec[p] & 0xFFFFu;
-        const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
-        uint32_t np = gs;
-        for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
-            const uint32_t lq = aux[q] & 0xFFFFu;
-            np += (lq < lead) | ((lq == lead) & (q < p));
-        }
-        out[np] = with_head(in[i], lead == i);
-        heads += lead == i;
-    }
-    return heads;
-}
-
-__device__ __forceinline__ void cmp_swap(unsigned long long* key, uint32_t* sec, uint32_t x, uint32_t y) {
-    const unsigned long long kx = key[x], ky = key[y];
-    const uint32_t sx = sec[x], sy = sec[y];
-    if ((kx > ky) | ((kx == ky) & (sx > sy))) {
-        key[x] = ky; key[y] = kx;
-        sec[x] = sy; sec[y] = sx;
+__device__ __forceinline__ void cmp_swap(unsigned long long* k0, unsigned long long* k1, uint32_t x, uint32_t y) {
+    const unsigned long long a0 = k0[x], b0 = k0[y], a1 = k1[x], b1 = k1[y];
+    if (key_lt(b0, b1, a0, a1)) {
+        k0[x] = b0; k0[y] = a0;
+        k1[x] = b1; k1[y] = a1;
     }
 }
 
-// One wave sorts key/sec[lo, lo+L) in place, ascending, with the all-ascending
+// One wave sorts k0/k1[lo, lo+L) in place, ascending, with the all-ascending
 // ("flip + half-cleaner") bitonic network over the next power of two: every
 // comparator puts the smaller value at the lower index, so the virtual +inf
 // padding never moves and comparators that reach past L are simply skipped.
-__device__ void wave_bitonic(unsigned long long* key, uint32_t* sec, uint32_t lo, uint32_t L) {
+__device__ void wave_bitonic(unsigned long long* k0, unsigned long long* k1, uint32_t lo, uint32_t L) {
     uint32_t P2 = 2;
     while (P2 < L) P2 <<= 1;
     const uint32_t lane = lane_id();
@@ -1438,22 +1349,22 @@ __device__ void wave_bitonic(unsigned long long* key, uint32_t* sec, uint32_t lo
         for (uint32_t t = lane; t < (P2 >> 1); t += 64) {
             const uint32_t base = (t / half) * k, off = t & (half - 1);
             const uint32_t l = base + k - 1 - off;
-            if (l < L) cmp_swap(key, sec, lo + base + off, lo + l);
+            if (l < L) cmp_swap(k0, k1, lo + base + off, lo + l);
         }
         wave_sync();
         for (uint32_t j = half >> 1; j > 0; j >>= 1) {
             for (uint32_t t = lane; t < (P2 >> 1); t += 64) {
                 const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
-                if (i + j < L) cmp_swap(key, sec, lo + i, lo + i + j);
+                if (i + j < L) cmp_swap(k0, k1, lo + i, lo + i + j);
             }
             wave_sync();
         }
     }
 }
 
-// The same network with the whole block (bins too big for one wave).
+// The same network with the whole block (runs too big for one wave).
 template <int NT>
-__device__ void block_bitonic(unsigned long long* key, uint32_t* sec, uint32_t lo, uint32_t L) {
+__device__ void block_bitonic(unsigned long long* k0, unsigned long long* k1, uint32_t lo, uint32_t L) {
     uint32_t P2 = 2;
     while (P2 < L) P2 <<= 1;
     for (uint32_t k = 2; k <= P2; k <<= 1) {
@@ -1461,44 +1372,162 @@ __device__ void block_bitonic(unsigned long long* key, uint32_t* sec, uint32_t l
         for (uint32_t t = threadIdx.x; t < (P2 >> 1); t += NT) {
             const uint32_t base = (t / half) * k, off = t & (half - 1);
             const uint32_t l = base + k - 1 - off;
-            if (l < L) cmp_swap(key, sec, lo + base + off, lo + l);
+            if (l < L) cmp_swap(k0, k1, lo + base + off, lo + l);
         }
         __syncthreads();
         for (uint32_t j = half >> 1; j > 0; j >>= 1) {
             for (uint32_t t = threadIdx.x; t < (P2 >> 1); t += NT) {
                 const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
-                if (i + j < L) cmp_swap(key, sec, lo + i, lo + i + j);
+                if (i + j < L) cmp_swap(k0, k1, lo + i, lo + i + j);
             }
             __syncthreads();
         }
     }
 }
 
-// Per chunk (<= CAP records, whole fine mass bins, insertion order inside every
-// bin): sort every bin by (mass bits, peptide tag, local index) — the pinned
-// unique order — then finish_sorted().  Bins of <= RANK_MAX_RUN
-// records: one lane per record counts the bin members ordered before it (all
-// LDS reads, no barriers); bigger bins (equal-mass spikes at SwissProt scale):
-// one wave each sorts the bin in place with wave_bitonic.  A chunk above CAP
-// goes to k_chunk_sort_big.  LDS: 8+4+4+2 B per record = 36 KiB at CAP 2048
-// -> 4 blocks per CU.
+// exclusive max of v over the block's lower threads (0 for thread 0)
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_max(uint32_t v, uint32_t* s_tmp) {
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if ((int)lane >= d) inc = max(inc, o);
+    }
+    if (lane == 63) s_tmp[w] = inc;
+    __syncthreads();
+    uint32_t r = __shfl_up(inc, 1, 64);
+    if (lane == 0) r = 0;
+    for (uint32_t q = 0; q < w; ++q) r = max(r, s_tmp[q]);
+    __syncthreads();
+    return r;
+}
+
+// exclusive min of v over the block's higher threads (`none` for the last)
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_min_rev(uint32_t v, uint32_t none, uint32_t* s_tmp) {
+    constexpr uint32_t NW = NT / 64;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_down(inc, d, 64);
+        if (lane + d < 64) inc = min(inc, o);
+    }
+    if (lane == 0) s_tmp[w] = inc;
+    __syncthreads();
+    uint32_t r = __shfl_down(inc, 1, 64);
+    if (lane == 63) r = none;
+    for (uint32_t q = w + 1; q < NW; ++q) r = min(r, s_tmp[q]);
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ bool same_tag_at(const unsigned long long* k0, const unsigned long long* k1, uint32_t p) {
+    return k0[p] == k0[p - 1] && (k1[p] >> 56) == (k1[p - 1] >> 56);
+}
+
+// Chunk in sorted order in LDS (k0, k1 = the record key): flag unique heads,
+// string-verify equal (mass, tag) neighbours, regroup a 16-bit tag collision
+// by string (first appearance first), write the records in final order with
+// the head flag in the low byte of q0.  aux: scratch (a16[2p] = head info of
+// p, a16[2q+1] = q-th verification pair).  Returns this thread's head count.
+template <int NT>
+__device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLoc& rl, const unsigned long long* k0,
+                                  const unsigned long long* k1, uint32_t* aux, uint32_t* s_u32, uint32_t* s_bad) {
+    uint16_t* a16 = reinterpret_cast<uint16_t*>(aux);
+    if (threadIdx.x == 0) {
+        *s_bad = 0;
+        s_u32[NT / 64] = 0;  // number of equal (mass, tag) neighbour pairs
+    }
+    __syncthreads();
+    uint32_t heads = 0;
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        const bool dup = p > 0 && same_tag_at(k0, k1, p);
+        if (dup) a16[2 * atomicAdd(&s_u32[NT / 64], 1u) + 1] = (uint16_t)p;
+        a16[2 * p] = (uint16_t)(dup ? 0u : p);
+        heads += !dup;
+    }
+    __syncthreads();
+    // string-verify every pair in one parallel round (each check is a chain
+    // of HBM loads: never serialise them per thread)
+    const uint32_t npairs = s_u32[NT / 64];
+    for (uint32_t q = threadIdx.x; q < npairs; q += NT) {
+        const uint32_t p = a16[2 * q + 1];
+        if (!rl.same(Rec{k0[p], k1[p]}, Rec{k0[p - 1], k1[p - 1]})) *s_bad = 1;
+    }
+    __syncthreads();
+    if (*s_bad == 0) {
+        for (uint32_t p = threadIdx.x; p < m; p += NT)
+            out[p] = Rec{(k0[p] & ~0xFFull) | (a16[2 * p] == p ? 1ull : 0ull), k1[p]};  // p == 0 always a head
+        return heads;
+    }
+    // 16-bit tag collision (rare, block-uniform): group start gs(p) = max head
+    // position <= p (block max-scan over contiguous per-thread ranges)
+    {
+        const uint32_t E = (m + NT - 1) / NT;
+        const uint32_t lo = min(threadIdx.x * E, m), hi = min(lo + E, m);
+        uint32_t run = 0;
+        for (uint32_t p = lo; p < hi; ++p) run = max(run, (uint32_t)a16[2 * p]);
+        uint32_t cur = block_excl_max<NT>(run, s_u32);
+        for (uint32_t p = lo; p < hi; ++p) {
+            cur = max(cur, (uint32_t)a16[2 * p]);
+            aux[p] = cur;  // group start of p (the pair list is dead)
+        }
+    }
+    __syncthreads();
+    // leader = position of the first occurrence of p's string in its group
+    // (sorted order inside a group = first appearance); group start kept in
+    // the high half
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        const uint32_t gs = aux[p];
+        const Rec me{k0[p], k1[p]};
+        uint32_t lead = p;
+        for (uint32_t q = gs; q < p; ++q)
+            if (rl.same(Rec{k0[q], k1[q]}, me)) { lead = q; break; }
+        aux[p] = (gs << 16) | lead;
+    }
+    __syncthreads();
+    heads = 0;
+    for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
+        uint32_t np = gs;
+        for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
+            const uint32_t lq = aux[q] & 0xFFFFu;
+            np += (lq < lead) | ((lq == lead) & (q < p));
+        }
+        out[np] = Rec{(k0[p] & ~0xFFull) | (lead == p ? 1ull : 0ull), k1[p]};
+        heads += lead == p;
+    }
+    return heads;
+}
+
+// Per chunk (<= CAP records, whole fine mass bins): sort every bin by the
+// record key (q0, q1) — mass, peptide tag, first appearance: the pinned unique
+// order, independent of the order the records arrive in — then
+// finish_sorted().  Bins of <= RANK_MAX_RUN records: each record's rank inside
+// its bin from LDS compares (no barriers), scattered from registers; bigger
+// bins (equal-mass spikes at SwissProt scale) are sorted in place, one wave
+// each up to WAVE_SORT_MAX, else by the whole block.  A chunk above CAP goes
+// to k_chunk_sort_big.  LDS: 8+8+4 B per record, 39 KiB at CAP 1984 -> 4
+// blocks per CU.
 constexpr uint32_t RANK_MAX_RUN = 64;
 constexpr uint32_t WAVE_SORT_MAX = 256;
 constexpr uint32_t MAX_BIG_RUNS = 64;
 
 template <int NT, int CAP>
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
              const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
              uint32_t* __restrict__ big_list, Counters* __restrict__ ctr) {
-    static_assert(CAP <= 65535 && CAP % NT == 0, "16-bit local indices");
+    static_assert(CAP <= 65535, "16-bit positions");
     static_assert(CAP / (RANK_MAX_RUN + 1) <= MAX_BIG_RUNS, "big-run list");
     constexpr uint32_t NW = NT / 64;
-    constexpr uint32_t E = CAP / NT;  // records per thread in the run-detection pass
-    __shared__ unsigned long long key[CAP];  // mass bits (positive doubles order as integers)
-    __shared__ uint32_t sec[CAP];            // tag << 16 | local index
-    __shared__ uint32_t aux[CAP];            // bin id -> run bounds lo | hi << 16 -> scratch
-    __shared__ uint16_t perm[CAP];           // run starts -> sorted position -> local index
+    constexpr uint32_t E = (CAP + NT - 1) / NT;  // records per thread (contiguous) in the run pass
+    __shared__ unsigned long long k0[CAP];
+    __shared__ unsigned long long k1[CAP];
+    __shared__ uint32_t aux[CAP];
     __shared__ uint32_t s_big[MAX_BIG_RUNS];  // runs above RANK_MAX_RUN: lo | hi << 16
     __shared__ uint32_t s_u32[NW + 1];
     __shared__ uint32_t s_nbig, s_bad;
@@ -1515,7 +1544,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
     }
     if (threadIdx.x == 0) s_nbig = 0;
     {
-        // all E loads in flight before the first use (Rec as 4 dwords: q0, q1)
+        // all loads in flight before the first use (a Rec as 4 dwords: q0, q1)
         const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in + a);
         uint4 rv[E];
 #pragma unroll
@@ -1527,119 +1556,122 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         for (uint32_t k = 0; k < E; ++k) {
             const uint32_t i = threadIdx.x + k * NT;
             if (i < m) {
-                key[i] = u4_q0(rv[k]);                  // mass, tag >> 8
-                sec[i] = ((rv[k].w >> 24) << 16) | i;   // tag & 0xFF, local index
-                aux[i] = bin_of(u4_mass(rv[k]), bm);
+                k0[i] = u4_q0(rv[k]);
+                k1[i] = u4_q1(rv[k]);
             }
         }
     }
     __syncthreads();
-    // runs of equal bin id: thread t owns records [t*E, t*E+E); run index of
-    // each record kept in registers, run starts compacted into perm[]
+    // bin runs: thread t owns records [t*E, t*E+E); run bounds of each record
+    // from a block max-scan (last run start <= i) and a reverse min-scan
+    // (first run start > i), kept in registers
     const uint32_t lo0 = threadIdx.x * E;
-    uint32_t runof[E];
-    uint32_t flags = 0, nruns;
+    uint32_t heads = 0;  // bit k: record lo0+k starts a run
     {
-        uint32_t cnt = 0;
+        uint32_t prev = (lo0 > 0 && lo0 - 1 < m) ? bin_of(q0_mass(k0[lo0 - 1]), bm) : ~0u;
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) {
             const uint32_t i = lo0 + k;
-            const bool h = i < m && (i == 0 || aux[i] != aux[i - 1]);
-            flags |= (uint32_t)h << k;
-            cnt += h;
-        }
-        uint32_t pos = block_excl_scan<NT, uint32_t>(cnt, s_u32, nruns);
-#pragma unroll
-        for (uint32_t k = 0; k < E; ++k) {
-            if (flags & (1u << k)) perm[pos++] = (uint16_t)(lo0 + k);
-            runof[k] = pos - 1;
+            if (i < m) {
+                const uint32_t b = bin_of(q0_mass(k0[i]), bm);
+                if (i == 0 || b != prev) heads |= 1u << k;
+                prev = b;
+            }
         }
     }
+    uint32_t rlo[E], rhi[E];
+    {
+        uint32_t cur = block_excl_max<NT>(heads ? lo0 + 31 - __clz(heads) : 0u, s_u32);
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            if (heads & (1u << k)) cur = lo0 + k;
+            rlo[k] = cur;
+        }
+        cur = block_excl_min_rev<NT>(heads ? lo0 + __ffs(heads) - 1 : m, m, s_u32);
+#pragma unroll
+        for (int k = (int)E - 1; k >= 0; --k) {
+            rhi[k] = cur;
+            if (heads & (1u << k)) cur = lo0 + (uint32_t)k;
+        }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k)
+        if ((heads & (1u << k)) && rhi[k] - rlo[k] > RANK_MAX_RUN)
+            s_big[atomicAdd(&s_nbig, 1u)] = rlo[k] | (rhi[k] << 16);
     __syncthreads();
+    // small bins: rank inside the bin, kept in registers with the key
+    unsigned long long v0[E], v1[E];
+    uint32_t dst[E];
 #pragma unroll
     for (uint32_t k = 0; k < E; ++k) {
         const uint32_t i = lo0 + k;
-        if (i < m) {
-            const uint32_t r = runof[k];
-            const uint32_t rlo = perm[r];
-            const uint32_t rhi = r + 1 < nruns ? perm[r + 1] : m;
-            aux[i] = rlo | (rhi << 16);
-            if ((flags & (1u << k)) && rhi - rlo > RANK_MAX_RUN) s_big[atomicAdd(&s_nbig, 1u)] = rlo | (rhi << 16);
+        dst[k] = ~0u;
+        if (i < m && rhi[k] - rlo[k] <= RANK_MAX_RUN) {
+            const unsigned long long a0 = k0[i], a1 = k1[i];
+            uint32_t rank = 0;
+            for (uint32_t j = rlo[k]; j < rhi[k]; ++j) rank += key_lt(k0[j], k1[j], a0, a1);
+            v0[k] = a0;
+            v1[k] = a1;
+            dst[k] = rlo[k] + rank;
         }
-    }
-    __syncthreads();
-    // small bins: rank inside the bin, one lane per record
-    for (uint32_t i = threadIdx.x; i < m; i += NT) {
-        const uint32_t b = aux[i];
-        const uint32_t rlo = b & 0xFFFFu, rhi = b >> 16;
-        if (rhi - rlo > RANK_MAX_RUN) continue;
-        const unsigned long long ki = key[i];
-        const uint32_t si = sec[i];
-        uint32_t rank = 0;
-#pragma unroll 4
-        for (uint32_t j = rlo; j < rhi; ++j) {
-            const unsigned long long kj = key[j];
-            rank += (kj < ki) | ((kj == ki) & (sec[j] < si));
-        }
-        perm[rlo + rank] = (uint16_t)i;
     }
     // big bins, sorted in place (disjoint from the small bins): up to
-    // WAVE_SORT_MAX records one wave each, above that the whole block
+    // WAVE_SORT_MAX records one wave each
     const uint32_t nbig = s_nbig;
     for (uint32_t r = threadIdx.x >> 6; r < nbig; r += NW) {
         const uint32_t b = s_big[r];
         const uint32_t L = (b >> 16) - (b & 0xFFFFu);
-        if (L <= WAVE_SORT_MAX) wave_bitonic(key, sec, b & 0xFFFFu, L);
+        if (L <= WAVE_SORT_MAX) wave_bitonic(k0, k1, b & 0xFFFFu, L);
     }
-    __syncthreads();
-    for (uint32_t r = 0; r < nbig; ++r) {
+    __syncthreads();  // every rank read done: scatter the small bins
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        if (dst[k] != ~0u) {
+            k0[dst[k]] = v0[k];
+            k1[dst[k]] = v1[k];
+        }
+    }
+    for (uint32_t r = 0; r < nbig; ++r) {  // above WAVE_SORT_MAX: the whole block
         const uint32_t b = s_big[r];
         const uint32_t L = (b >> 16) - (b & 0xFFFFu);
-        if (L > WAVE_SORT_MAX) block_bitonic<NT>(key, sec, b & 0xFFFFu, L);
-    }
-    // whole chunk into sorted order: small bins gather through perm, big bins
-    // are already in place (registers first, then one barrier, then store)
-    unsigned long long kv[E];
-    uint32_t sv[E];
-#pragma unroll
-    for (uint32_t k = 0; k < E; ++k) {
-        const uint32_t p = lo0 + k;
-        if (p < m) {
-            const uint32_t b = aux[p];
-            const uint32_t src = ((b >> 16) - (b & 0xFFFFu) > RANK_MAX_RUN) ? p : perm[p];
-            kv[k] = key[src];
-            sv[k] = sec[src];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < E; ++k) {
-        const uint32_t p = lo0 + k;
-        if (p < m) {
-            key[p] = kv[k];
-            sec[p] = sv[k];
-        }
+        if (L > WAVE_SORT_MAX) block_bitonic<NT>(k0, k1, b & 0xFFFFu, L);
     }
     __syncthreads();
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
-    const uint32_t h = finish_sorted<NT>(in + a, out + a, m, rl, key, sec, aux, perm, s_u32, &s_bad);
+    const uint32_t h = finish_sorted<NT>(out + a, m, rl, k0, k1, aux, s_u32, &s_bad);
     const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
     if (threadIdx.x == 0) ucount[c] = tot;
 }
 
+// One chunk of m <= CAP records sorted in LDS by the record key with the flip
+// bitonic network (cost independent of how the masses cluster), then
+// finish_sorted.  k0/k1/aux: CAP entries each.  Returns this thread's head count.
+template <int NT, int CAP>
+__device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const RecLoc& rl,
+                                  unsigned long long* k0, unsigned long long* k1, uint32_t* aux, uint32_t* s_u32,
+                                  uint32_t* s_bad) {
+    for (uint32_t i = threadIdx.x; i < m; i += NT) {
+        const Rec r = in[i];
+        k0[i] = r.q0;
+        k1[i] = r.q1;
+    }
+    __syncthreads();
+    block_bitonic<NT>(k0, k1, 0, m);
+    return finish_sorted<NT>(out, m, rl, k0, k1, aux, s_u32, s_bad);
+}
+
 // chunks of (CHUNK_CAP, BIG_CAP] records (bins of very frequent masses at
-// SwissProt scale): 1024 threads, 128 KiB LDS, one block per CU; larger
+// SwissProt scale): 1024 threads, 155 KiB LDS, one block per CU; larger
 // chunks go on to the global-memory path.
 __global__ void __launch_bounds__(BIG_THREADS)
 k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
                  const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
                  const uint32_t* __restrict__ big_list, uint32_t* __restrict__ giant_list,
                  Counters* __restrict__ ctr) {
-    static_assert(BIG_CAP <= 65536, "16-bit local indices");
-    __shared__ unsigned long long key[BIG_CAP];
-    __shared__ uint32_t sec[BIG_CAP];
+    static_assert(BIG_CAP <= 65535, "16-bit positions");
+    __shared__ unsigned long long k0[BIG_CAP];
+    __shared__ unsigned long long k1[BIG_CAP];
     __shared__ uint32_t aux[BIG_CAP];
-    __shared__ uint16_t pairs[BIG_CAP];
     __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
     __shared__ uint32_t s_bad;
     const uint32_t nbig = ctr->n_big;
@@ -1652,8 +1684,7 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
             if (threadIdx.x == 0) giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
             continue;
         }
-        const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, rl, key, sec, aux, pairs, s_u32,
-                                                               &s_bad);
+        const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, rl, k0, k1, aux, s_u32, &s_bad);
         const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
         if (threadIdx.x == 0) ucount[c] = tot;
         __syncthreads();
@@ -1683,8 +1714,8 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
 __global__ void __launch_bounds__(BIG_THREADS)
 k_big_chunks(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
              const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
-             const uint32_t* __restrict__ big_list,
-             unsigned long long* ws_key, uint32_t* ws_k2, Counters* __restrict__ ctr) {
+             const uint32_t* __restrict__ big_list, unsigned long long* ws_key, uint32_t* ws_k2,
+             Counters* __restrict__ ctr) {
     __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
     __shared__ unsigned long long s_flag;
     const uint32_t nbig = ctr->n_giant;
@@ -1693,12 +1724,11 @@ k_big_chunks(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* 
         const uint32_t c = big_list[j];
         const uint32_t a = chunk_lo[c];
         const uint32_t m = chunk_lo[c + 1] - a;
-        unsigned long long* key = ws_key + 4ull * a;   // [4a, 4a+2m): key, [4a+2m, 4a+4m): hash
+        unsigned long long* key = ws_key + 4ull * a;   // [4a, 4a+2m): key, [4a+2m, 4a+4m): hsh
         unsigned long long* hsh = key + 2ull * m;
         uint32_t* k2 = ws_k2 + 4ull * a;               // [4a, 4a+2m): idx, [4a+2m, 4a+3m): runs
         uint32_t* k3 = k2 + 2ull * m;
-        const uint32_t h = process_chunk<BIG_THREADS, false>(in + a, const_cast<Rec*>(in + a), out + a, m, rl, key,
-                                                              hsh, k2, k3, s_u32, &s_flag);
+        const uint32_t h = process_chunk<BIG_THREADS>(in + a, out + a, m, rl, key, hsh, k2, k3, s_u32, &s_flag);
         const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
         if (threadIdx.x == 0) ucount[c] = tot;
         __syncthreads();

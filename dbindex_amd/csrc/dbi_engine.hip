@@ -242,8 +242,10 @@ Bytes by(double cR, double cN, double cU, double cP, double cB) {
 }
 
 // Steps 4-6 over n records in recA: partition by mass bin, per-bin sort +
-// dedup, finalize.  lo/hi bound every record mass.
-int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
+// dedup, finalize.  lo/hi bound every record mass.  sparse: recA holds n_in
+// slots, n of them records and the rest REC_SENTINEL (bounded digest); the
+// first radix pass leaves the sentinels behind.
+int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse) {
     hipStream_t s = h->stream;
     int rc;
     const uint32_t n32 = (uint32_t)n;
@@ -253,9 +255,10 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
     bm.nbins = nbins;
     bm.scale = (hi > lo) ? (double)nbins / (hi - lo) : 0.0;
     const int total_bits = log2_ceil(nbins);
-    const int passes = (total_bits + RADIX_BITS - 1) / RADIX_BITS;
-    const int bits_per = passes ? (total_bits + passes - 1) / passes : 0;
-    const size_t hist_elems = passes ? radix_hist_elems(n32, bits_per) : 1;
+    const int passes = std::max((total_bits + RADIX_BITS - 1) / RADIX_BITS, sparse ? 1 : 0);
+    const int bits_per = total_bits ? (total_bits + passes - 1) / passes : 0;
+    const uint32_t n_in32 = sparse ? (uint32_t)n_in : n32;
+    const size_t hist_elems = passes ? radix_hist_elems(n_in32, bits_per) : 1;
 
     // every allocation before the first launch of this stage: a reallocation
     // must never free a buffer that queued kernels still use
@@ -277,14 +280,17 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi) {
     int shift = 0;
     for (int ps = 0; ps < passes; ++ps) {
         const int bits = std::min(bits_per, total_bits - shift);
-        const double hbytes = 8.0 * (double)radix_blocks(n32) * (double)(1u << bits);  // hist write + scan
+        const bool sp = sparse && ps == 0;
+        const uint32_t nin = sp ? n_in32 : n32;
+        const double hbytes = 8.0 * (double)radix_blocks(nin) * (double)(1u << bits);  // hist write + scan
         // hist reads the 8-B mass of every record; scatter moves 16 B in + 16 B out
-        STAGE(h, "radix_hist", by(0, 8, 0, 0, 0), launch_radix_hist(src, n32, bm, shift, bits, h->hist.p, s));
+        STAGE(h, "radix_hist", by(0, 8, 0, 0, 0), launch_radix_hist(src, nin, bm, shift, bits, sp, h->hist.p, s));
         STAGE(h, "radix_scan", by(0, 0, 0, 0, 0),
-              launch_scan_u32(h->hist.p, h->hist.p, (uint64_t)radix_blocks(n32) << bits, h->scan_tmp.p,
+              launch_scan_u32(h->hist.p, h->hist.p, (uint64_t)radix_blocks(nin) << bits, h->scan_tmp.p,
                               h->scan_tmp.cap, nullptr, s));
         h->stages[h->nstage - 1].cB = hbytes / std::max<double>(nbins, 1.0);
-        STAGE(h, "radix_scatter", by(0, 32, 0, 0, 0), launch_radix_scatter(src, dst, n32, bm, shift, bits, h->hist.p, s));
+        STAGE(h, "radix_scatter", by(0, 32, 0, 0, 0),
+              launch_radix_scatter(src, dst, nin, bm, shift, bits, sp, h->hist.p, s));
         std::swap(src, dst);
         shift += bits;
     }
@@ -374,30 +380,43 @@ int build_digest(dbi_handle* h) {
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(nblk), h->scan_tmp.cap)))) return rc;
     if ((rc = prepare_tiles(h))) return rc;
     uint64_t n;
+    // full enzyme, no mandatory residues, <= 2 missed cleavages: one walk into
+    // bounded per-tile reservations (<= 4 slots per cleavage-site start)
+    const bool bounded = !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2;
     if (h->recA.cap >= 1024) {
-        // warm: one fused pass into the capacity of the previous build; the
-        // exact total comes back with the counters, and a short buffer is
-        // grown and the pass run again
+        // warm: one pass into the capacity of the previous build; the exact
+        // need comes back with the counters, and a short buffer is grown and
+        // the pass run again
         if ((rc = h->status.ensure(nblk))) return rc;
         for (int attempt = 0;; ++attempt) {
             if (++h->epoch >= 0xFFFFu) {
                 DBI_HIP(hipMemsetAsync(h->status.p, 0, sizeof(unsigned long long) * h->status.cap, s));
                 h->epoch = 1;
             }
-            const uint32_t cap = (uint32_t)std::min<size_t>(h->recA.cap, 0xFFFFFFFFull);
-            STAGE(h, "digest", by(1, 16, 0, 4, 0),
-                  launch_digest_fused(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
-                                      (uint32_t)R, h->tile_pf.p, h->status.p, h->epoch, h->recA.p, cap, h->ctr.p, s));
+            const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
+            if (bounded)
+                STAGE(h, "digest", by(1, 16, 0, 4, 0),
+                      launch_digest_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p,
+                                            (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->status.p, h->epoch,
+                                            h->recA.p, cap, h->ctr.p, s));
+            else
+                STAGE(h, "digest", by(1, 16, 0, 4, 0),
+                      launch_digest_fused(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p,
+                                          (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->status.p, h->epoch,
+                                          h->recA.p, (uint32_t)cap, h->ctr.p, s));
             if ((rc = read_counters(h))) return rc;
             n = h->hc.n_kept;
-            if (n >= (1ull << 32) - 1)
-                return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences on one device: shard the FASTA");
-            if (n <= cap) break;
+            const uint64_t need = bounded ? h->hc.n_slots : n;
+            if (need >= (1ull << 32) - 1)
+                return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences (or bounded-digest slots) on "
+                                                "one device: shard the FASTA");
+            if (need <= cap) break;
             if (attempt > 0) return set_error(DBI_E_STATE, "digest output grew between identical passes");
-            if ((rc = h->recA.ensure(n + n / 8))) return rc;
+            if ((rc = h->recA.ensure(need + need / 8))) return rc;
             // counters back to zero, except the record layout (max_plen) set by prepare_tiles
             DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
         }
+        if (bounded) return build_tail(h, n, h->params.min_mh, h->params.max_mh, h->hc.n_slots, true);
     } else {
         // cold: count, scan, size the output, emit
         STAGE(h, "digest_count", by(1, 0, 0, 4, 0),
@@ -415,7 +434,7 @@ int build_digest(dbi_handle* h) {
               launch_digest_emit(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
                                  (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->recA.p, h->ctr.p, s));
     }
-    return build_tail(h, n, h->params.min_mh, h->params.max_mh);
+    return build_tail(h, n, h->params.min_mh, h->params.max_mh, n, false);
 }
 
 int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
@@ -658,7 +677,7 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
     DBI_HIP(hipMemcpyAsync(&h->ctr.p->n_kept, &kept, sizeof(kept), hipMemcpyHostToDevice, h->stream));
     DBI_HIP(hipStreamSynchronize(h->stream));
     h->n_total_extra = n_dropped_extra;
-    if ((rc = build_tail(h, n_occ, lo, hi))) return rc;
+    if ((rc = build_tail(h, n_occ, lo, hi, n_occ, false))) return rc;
     return finish_build(h);
 }
 

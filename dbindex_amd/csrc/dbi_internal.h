@@ -107,13 +107,15 @@ struct Counters {
     unsigned long long n_unique;
     unsigned long long n_keys;
     unsigned long long n_keys_shard[8];  // per-XCD-group partial key counts (summed on readback)
+    unsigned long long n_slots;    // bounded digest: record slots reserved (kept + sentinels)
     unsigned int n_big;            // chunks above CHUNK_CAP (sorted by the 1024-thread LDS kernel)
     unsigned int err;              // device error bits
     unsigned int n_giant;          // chunks above BIG_CAP (global-memory path)
-    unsigned int tile_ticket;      // k_digest_fused: tiles in dispatch order
-    // read by every block of every kernel: its own cache line, away from the
-    // atomics above (sharing the tile ticket's line cost the digest 30%)
-    alignas(256) unsigned int max_plen;  // longest protein (k_tile_proteins): the record field width
+    // hot lines apart: the digest's per-tile ticket (every block, waits for
+    // the result), and the layout word every block of every kernel reads
+    // (sharing the ticket's line cost the digest 30%)
+    alignas(256) unsigned int tile_ticket;  // k_digest_fused / k_digest_bounded: tiles in dispatch order
+    alignas(256) unsigned int max_plen;     // longest protein (k_tile_proteins): the record field width
 };
 constexpr unsigned ERR_LAYOUT = 1;  // 2*bits(longest protein) + bits(proteins) > 56
 
@@ -125,11 +127,11 @@ constexpr int RADIX_BITS = 9;        // max digit width (512 buckets)
 constexpr int RADIX_THREADS = 256;
 constexpr int RADIX_ITEMS = 16;     // records per thread per radix block
 constexpr int CHUNK_THREADS = 512;
-constexpr int CHUNK_CAP = 2048;     // records per chunk sorted in LDS
+constexpr int CHUNK_CAP = 1984;     // records per chunk sorted in LDS (20 B each: 4 blocks per CU)
 constexpr int CHUNK_T = 1024;       // target chunk size (whole mass bins, ~T..T+maxbin)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
 constexpr int BIG_THREADS = 1024;
-constexpr int BIG_CAP = 8192;       // records per oversize chunk sorted in LDS (1 block per CU)
+constexpr int BIG_CAP = 7936;       // records per oversize chunk sorted in LDS (1 block per CU)
 
 // ---- launchers (dbi_device.hip) -------------------------------------------------
 // All return hipError_t of the launch.
@@ -149,6 +151,17 @@ hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, co
                                const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                const uint32_t* d_tile_pf, unsigned long long* d_status, uint32_t epoch,
                                Rec* d_out, uint32_t cap, Counters* d_ctr, hipStream_t s);
+// Full-enzyme digest without mandatory residues in one walk: a start emits at
+// most max_missed + 2 records, so tile t reserves ncand_t * (max_missed + 2)
+// slots (decoupled look-back over the reservations), fills them in start order
+// and marks unused slots with REC_SENTINEL (q0 == ~0).  ctr->n_slots = slots
+// reserved, ctr->n_kept = records kept; nothing is written when n_slots > cap
+// (the caller grows the buffer and runs it again).
+constexpr unsigned long long REC_SENTINEL = ~0ull;
+hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                                 const uint32_t* d_tile_pf, unsigned long long* d_status, uint32_t epoch,
+                                 Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s);
 hipError_t launch_digest_emit(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                               const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
                               uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk_off, uint32_t* d_thr,
@@ -163,10 +176,11 @@ struct BinMap {
     double scale;     // nbins / (hi - lo)
     uint32_t nbins;
 };
-hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, uint32_t* d_hist,
-                             hipStream_t s);
+// sparse: the input holds REC_SENTINEL slots (bounded digest), left out of the output
+hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,
+                             uint32_t* d_hist, hipStream_t s);
 hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
-                                const uint32_t* d_hist, hipStream_t s);
+                                bool sparse, const uint32_t* d_hist, hipStream_t s);
 uint64_t radix_blocks(uint32_t n);
 size_t radix_hist_elems(uint32_t n, int bits);
 // chunk_lo[c] = first bin start at or after c*T in the bin-sorted records (nchunks+1 entries)
