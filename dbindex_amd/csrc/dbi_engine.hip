@@ -49,6 +49,15 @@ struct DevBuf {
         cap = want;
         return 0;
     }
+    // look-back status words: a fresh allocation may hold words of an earlier
+    // (freed) status array whose epoch tags match; start from zero
+    int ensure_zeroed(size_t n, hipStream_t s) {
+        if (n <= cap && p) return 0;
+        int rc = ensure(n);
+        if (rc) return rc;
+        const hipError_t e = hipMemsetAsync(p, 0, cap * sizeof(T), s);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -387,7 +396,7 @@ int build_digest(dbi_handle* h) {
         // warm: one pass into the capacity of the previous build; the exact
         // need comes back with the counters, and a short buffer is grown and
         // the pass run again
-        if ((rc = h->status.ensure(nblk))) return rc;
+        if ((rc = h->status.ensure_zeroed(nblk, s))) return rc;
         for (int attempt = 0;; ++attempt) {
             if (++h->epoch >= 0xFFFFu) {
                 DBI_HIP(hipMemsetAsync(h->status.p, 0, sizeof(unsigned long long) * h->status.cap, s));

@@ -124,7 +124,7 @@ constexpr int DIGEST_THREADS = 256;
 constexpr int DIGEST_TILE = 2048;   // starts per digest block
 constexpr int DIGEST_HALO = 256;    // residues staged past the tile
 constexpr int RADIX_BITS = 9;        // max digit width (512 buckets)
-constexpr int RADIX_THREADS = 256;
+constexpr int RADIX_THREADS = 512;
 constexpr int RADIX_ITEMS = 16;     // records per thread per radix block
 constexpr int CHUNK_THREADS = 512;
 constexpr int CHUNK_CAP = 1984;     // records per chunk sorted in LDS (20 B each: 4 blocks per CU)
