@@ -1027,7 +1027,11 @@ template <bool SPARSE>
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, BinMap bm, int shift,
                 int bits, const uint32_t* __restrict__ offs) {
+    static_assert(RADIX_D <= RADIX_THREADS, "one digit per thread");
     __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
+    __shared__ uint4 stage[RADIX_CHUNK];  // the block's records in digit order
+    __shared__ uint32_t gofs[RADIX_D];    // global position of digit d's first record - its local start
+    __shared__ uint32_t s_tmp[RADIX_NW + 1];
     const uint32_t D = 1u << bits, mask = D - 1;
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
@@ -1059,21 +1063,38 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, B
         pos[k] = before + rank;
     }
     __syncthreads();
-    // per digit: global offset of this block, then the waves in order
-    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) {
-        uint32_t acc = offs[(size_t)d * gridDim.x + blockIdx.x];
+    // per digit (one per thread): block-local start (scan over digits), the
+    // waves in order inside it, and the global offset of this block's run
+    const uint32_t d = threadIdx.x;
+    uint32_t tot = 0;
+    if (d < D) {
+#pragma unroll
+        for (int ww = 0; ww < RADIX_NW; ++ww) tot += cnt[ww][d];
+    }
+    uint32_t nvalid;
+    const uint32_t lstart = block_excl_scan<RADIX_THREADS, uint32_t>(tot, s_tmp, nvalid);
+    if (d < D) {
+        uint32_t acc = lstart;
 #pragma unroll
         for (int ww = 0; ww < RADIX_NW; ++ww) {
             const uint32_t t = cnt[ww][d];
             cnt[ww][d] = acc;
             acc += t;
         }
+        gofs[d] = offs[(size_t)d * gridDim.x + blockIdx.x] - lstart;
     }
     __syncthreads();
-    uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
+    // exchange through LDS, then write digit runs with consecutive lanes on
+    // consecutive addresses
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k)
-        if (vmask & (1u << k)) out4[cnt[w][dg[k]] + pos[k]] = rv[k];
+        if (vmask & (1u << k)) stage[cnt[w][dg[k]] + pos[k]] = rv[k];
+    __syncthreads();
+    uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
+    for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) {
+        const uint4 r = stage[t];
+        out4[gofs[(bin_of(u4_mass(r), bm) >> shift) & mask] + t] = r;
+    }
 }
 
 hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,

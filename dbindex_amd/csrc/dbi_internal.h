@@ -121,11 +121,11 @@ constexpr unsigned ERR_LAYOUT = 1;  // 2*bits(longest protein) + bits(proteins) 
 
 // Tunables
 constexpr int DIGEST_THREADS = 256;
-constexpr int DIGEST_TILE = 2048;   // starts per digest block
+constexpr int DIGEST_TILE = 4096;   // starts per digest block
 constexpr int DIGEST_HALO = 256;    // residues staged past the tile
-constexpr int RADIX_BITS = 9;        // max digit width (512 buckets)
+constexpr int RADIX_BITS = 8;        // max digit width (256 buckets; 3 passes cover the 2^24 bins)
 constexpr int RADIX_THREADS = 512;
-constexpr int RADIX_ITEMS = 16;     // records per thread per radix block
+constexpr int RADIX_ITEMS = 8;      // records per thread per radix block (4096: 64 KiB LDS exchange)
 constexpr int CHUNK_THREADS = 512;
 constexpr int CHUNK_CAP = 1984;     // records per chunk sorted in LDS (20 B each: 4 blocks per CU)
 constexpr int CHUNK_T = 1024;       // target chunk size (whole mass bins, ~T..T+maxbin)

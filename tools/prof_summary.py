@@ -23,11 +23,12 @@ import sys
 STAGES = [
     ("dbi::k_tile_proteins", "tile_proteins"),
     ("void dbi::k_digest_fused<", "digest"),
+    ("dbi::k_digest_bounded", "digest"),
     ("dbi::k_digest_count_cuts", "digest_count"),
     ("void dbi::k_digest<false", "digest_count"),
     ("void dbi::k_digest<true", "digest_emit"),
-    ("dbi::k_radix_hist", "radix_hist"),
-    ("dbi::k_radix_scatter", "radix_scatter"),
+    ("void dbi::k_radix_hist<", "radix_hist"),
+    ("void dbi::k_radix_scatter<", "radix_scatter"),
     ("dbi::k_chunk_bounds", "chunk_bounds"),
     ("void dbi::k_chunk_sort<", "chunk_sort"),
     ("dbi::k_chunk_sort_big", "chunk_sort_big"),
