@@ -1616,24 +1616,28 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         }
     }
 #pragma unroll
-    for (uint32_t k = 0; k < E; ++k)
+    for (uint32_t k = 0; k < E; ++k) {
         if ((heads & (1u << k)) && rhi[k] - rlo[k] > RANK_MAX_RUN)
             s_big[atomicAdd(&s_nbig, 1u)] = rlo[k] | (rhi[k] << 16);
+        if (lo0 + k < m) aux[lo0 + k] = rlo[k] | (rhi[k] << 16);
+    }
     __syncthreads();
-    // small bins: rank inside the bin, kept in registers with the key
+    // small bins: rank inside the bin (k-major: a wave's lanes share bins), kept in registers with the key
     unsigned long long v0[E], v1[E];
     uint32_t dst[E];
 #pragma unroll
     for (uint32_t k = 0; k < E; ++k) {
-        const uint32_t i = lo0 + k;
+        const uint32_t i = threadIdx.x + k * NT;
         dst[k] = ~0u;
-        if (i < m && rhi[k] - rlo[k] <= RANK_MAX_RUN) {
+        const uint32_t bb = i < m ? aux[i] : 0u;
+        const uint32_t blo = bb & 0xFFFFu, bhi = bb >> 16;
+        if (i < m && bhi - blo <= RANK_MAX_RUN) {
             const unsigned long long a0 = k0[i], a1 = k1[i];
             uint32_t rank = 0;
-            for (uint32_t j = rlo[k]; j < rhi[k]; ++j) rank += key_lt(k0[j], k1[j], a0, a1);
+            for (uint32_t j = blo; j < bhi; ++j) rank += key_lt(k0[j], k1[j], a0, a1);
             v0[k] = a0;
             v1[k] = a1;
-            dst[k] = rlo[k] + rank;
+            dst[k] = blo + rank;
         }
     }
     // big bins, sorted in place (disjoint from the small bins): up to
