@@ -773,6 +773,58 @@ hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, co
     return hipGetLastError();
 }
 
+// Length-balanced walk order.  A full-enzyme walk from candidate j ends near
+// the B-th next cleavage site, so cand[j+B] - cand[j] estimates its length; a
+// counting sort of the candidates by that estimate (in place, through
+// registers) gives each wave's lanes walks of about the same length, instead
+// of every wave waiting for its longest one.  Any order is valid: candidate j
+// (in the new order) fills slots [j*B, j*B + B).  Tiles of more than
+// BAL_MAX candidates keep their order.
+constexpr uint32_t BAL_ITEMS = 4;
+constexpr uint32_t BAL_MAX = BAL_ITEMS * DIGEST_THREADS;
+constexpr uint32_t BAL_BUCKETS = 128;
+
+__device__ void balance_candidates(DigestSmem& sm, uint32_t ncand, uint32_t B, uint32_t tile_len) {
+    if (ncand > BAL_MAX || ncand < 2) return;  // block-uniform
+    __shared__ uint32_t s_cnt[BAL_BUCKETS];
+    for (uint32_t b = threadIdx.x; b < BAL_BUCKETS; b += DIGEST_THREADS) s_cnt[b] = 0;
+    __syncthreads();
+    uint32_t cv[BAL_ITEMS], key[BAL_ITEMS], rk[BAL_ITEMS];
+#pragma unroll
+    for (uint32_t k = 0; k < BAL_ITEMS; ++k) {
+        const uint32_t j = threadIdx.x + k * DIGEST_THREADS;
+        if (j < ncand) {
+            cv[k] = sm.cand[j];
+            const uint32_t nxt = j + B < ncand ? sm.cand[j + B] : tile_len + (uint32_t)DIGEST_HALO;
+            key[k] = min(nxt - cv[k], BAL_BUCKETS - 1);
+            rk[k] = atomicAdd(&s_cnt[key[k]], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the bucket counts, one wave
+        constexpr uint32_t PER = BAL_BUCKETS / 64;
+        uint32_t v[PER], loc = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            v[q] = s_cnt[threadIdx.x * PER + q];
+            loc += v[q];
+        }
+        uint32_t run = wave_incl_scan(loc) - loc;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            s_cnt[threadIdx.x * PER + q] = run;
+            run += v[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < BAL_ITEMS; ++k) {
+        const uint32_t j = threadIdx.x + k * DIGEST_THREADS;
+        if (j < ncand) sm.cand[s_cnt[key[k]] + rk[k]] = (uint16_t)cv[k];
+    }
+    __syncthreads();
+}
+
 // One walk per start (see launch_digest_bounded): reservation look-back right
 // after compaction, then emit into the thread's own slots.
 __global__ void __launch_bounds__(DIGEST_THREADS)
@@ -802,6 +854,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     if (base + (unsigned long long)ncand * B > cap) return;  // too small: the caller grows it and runs again
     tc.w = rec_width(d_ctr->max_plen);
     if (tile == 0 && threadIdx.x == 0 && !rec_layout_ok(tc.w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
+    balance_candidates(sm, ncand, B, tc.t_end - tc.t0);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
     Rec* __restrict__ o = d_out + base + (unsigned long long)jb * B;
