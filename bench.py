@@ -7,8 +7,14 @@ HBM.  Default workload at N=1: the SwissProt-scale FASTA the metric is quoted
 on (BASELINE.json configs[2] "SwissProt (~560k proteins), trypsin, 2 missed
 cleavages", which fits one MI355X) as a seeded synthetic proteome (SURVEY.md
 §8(d), seed 3).  --config human is configs[1] (20k proteins, seed 2).
-N>1 (torchrun, one rank per GPU): every rank builds its own protein shard of
-the same size (seed + 1000*rank) -> weak scaling, no data-path collective.
+N>1 (torchrun, one rank per GPU): every rank contributes its own protein shard
+of the same size (seed + 1000*rank) -> weak scaling.  One step builds ONE index
+over the proteins of all ranks (dbi_build_sharded): each rank digests its
+shard, routes every record to the rank owning its mass key over RCCL (grouped
+point-to-point sends over xGMI), and each owner sorts + de-duplicates its key
+range.  The residues of every shard are all-gathered into each GPU's HBM once,
+before the timed region (input staging: the owner merge compares peptide
+strings of any shard).  --no-merge: independent shard-local indexes instead.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config swissprot|human|1k]
 Prints ONE JSON line on rank 0.
@@ -62,6 +68,9 @@ def main() -> None:
     ap.add_argument("--config", default="swissprot", choices=sorted(WORKLOADS))
     ap.add_argument("--queries", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-merge", action="store_true",
+                    help="N>1: shard-local indexes (no exchange) instead of one merged index")
+    ap.add_argument("--merge", action="store_true", help="N=1: run the sharded (RCCL) build with one rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,10 +83,11 @@ def main() -> None:
     from dbindex_amd.params import DBIndexSearchParams
 
     dist = None
+    merge = (world > 1 and not args.no_merge) or args.merge
     if world > 1:
-        # coordination only (barrier, max time, sum of counts): the shards are
-        # independent, so there is no data-path collective; gloo keeps torch's
-        # own HIP runtime out of this process (see dbindex_amd/_native.py)
+        # gloo for coordination only (barrier, max time, sums, the RCCL id):
+        # the data path runs over RCCL inside the engine's library, and gloo
+        # keeps torch's own HIP runtime out of this process (dbindex_amd/_native.py)
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -92,15 +102,48 @@ def main() -> None:
     log(f"[rank {rank}] synthetic {args.config}: P={pp.n_proteins} R={pp.n_residues} ({time.time() - t0:.1f}s)")
     prm = DBIndexSearchParams.trypsin(missed)
 
-    # inputs resident in HBM before the timed region
-    d_res = DeviceBuffer.from_numpy(pp.residues, dev)
-    d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), dev)
-    synchronize(dev)
-
     eng = Engine(prm, device=dev)
+    if merge:
+        from dbindex_amd import shard
+        # global layout: every rank's residues and offsets, in rank order
+        sizes = [(pp.n_residues, pp.n_proteins, pp.offsets.astype(np.uint64))] * world
+        if world > 1:
+            dist.all_gather_object(sizes, sizes[0])
+        res_base = np.concatenate([[0], np.cumsum([x[0] for x in sizes])]).astype(np.uint64)
+        prot_base = np.concatenate([[0], np.cumsum([x[1] for x in sizes])]).astype(np.int64)
+        R_all, P_all = int(res_base[-1]), int(prot_base[-1])
+        off_all = np.concatenate([sizes[r][2][:-1] + res_base[r] for r in range(world)] +
+                                 [np.array([R_all], np.uint64)])
+        uid = [shard.ShardComm.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        comm = shard.ShardComm(uid[0], world, rank, dev)
+        # input staging (untimed): every shard's residues into every GPU's HBM
+        d_res = DeviceBuffer(R_all + 16, dev)
+        mine = d_res.ptr + int(res_base[rank])
+        from dbindex_amd._native import lib as _lib
+        import ctypes
+        _lib().dbi_dev_copy_h2d(dev, ctypes.c_void_p(mine), pp.residues.ctypes.data_as(ctypes.c_void_p),
+                                pp.n_residues)
+        t_ag = time.perf_counter()
+        comm.allgatherv(mine, d_res.ptr, [x[0] for x in sizes])
+        t_ag = time.perf_counter() - t_ag
+        d_off = DeviceBuffer.from_numpy(off_all, dev)
+        synchronize(dev)
+        p_begin, p_end = int(prot_base[rank]), int(prot_base[rank + 1])
+        log(f"[rank {rank}] merged index over {P_all} proteins / {R_all} residues; residue all-gather "
+            f"{t_ag * 1e3:.1f} ms")
 
-    def step():
-        return eng.build_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins)
+        def step():
+            return shard.build_sharded(eng, comm, d_res.ptr, R_all, d_off.ptr, P_all, p_begin, p_end)
+    else:
+        # inputs resident in HBM before the timed region
+        d_res = DeviceBuffer.from_numpy(pp.residues, dev)
+        d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), dev)
+        synchronize(dev)
+
+        def step():
+            return eng.build_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins)
 
     def accumulate(acc):
         for name, ms, by in eng.stage_times():
@@ -133,10 +176,13 @@ def main() -> None:
     synchronize(dev)
     t_start = time.perf_counter()
     n_total = 0
+    shard_acc = []
     for _ in range(args.steps):
         st = step()
         n_total += st.n_total
         accumulate(stage_acc)
+        if merge:
+            shard_acc.append((st.digest_ms, st.partition_ms, st.exchange_ms, st.merge_ms))
     synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -181,11 +227,21 @@ def main() -> None:
     kernels = kernel_table(warm_acc, n_warm - skip)
     timed = kernel_table(stage_acc, args.steps)
     dom = timed[0] if timed else None
-    build_alg = st.n_residues + 8.0 * (st.n_proteins + 1) + 48.0 * st.n_total
+    build_alg = pp.n_residues + 8.0 * (pp.n_proteins + 1) + 48.0 * st.n_total  # SURVEY.md §8(d), this rank
+    est = eng.stats()  # merged: this rank's owner slice
+    if merge:
+        unique_all, keys_all = st.g_unique, st.g_keys
+        ph = np.mean(np.array(shard_acc), axis=0) if shard_acc else np.zeros(4)
+        phases = dict(zip(("digest_ms", "partition_ms", "exchange_ms", "merge_ms"), map(float, ph)))
+        phases["residue_allgather_ms_untimed"] = t_ag * 1e3
+        phases["owner_records"] = st.n_received
+        phases["records_sent"] = st.n_sent
+    else:
+        unique_all, keys_all, phases = st.n_unique, st.n_keys, None
 
     # secondary: mass-window queries/sec on the built index (1M queries, +-20 ppm)
     qps = None
-    if args.queries > 0:
+    if args.queries > 0 and not merge:
         ex = eng.export()["mass"]
         rng = np.random.Generator(np.random.PCG64(7 + rank))
         nq = args.queries
@@ -244,11 +300,12 @@ def main() -> None:
                 "proteins_per_gpu": pp.n_proteins,
                 "residues_per_gpu": pp.n_residues,
                 "peptides_per_step_per_gpu": st.n_total,
-                "unique_peptides": st.n_unique,
-                "mass_keys": st.n_keys,
-                "parallelism": f"protein-sharded x{world}, shard-local index" if world > 1 else "single GPU",
-                "n_bins": st.n_bins,
-                "n_big_bins": st.n_big_bins,
+                "unique_peptides": unique_all,
+                "mass_keys": keys_all,
+                "parallelism": (f"protein-sharded x{world}, one index: RCCL owner exchange by mass key" if merge
+                                else f"protein-sharded x{world}, shard-local indexes" if world > 1 else "single GPU"),
+                "n_bins": est.n_bins,
+                "n_big_bins": est.n_big_bins,
             },
             "roofline": None if dom is None else {
                 "bound": "hbm",
@@ -271,6 +328,7 @@ def main() -> None:
             "kernels": kernels,
             "kernels_note": "per-kernel HIP events (dispatch-packet start/stop) over the warmup builds; "
                             "the roofline kernel is re-timed inside the timed region",
+            "sharded_phases": phases,
             "queries": qps,
             "cpu_baseline": cpu,
         }

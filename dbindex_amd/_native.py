@@ -38,6 +38,21 @@ class DbiStats(ctypes.Structure):
     ]
 
 
+class DbiShardStats(ctypes.Structure):
+    _fields_ = [
+        ("rank", c_int32), ("nshards", c_int32), ("p_begin", c_uint64), ("p_end", c_uint64),
+        ("key_lo", c_int32), ("key_hi", c_int32), ("n_total", c_uint64), ("n_dropped", c_uint64),
+        ("n_sent", c_uint64), ("n_received", c_uint64), ("n_unique", c_uint64), ("n_keys", c_uint64),
+        ("g_total", c_uint64), ("g_dropped", c_uint64), ("g_kept", c_uint64), ("g_unique", c_uint64),
+        ("g_keys", c_uint64), ("digest_ms", c_double), ("partition_ms", c_double),
+        ("exchange_ms", c_double), ("merge_ms", c_double),
+    ]
+
+
+SHARD_SAMPLES = 4096  # DBI_SHARD_SAMPLES
+MAX_SHARDS = 64       # DBI_MAX_SHARDS
+
+
 class DbiQueryResult(ctypes.Structure):
     _fields_ = [("nq", c_uint64), ("n_hits", c_uint64), ("row_ptr", POINTER(c_uint64)),
                 ("ids", POINTER(c_uint64))]
@@ -79,6 +94,18 @@ SIGNATURES = [
     ("dbi_device_view", c_int, [P, POINTER(DbiDeviceIndex)]),
     ("dbi_set_timing", c_int, [P, c_int, c_char_p]),
     ("dbi_stage_times", c_int, [P, P, P, P, c_uint64, POINTER(c_uint64)]),
+    ("dbi_shard_digest", c_int, [P, P, c_uint64, P, c_uint64, c_uint64, c_uint64, c_int, c_int]),
+    ("dbi_shard_samples", c_int, [P, P]),
+    ("dbi_shard_splitters", c_int, [P, c_int, c_int32, P]),
+    ("dbi_shard_partition", c_int, [P, P, P]),
+    ("dbi_shard_exchange_local", c_int, [P, c_int]),
+    ("dbi_shard_merge", c_int, [P]),
+    ("dbi_shard_stats_get", c_int, [P, POINTER(DbiShardStats)]),
+    ("dbi_comm_unique_id", c_int, [P]),
+    ("dbi_comm_init", c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
+    ("dbi_comm_destroy", None, [P]),
+    ("dbi_comm_allgatherv", c_int, [P, P, P, P, P]),
+    ("dbi_build_sharded", c_int, [P, P, P, c_uint64, P, c_uint64, c_uint64, c_uint64]),
     ("dbi_store_create", c_int, [POINTER(DbiParams), c_int, POINTER(c_void_p)]),
     ("dbi_store_close", None, [P]),
     ("dbi_store_set_device_digest", c_int, [P, c_int]),

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libdbindex_hip.so")
-SOURCES = ["dbi_device.hip", "dbi_engine.hip", "dbi_store.cpp"]
+SOURCES = ["dbi_device.hip", "dbi_engine.hip", "dbi_shard.hip", "dbi_store.cpp"]
 ARCH = os.environ.get("DBI_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
          "-Wno-unused-result", "-Wshadow", f"--offload-arch={ARCH}"]
@@ -37,7 +37,7 @@ def _newer(target: str, deps) -> bool:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     deps = [os.path.join(CSRC, s) for s in SOURCES]
-    deps += [os.path.join(CSRC, "dbi_internal.h"), os.path.join(ROOT, "include", "dbindex_hip.h")]
+    deps += [os.path.join(CSRC, "dbi_internal.h"), os.path.join(CSRC, "dbi_engine.h"), os.path.join(ROOT, "include", "dbindex_hip.h")]
     if not force and _newer(LIB, deps):
         return LIB
     objdir = os.path.join(HERE, "build")
@@ -62,7 +62,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if out:  # warnings are never silent
             print(out.decode(errors="replace"), file=sys.stderr)
     tmp = LIB + ".tmp"
-    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-L/opt/rocm/lib", "-lrccl",
+           "-Wl,-rpath,/opt/rocm/lib"]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout.decode(errors='replace')}")

@@ -20,6 +20,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <algorithm>
 
 #include "dbi_internal.h"
 
@@ -1028,6 +1029,30 @@ size_t radix_hist_elems(uint32_t n, int bits) {
     return (size_t)g * (size_t)(1u << bits);
 }
 
+// Digit policies of a stable pass: the digit of a record from its mass, and
+// what happens to the record on its way out.
+struct BinDigit {  // LSD radix over the fine mass bin: (bin >> shift) & mask
+    BinMap bm;
+    int shift;
+    uint32_t mask;
+    __device__ __forceinline__ uint32_t operator()(double m) const { return (bin_of(m, bm) >> shift) & mask; }
+    __device__ __forceinline__ void xform(uint4&) const {}
+};
+struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor)
+    OwnerMap om;
+    __device__ __forceinline__ uint32_t operator()(double m) const {
+        const int32_t k = java_d2i(m * (double)om.factor);
+        uint32_t d = 0;
+        for (uint32_t j = 0; j + 1 < om.nshards; ++j) d += k >= om.split[j] ? 1u : 0u;
+        return d;
+    }
+    __device__ __forceinline__ void xform(uint4& r) const {  // local -> global protein id
+        const uint64_t q1 = u4_q1(r) + om.pid_add;
+        r.z = (uint32_t)q1;
+        r.w = (uint32_t)(q1 >> 32);
+    }
+};
+
 // Digit of record r for this pass, and the wave's peers holding the same digit.
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits) {
     uint64_t peers = __ballot(valid);
@@ -1042,12 +1067,11 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits
 // +RADIX_ITEMS*64), item k = lanes' records k*64 + lane: per-wave digit counts
 // accumulate in input order, so ranks are stable with no block barrier inside
 // the item loop.
-template <bool SPARSE>
+template <bool SPARSE, typename Digit>
 __global__ void __launch_bounds__(RADIX_THREADS)
-k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int bits,
-             uint32_t* __restrict__ hist) {
+k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32_t* __restrict__ hist) {
     __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
-    const uint32_t D = 1u << bits, mask = D - 1;
+    const uint32_t D = 1u << bits;
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
     wave_sync();
@@ -1062,7 +1086,7 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int b
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
         const bool valid = i < n && (!SPARSE || qv[k] != REC_SENTINEL);
-        const uint32_t d = (bin_of(q0_mass(qv[k]), bm) >> shift) & mask;
+        const uint32_t d = dig(q0_mass(qv[k]));
         const uint64_t peers = digit_peers(d, valid, bits);
         if (valid && __popcll(peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
         wave_sync();
@@ -1076,16 +1100,16 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, BinMap bm, int shift, int b
     }
 }
 
-template <bool SPARSE>
+template <bool SPARSE, typename Digit>
 __global__ void __launch_bounds__(RADIX_THREADS)
-k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, BinMap bm, int shift,
-                int bits, const uint32_t* __restrict__ offs) {
+k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, Digit dig, int bits,
+                const uint32_t* __restrict__ offs) {
     static_assert(RADIX_D <= RADIX_THREADS, "one digit per thread");
     __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
     __shared__ uint4 stage[RADIX_CHUNK];  // the block's records in digit order
     __shared__ uint32_t gofs[RADIX_D];    // global position of digit d's first record - its local start
     __shared__ uint32_t s_tmp[RADIX_NW + 1];
-    const uint32_t D = 1u << bits, mask = D - 1;
+    const uint32_t D = 1u << bits;
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
     wave_sync();
@@ -1105,7 +1129,7 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, B
         const uint32_t i = base + k * 64 + lane;
         const bool valid = i < n && (!SPARSE || (rv[k].x & rv[k].y) != 0xFFFFFFFFu);
         vmask |= (uint32_t)valid << k;
-        const uint32_t d = (bin_of(u4_mass(rv[k]), bm) >> shift) & mask;
+        const uint32_t d = dig(u4_mass(rv[k]));
         const uint64_t peers = digit_peers(d, valid, bits);
         const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t before = cnt[w][d];
@@ -1145,33 +1169,60 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, B
     __syncthreads();
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
     for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) {
-        const uint4 r = stage[t];
-        out4[gofs[(bin_of(u4_mass(r), bm) >> shift) & mask] + t] = r;
+        uint4 r = stage[t];
+        const uint32_t dr = dig(u4_mass(r));
+        dig.xform(r);
+        out4[gofs[dr] + t] = r;
     }
+}
+
+template <typename Digit>
+static hipError_t radix_hist(const Rec* d_in, uint32_t n, const Digit& dig, int bits, bool sparse, uint32_t* d_hist,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    if (sparse)
+        DBI_LAUNCH((k_radix_hist<true, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, dig, bits, d_hist);
+    else
+        DBI_LAUNCH((k_radix_hist<false, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, dig, bits, d_hist);
+    return hipGetLastError();
+}
+
+template <typename Digit>
+static hipError_t radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const Digit& dig, int bits, bool sparse,
+                                const uint32_t* d_hist, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    if (sparse)
+        DBI_LAUNCH((k_radix_scatter<true, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, dig, bits,
+                   d_hist);
+    else
+        DBI_LAUNCH((k_radix_scatter<false, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, dig, bits,
+                   d_hist);
+    return hipGetLastError();
 }
 
 hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,
                              uint32_t* d_hist, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
-    if (sparse)
-        DBI_LAUNCH(k_radix_hist<true>, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, bm, shift, bits, d_hist);
-    else
-        DBI_LAUNCH(k_radix_hist<false>, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, bm, shift, bits, d_hist);
-    return hipGetLastError();
+    return radix_hist(d_in, n, BinDigit{bm, shift, (1u << bits) - 1}, bits, sparse, d_hist, s);
 }
 
 hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
                                 bool sparse, const uint32_t* d_hist, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
-    if (sparse)
-        DBI_LAUNCH(k_radix_scatter<true>, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, bm, shift, bits,
-                   d_hist);
-    else
-        DBI_LAUNCH(k_radix_scatter<false>, dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, bm, shift, bits,
-                   d_hist);
-    return hipGetLastError();
+    return radix_scatter(d_in, d_out, n, BinDigit{bm, shift, (1u << bits) - 1}, bits, sparse, d_hist, s);
+}
+
+// owner partition of a sharded build: the same stable pass with digit = owner
+// shard of the record's mass key, and the shard's first global protein id
+// folded into every record on the way out
+hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bool sparse, uint32_t* d_hist,
+                             hipStream_t s) {
+    return radix_hist(d_in, n, OwnerDigit{om}, owner_bits(om.nshards), sparse, d_hist, s);
+}
+
+hipError_t launch_owner_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const OwnerMap& om, bool sparse,
+                                const uint32_t* d_hist, hipStream_t s) {
+    return radix_scatter(d_in, d_out, n, OwnerDigit{om}, owner_bits(om.nshards), sparse, d_hist, s);
 }
 
 uint64_t radix_blocks(uint32_t n) { return (n + RADIX_CHUNK - 1) / RADIX_CHUNK; }
@@ -2120,6 +2171,59 @@ __global__ void k_off64_to_32(const uint64_t* __restrict__ in, uint32_t* __restr
 hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
     DBI_LAUNCH(k_off64_to_32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, d_out, n);
+    return hipGetLastError();
+}
+
+}  // namespace dbi
+
+namespace dbi {
+
+// ---------------------------------------------------------------------------
+// sharded build helpers (dbi_shard.hip)
+// ---------------------------------------------------------------------------
+__global__ void k_sample_masses(const Rec* __restrict__ recs, uint64_t n, uint32_t ns, double* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ns) return;
+    const uint64_t j = (uint64_t)(((unsigned __int128)i * n) / ns);
+    const uint64_t q0 = recs[j].q0;
+    out[i] = q0 == REC_SENTINEL ? __builtin_nan("") : q0_mass(q0);
+}
+
+hipError_t launch_sample_masses(const Rec* d_recs, uint64_t n, uint32_t ns, double* d_out, hipStream_t s) {
+    if (ns == 0) return hipSuccess;
+    if (n == 0) return hipMemsetAsync(d_out, 0xFF, sizeof(double) * ns, s);  // all NaN
+    DBI_LAUNCH(k_sample_masses, dim3((ns + 255) / 256), dim3(256), 0, s, d_recs, n, ns, d_out);
+    return hipGetLastError();
+}
+
+__global__ void k_off_rebase(const uint64_t* __restrict__ in, uint64_t base, uint32_t* __restrict__ out, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)(in[i] - base);
+}
+
+hipError_t launch_off_rebase(const uint64_t* d_in, uint64_t base, uint32_t* d_out, uint64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    DBI_LAUNCH(k_off_rebase, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, base, d_out, n);
+    return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) k_max_plen(const uint32_t* __restrict__ poff, uint32_t n_prot,
+                                                  Counters* __restrict__ ctr) {
+    uint32_t m = 0;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n_prot; p += gridDim.x * blockDim.x)
+        m = max(m, poff[p + 1] - poff[p]);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+    __shared__ uint32_t s_max[4];
+    if (lane_id() == 0) s_max[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&ctr->max_plen, max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3])));
+}
+
+hipError_t launch_max_plen(const uint32_t* d_poff, uint32_t n_prot, Counters* d_ctr, hipStream_t s) {
+    if (n_prot == 0) return hipSuccess;
+    const uint32_t g = std::min<uint32_t>((n_prot + 255) / 256, 1024u);
+    DBI_LAUNCH(k_max_plen, dim3(g), dim3(256), 0, s, d_poff, n_prot, d_ctr);
     return hipGetLastError();
 }
 

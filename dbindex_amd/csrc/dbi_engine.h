@@ -1,0 +1,209 @@
+// dbi_engine.h — the engine handle and the build phases shared by the
+// single-device build (dbi_engine.hip) and the sharded build (dbi_shard.hip).
+// Internal: not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "dbi_internal.h"
+
+namespace dbi {
+
+// Growable device buffer.
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;  // elements
+    int ensure(size_t n) {
+        if (n <= cap && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1);
+        hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            return hip_fail(e, "hipMalloc");
+        }
+        cap = want;
+        return 0;
+    }
+    // look-back status words: a fresh allocation may hold words of an earlier
+    // (freed) status array whose epoch tags match; start from zero
+    int ensure_zeroed(size_t n, hipStream_t s) {
+        if (n <= cap && p) return 0;
+        int rc = ensure(n);
+        if (rc) return rc;
+        const hipError_t e = hipMemsetAsync(p, 0, cap * sizeof(T), s);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    size_t bytes() const { return cap * sizeof(T); }
+};
+
+// State of a sharded build on this handle (dbi_shard_* phases, dbi_shard.hip).
+struct ShardState {
+    int phase = 0;  // 0 none, 1 digested, 2 partitioned, 3 exchanged, 4 merged
+    int rank = 0, nshards = 1;
+    uint64_t p_begin = 0, p_end = 0;        // this shard's proteins (global ids)
+    uint64_t n_res_global = 0, n_prot_global = 0;
+    const uint8_t* d_res_global = nullptr;  // every shard's residues (owner merge reads any peptide)
+    uint64_t n_digest = 0, n_in = 0;        // digest records / slots in recA
+    bool sparse = false;
+    uint64_t n_total = 0, n_dropped = 0;    // this shard's digest: totalSeqCount, bucket drops
+    uint32_t width = 0;                     // global record field width W
+    int32_t split[MAX_SHARDS - 1] = {};
+    std::vector<uint64_t> send_count, send_off;  // per owner, records in recB
+    std::vector<uint64_t> recv_count;            // per source shard
+    uint64_t n_recv = 0;
+    double ms_digest = 0, ms_partition = 0, ms_exchange = 0, ms_merge = 0;
+    dbi_shard_stats global{};               // filled by dbi_build_sharded (RCCL sums)
+};
+
+}  // namespace dbi
+
+// the C-ABI handle (include/dbindex_hip.h)
+struct dbi_handle {
+    template <typename T>
+    using DevBuf = dbi::DevBuf<T>;
+    using DevParams = dbi::DevParams;
+    using Counters = dbi::Counters;
+    using Rec = dbi::Rec;
+
+    dbi_params params;
+    DevParams dp;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool timing = true;                  // per-stage kernel-attached events (dbi_set_timing)
+    std::string timing_only;             // "" = every stage
+    std::chrono::steady_clock::time_point t0;
+
+    DevBuf<double> mass_tab;
+    DevBuf<uint8_t> flags_tab;
+    DevBuf<Counters> ctr;
+
+    // inputs (owned copies for host builds)
+    DevBuf<uint8_t> res;
+    DevBuf<uint64_t> poff64;
+    DevBuf<uint32_t> poff;
+    DevBuf<uint32_t> poff_g;            // sharded build: global u32 offsets (owner merge)
+    const uint32_t* d_poff = nullptr;   // offsets the current stage reads (poff or poff_g)
+    const uint8_t* d_res = nullptr;  // residues the index refers to
+    uint64_t n_res = 0, n_prot = 0;
+
+    // workspace
+    DevBuf<uint32_t> blk;       // digest tile counts / offsets
+    DevBuf<unsigned long long> status;  // fused digest: per-tile look-back words
+    uint32_t epoch = 0;                 // tag of the current fused launch in `status`
+    DevBuf<uint32_t> thr;       // digest per-thread counts
+    DevBuf<uint32_t> tile_pf;   // first protein of every digest tile (+1)
+    DevBuf<uint32_t> scan_tmp;
+    DevBuf<Rec> recA, recB;
+    DevBuf<uint32_t> hist;
+    DevBuf<uint32_t> ucount, big_list, giant_list, chunk_lo;
+    DevBuf<unsigned long long> ws_key;
+    DevBuf<uint32_t> ws_k2;
+
+    // index
+    DevBuf<double> umass;
+    DevBuf<uint32_t> upid, uoff, ulen, occ_off, occ_pid;
+    bool built = false;
+
+    // host-input occurrences (addSequence path)
+    DevBuf<double> o_mass;
+    DevBuf<uint32_t> o_pid, o_off, o_len;
+
+    // query scratch
+    DevBuf<double> q_mass, q_tol;
+    DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
+    DevBuf<double> g_mass;
+    DevBuf<uint32_t> g_pid, g_off, g_len;
+    DevBuf<uint64_t> g_b, g_e;
+
+    dbi_stats stats{};
+    dbi::ShardState shard;
+    DevBuf<double> samp;                // sharded build: mass samples (splitters)
+    DevBuf<unsigned long long> xcount;  // sharded build: send counts of every shard (RCCL all-gather)
+    Counters hc{};
+    uint64_t n_total_extra = 0;
+
+    // per-launch HIP events on the engine stream (dbi_stage_times)
+    struct Stage {
+        const char* name;
+        int eb, ee;                     // event pool slots
+        double cR, cN, cU, cP, cB;      // algorithmic bytes = cR*R + cN*N + cU*U + cP*P + cB*nbins
+        double ms, bytes;
+        double c0;                      // + fixed bytes (exchange)
+        bool launched;
+    };
+    static constexpr int MAX_STAGES = 48;
+    hipEvent_t evpool[2 * MAX_STAGES] = {};
+    Stage stages[MAX_STAGES];
+    int nstage = 0;
+};
+
+
+namespace dbi {
+
+struct Bytes {
+    double cR = 0, cN = 0, cU = 0, cP = 0, cB = 0;
+};
+
+inline int stage_begin(dbi_handle* h, const char* name, Bytes b) {
+    if (h->nstage >= dbi_handle::MAX_STAGES) return -1;
+    const int i = h->nstage++;
+    auto& st = h->stages[i];
+    st.name = name;
+    st.eb = 2 * i;
+    st.ee = 2 * i + 1;
+    st.cR = b.cR; st.cN = b.cN; st.cU = b.cU; st.cP = b.cP; st.cB = b.cB;
+    st.ms = 0;
+    st.c0 = 0;
+    st.bytes = 0;
+    st.launched = false;
+    if (h->timing && (h->timing_only.empty() || h->timing_only == name))
+        t_launch_ev = LaunchEvents{h->evpool[st.eb], h->evpool[st.ee]};
+    else
+        t_launch_ev = LaunchEvents{};
+    return i;
+}
+
+inline void stage_end(dbi_handle* h, int i) {
+    // the first launch of the stage consumed `start`: otherwise nothing ran
+    if (i >= 0) h->stages[i].launched = t_launch_ev.stop != nullptr && t_launch_ev.start == nullptr;
+    t_launch_ev = LaunchEvents{};
+}
+
+#define STAGE(h, NAME, BYTES, EXPR)                  \
+    do {                                             \
+        const int _si = stage_begin(h, NAME, BYTES); \
+        const hipError_t _stage_err = (EXPR);        \
+        stage_end(h, _si);                           \
+        DBI_HIP(_stage_err);                         \
+    } while (0)
+
+inline Bytes by(double cR, double cN, double cU, double cP, double cB) {
+    Bytes b;
+    b.cR = cR; b.cN = cN; b.cU = cU; b.cP = cP; b.cB = cB;
+    return b;
+}
+
+int read_counters(dbi_handle* h);
+int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot);
+int prepare_tiles(dbi_handle* h);
+// digest of h->d_res / h->d_poff into recA: *n records (*n_in slots, REC_SENTINEL
+// in the unused ones when *sparse)
+int run_digest(dbi_handle* h, uint64_t* n, uint64_t* n_in, bool* sparse);
+int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse);
+int finish_build(dbi_handle* h);
+
+}  // namespace dbi

@@ -14,7 +14,7 @@
 #include <string>
 #include <vector>
 
-#include "dbi_internal.h"
+#include "dbi_engine.h"
 
 namespace dbi {
 
@@ -30,42 +30,6 @@ int hip_fail(hipError_t e, const char* what) {
     return e == hipErrorOutOfMemory ? DBI_E_OOM : DBI_E_HIP;
 }
 
-// Growable device buffer.
-template <typename T>
-struct DevBuf {
-    T* p = nullptr;
-    size_t cap = 0;  // elements
-    int ensure(size_t n) {
-        if (n <= cap && p) return 0;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(n, 1);
-        hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
-        if (e != hipSuccess) {
-            p = nullptr;
-            return hip_fail(e, "hipMalloc");
-        }
-        cap = want;
-        return 0;
-    }
-    // look-back status words: a fresh allocation may hold words of an earlier
-    // (freed) status array whose epoch tags match; start from zero
-    int ensure_zeroed(size_t n, hipStream_t s) {
-        if (n <= cap && p) return 0;
-        int rc = ensure(n);
-        if (rc) return rc;
-        const hipError_t e = hipMemsetAsync(p, 0, cap * sizeof(T), s);
-        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-    size_t bytes() const { return cap * sizeof(T); }
-};
-
 }  // namespace dbi
 
 using namespace dbi;
@@ -74,74 +38,7 @@ namespace dbi {
 thread_local LaunchEvents t_launch_ev;
 }
 
-struct dbi_handle {
-    dbi_params params;
-    DevParams dp;
-    int device = 0;
-    hipStream_t stream = nullptr;
-    bool timing = true;                  // per-stage kernel-attached events (dbi_set_timing)
-    std::string timing_only;             // "" = every stage
-    std::chrono::steady_clock::time_point t0;
-
-    DevBuf<double> mass_tab;
-    DevBuf<uint8_t> flags_tab;
-    DevBuf<Counters> ctr;
-
-    // inputs (owned copies for host builds)
-    DevBuf<uint8_t> res;
-    DevBuf<uint64_t> poff64;
-    DevBuf<uint32_t> poff;
-    const uint8_t* d_res = nullptr;  // residues the index refers to
-    uint64_t n_res = 0, n_prot = 0;
-
-    // workspace
-    DevBuf<uint32_t> blk;       // digest tile counts / offsets
-    DevBuf<unsigned long long> status;  // fused digest: per-tile look-back words
-    uint32_t epoch = 0;                 // tag of the current fused launch in `status`
-    DevBuf<uint32_t> thr;       // digest per-thread counts
-    DevBuf<uint32_t> tile_pf;   // first protein of every digest tile (+1)
-    DevBuf<uint32_t> scan_tmp;
-    DevBuf<Rec> recA, recB;
-    DevBuf<uint32_t> hist;
-    DevBuf<uint32_t> ucount, big_list, giant_list, chunk_lo;
-    DevBuf<unsigned long long> ws_key;
-    DevBuf<uint32_t> ws_k2;
-
-    // index
-    DevBuf<double> umass;
-    DevBuf<uint32_t> upid, uoff, ulen, occ_off, occ_pid;
-    bool built = false;
-
-    // host-input occurrences (addSequence path)
-    DevBuf<double> o_mass;
-    DevBuf<uint32_t> o_pid, o_off, o_len;
-
-    // query scratch
-    DevBuf<double> q_mass, q_tol;
-    DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
-    DevBuf<double> g_mass;
-    DevBuf<uint32_t> g_pid, g_off, g_len;
-    DevBuf<uint64_t> g_b, g_e;
-
-    dbi_stats stats{};
-    Counters hc{};
-    uint64_t n_total_extra = 0;
-
-    // per-launch HIP events on the engine stream (dbi_stage_times)
-    struct Stage {
-        const char* name;
-        int eb, ee;                     // event pool slots
-        double cR, cN, cU, cP, cB;      // algorithmic bytes = cR*R + cN*N + cU*U + cP*P + cB*nbins
-        double ms, bytes;
-        bool launched;
-    };
-    static constexpr int MAX_STAGES = 48;
-    hipEvent_t evpool[2 * MAX_STAGES] = {};
-    Stage stages[MAX_STAGES];
-    int nstage = 0;
-};
-
-namespace {
+namespace dbi {
 
 int check_params(const dbi_params* p) {
     if (!p) return set_error(DBI_E_INVALID, "params is NULL");
@@ -208,48 +105,6 @@ int read_counters(dbi_handle* h) {
     return 0;
 }
 
-struct Bytes {
-    double cR = 0, cN = 0, cU = 0, cP = 0, cB = 0;
-};
-
-int stage_begin(dbi_handle* h, const char* name, Bytes b) {
-    if (h->nstage >= dbi_handle::MAX_STAGES) return -1;
-    const int i = h->nstage++;
-    auto& st = h->stages[i];
-    st.name = name;
-    st.eb = 2 * i;
-    st.ee = 2 * i + 1;
-    st.cR = b.cR; st.cN = b.cN; st.cU = b.cU; st.cP = b.cP; st.cB = b.cB;
-    st.ms = 0;
-    st.bytes = 0;
-    st.launched = false;
-    if (h->timing && (h->timing_only.empty() || h->timing_only == name))
-        t_launch_ev = LaunchEvents{h->evpool[st.eb], h->evpool[st.ee]};
-    else
-        t_launch_ev = LaunchEvents{};
-    return i;
-}
-
-void stage_end(dbi_handle* h, int i) {
-    // the first launch of the stage consumed `start`: otherwise nothing ran
-    if (i >= 0) h->stages[i].launched = t_launch_ev.stop != nullptr && t_launch_ev.start == nullptr;
-    t_launch_ev = LaunchEvents{};
-}
-
-#define STAGE(h, NAME, BYTES, EXPR)                  \
-    do {                                             \
-        const int _si = stage_begin(h, NAME, BYTES); \
-        const hipError_t _stage_err = (EXPR);        \
-        stage_end(h, _si);                           \
-        DBI_HIP(_stage_err);                         \
-    } while (0)
-
-Bytes by(double cR, double cN, double cU, double cP, double cB) {
-    Bytes b;
-    b.cR = cR; b.cN = cN; b.cU = cU; b.cP = cP; b.cB = cB;
-    return b;
-}
-
 // Steps 4-6 over n records in recA: partition by mass bin, per-bin sort +
 // dedup, finalize.  lo/hi bound every record mass.  sparse: recA holds n_in
 // slots, n of them records and the rest REC_SENTINEL (bounded digest); the
@@ -308,13 +163,13 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
           launch_chunk_bounds(src, n32, bm, CHUNK_T, nchunks, h->chunk_lo.p, s));
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
-          launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->poff.p, h->ucount.p, h->big_list.p,
+          launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                             h->ctr.p, s));
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
-          launch_chunk_sort_big(src, dst, h->chunk_lo.p, h->d_res, h->poff.p, h->ucount.p, h->big_list.p,
+          launch_chunk_sort_big(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                                 h->giant_list.p, std::min<uint32_t>(nchunks, 256u), h->ctr.p, s));
     STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
-          launch_big_chunks(src, dst, h->chunk_lo.p, h->d_res, h->poff.p, h->ucount.p, h->giant_list.p,
+          launch_big_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,
                             std::min<uint32_t>(nchunks, 256u), h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
     // unique offsets per chunk
     STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
@@ -354,10 +209,10 @@ int finish_build(dbi_handle* h) {
         sg.ms = t;
         if (std::strncmp(sg.name, "digest", 6) == 0) st.digest_ms += t;
         sg.bytes = sg.cR * (double)h->n_res + sg.cN * (double)st.n_kept + sg.cU * (double)st.n_unique +
-                   sg.cP * (double)(h->n_prot + 1) + sg.cB * (double)st.n_bins;
+                   sg.cP * (double)(h->n_prot + 1) + sg.cB * (double)st.n_bins + sg.c0;
     }
     size_t bytes = 0;
-    bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
+    bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->poff_g.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
     bytes += h->thr.bytes() + h->tile_pf.bytes() + h->chunk_lo.bytes();
     bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->ucount.bytes();
     bytes += h->big_list.bytes() + h->giant_list.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
@@ -373,13 +228,13 @@ int prepare_tiles(dbi_handle* h) {
     int rc;
     if ((rc = h->tile_pf.ensure((size_t)ntiles + 2))) return rc;
     STAGE(h, "tile_proteins", by(0, 0, 0, 4, 0),
-          launch_tile_proteins(h->poff.p, (uint32_t)h->n_prot, (uint32_t)h->n_res, h->tile_pf.p, h->ctr.p,
+          launch_tile_proteins(h->d_poff, (uint32_t)h->n_prot, (uint32_t)h->n_res, h->tile_pf.p, h->ctr.p,
                                h->stream));
     return 0;
 }
 
-// Device digest build over residues at d_res (n_res) with u32 offsets in h->poff.
-int build_digest(dbi_handle* h) {
+// Device digest over residues at d_res (n_res) with u32 offsets at h->d_poff.
+int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_out) {
     hipStream_t s = h->stream;
     int rc;
     const uint64_t R = h->n_res;
@@ -405,12 +260,12 @@ int build_digest(dbi_handle* h) {
             const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
             if (bounded)
                 STAGE(h, "digest", by(1, 16, 0, 4, 0),
-                      launch_digest_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p,
+                      launch_digest_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
                                             (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->status.p, h->epoch,
                                             h->recA.p, cap, h->ctr.p, s));
             else
                 STAGE(h, "digest", by(1, 16, 0, 4, 0),
-                      launch_digest_fused(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p,
+                      launch_digest_fused(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
                                           (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->status.p, h->epoch,
                                           h->recA.p, (uint32_t)cap, h->ctr.p, s));
             if ((rc = read_counters(h))) return rc;
@@ -425,11 +280,16 @@ int build_digest(dbi_handle* h) {
             // counters back to zero, except the record layout (max_plen) set by prepare_tiles
             DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
         }
-        if (bounded) return build_tail(h, n, h->params.min_mh, h->params.max_mh, h->hc.n_slots, true);
+        if (bounded) {
+            *n_out = n;
+            *n_in_out = h->hc.n_slots;
+            *sparse_out = true;
+            return 0;
+        }
     } else {
         // cold: count, scan, size the output, emit
         STAGE(h, "digest_count", by(1, 0, 0, 4, 0),
-              launch_digest_count(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
+              launch_digest_count(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff, (uint32_t)h->n_prot,
                                   (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->ctr.p, s));
         STAGE(h, "digest_scan", by(0, 0, 0, 0, 0),
               launch_scan_u32(h->blk.p, h->blk.p, nblk, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_kept, s));
@@ -440,10 +300,21 @@ int build_digest(dbi_handle* h) {
         if ((rc = h->recA.ensure(n))) return rc;
         // digest emit: residues in, one 16-B record per kept occurrence out
         STAGE(h, "digest_emit", by(1, 16, 0, 4, 0),
-              launch_digest_emit(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->poff.p, (uint32_t)h->n_prot,
+              launch_digest_emit(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff, (uint32_t)h->n_prot,
                                  (uint32_t)R, h->tile_pf.p, h->blk.p, h->thr.p, h->recA.p, h->ctr.p, s));
     }
-    return build_tail(h, n, h->params.min_mh, h->params.max_mh, n, false);
+    *n_out = n;
+    *n_in_out = n;
+    *sparse_out = false;
+    return 0;
+}
+
+int build_digest(dbi_handle* h) {
+    uint64_t n = 0, n_in = 0;
+    bool sparse = false;
+    int rc = run_digest(h, &n, &n_in, &sparse);
+    if (rc) return rc;
+    return build_tail(h, n, h->params.min_mh, h->params.max_mh, n_in, sparse);
 }
 
 int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
@@ -451,6 +322,7 @@ int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
     if (n_prot >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_prot must be < 2^32-1");
     DBI_HIP(hipSetDevice(h->device));
     h->built = false;
+    h->shard.phase = 0;
     h->n_res = n_res;
     h->n_prot = n_prot;
     h->n_total_extra = 0;
@@ -485,6 +357,7 @@ int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const 
     DBI_HIP(hipMemcpyAsync(h->poff.p, off32.data(), sizeof(uint32_t) * (n_prot + 1), hipMemcpyHostToDevice, h->stream));
     DBI_HIP(hipStreamSynchronize(h->stream));  // off32 is a stack vector
     h->d_res = h->res.p;
+    h->d_poff = h->poff.p;
     return 0;
 }
 
@@ -600,7 +473,8 @@ void dbi_close(dbi_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
-    h->res.release(); h->poff64.release(); h->poff.release(); h->blk.release(); h->scan_tmp.release();
+    h->res.release(); h->poff64.release(); h->poff.release(); h->poff_g.release();
+    h->samp.release(); h->xcount.release(); h->blk.release(); h->scan_tmp.release();
     h->status.release();
     h->thr.release(); h->tile_pf.release(); h->chunk_lo.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
@@ -644,6 +518,7 @@ int dbi_build_device(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, c
     if ((rc = h->poff.ensure(n_prot + 1))) return rc;
     DBI_HIP(launch_off64_to_32(d_prot_off, h->poff.p, n_prot + 1, h->stream));
     h->d_res = d_residues;
+    h->d_poff = h->poff.p;
     if ((rc = build_digest(h))) return rc;
     return finish_build(h);
 }
@@ -679,7 +554,7 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
         DBI_HIP(hipMemcpyAsync(h->o_len.p, length, 4 * n_occ, hipMemcpyHostToDevice, h->stream));
     }
     if ((rc = prepare_tiles(h))) return rc;  // record layout first
-    DBI_HIP(launch_occ_to_recs(h->o_mass.p, h->o_pid.p, h->o_off.p, h->o_len.p, h->poff.p, h->d_res, n_occ, n_prot,
+    DBI_HIP(launch_occ_to_recs(h->o_mass.p, h->o_pid.p, h->o_off.p, h->o_len.p, h->d_poff, h->d_res, n_occ, n_prot,
                                h->recA.p, h->ctr.p, h->stream));
     // n_kept known on the host: seed the device counter
     const unsigned long long kept = n_occ;

@@ -176,12 +176,39 @@ struct BinMap {
     double scale;     // nbins / (hi - lo)
     uint32_t nbins;
 };
+// Owner map of a sharded build (dbi_shard_*): shard d owns the mass keys
+// (int)(m * factor) in [split[d-1], split[d]) (split[-1] = -inf, split[n-1] =
+// +inf), so a key, and every occurrence of a peptide, has exactly one owner.
+// pid_add = (first global protein id of the sending shard) << 2W.
+constexpr int MAX_SHARDS = 64;
+struct OwnerMap {
+    int32_t split[MAX_SHARDS - 1];
+    uint32_t nshards;
+    int32_t factor;
+    uint64_t pid_add;
+};
+inline int owner_bits(uint32_t nshards) {
+    int b = 0;
+    while ((1u << b) < nshards) ++b;
+    return b;
+}
 // sparse: the input holds REC_SENTINEL slots (bounded digest), left out of the output
 hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,
                              uint32_t* d_hist, hipStream_t s);
 hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
                                 bool sparse, const uint32_t* d_hist, hipStream_t s);
 uint64_t radix_blocks(uint32_t n);
+// stable partition pass by owner shard (digit = OwnerDigit), global protein ids out
+hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bool sparse, uint32_t* d_hist,
+                             hipStream_t s);
+hipError_t launch_owner_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const OwnerMap& om, bool sparse,
+                                const uint32_t* d_hist, hipStream_t s);
+// out[i] = mass of slot i * n / ns (NaN for a sentinel slot), i < ns
+hipError_t launch_sample_masses(const Rec* d_recs, uint64_t n, uint32_t ns, double* d_out, hipStream_t s);
+// out[i] = in[i] - base (u64 -> u32 offsets of a protein range)
+hipError_t launch_off_rebase(const uint64_t* d_in, uint64_t base, uint32_t* d_out, uint64_t n, hipStream_t s);
+// ctr->max_plen = max(ctr->max_plen, longest protein of poff[0..n_prot])
+hipError_t launch_max_plen(const uint32_t* d_poff, uint32_t n_prot, Counters* d_ctr, hipStream_t s);
 size_t radix_hist_elems(uint32_t n, int bits);
 // chunk_lo[c] = first bin start at or after c*T in the bin-sorted records (nchunks+1 entries)
 hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,

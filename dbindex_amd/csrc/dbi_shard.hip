@@ -1,0 +1,505 @@
+// dbi_shard.hip — sharded build: one index over the proteins of every shard.
+//
+// The reference builds one index over the whole FASTA in one thread
+// (DBIndexer.run, DBIndexer.java:508-684).  Here the proteome is split into
+// contiguous protein ranges, one per GPU.  Each shard digests its own proteins
+// (cutSeq, DBIndexer.java:237-405), then every record goes to the shard that
+// OWNS its mass key (int)(mass*factor) (DBIndexStoreSQLiteByte.java:187): the
+// owners hold contiguous key ranges, so the same peptide — same string, same
+// bit-identical mass, same key — from any shard meets at one owner, which
+// sorts, de-duplicates and finalises its range exactly like a single-device
+// build (IndexMerge.getMergedData, DBIndexStoreSQLiteByteIndexMerge.java:620-719).
+// The record carries (mass, tag, global protein id, offset, length), and the
+// owner's result is a pure function of the set of records it receives, so the
+// order in which shards' records arrive does not matter.
+//
+// Exchange: RCCL point-to-point sends/receives grouped over all peers (each
+// pair of MI355X GPUs has its own xGMI link, so the grouped exchange drives
+// all links at once; a ring would serialise them), or device copies between
+// the handles of one process (dbi_shard_exchange_local).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstddef>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "dbi_engine.h"
+
+using namespace dbi;
+
+struct dbi_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1;
+    int rank = 0;
+    int device = 0;
+};
+
+namespace dbi {
+namespace {
+
+constexpr uint32_t NS = DBI_SHARD_SAMPLES;
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int nccl_fail(ncclResult_t r, const char* what) {
+    return set_error(DBI_E_RCCL, std::string("RCCL error ") + ncclGetErrorString(r) + " in " + what);
+}
+
+#define DBI_NCCL(expr)                                        \
+    do {                                                      \
+        ncclResult_t _r = (expr);                             \
+        if (_r != ncclSuccess) return nccl_fail(_r, #expr);   \
+    } while (0)
+
+int need_phase(const dbi_handle* h, int phase, const char* what) {
+    if (h->shard.phase != phase)
+        return set_error(DBI_E_STATE, std::string(what) + ": sharded build phases must run in order "
+                                                          "(digest, samples/splitters, partition, exchange, merge)");
+    return 0;
+}
+
+// Stage whose time comes from events recorded around non-kernel work (RCCL,
+// copies) rather than from a dispatch packet; `bytes` = bytes this rank moves.
+struct ManualStage {
+    dbi_handle* h;
+    int i;
+    hipEvent_t e1 = nullptr;
+    ManualStage(dbi_handle* hh, const char* name, double bytes) : h(hh) {
+        i = stage_begin(h, name, by(0, 0, 0, 0, 0));
+        hipEvent_t e0 = t_launch_ev.start;
+        e1 = t_launch_ev.stop;
+        t_launch_ev = LaunchEvents{};
+        if (i >= 0) {
+            h->stages[i].c0 = bytes;
+            h->stages[i].launched = e0 != nullptr && hipEventRecord(e0, h->stream) == hipSuccess;
+        }
+    }
+    void end() {
+        if (i >= 0 && h->stages[i].launched && e1) h->stages[i].launched = hipEventRecord(e1, h->stream) == hipSuccess;
+    }
+};
+
+// owner key range of shard r under `split`
+void key_range(const int32_t* split, int nshards, int r, int32_t* lo, int32_t* hi) {
+    *lo = r == 0 ? INT32_MIN : split[r - 1];
+    *hi = r == nshards - 1 ? INT32_MAX : split[r];
+}
+
+}  // namespace
+}  // namespace dbi
+
+extern "C" {
+
+int dbi_shard_digest(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_poff, uint64_t n_prot,
+                     uint64_t p_begin, uint64_t p_end, int rank, int nshards) {
+    if (!h || (!d_res && n_res) || !d_poff) return set_error(DBI_E_INVALID, "NULL argument");
+    if (nshards < 1 || nshards > MAX_SHARDS || rank < 0 || rank >= nshards)
+        return set_error(DBI_E_INVALID, "shard rank / count out of range (1..64 shards)");
+    if (p_begin > p_end || p_end > n_prot) return set_error(DBI_E_INVALID, "shard protein range out of bounds");
+    int rc;
+    if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    const double t0 = now_ms();
+    hipStream_t s = h->stream;
+    uint64_t ends[2] = {0, 0};
+    DBI_HIP(hipMemcpyAsync(&ends[0], d_poff + p_begin, 8, hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipMemcpyAsync(&ends[1], d_poff + p_end, 8, hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    if (ends[0] > ends[1] || ends[1] > n_res) return set_error(DBI_E_INVALID, "prot_off is not a valid offset table");
+    const uint64_t np = p_end - p_begin;
+    if ((rc = h->poff_g.ensure(n_prot + 1)) || (rc = h->poff.ensure(np + 1))) return rc;
+    // global u32 offsets (owner merge) + this shard's offsets rebased to its first residue
+    DBI_HIP(launch_off_rebase(d_poff, 0, h->poff_g.p, n_prot + 1, s));
+    DBI_HIP(launch_off_rebase(d_poff + p_begin, ends[0], h->poff.p, np + 1, s));
+    // the record field width W comes from the longest protein of the WHOLE
+    // proteome, so every shard packs records the same way
+    DBI_HIP(launch_max_plen(h->poff_g.p, (uint32_t)n_prot, h->ctr.p, s));
+
+    ShardState& sh = h->shard;
+    sh = ShardState{};
+    sh.rank = rank;
+    sh.nshards = nshards;
+    sh.p_begin = p_begin;
+    sh.p_end = p_end;
+    sh.n_res_global = n_res;
+    sh.n_prot_global = n_prot;
+    sh.d_res_global = d_res;
+    h->d_res = d_res + ends[0];
+    h->d_poff = h->poff.p;
+    h->n_res = ends[1] - ends[0];
+    h->n_prot = np;
+    uint64_t n = 0, n_in = 0;
+    bool sparse = false;
+    if (h->n_res > 0) {
+        if ((rc = run_digest(h, &n, &n_in, &sparse))) return rc;
+    } else if ((rc = read_counters(h))) {
+        return rc;
+    }
+    if (h->hc.err & ERR_LAYOUT) return set_error(DBI_E_INVALID, "record layout overflow in the shard digest");
+    // the digest stages' algorithmic bytes are this shard's (the handle turns
+    // into the owner of a slice of the whole proteome at the merge)
+    for (int i = 0; i < h->nstage; ++i) {
+        auto& st = h->stages[i];
+        st.c0 += st.cR * (double)h->n_res + st.cN * (double)h->hc.n_kept + st.cP * (double)(np + 1);
+        st.cR = st.cN = st.cU = st.cP = st.cB = 0;
+    }
+    sh.width = rec_width(h->hc.max_plen);
+    if (!rec_layout_ok(sh.width, n_prot))
+        return set_error(DBI_E_INVALID, "2 x bits(longest protein) + bits(protein count) of the whole proteome "
+                                        "exceeds the 56 bits of the 16-B occurrence record");
+    sh.n_digest = n;
+    sh.n_in = n_in;
+    sh.sparse = sparse;
+    sh.n_total = h->hc.n_kept + h->hc.n_dropped;
+    sh.n_dropped = h->hc.n_dropped;
+    sh.ms_digest = now_ms() - t0;
+    sh.phase = 1;
+    return 0;
+}
+
+int dbi_shard_samples(dbi_handle* h, double* samples) {
+    if (!h || !samples) return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = need_phase(h, 1, "dbi_shard_samples"))) return rc;
+    if ((rc = h->samp.ensure(NS))) return rc;
+    DBI_HIP(launch_sample_masses(h->recA.p, h->shard.n_in, NS, h->samp.p, h->stream));
+    DBI_HIP(hipMemcpyAsync(samples, h->samp.p, sizeof(double) * NS, hipMemcpyDeviceToHost, h->stream));
+    DBI_HIP(hipStreamSynchronize(h->stream));
+    uint64_t valid = 0;
+    for (uint32_t i = 0; i < NS; ++i) valid += samples[i] == samples[i];
+    samples[NS] = valid ? (double)h->shard.n_digest / (double)valid : 0.0;
+    return 0;
+}
+
+int dbi_shard_splitters(const double* samples, int nshards, int32_t factor, int32_t* split) {
+    if (!samples || (!split && nshards > 1)) return set_error(DBI_E_INVALID, "NULL argument");
+    if (nshards < 1 || nshards > MAX_SHARDS) return set_error(DBI_E_INVALID, "1..64 shards");
+    if (factor <= 0) return set_error(DBI_E_INVALID, "mass_group_factor must be > 0");
+    std::vector<std::pair<int32_t, double>> ks;
+    for (int r = 0; r < nshards; ++r) {
+        const double* b = samples + (size_t)r * (NS + 1);
+        const double w = b[NS];
+        if (!(w > 0.0)) continue;
+        for (uint32_t i = 0; i < NS; ++i)
+            if (b[i] == b[i]) ks.emplace_back(java_d2i(b[i] * (double)factor), w);
+    }
+    std::sort(ks.begin(), ks.end());
+    double total = 0.0;
+    for (const auto& k : ks) total += k.second;
+    // split[j-1] = first key whose preceding weight reaches j/n of the total
+    size_t i = 0;
+    double cum = 0.0;
+    for (int j = 1; j < nshards; ++j) {
+        const double target = total * (double)j / (double)nshards;
+        int32_t sp = INT32_MAX;
+        for (; i < ks.size(); ++i) {
+            if (cum >= target && (i == 0 || ks[i].first != ks[i - 1].first)) {
+                sp = ks[i].first;
+                break;
+            }
+            cum += ks[i].second;
+        }
+        split[j - 1] = sp;
+    }
+    return 0;
+}
+
+int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_count) {
+    if (!h || (!split && h->shard.nshards > 1)) return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = need_phase(h, 1, "dbi_shard_partition"))) return rc;
+    ShardState& sh = h->shard;
+    const int ns = sh.nshards;
+    for (int j = 0; j + 2 < ns; ++j)
+        if (split[j] > split[j + 1]) return set_error(DBI_E_INVALID, "splitter keys must be non-decreasing");
+    const double t0 = now_ms();
+    hipStream_t s = h->stream;
+    OwnerMap om{};
+    for (int j = 0; j + 1 < ns; ++j) om.split[j] = sh.split[j] = split[j];
+    om.nshards = (uint32_t)ns;
+    om.factor = h->params.mass_group_factor;
+    om.pid_add = sh.p_begin << (2 * sh.width);
+    const int bits = owner_bits((uint32_t)ns);
+    const uint32_t n_in = (uint32_t)sh.n_in;
+    const uint64_t g = radix_blocks(n_in);
+    const size_t hist_elems = std::max<size_t>(radix_hist_elems(n_in, bits), 1);
+    if ((rc = h->hist.ensure(hist_elems)) || (rc = h->recB.ensure(std::max<uint64_t>(sh.n_digest, 1))) ||
+        (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(hist_elems), h->scan_tmp.cap))))
+        return rc;
+    std::vector<uint32_t> start(ns + 1, 0);
+    if (n_in > 0) {
+        STAGE(h, "owner_hist", by(0, 0, 0, 0, 0), launch_owner_hist(h->recA.p, n_in, om, sh.sparse, h->hist.p, s));
+        h->stages[h->nstage - 1].c0 = 8.0 * (double)n_in;
+        STAGE(h, "owner_scan", by(0, 0, 0, 0, 0),
+              launch_scan_u32(h->hist.p, h->hist.p, g << bits, h->scan_tmp.p, h->scan_tmp.cap, nullptr, s));
+        STAGE(h, "owner_scatter", by(0, 0, 0, 0, 0),
+              launch_owner_scatter(h->recA.p, h->recB.p, n_in, om, sh.sparse, h->hist.p, s));
+        h->stages[h->nstage - 1].c0 = 16.0 * (double)(sh.sparse ? n_in : sh.n_digest) + 16.0 * (double)sh.n_digest;
+        // first output position of every owner's run: hist[d * g] after the scan
+        DBI_HIP(hipMemcpy2DAsync(start.data(), sizeof(uint32_t), h->hist.p, g * sizeof(uint32_t), sizeof(uint32_t),
+                                 (size_t)ns, hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipStreamSynchronize(s));
+    }
+    start[ns] = (uint32_t)sh.n_digest;
+    sh.send_count.assign(ns, 0);
+    sh.send_off.assign(ns, 0);
+    for (int d = 0; d < ns; ++d) {
+        sh.send_off[d] = start[d];
+        sh.send_count[d] = (uint64_t)start[d + 1] - start[d];
+        if (send_count) send_count[d] = sh.send_count[d];
+    }
+    sh.ms_partition = now_ms() - t0;
+    sh.phase = 2;
+    return 0;
+}
+
+int dbi_shard_exchange_local(dbi_handle* const* hs, int nshards) {
+    if (!hs || nshards < 1) return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    for (int i = 0; i < nshards; ++i) {
+        if (!hs[i]) return set_error(DBI_E_INVALID, "NULL handle");
+        if ((rc = need_phase(hs[i], 2, "dbi_shard_exchange_local"))) return rc;
+        if (hs[i]->shard.nshards != nshards || hs[i]->shard.rank != i)
+            return set_error(DBI_E_INVALID, "hs[i] must be shard i of nshards");
+    }
+    for (int j = 0; j < nshards; ++j) {
+        dbi_handle* o = hs[j];
+        const double t0 = now_ms();
+        ShardState& sh = o->shard;
+        sh.recv_count.assign(nshards, 0);
+        uint64_t tot = 0, from_others = 0;
+        for (int i = 0; i < nshards; ++i) {
+            sh.recv_count[i] = hs[i]->shard.send_count[j];
+            tot += sh.recv_count[i];
+            if (i != j) from_others += sh.recv_count[i];
+        }
+        DBI_HIP(hipSetDevice(o->device));
+        DBI_HIP(hipStreamSynchronize(o->stream));  // recA (the digest slots) is free: partition read it
+        if ((rc = o->recA.ensure(std::max<uint64_t>(tot, 1)))) return rc;
+        ManualStage ms(o, "exchange", 16.0 * (double)(from_others + (sh.n_digest - sh.send_count[j])));
+        uint64_t off = 0;
+        for (int i = 0; i < nshards; ++i) {
+            const uint64_t c = sh.recv_count[i];
+            if (c)
+                DBI_HIP(hipMemcpyAsync(o->recA.p + off, hs[i]->recB.p + hs[i]->shard.send_off[j], c * sizeof(Rec),
+                                       hipMemcpyDeviceToDevice, o->stream));
+            off += c;
+        }
+        ms.end();
+        DBI_HIP(hipStreamSynchronize(o->stream));
+        sh.n_recv = tot;
+        sh.ms_exchange = now_ms() - t0;
+    }
+    for (int j = 0; j < nshards; ++j) hs[j]->shard.phase = 3;
+    return 0;
+}
+
+int dbi_shard_merge(dbi_handle* h) {
+    if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    int rc;
+    if ((rc = need_phase(h, 3, "dbi_shard_merge"))) return rc;
+    ShardState& sh = h->shard;
+    const double t0 = now_ms();
+    DBI_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    // from here on the handle describes the owner's slice of the whole proteome
+    h->d_res = sh.d_res_global;
+    h->d_poff = h->poff_g.p;
+    h->n_res = sh.n_res_global;
+    h->n_prot = sh.n_prot_global;
+    h->n_total_extra = 0;
+    // counters back to zero (the layout word max_plen stays), n_kept = records received
+    DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
+    const unsigned long long kept = sh.n_recv;
+    DBI_HIP(hipMemcpyAsync(&h->ctr.p->n_kept, &kept, sizeof(kept), hipMemcpyHostToDevice, s));
+    DBI_HIP(hipStreamSynchronize(s));  // `kept` is a stack value
+    int32_t klo, khi;
+    key_range(sh.split, sh.nshards, sh.rank, &klo, &khi);
+    const double f = (double)h->params.mass_group_factor;
+    const double lo = klo == INT32_MIN ? h->params.min_mh : std::max(h->params.min_mh, (double)klo / f);
+    const double hi = khi == INT32_MAX ? h->params.max_mh : std::min(h->params.max_mh, (double)khi / f);
+    if ((rc = build_tail(h, sh.n_recv, lo, std::max(hi, lo), sh.n_recv, false))) return rc;
+    if ((rc = finish_build(h))) return rc;
+    sh.ms_merge = now_ms() - t0;
+    sh.phase = 4;
+    return 0;
+}
+
+int dbi_shard_stats_get(dbi_handle* h, dbi_shard_stats* out) {
+    if (!h || !out) return set_error(DBI_E_INVALID, "NULL argument");
+    const ShardState& sh = h->shard;
+    if (sh.phase < 1) return set_error(DBI_E_STATE, "no sharded build on this handle");
+    dbi_shard_stats st = sh.global;
+    st.rank = sh.rank;
+    st.nshards = sh.nshards;
+    st.p_begin = sh.p_begin;
+    st.p_end = sh.p_end;
+    key_range(sh.split, sh.nshards, sh.rank, &st.key_lo, &st.key_hi);
+    st.n_total = sh.n_total;
+    st.n_dropped = sh.n_dropped;
+    st.n_sent = sh.phase >= 2 ? sh.n_digest - sh.send_count[sh.rank] : 0;
+    st.n_received = sh.n_recv;
+    st.n_unique = sh.phase >= 4 ? h->stats.n_unique : 0;
+    st.n_keys = sh.phase >= 4 ? h->stats.n_keys : 0;
+    st.digest_ms = sh.ms_digest;
+    st.partition_ms = sh.ms_partition;
+    st.exchange_ms = sh.ms_exchange;
+    st.merge_ms = sh.ms_merge;
+    *out = st;
+    return 0;
+}
+
+// ---- RCCL -------------------------------------------------------------------------
+
+int dbi_comm_unique_id(uint8_t* id128) {
+    if (!id128) return set_error(DBI_E_INVALID, "NULL argument");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId id;
+    DBI_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(id128, &id, sizeof(id));
+    return 0;
+}
+
+int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_comm** out) {
+    if (!id128 || !out) return set_error(DBI_E_INVALID, "NULL argument");
+    *out = nullptr;
+    if (nranks < 1 || nranks > MAX_SHARDS || rank < 0 || rank >= nranks)
+        return set_error(DBI_E_INVALID, "rank / nranks out of range (1..64 ranks)");
+    DBI_HIP(hipSetDevice(device));
+    ncclUniqueId id;
+    std::memcpy(&id, id128, sizeof(id));
+    dbi_comm* c = new dbi_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return nccl_fail(r, "ncclCommInitRank");
+    }
+    *out = c;
+    return 0;
+}
+
+void dbi_comm_destroy(dbi_comm* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    delete c;
+}
+
+int dbi_comm_allgatherv(dbi_comm* c, const void* d_send, void* d_recv, const uint64_t* rank_bytes, void* stream) {
+    if (!c || !d_recv || !rank_bytes) return set_error(DBI_E_INVALID, "NULL argument");
+    DBI_HIP(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<uint64_t> off(c->nranks + 1, 0);
+    for (int r = 0; r < c->nranks; ++r) off[r + 1] = off[r] + rank_bytes[r];
+    uint8_t* recv = static_cast<uint8_t*>(d_recv);
+    uint8_t* mine = recv + off[c->rank];
+    const uint64_t my_bytes = rank_bytes[c->rank];
+    if (d_send && d_send != mine && my_bytes)
+        DBI_HIP(hipMemcpyAsync(mine, d_send, my_bytes, hipMemcpyDeviceToDevice, s));
+    DBI_NCCL(ncclGroupStart());
+    for (int p = 0; p < c->nranks; ++p) {
+        if (p == c->rank) continue;
+        if (my_bytes) DBI_NCCL(ncclSend(mine, my_bytes, ncclUint8, p, c->comm, s));
+        if (rank_bytes[p]) DBI_NCCL(ncclRecv(recv + off[p], rank_bytes[p], ncclUint8, p, c->comm, s));
+    }
+    DBI_NCCL(ncclGroupEnd());
+    DBI_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_poff,
+                      uint64_t n_prot, uint64_t p_begin, uint64_t p_end) {
+    if (!h || !c) return set_error(DBI_E_INVALID, "NULL argument");
+    if (c->device != h->device) return set_error(DBI_E_INVALID, "communicator and engine on different devices");
+    const int n = c->nranks, me = c->rank;
+    int rc;
+    if ((rc = dbi_shard_digest(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n))) return rc;
+    ShardState& sh = h->shard;
+    hipStream_t s = h->stream;
+
+    // samples of every shard -> the same owner splitters everywhere
+    const size_t blk = NS + 1;
+    std::vector<double> samples((size_t)n * blk);
+    if ((rc = dbi_shard_samples(h, samples.data() + (size_t)me * blk))) return rc;
+    if ((rc = h->samp.ensure((size_t)n * blk))) return rc;
+    DBI_HIP(hipMemcpyAsync(h->samp.p + (size_t)me * blk, samples.data() + (size_t)me * blk, sizeof(double) * blk,
+                           hipMemcpyHostToDevice, s));
+    DBI_NCCL(ncclAllGather(h->samp.p + (size_t)me * blk, h->samp.p, blk, ncclFloat64, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(samples.data(), h->samp.p, sizeof(double) * n * blk, hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    int32_t split[MAX_SHARDS - 1] = {};
+    if ((rc = dbi_shard_splitters(samples.data(), n, h->params.mass_group_factor, split))) return rc;
+    if ((rc = dbi_shard_partition(h, split, nullptr))) return rc;
+
+    // send counts of every shard: counts[i * n + j] = records shard i sends owner j
+    const double t0 = now_ms();
+    if ((rc = h->xcount.ensure((size_t)n * n + 8))) return rc;
+    std::vector<unsigned long long> counts((size_t)n * n);
+    for (int j = 0; j < n; ++j) counts[(size_t)me * n + j] = sh.send_count[j];
+    DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * n, counts.data() + (size_t)me * n, sizeof(uint64_t) * n,
+                           hipMemcpyHostToDevice, s));
+    DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * n, h->xcount.p, n, ncclUint64, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(counts.data(), h->xcount.p, sizeof(uint64_t) * n * n, hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    sh.recv_count.assign(n, 0);
+    std::vector<uint64_t> roff(n + 1, 0);
+    uint64_t from_others = 0;
+    for (int i = 0; i < n; ++i) {
+        sh.recv_count[i] = counts[(size_t)i * n + me];
+        roff[i + 1] = roff[i] + sh.recv_count[i];
+        if (i != me) from_others += sh.recv_count[i];
+    }
+    if (sh.send_count[me] != sh.recv_count[me]) return set_error(DBI_E_STATE, "shard count exchange mismatch");
+    if (roff[n] >= (1ull << 32) - 1)
+        return set_error(DBI_E_INVALID, "more than 2^32-2 records for one owner: use more shards");
+    if ((rc = h->recA.ensure(std::max<uint64_t>(roff[n], 1)))) return rc;  // digest slots are free after partition
+
+    // records to their owners: one group of point-to-point transfers over all peers
+    {
+        ManualStage ms(h, "exchange", 16.0 * (double)(from_others + (sh.n_digest - sh.send_count[me])));
+        if (sh.send_count[me])
+            DBI_HIP(hipMemcpyAsync(h->recA.p + roff[me], h->recB.p + sh.send_off[me], sh.send_count[me] * sizeof(Rec),
+                                   hipMemcpyDeviceToDevice, s));
+        DBI_NCCL(ncclGroupStart());
+        for (int p = 0; p < n; ++p) {
+            if (p == me) continue;
+            if (sh.send_count[p])
+                DBI_NCCL(ncclSend(h->recB.p + sh.send_off[p], sh.send_count[p] * sizeof(Rec), ncclUint8, p, c->comm, s));
+            if (sh.recv_count[p])
+                DBI_NCCL(ncclRecv(h->recA.p + roff[p], sh.recv_count[p] * sizeof(Rec), ncclUint8, p, c->comm, s));
+        }
+        DBI_NCCL(ncclGroupEnd());
+        ms.end();
+    }
+    DBI_HIP(hipStreamSynchronize(s));
+    sh.n_recv = roff[n];
+    sh.ms_exchange = now_ms() - t0;
+    sh.phase = 3;
+    if ((rc = dbi_shard_merge(h))) return rc;
+
+    // whole-index totals
+    unsigned long long tot[5] = {sh.n_total, sh.n_dropped, sh.n_recv, h->stats.n_unique, h->stats.n_keys};
+    DBI_HIP(hipMemcpyAsync(h->xcount.p, tot, sizeof(tot), hipMemcpyHostToDevice, s));
+    DBI_NCCL(ncclAllReduce(h->xcount.p, h->xcount.p, 5, ncclUint64, ncclSum, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(tot, h->xcount.p, sizeof(tot), hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    sh.global.g_total = tot[0];
+    sh.global.g_dropped = tot[1];
+    sh.global.g_kept = tot[2];
+    sh.global.g_unique = tot[3];
+    sh.global.g_keys = tot[4];
+    return 0;
+}
+
+}  // extern "C"

@@ -206,6 +206,89 @@ int dbi_stage_times(dbi_handle* h, const char** names, double* ms, double* bytes
                     uint64_t* n);
 
 /* ------------------------------------------------------------------------ */
+/* Sharded build: one index over the proteins of every shard (GPU)           */
+/* ------------------------------------------------------------------------ */
+/*
+ * The proteome is split into contiguous protein ranges, one per shard (one
+ * shard per GPU, one process per GPU).  Every shard digests its own proteins
+ * (DBIndexer.cutSeq, DBIndexer.java:237-405); the records are then routed to
+ * the shard that OWNS their mass key (int)(mass*factor) — owners hold
+ * contiguous key ranges chosen from a sample of every shard's masses — and each
+ * owner sorts, de-duplicates across shards and finalises its key range
+ * (IndexMerge.getMergedData, DBIndexStoreSQLiteByteIndexMerge.java:620-719).
+ * The owners' unique tables, concatenated in shard order, ARE the index of the
+ * whole proteome: identical, row for row, to a single-device build.  Protein
+ * ids are global (FASTA order, DBIndexer.java:251,418).
+ *
+ * Every shard must hold the residues and offsets of the WHOLE proteome in HBM
+ * (the owner merge compares peptide strings of any shard); dbi_comm_allgatherv
+ * assembles them from per-shard pieces.
+ *
+ * Phases (each call is per handle; dbi_build_sharded runs them all over RCCL):
+ *   dbi_shard_digest     digest proteins [p_begin, p_end) of the global arrays
+ *   dbi_shard_samples    DBI_SHARD_SAMPLES masses of this shard's records + weight
+ *   dbi_shard_splitters  (host only) owner key ranges from every shard's samples
+ *   dbi_shard_partition  route records by owner; per-owner send counts
+ *   dbi_shard_exchange_local / RCCL exchange   records to their owners
+ *   dbi_shard_merge      owner sort + cross-shard dedup + finalize
+ * After the merge the handle answers dbi_query / dbi_peptides / dbi_export for
+ * its own key range (ids are local to the owner's table).
+ */
+#define DBI_SHARD_SAMPLES 4096
+#define DBI_MAX_SHARDS 64
+
+typedef struct dbi_shard_stats {
+    int32_t rank, nshards;
+    uint64_t p_begin, p_end;      /* this shard's proteins (global ids)                   */
+    int32_t key_lo, key_hi;       /* owned mass keys [key_lo, key_hi) (INT32_MIN/MAX ends)  */
+    uint64_t n_total;             /* this shard's digest: totalSeqCount                    */
+    uint64_t n_dropped;           /*   of which bucket drops (not routed)                  */
+    uint64_t n_sent;              /*   records routed to other owners                      */
+    uint64_t n_received;          /* records this owner merged (from every shard, incl. self) */
+    uint64_t n_unique, n_keys;    /* this owner's unique peptides / distinct mass keys     */
+    /* whole-index totals (sums over shards; filled by dbi_build_sharded) */
+    uint64_t g_total, g_dropped, g_kept, g_unique, g_keys;
+    double digest_ms, partition_ms, exchange_ms, merge_ms; /* wall time of each phase      */
+} dbi_shard_stats;
+
+/* Digest proteins [p_begin, p_end) of the global arrays (device pointers:
+ * d_residues[n_res], d_prot_off[n_prot+1]) as shard `rank` of `nshards`. */
+int dbi_shard_digest(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, const uint64_t* d_prot_off,
+                     uint64_t n_prot, uint64_t p_begin, uint64_t p_end, int rank, int nshards);
+/* samples[0..DBI_SHARD_SAMPLES) = masses of evenly spaced records (NaN = no
+ * record there), samples[DBI_SHARD_SAMPLES] = records per valid sample. */
+int dbi_shard_samples(dbi_handle* h, double* samples);
+/* Host only.  samples = nshards blocks of DBI_SHARD_SAMPLES+1 (dbi_shard_samples
+ * of every shard, in shard order); split[0..nshards-1) = first key of owners
+ * 1..nshards-1 (weighted quantiles: balanced record counts).  Deterministic: every
+ * shard computes the same split from the same samples. */
+int dbi_shard_splitters(const double* samples, int nshards, int32_t factor, int32_t* split);
+/* Route this shard's records by owner (stable; global protein ids);
+ * send_count[0..nshards) = records for each owner. */
+int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_count);
+/* Single-process exchange between the handles of all shards (same device or
+ * peer-accessible devices): hs[i] = shard i. */
+int dbi_shard_exchange_local(dbi_handle* const* hs, int nshards);
+/* Owner merge of the received records: the index of this owner's key range. */
+int dbi_shard_merge(dbi_handle* h);
+int dbi_shard_stats_get(dbi_handle* h, dbi_shard_stats* out);
+
+/* RCCL communicator (one rank per GPU, xGMI).  The 128-byte id comes from
+ * rank 0's dbi_comm_unique_id and is passed to every rank out of band. */
+typedef struct dbi_comm dbi_comm;
+int dbi_comm_unique_id(uint8_t* id128);
+int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_comm** out);
+void dbi_comm_destroy(dbi_comm* c);
+/* d_recv = concatenation over ranks of rank_bytes[r] bytes; this rank's piece
+ * (rank_bytes[rank] bytes at d_send) lands at its offset (d_send may be that
+ * spot).  Point-to-point sends/receives grouped over all peers. */
+int dbi_comm_allgatherv(dbi_comm* c, const void* d_send, void* d_recv, const uint64_t* rank_bytes, void* stream);
+/* All phases over RCCL: digest, sample all-gather, splitters, partition,
+ * count all-gather, grouped send/recv exchange, owner merge, totals all-reduce. */
+int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_residues, uint64_t n_res,
+                      const uint64_t* d_prot_off, uint64_t n_prot, uint64_t p_begin, uint64_t p_end);
+
+/* ------------------------------------------------------------------------ */
 /* DBIndexStore mirror                                                      */
 /* ------------------------------------------------------------------------ */
 typedef struct dbi_store dbi_store;

@@ -1,0 +1,156 @@
+"""GPU parity of the sharded build (dbi_shard_* / dbi_build_sharded): the
+owners' unique tables, concatenated in shard order, must equal the oracle's
+single-store index of the whole proteome bit for bit, and queries answered by
+the owners must equal the oracle's getSequences(m, tol).
+
+Several shards run in one process on one GPU (dbi_shard_exchange_local);
+the RCCL driver runs with one rank (a real multi-rank exchange needs one GPU
+per rank: bench.py --gpus N).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from dbindex_amd import fasta, shard
+from dbindex_amd.params import DBIndexSearchParams
+from oracle import cref
+from tests.helpers import query_masses
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def native():
+    from dbindex_amd import _native
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    return _native
+
+
+def _inputs(native, pp):
+    d_res = native.DeviceBuffer.from_numpy(np.concatenate([pp.residues, np.zeros(16, np.uint8)]), 0)
+    d_off = native.DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), 0)
+    return d_res, d_off
+
+
+def _assert_sharded_equal(engines, oix, ctx, nq=1500):
+    parts = [e.export() for e in engines]
+    g = shard.concat_exports(parts)
+    o = oix.unique()
+    sts = [shard.shard_stats(e) for e in engines]
+    assert sum(s.n_total for s in sts) == oix.n_total, (ctx, "n_total")
+    assert sum(s.n_dropped for s in sts) == oix.n_dropped, (ctx, "n_dropped")
+    assert sum(s.n_received for s in sts) == oix.n_kept, (ctx, "n_kept")
+    assert sum(s.n_unique for s in sts) == oix.n_unique, (ctx, "n_unique")
+    assert sum(s.n_keys for s in sts) == oix.n_keys, (ctx, "n_keys")
+    assert np.array_equal(g["mass"].view(np.uint64), o["mass"].view(np.uint64)), (ctx, "mass")
+    for k in ("prot_id", "offset", "length", "occ_off", "occ_prot"):
+        a, b = g[k].astype(np.uint64), o[k].astype(np.uint64)
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0][:5] if a.shape == b.shape else "shape"
+            raise AssertionError(f"{ctx}: {k} differs at {bad}")
+    keys = np.concatenate([e.entry_keys() for e in engines])
+    assert np.array_equal(keys, oix.entry_keys()), (ctx, "entry keys")
+    # owner key ranges tile the key line in shard order
+    for a, b in zip(sts, sts[1:]):
+        assert a.key_hi == b.key_lo, (ctx, "key ranges")
+    # queries: every owner answers for its slice; slices are adjacent in the
+    # global table, so the union is one contiguous id range
+    m, t = query_masses(oix, nq)
+    of, oc = oix.query_batch(m, t)
+    first = np.full(m.shape[0], np.iinfo(np.uint64).max, np.uint64)
+    count = np.zeros(m.shape[0], np.uint64)
+    base = 0
+    for e, p in zip(engines, parts):
+        f, c = e.query(m, t)
+        hit = c > 0
+        first[hit] = np.minimum(first[hit], f[hit] + np.uint64(base))
+        count += c
+        base += p["mass"].shape[0]
+    assert np.array_equal(count, oc), (ctx, "query counts")
+    hit = oc > 0
+    assert np.array_equal(first[hit], of[hit]), (ctx, "query first ids")
+
+
+def _run_local(native, prm, pp, k, ranges=None, ctx=""):
+    from dbindex_amd.engine import Engine
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    d_res, d_off = _inputs(native, pp)
+    ranges = ranges or shard.protein_ranges(pp.offsets, k)
+    engines = [Engine(cp, 0) for _ in range(k)]
+    try:
+        for rep in ("cold", "warm"):
+            shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, ranges)
+            _assert_sharded_equal(engines, oix, f"{ctx} k={k} [{rep}]")
+    finally:
+        for e in engines:
+            e.close()
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8])
+def test_sharded_local_tryptic(native, k):
+    _run_local(native, DBIndexSearchParams.trypsin(2), fasta.config("1k"), k, ctx="1k tryp2")
+
+
+@pytest.mark.parametrize("name,prm,nprot,k", [
+    ("semi2", DBIndexSearchParams.semi_tryptic(2), 300, 3),
+    ("tryp3", DBIndexSearchParams.trypsin(3), 1000, 4),
+    ("tryp0", DBIndexSearchParams.trypsin(0), 1000, 2),
+    ("nonspec", DBIndexSearchParams.non_specific(50), 60, 4),
+    ("mand_K", DBIndexSearchParams.trypsin(2, mandatory_internal_aas="K"), 500, 3),
+])
+def test_sharded_local_params(native, name, prm, nprot, k):
+    _run_local(native, prm, fasta.config("1k").slice(0, nprot), k, ctx=name)
+
+
+def test_sharded_local_uneven_and_empty_shards(native):
+    pp = fasta.config("1k").slice(0, 200)
+    # an empty shard, a one-protein shard, and the rest
+    ranges = [(0, 0), (0, 1), (1, 150), (150, 150), (150, 200)]
+    _run_local(native, DBIndexSearchParams.trypsin(2), pp, 5, ranges=ranges, ctx="uneven")
+
+
+def test_sharded_local_duplicates_across_shards(native):
+    # the same proteins in every shard: every peptide has one owner and its
+    # occurrence list spans all shards in protein order
+    base = fasta.config("1k").slice(0, 50).sequences()
+    pp = fasta.PackedProteins.from_sequences(base * 4)
+    _run_local(native, DBIndexSearchParams.trypsin(2), pp, 4, ctx="dups")
+
+
+def test_sharded_human_scale(native):
+    _run_local(native, DBIndexSearchParams.trypsin(2), fasta.config("human"), 4, ctx="human")
+
+
+def test_sharded_rccl_single_rank(native):
+    from dbindex_amd.engine import Engine
+    pp = fasta.config("1k")
+    prm = DBIndexSearchParams.trypsin(2)
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    d_res, d_off = _inputs(native, pp)
+    comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
+    try:
+        with Engine(cp, 0) as eng:
+            for rep in ("cold", "warm"):
+                st = shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
+                                         0, pp.n_proteins)
+                assert st.g_total == oix.n_total and st.g_unique == oix.n_unique and st.g_keys == oix.n_keys
+                _assert_sharded_equal([eng], oix, f"rccl x1 [{rep}]")
+            # all-gatherv of one rank: a copy
+            src = native.DeviceBuffer.from_numpy(np.arange(100, dtype=np.uint8), 0)
+            dst = native.DeviceBuffer(100, 0)
+            comm.allgatherv(src.ptr, dst.ptr, [100])
+            assert np.array_equal(dst.download(np.uint8, 100), np.arange(100, dtype=np.uint8))
+    finally:
+        comm.close()
+
+
+def test_shard_phase_order(native):
+    from dbindex_amd import _native
+    from dbindex_amd.engine import Engine
+    with Engine(DBIndexSearchParams.trypsin(2).to_c(), 0) as eng:
+        with pytest.raises(_native.DBIndexStoreException):
+            _native.check(_native.lib().dbi_shard_merge(eng.h))
