@@ -34,19 +34,46 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from dbindex_amd.params import DBIndexSearchParams  # noqa: E402
+
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BASELINE_METRIC = "peptides indexed/sec + mass-window queries/sec, SwissProt-scale FASTA"
+# name -> (description, synthetic proteome (fasta.CONFIGS), params, CPU-baseline sample proteins)
 WORKLOADS = {
     "human": ("UniProt-human-scale synthetic proteome (20,000 proteins, seed 2), trypsin, "
-              "2 missed cleavages, 500-6000 Da MH+ (BASELINE.json configs[1])", 2),
-    "1k": ("1k-protein synthetic proteome (seed 1), trypsin, 0 missed cleavages (configs[0])", 0),
+              "2 missed cleavages, 500-6000 Da MH+ (BASELINE.json configs[1])", "human",
+              lambda: DBIndexSearchParams.trypsin(2), 20000),
+    "1k": ("1k-protein synthetic proteome (seed 1), trypsin, 0 missed cleavages (configs[0])", "1k",
+           lambda: DBIndexSearchParams.trypsin(0), 1000),
     "swissprot": ("SwissProt-scale synthetic proteome (560,000 proteins, seed 3), trypsin, "
-                  "2 missed cleavages (configs[2], single GPU)", 2),
+                  "2 missed cleavages (configs[2], single GPU)", "swissprot",
+                  lambda: DBIndexSearchParams.trypsin(2), 100000),
+    "semi": ("SwissProt-scale synthetic proteome (560,000 proteins, seed 3), semi-tryptic, "
+             "2 missed cleavages + 1M precursor-mass queries +-20 ppm (configs[3])", "swissprot",
+             lambda: DBIndexSearchParams.semi_tryptic(2), 5000),
 }
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def stdout_to_stderr(fn):
+    """Runs fn with fd 1 pointed at stderr (RCCL prints a version banner on
+    stdout at init; the bench's stdout carries exactly one JSON line)."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    sys.stdout.flush()
+    libc.fflush(None)
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return fn()
+    finally:
+        sys.stdout.flush()
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def cpu_model() -> str:
@@ -94,13 +121,13 @@ def main() -> None:
         dist.init_process_group("gloo")
     dev = local_rank
 
-    desc, missed = WORKLOADS[args.config]
-    base = dict(fasta.CONFIGS[args.config])
+    desc, proteome, make_params, cpu_sample = WORKLOADS[args.config]
+    base = dict(fasta.CONFIGS[proteome])
     base["seed"] = base["seed"] + 1000 * rank  # each rank its own shard of equal size
     t0 = time.time()
     pp = fasta.synthetic(with_defs=False, **base)
     log(f"[rank {rank}] synthetic {args.config}: P={pp.n_proteins} R={pp.n_residues} ({time.time() - t0:.1f}s)")
-    prm = DBIndexSearchParams.trypsin(missed)
+    prm = make_params()
 
     eng = Engine(prm, device=dev)
     if merge:
@@ -114,10 +141,10 @@ def main() -> None:
         R_all, P_all = int(res_base[-1]), int(prot_base[-1])
         off_all = np.concatenate([sizes[r][2][:-1] + res_base[r] for r in range(world)] +
                                  [np.array([R_all], np.uint64)])
-        uid = [shard.ShardComm.unique_id() if rank == 0 else None]
+        uid = [stdout_to_stderr(shard.ShardComm.unique_id) if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
-        comm = shard.ShardComm(uid[0], world, rank, dev)
+        comm = stdout_to_stderr(lambda: shard.ShardComm(uid[0], world, rank, dev))
         # input staging (untimed): every shard's residues into every GPU's HBM
         d_res = DeviceBuffer(R_all + 16, dev)
         mine = d_res.ptr + int(res_base[rank])
@@ -241,6 +268,46 @@ def main() -> None:
 
     # secondary: mass-window queries/sec on the built index (1M queries, +-20 ppm)
     qps = None
+    if args.queries > 0 and merge:
+        # routed queries on the one merged index: every rank brings its own 1M
+        # batch (90 % near indexed masses of ANY owner), windows go to their key
+        # owners over RCCL and the whole-index ids come back
+        ex = eng.export()["mass"]
+        rng = np.random.Generator(np.random.PCG64(7 + rank))
+        pick = ex[rng.integers(0, ex.shape[0], min(ex.shape[0], args.queries // world + 1))] if ex.shape[0] else ex
+        pool = [pick] * world
+        if world > 1:
+            dist.all_gather_object(pool, pick)
+        pool = np.concatenate(pool) if sum(p.shape[0] for p in pool) else np.array([1000.0])
+        nq = args.queries
+        k = int(nq * 0.9)
+        m = np.empty(nq)
+        m[:k] = pool[rng.integers(0, pool.shape[0], k)] * (1 + rng.normal(0, 5e-6, k))
+        m[k:] = rng.uniform(500, 6000, nq - k)
+        tol = m * (1 - 1 / (20.0 / 1e6 + 1))
+        dm, dt = DeviceBuffer.from_numpy(m, dev), DeviceBuffer.from_numpy(tol, dev)
+        df, dc = DeviceBuffer(8 * nq, dev), DeviceBuffer(8 * nq, dev)
+        synchronize(dev)
+        for _ in range(3):
+            shard.query_sharded(eng, comm, dm.ptr, dt.ptr, nq, df.ptr, dc.ptr)
+        reps = 20
+        if world > 1:
+            dist.barrier()
+        tq = time.perf_counter()
+        for _ in range(reps):
+            shard.query_sharded(eng, comm, dm.ptr, dt.ptr, nq, df.ptr, dc.ptr)
+        synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        tq = time.perf_counter() - tq
+        hits = int(dc.download(np.uint64, nq).sum())
+        if world > 1:
+            t = torch.tensor([tq], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tq = float(t.item())
+        qps = dict(value=world * nq * reps / tq, unit="queries/s", queries_per_rank=nq, tol_ppm=20.0,
+                   avg_hits=hits / nq, index=f"the merged index above, queries routed to key owners over RCCL "
+                                             f"({world} ranks)")
     if args.queries > 0 and not merge:
         ex = eng.export()["mass"]
         rng = np.random.Generator(np.random.PCG64(7 + rank))
@@ -271,7 +338,7 @@ def main() -> None:
         # reference-semantics CPU restatement (oracle/cpu_ref.cpp), single thread
         # like the reference; bounded sample of the same workload
         from oracle import cref
-        sample = pp if args.config != "swissprot" else pp.slice(0, 40000)
+        sample = pp.slice(0, min(cpu_sample, pp.n_proteins))
         t1 = time.perf_counter()
         oix = cref.Index(prm.to_c(), sample.residues, sample.offsets)
         t1 = time.perf_counter() - t1

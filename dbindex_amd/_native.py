@@ -101,6 +101,8 @@ SIGNATURES = [
     ("dbi_shard_exchange_local", c_int, [P, c_int]),
     ("dbi_shard_merge", c_int, [P]),
     ("dbi_shard_stats_get", c_int, [P, POINTER(DbiShardStats)]),
+    ("dbi_query_sharded", c_int, [P, P, P, P, c_uint64, P, P]),
+    ("dbi_query_sharded_local", c_int, [P, c_int, P, P, P, P, P]),
     ("dbi_comm_unique_id", c_int, [P]),
     ("dbi_comm_init", c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
     ("dbi_comm_destroy", None, [P]),

@@ -1029,19 +1029,21 @@ size_t radix_hist_elems(uint32_t n, int bits) {
     return (size_t)g * (size_t)(1u << bits);
 }
 
-// Digit policies of a stable pass: the digit of a record from its mass, and
-// what happens to the record on its way out.
+// Digit policies of a stable pass: the digit of a record from its first word
+// q0, and what happens to the record on its way out.
 struct BinDigit {  // LSD radix over the fine mass bin: (bin >> shift) & mask
     BinMap bm;
     int shift;
     uint32_t mask;
-    __device__ __forceinline__ uint32_t operator()(double m) const { return (bin_of(m, bm) >> shift) & mask; }
+    __device__ __forceinline__ uint32_t operator()(uint64_t q0) const {
+        return (bin_of(q0_mass(q0), bm) >> shift) & mask;
+    }
     __device__ __forceinline__ void xform(uint4&) const {}
 };
 struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor)
     OwnerMap om;
-    __device__ __forceinline__ uint32_t operator()(double m) const {
-        const int32_t k = java_d2i(m * (double)om.factor);
+    __device__ __forceinline__ uint32_t operator()(uint64_t q0) const {
+        const int32_t k = java_d2i(q0_mass(q0) * (double)om.factor);
         uint32_t d = 0;
         for (uint32_t j = 0; j + 1 < om.nshards; ++j) d += k >= om.split[j] ? 1u : 0u;
         return d;
@@ -1051,6 +1053,10 @@ struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor
         r.z = (uint32_t)q1;
         r.w = (uint32_t)(q1 >> 32);
     }
+};
+struct PairDigit {  // query routing pairs: q0 = owner shard, q1 = query index
+    __device__ __forceinline__ uint32_t operator()(uint64_t q0) const { return (uint32_t)q0; }
+    __device__ __forceinline__ void xform(uint4&) const {}
 };
 
 // Digit of record r for this pass, and the wave's peers holding the same digit.
@@ -1086,7 +1092,7 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
         const bool valid = i < n && (!SPARSE || qv[k] != REC_SENTINEL);
-        const uint32_t d = dig(q0_mass(qv[k]));
+        const uint32_t d = dig(qv[k]);
         const uint64_t peers = digit_peers(d, valid, bits);
         if (valid && __popcll(peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
         wave_sync();
@@ -1129,7 +1135,7 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, D
         const uint32_t i = base + k * 64 + lane;
         const bool valid = i < n && (!SPARSE || (rv[k].x & rv[k].y) != 0xFFFFFFFFu);
         vmask |= (uint32_t)valid << k;
-        const uint32_t d = dig(u4_mass(rv[k]));
+        const uint32_t d = dig(u4_q0(rv[k]));
         const uint64_t peers = digit_peers(d, valid, bits);
         const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t before = cnt[w][d];
@@ -1170,7 +1176,7 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, D
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
     for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) {
         uint4 r = stage[t];
-        const uint32_t dr = dig(u4_mass(r));
+        const uint32_t dr = dig(u4_q0(r));
         dig.xform(r);
         out4[gofs[dr] + t] = r;
     }
@@ -1223,6 +1229,15 @@ hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bo
 hipError_t launch_owner_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const OwnerMap& om, bool sparse,
                                 const uint32_t* d_hist, hipStream_t s) {
     return radix_scatter(d_in, d_out, n, OwnerDigit{om}, owner_bits(om.nshards), sparse, d_hist, s);
+}
+
+hipError_t launch_pair_hist(const Rec* d_in, uint32_t n, uint32_t nshards, uint32_t* d_hist, hipStream_t s) {
+    return radix_hist(d_in, n, PairDigit{}, owner_bits(nshards), false, d_hist, s);
+}
+
+hipError_t launch_pair_scatter(const Rec* d_in, Rec* d_out, uint32_t n, uint32_t nshards, const uint32_t* d_hist,
+                               hipStream_t s) {
+    return radix_scatter(d_in, d_out, n, PairDigit{}, owner_bits(nshards), false, d_hist, s);
 }
 
 uint64_t radix_blocks(uint32_t n) { return (n + RADIX_CHUNK - 1) / RADIX_CHUNK; }
@@ -1838,42 +1853,6 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
     return hipGetLastError();
 }
 
-// chunks above the LDS capacity (runs of very frequent peptides): same body,
-// scratch in a global workspace (region [4a, 4a+4m) of each array)
-__global__ void __launch_bounds__(BIG_THREADS)
-k_big_chunks(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
-             const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
-             const uint32_t* __restrict__ big_list, unsigned long long* ws_key, uint32_t* ws_k2,
-             Counters* __restrict__ ctr) {
-    __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
-    __shared__ unsigned long long s_flag;
-    const uint32_t nbig = ctr->n_giant;
-    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
-    for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {
-        const uint32_t c = big_list[j];
-        const uint32_t a = chunk_lo[c];
-        const uint32_t m = chunk_lo[c + 1] - a;
-        unsigned long long* key = ws_key + 4ull * a;   // [4a, 4a+2m): key, [4a+2m, 4a+4m): hsh
-        unsigned long long* hsh = key + 2ull * m;
-        uint32_t* k2 = ws_k2 + 4ull * a;               // [4a, 4a+2m): idx, [4a+2m, 4a+3m): runs
-        uint32_t* k3 = k2 + 2ull * m;
-        const uint32_t h = process_chunk<BIG_THREADS>(in + a, out + a, m, rl, key, hsh, k2, k3, s_u32, &s_flag);
-        const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
-        if (threadIdx.x == 0) ucount[c] = tot;
-        __syncthreads();
-    }
-}
-
-hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                             const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list,
-                             uint32_t max_blocks, unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr,
-                             hipStream_t s) {
-    if (max_blocks == 0) return hipSuccess;
-    DBI_LAUNCH(k_big_chunks, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res, d_poff,
-                       d_ucount, d_big_list, d_ws_key, d_ws_k2, d_ctr);
-    return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------
 // 6. finalize: unique table + occurrence CSR (per chunk)
 // ---------------------------------------------------------------------------
@@ -2224,6 +2203,395 @@ hipError_t launch_max_plen(const uint32_t* d_poff, uint32_t n_prot, Counters* d_
     if (n_prot == 0) return hipSuccess;
     const uint32_t g = std::min<uint32_t>((n_prot + 255) / 256, 1024u);
     DBI_LAUNCH(k_max_plen, dim3(g), dim3(256), 0, s, d_poff, n_prot, d_ctr);
+    return hipGetLastError();
+}
+
+}  // namespace dbi
+
+namespace dbi {
+
+// ---------------------------------------------------------------------------
+// sharded queries: route windows to key owners, answer, fold back
+// (getSequences(m, tol), DBIndexStoreSQLiteMult.java:315-350)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool query_window(double m, double t, int32_t nb, int32_t br, double& lo, double& hi) {
+    lo = m - t;
+    if (lo < 0) lo = 0;
+    hi = m + t;
+    const int b0 = java_d2i(lo) / br, b1 = java_d2i(hi) / br;
+    return !(b0 > nb - 1 || b1 > nb - 1);
+}
+
+__device__ __forceinline__ uint32_t owner_of_key(const RouteMap& rm, int32_t k) {
+    uint32_t d = 0;
+    for (uint32_t j = 0; j + 1 < rm.nshards; ++j) d += k >= rm.split[j] ? 1u : 0u;
+    return d;
+}
+
+__device__ __forceinline__ bool route_span(const RouteMap& rm, double m, double t, uint32_t& o0, uint32_t& o1) {
+    double lo, hi;
+    if (!query_window(m, t, rm.nb, rm.br, lo, hi)) return false;
+    o0 = owner_of_key(rm, java_d2i(lo * (double)rm.factor));
+    o1 = owner_of_key(rm, java_d2i(hi * (double)rm.factor));
+    if (o1 < o0) o1 = o0;  // NaN bounds: key 0 on both sides
+    return true;
+}
+
+__global__ void k_qroute_count(const double* __restrict__ qm, const double* __restrict__ qt, uint64_t nq, RouteMap rm,
+                               uint32_t* __restrict__ cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    uint32_t o0 = 0, o1 = 0;
+    cnt[i] = route_span(rm, qm[i], qt[i], o0, o1) ? o1 - o0 + 1 : 0u;
+}
+
+hipError_t launch_qroute_count(const double* d_qm, const double* d_qt, uint64_t nq, const RouteMap& rm,
+                               uint32_t* d_cnt, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    DBI_LAUNCH(k_qroute_count, dim3((uint32_t)((nq + 255) / 256)), dim3(256), 0, s, d_qm, d_qt, nq, rm, d_cnt);
+    return hipGetLastError();
+}
+
+__global__ void k_qroute_emit(const double* __restrict__ qm, const double* __restrict__ qt, uint64_t nq, RouteMap rm,
+                              const uint32_t* __restrict__ offs, Rec* __restrict__ pairs) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    uint32_t o0 = 0, o1 = 0;
+    if (!route_span(rm, qm[i], qt[i], o0, o1)) return;
+    Rec* __restrict__ out = pairs + offs[i];
+    for (uint32_t o = o0; o <= o1; ++o) {
+        Rec r;
+        r.q0 = o;
+        r.q1 = i;
+        out[o - o0] = r;
+    }
+}
+
+hipError_t launch_qroute_emit(const double* d_qm, const double* d_qt, uint64_t nq, const RouteMap& rm,
+                              const uint32_t* d_offs, Rec* d_pairs, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    DBI_LAUNCH(k_qroute_emit, dim3((uint32_t)((nq + 255) / 256)), dim3(256), 0, s, d_qm, d_qt, nq, rm, d_offs,
+               d_pairs);
+    return hipGetLastError();
+}
+
+__global__ void k_qpack(const Rec* __restrict__ pairs, uint64_t np, const double* __restrict__ qm,
+                        const double* __restrict__ qt, Rec* __restrict__ out) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const uint64_t i = pairs[p].q1;
+    Rec r;
+    r.q0 = (uint64_t)__double_as_longlong(qm[i]);
+    r.q1 = (uint64_t)__double_as_longlong(qt[i]);
+    out[p] = r;
+}
+
+hipError_t launch_qpack(const Rec* d_pairs, uint64_t np, const double* d_qm, const double* d_qt, Rec* d_out,
+                        hipStream_t s) {
+    if (np == 0) return hipSuccess;
+    DBI_LAUNCH(k_qpack, dim3((uint32_t)((np + 255) / 256)), dim3(256), 0, s, d_pairs, np, d_qm, d_qt, d_out);
+    return hipGetLastError();
+}
+
+__global__ void k_query_pairs(DevParams dp, int32_t factor, const double* __restrict__ umass, uint32_t nu,
+                              const Rec* __restrict__ in, uint64_t n, uint64_t base, Rec* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Rec q = in[i];
+    const double precMass = __longlong_as_double((long long)q.q0), tol = __longlong_as_double((long long)q.q1);
+    double lo, hi;
+    uint64_t f = 0, c = 0;
+    if (query_window(precMass, tol, dp.nb, dp.br, lo, hi)) {
+        if (lo != lo || hi != hi) {
+            c = key_upper(umass, nu, factor, 0);  // k_query: NaN bounds select key 0
+        } else {
+            const uint32_t a = lower_bound_d(umass, nu, lo);
+            const uint32_t e = upper_bound_d(umass, nu, hi);
+            if (e > a) { f = a; c = e - a; }
+        }
+    }
+    Rec r;
+    r.q0 = c ? base + f : ~0ull;
+    r.q1 = c;
+    out[i] = r;
+}
+
+hipError_t launch_query_pairs(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,
+                              const Rec* d_in, uint64_t n, uint64_t base, Rec* d_out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    DBI_LAUNCH(k_query_pairs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, dp, factor, d_umass, n_unique,
+               d_in, n, base, d_out);
+    return hipGetLastError();
+}
+
+__global__ void k_qcombine_init(uint64_t* __restrict__ first, uint64_t* __restrict__ count, uint64_t nq) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    first[i] = ~0ull;
+    count[i] = 0;
+}
+
+// a window's owners are consecutive and their id ranges adjacent in the
+// concatenated table: first = min over owners that hit, count = sum
+__global__ void k_qcombine(const Rec* __restrict__ pairs, const Rec* __restrict__ res, uint64_t np,
+                           unsigned long long* __restrict__ first, unsigned long long* __restrict__ count) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const Rec r = res[p];
+    if (r.q1 == 0) return;
+    const uint64_t q = pairs[p].q1;
+    atomicAdd(&count[q], (unsigned long long)r.q1);
+    atomicMin(&first[q], (unsigned long long)r.q0);
+}
+
+__global__ void k_qcombine_fix(uint64_t* __restrict__ first, uint64_t nq) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nq && first[i] == ~0ull) first[i] = 0;
+}
+
+hipError_t launch_qcombine(const Rec* d_pairs, const Rec* d_res, uint64_t np, uint64_t* d_first, uint64_t* d_count,
+                           uint64_t nq, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    const dim3 gq((uint32_t)((nq + 255) / 256));
+    DBI_LAUNCH(k_qcombine_init, gq, dim3(256), 0, s, d_first, d_count, nq);
+    if (np)
+        DBI_LAUNCH(k_qcombine, dim3((uint32_t)((np + 255) / 256)), dim3(256), 0, s, d_pairs, d_res, np,
+                   (unsigned long long*)d_first, (unsigned long long*)d_count);
+    DBI_LAUNCH(k_qcombine_fix, gq, dim3(256), 0, s, d_first, nq);
+    return hipGetLastError();
+}
+
+}  // namespace dbi
+
+namespace dbi {
+
+// ---------------------------------------------------------------------------
+// 5c. chunks above BIG_CAP: MSD split on the 72-bit (mass, tag) key
+// ---------------------------------------------------------------------------
+// Such chunks are equal-mass spikes: thousands of isobaric peptides with
+// bit-identical fp64 masses (semi-tryptic SwissProt: tens of thousands).  Their
+// sorted order is by (q0, q1) = (mass, tag, first appearance), so a split on
+// the top varying bits of X = (q0, q1 >> 56) — the tag splits an equal-mass
+// spike 65536 ways — gives ordered sub-buckets, and an equal-(mass, tag) group
+// (the only place dedup compares strings) never straddles two of them.
+// Adjacent small sub-buckets are packed into leaves of <= CHUNK_CAP records,
+// sorted in LDS like any chunk; their unique counts add into the chunk's.
+// A segment is uint4 {lo, n, chunk, buf}: records [lo, lo+n) in `in` (buf 0)
+// or `out` (buf 1).
+struct GiantLists {
+    uint4* work[GIANT_PASSES + 1];
+    uint4* leaf_small;
+    uint4* leaf_big;
+    uint4* fallback;
+    uint32_t cap;
+};
+
+size_t giant_seg_cap(uint64_t n) { return (size_t)(n / 64 + 4096); }
+
+__device__ __forceinline__ unsigned __int128 key72(const Rec& r) {
+    return ((unsigned __int128)r.q0 << 8) | (unsigned __int128)(r.q1 >> 56);
+}
+
+__device__ __forceinline__ void seg_push(uint4* list, unsigned int* cnt, uint32_t cap, uint4 seg,
+                                         Counters* ctr) {
+    const unsigned int i = atomicAdd(cnt, 1u);
+    if (i < cap) list[i] = seg;
+    else atomicOr(&ctr->err, ERR_SEGS);
+}
+
+__global__ void k_giant_init(const uint32_t* __restrict__ giant_list, const uint32_t* __restrict__ chunk_lo,
+                             uint32_t* __restrict__ ucount, GiantLists gl, Counters* __restrict__ ctr) {
+    const uint32_t n = ctr->n_giant;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const uint32_t c = giant_list[j];
+        const uint32_t a = chunk_lo[c];
+        ucount[c] = 0;
+        if (j < gl.cap) gl.work[0][j] = make_uint4(a, chunk_lo[c + 1] - a, c, 0u);
+        else atomicOr(&ctr->err, ERR_SEGS);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->n_seg[0] = min(n, gl.cap);
+}
+
+constexpr int SPLIT_THREADS = 1024;
+
+__global__ void __launch_bounds__(SPLIT_THREADS)
+k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__ ctr) {
+    __shared__ uint32_t cnt[256];
+    __shared__ uint32_t cur[256];
+    __shared__ unsigned long long s_lo0[SPLIT_THREADS / 64], s_hi0[SPLIT_THREADS / 64];
+    __shared__ uint32_t s_lo1[SPLIT_THREADS / 64], s_hi1[SPLIT_THREADS / 64];
+    __shared__ uint32_t s_shift, s_same;
+    const uint32_t nseg = ctr->n_seg[pass];
+    const bool last = pass + 1 == GIANT_PASSES;
+    for (uint32_t j = blockIdx.x; j < nseg; j += gridDim.x) {
+        const uint4 seg = gl.work[pass][j];
+        const uint32_t lo = seg.x, n = seg.y;
+        const Rec* __restrict__ from = seg.w ? out : in;
+        Rec* __restrict__ to = seg.w ? in : out;
+        // min / max of the 72-bit key over the segment
+        unsigned __int128 kmin = ~(unsigned __int128)0, kmax = 0;
+        for (uint32_t i = threadIdx.x; i < n; i += SPLIT_THREADS) {
+            const unsigned __int128 x = key72(from[lo + i]);
+            kmin = x < kmin ? x : kmin;
+            kmax = x > kmax ? x : kmax;
+        }
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) {
+            const uint64_t a0 = (uint64_t)(kmin >> 8), b0 = (uint64_t)(kmax >> 8);
+            const uint32_t a1 = (uint32_t)(kmin & 0xFF), b1 = (uint32_t)(kmax & 0xFF);
+            const uint64_t o0 = (uint64_t)__shfl_xor((long long)a0, d, 64), p0 = (uint64_t)__shfl_xor((long long)b0, d, 64);
+            const uint32_t o1 = (uint32_t)__shfl_xor((int)a1, d, 64), p1 = (uint32_t)__shfl_xor((int)b1, d, 64);
+            const unsigned __int128 om = ((unsigned __int128)o0 << 8) | o1, pm = ((unsigned __int128)p0 << 8) | p1;
+            kmin = om < kmin ? om : kmin;
+            kmax = pm > kmax ? pm : kmax;
+        }
+        const uint32_t w = threadIdx.x >> 6;
+        if (lane_id() == 0) {
+            s_lo0[w] = (uint64_t)(kmin >> 8); s_lo1[w] = (uint32_t)(kmin & 0xFF);
+            s_hi0[w] = (uint64_t)(kmax >> 8); s_hi1[w] = (uint32_t)(kmax & 0xFF);
+        }
+        if (threadIdx.x < 256) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned __int128 a = ~(unsigned __int128)0, b = 0;
+            for (int q = 0; q < SPLIT_THREADS / 64; ++q) {
+                const unsigned __int128 x = ((unsigned __int128)s_lo0[q] << 8) | s_lo1[q];
+                const unsigned __int128 y = ((unsigned __int128)s_hi0[q] << 8) | s_hi1[q];
+                a = x < a ? x : a;
+                b = y > b ? y : b;
+            }
+            const unsigned __int128 diff = a ^ b;
+            uint32_t v = 0;  // varying bits
+            if (diff >> 64) v = 128 - __clzll((unsigned long long)(diff >> 64));
+            else if (diff) v = 64 - __clzll((unsigned long long)diff);
+            s_same = diff == 0;
+            s_shift = v > 8 ? v - 8 : 0;
+        }
+        __syncthreads();
+        if (s_same) {
+            // one (mass, tag) key: strings decide, no key bits left to split on
+            if (threadIdx.x == 0) seg_push(gl.fallback, &ctr->n_fallback, gl.cap, seg, ctr);
+            __syncthreads();
+            continue;
+        }
+        const uint32_t sh = s_shift;
+        for (uint32_t i = threadIdx.x; i < n; i += SPLIT_THREADS)
+            atomicAdd(&cnt[(uint32_t)(key72(from[lo + i]) >> sh) & 0xFFu], 1u);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            // offsets + the next work list / leaves (adjacent small buckets packed)
+            uint32_t acc = 0, leaf_lo = 0, leaf_n = 0;
+            auto flush = [&]() {
+                if (leaf_n == 0) return;
+                const uint4 lf = make_uint4(lo + leaf_lo, leaf_n, seg.z, seg.w ^ 1u);
+                if (leaf_n <= (uint32_t)CHUNK_CAP) seg_push(gl.leaf_small, &ctr->n_leaf_small, gl.cap, lf, ctr);
+                else seg_push(gl.leaf_big, &ctr->n_leaf_big, gl.cap, lf, ctr);
+                leaf_n = 0;
+            };
+            for (uint32_t d = 0; d < 256; ++d) {
+                const uint32_t c = cnt[d];
+                cur[d] = acc;
+                if (c == 0) continue;
+                if (c > (uint32_t)BIG_CAP) {
+                    flush();
+                    const uint4 ws = make_uint4(lo + acc, c, seg.z, seg.w ^ 1u);
+                    if (last) seg_push(gl.fallback, &ctr->n_fallback, gl.cap, ws, ctr);
+                    else seg_push(gl.work[pass + 1], &ctr->n_seg[pass + 1], gl.cap, ws, ctr);
+                } else if (c > (uint32_t)CHUNK_CAP) {
+                    flush();
+                    leaf_lo = acc;
+                    leaf_n = c;
+                    flush();
+                } else {
+                    if (leaf_n + c > (uint32_t)CHUNK_CAP) flush();
+                    if (leaf_n == 0) leaf_lo = acc;
+                    leaf_n += c;
+                }
+                acc += c;
+            }
+            flush();
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n; i += SPLIT_THREADS) {
+            const Rec r = from[lo + i];
+            const uint32_t d = (uint32_t)(key72(r) >> sh) & 0xFFu;
+            to[lo + atomicAdd(&cur[d], 1u)] = r;
+        }
+        __syncthreads();
+    }
+}
+
+// leaves: sorted in LDS into out[lo, lo+n) (in place when they live in out)
+template <int NT, int CAP>
+__global__ void __launch_bounds__(NT)
+k_giant_leaf(const Rec* in, Rec* out, const uint4* __restrict__ list, const unsigned int* __restrict__ n_list,
+             uint32_t cap, const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff,
+             uint32_t* __restrict__ ucount, Counters* __restrict__ ctr) {
+    __shared__ unsigned long long k0[CAP];
+    __shared__ unsigned long long k1[CAP];
+    __shared__ uint32_t aux[CAP];
+    __shared__ uint32_t s_u32[NT / 64 + 1];
+    __shared__ uint32_t s_bad;
+    const uint32_t nl = min(*n_list, cap);
+    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
+        const uint4 lf = list[j];
+        const Rec* from = (lf.w ? out : in) + lf.x;
+        const uint32_t h = bitonic_chunk<NT, CAP>(from, out + lf.x, lf.y, rl, k0, k1, aux, s_u32, &s_bad);
+        const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
+        if (threadIdx.x == 0) atomicAdd(&ucount[lf.z], tot);
+        __syncthreads();
+    }
+}
+
+// segments of one (mass, tag) key above BIG_CAP: global-memory scratch
+__global__ void __launch_bounds__(BIG_THREADS)
+k_giant_fallback(Rec* in, Rec* out, const uint4* __restrict__ list, uint32_t cap, const uint8_t* __restrict__ res,
+                 const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount, unsigned long long* ws_key,
+                 uint32_t* ws_k2, Counters* __restrict__ ctr) {
+    __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
+    __shared__ unsigned long long s_flag;
+    const uint32_t nl = min(ctr->n_fallback, cap);
+    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
+        const uint4 sg = list[j];
+        const uint32_t a = sg.x, m = sg.y;
+        if (sg.w) {  // lives in out: move it back to in (free there) so out is written once
+            for (uint32_t i = threadIdx.x; i < m; i += BIG_THREADS) in[a + i] = out[a + i];
+            __syncthreads();
+        }
+        unsigned long long* key = ws_key + 4ull * a;
+        unsigned long long* hsh = key + 2ull * m;
+        uint32_t* k2 = ws_k2 + 4ull * a;
+        uint32_t* k3 = k2 + 2ull * m;
+        const uint32_t h = process_chunk<BIG_THREADS>(in + a, out + a, m, rl, key, hsh, k2, k3, s_u32, &s_flag);
+        const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
+        if (threadIdx.x == 0) atomicAdd(&ucount[sg.z], tot);
+        __syncthreads();
+    }
+}
+
+hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
+                               const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_giant_list,
+                               uint4* d_segs, size_t seg_cap, unsigned long long* d_ws_key, uint32_t* d_ws_k2,
+                               Counters* d_ctr, hipStream_t s) {
+    GiantLists gl;
+    for (int p = 0; p <= GIANT_PASSES; ++p) gl.work[p] = d_segs + (size_t)p * seg_cap;
+    gl.leaf_small = d_segs + (size_t)(GIANT_PASSES + 1) * seg_cap;
+    gl.leaf_big = gl.leaf_small + seg_cap;
+    gl.fallback = gl.leaf_big + seg_cap;
+    gl.cap = (uint32_t)std::min<size_t>(seg_cap, 0xFFFFFFFFu);
+    Rec* in = const_cast<Rec*>(d_in);  // the radix output: free scratch once the chunk sort read it
+    // (work lists are counted in ctr->n_seg, zeroed with the counters at the start of the build)
+    DBI_LAUNCH(k_giant_init, dim3(64), dim3(256), 0, s, d_giant_list, d_chunk_lo, d_ucount, gl, d_ctr);
+    for (int p = 0; p < GIANT_PASSES; ++p)
+        DBI_LAUNCH(k_giant_split, dim3(512), dim3(SPLIT_THREADS), 0, s, in, d_out, gl, p, d_ctr);
+    DBI_LAUNCH((k_giant_leaf<CHUNK_THREADS, CHUNK_CAP>), dim3(2048), dim3(CHUNK_THREADS), 0, s, in, d_out,
+               gl.leaf_small, &d_ctr->n_leaf_small, gl.cap, d_res, d_poff, d_ucount, d_ctr);
+    DBI_LAUNCH((k_giant_leaf<BIG_THREADS, BIG_CAP>), dim3(256), dim3(BIG_THREADS), 0, s, in, d_out, gl.leaf_big,
+               &d_ctr->n_leaf_big, gl.cap, d_res, d_poff, d_ucount, d_ctr);
+    DBI_LAUNCH(k_giant_fallback, dim3(256), dim3(BIG_THREADS), 0, s, in, d_out, gl.fallback, gl.cap, d_res, d_poff,
+               d_ucount, d_ws_key, d_ws_k2, d_ctr);
     return hipGetLastError();
 }
 

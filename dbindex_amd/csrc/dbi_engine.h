@@ -67,6 +67,11 @@ struct ShardState {
     uint64_t n_recv = 0;
     double ms_digest = 0, ms_partition = 0, ms_exchange = 0, ms_merge = 0;
     dbi_shard_stats global{};               // filled by dbi_build_sharded (RCCL sums)
+    uint64_t u_base = 0;                    // first global id of this owner's unique table
+    bool u_base_known = false;
+    // routed query batch (dbi_query_sharded*)
+    uint64_t q_n = 0, q_pairs = 0, q_recv = 0;
+    std::vector<uint64_t> qsend_count, qsend_off, qrecv_count, qrecv_off;
 };
 
 }  // namespace dbi
@@ -110,6 +115,7 @@ struct dbi_handle {
     DevBuf<Rec> recA, recB;
     DevBuf<uint32_t> hist;
     DevBuf<uint32_t> ucount, big_list, giant_list, chunk_lo;
+    DevBuf<uint4> segs;                 // giant-chunk split: segment lists
     DevBuf<unsigned long long> ws_key;
     DevBuf<uint32_t> ws_k2;
 
@@ -133,6 +139,10 @@ struct dbi_handle {
     dbi::ShardState shard;
     DevBuf<double> samp;                // sharded build: mass samples (splitters)
     DevBuf<unsigned long long> xcount;  // sharded build: send counts of every shard (RCCL all-gather)
+    DevBuf<uint32_t> qcnt;              // sharded queries: owners per query -> pair offsets
+    DevBuf<Rec> qpairA, qpairB;         //   (owner, query) pairs, then grouped by owner
+    DevBuf<Rec> qsend, qrecv;           //   (mass, tol) out / in
+    DevBuf<Rec> qres, qback;            //   (first, count) answered here / returned to the origin
     Counters hc{};
     uint64_t n_total_extra = 0;
 

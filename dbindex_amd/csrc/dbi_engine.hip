@@ -127,12 +127,13 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     // every allocation before the first launch of this stage: a reallocation
     // must never free a buffer that queued kernels still use
     const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + CHUNK_T - 1) / CHUNK_T, 1);
+    const size_t seg_cap = giant_seg_cap(n);
     const size_t scan_need = std::max(scan_u32_tmp_elems(hist_elems), scan_u32_tmp_elems(nchunks));
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_need, h->scan_tmp.cap)))) return rc;
     if ((rc = h->recB.ensure(n)) || (rc = h->hist.ensure(hist_elems)) ||
         (rc = h->ucount.ensure(nchunks)) || (rc = h->chunk_lo.ensure((size_t)nchunks + 1)) ||
         (rc = h->big_list.ensure(nchunks)) ||
-        (rc = h->giant_list.ensure(nchunks)) ||
+        (rc = h->giant_list.ensure(nchunks)) || (rc = h->segs.ensure((GIANT_PASSES + 4) * seg_cap)) ||
         (rc = h->ws_key.ensure(4 * n)) || (rc = h->ws_k2.ensure(4 * n)) ||
         (rc = h->umass.ensure(n)) || (rc = h->upid.ensure(n)) || (rc = h->uoff.ensure(n)) ||
         (rc = h->ulen.ensure(n)) || (rc = h->occ_off.ensure(n + 1)) || (rc = h->occ_pid.ensure(n)))
@@ -169,8 +170,8 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
           launch_chunk_sort_big(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                                 h->giant_list.p, std::min<uint32_t>(nchunks, 256u), h->ctr.p, s));
     STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
-          launch_big_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,
-                            std::min<uint32_t>(nchunks, 256u), h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
+          launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p, h->segs.p,
+                              seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
     // unique offsets per chunk
     STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
           launch_scan_u32(h->ucount.p, h->ucount.p, nchunks, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_unique, s));
@@ -186,6 +187,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
 int finish_build(dbi_handle* h) {
     int rc = read_counters(h);
     if (rc) return rc;
+    if (h->hc.err & ERR_SEGS) return set_error(DBI_E_STATE, "internal: giant-chunk segment list overflow");
     if (h->hc.err & ERR_LAYOUT)
         return set_error(DBI_E_INVALID, "2 x bits(longest protein) + bits(protein count) exceeds the 56 bits of the "
                                         "16-B occurrence record: shard the FASTA");
@@ -215,7 +217,7 @@ int finish_build(dbi_handle* h) {
     bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->poff_g.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
     bytes += h->thr.bytes() + h->tile_pf.bytes() + h->chunk_lo.bytes();
     bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->ucount.bytes();
-    bytes += h->big_list.bytes() + h->giant_list.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
+    bytes += h->big_list.bytes() + h->giant_list.bytes() + h->segs.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
     bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes();
     st.device_bytes = bytes;
     h->built = true;
@@ -474,11 +476,13 @@ void dbi_close(dbi_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
     h->res.release(); h->poff64.release(); h->poff.release(); h->poff_g.release();
-    h->samp.release(); h->xcount.release(); h->blk.release(); h->scan_tmp.release();
+    h->samp.release(); h->xcount.release();
+    h->qcnt.release(); h->qpairA.release(); h->qpairB.release(); h->qsend.release(); h->qrecv.release();
+    h->qres.release(); h->qback.release(); h->blk.release(); h->scan_tmp.release();
     h->status.release();
     h->thr.release(); h->tile_pf.release(); h->chunk_lo.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
-    h->big_list.release(); h->giant_list.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
+    h->big_list.release(); h->giant_list.release(); h->segs.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
     h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release();
     h->o_mass.release(); h->o_pid.release(); h->o_off.release(); h->o_len.release();
     h->q_mass.release(); h->q_tol.release(); h->q_first.release(); h->q_count.release(); h->q_row.release();

@@ -100,6 +100,8 @@ struct DevParams {
     int32_t cut_count;        // count by cut stepping (full enzyme, no mandatory AAs, residue masses < 1024 Da)
 };
 
+constexpr int GIANT_PASSES = 3;  // MSD split passes over chunks above BIG_CAP (then the global-memory fallback)
+
 // Device counters block (one per engine), read back once per build.
 struct Counters {
     unsigned long long n_kept;     // occurrences stored
@@ -110,7 +112,9 @@ struct Counters {
     unsigned long long n_slots;    // bounded digest: record slots reserved (kept + sentinels)
     unsigned int n_big;            // chunks above CHUNK_CAP (sorted by the 1024-thread LDS kernel)
     unsigned int err;              // device error bits
-    unsigned int n_giant;          // chunks above BIG_CAP (global-memory path)
+    unsigned int n_giant;          // chunks above BIG_CAP (MSD split into LDS-sized leaves)
+    unsigned int n_seg[GIANT_PASSES + 1];  // giant split: segments in work list p
+    unsigned int n_leaf_small, n_leaf_big, n_fallback;
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads
     // (sharing the ticket's line cost the digest 30%)
@@ -118,6 +122,7 @@ struct Counters {
     alignas(256) unsigned int max_plen;     // longest protein (k_tile_proteins): the record field width
 };
 constexpr unsigned ERR_LAYOUT = 1;  // 2*bits(longest protein) + bits(proteins) > 56
+constexpr unsigned ERR_SEGS = 2;    // giant split: a segment list overflowed (internal)
 
 // Tunables
 constexpr int DIGEST_THREADS = 256;
@@ -192,6 +197,14 @@ inline int owner_bits(uint32_t nshards) {
     while ((1u << b) < nshards) ++b;
     return b;
 }
+// Query routing of a sharded index: a window [lo, hi] goes to every owner
+// whose key range meets [(int)(lo*factor), (int)(hi*factor)].
+struct RouteMap {
+    int32_t split[MAX_SHARDS - 1];
+    uint32_t nshards;
+    int32_t factor;
+    int32_t nb, br;  // NUM_BUCKETS / BUCKET_MASS_RANGE: windows past the last bucket are empty
+};
 // sparse: the input holds REC_SENTINEL slots (bounded digest), left out of the output
 hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,
                              uint32_t* d_hist, hipStream_t s);
@@ -203,6 +216,25 @@ hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bo
                              hipStream_t s);
 hipError_t launch_owner_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const OwnerMap& om, bool sparse,
                                 const uint32_t* d_hist, hipStream_t s);
+// stable partition of query routing pairs (q0 = owner, q1 = query index) by owner
+hipError_t launch_pair_hist(const Rec* d_in, uint32_t n, uint32_t nshards, uint32_t* d_hist, hipStream_t s);
+hipError_t launch_pair_scatter(const Rec* d_in, Rec* d_out, uint32_t n, uint32_t nshards, const uint32_t* d_hist,
+                               hipStream_t s);
+// cnt[i] = owners query i's window meets (0: empty window)
+hipError_t launch_qroute_count(const double* d_qm, const double* d_qt, uint64_t nq, const RouteMap& rm,
+                               uint32_t* d_cnt, hipStream_t s);
+// pairs[offs[i] + k] = (owner o0 + k, i)
+hipError_t launch_qroute_emit(const double* d_qm, const double* d_qt, uint64_t nq, const RouteMap& rm,
+                              const uint32_t* d_offs, Rec* d_pairs, hipStream_t s);
+// out[p] = (mass, tol) bits of pair p's query
+hipError_t launch_qpack(const Rec* d_pairs, uint64_t np, const double* d_qm, const double* d_qt, Rec* d_out,
+                        hipStream_t s);
+// owner side: (mass, tol) -> (base + first, count), first = ~0 when count = 0
+hipError_t launch_query_pairs(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,
+                              const Rec* d_in, uint64_t n, uint64_t base, Rec* d_out, hipStream_t s);
+// origin side: fold the owners' answers into per-query (first, count)
+hipError_t launch_qcombine(const Rec* d_pairs, const Rec* d_res, uint64_t np, uint64_t* d_first,
+                           uint64_t* d_count, uint64_t nq, hipStream_t s);
 // out[i] = mass of slot i * n / ns (NaN for a sentinel slot), i < ns
 hipError_t launch_sample_masses(const Rec* d_recs, uint64_t n, uint32_t ns, double* d_out, hipStream_t s);
 // out[i] = in[i] - base (u64 -> u32 offsets of a protein range)
@@ -220,10 +252,15 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
                                  const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t* d_giant_list,
                                  uint32_t max_blocks, Counters* d_ctr, hipStream_t s);
-// chunks above BIG_CAP listed in d_giant_list: global-memory scratch
-hipError_t launch_big_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                             const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_giant_list, uint32_t max_blocks,
-                             unsigned long long* d_ws_key, uint32_t* d_ws_k2, Counters* d_ctr, hipStream_t s);
+// chunks above BIG_CAP listed in d_giant_list: MSD split on the (mass, tag)
+// key into leaves sorted in LDS; a segment of one (mass, tag) key above
+// BIG_CAP falls back to global-memory scratch (ws_key / ws_k2).  segs: 5 lists
+// of seg_cap entries (two work lists, small leaves, big leaves, fallback).
+size_t giant_seg_cap(uint64_t n);
+hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
+                               const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_giant_list,
+                               uint4* d_segs, size_t seg_cap, unsigned long long* d_ws_key, uint32_t* d_ws_k2,
+                               Counters* d_ctr, hipStream_t s);
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
                            uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, Counters* d_ctr, hipStream_t s);

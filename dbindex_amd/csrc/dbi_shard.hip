@@ -94,6 +94,111 @@ void key_range(const int32_t* split, int nshards, int r, int32_t* lo, int32_t* h
     *hi = r == nshards - 1 ? INT32_MAX : split[r];
 }
 
+// 16-B items from every rank to every rank: item slices [soff[p], +scnt[p]) of
+// `send` go to rank p, which receives them at its roff[me]; one group of
+// point-to-point transfers over all peers, the rank's own slice by a copy
+int nccl_alltoallv(dbi_comm* c, const Rec* send, const std::vector<uint64_t>& soff, const std::vector<uint64_t>& scnt,
+                   Rec* recv, const std::vector<uint64_t>& roff, const std::vector<uint64_t>& rcnt, hipStream_t s) {
+    const int me = c->rank;
+    if (scnt[me])
+        DBI_HIP(hipMemcpyAsync(recv + roff[me], send + soff[me], scnt[me] * sizeof(Rec), hipMemcpyDeviceToDevice, s));
+    DBI_NCCL(ncclGroupStart());
+    for (int p = 0; p < c->nranks; ++p) {
+        if (p == me) continue;
+        if (scnt[p]) DBI_NCCL(ncclSend(send + soff[p], scnt[p] * sizeof(Rec), ncclUint8, p, c->comm, s));
+        if (rcnt[p]) DBI_NCCL(ncclRecv(recv + roff[p], rcnt[p] * sizeof(Rec), ncclUint8, p, c->comm, s));
+    }
+    DBI_NCCL(ncclGroupEnd());
+    return 0;
+}
+
+// all[i * n + j] = mine_i[j] of every rank i (u64 all-gather through h->xcount)
+int nccl_count_matrix(dbi_handle* h, dbi_comm* c, const std::vector<uint64_t>& mine, std::vector<uint64_t>& all) {
+    const int n = c->nranks, me = c->rank;
+    hipStream_t s = h->stream;
+    int rc;
+    if ((rc = h->xcount.ensure((size_t)n * n + 8))) return rc;
+    all.assign((size_t)n * n, 0);
+    for (int j = 0; j < n; ++j) all[(size_t)me * n + j] = mine[j];
+    DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * n, all.data() + (size_t)me * n, sizeof(uint64_t) * n,
+                           hipMemcpyHostToDevice, s));
+    DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * n, h->xcount.p, n, ncclUint64, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(all.data(), h->xcount.p, sizeof(uint64_t) * n * n, hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+void offsets_of(const std::vector<uint64_t>& cnt, std::vector<uint64_t>& off) {
+    off.assign(cnt.size() + 1, 0);
+    for (size_t i = 0; i < cnt.size(); ++i) off[i + 1] = off[i] + cnt[i];
+}
+
+// ---- routed queries (the owner slices of a sharded index) ----
+int query_route(dbi_handle* h, const double* d_m, const double* d_t, uint64_t nq) {
+    ShardState& sh = h->shard;
+    hipStream_t s = h->stream;
+    if (nq >= (1ull << 31)) return set_error(DBI_E_INVALID, "at most 2^31-1 queries per batch and rank");
+    RouteMap rm{};
+    for (int j = 0; j + 1 < sh.nshards; ++j) rm.split[j] = sh.split[j];
+    rm.nshards = (uint32_t)sh.nshards;
+    rm.factor = h->params.mass_group_factor;
+    rm.nb = h->dp.nb;
+    rm.br = h->dp.br;
+    int rc;
+    if ((rc = h->qcnt.ensure(nq + 1)) || (rc = h->xcount.ensure(std::max<size_t>(h->xcount.cap, 8))) ||
+        (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(nq + 1), h->scan_tmp.cap))))
+        return rc;
+    DBI_HIP(launch_qroute_count(d_m, d_t, nq, rm, h->qcnt.p, s));
+    unsigned long long np = 0;
+    if (nq) {
+        DBI_HIP(launch_scan_u32(h->qcnt.p, h->qcnt.p, nq, h->scan_tmp.p, h->scan_tmp.cap, h->xcount.p, s));
+        DBI_HIP(hipMemcpyAsync(&np, h->xcount.p, sizeof(np), hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipStreamSynchronize(s));
+    }
+    const int ns = sh.nshards, bits = owner_bits((uint32_t)ns);
+    const uint32_t n32 = (uint32_t)np;
+    const uint64_t g = radix_blocks(n32);
+    const size_t hist_elems = std::max<size_t>(radix_hist_elems(n32, bits), 1);
+    if ((rc = h->qpairA.ensure(np + 1)) || (rc = h->qpairB.ensure(np + 1)) || (rc = h->qsend.ensure(np + 1)) ||
+        (rc = h->qback.ensure(np + 1)) || (rc = h->hist.ensure(std::max<size_t>(hist_elems, h->hist.cap))) ||
+        (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(hist_elems), h->scan_tmp.cap))))
+        return rc;
+    std::vector<uint32_t> start(ns + 1, 0);
+    if (np) {
+        DBI_HIP(launch_qroute_emit(d_m, d_t, nq, rm, h->qcnt.p, h->qpairA.p, s));
+        DBI_HIP(launch_pair_hist(h->qpairA.p, n32, (uint32_t)ns, h->hist.p, s));
+        DBI_HIP(launch_scan_u32(h->hist.p, h->hist.p, g << bits, h->scan_tmp.p, h->scan_tmp.cap, nullptr, s));
+        DBI_HIP(launch_pair_scatter(h->qpairA.p, h->qpairB.p, n32, (uint32_t)ns, h->hist.p, s));
+        DBI_HIP(launch_qpack(h->qpairB.p, np, d_m, d_t, h->qsend.p, s));
+        DBI_HIP(hipMemcpy2DAsync(start.data(), sizeof(uint32_t), h->hist.p, g * sizeof(uint32_t), sizeof(uint32_t),
+                                 (size_t)ns, hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipStreamSynchronize(s));
+    }
+    start[ns] = n32;
+    sh.q_n = nq;
+    sh.q_pairs = np;
+    sh.qsend_count.assign(ns, 0);
+    for (int d = 0; d < ns; ++d) sh.qsend_count[d] = (uint64_t)start[d + 1] - start[d];
+    offsets_of(sh.qsend_count, sh.qsend_off);
+    return 0;
+}
+
+int query_answer(dbi_handle* h) {
+    ShardState& sh = h->shard;
+    int rc;
+    if ((rc = h->qres.ensure(sh.q_recv + 1))) return rc;
+    DBI_HIP(launch_query_pairs(h->dp, h->params.mass_group_factor, h->umass.p, (uint32_t)h->stats.n_unique,
+                               h->qrecv.p, sh.q_recv, sh.u_base, h->qres.p, h->stream));
+    return 0;
+}
+
+int query_need(const dbi_handle* h) {
+    if (h->shard.phase != 4 || !h->built || !h->shard.u_base_known)
+        return set_error(DBI_E_STATE, "sharded queries need a finished sharded build (dbi_build_sharded, or the "
+                                      "phases through dbi_shard_merge on every shard)");
+    return 0;
+}
+
 }  // namespace
 }  // namespace dbi
 
@@ -357,6 +462,87 @@ int dbi_shard_stats_get(dbi_handle* h, dbi_shard_stats* out) {
     return 0;
 }
 
+int dbi_query_sharded_local(dbi_handle* const* hs, int nshards, const double* const* d_mass,
+                            const double* const* d_tol, const uint64_t* nq, uint64_t* const* d_first,
+                            uint64_t* const* d_count) {
+    if (!hs || !d_mass || !d_tol || !nq || !d_first || !d_count || nshards < 1)
+        return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    uint64_t base = 0;
+    for (int i = 0; i < nshards; ++i) {
+        dbi_handle* h = hs[i];
+        if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+        if (h->shard.nshards != nshards || h->shard.rank != i)
+            return set_error(DBI_E_INVALID, "hs[i] must be shard i of nshards");
+        h->shard.u_base = base;  // owners' tables concatenate in shard order
+        h->shard.u_base_known = h->shard.phase == 4;
+        base += h->stats.n_unique;
+        if ((rc = query_need(h))) return rc;
+    }
+    for (int i = 0; i < nshards; ++i) {
+        DBI_HIP(hipSetDevice(hs[i]->device));
+        if ((rc = query_route(hs[i], d_mass[i], d_tol[i], nq[i]))) return rc;
+    }
+    // forward: origin i's pairs for owner j -> owner j; answer; back to the origins
+    for (int j = 0; j < nshards; ++j) {
+        dbi_handle* o = hs[j];
+        ShardState& sh = o->shard;
+        sh.qrecv_count.assign(nshards, 0);
+        for (int i = 0; i < nshards; ++i) sh.qrecv_count[i] = hs[i]->shard.qsend_count[j];
+        offsets_of(sh.qrecv_count, sh.qrecv_off);
+        sh.q_recv = sh.qrecv_off[nshards];
+        DBI_HIP(hipSetDevice(o->device));
+        if ((rc = o->qrecv.ensure(sh.q_recv + 1))) return rc;
+        for (int i = 0; i < nshards; ++i)
+            if (sh.qrecv_count[i])
+                DBI_HIP(hipMemcpyAsync(o->qrecv.p + sh.qrecv_off[i], hs[i]->qsend.p + hs[i]->shard.qsend_off[j],
+                                       sh.qrecv_count[i] * sizeof(Rec), hipMemcpyDeviceToDevice, o->stream));
+        if ((rc = query_answer(o))) return rc;
+        DBI_HIP(hipStreamSynchronize(o->stream));
+    }
+    for (int i = 0; i < nshards; ++i) {
+        dbi_handle* h = hs[i];
+        ShardState& sh = h->shard;
+        DBI_HIP(hipSetDevice(h->device));
+        for (int j = 0; j < nshards; ++j)
+            if (sh.qsend_count[j])
+                DBI_HIP(hipMemcpyAsync(h->qback.p + sh.qsend_off[j], hs[j]->qres.p + hs[j]->shard.qrecv_off[i],
+                                       sh.qsend_count[j] * sizeof(Rec), hipMemcpyDeviceToDevice, h->stream));
+        DBI_HIP(launch_qcombine(h->qpairB.p, h->qback.p, sh.q_pairs, d_first[i], d_count[i], sh.q_n, h->stream));
+        DBI_HIP(hipStreamSynchronize(h->stream));
+    }
+    return 0;
+}
+
+int dbi_query_sharded(dbi_handle* h, dbi_comm* c, const double* d_mass, const double* d_tol, uint64_t nq,
+                      uint64_t* d_first, uint64_t* d_count) {
+    if (!h || !c || (nq && (!d_mass || !d_tol || !d_first || !d_count))) return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = query_need(h))) return rc;
+    if (h->shard.nshards != c->nranks || h->shard.rank != c->rank)
+        return set_error(DBI_E_INVALID, "communicator does not match the sharded build");
+    DBI_HIP(hipSetDevice(h->device));
+    ShardState& sh = h->shard;
+    hipStream_t s = h->stream;
+    const int n = c->nranks, me = c->rank;
+    if ((rc = query_route(h, d_mass, d_tol, nq))) return rc;
+    std::vector<uint64_t> counts;
+    if ((rc = nccl_count_matrix(h, c, sh.qsend_count, counts))) return rc;
+    sh.qrecv_count.assign(n, 0);
+    for (int i = 0; i < n; ++i) sh.qrecv_count[i] = counts[(size_t)i * n + me];
+    offsets_of(sh.qrecv_count, sh.qrecv_off);
+    sh.q_recv = sh.qrecv_off[n];
+    if ((rc = h->qrecv.ensure(sh.q_recv + 1))) return rc;
+    if ((rc = nccl_alltoallv(c, h->qsend.p, sh.qsend_off, sh.qsend_count, h->qrecv.p, sh.qrecv_off, sh.qrecv_count, s)))
+        return rc;
+    if ((rc = query_answer(h))) return rc;
+    if ((rc = nccl_alltoallv(c, h->qres.p, sh.qrecv_off, sh.qrecv_count, h->qback.p, sh.qsend_off, sh.qsend_count, s)))
+        return rc;
+    DBI_HIP(launch_qcombine(h->qpairB.p, h->qback.p, sh.q_pairs, d_first, d_count, sh.q_n, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
 // ---- RCCL -------------------------------------------------------------------------
 
 int dbi_comm_unique_id(uint8_t* id128) {
@@ -444,22 +630,16 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
 
     // send counts of every shard: counts[i * n + j] = records shard i sends owner j
     const double t0 = now_ms();
-    if ((rc = h->xcount.ensure((size_t)n * n + 8))) return rc;
-    std::vector<unsigned long long> counts((size_t)n * n);
-    for (int j = 0; j < n; ++j) counts[(size_t)me * n + j] = sh.send_count[j];
-    DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * n, counts.data() + (size_t)me * n, sizeof(uint64_t) * n,
-                           hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * n, h->xcount.p, n, ncclUint64, c->comm, s));
-    DBI_HIP(hipMemcpyAsync(counts.data(), h->xcount.p, sizeof(uint64_t) * n * n, hipMemcpyDeviceToHost, s));
-    DBI_HIP(hipStreamSynchronize(s));
+    std::vector<uint64_t> counts;
+    if ((rc = nccl_count_matrix(h, c, sh.send_count, counts))) return rc;
     sh.recv_count.assign(n, 0);
-    std::vector<uint64_t> roff(n + 1, 0);
     uint64_t from_others = 0;
     for (int i = 0; i < n; ++i) {
         sh.recv_count[i] = counts[(size_t)i * n + me];
-        roff[i + 1] = roff[i] + sh.recv_count[i];
         if (i != me) from_others += sh.recv_count[i];
     }
+    std::vector<uint64_t> roff;
+    offsets_of(sh.recv_count, roff);
     if (sh.send_count[me] != sh.recv_count[me]) return set_error(DBI_E_STATE, "shard count exchange mismatch");
     if (roff[n] >= (1ull << 32) - 1)
         return set_error(DBI_E_INVALID, "more than 2^32-2 records for one owner: use more shards");
@@ -468,18 +648,8 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // records to their owners: one group of point-to-point transfers over all peers
     {
         ManualStage ms(h, "exchange", 16.0 * (double)(from_others + (sh.n_digest - sh.send_count[me])));
-        if (sh.send_count[me])
-            DBI_HIP(hipMemcpyAsync(h->recA.p + roff[me], h->recB.p + sh.send_off[me], sh.send_count[me] * sizeof(Rec),
-                                   hipMemcpyDeviceToDevice, s));
-        DBI_NCCL(ncclGroupStart());
-        for (int p = 0; p < n; ++p) {
-            if (p == me) continue;
-            if (sh.send_count[p])
-                DBI_NCCL(ncclSend(h->recB.p + sh.send_off[p], sh.send_count[p] * sizeof(Rec), ncclUint8, p, c->comm, s));
-            if (sh.recv_count[p])
-                DBI_NCCL(ncclRecv(h->recA.p + roff[p], sh.recv_count[p] * sizeof(Rec), ncclUint8, p, c->comm, s));
-        }
-        DBI_NCCL(ncclGroupEnd());
+        if ((rc = nccl_alltoallv(c, h->recB.p, sh.send_off, sh.send_count, h->recA.p, roff, sh.recv_count, s)))
+            return rc;
         ms.end();
     }
     DBI_HIP(hipStreamSynchronize(s));
@@ -488,12 +658,25 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     sh.phase = 3;
     if ((rc = dbi_shard_merge(h))) return rc;
 
-    // whole-index totals
-    unsigned long long tot[5] = {sh.n_total, sh.n_dropped, sh.n_recv, h->stats.n_unique, h->stats.n_keys};
-    DBI_HIP(hipMemcpyAsync(h->xcount.p, tot, sizeof(tot), hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllReduce(h->xcount.p, h->xcount.p, 5, ncclUint64, ncclSum, c->comm, s));
-    DBI_HIP(hipMemcpyAsync(tot, h->xcount.p, sizeof(tot), hipMemcpyDeviceToHost, s));
-    DBI_HIP(hipStreamSynchronize(s));
+    // whole-index totals, and where this owner's rows start in the whole index
+    std::vector<uint64_t> tot(5, 0);
+    {
+        const int w = 5;
+        if ((rc = h->xcount.ensure((size_t)n * w + 8))) return rc;
+        std::vector<unsigned long long> row(w, 0), rows((size_t)n * w);
+        row[0] = sh.n_total; row[1] = sh.n_dropped; row[2] = sh.n_recv; row[3] = h->stats.n_unique;
+        row[4] = h->stats.n_keys;
+        DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * w, row.data(), sizeof(uint64_t) * w, hipMemcpyHostToDevice, s));
+        DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * w, h->xcount.p, w, ncclUint64, c->comm, s));
+        DBI_HIP(hipMemcpyAsync(rows.data(), h->xcount.p, sizeof(uint64_t) * n * w, hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipStreamSynchronize(s));
+        sh.u_base = 0;
+        for (int i = 0; i < n; ++i) {
+            for (int k = 0; k < 5; ++k) tot[k] += rows[(size_t)i * w + k];
+            if (i < me) sh.u_base += rows[(size_t)i * w + 3];
+        }
+        sh.u_base_known = true;
+    }
     sh.global.g_total = tot[0];
     sh.global.g_dropped = tot[1];
     sh.global.g_kept = tot[2];

@@ -166,3 +166,34 @@ def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off
     for eng in engines:
         check(L.dbi_shard_merge(eng.h))
     return split
+
+
+def query_sharded(eng: Engine, comm: ShardComm, d_mass: int, d_tol: int, nq: int, d_first: int,
+                  d_count: int) -> None:
+    """This rank's batch against the sharded index (dbi_query_sharded): windows
+    routed to their key owners over RCCL; ids of the whole index come back."""
+    check(_native.lib().dbi_query_sharded(eng.h, comm.h, ctypes.c_void_p(d_mass), ctypes.c_void_p(d_tol), nq,
+                                          ctypes.c_void_p(d_first), ctypes.c_void_p(d_count)))
+
+
+def query_sharded_local(engines: Sequence[Engine], batches: Sequence[Tuple[np.ndarray, np.ndarray]]):
+    """Every shard's batch routed between the handles of this process
+    (dbi_query_sharded_local).  Returns [(first, count)] per shard, ids of the
+    whole index."""
+    from ._native import DeviceBuffer
+    n = len(engines)
+    assert len(batches) == n
+    dev = engines[0].device
+    bufs = []
+    for m, t in batches:
+        m = np.ascontiguousarray(m, np.float64)
+        t = np.ascontiguousarray(np.broadcast_to(t, m.shape), np.float64)
+        k = m.shape[0]
+        bufs.append((DeviceBuffer.from_numpy(m, dev) if k else DeviceBuffer(8, dev),
+                     DeviceBuffer.from_numpy(t, dev) if k else DeviceBuffer(8, dev),
+                     DeviceBuffer(8 * max(k, 1), dev), DeviceBuffer(8 * max(k, 1), dev), k))
+    arr = lambda i: (ctypes.c_void_p * n)(*[b[i].ptr for b in bufs])  # noqa: E731
+    nq = np.array([b[4] for b in bufs], np.uint64)
+    hs = (ctypes.c_void_p * n)(*[e.h.value for e in engines])
+    check(_native.lib().dbi_query_sharded_local(hs, n, arr(0), arr(1), _p(nq), arr(2), arr(3)))
+    return [(b[2].download(np.uint64, b[4]), b[3].download(np.uint64, b[4])) for b in bufs]

@@ -235,6 +235,7 @@ int dbi_stage_times(dbi_handle* h, const char** names, double* ms, double* bytes
  * its own key range (ids are local to the owner's table).
  */
 #define DBI_SHARD_SAMPLES 4096
+typedef struct dbi_comm dbi_comm; /* RCCL communicator, below */
 #define DBI_MAX_SHARDS 64
 
 typedef struct dbi_shard_stats {
@@ -273,9 +274,21 @@ int dbi_shard_exchange_local(dbi_handle* const* hs, int nshards);
 int dbi_shard_merge(dbi_handle* h);
 int dbi_shard_stats_get(dbi_handle* h, dbi_shard_stats* out);
 
+/* Mass-window queries against a sharded index, getSequences(m, tol) semantics
+ * (DBIndexStoreSQLiteMult.java:315-350): each rank passes its own batch
+ * (device arrays); every window goes to the owners whose key range it meets,
+ * is answered there, and comes back as ids first..first+count-1 of the WHOLE
+ * index (the owners' unique tables concatenated in shard order). */
+int dbi_query_sharded(dbi_handle* h, dbi_comm* c, const double* d_mass, const double* d_tol, uint64_t nq,
+                      uint64_t* d_first, uint64_t* d_count);
+/* The same over the handles of one process: shard i's batch is
+ * (d_mass[i], d_tol[i], nq[i]) with results in (d_first[i], d_count[i]). */
+int dbi_query_sharded_local(dbi_handle* const* hs, int nshards, const double* const* d_mass,
+                            const double* const* d_tol, const uint64_t* nq, uint64_t* const* d_first,
+                            uint64_t* const* d_count);
+
 /* RCCL communicator (one rank per GPU, xGMI).  The 128-byte id comes from
  * rank 0's dbi_comm_unique_id and is passed to every rank out of band. */
-typedef struct dbi_comm dbi_comm;
 int dbi_comm_unique_id(uint8_t* id128);
 int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_comm** out);
 void dbi_comm_destroy(dbi_comm* c);

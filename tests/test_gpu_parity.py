@@ -111,6 +111,37 @@ def test_big_bins_and_duplicates(Engine, copies):
         assert_index_equal(eng, oix, f"bigbins x{copies}")
 
 
+def _giant_isobaric():
+    """~12k proteins whose tryptic peptides are permutations of one
+    composition: thousands of bit-identical fp64 masses with different strings
+    (one chunk far above BIG_CAP, split on the peptide tag), some repeated."""
+    import itertools
+    rng = np.random.default_rng(3)
+    perms = ["".join(p) for p in itertools.permutations("ACDEFGHM")]
+    pick = [perms[i] for i in rng.choice(len(perms), 11000, replace=False)]
+    pick += pick[:1500]  # duplicates across proteins
+    return [f"MK{p}KWWR" for p in pick]
+
+
+def _giant_near_isobaric(prm):
+    """Peptides with distinct masses packed into a few mDa (residue masses of
+    a few letters overridden to tiny values): one mass bin far above BIG_CAP
+    holding thousands of different masses (split on the mass bits)."""
+    prm.residue_mass.update({"B": 0.0013, "J": 0.00071, "O": 0.000029, "U": 0.0000037, "Z": 0.19})
+    rng = np.random.default_rng(5)
+    tail = ["".join(rng.choice(list("BJOUZ"), 7)) for _ in range(14000)]
+    return [f"MRGGGGGGGGGW{t}K" for t in tail]
+
+
+@pytest.mark.parametrize("kind", ["isobaric", "near_isobaric"])
+def test_giant_chunks(Engine, kind):
+    prm = DBIndexSearchParams.trypsin(1)
+    seqs = _giant_isobaric() if kind == "isobaric" else _giant_near_isobaric(prm)
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    oix = _check(Engine, prm, pp, f"giant {kind}", nq=800)
+    assert oix.n_kept > 8000
+
+
 def test_isobaric_runs(Engine):
     """I/L swaps give bit-identical masses: equal-mass runs holding several
     peptide strings must group by string, first appearance first."""

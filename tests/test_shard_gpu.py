@@ -58,6 +58,9 @@ def _assert_sharded_equal(engines, oix, ctx, nq=1500):
     # queries: every owner answers for its slice; slices are adjacent in the
     # global table, so the union is one contiguous id range
     m, t = query_masses(oix, nq)
+    # windows wide enough to meet several owners, and past the last bucket
+    m = np.concatenate([m, [3000.0, 1000.0, 5999.0, 7999.0, 600.0]])
+    t = np.concatenate([t, [2500.0, 600.0, 0.5, 5.0, 700.0]])
     of, oc = oix.query_batch(m, t)
     first = np.full(m.shape[0], np.iinfo(np.uint64).max, np.uint64)
     count = np.zeros(m.shape[0], np.uint64)
@@ -71,6 +74,18 @@ def _assert_sharded_equal(engines, oix, ctx, nq=1500):
     assert np.array_equal(count, oc), (ctx, "query counts")
     hit = oc > 0
     assert np.array_equal(first[hit], of[hit]), (ctx, "query first ids")
+    # routed queries: each shard brings its own part of the batch (one shard none)
+    k = len(engines)
+    cuts = np.linspace(0, m.shape[0], k + 1).astype(int)
+    if k > 2:
+        cuts[1] = 0
+    batches = [(m[a:b], t[a:b]) for a, b in zip(cuts, cuts[1:])]
+    res = shard.query_sharded_local(engines, batches)
+    rf = np.concatenate([f for f, _ in res])
+    rc = np.concatenate([c for _, c in res])
+    assert np.array_equal(rc, oc), (ctx, "routed query counts")
+    assert np.array_equal(rf[hit], of[hit]), (ctx, "routed query first ids")
+    assert np.all(rf[~hit] == 0), (ctx, "routed empty queries")
 
 
 def _run_local(native, prm, pp, k, ranges=None, ctx=""):
@@ -139,6 +154,14 @@ def test_sharded_rccl_single_rank(native):
                                          0, pp.n_proteins)
                 assert st.g_total == oix.n_total and st.g_unique == oix.n_unique and st.g_keys == oix.n_keys
                 _assert_sharded_equal([eng], oix, f"rccl x1 [{rep}]")
+            # routed queries over RCCL (one rank: the owner is this rank)
+            m, t = query_masses(oix, 3000)
+            of, oc = oix.query_batch(m, t)
+            dm, dt = native.DeviceBuffer.from_numpy(m, 0), native.DeviceBuffer.from_numpy(t, 0)
+            df, dc = native.DeviceBuffer(8 * m.shape[0], 0), native.DeviceBuffer(8 * m.shape[0], 0)
+            shard.query_sharded(eng, comm, dm.ptr, dt.ptr, m.shape[0], df.ptr, dc.ptr)
+            f, c = df.download(np.uint64, m.shape[0]), dc.download(np.uint64, m.shape[0])
+            assert np.array_equal(c, oc) and np.array_equal(f[oc > 0], of[oc > 0])
             # all-gatherv of one rank: a copy
             src = native.DeviceBuffer.from_numpy(np.arange(100, dtype=np.uint8), 0)
             dst = native.DeviceBuffer(100, 0)
