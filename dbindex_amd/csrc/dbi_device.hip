@@ -1810,7 +1810,7 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
 __global__ void __launch_bounds__(BIG_THREADS)
 k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
                  const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
-                 const uint32_t* __restrict__ big_list, uint32_t* __restrict__ giant_list,
+                 const uint32_t* __restrict__ big_list, uint32_t* __restrict__ giant_list, uint32_t split_above,
                  Counters* __restrict__ ctr) {
     static_assert(BIG_CAP <= 65535, "16-bit positions");
     __shared__ unsigned long long k0[BIG_CAP];
@@ -1824,7 +1824,7 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
         const uint32_t c = big_list[j];
         const uint32_t a = chunk_lo[c];
         const uint32_t m = chunk_lo[c + 1] - a;
-        if (m > (uint32_t)BIG_CAP) {
+        if (m > split_above) {
             if (threadIdx.x == 0) giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
             continue;
         }
@@ -1837,10 +1837,11 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
 
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
                                  const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list,
-                                 uint32_t* d_giant_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s) {
+                                 uint32_t* d_giant_list, uint32_t max_blocks, uint32_t split_above, Counters* d_ctr,
+                                 hipStream_t s) {
     if (max_blocks == 0) return hipSuccess;
     DBI_LAUNCH(k_chunk_sort_big, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res, d_poff,
-               d_ucount, d_big_list, d_giant_list, d_ctr);
+               d_ucount, d_big_list, d_giant_list, std::min<uint32_t>(split_above, (uint32_t)BIG_CAP), d_ctr);
     return hipGetLastError();
 }
 

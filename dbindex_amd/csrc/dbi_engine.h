@@ -88,6 +88,8 @@ struct dbi_handle {
     DevParams dp;
     int device = 0;
     hipStream_t stream = nullptr;
+    int bin_bits_max = 24;               // fine mass bins <= 2^bin_bits_max (radix passes of <= 8 bits)
+    uint32_t split_above = dbi::BIG_CAP; // chunks above this many records take the MSD split path
     bool timing = true;                  // per-stage kernel-attached events (dbi_set_timing)
     std::string timing_only;             // "" = every stage
     std::chrono::steady_clock::time_point t0;

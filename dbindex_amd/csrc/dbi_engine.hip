@@ -11,6 +11,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -86,10 +87,10 @@ DevParams make_dev_params(const dbi_params& p) {
     return d;
 }
 
-uint32_t choose_nbins(uint64_t n) {
+uint32_t choose_nbins(uint64_t n, int max_bits) {
     uint64_t want = n / BIN_AVG;  // fine mass bins; chunks group them to ~CHUNK_T records
     uint32_t b = 1;
-    while (b < want && b < (1u << 24)) b <<= 1;
+    while (b < want && b < (1u << max_bits)) b <<= 1;
     return b;
 }
 
@@ -113,7 +114,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     hipStream_t s = h->stream;
     int rc;
     const uint32_t n32 = (uint32_t)n;
-    const uint32_t nbins = choose_nbins(n);
+    const uint32_t nbins = choose_nbins(n, h->bin_bits_max);
     BinMap bm;
     bm.lo = lo;
     bm.nbins = nbins;
@@ -168,7 +169,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
                             h->ctr.p, s));
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
           launch_chunk_sort_big(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                                h->giant_list.p, std::min<uint32_t>(nchunks, 256u), h->ctr.p, s));
+                                h->giant_list.p, std::min<uint32_t>(nchunks, 256u), h->split_above, h->ctr.p, s));
     STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
           launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p, h->segs.p,
                               seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
@@ -448,6 +449,9 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     h->params = *params;
     h->dp = make_dev_params(*params);
     h->device = device;
+    // tuning knobs (defaults are the measured best; environment overrides for experiments)
+    if (const char* ev = std::getenv("DBI_BIN_BITS_MAX")) h->bin_bits_max = std::max(1, std::min(32, std::atoi(ev)));
+    if (const char* ev = std::getenv("DBI_SPLIT_ABOVE")) h->split_above = (uint32_t)std::max(1, std::atoi(ev));
     auto fail = [&](int code) {
         dbi_close(h);
         return code;

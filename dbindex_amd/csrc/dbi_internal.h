@@ -251,7 +251,7 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
 // chunks of (CHUNK_CAP, BIG_CAP] records listed in d_big_list: LDS bitonic, 1024 threads
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
                                  const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t* d_giant_list,
-                                 uint32_t max_blocks, Counters* d_ctr, hipStream_t s);
+                                 uint32_t max_blocks, uint32_t split_above, Counters* d_ctr, hipStream_t s);
 // chunks above BIG_CAP listed in d_giant_list: MSD split on the (mass, tag)
 // key into leaves sorted in LDS; a segment of one (mass, tag) key above
 // BIG_CAP falls back to global-memory scratch (ws_key / ws_k2).  segs: 5 lists
