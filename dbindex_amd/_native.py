@@ -103,6 +103,9 @@ SIGNATURES = [
     ("dbi_shard_stats_get", c_int, [P, POINTER(DbiShardStats)]),
     ("dbi_query_sharded", c_int, [P, P, P, P, c_uint64, P, P]),
     ("dbi_query_sharded_local", c_int, [P, c_int, P, P, P, P, P]),
+    ("dbi_synth_proteome", c_int, [P, c_uint64, c_uint64, c_uint64, c_uint64, P, P, POINTER(c_void_p),
+                                   POINTER(c_void_p), POINTER(c_uint64)]),
+    ("dbi_count", c_int, [P, P, c_uint64, P, c_uint64, POINTER(c_uint64), POINTER(c_uint64)]),
     ("dbi_comm_unique_id", c_int, [P]),
     ("dbi_comm_init", c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
     ("dbi_comm_destroy", None, [P]),
@@ -132,6 +135,7 @@ SIGNATURES = [
     ("dbi_dev_free", c_int, [c_int, P]),
     ("dbi_dev_copy_h2d", c_int, [c_int, P, P, c_uint64]),
     ("dbi_dev_copy_d2h", c_int, [c_int, P, P, c_uint64]),
+    ("dbi_dev_copy_d2d", c_int, [c_int, P, P, c_uint64]),
     ("dbi_dev_synchronize", c_int, [c_int]),
     ("dbi_last_error", c_char_p, []),
     ("dbi_abi_version", c_int, []),
@@ -214,6 +218,10 @@ class DeviceBuffer:
         assert out.nbytes <= self.nbytes
         check(lib().dbi_dev_copy_d2h(self.device, out.ctypes.data_as(c_void_p), c_void_p(self.ptr), out.nbytes))
         return out
+
+    def copy_from_device(self, offset: int, src_ptr: int, nbytes: int) -> None:
+        assert offset + nbytes <= self.nbytes
+        check(lib().dbi_dev_copy_d2d(self.device, c_void_p(self.ptr + offset), c_void_p(src_ptr), nbytes))
 
     def free(self) -> None:
         if self.ptr:

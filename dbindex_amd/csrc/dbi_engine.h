@@ -118,6 +118,8 @@ struct dbi_handle {
     DevBuf<uint32_t> hist;
     DevBuf<uint32_t> ucount, big_list, giant_list, chunk_lo;
     DevBuf<uint4> segs;                 // giant-chunk split: segment lists
+    DevBuf<uint16_t> synth_len;         // dbi_synth_proteome: length quantile table
+    DevBuf<uint8_t> synth_res;          //   residue table
     DevBuf<unsigned long long> ws_key;
     DevBuf<uint32_t> ws_k2;
 

@@ -94,6 +94,25 @@ class Engine:
                                                   _p(m), _p(pid), _p(o), _p(ln), m.shape[0], n_dropped_extra))
         return self.stats()
 
+    def synth_proteome(self, seed: int, p_begin: int, n_prot: int, res_base: int, tables):
+        """Proteins [p_begin, p_begin+n_prot) of the counter-based synthetic
+        proteome, generated in HBM (dbi_synth_proteome): (d_res, d_off, n_res),
+        device pointers owned by this engine until its next call."""
+        lt = np.ascontiguousarray(tables[0], np.uint16)
+        rt = np.ascontiguousarray(tables[1], np.uint8)
+        assert lt.shape == (4096,) and rt.shape == (65536,)
+        d_res, d_off, n_res = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        check(_native.lib().dbi_synth_proteome(self.h, seed, p_begin, n_prot, res_base, _p(lt), _p(rt),
+                                               ctypes.byref(d_res), ctypes.byref(d_off), ctypes.byref(n_res)))
+        return d_res.value or 0, d_off.value or 0, n_res.value
+
+    def count_device(self, d_residues: int, n_res: int, d_offsets: int, n_prot: int) -> Tuple[int, int]:
+        """COUNT-mode digest (dbi_count): (totalSeqCount, bucket drops)."""
+        t, d = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_native.lib().dbi_count(self.h, ctypes.c_void_p(d_residues), n_res, ctypes.c_void_p(d_offsets),
+                                      n_prot, ctypes.byref(t), ctypes.byref(d)))
+        return t.value, d.value
+
     def stats(self) -> BuildStats:
         st = DbiStats()
         check(_native.lib().dbi_stats_get(self.h, ctypes.byref(st)))

@@ -117,6 +117,69 @@ def synthetic(n_proteins: int, seed: int, copy_frac: float = 0.10,
     return PackedProteins(res, offs, defs)
 
 
+# ----------------------------------------------------------------------------
+# Counter-based synthetic proteome (TrEMBL scale, generated on the device by
+# dbi_synth_proteome; this is its numpy twin for tests and the CPU baseline)
+# ----------------------------------------------------------------------------
+_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+_RES_SALT = np.uint64(0xD1B54A32D192ED03)
+
+
+def _fmix64(k: np.ndarray) -> np.ndarray:
+    k = k.copy()
+    k ^= k >> np.uint64(33)
+    k *= np.uint64(0xFF51AFD7ED558CCD)
+    k ^= k >> np.uint64(33)
+    k *= np.uint64(0xC4CEB9FE1A85EC53)
+    k ^= k >> np.uint64(33)
+    return k
+
+
+def synth_tables(len_mu: float = float(np.log(300.0)), len_sigma: float = 0.6, len_min: int = 30,
+                 len_max: int = 35000):
+    """(len_table u16[4096], res_table u8[65536]): lognormal length quantiles
+    clipped to [len_min, len_max] (SURVEY.md §8(d) length model) and the
+    residue CDF at SwissProt frequencies."""
+    from statistics import NormalDist
+    nd = NormalDist()
+    q = [(k + 0.5) / 4096 for k in range(4096)]
+    lens = np.array([np.exp(len_mu + len_sigma * nd.inv_cdf(x)) for x in q])
+    len_table = np.clip(np.rint(lens), len_min, len_max).astype(np.uint16)
+    letters = np.frombuffer(CANONICAL.encode("ascii"), dtype=np.uint8)
+    probs = np.array([AA_FREQ[c] for c in CANONICAL], np.float64)
+    cdf = np.cumsum(probs / probs.sum())
+    idx = np.searchsorted(cdf, (np.arange(65536) + 0.5) / 65536.0, side="right")
+    res_table = letters[np.minimum(idx, len(letters) - 1)]
+    return len_table, np.ascontiguousarray(res_table, np.uint8)
+
+
+def synth_lengths(seed: int, p_begin: int, n: int, len_table: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        k = np.uint64(seed) * _GOLDEN + np.arange(p_begin + 1, p_begin + n + 1, dtype=np.uint64)
+        return len_table[(_fmix64(k) >> np.uint64(52)).astype(np.int64)].astype(np.uint64)
+
+
+def synth_residue_base(seed: int, p_begin: int, len_table: np.ndarray, chunk: int = 1 << 22) -> int:
+    """Global index of protein p_begin's first residue (sum of earlier lengths)."""
+    tot = 0
+    for a in range(0, p_begin, chunk):
+        tot += int(synth_lengths(seed, a, min(chunk, p_begin - a), len_table).sum())
+    return tot
+
+
+def synth_proteome(seed: int, p_begin: int, n: int, res_base: int, tables=None) -> PackedProteins:
+    len_table, res_table = tables or synth_tables()
+    lens = synth_lengths(seed, p_begin, n, len_table)
+    offs = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    total = int(offs[-1])
+    with np.errstate(over="ignore"):
+        key = (np.uint64(seed) ^ _RES_SALT) * _GOLDEN + np.uint64(res_base)
+        g = key + np.arange(total, dtype=np.uint64)
+        res = res_table[(_fmix64(g) >> np.uint64(48)).astype(np.int64)]
+    return PackedProteins(np.ascontiguousarray(res, np.uint8), offs, [])
+
+
 def config(name: str, **kw) -> PackedProteins:
     c = dict(CONFIGS[name])
     c.update(kw)

@@ -302,6 +302,27 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_residues, uin
                       const uint64_t* d_prot_off, uint64_t n_prot, uint64_t p_begin, uint64_t p_end);
 
 /* ------------------------------------------------------------------------ */
+/* Count-only streaming (proteomes too large to index: TrEMBL scale)         */
+/* ------------------------------------------------------------------------ */
+/* Seeded synthetic proteome generated on the device: protein p has length
+ * len_table[fmix64(seed*G + p + 1) >> 52] (4096 entries), the residue at
+ * global residue index g is res_table[fmix64((seed ^ S)*G + g) >> 48] (65536
+ * entries), G = 0x9E3779B97F4A7C15, S = 0xD1B54A32D192ED03, fmix64 = the
+ * MurmurHash3 finaliser.  Writes proteins [p_begin, p_begin+n_prot), whose
+ * first residue has global index res_base, into buffers owned by the handle
+ * (valid until the next call on it): *d_residues[*n_res], *d_prot_off[n_prot+1]
+ * (offsets from 0).  dbindex_amd/fasta.py holds the numpy twin. */
+int dbi_synth_proteome(dbi_handle* h, uint64_t seed, uint64_t p_begin, uint64_t n_prot, uint64_t res_base,
+                       const uint16_t* len_table, const uint8_t* res_table, const uint8_t** d_residues,
+                       const uint64_t** d_prot_off, uint64_t* n_res);
+/* Digest proteins in COUNT mode (device pointers, < 2^32 residues): the
+ * cutSeq loop (DBIndexer.java:237-405) without records.  *n_total =
+ * totalSeqCount (DBIndexStoreSQLiteMult.java:277), *n_dropped = its bucket
+ * drops.  Builds no index (the handle's index, if any, is discarded). */
+int dbi_count(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, const uint64_t* d_prot_off,
+              uint64_t n_prot, uint64_t* n_total, uint64_t* n_dropped);
+
+/* ------------------------------------------------------------------------ */
 /* DBIndexStore mirror                                                      */
 /* ------------------------------------------------------------------------ */
 typedef struct dbi_store dbi_store;
@@ -369,6 +390,7 @@ int dbi_dev_alloc(int device, uint64_t bytes, void** out);
 int dbi_dev_free(int device, void* p);
 int dbi_dev_copy_h2d(int device, void* dst, const void* src, uint64_t bytes);
 int dbi_dev_copy_d2h(int device, void* dst, const void* src, uint64_t bytes);
+int dbi_dev_copy_d2d(int device, void* dst, const void* src, uint64_t bytes);
 int dbi_dev_synchronize(int device);
 
 /* ------------------------------------------------------------------------ */
