@@ -118,7 +118,8 @@ constexpr uint32_t PST_CAP = 512;  // protein starts of a tile kept in LDS (else
 struct DigestSmem {
     double mass[256];
     uint32_t pst[PST_CAP];      // poff[pf .. pl+1] (protein of a start: binary search)
-    uint16_t win[WIN];          // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST)
+    uint16_t win[WIN + 2];      // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST);
+                                // +2: walk_bounded reads one entry ahead without a clamp
     uint8_t flags[256];
     uint8_t pbit[WIN + 1];      // 1 = a protein starts at this window position (incl. one past the window)
     uint16_t cand[DIGEST_TILE]; // compacted candidate starts (tile-local), in order
@@ -826,8 +827,87 @@ __device__ void balance_candidates(DigestSmem& sm, uint32_t ncand, uint32_t B, u
     __syncthreads();
 }
 
+// The bounded digest's walk (full enzyme, no mandatory residues, <= 2 missed
+// cleavages): walk_lds<EMIT, !SEMI, !MAND> with what that mode makes
+// redundant taken out of the per-residue loop — a start emits at most
+// max_missed + 2 records (its slots are reserved: no bound check), the bucket
+// drop is compiled in only when it can happen (DROP), and the window is read
+// through a running LDS pointer one entry ahead (the array has slack, and an
+// entry past the window is never used: that step overflows).
+template <bool DROP>
+__device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const DigestSmem& sm, uint32_t i0,
+                                                uint32_t nbytes, uint64_t loc, Rec* __restrict__ out) {
+    WalkOut r{0u, 0u, false};
+    double m = dp.m0;
+    if (!(m <= dp.max_mh)) return r;
+    int mc = -1;
+    uint32_t hsh = FNV32_OFFSET;
+    uint32_t kept = 0, dropped = 0;
+    const uint16_t* wp = &sm.win[i0];
+    const uint16_t* const wlast = &sm.win[nbytes - 1];          // last staged entry
+    const uint16_t* const wmin = wp + (dp.min_len - 1);          // pepSize >= MIN_PEP_LENGTH (:331)
+    uint32_t len = 1;
+    uint32_t cur = *wp;
+    bool ovf;
+    for (;;) {
+        const uint32_t nxt = wp[1];
+        const uint32_t c = cur & 0xFFu;
+        const uint32_t fl = cur >> 8;
+        m = m + sm.mass[c];                                      // :306-308
+        mc += (int)(fl & F_CLEAVE);                              // :314-316
+        hsh = fnv32_step(hsh, c);
+        const bool last = (fl & F_LAST) != 0;
+        ovf = !last & (wp >= wlast);
+        const bool cut = (fl & F_CUT) != 0;                      // checkCleavage (:318)
+        const bool over = m > dp.max_mh;
+        const bool brk = cut & ((mc > dp.max_missed) | over);   // :322-329
+        const bool emit = cut & !brk & !ovf & (wp >= wmin) & (m >= dp.min_mh);  // :331
+        bool keep = emit;
+        if (DROP) {
+            const bool drop = emit & (m >= dp.drop_mass);        // bucket > NUM_BUCKETS-1 (:282-288)
+            keep = emit & !drop;
+            dropped += drop;
+        }
+        if (keep) {
+            const uint32_t tag = fold_tag(hsh);
+            Rec rec;
+            rec.q0 = rec_q0(m, tag);
+            rec.q1 = rec_q1(tag, loc, len);
+            out[kept] = rec;
+        }
+        kept += keep;
+        if (brk | last | over | ovf) break;                      // breaks + while condition (:284)
+        ++wp;
+        ++len;
+        cur = nxt;
+    }
+    r.kept = kept;
+    r.dropped = dropped;
+    r.overflow = ovf;
+    return r;
+}
+
+template <bool DROP>
+__device__ __forceinline__ WalkOut walk_candidate_bounded(const DevParams& dp, const DigestSmem& sm,
+                                                          const TileCtx& tc, const uint8_t* __restrict__ d_res,
+                                                          const uint32_t* __restrict__ d_poff, uint32_t j,
+                                                          Rec* __restrict__ o, const Rec* o_end) {
+    const uint32_t i = sm.cand[j];
+    const uint32_t s = tc.t0 + i;
+    uint32_t pstart;
+    const uint32_t p = tile_protein(sm, tc, d_poff, s, pstart);
+    const uint64_t loc = rec_loc(p, s - pstart, tc.w);
+    WalkOut w = walk_bounded<DROP>(dp, sm, s - tc.w0, tc.nbytes, loc, o);
+    if (w.overflow) {
+        const uint32_t pe = d_poff[find_le(d_poff, tc.pf, tc.pl + 1, s) + 1];
+        w = walk_global<true, false, false>(dp, sm, d_res, s, pe, true, loc, o, o_end);
+    }
+    return w;
+}
+
 // One walk per start (see launch_digest_bounded): reservation look-back right
 // after compaction, then emit into the thread's own slots.
+template <bool DROP>
 __global__ void __launch_bounds__(DIGEST_THREADS)
 k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                  const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
@@ -862,7 +942,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     const uint32_t lim = (je - jb) * B;
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
-        const WalkOut w = walk_candidate<true, false, false>(dp, sm, tc, d_res, d_poff, j, o + kept, o + lim);
+        const WalkOut w = walk_candidate_bounded<DROP>(dp, sm, tc, d_res, d_poff, j, o + kept, o + lim);
         kept += w.kept;
         dropped += w.dropped;
     }
@@ -883,8 +963,12 @@ hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, 
     const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     if (nblk == 0) return hipSuccess;
     if (dp.semi || dp.mand_mode) return hipErrorInvalidValue;
-    DBI_LAUNCH(k_digest_bounded, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res, d_poff,
-               n_prot, n_res, d_tile_pf, d_status, epoch, d_out, cap, d_ctr);
+    if (dp.drop_mass <= dp.max_mh)
+        DBI_LAUNCH(k_digest_bounded<true>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
+                   d_poff, n_prot, n_res, d_tile_pf, d_status, epoch, d_out, cap, d_ctr);
+    else
+        DBI_LAUNCH(k_digest_bounded<false>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
+                   d_poff, n_prot, n_res, d_tile_pf, d_status, epoch, d_out, cap, d_ctr);
     return hipGetLastError();
 }
 
