@@ -13,7 +13,7 @@ from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint3
 from .params import DbiParams
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdbindex_hip.so")
+LIB_PATH = os.environ.get("DBI_LIB_PATH") or os.path.join(HERE, "libdbindex_hip.so")  # override: experiments
 
 DBI_OK, DBI_E_INVALID, DBI_E_OOM, DBI_E_HIP, DBI_E_RCCL, DBI_E_STATE = 0, -1, -2, -3, -4, -5
 FILTER_INCLUDE, FILTER_SKIP, FILTER_SKIP_PROTEIN_START = 0, 1, 2

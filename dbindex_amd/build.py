@@ -35,19 +35,21 @@ def _newer(target: str, deps) -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, lib_out: str = LIB, defines=()) -> str:
+    """Compile + link the library (``defines``: extra -D flags for experiment variants)."""
     deps = [os.path.join(CSRC, s) for s in SOURCES]
     deps += [os.path.join(CSRC, "dbi_internal.h"), os.path.join(CSRC, "dbi_engine.h"), os.path.join(ROOT, "include", "dbindex_hip.h")]
-    if not force and _newer(LIB, deps):
-        return LIB
-    objdir = os.path.join(HERE, "build")
+    if not force and _newer(lib_out, deps):
+        return lib_out
+    objdir = os.path.join(HERE, "build") if lib_out == LIB else \
+        os.path.join(HERE, "build", os.path.basename(lib_out).replace(".so", ""))
     os.makedirs(objdir, exist_ok=True)
     cc = hipcc()
     objs = []
     procs = []
     for src in SOURCES:
         obj = os.path.join(objdir, src.replace(".", "_") + ".o")
-        cmd = [cc, *FLAGS, "-I", os.path.join(ROOT, "include")]
+        cmd = [cc, *FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include")]
         if src.endswith(".cpp"):
             cmd += ["-x", "hip"]
         cmd += ["-c", os.path.join(CSRC, src), "-o", obj]
@@ -61,14 +63,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
             raise RuntimeError(f"hipcc failed on {src}:\n{out.decode(errors='replace')}")
         if out:  # warnings are never silent
             print(out.decode(errors="replace"), file=sys.stderr)
-    tmp = LIB + ".tmp"
+    tmp = lib_out + ".tmp"
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-L/opt/rocm/lib", "-lrccl",
            "-Wl,-rpath,/opt/rocm/lib"]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout.decode(errors='replace')}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib_out)
+    return lib_out
 
 
 if __name__ == "__main__":

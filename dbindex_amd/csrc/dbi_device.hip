@@ -136,13 +136,23 @@ __device__ __forceinline__ uint32_t find_le(const uint32_t* poff, uint32_t lo, u
 }
 
 // tile_pf[t] = protein containing residue min(t*TILE, R-1), t in [0, ntiles];
-// threads < n_prot also fold their protein's length into ctr->max_plen
+// tile_pf[ntiles + 1 + t] = protein containing the last residue of tile t's
+// staged window (t < ntiles), so a digest block starts with two independent
+// loads instead of a chain of dependent ones; threads < n_prot also fold their
+// protein's length into ctr->max_plen
 __global__ void k_tile_proteins(const uint32_t* __restrict__ poff, uint32_t n_prot, uint32_t n_res, uint32_t ntiles,
                                 uint32_t* __restrict__ tile_pf, Counters* __restrict__ ctr) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t <= ntiles) {
         const uint32_t x = min(t * (uint32_t)DIGEST_TILE, n_res - 1);
-        tile_pf[t] = find_le(poff, 0, n_prot, x);
+        const uint32_t pf = find_le(poff, 0, n_prot, x);
+        tile_pf[t] = pf;
+        if (t < ntiles) {
+            const uint32_t t0 = t * (uint32_t)DIGEST_TILE;
+            const uint32_t w0 = t0 >= (uint32_t)WIN_PRE ? t0 - WIN_PRE : 0u;
+            const uint32_t w_end = min(w0 + (uint32_t)WIN, n_res);
+            tile_pf[ntiles + 1 + t] = find_le(poff, pf, n_prot, w_end - 1);
+        }
     }
     // block max, then one atomic per block that can still raise the value
     __shared__ uint32_t s_max[4];
@@ -311,12 +321,12 @@ __device__ __forceinline__ bool n_ok_at(const DigestSmem& sm, const TileCtx& tc,
 // and the residue tables in LDS, and compact the candidate starts (every start
 // in SEMI mode, else the N_ok ones) into sm.cand.  Returns the candidate count.
 template <bool SEMI>
-__device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, const double* __restrict__ d_mass_tab,
+__device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, uint32_t ntiles,
+                                   const double* __restrict__ d_mass_tab,
                                    const uint8_t* __restrict__ d_flags, const uint8_t* __restrict__ d_res,
                                    const uint32_t* __restrict__ d_poff, uint32_t n_prot, uint32_t n_res,
                                    const uint32_t* __restrict__ d_tile_pf) {
     const uint32_t tid = threadIdx.x;
-    const uint32_t ntiles = gridDim.x;
     tc.t0 = tile * (uint32_t)DIGEST_TILE;
     tc.t_end = min(tc.t0 + (uint32_t)DIGEST_TILE, n_res);
     tc.w0 = tc.t0 >= (uint32_t)WIN_PRE ? tc.t0 - WIN_PRE : 0u;
@@ -324,40 +334,47 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, c
     tc.nbytes = tc.w_end - tc.w0;
     const uint32_t w0 = tc.w0, w_end = tc.w_end, nbytes = tc.nbytes;
 
-    // residue tables -> LDS
+    // every independent global load first: the residue window (16-B vectors
+    // over its 16-B aligned interior, bytes at the ragged ends), the tile's
+    // protein range, the residue tables
+    constexpr uint32_t NV = (WIN / 16 + DIGEST_THREADS - 1) / DIGEST_THREADS + 1;
+    const uint32_t head = (uint32_t)((16u - ((uintptr_t)(d_res + w0) & 15u)) & 15u);  // bytes before the first vector
+    const uint32_t hb = min(head, nbytes);
+    const uint32_t nvec = (nbytes - hb) >> 4;
+    const uint32_t tail0 = hb + (nvec << 4);
+    const uint4* __restrict__ vbase = reinterpret_cast<const uint4*>(d_res + w0 + hb);
+    uint4 rv[NV];
+#pragma unroll
+    for (uint32_t k = 0; k < NV; ++k) {
+        const uint32_t i = tid + k * DIGEST_THREADS;
+        rv[k] = i < nvec ? vbase[i] : make_uint4(0, 0, 0, 0);
+    }
+    // ragged ends: thread t < 16 the head byte t, 16 <= t < 32 the tail byte t-16
+    uint32_t edge = 0;
+    const uint32_t epos = tid < 16 ? tid : tail0 + (tid - 16);
+    const bool has_edge = tid < 16 ? tid < hb : (tid < 32 && epos < nbytes);
+    if (has_edge) edge = d_res[w0 + epos];
+    tc.pf = d_tile_pf[tile];
+    tc.pl = d_tile_pf[ntiles + 1 + tile];  // proteins overlapping [t0, w_end]: [pf, pl]
     sm.mass[tid] = d_mass_tab[tid];
     sm.flags[tid] = d_flags[tid];
     for (uint32_t i = tid; i <= (uint32_t)WIN; i += DIGEST_THREADS) sm.pbit[i] = 0;
-    // proteins overlapping [t0, w_end]: [pf, pl] narrowed by the tile table
-    tc.pf = d_tile_pf[tile];
-    tc.pl = find_le(d_poff, tc.pf, min(d_tile_pf[min(tile + 2, ntiles)] + 1, n_prot), w_end - 1);
     const uint32_t np_all = tc.pl - tc.pf + 2;
     __syncthreads();
-    // residue window -> LDS as (residue | flags << 8), 16 residues per load when aligned
-    {
-        const uintptr_t base = (uintptr_t)(d_res + w0);
-        if ((base & 15u) == 0) {
-            const uint32_t nvec = nbytes >> 4;
-            for (uint32_t i = tid; i < nvec; i += DIGEST_THREADS) {
-                const uint4 v = reinterpret_cast<const uint4*>(d_res + w0)[i];
-                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    // residue window -> LDS as (residue | flags << 8)
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint32_t c = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-                    sm.win[i * 16 + k] = (uint16_t)(c | ((uint32_t)sm.flags[c] << 8));
-                }
-            }
-            for (uint32_t i = (nvec << 4) + tid; i < nbytes; i += DIGEST_THREADS) {
-                const uint32_t c = d_res[w0 + i];
-                sm.win[i] = (uint16_t)(c | ((uint32_t)sm.flags[c] << 8));
-            }
-        } else {
-            for (uint32_t i = tid; i < nbytes; i += DIGEST_THREADS) {
-                const uint32_t c = d_res[w0 + i];
-                sm.win[i] = (uint16_t)(c | ((uint32_t)sm.flags[c] << 8));
+    for (uint32_t k = 0; k < NV; ++k) {
+        const uint32_t i = tid + k * DIGEST_THREADS;
+        if (i < nvec) {
+            const uint32_t wv[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+                const uint32_t c = (wv[b >> 2] >> (8 * (b & 3))) & 0xFFu;
+                sm.win[hb + i * 16 + b] = (uint16_t)(c | ((uint32_t)sm.flags[c] << 8));
             }
         }
     }
+    if (has_edge) sm.win[epos] = (uint16_t)(edge | ((uint32_t)sm.flags[edge] << 8));
     tc.npst = np_all <= PST_CAP ? np_all : 0u;
     for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
         const uint32_t o = d_poff[tc.pf + i];
@@ -482,7 +499,7 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
          uint32_t* __restrict__ d_thr, Rec* __restrict__ d_out, Counters* __restrict__ d_ctr) {
     __shared__ DigestSmem sm;
     TileCtx tc;
-    const uint32_t ncand = digest_prepare<SEMI>(sm, tc, blockIdx.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
+    const uint32_t ncand = digest_prepare<SEMI>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
                                                 d_tile_pf);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
@@ -641,7 +658,7 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     __shared__ CutSmem cs;
     __shared__ double s_dtmp[DIGEST_THREADS / 64 + 1];
     TileCtx tc;
-    const uint32_t ncand = digest_prepare<false>(sm, tc, blockIdx.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
+    const uint32_t ncand = digest_prepare<false>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
                                                  d_tile_pf);
     build_cut_tables(sm, cs, tc.nbytes, s_dtmp);
     uint32_t jb, je;
@@ -724,7 +741,7 @@ k_digest_fused(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_
     __syncthreads();
     const uint32_t tile = s_tile;
     TileCtx tc;
-    const uint32_t ncand = digest_prepare<SEMI>(sm, tc, tile, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
+    const uint32_t ncand = digest_prepare<SEMI>(sm, tc, tile, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
                                                 d_tile_pf);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
@@ -906,7 +923,8 @@ __device__ __forceinline__ WalkOut walk_candidate_bounded(const DevParams& dp, c
 }
 
 // One walk per start (see launch_digest_bounded): reservation look-back right
-// after compaction, then emit into the thread's own slots.
+// after compaction, then emit into the thread's own slots.  (A persistent grid
+// taking tiles from the ticket measured slower: 2.25 vs 1.60 ms.)
 template <bool DROP>
 __global__ void __launch_bounds__(DIGEST_THREADS)
 k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
@@ -920,8 +938,8 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     __syncthreads();
     const uint32_t tile = s_tile;
     TileCtx tc;
-    const uint32_t ncand = digest_prepare<false>(sm, tc, tile, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
-                                                 d_tile_pf);
+    const uint32_t ncand = digest_prepare<false>(sm, tc, tile, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot,
+                                                 n_res, d_tile_pf);
     const uint32_t B = (uint32_t)dp.max_missed + 2u;  // records per start, at most
     if (threadIdx.x < 64) {
         const unsigned long long excl = tile_lookback(status, tile, epoch, (unsigned long long)ncand * B);

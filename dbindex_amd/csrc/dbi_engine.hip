@@ -229,7 +229,7 @@ int finish_build(dbi_handle* h) {
 int prepare_tiles(dbi_handle* h) {
     const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
     int rc;
-    if ((rc = h->tile_pf.ensure((size_t)ntiles + 2))) return rc;
+    if ((rc = h->tile_pf.ensure(2 * ((size_t)ntiles + 2)))) return rc;  // first + last protein of every tile
     STAGE(h, "tile_proteins", by(0, 0, 0, 4, 0),
           launch_tile_proteins(h->d_poff, (uint32_t)h->n_prot, (uint32_t)h->n_res, h->tile_pf.p, h->ctr.p,
                                h->stream));

@@ -1,0 +1,16 @@
+#!/bin/bash
+# tools/ab_variants.sh TAG variant... — bench experiment builds of the library
+# (dbindex_amd/exp/<variant>.so via DBI_LIB_PATH; "base" = the in-tree build)
+set -u -o pipefail
+TAG=$1; shift
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"; cd "$ROOT"
+for v in "$@"; do
+    if [ "$v" = base ]; then unset DBI_LIB_PATH; else export DBI_LIB_PATH=dbindex_amd/exp/$v.so; fi
+    timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --queries 0 > "$OUT/$v.json" 2> "$OUT/$v.err" \
+        || { echo "$v failed"; tail -5 "$OUT/$v.err"; exit 1; }
+    python3 -c "
+import json; d=json.loads(open('$OUT/$v.json').read().strip().splitlines()[-1])
+print('$v', round(d['ms_per_step'],3), [(k['kernel'], round(k['ms_per_build'],3)) for k in d['kernels']][:6])"
+done
