@@ -117,11 +117,12 @@ constexpr uint32_t PST_CAP = 512;  // protein starts of a tile kept in LDS (else
 
 struct DigestSmem {
     double mass[256];
+    uint64_t nokm[WIN / 64 + 2];  // bit p = N_ok at window position p (protein start, or a cut at p-1)
     uint32_t pst[PST_CAP];      // poff[pf .. pl+1] (protein of a start: binary search)
-    uint16_t win[WIN + 2];      // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST);
-                                // +2: walk_bounded reads one entry ahead without a clamp
+    alignas(16) uint16_t win[WIN + 8];  // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST);
+                                // slack: walk_bounded reads one entry ahead without a clamp
+    alignas(4) uint8_t pbit[WIN + 4];  // 1 = a protein starts at this window position (incl. one past the window)
     uint8_t flags[256];
-    uint8_t pbit[WIN + 1];      // 1 = a protein starts at this window position (incl. one past the window)
     uint16_t cand[DIGEST_TILE]; // compacted candidate starts (tile-local), in order
     uint32_t tmp[DIGEST_THREADS / 64 + 1];
 };
@@ -358,19 +359,29 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
     tc.pl = d_tile_pf[ntiles + 1 + tile];  // proteins overlapping [t0, w_end]: [pf, pl]
     sm.mass[tid] = d_mass_tab[tid];
     sm.flags[tid] = d_flags[tid];
-    for (uint32_t i = tid; i <= (uint32_t)WIN; i += DIGEST_THREADS) sm.pbit[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)(WIN + 4) / 4; i += DIGEST_THREADS) reinterpret_cast<uint32_t*>(sm.pbit)[i] = 0;
     const uint32_t np_all = tc.pl - tc.pf + 2;
     __syncthreads();
-    // residue window -> LDS as (residue | flags << 8)
+    // residue window -> LDS as (residue | flags << 8): a vector's 16 entries
+    // leave as two 16-B LDS stores when the window is 8-entry aligned
 #pragma unroll
     for (uint32_t k = 0; k < NV; ++k) {
         const uint32_t i = tid + k * DIGEST_THREADS;
         if (i < nvec) {
             const uint32_t wv[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+            uint32_t e[16];
 #pragma unroll
             for (int b = 0; b < 16; ++b) {
                 const uint32_t c = (wv[b >> 2] >> (8 * (b & 3))) & 0xFFu;
-                sm.win[hb + i * 16 + b] = (uint16_t)(c | ((uint32_t)sm.flags[c] << 8));
+                e[b] = c | ((uint32_t)sm.flags[c] << 8);
+            }
+            if ((hb & 7u) == 0) {
+                uint4* dst = reinterpret_cast<uint4*>(&sm.win[hb + i * 16]);
+                dst[0] = make_uint4(e[0] | e[1] << 16, e[2] | e[3] << 16, e[4] | e[5] << 16, e[6] | e[7] << 16);
+                dst[1] = make_uint4(e[8] | e[9] << 16, e[10] | e[11] << 16, e[12] | e[13] << 16, e[14] | e[15] << 16);
+            } else {
+#pragma unroll
+                for (int b = 0; b < 16; ++b) sm.win[hb + i * 16 + b] = (uint16_t)e[b];
             }
         }
     }
@@ -382,23 +393,35 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
         if (i < PST_CAP) sm.pst[i] = o;
     }
     __syncthreads();
-    // cleavage-cut and protein-end flags of every window position.  At the
-    // window's last position (w_end < R) the next residue is unknown; a walk
-    // that reaches it without a protein end overflows to walk_global first.
+    // cleavage-cut and protein-end flags of every window position, and the
+    // N_ok bit map (a protein start, or a cut just before: the candidate
+    // starts of a full enzyme).  At the window's last position (w_end < R) the
+    // next residue is unknown; a walk that reaches it without a protein end
+    // overflows to walk_global first.
     {
         constexpr uint32_t K = (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS;
+        static_assert(DIGEST_THREADS % 64 == 0, "ballot words");
         uint32_t cf[K];
 #pragma unroll
         for (uint32_t k = 0; k < K; ++k) {
             const uint32_t i = tid + k * DIGEST_THREADS;
             cf[k] = 0;
+            bool nok = false;
             if (i < nbytes) {
-                const uint32_t fl = sm.win[i] >> 8;
-                const uint32_t last = sm.pbit[i + 1];
-                const bool nocut_next = i + 1 < nbytes && ((sm.win[i + 1] >> 8) & F_NOCUT);
-                const bool cut = last || ((fl & F_CLEAVE) && !nocut_next);
+                const uint32_t e = sm.win[i];
+                const uint32_t en = sm.win[i + 1];
+                const uint32_t ep = i > 0 ? (uint32_t)sm.win[i - 1] : 0u;
+                const bool first = sm.pbit[i] != 0;
+                const bool last = sm.pbit[i + 1] != 0;
+                const bool nocut_next = i + 1 < nbytes && ((en >> 8) & F_NOCUT);
+                const bool cut = last || (((e >> 8) & F_CLEAVE) && !nocut_next);
                 cf[k] = (cut ? F_CUT : 0u) | (last ? F_LAST : 0u);
+                // cut at i-1 (its protein-end case is `first`)
+                const bool cut_prev = i > 0 && ((ep >> 8) & F_CLEAVE) && !((e >> 8) & F_NOCUT);
+                nok = first || cut_prev;
             }
+            const uint64_t m = __ballot(nok);
+            if (lane_id() == 0 && i < nbytes) sm.nokm[i / 64] = m;  // lane 0: the word's first position
         }
         __syncthreads();
 #pragma unroll
@@ -409,13 +432,14 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
     }
     __syncthreads();
     // cleavage-site compaction: thread t owns starts [t*SPT, t*SPT+SPT) in order
-    uint32_t mybits = 0, mycnt = 0;
-#pragma unroll
-    for (int k = 0; k < STARTS_PER_THREAD; ++k) {
-        const uint32_t i = tid * STARTS_PER_THREAD + k;
-        const bool ok = (tc.t0 + i < tc.t_end) && (SEMI || n_ok_at(sm, tc, i));
-        if (ok) { mybits |= 1u << k; ++mycnt; }
-    }
+    static_assert(STARTS_PER_THREAD == 16 && WIN_PRE % 16 == 0, "16-bit slices of the N_ok map");
+    const uint32_t off = tc.t0 - w0;  // window position of start 0 (0 or WIN_PRE)
+    const uint32_t p0 = off + tid * STARTS_PER_THREAD;
+    const uint32_t n_here = tc.t0 + tid * STARTS_PER_THREAD < tc.t_end
+                                ? min((uint32_t)STARTS_PER_THREAD, tc.t_end - tc.t0 - tid * STARTS_PER_THREAD) : 0u;
+    const uint32_t valid = n_here >= 16 ? 0xFFFFu : ((1u << n_here) - 1u);
+    uint32_t mybits = SEMI ? valid : ((uint32_t)(sm.nokm[p0 / 64] >> (p0 % 64)) & valid);
+    uint32_t mycnt = (uint32_t)__popc(mybits);
     uint32_t ncand;
     uint32_t pos = block_excl_scan<DIGEST_THREADS, uint32_t>(mycnt, sm.tmp, ncand);
 #pragma unroll
