@@ -42,7 +42,23 @@ STAGES = [
 ]
 
 
+# substrings checked first (template arguments tell the stages apart)
+CONTAINS = [
+    ("OwnerDigit", "owner_partition"),
+    ("PairDigit", "query_route"),
+    ("k_giant_", "chunk_sort_giant"),
+    ("k_digest_bounded", "digest"),
+    ("k_synth_", "synth"),
+    ("k_qroute", "query_route"),
+    ("k_query_pairs", "query"),
+    ("k_qcombine", "query"),
+]
+
+
 def stage_of(name: str) -> str:
+    for sub, st in CONTAINS:
+        if sub in name:
+            return st
     for pre, st in STAGES:
         if name.startswith(pre):
             return st
