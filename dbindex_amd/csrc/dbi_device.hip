@@ -118,6 +118,9 @@ constexpr uint32_t PST_CAP = 512;  // protein starts of a tile kept in LDS (else
 struct DigestSmem {
     double mass[256];
     uint64_t nokm[WIN / 64 + 2];  // bit p = N_ok at window position p (protein start, or a cut at p-1)
+    uint64_t cutm[WIN / 64 + 2];  // bit p = F_CUT at p            (bounded digest: slot bounds)
+    uint64_t clvm[WIN / 64 + 2];  // bit p = cleave residue at p
+    uint64_t stm[WIN / 64 + 2];   // bit p = a protein starts at p
     uint32_t pst[PST_CAP];      // poff[pf .. pl+1] (protein of a start: binary search)
     alignas(16) uint16_t win[WIN + 8];  // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST);
                                 // slack: walk_bounded reads one entry ahead without a clamp
@@ -406,12 +409,13 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
         for (uint32_t k = 0; k < K; ++k) {
             const uint32_t i = tid + k * DIGEST_THREADS;
             cf[k] = 0;
-            bool nok = false;
+            bool nok = false, clv = false, first = false;
             if (i < nbytes) {
                 const uint32_t e = sm.win[i];
                 const uint32_t en = sm.win[i + 1];
                 const uint32_t ep = i > 0 ? (uint32_t)sm.win[i - 1] : 0u;
-                const bool first = sm.pbit[i] != 0;
+                first = sm.pbit[i] != 0;
+                clv = ((e >> 8) & F_CLEAVE) != 0;
                 const bool last = sm.pbit[i + 1] != 0;
                 const bool nocut_next = i + 1 < nbytes && ((en >> 8) & F_NOCUT);
                 const bool cut = last || (((e >> 8) & F_CLEAVE) && !nocut_next);
@@ -421,7 +425,15 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
                 nok = first || cut_prev;
             }
             const uint64_t m = __ballot(nok);
-            if (lane_id() == 0 && i < nbytes) sm.nokm[i / 64] = m;  // lane 0: the word's first position
+            const uint64_t mc = __ballot((cf[k] & F_CUT) != 0);
+            const uint64_t ml = __ballot(clv);
+            const uint64_t ms = __ballot(first);
+            if (lane_id() == 0 && i < nbytes) {  // lane 0: the word's first position
+                sm.nokm[i / 64] = m;
+                sm.cutm[i / 64] = mc;
+                sm.clvm[i / 64] = ml;
+                sm.stm[i / 64] = ms;
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -946,8 +958,39 @@ __device__ __forceinline__ WalkOut walk_candidate_bounded(const DevParams& dp, c
     return w;
 }
 
-// One walk per start (see launch_digest_bounded): reservation look-back right
-// after compaction, then emit into the thread's own slots.  (A persistent grid
+// Records a full-enzyme start at window position p can emit, at most: the
+// cuts at [p + min_len - 1, stop), stop = the kcl-th (max_missed + 2) cleave
+// residue at or after p (from there on every cut breaks, :322-329) or the next
+// protein start, whichever comes first; `cap` when neither lies within the 64
+// positions from p (or the window ends first: the walk may leave it).  Mass
+// filters only lower the real count.  Branch-free over 64-position slices.
+__device__ __forceinline__ uint64_t bits_from(const uint64_t* m, uint32_t p) {
+    const uint32_t w = p >> 6, b = p & 63;
+    return b ? (m[w] >> b) | (m[w + 1] << (64 - b)) : m[w];
+}
+
+__device__ __forceinline__ uint32_t slot_bound(const DigestSmem& sm, uint32_t p, uint32_t nbytes, uint32_t kcl,
+                                               uint32_t min_len, uint32_t cap) {
+    uint64_t cl = bits_from(sm.clvm, p);               // bit r: cleave residue at p + r
+    const uint64_t st = bits_from(sm.stm, p) & ~1ull;  // protein starts after p
+    const uint64_t cu = bits_from(sm.cutm, p);
+    for (uint32_t q = 1; q < kcl; ++q) cl &= cl - 1;   // drop the first kcl-1 cleave residues
+    const uint32_t r_cl = cl ? (uint32_t)__ffsll((long long)cl) - 1 : 64u;
+    const uint32_t r_st = st ? (uint32_t)__ffsll((long long)st) - 1 : 64u;
+    const uint32_t r = min(r_cl, r_st);                // stop - p
+    if (r >= 64 || p + r >= nbytes) return cap;        // bits at or past nbytes are not this window's
+    const uint32_t a = min_len - 1;
+    if (a >= r) return 0;
+    const uint64_t keep = (~0ull << a) & ((1ull << r) - 1);  // r < 64
+    return min((uint32_t)__popcll(cu & keep), cap);
+}
+
+// One walk per start (see launch_digest_bounded): each thread's candidates
+// reserve their slot bounds (slot_bound), the tile's total by decoupled
+// look-back, then every walk emits into the thread's own slots and the rest
+// are sentinel-filled (~3 % of the slots at SwissProt scale; a flat
+// max_missed + 2 per start left 41 %).  (Bounds computed during the
+// compaction instead, so the look-back could start earlier: slower.)  (A persistent grid
 // taking tiles from the ticket measured slower: 2.25 vs 1.60 ms.)
 template <bool DROP>
 __global__ void __launch_bounds__(DIGEST_THREADS)
@@ -965,29 +1008,34 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     const uint32_t ncand = digest_prepare<false>(sm, tc, tile, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot,
                                                  n_res, d_tile_pf);
     const uint32_t B = (uint32_t)dp.max_missed + 2u;  // records per start, at most
-    if (threadIdx.x < 64) {
-        const unsigned long long excl = tile_lookback(status, tile, epoch, (unsigned long long)ncand * B);
-        if (threadIdx.x == 0) {
-            if (tile == gridDim.x - 1) d_ctr->n_slots = excl + (unsigned long long)ncand * B;
-            s_base = excl;
-        }
-    }
-    __syncthreads();
-    const unsigned long long base = s_base;
-    if (base + (unsigned long long)ncand * B > cap) return;  // too small: the caller grows it and runs again
     tc.w = rec_width(d_ctr->max_plen);
     if (tile == 0 && threadIdx.x == 0 && !rec_layout_ok(tc.w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
     balance_candidates(sm, ncand, B, tc.t_end - tc.t0);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
-    Rec* __restrict__ o = d_out + base + (unsigned long long)jb * B;
-    const uint32_t lim = (je - jb) * B;
+    uint32_t lim = 0;
+    for (uint32_t j = jb; j < je; ++j)
+        lim += slot_bound(sm, tc.t0 - tc.w0 + sm.cand[j], tc.nbytes, B, (uint32_t)dp.min_len, B);
+    uint32_t tile_slots;
+    const uint32_t excl_t = block_excl_scan<DIGEST_THREADS, uint32_t>(lim, sm.tmp, tile_slots);
+    if (threadIdx.x < 64) {
+        const unsigned long long excl = tile_lookback(status, tile, epoch, (unsigned long long)tile_slots);
+        if (threadIdx.x == 0) {
+            if (tile == gridDim.x - 1) d_ctr->n_slots = excl + tile_slots;
+            s_base = excl;
+        }
+    }
+    __syncthreads();
+    const unsigned long long base = s_base;
+    if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
+    Rec* __restrict__ o = d_out + base + excl_t;
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
         const WalkOut w = walk_candidate_bounded<DROP>(dp, sm, tc, d_res, d_poff, j, o + kept, o + lim);
         kept += w.kept;
         dropped += w.dropped;
     }
+    if (kept > lim) atomicOr(&d_ctr->err, ERR_SLOTS);  // slot_bound is an upper bound: never
     const Rec sent{REC_SENTINEL, REC_SENTINEL};
     for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
     const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);

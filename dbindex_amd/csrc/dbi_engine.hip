@@ -189,6 +189,7 @@ int finish_build(dbi_handle* h) {
     int rc = read_counters(h);
     if (rc) return rc;
     if (h->hc.err & ERR_SEGS) return set_error(DBI_E_STATE, "internal: giant-chunk segment list overflow");
+    if (h->hc.err & ERR_SLOTS) return set_error(DBI_E_STATE, "internal: digest slot bound exceeded");
     if (h->hc.err & ERR_LAYOUT)
         return set_error(DBI_E_INVALID, "2 x bits(longest protein) + bits(protein count) exceeds the 56 bits of the "
                                         "16-B occurrence record: shard the FASTA");

@@ -123,6 +123,7 @@ struct Counters {
 };
 constexpr unsigned ERR_LAYOUT = 1;  // 2*bits(longest protein) + bits(proteins) > 56
 constexpr unsigned ERR_SEGS = 2;    // giant split: a segment list overflowed (internal)
+constexpr unsigned ERR_SLOTS = 4;   // bounded digest: a thread emitted more records than it reserved (internal)
 
 // Tunables
 constexpr int DIGEST_THREADS = 256;
