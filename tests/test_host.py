@@ -169,3 +169,19 @@ def test_slice_and_from_sequences():
     assert s.sequences() == pp.sequences()[10:20]
     t = fasta.PackedProteins.from_sequences(s.sequences())
     assert np.array_equal(t.residues, s.residues) and np.array_equal(t.offsets, s.offsets)
+
+
+def test_synth_proteome_twin_is_range_consistent():
+    """The counter-based proteome (numpy twin of dbi_synth_proteome): any
+    protein range is the matching slice of the whole, so ranks can generate
+    their own ranges with no data movement."""
+    t = fasta.synth_tables()
+    assert t[0].shape == (4096,) and t[1].shape == (65536,)
+    assert set(np.unique(t[1]).tobytes().decode()) == set(fasta.CANONICAL)
+    whole = fasta.synth_proteome(11, 0, 700, 0, t)
+    for a, n in ((0, 1), (123, 300), (699, 1)):
+        base = fasta.synth_residue_base(11, a, t[0])
+        assert base == int(whole.offsets[a])
+        part = fasta.synth_proteome(11, a, n, base, t)
+        assert np.array_equal(part.residues, whole.residues[int(whole.offsets[a]):int(whole.offsets[a + n])])
+        assert np.array_equal(part.offsets, whole.offsets[a:a + n + 1] - whole.offsets[a])
