@@ -127,7 +127,8 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
 
     // every allocation before the first launch of this stage: a reallocation
     // must never free a buffer that queued kernels still use
-    const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + CHUNK_T - 1) / CHUNK_T, 1);
+    const uint32_t T = h->chunk_t;
+    const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + T - 1) / T, 1);
     const size_t seg_cap = giant_seg_cap(n);
     const size_t scan_need = std::max(scan_u32_tmp_elems(hist_elems), scan_u32_tmp_elems(nchunks));
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_need, h->scan_tmp.cap)))) return rc;
@@ -163,7 +164,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     // src: records grouped by bin, insertion order inside each bin
     // chunk sort: 16 B in + 16 B out per record (+ the residues of every peptide for its hash)
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
-          launch_chunk_bounds(src, n32, bm, CHUNK_T, nchunks, h->chunk_lo.p, s));
+          launch_chunk_bounds(src, n32, bm, T, nchunks, h->chunk_lo.p, s));
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                             h->ctr.p, s));
@@ -459,6 +460,7 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     // tuning knobs (defaults are the measured best; environment overrides for experiments)
     if (const char* ev = std::getenv("DBI_BIN_BITS_MAX")) h->bin_bits_max = std::max(1, std::min(32, std::atoi(ev)));
     if (const char* ev = std::getenv("DBI_SPLIT_ABOVE")) h->split_above = (uint32_t)std::max(1, std::atoi(ev));
+    if (const char* ev = std::getenv("DBI_CHUNK_T")) h->chunk_t = (uint32_t)std::max(64, std::min(CHUNK_CAP, std::atoi(ev)));
     auto fail = [&](int code) {
         dbi_close(h);
         return code;

@@ -18,6 +18,6 @@ k={x['kernel']:round(x['ms_per_build'],2) for x in d['kernels']}
 print('$name', round(d['ms_per_step'],3), k)"
 }
 for spec in "$@"; do
-    IFS=: read -r name cfg bits split <<< "$spec"
-    run "$name" "$cfg" DBI_BIN_BITS_MAX=$bits DBI_SPLIT_ABOVE=$split
+    IFS=: read -r name cfg bits split ct <<< "$spec"
+    run "$name" "$cfg" DBI_BIN_BITS_MAX=$bits DBI_SPLIT_ABOVE=$split DBI_CHUNK_T=${ct:-1024}
 done
