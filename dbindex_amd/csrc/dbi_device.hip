@@ -1262,14 +1262,12 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
         const uint32_t i = base + k * 64 + lane;
         qv[k] = i < n ? in[i].q0 : REC_SENTINEL;
     }
+    // counts only (no ranks): one LDS atomic per record into the wave's own row
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
         const bool valid = i < n && (!SPARSE || qv[k] != REC_SENTINEL);
-        const uint32_t d = dig(qv[k]);
-        const uint64_t peers = digit_peers(d, valid, bits);
-        if (valid && __popcll(peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
-        wave_sync();
+        if (valid) atomicAdd(&cnt[w][dig(qv[k])], 1u);
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) {

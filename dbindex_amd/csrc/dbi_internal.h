@@ -134,7 +134,7 @@ constexpr int RADIX_THREADS = 512;
 constexpr int RADIX_ITEMS = 8;      // records per thread per radix block (4096: 64 KiB LDS exchange)
 constexpr int CHUNK_THREADS = 512;
 constexpr int CHUNK_CAP = 1984;     // records per chunk sorted in LDS (20 B each: 4 blocks per CU)
-constexpr int CHUNK_T = 1024;       // target chunk size (whole mass bins, ~T..T+maxbin)
+constexpr int CHUNK_T = 1280;       // target chunk size (whole mass bins, ~T..T+maxbin; tools/ab_knobs.sh: 768-1536 measured)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
 constexpr int BIG_THREADS = 1024;
 constexpr int BIG_CAP = 7936;       // records per oversize chunk sorted in LDS (1 block per CU)
