@@ -6,11 +6,14 @@ TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"; cd "$ROOT"
-for v in "$@"; do
+for spec in "$@"; do
+    IFS=: read -r v ct <<< "$spec"   # variant[:chunk target]
+    if [ -n "${ct:-}" ]; then export DBI_CHUNK_T=$ct; else unset DBI_CHUNK_T; fi
     if [ "$v" = base ]; then unset DBI_LIB_PATH; else export DBI_LIB_PATH=dbindex_amd/exp/$v.so; fi
-    timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --queries 0 > "$OUT/$v.json" 2> "$OUT/$v.err" \
-        || { echo "$v failed"; tail -5 "$OUT/$v.err"; exit 1; }
+    name=$v${ct:+_$ct}
+    timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --queries 0 > "$OUT/$name.json" 2> "$OUT/$name.err" \
+        || { echo "$name failed"; tail -5 "$OUT/$name.err"; exit 1; }
     python3 -c "
-import json; d=json.loads(open('$OUT/$v.json').read().strip().splitlines()[-1])
-print('$v', round(d['ms_per_step'],3), [(k['kernel'], round(k['ms_per_build'],3)) for k in d['kernels']][:6])"
+import json; d=json.loads(open('$OUT/$name.json').read().strip().splitlines()[-1])
+print('$name', round(d['ms_per_step'],3), [(k['kernel'], round(k['ms_per_build'],3)) for k in d['kernels']][:6])"
 done
