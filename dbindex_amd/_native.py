@@ -53,6 +53,12 @@ SHARD_SAMPLES = 4096  # DBI_SHARD_SAMPLES
 MAX_SHARDS = 64       # DBI_MAX_SHARDS
 
 
+class DbiFasta(ctypes.Structure):
+    _fields_ = [("n_proteins", c_uint64), ("n_residues", c_uint64), ("residues", c_void_p),
+                ("offsets", POINTER(c_uint64)), ("defs", c_void_p), ("def_off", POINTER(c_uint64)),
+                ("n_uniprot", c_uint64)]
+
+
 class DbiQueryResult(ctypes.Structure):
     _fields_ = [("nq", c_uint64), ("n_hits", c_uint64), ("row_ptr", POINTER(c_uint64)),
                 ("ids", POINTER(c_uint64))]
@@ -131,6 +137,9 @@ SIGNATURES = [
     ("dbi_store_protein_count", c_int, [P, POINTER(c_uint64)]),
     ("dbi_store_protein_def", c_int, [P, c_uint64, POINTER(c_char_p), POINTER(c_uint64)]),
     ("dbi_store_protein_sequence", c_int, [P, c_uint64, POINTER(c_void_p), POINTER(c_uint64)]),
+    ("dbi_fasta_parse", c_int, [P, c_uint64, c_int, POINTER(POINTER(DbiFasta))]),
+    ("dbi_fasta_read", c_int, [c_char_p, c_int, POINTER(POINTER(DbiFasta))]),
+    ("dbi_fasta_free", None, [POINTER(DbiFasta)]),
     ("dbi_dev_alloc", c_int, [c_int, c_uint64, POINTER(c_void_p)]),
     ("dbi_dev_free", c_int, [c_int, P]),
     ("dbi_dev_copy_h2d", c_int, [c_int, P, P, c_uint64]),

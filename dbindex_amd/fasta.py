@@ -215,13 +215,46 @@ def iter_fasta(lines: Iterable[str]) -> Iterator[Tuple[str, str]]:
         yield d, "".join(parts)
 
 
-def read_fasta(path: str) -> PackedProteins:
-    defs, seqs = [], []
-    with open(path, "r") as fh:
-        for d, s in iter_fasta(fh):
-            defs.append(d)
-            seqs.append(s)
-    return PackedProteins.from_sequences(seqs, defs)
+def read_fasta(path: str, threads: int = 0, with_defs: bool = True) -> PackedProteins:
+    """Packs a FASTA file with the library's multi-threaded parser
+    (dbi_fasta_read; same semantics as iter_fasta)."""
+    return _from_native(lambda out: _native_lib().dbi_fasta_read(path.encode(), threads, out), with_defs)
+
+
+def parse_fasta(text, threads: int = 0, with_defs: bool = True) -> PackedProteins:
+    """Packs FASTA text (str or bytes) with dbi_fasta_parse."""
+    import ctypes
+    b = text.encode() if isinstance(text, str) else bytes(text)
+    buf = ctypes.create_string_buffer(b, len(b))
+    return _from_native(lambda out: _native_lib().dbi_fasta_parse(buf, len(b), threads, out), with_defs)
+
+
+def _native_lib():
+    from . import _native
+    return _native.lib()
+
+
+def _from_native(call, with_defs: bool) -> PackedProteins:
+    import ctypes
+    from . import _native
+    out = ctypes.POINTER(_native.DbiFasta)()
+    _native.check(call(ctypes.byref(out)))
+    try:
+        f = out.contents
+        P, R = f.n_proteins, f.n_residues
+        res = np.ctypeslib.as_array((ctypes.c_uint8 * max(R, 1)).from_address(f.residues))[:R].copy() if R else \
+            np.zeros(0, np.uint8)
+        offs = np.ctypeslib.as_array(f.offsets, shape=(P + 1,)).astype(np.uint64)
+        defs: List[str] = []
+        if with_defs and P:
+            doff = np.ctypeslib.as_array(f.def_off, shape=(P + 1,))
+            raw = ctypes.string_at(f.defs, int(doff[-1])).decode("latin-1")
+            defs = [raw[int(doff[i]):int(doff[i + 1])] for i in range(P)]
+        pp = PackedProteins(res, offs, defs)
+        pp.n_uniprot = int(f.n_uniprot)
+        return pp
+    finally:
+        _native.lib().dbi_fasta_free(out)
 
 
 def uniprot_accession(definition: str) -> Optional[str]:

@@ -384,6 +384,29 @@ int dbi_store_protein_def(dbi_store* s, uint64_t id, const char** def, uint64_t*
 int dbi_store_protein_sequence(dbi_store* s, uint64_t id, const char** seq, uint64_t* len);
 
 /* ------------------------------------------------------------------------ */
+/* FASTA parsing (host, multi-threaded): the packed layout the builds read   */
+/* ------------------------------------------------------------------------ */
+/* Records start at a '>' at a line start (DBIndexer.run / FastaReader,
+ * DBIndexer.java:546-616); definition = the rest of that line without
+ * trailing CR/LF; sequence = the following lines with ASCII whitespace
+ * removed; text before the first record is ignored.  Protein id = position
+ * (ProteinCache.addProtein, ProteinCache.java:84-95). */
+typedef struct dbi_fasta {
+    uint64_t n_proteins;
+    uint64_t n_residues;
+    uint8_t* residues;  /* n_residues (+16 zero bytes of padding)              */
+    uint64_t* offsets;  /* n_proteins + 1                                      */
+    char* defs;         /* definitions, concatenated                           */
+    uint64_t* def_off;  /* n_proteins + 1: definition i = defs[def_off[i]..)  */
+    uint64_t n_uniprot; /* definitions with a UniProt accession (sp|ACC|/tr|ACC|):
+                           DBIndexer.run rejects a FASTA with none (:560-565) */
+} dbi_fasta;
+/* threads <= 0: one per hardware thread.  Free with dbi_fasta_free. */
+int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out);
+int dbi_fasta_read(const char* path, int threads, dbi_fasta** out);
+void dbi_fasta_free(dbi_fasta* f);
+
+/* ------------------------------------------------------------------------ */
 /* Device memory helpers (so host code needs no other HIP runtime binding)  */
 /* ------------------------------------------------------------------------ */
 int dbi_dev_alloc(int device, uint64_t bytes, void** out);

@@ -6,6 +6,7 @@ FASTA generator / reader.  Nothing here launches a kernel.
 from __future__ import annotations
 
 import ctypes
+import io
 import os
 import re
 
@@ -185,3 +186,41 @@ def test_synth_proteome_twin_is_range_consistent():
         part = fasta.synth_proteome(11, a, n, base, t)
         assert np.array_equal(part.residues, whole.residues[int(whole.offsets[a]):int(whole.offsets[a + n])])
         assert np.array_equal(part.offsets, whole.offsets[a:a + n + 1] - whole.offsets[a])
+
+
+FASTA_EDGE_CASES = [
+    "",
+    "no header at all\nACDE\n",
+    ">only\n",
+    ">a\nACD\nEFG\n>b\n\n>c\nKKK",                     # empty sequence, no final newline
+    "junk before\n>x y z\r\nAC DE\r\n\tFG\r\n>y\r\n",      # CRLF, inner whitespace, text before the first record
+    ">p1\nAAA>BBB\n>p2 desc > with >\nCC\n",              # '>' inside a line is a residue / part of the definition
+    ">\nMK\n>>double\nRR\n",                               # empty definition, definition starting with '>'
+]
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_native_fasta_parser_matches_iter_fasta(threads):
+    texts = list(FASTA_EDGE_CASES)
+    buf = io.StringIO()
+    fasta.write_fasta(fasta.config("1k"), buf, width=37)
+    texts.append(buf.getvalue())
+    for t in texts:
+        want = list(fasta.iter_fasta(io.StringIO(t)))
+        got = fasta.parse_fasta(t, threads=threads)
+        assert got.n_proteins == len(want), (t[:40], got.n_proteins, len(want))
+        assert got.defs == [d for d, _ in want]
+        assert got.sequences() == [s for _, s in want]
+        assert got.n_uniprot == sum(fasta.uniprot_accession(d) is not None for d, _ in want)
+
+
+def test_native_fasta_read_file(tmp_path):
+    pp = fasta.config("1k")
+    path = tmp_path / "p.fasta"
+    with open(path, "w") as fh:
+        fasta.write_fasta(pp, fh)
+    back = fasta.read_fasta(str(path), threads=4)
+    assert np.array_equal(back.residues, pp.residues) and np.array_equal(back.offsets, pp.offsets)
+    assert back.defs == pp.defs and back.n_uniprot == pp.n_proteins
+    with pytest.raises(_native.DBIndexStoreException):
+        fasta.read_fasta(str(tmp_path / "missing.fasta"))
