@@ -137,6 +137,10 @@ SIGNATURES = [
     ("dbi_store_protein_count", c_int, [P, POINTER(c_uint64)]),
     ("dbi_store_protein_def", c_int, [P, c_uint64, POINTER(c_char_p), POINTER(c_uint64)]),
     ("dbi_store_protein_sequence", c_int, [P, c_uint64, POINTER(c_void_p), POINTER(c_uint64)]),
+    ("dbi_index_save", c_int, [P, c_char_p]),
+    ("dbi_index_load", c_int, [P, c_char_p]),
+    ("dbi_index_file_matches", c_int, [POINTER(DbiParams), c_char_p, POINTER(c_int)]),
+    ("dbi_store_set_persist", c_int, [P, c_int]),
     ("dbi_fasta_parse", c_int, [P, c_uint64, c_int, POINTER(POINTER(DbiFasta))]),
     ("dbi_fasta_read", c_int, [c_char_p, c_int, POINTER(POINTER(DbiFasta))]),
     ("dbi_fasta_free", None, [POINTER(DbiFasta)]),

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libdbindex_hip.so")
-SOURCES = ["dbi_device.hip", "dbi_engine.hip", "dbi_shard.hip", "dbi_stream.hip", "dbi_store.cpp", "dbi_fasta.cpp"]
+SOURCES = ["dbi_device.hip", "dbi_engine.hip", "dbi_shard.hip", "dbi_stream.hip", "dbi_persist.hip", "dbi_store.cpp", "dbi_fasta.cpp"]
 ARCH = os.environ.get("DBI_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
          "-Wno-unused-result", "-Wshadow", f"--offload-arch={ARCH}"]

@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/dbindex_hip.h"
 
@@ -297,6 +298,12 @@ struct LaunchEvents {
     hipEvent_t stop = nullptr;
 };
 extern thread_local LaunchEvents t_launch_ev;
+
+// ---- persistence (dbi_persist.hip) ---------------------------------------------------
+int index_save(dbi_handle* h, const char* path, const std::string* defs, const std::vector<uint64_t>* def_off);
+int index_load(dbi_handle* h, const char* path, std::vector<uint8_t>* res_out, std::vector<uint64_t>* off_out,
+               std::string* defs_out, std::vector<uint64_t>* def_off_out);
+int index_file_matches(const dbi_params& p, const char* path, bool* out);
 
 // ---- error plumbing (dbi_engine.hip) ------------------------------------------------
 int set_error(int code, const std::string& msg);

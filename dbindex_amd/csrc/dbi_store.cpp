@@ -35,7 +35,7 @@ struct dbi_store {
     dbi_params p;
     int device = 0;
     dbi_handle* eng = nullptr;
-    bool inited = false, in_tx = false, device_digest = false;
+    bool inited = false, in_tx = false, device_digest = false, persist = false;
     std::string db_id;
     // ProteinCache (ProteinCache.java:24-95): defs + sequences in id order
     std::vector<std::string> defs;
@@ -169,12 +169,37 @@ int dbi_store_set_device_digest(dbi_store* s, int on) {
     return 0;
 }
 
+int dbi_store_set_persist(dbi_store* s, int on) {
+    if (!s) return set_error(DBI_E_INVALID, "NULL store");
+    if (s->inited) return set_error(DBI_E_STATE, "set persistence before init()");
+    s->persist = on != 0;
+    return 0;
+}
+
 int dbi_store_init(dbi_store* s, const char* database_id) {
     if (!s) return set_error(DBI_E_INVALID, "NULL store");
     if (!database_id || !*database_id)
         return set_error(DBI_E_INVALID, "Index path is missing, cannot initialize the indexer.");
     if (s->inited) return set_error(DBI_E_STATE, "Already intialized");
     s->db_id = database_id;
+    if (s->persist) {
+        // an index of these parameters on disk: load it (DBIndexStoreSQLiteMult.init :92-149)
+        const std::string path = s->db_id + ".dbihip";
+        bool match = false;
+        int rc = index_file_matches(s->p, path.c_str(), &match);
+        if (rc) return rc;
+        if (match) {
+            if ((rc = ensure_engine(s))) return rc;
+            std::string defs;
+            std::vector<uint64_t> doff;
+            if ((rc = index_load(s->eng, path.c_str(), &s->residues, &s->off, &defs, &doff))) return rc;
+            s->defs.clear();
+            for (size_t i = 0; i + 1 < doff.size(); ++i) s->defs.emplace_back(defs, doff[i], doff[i + 1] - doff[i]);
+            dbi_stats st{};
+            dbi_stats_get(s->eng, &st);
+            s->total_seq_count = (int64_t)st.n_total;
+        }
+    }
     s->inited = true;
     return 0;
 }
@@ -202,6 +227,16 @@ int dbi_store_stop_add_seq(dbi_store* s) {
     }
     if (rc) return rc;
     s->in_tx = false;
+    if (s->persist) {  // commit to disk (DBIndexStoreSQLiteMult.stopAddSeq -> commitCachedData)
+        std::string defs;
+        std::vector<uint64_t> doff{0};
+        for (const auto& d : s->defs) {
+            defs += d;
+            doff.push_back(defs.size());
+        }
+        const std::string path = s->db_id + ".dbihip";
+        if ((rc = index_save(s->eng, path.c_str(), &defs, &doff))) return rc;
+    }
     return 0;
 }
 

@@ -113,6 +113,15 @@ class Engine:
                                       n_prot, ctypes.byref(t), ctypes.byref(d)))
         return t.value, d.value
 
+    def save(self, path: str) -> None:
+        """The built index + its proteome to one file (dbi_index_save)."""
+        check(_native.lib().dbi_index_save(self.h, path.encode()))
+
+    def load(self, path: str) -> BuildStats:
+        """Replace this engine's index by a saved one (same parameters only)."""
+        check(_native.lib().dbi_index_load(self.h, path.encode()))
+        return self.stats()
+
     def stats(self) -> BuildStats:
         st = DbiStats()
         check(_native.lib().dbi_stats_get(self.h, ctypes.byref(st)))

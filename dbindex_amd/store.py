@@ -129,7 +129,7 @@ def _seq_list(ptr) -> List[IndexedSequence]:
 class DBIndexStoreHip:
     """``implements DBIndexStore`` on the MI355X engine."""
 
-    def __init__(self, sparam, device: int = 0, device_digest: bool = False):
+    def __init__(self, sparam, device: int = 0, device_digest: bool = False, persist: bool = False):
         if isinstance(sparam, DBIndexSearchParams):
             self.sparam = sparam
             cp = sparam.to_c()
@@ -143,6 +143,8 @@ class DBIndexStoreHip:
         self.s = s
         if device_digest:
             self.setDeviceDigest(True)
+        if persist:  # <databaseID>.dbihip: loaded by init() when it matches, written by stopAddSeq()
+            check(_native.lib().dbi_store_set_persist(self.s, 1))
 
     def close(self) -> None:
         if getattr(self, "s", None):

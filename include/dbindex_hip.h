@@ -323,6 +323,18 @@ int dbi_count(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, const ui
               uint64_t n_prot, uint64_t* n_total, uint64_t* n_dropped);
 
 /* ------------------------------------------------------------------------ */
+/* Persisted index (the reference's SQLite index files + indexExists reuse)  */
+/* ------------------------------------------------------------------------ */
+/* One binary file: the proteome the index refers to + the unique table and
+ * occurrence CSR; the header fingerprints every build parameter (the role of
+ * the params md5 in the reference's file name, IndexUtil.java:270-324), and a
+ * file is only loaded under the same parameters. */
+int dbi_index_save(dbi_handle* h, const char* path);
+int dbi_index_load(dbi_handle* h, const char* path);  /* replaces the handle's index */
+/* *out = 1 when `path` holds an index built with exactly these parameters (host only) */
+int dbi_index_file_matches(const dbi_params* params, const char* path, int* out);
+
+/* ------------------------------------------------------------------------ */
 /* DBIndexStore mirror                                                      */
 /* ------------------------------------------------------------------------ */
 typedef struct dbi_store dbi_store;
@@ -337,6 +349,12 @@ void dbi_store_close(dbi_store* s);
  * out of every start (DBIndexer.java:351-354).  When off (default), the store
  * indexes exactly the occurrences passed to addSequence, like the reference. */
 int dbi_store_set_device_digest(dbi_store* s, int on);
+
+/* Persistence switch (default off): when on, init(database_id) loads
+ * `<database_id>.dbihip` if it holds an index built with the store's
+ * parameters (then indexExists() is true and DBIndexer.run skips indexing,
+ * DBIndexer.java:522-527), and stopAddSeq() writes it (index + ProteinCache). */
+int dbi_store_set_persist(dbi_store* s, int on);
 
 int dbi_store_init(dbi_store* s, const char* database_id);              /* init(String)      */
 int dbi_store_start_add_seq(dbi_store* s);                              /* startAddSeq()     */

@@ -224,3 +224,15 @@ def test_native_fasta_read_file(tmp_path):
     assert back.defs == pp.defs and back.n_uniprot == pp.n_proteins
     with pytest.raises(_native.DBIndexStoreException):
         fasta.read_fasta(str(tmp_path / "missing.fasta"))
+
+
+def test_index_file_matches_header(tmp_path):
+    """dbi_index_file_matches (host only): missing / foreign files never match."""
+    p = DBIndexSearchParams.trypsin(2).to_c()
+    v = ctypes.c_int(7)
+    _native.check(_native.lib().dbi_index_file_matches(ctypes.byref(p), str(tmp_path / "none").encode(), ctypes.byref(v)))
+    assert v.value == 0
+    junk = tmp_path / "junk.dbihip"
+    junk.write_bytes(b"NOTANIDX" + bytes(200))
+    _native.check(_native.lib().dbi_index_file_matches(ctypes.byref(p), str(junk).encode(), ctypes.byref(v)))
+    assert v.value == 0

@@ -1,0 +1,84 @@
+"""GPU: a built index on disk and back (dbi_index_save / dbi_index_load) and
+the DBIndexStore mirror's indexExists reuse contract (DBIndexer.java:522-527):
+the loaded index answers exactly like the oracle's."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from dbindex_amd import fasta
+from dbindex_amd.params import DBIndexSearchParams
+from oracle import cref
+from tests.helpers import assert_index_equal, assert_queries_equal, query_masses
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def Engine():
+    from dbindex_amd import _native
+    from dbindex_amd.engine import Engine
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    return Engine
+
+
+def test_engine_save_load_roundtrip(Engine, tmp_path):
+    from dbindex_amd import _native
+    pp = fasta.config("1k")
+    prm = DBIndexSearchParams.trypsin(2)
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    path = str(tmp_path / "idx.dbihip")
+    with Engine(cp) as a:
+        a.build(pp)
+        a.save(path)
+    with Engine(cp) as b:
+        st = b.load(path)
+        assert st.n_total == oix.n_total and st.n_unique == oix.n_unique
+        assert_index_equal(b, oix, "loaded")
+        m, t = query_masses(oix, 1500)
+        assert_queries_equal(b, oix, m, t, "loaded")
+        # a loaded index saves again byte for byte
+        b.save(str(tmp_path / "again.dbihip"))
+    assert open(path, "rb").read() == open(tmp_path / "again.dbihip", "rb").read()
+    # other parameters: the file is refused, loudly
+    with Engine(DBIndexSearchParams.trypsin(1).to_c()) as c:
+        with pytest.raises(_native.DBIndexStoreException):
+            c.load(path)
+
+
+def test_store_persist_and_reuse(tmp_path):
+    from dbindex_amd.indexer import DBIndexer
+    from dbindex_amd.store import DBIndexStoreHip
+    pp = fasta.config("1k").slice(0, 300)
+    prm = DBIndexSearchParams.trypsin(2)
+    name = str(tmp_path / "db.fasta")
+    oix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    m, t = query_masses(oix, 300)
+
+    def answers(ix):
+        out = []
+        for mm, tt in zip(m[:60], t[:60]):
+            out.append(sorted((s.getSequence(), tuple(sorted(p.getId() for p in ix.getProteins(s))))
+                              for s in ix.getSequencesUsingDaltonTolerance(float(mm), float(tt))))
+        return out
+
+    first = DBIndexer(prm, indexStore=DBIndexStoreHip(prm, persist=True), database_name=name)
+    first.init()
+    assert not first.indexStore.indexExists()
+    first.run(pp)
+    want = answers(first)
+    n_keys = first.getNumParentMasses()
+    # a new process-like store with the same parameters finds the file and skips indexing
+    second = DBIndexer(prm, indexStore=DBIndexStoreHip(prm, persist=True), database_name=name)
+    second.init()
+    assert second.indexStore.indexExists()
+    second.run(iter(()))  # would raise "no UniProt accession" if it indexed
+    assert answers(second) == want
+    assert second.getNumParentMasses() == n_keys
+    # other parameters: not reused
+    other = DBIndexer(DBIndexSearchParams.trypsin(1),
+                      indexStore=DBIndexStoreHip(DBIndexSearchParams.trypsin(1), persist=True), database_name=name)
+    other.init()
+    assert not other.indexStore.indexExists()
