@@ -99,6 +99,7 @@ SIGNATURES = [
     ("dbi_entry_keys", c_int, [P, P, c_uint64, POINTER(c_uint64)]),
     ("dbi_device_view", c_int, [P, POINTER(DbiDeviceIndex)]),
     ("dbi_set_timing", c_int, [P, c_int, c_char_p]),
+    ("dbi_set_bucket_drop", c_int, [P, c_int]),
     ("dbi_stage_times", c_int, [P, P, P, P, c_uint64, POINTER(c_uint64)]),
     ("dbi_shard_digest", c_int, [P, P, c_uint64, P, c_uint64, c_uint64, c_uint64, c_int, c_int]),
     ("dbi_shard_samples", c_int, [P, P]),
@@ -133,6 +134,7 @@ SIGNATURES = [
     ("dbi_store_engine", c_void_p, [P]),
     ("dbi_store_get_sequences", c_int, [P, c_double, c_double, POINTER(POINTER(DbiSeqList))]),
     ("dbi_store_get_sequences_ranges", c_int, [P, P, P, c_uint64, POINTER(POINTER(DbiSeqList))]),
+    ("dbi_store_cut_and_search", c_int, [P, P, P, c_uint64, POINTER(POINTER(DbiSeqList))]),
     ("dbi_seq_list_free", None, [POINTER(DbiSeqList)]),
     ("dbi_store_protein_count", c_int, [P, POINTER(c_uint64)]),
     ("dbi_store_protein_def", c_int, [P, c_uint64, POINTER(c_char_p), POINTER(c_uint64)]),
@@ -141,6 +143,7 @@ SIGNATURES = [
     ("dbi_index_load", c_int, [P, c_char_p]),
     ("dbi_index_file_matches", c_int, [POINTER(DbiParams), c_char_p, POINTER(c_int)]),
     ("dbi_store_set_persist", c_int, [P, c_int]),
+    ("dbi_store_set_unindexed", c_int, [P, c_int]),
     ("dbi_fasta_parse", c_int, [P, c_uint64, c_int, POINTER(POINTER(DbiFasta))]),
     ("dbi_fasta_read", c_int, [c_char_p, c_int, POINTER(POINTER(DbiFasta))]),
     ("dbi_fasta_free", None, [POINTER(DbiFasta)]),

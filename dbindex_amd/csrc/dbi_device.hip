@@ -2232,7 +2232,15 @@ __global__ void k_query(DevParams dp, int32_t factor, const double* __restrict__
     const double hi = precMass + tol;
     const int b0 = java_d2i(lo) / dp.br, b1 = java_d2i(hi) / dp.br;
     uint64_t f = 0, c = 0;
-    if (!(b0 > dp.nb - 1 || b1 > dp.nb - 1)) {
+    if (!dp.buckets) {
+        // MassRangeFilteringIndex.filterSequence (:90-108): minMass <= m <= maxMass,
+        // no buckets; a NaN bound includes nothing
+        if (lo == lo && hi == hi) {
+            const uint32_t a = lower_bound_d(umass, nu, lo);
+            const uint32_t e = upper_bound_d(umass, nu, hi);
+            if (e > a) { f = a; c = e - a; }
+        }
+    } else if (!(b0 > dp.nb - 1 || b1 > dp.nb - 1)) {
         if (lo != lo || hi != hi) {
             // NaN bounds: rows BETWEEN (int)NaN=0 AND 0, and no mass test rejects
             // (comparisons with NaN are false) -> every unique with key 0.

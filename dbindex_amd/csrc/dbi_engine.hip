@@ -81,6 +81,7 @@ DevParams make_dev_params(const dbi_params& p) {
     d.mand_filter = (p.mandatory_mode && p.mandatory_count > 0) ? 1 : 0;
     d.semi = p.semi ? 1 : 0;
     d.drop_mass = (double)(d.nb * d.br);
+    d.buckets = 1;
     double mmax = 0.0;
     for (int c = 0; c < 256; ++c) mmax = std::max(mmax, p.mass[c]);
     d.cut_count = (!p.semi && !p.mandatory_mode && mmax < 1024.0) ? 1 : 0;  // fixed-point prefix tables fit u32
@@ -755,6 +756,17 @@ int dbi_entry_keys(dbi_handle* h, int32_t* keys, uint64_t cap, uint64_t* n) {
     pos.release();
     dk.release();
     if (e != hipSuccess) return hip_fail(e, "dbi_entry_keys");
+    return 0;
+}
+
+int dbi_set_bucket_drop(dbi_handle* h, int on) {
+    if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    if (!on && !(h->params.max_mh < 65536.0))
+        return set_error(DBI_E_INVALID, "without buckets every peptide up to the max precursor mass is kept: "
+                                        "max precursor mass must be < 65536 Da");
+    h->dp.buckets = on ? 1 : 0;
+    h->dp.drop_mass = on ? (double)(h->dp.nb * h->dp.br) : INFINITY;
+    h->built = false;  // an index built under the other setting no longer answers
     return 0;
 }
 

@@ -99,6 +99,7 @@ struct DevParams {
     int32_t semi;
     double drop_mass;         // bucket > NUM_BUCKETS-1  <=>  (int)m >= nb*br  <=>  m >= nb*br
     int32_t cut_count;        // count by cut stepping (full enzyme, no mandatory AAs, residue masses < 1024 Da)
+    int32_t buckets;          // 1: bucketed store (drop + query bucket test); 0: MassRangeFilteringIndex (none)
 };
 
 constexpr int GIANT_PASSES = 3;  // MSD split passes over chunks above BIG_CAP (then the global-memory fallback)

@@ -36,6 +36,8 @@ struct dbi_store {
     int device = 0;
     dbi_handle* eng = nullptr;
     bool inited = false, in_tx = false, device_digest = false, persist = false;
+    bool unindexed = false;     // MassRangeFilteringIndex mode (SEARCH_UNINDEXED)
+    uint64_t last_matches = 0;  // unindexed: size of the last cutAndSearch result
     std::string db_id;
     // ProteinCache (ProteinCache.java:24-95): defs + sequences in id order
     std::vector<std::string> defs;
@@ -91,15 +93,17 @@ struct ListBuilder {
     }
 };
 
-// Util.getResidues(peptide, seqOffset, seqLen, proteinSequence) (Util.java:130-162)
+// Util.getResidues(peptide, seqOffset, seqLen, proteinSequence) (Util.java:130-162);
+// cut_flanks: the flanks cutSeq itself computes (DBIndexer.java:356-383, end
+// inclusive there, so no one-short right flank), kept by MassRangeFilteringIndex
 void get_residues(const uint8_t* prot, uint64_t protLen, uint64_t seqOffset, uint64_t seqLen, std::string& left,
-                  std::string& right) {
+                  std::string& right, bool cut_flanks = false) {
     const uint64_t L = 3;  // Constants.MAX_INDEX_RESIDUE_LEN
     const uint64_t resLeftI = seqOffset >= L ? seqOffset - L : 0;
     const uint64_t resLeftLen = std::min<uint64_t>(L, seqOffset);
     std::string sl((const char*)prot + resLeftI, resLeftLen);
     const uint64_t end = seqOffset + seqLen;
-    const int64_t rr = (int64_t)protLen - (int64_t)end - 1;  // protLen - end - 1 (quirk)
+    const int64_t rr = (int64_t)protLen - (int64_t)end - (cut_flanks ? 0 : 1);  // protLen - end - 1 (quirk)
     const int64_t resRightLen = std::min<int64_t>((int64_t)L, rr);
     std::string sr;
     if (end < protLen && resRightLen > 0) sr.assign((const char*)prot + end, (size_t)resRightLen);
@@ -110,7 +114,10 @@ void get_residues(const uint8_t* prot, uint64_t protLen, uint64_t seqOffset, uin
 }
 
 // materialise unique ids [first, first+count) (contiguous, ascending) into lb
-int materialise(dbi_store* s, const std::vector<uint64_t>& ids, ListBuilder& lb) {
+// filtering: MassRangeFilteringIndex entries -- protein ids without repeats
+// (addSequence :124-127, `!protIds.contains`; occurrences are in protein order,
+// so repeats are adjacent) and cutSeq's own flanks (IndexedSequence resLeft/resRight)
+int materialise(dbi_store* s, const std::vector<uint64_t>& ids, ListBuilder& lb, bool filtering = false) {
     const uint64_t n = ids.size();
     if (n == 0) return 0;
     std::vector<double> mass(n);
@@ -118,15 +125,26 @@ int materialise(dbi_store* s, const std::vector<uint64_t>& ids, ListBuilder& lb)
     std::vector<uint64_t> ob(n), oe(n);
     int rc = dbi_peptides(s->eng, ids.data(), n, mass.data(), pid.data(), off.data(), len.data(), ob.data(), oe.data());
     if (rc) return rc;
+    // occurrence lists of consecutive ids are adjacent: one read per run of ids
+    std::vector<uint32_t> run;
+    uint64_t run_b = 0, run_e = 0;
     for (uint64_t i = 0; i < n; ++i) {
-        std::vector<uint32_t> occ(oe[i] - ob[i]);
-        if (!occ.empty() && (rc = dbi_occurrences(s->eng, ob[i], oe[i], occ.data()))) return rc;
+        if (i == 0 || ids[i] != ids[i - 1] + 1) {
+            uint64_t j = i;
+            while (j + 1 < n && ids[j + 1] == ids[j] + 1) ++j;
+            run_b = ob[i];
+            run_e = oe[j];
+            run.resize(run_e - run_b);
+            if (!run.empty() && (rc = dbi_occurrences(s->eng, run_b, run_e, run.data()))) return rc;
+        }
+        std::vector<uint32_t> occ(run.begin() + (ob[i] - run_b), run.begin() + (oe[i] - run_b));
         const uint8_t* prot = s->residues.data() + s->off[pid[i]];
         const uint64_t plen = s->off[pid[i] + 1] - s->off[pid[i]];
         lb.mass.push_back(mass[i]);
         lb.chars.append((const char*)prot + off[i], len[i]);
         lb.seq_off.push_back(lb.chars.size());
-        get_residues(prot, plen, off[i], len[i], lb.left, lb.right);
+        get_residues(prot, plen, off[i], len[i], lb.left, lb.right, filtering);
+        if (filtering) occ.erase(std::unique(occ.begin(), occ.end()), occ.end());
         lb.prot_ids.insert(lb.prot_ids.end(), occ.begin(), occ.end());
         lb.prot_off.push_back(lb.prot_ids.size());
         lb.offset.push_back(off[i]);
@@ -138,7 +156,9 @@ int materialise(dbi_store* s, const std::vector<uint64_t>& ids, ListBuilder& lb)
 
 int ensure_engine(dbi_store* s) {
     if (s->eng) return 0;
-    return dbi_open(&s->p, s->device, &s->eng);
+    int rc = dbi_open(&s->p, s->device, &s->eng);
+    if (!rc && s->unindexed) rc = dbi_set_bucket_drop(s->eng, 0);
+    return rc;
 }
 
 }  // namespace
@@ -164,6 +184,7 @@ void dbi_store_close(dbi_store* s) {
 
 int dbi_store_set_device_digest(dbi_store* s, int on) {
     if (!s) return set_error(DBI_E_INVALID, "NULL store");
+    if (!on && s->unindexed) return set_error(DBI_E_STATE, "the unindexed store digests on the device");
     if (s->in_tx && !s->om.empty()) return set_error(DBI_E_STATE, "occurrences already added in this transaction");
     s->device_digest = on != 0;
     return 0;
@@ -172,7 +193,29 @@ int dbi_store_set_device_digest(dbi_store* s, int on) {
 int dbi_store_set_persist(dbi_store* s, int on) {
     if (!s) return set_error(DBI_E_INVALID, "NULL store");
     if (s->inited) return set_error(DBI_E_STATE, "set persistence before init()");
+    if (on && s->unindexed) return set_error(DBI_E_STATE, "the unindexed store keeps no index on disk");
     s->persist = on != 0;
+    return 0;
+}
+
+int dbi_store_set_unindexed(dbi_store* s, int on) {
+    if (!s) return set_error(DBI_E_INVALID, "NULL store");
+    if (s->inited) return set_error(DBI_E_STATE, "set the unindexed mode before init()");
+    if (on) {
+        // SKIP_PROTEIN_START ends a start's walk once its mass passes every range
+        // (DBIndexer.java:351-354); that drops nothing only while masses never decrease
+        for (int c = 0; c < 256; ++c)
+            if (!(s->p.mass[c] >= 0.0))
+                return set_error(DBI_E_INVALID, "unindexed search needs non-negative residue masses");
+        if (!(s->p.max_mh < 65536.0))
+            return set_error(DBI_E_INVALID, "unindexed search needs a max precursor mass < 65536 Da");
+        s->device_digest = true;
+        s->persist = false;
+        // MassRangeFilteringIndex.filterSequence has no mandatory-residue test;
+        // cutSeq's own test (DBIndexer.java:334-344, mandatory[]) stays
+        s->p.mandatory_count = 0;
+    }
+    s->unindexed = on != 0;
     return 0;
 }
 
@@ -243,6 +286,10 @@ int dbi_store_stop_add_seq(dbi_store* s) {
 int dbi_store_index_exists(dbi_store* s, int* out) {
     if (!s || !out) return set_error(DBI_E_INVALID, "NULL argument");
     if (!s->inited) return set_error(DBI_E_STATE, "Not intialized");
+    if (s->unindexed) {  // MassRangeFilteringIndex.indexExists (:83-87)
+        *out = 0;
+        return 0;
+    }
     dbi_stats st{};
     if (s->eng && engine_built(s->eng)) dbi_stats_get(s->eng, &st);
     *out = st.n_keys > 0;  // hasSequences(): any bucket with rows (SQLiteMult:204-213)
@@ -309,6 +356,10 @@ int dbi_store_add_sequence(dbi_store* s, double mass, int32_t offset, int32_t le
 int dbi_store_get_number_sequences(dbi_store* s, int64_t* out) {
     if (!s || !out) return set_error(DBI_E_INVALID, "NULL argument");
     if (!s->inited) return set_error(DBI_E_STATE, "Indexer is not initialized");
+    if (s->unindexed) {  // MassRangeFilteringIndex.getNumberSequences (:181-183): the last result's size
+        *out = (int64_t)s->last_matches;
+        return 0;
+    }
     dbi_stats st{};
     if (s->eng && engine_built(s->eng)) dbi_stats_get(s->eng, &st);
     *out = (int64_t)st.n_keys;
@@ -330,6 +381,7 @@ int dbi_store_get_total_seq_count(dbi_store* s, int64_t* out) {
 int dbi_store_get_entry_keys(dbi_store* s, int32_t* keys, uint64_t cap, uint64_t* n) {
     if (!s || !n) return set_error(DBI_E_INVALID, "NULL argument");
     if (!s->inited) return set_error(DBI_E_STATE, "Indexer is not initialized");
+    if (s->unindexed) return set_error(DBI_E_STATE, "Method not implemented");  // MassRangeFilteringIndex:212-215
     if (!s->eng || !engine_built(s->eng)) {
         *n = 0;
         return 0;
@@ -339,9 +391,39 @@ int dbi_store_get_entry_keys(dbi_store* s, int32_t* keys, uint64_t cap, uint64_t
 
 dbi_handle* dbi_store_engine(dbi_store* s) { return s ? s->eng : nullptr; }
 
+int dbi_store_cut_and_search(dbi_store* s, const double* mass, const double* tol, uint64_t n_ranges,
+                             dbi_seq_list** out) {
+    if (!s || !out || (n_ranges && (!mass || !tol))) return set_error(DBI_E_INVALID, "NULL argument");
+    *out = nullptr;
+    if (!s->unindexed) return set_error(DBI_E_STATE, "Cut and search only supported for SEARCH_UNINDEXED mode !");
+    if (!s->inited) return set_error(DBI_E_STATE, "Indexer is not initialized");
+    ListBuilder lb;
+    s->last_matches = 0;
+    if (n_ranges == 0 || !s->eng || !engine_built(s->eng)) return lb.finish(out);
+    // every range is one window of the mass-sorted unique table (the engine
+    // is built without buckets); their union, each sequence once
+    std::vector<uint64_t> first(n_ranges), count(n_ranges);
+    int rc = dbi_query(s->eng, mass, tol, n_ranges, first.data(), count.data());
+    if (rc) return rc;
+    std::vector<std::pair<uint64_t, uint64_t>> iv;
+    for (uint64_t i = 0; i < n_ranges; ++i)
+        if (count[i]) iv.push_back({first[i], first[i] + count[i]});
+    std::sort(iv.begin(), iv.end());
+    std::vector<uint64_t> ids;
+    uint64_t next = 0;
+    for (auto& r : iv) {
+        for (uint64_t u = std::max(r.first, next); u < r.second; ++u) ids.push_back(u);
+        next = std::max(next, r.second);
+    }
+    if ((rc = materialise(s, ids, lb, true))) return rc;
+    s->last_matches = ids.size();
+    return lb.finish(out);
+}
+
 int dbi_store_get_sequences(dbi_store* s, double mass, double tol, dbi_seq_list** out) {
     if (!s || !out) return set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
+    if (s->unindexed) return dbi_store_cut_and_search(s, &mass, &tol, 1, out);
     if (!s->inited) return set_error(DBI_E_STATE, "Indexer is not initialized");
     ListBuilder lb;
     if (s->eng && engine_built(s->eng)) {
@@ -359,6 +441,7 @@ int dbi_store_get_sequences_ranges(dbi_store* s, const double* mass, const doubl
                                    dbi_seq_list** out) {
     if (!s || !out || (n_ranges && (!mass || !tol))) return set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
+    if (s->unindexed) return dbi_store_cut_and_search(s, mass, tol, n_ranges, out);
     if (n_ranges == 1) return dbi_store_get_sequences(s, mass[0], tol[0], out);
     if (!s->inited) return set_error(DBI_E_STATE, "Indexer is not initialized");
     ListBuilder lb;

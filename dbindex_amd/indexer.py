@@ -11,11 +11,13 @@ the store's ``getSequences``.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Iterable, List, Optional, Set, Tuple, Union
 
 from .fasta import PackedProteins, iter_fasta, uniprot_accession
 from .params import DBIndexSearchParams, calculate_mass, tolerance_in_dalton
-from .store import DBIndexStoreHip, IndexedProtein, IndexedSequence, MassRange
+from .store import DBIndexStoreHip, IndexedProtein, IndexedSequence, MassRange, MassRangeFilteringIndexHip
 
 PRECISION = 0.000001  # Constants.java:50
 
@@ -27,6 +29,7 @@ class DBIndexerException(Exception):
 class IndexerMode:
     INDEX = "INDEX"
     SEARCH_INDEXED = "SEARCH_INDEXED"
+    SEARCH_UNINDEXED = "SEARCH_UNINDEXED"
 
 
 class DBIndexer:
@@ -37,11 +40,17 @@ class DBIndexer:
                  database_name: str = "synthetic.fasta"):
         self.sparam = sparam
         self.mode = mode
-        self.indexStore = indexStore if indexStore is not None else DBIndexStoreHip(sparam, device)
+        if indexStore is None:  # DBIndexer(sparam, mode) (:167-200)
+            indexStore = (MassRangeFilteringIndexHip(sparam, device) if mode == IndexerMode.SEARCH_UNINDEXED
+                          else DBIndexStoreHip(sparam, device))
+        if mode == IndexerMode.SEARCH_UNINDEXED and not isinstance(indexStore, MassRangeFilteringIndexHip):
+            raise DBIndexerException("SEARCH_UNINDEXED needs the MassRangeFilteringIndex store")
+        self.indexStore = indexStore
         self.indexStore.setDeviceDigest(True)
         self.protNum = -1
         self.inited = False
         self.database_name = database_name
+        self._cache_populated = False
 
     # DBIndexer.init (:412-451)
     def init(self) -> None:
@@ -49,7 +58,22 @@ class DBIndexer:
             raise RuntimeError("Already inited")
         self.protNum = -1
         self.indexStore.init(self.database_name + "_dbindex_hip")
+        if self.mode == IndexerMode.SEARCH_UNINDEXED and os.path.isfile(self.database_name):
+            self._set_protein_cache(self.database_name)  # setProteinCache() (:443-444, :463-500)
         self.inited = True
+
+    def _set_protein_cache(self, fasta) -> None:
+        """SEARCH_UNINDEXED: every FASTA protein into the ProteinCache (no decoy
+        filter, :482-488), digested once on the device."""
+        if self._cache_populated:
+            return
+        self.indexStore.startAddSeq()
+        try:
+            for d, s in _fasta_items(fasta):
+                self.cutSeq(d, s)
+        finally:
+            self.indexStore.stopAddSeq()
+        self._cache_populated = True
 
     # DBIndexerHip.cutSeq: only hand the protein to the store (DBIndexer.java:251)
     def cutSeq(self, protAccession: str, protSeq: str) -> None:
@@ -59,9 +83,15 @@ class DBIndexer:
         self.indexStore.addProteinDef(self.protNum, protAccession, protSeq)
 
     # DBIndexer.run (:508-684), INDEX mode
-    def run(self, fasta: Union[PackedProteins, str, Iterable[Tuple[str, str]]]) -> None:
+    def run(self, fasta: Union[PackedProteins, str, Iterable[Tuple[str, str]], None] = None) -> None:
         if not self.inited:
             raise RuntimeError("Not initialized.")
+        if self.mode == IndexerMode.SEARCH_UNINDEXED:
+            # the reference returns here (:516-518) and cuts the ProteinCache per
+            # search; a FASTA given here fills the cache when init() had no file
+            if fasta is not None:
+                self._set_protein_cache(fasta)
+            return
         if self.indexStore.indexExists():
             return  # "Found existing index, skipping indexing." (:522-527)
         items = _fasta_items(fasta)
@@ -77,10 +107,14 @@ class DBIndexer:
 
     # --- queries (DBIndexer.java:762-871) -------------------------------------
     def getSequencesUsingDaltonTolerance(self, precursorMass: float, massToleranceInDa: float):
+        if self.mode == IndexerMode.SEARCH_UNINDEXED:
+            return self.indexStore.cutAndSearch([MassRange(precursorMass, massToleranceInDa)])
         return self.indexStore.getSequences(precursorMass, massToleranceInDa)
 
     def getSequencesUsingPPMTolerance(self, precursorMass: float, massToleranceInPPM: float):
         massTolerance = tolerance_in_dalton(precursorMass, massToleranceInPPM)
+        if self.mode == IndexerMode.SEARCH_UNINDEXED:  # no upper-bound probe loop (:797-802)
+            return self.indexStore.cutAndSearch([MassRange(precursorMass, massTolerance)])
         sequences = self.indexStore.getSequences(precursorMass, massTolerance)
         seen = {s.getSequence() for s in sequences}
         upperBound = precursorMass + massTolerance
@@ -104,6 +138,8 @@ class DBIndexer:
         return sequences
 
     def getSequences(self, massRanges: List[MassRange]):
+        if self.mode == IndexerMode.SEARCH_UNINDEXED:
+            return self.indexStore.cutAndSearch(massRanges)
         return self.indexStore.getSequences(massRanges)
 
     def getProteins(self, seq: Union[IndexedSequence, str]):

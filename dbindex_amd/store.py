@@ -279,6 +279,42 @@ class DBIndexStoreHip:
         return _native.lib().dbi_store_engine(self.s)
 
 
+class MassRangeFilteringIndexHip(DBIndexStoreHip):
+    """``MassRangeFilteringIndex`` (the SEARCH_UNINDEXED store,
+    MassRangeFilteringIndex.java) on the engine.
+
+    The reference re-cuts every cached protein per search and keeps the
+    peptides whose mass lies in a range (``filterSequence`` :90-108,
+    ``addSequence`` :111-130).  Here the proteins given to ``addProteinDef``
+    are digested once on the device at ``stopAddSeq`` (no buckets, no
+    mandatory-residue filter: ``dbi_store_set_unindexed``) and every search is
+    a union of windows over the mass-sorted table -- the same set: one entry
+    per sequence (its first occurrence), protein ids without repeats, cutSeq's
+    own flanks.  Order is ascending mass (the reference's is THashMap order).
+    """
+
+    def __init__(self, sparam, device: int = 0):
+        super().__init__(sparam, device)
+        check(_native.lib().dbi_store_set_unindexed(self.s, 1))
+
+    def cutAndSearch(self, massRanges: Sequence[MassRange]) -> List[IndexedSequence]:
+        """``DBIndexer.cutAndSearch`` (DBIndexer.java:707-747)."""
+        L = _native.lib()
+        r = ctypes.POINTER(DbiSeqList)()
+        m = np.ascontiguousarray([x.getPrecMass() for x in massRanges], np.float64)
+        t = np.ascontiguousarray([x.getTolerance() for x in massRanges], np.float64)
+        check(L.dbi_store_cut_and_search(self.s, m.ctypes.data_as(ctypes.c_void_p),
+                                         t.ctypes.data_as(ctypes.c_void_p), m.shape[0], ctypes.byref(r)))
+        try:
+            return _seq_list(r)
+        finally:
+            L.dbi_seq_list_free(r)
+
+    def getResidues(self, peptideSequence: IndexedSequence, protein: IndexedProtein) -> ResidueInfo:
+        # stored in the sequence itself (MassRangeFilteringIndex.java:185-191)
+        return ResidueInfo(peptideSequence.getResLeft(), peptideSequence.getResRight())
+
+
 def get_residues(offset: int, length: int, prot: str) -> ResidueInfo:
     """Util.getResidues (Util.java:130-162), incl. the right-flank quirk
     ``min(3, protLen - end - 1)``."""

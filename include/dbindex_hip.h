@@ -131,6 +131,14 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
 
 int dbi_stats_get(dbi_handle* h, dbi_stats* out);
 
+/* Bucket switch (default on = the SQLite store: peptides with bucket >
+ * NUM_BUCKETS-1 are dropped, DBIndexStoreSQLiteMult.java:282-288, and queries
+ * reaching such a bucket are empty).  Off = MassRangeFilteringIndex semantics
+ * (SEARCH_UNINDEXED): every peptide is kept and queries are plain
+ * minMass <= m <= maxMass windows (MassRangeFilteringIndex.java:90-108).
+ * Clears the built index. */
+int dbi_set_bucket_drop(dbi_handle* h, int on);
+
 /* Batched single-range mass-window queries, getSequences(m, tol) semantics
  * (DBIndexStoreSQLiteMult.java:315-350 + IndexMerge.java:146-217,386-481):
  * for query i, the unique peptides with lo<=mass<=hi, lo=max(0,m-tol),
@@ -356,6 +364,17 @@ int dbi_store_set_device_digest(dbi_store* s, int on);
  * DBIndexer.java:522-527), and stopAddSeq() writes it (index + ProteinCache). */
 int dbi_store_set_persist(dbi_store* s, int on);
 
+/* SEARCH_UNINDEXED switch (before init; default off): the store becomes the
+ * MassRangeFilteringIndex (DBIndexer.java:175-200, MassRangeFilteringIndex.java):
+ * device digestion over the ProteinCache (addProteinDef) without buckets and
+ * without the SQLite store's mandatory-residue filter; getSequences and
+ * cutAndSearch return every peptide with a mass in any [m - tol, m + tol],
+ * one entry per sequence (first occurrence), protein ids without repeats;
+ * indexExists() is false, getNumberSequences() is the last result's size,
+ * getEntryKeys() is not supported.  Needs non-negative residue masses and a
+ * max precursor mass < 65536 Da. */
+int dbi_store_set_unindexed(dbi_store* s, int on);
+
 int dbi_store_init(dbi_store* s, const char* database_id);              /* init(String)      */
 int dbi_store_start_add_seq(dbi_store* s);                              /* startAddSeq()     */
 int dbi_store_stop_add_seq(dbi_store* s);                               /* stopAddSeq()      */
@@ -394,6 +413,11 @@ int dbi_store_get_sequences(dbi_store* s, double mass, double tol, dbi_seq_list*
 /* getSequences(List<MassRange>) (DBIndexStoreSQLiteMult.java:353-430) */
 int dbi_store_get_sequences_ranges(dbi_store* s, const double* mass, const double* tol,
                                    uint64_t n_ranges, dbi_seq_list** out);
+/* DBIndexer.cutAndSearch(List<MassRange>) (DBIndexer.java:707-747) over the
+ * unindexed store: ranges minMass = m - tol, maxMass = m + tol; results in
+ * ascending mass (the reference returns THashMap order, i.e. unspecified). */
+int dbi_store_cut_and_search(dbi_store* s, const double* mass, const double* tol,
+                             uint64_t n_ranges, dbi_seq_list** out);
 void dbi_seq_list_free(dbi_seq_list* l);
 
 /* ProteinCache accessors (ProteinCache.java:60-127) */

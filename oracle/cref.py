@@ -199,3 +199,41 @@ def calculate_mass(cparams, seq: str) -> float:
 
 def tolerance_in_dalton(mass: float, ppm: float) -> float:
     return lib().oref_tolerance_in_dalton(mass, ppm)
+
+
+def cut_and_search(cparams, residues: np.ndarray, offsets: np.ndarray, masses, tols) -> dict:
+    """DBIndexer.cutAndSearch over MassRangeFilteringIndex (DBIndexer.java:707-747,
+    MassRangeFilteringIndex.java:40-130) on the C++ digest: the filtering store
+    has no buckets and no mandatory-residue filter (so mandatory_count = 0 and
+    every occurrence counts, dropped or not), and keeps the peptides with
+    min <= m <= max for some range.  SKIP_PROTEIN_START only ends a start's walk
+    once m exceeds every range, after which masses never fall back in range
+    (residue masses >= 0), so filtering the full digest gives the same set --
+    tests/test_oracle.py pins this against pyref.cut_and_search, which runs the
+    filter inside the walk.  Same return form as pyref.cut_and_search."""
+    cp = type(cparams)()
+    ctypes.memmove(ctypes.byref(cp), ctypes.byref(cparams), ctypes.sizeof(cparams))
+    cp.mandatory_count = 0
+    d = digest(cp, residues, offsets)
+    lo = np.asarray(masses, np.float64) - np.asarray(tols, np.float64)
+    hi = np.asarray(masses, np.float64) + np.asarray(tols, np.float64)
+    keep = np.zeros(d.mass.shape[0], bool)
+    for a, b in zip(lo, hi):  # NaN bounds select nothing
+        keep |= (d.mass >= a) & (d.mass <= b)
+    res = np.asarray(residues, np.uint8).tobytes()
+    offs = np.asarray(offsets, np.uint64)
+    out: dict = {}
+    for i in np.nonzero(keep)[0]:
+        pid, off, ln = int(d.pid[i]), int(d.offset[i]), int(d.length[i])
+        p0, p1 = int(offs[pid]), int(offs[pid + 1])
+        seq = res[p0 + off: p0 + off + ln].decode("ascii")
+        e = out.get(seq)
+        if e is None:
+            prot = res[p0:p1].decode("ascii")
+            end = off + ln - 1
+            left = prot[max(0, off - 3): off].rjust(3, "-")
+            right = prot[end + 1: end + 1 + max(0, min(3, len(prot) - end - 1))].ljust(3, "-")
+            out[seq] = (float(d.mass[i]), off, ln, left, right, [pid])
+        elif pid not in e[5]:
+            e[5].append(pid)
+    return out

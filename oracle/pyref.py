@@ -11,6 +11,8 @@ sources (paths relative to /root/reference/src/main/java/edu/scripps/yates/dbind
 * ``Store.get_sequences`` — SQLiteMult.getSequences(m,tol) :315-350 +
                         IndexMerge.getSequences/parseAddPeptideInfo :146-217,386-481
 * ``get_residues``    — Util.getResidues, Util.java:130-162
+* ``cut_and_search``  — DBIndexer.cutAndSearch :707-747 over MassRangeFilteringIndex
+                        (init :40-67, filterSequence :90-108, addSequence :111-130)
 
 Only for small inputs (pure-Python loops).  Agreement with the C++ oracle is
 bit-exact (masses compared as float64 bit patterns).  Ties between different
@@ -77,8 +79,10 @@ def filter_sequence(params, prec_mass: float, sequence: str) -> int:
     return INCLUDE
 
 
-def cut_seq(params, prot_seq: str, protein_id: int, out: list) -> None:
-    """Appends (mass, protein_id, offset, length, dropped) per INCLUDE'd peptide."""
+def cut_seq(params, prot_seq: str, protein_id: int, out: list, filt=None) -> None:
+    """Appends (mass, protein_id, offset, length, dropped) per INCLUDE'd peptide;
+    ``filt`` replaces the store's filterSequence (default: SQLiteMult's)."""
+    filt = filt or filter_sequence
     enz = Enzyme(params.enzyme_residues, params.enzyme_nocut_residues, params.semi_cleavage)
     table = params.residue_mass
     length = len(prot_seq)
@@ -108,7 +112,7 @@ def cut_seq(params, prot_seq: str, protein_id: int, out: list) -> None:
                     if params.mandatory_internal_aas is not None:
                         if not any(aa in pep for aa in params.mandatory_internal_aas):
                             break
-                    fr = filter_sequence(params, prec, pep)
+                    fr = filt(params, prec, pep)
                     if fr == SKIP_PROTEIN_START:
                         break
                     if fr == INCLUDE:
@@ -232,3 +236,47 @@ def build(params, proteins: Sequence[str]) -> Store:
         st.add_sequence(mass, off, ln, pid)
     st.stop_add_seq()
     return st
+
+
+def range_filter(min_masses: Sequence[float], max_masses: Sequence[float]):
+    """MassRangeFilteringIndex.filterSequence (MassRangeFilteringIndex.java:90-108)."""
+    def filt(params, prec_mass: float, sequence: str) -> int:
+        skip_start = True
+        for lo, hi in zip(min_masses, max_masses):
+            if prec_mass <= hi:
+                skip_start = False
+                if prec_mass >= lo:
+                    return INCLUDE
+        return SKIP_PROTEIN_START if skip_start else SKIP
+    return filt
+
+
+def cut_flanks(prot: str, offset: int, length: int) -> Tuple[str, str]:
+    """The flanks cutSeq builds for addSequence (DBIndexer.java:356-383)."""
+    end = offset + length - 1
+    left = prot[max(0, offset - 3): offset].rjust(3, "-")
+    right = prot[end + 1: end + 1 + max(0, min(3, len(prot) - end - 1))].ljust(3, "-")
+    return left, right
+
+
+def cut_and_search(params, proteins: Sequence[str], ranges: Sequence[Tuple[float, float]]) -> Dict[str, tuple]:
+    """DBIndexer.cutAndSearch: every protein of the cache re-cut through the
+    range filter; one entry per sequence (the first occurrence's mass, offset,
+    length and flanks) with its protein ids without repeats.  Returns
+    {sequence: (mass, offset, length, left, right, [protein ids])}."""
+    mins = [m - t for m, t in ranges]  # `if (minMass == 0) minMass = 0f` changes nothing
+    maxs = [m + t for m, t in ranges]
+    filt = range_filter(mins, maxs)
+    occ: list = []
+    for pid, s in enumerate(proteins):
+        cut_seq(params, s, pid, occ, filt)
+    out: Dict[str, tuple] = {}
+    for mass, pid, off, ln, _ in occ:
+        seq = proteins[pid][off: off + ln]
+        e = out.get(seq)
+        if e is None:
+            left, right = cut_flanks(proteins[pid], off, ln)
+            out[seq] = (mass, off, ln, left, right, [pid])
+        elif pid not in e[5]:
+            e[5].append(pid)
+    return out

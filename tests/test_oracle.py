@@ -220,3 +220,59 @@ def test_oracle_matches_golden(fname, prm, nprot):
     assert np.array_equal(u["occ_prot"], g["u_occ_prot"])
     first, count = ix.query_batch(g["q_mass"][:300], g["q_tol"][:300])
     assert np.array_equal(first, g["q_first"][:300]) and np.array_equal(count, g["q_count"][:300])
+
+
+def _unindexed_ranges(masses: np.ndarray, rng: np.random.Generator, n: int):
+    """Ranges for cutAndSearch: exact masses (tol 0), narrow and wide windows,
+    overlapping ones, a NaN one, one below zero and one past every peptide."""
+    pick = masses[rng.integers(0, masses.shape[0], n)] if masses.shape[0] else np.zeros(n)
+    tol = rng.choice([0.0, 0.005, 0.05, 1.0, 25.0], n)
+    m = np.concatenate([pick, [float("nan"), -5.0, 9.0e4, pick[0] if n else 800.0]])
+    t = np.concatenate([tol, [1.0, 2.0, 10.0, 30.0]])
+    return m, t
+
+
+@pytest.mark.parametrize("name,prm,n", [
+    ("tryp2", DBIndexSearchParams.trypsin(2), 40),
+    ("semi1", DBIndexSearchParams.semi_tryptic(1), 12),
+    ("nonspec", DBIndexSearchParams.non_specific(12), 5),
+    ("mandK", DBIndexSearchParams.trypsin(2, mandatory_internal_aas="K"), 40),
+    ("no_drop", DBIndexSearchParams.trypsin(4, max_precursor_mass=9500.0), 30),
+])
+def test_cut_and_search_twins_agree(name, prm, n):
+    """pyref.cut_and_search filters inside the walk (SKIP_PROTEIN_START breaks);
+    cref.cut_and_search filters the full digest: same result."""
+    pp = fasta.config("1k").slice(0, n)
+    seqs = pp.sequences()
+    d = cref.digest(prm.to_c(), pp.residues, pp.offsets)
+    rng = np.random.default_rng(7)
+    for k in (1, 3, 12):
+        m, t = _unindexed_ranges(d.mass, rng, k)
+        for sel in (slice(0, k), slice(0, None), slice(k, k + 1)):
+            rs = list(zip(m[sel].tolist(), t[sel].tolist()))
+            py = pyref.cut_and_search(prm, seqs, rs)
+            c = cref.cut_and_search(prm.to_c(), pp.residues, pp.offsets, m[sel], t[sel])
+            assert py.keys() == c.keys(), (name, k, sel)
+            for s_, e in py.items():
+                assert np.float64(e[0]).view(np.uint64) == np.float64(c[s_][0]).view(np.uint64)
+                assert e[1:] == c[s_][1:], (name, s_)
+    # a wide window past 8000 Da keeps the peptides the bucketed store drops
+    if name == "no_drop":
+        c = cref.cut_and_search(prm.to_c(), pp.residues, pp.offsets, [8700.0], [800.0])
+        assert any(v[0] >= 8000.0 for v in c.values())
+        assert int(d.dropped.sum()) > 0
+
+
+def test_cut_and_search_flanks_and_protein_ids():
+    # a peptide repeated inside one protein and across proteins: ids once each,
+    # first occurrence kept; cutSeq's right flank is the full remainder
+    prm = DBIndexSearchParams.trypsin(0, min_precursor_mass=300.0)
+    seqs = ["MPEPTIDEKAAGGKPEPTIDEK", "GGGKPEPTIDEK", "PEPTIDEKW"]
+    mass = cref.calculate_mass(prm.to_c(), "PEPTIDEK")
+    py = pyref.cut_and_search(prm, seqs, [(mass, 0.0)])
+    assert set(py) == {"PEPTIDEK"}
+    m_, off, ln, left, right, pids = py["PEPTIDEK"]
+    assert (off, ln, pids) == (14, 8, [0, 1, 2])
+    assert (left, right) == ("GGK", "---")
+    assert pyref.cut_flanks("PEPTIDEKW", 0, 8) == ("---", "W--")
+    assert pyref.get_residues(0, 8, "PEPTIDEKW") == ("---", "---")  # Util's one-short quirk
