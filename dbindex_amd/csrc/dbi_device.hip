@@ -201,6 +201,18 @@ struct WalkOut {
 // fp64 sum; once m > maxMH the reference stops (a break at a cut, the while
 // condition elsewhere); m <= maxMH and m >= minMH hold at every emit, so the
 // non-mandatory filterSequence is always INCLUDE.
+// dbi_set_windows filter: m inside one of the sorted disjoint closed intervals
+// (MassRangeFilteringIndex.filterSequence :90-108 INCLUDE)
+__device__ __forceinline__ bool in_windows(const DevParams& dp, double m) {
+    uint32_t lo = 0, hi = dp.n_win;  // first interval starting above m
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (dp.win_lo[mid] <= m) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo > 0 && m <= dp.win_hi[lo - 1];
+}
+
 template <bool EMIT, bool SEMI, bool MAND>
 __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSmem& sm, uint32_t w0, uint32_t wlim,
                                             uint32_t s, bool n_ok, uint64_t loc, Rec* __restrict__ out,
@@ -239,7 +251,8 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
             mand_excl = mand_excl | ((fl & F_MAND) != 0);
         }
         const bool drop = can_drop & emit & (m >= dp.drop_mass);  // bucket > NUM_BUCKETS-1 (:282-288)
-        const bool keep = emit & !drop;
+        bool keep = emit & !drop;
+        if (dp.filter && keep) keep = in_windows(dp, m);
         if (EMIT && keep) {
             const uint32_t tag = fold_tag(hsh);
             Rec rec;
@@ -249,7 +262,8 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
         }
         kept += keep;
         dropped += drop;
-        if (brk | mbrk | last | over | ovf) break;            // breaks + while condition (:284)
+        const bool past = m > dp.win_max;                     // SKIP_PROTEIN_START (:351-354)
+        if (brk | mbrk | last | over | ovf | past) break;     // breaks + while condition (:284)
         ++e;
         cur = nxt;
     }
@@ -292,16 +306,17 @@ __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const 
             mand_excl = mand_excl || (fl & F_MAND);
         }
         const bool drop = emit && m >= dp.drop_mass;
-        if (EMIT && emit && !drop) {
+        const bool keep = emit && !drop && (!dp.filter || in_windows(dp, m));
+        if (EMIT && keep) {
             const uint32_t tag = fold_tag(hsh);
             Rec rec;
             rec.q0 = rec_q0(m, tag);
             rec.q1 = rec_q1(tag, loc, e - s + 1);
             if (out + kept < out_end) out[kept] = rec;
         }
-        kept += emit && !drop;
+        kept += keep;
         dropped += drop;
-        if (brk || mbrk || last || over) break;
+        if (brk || mbrk || last || over || m > dp.win_max) break;
     }
     r.kept = kept;
     r.dropped = dropped;

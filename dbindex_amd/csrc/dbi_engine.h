@@ -134,6 +134,8 @@ struct dbi_handle {
     DevBuf<uint32_t> o_pid, o_off, o_len;
 
     // query scratch
+    DevBuf<double> win_lo, win_hi;      // dbi_set_windows: merged mass windows
+    bool inputs_resident = false;       // res/poff hold the last host build's inputs (dbi_rebuild)
     DevBuf<double> q_mass, q_tol;
     DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
     DevBuf<double> g_mass;

@@ -82,6 +82,10 @@ DevParams make_dev_params(const dbi_params& p) {
     d.semi = p.semi ? 1 : 0;
     d.drop_mass = (double)(d.nb * d.br);
     d.buckets = 1;
+    d.filter = 0;
+    d.n_win = 0;
+    d.win_max = INFINITY;
+    d.win_lo = d.win_hi = nullptr;
     double mmax = 0.0;
     for (int c = 0; c < 256; ++c) mmax = std::max(mmax, p.mass[c]);
     d.cut_count = (!p.semi && !p.mandatory_mode && mmax < 1024.0) ? 1 : 0;  // fixed-point prefix tables fit u32
@@ -252,7 +256,7 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
     uint64_t n;
     // full enzyme, no mandatory residues, <= 2 missed cleavages: one walk into
     // bounded per-tile reservations (<= 4 slots per cleavage-site start)
-    const bool bounded = !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2;
+    const bool bounded = !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2 && !h->dp.filter;
     if (h->recA.cap >= 1024) {
         // warm: one pass into the capacity of the previous build; the exact
         // need comes back with the counters, and a short buffer is grown and
@@ -364,6 +368,7 @@ int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const 
     DBI_HIP(hipStreamSynchronize(h->stream));  // off32 is a stack vector
     h->d_res = h->res.p;
     h->d_poff = h->poff.p;
+    h->inputs_resident = true;
     return 0;
 }
 
@@ -493,7 +498,7 @@ void dbi_close(dbi_handle* h) {
     h->samp.release(); h->xcount.release();
     h->qcnt.release(); h->qpairA.release(); h->qpairB.release(); h->qsend.release(); h->qrecv.release();
     h->qres.release(); h->qback.release(); h->blk.release(); h->scan_tmp.release();
-    h->status.release();
+    h->status.release(); h->win_lo.release(); h->win_hi.release();
     h->thr.release(); h->tile_pf.release(); h->chunk_lo.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
     h->big_list.release(); h->giant_list.release(); h->segs.release(); h->synth_len.release(); h->synth_res.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
@@ -768,6 +773,61 @@ int dbi_set_bucket_drop(dbi_handle* h, int on) {
     h->dp.drop_mass = on ? (double)(h->dp.nb * h->dp.br) : INFINITY;
     h->built = false;  // an index built under the other setting no longer answers
     return 0;
+}
+
+int dbi_set_windows(dbi_handle* h, const double* mass, const double* tol, uint64_t n, int on) {
+    if (!h || (n && on && (!mass || !tol))) return set_error(DBI_E_INVALID, "NULL argument");
+    if (on && h->dp.buckets) return set_error(DBI_E_STATE, "a window filter needs the bucket drop off");
+    h->built = false;
+    if (!on) {
+        h->dp.filter = 0;
+        h->dp.n_win = 0;
+        h->dp.win_max = INFINITY;
+        h->dp.win_lo = h->dp.win_hi = nullptr;
+        h->dp.cut_count = make_dev_params(h->params).cut_count;
+        return 0;
+    }
+    // MassRangeFilteringIndex.init (:51-65): [m - tol, m + tol]; a NaN bound
+    // includes nothing; sorted and merged into disjoint intervals
+    std::vector<std::pair<double, double>> iv;
+    for (uint64_t i = 0; i < n; ++i) {
+        const double lo = mass[i] - tol[i], hi = mass[i] + tol[i];
+        if (lo == lo && hi == hi && lo <= hi) iv.push_back({lo, hi});
+    }
+    std::sort(iv.begin(), iv.end());
+    std::vector<double> wl, wh;
+    for (auto& r : iv) {
+        if (!wl.empty() && r.first <= wh.back()) wh.back() = std::max(wh.back(), r.second);
+        else { wl.push_back(r.first); wh.push_back(r.second); }
+    }
+    int rc;
+    if ((rc = h->win_lo.ensure(std::max<size_t>(wl.size(), 1))) || (rc = h->win_hi.ensure(std::max<size_t>(wh.size(), 1))))
+        return rc;
+    if (!wl.empty()) {
+        DBI_HIP(hipMemcpyAsync(h->win_lo.p, wl.data(), 8 * wl.size(), hipMemcpyHostToDevice, h->stream));
+        DBI_HIP(hipMemcpyAsync(h->win_hi.p, wh.data(), 8 * wh.size(), hipMemcpyHostToDevice, h->stream));
+        DBI_HIP(hipStreamSynchronize(h->stream));
+    }
+    h->dp.filter = 1;
+    h->dp.n_win = (uint32_t)wl.size();
+    h->dp.win_max = wl.empty() ? -INFINITY : wh.back();
+    h->dp.win_lo = h->win_lo.p;
+    h->dp.win_hi = h->win_hi.p;
+    h->dp.cut_count = 0;  // the stepping count does not see masses per peptide
+    return 0;
+}
+
+int dbi_rebuild(dbi_handle* h) {
+    if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    if (!h->inputs_resident || h->d_res != h->res.p || h->d_poff != h->poff.p)
+        return set_error(DBI_E_STATE, "no resident inputs: dbi_build from host arrays first");
+    int rc;
+    const uint64_t n_res = h->n_res, n_prot = h->n_prot;
+    if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    h->d_res = h->res.p;
+    h->d_poff = h->poff.p;
+    if ((rc = build_digest(h))) return rc;
+    return finish_build(h);
 }
 
 int dbi_set_timing(dbi_handle* h, int on, const char* only) {

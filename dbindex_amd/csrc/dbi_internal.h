@@ -100,6 +100,14 @@ struct DevParams {
     double drop_mass;         // bucket > NUM_BUCKETS-1  <=>  (int)m >= nb*br  <=>  m >= nb*br
     int32_t cut_count;        // count by cut stepping (full enzyme, no mandatory AAs, residue masses < 1024 Da)
     int32_t buckets;          // 1: bucketed store (drop + query bucket test); 0: MassRangeFilteringIndex (none)
+    // mass-window filter (dbi_set_windows): keep only peptides inside one of
+    // n_win sorted disjoint closed intervals; a start's walk ends once its mass
+    // passes win_max (SKIP_PROTEIN_START, DBIndexer.java:351-354)
+    int32_t filter;
+    uint32_t n_win;
+    double win_max;           // +inf without a filter
+    const double* win_lo;     // device arrays, n_win each
+    const double* win_hi;
 };
 
 constexpr int GIANT_PASSES = 3;  // MSD split passes over chunks above BIG_CAP (then the global-memory fallback)

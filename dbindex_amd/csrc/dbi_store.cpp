@@ -36,7 +36,7 @@ struct dbi_store {
     int device = 0;
     dbi_handle* eng = nullptr;
     bool inited = false, in_tx = false, device_digest = false, persist = false;
-    bool unindexed = false;     // MassRangeFilteringIndex mode (SEARCH_UNINDEXED)
+    int unindexed = 0;          // MassRangeFilteringIndex mode (SEARCH_UNINDEXED): 0 off, 1 resident, 2 stream
     uint64_t last_matches = 0;  // unindexed: size of the last cutAndSearch result
     std::string db_id;
     // ProteinCache (ProteinCache.java:24-95): defs + sequences in id order
@@ -215,7 +215,8 @@ int dbi_store_set_unindexed(dbi_store* s, int on) {
         // cutSeq's own test (DBIndexer.java:334-344, mandatory[]) stays
         s->p.mandatory_count = 0;
     }
-    s->unindexed = on != 0;
+    if (on < 0 || on > DBI_UNINDEXED_STREAM) return set_error(DBI_E_INVALID, "unknown unindexed mode");
+    s->unindexed = on;
     return 0;
 }
 
@@ -262,7 +263,11 @@ int dbi_store_stop_add_seq(dbi_store* s) {
     int rc = ensure_engine(s);
     if (rc) return rc;
     const uint64_t P = s->defs.size();
-    if (s->device_digest) {
+    if (s->unindexed == DBI_UNINDEXED_STREAM) {
+        // proteins to HBM once; each search digests them through its windows
+        if ((rc = dbi_set_windows(s->eng, nullptr, nullptr, 0, 1))) return rc;
+        rc = dbi_build(s->eng, s->residues.data(), s->residues.size(), s->off.data(), P);
+    } else if (s->device_digest) {
         rc = dbi_build(s->eng, s->residues.data(), s->residues.size(), s->off.data(), P);
     } else {
         rc = dbi_build_occurrences(s->eng, s->residues.data(), s->residues.size(), s->off.data(), P, s->om.data(),
@@ -399,11 +404,16 @@ int dbi_store_cut_and_search(dbi_store* s, const double* mass, const double* tol
     if (!s->inited) return set_error(DBI_E_STATE, "Indexer is not initialized");
     ListBuilder lb;
     s->last_matches = 0;
-    if (n_ranges == 0 || !s->eng || !engine_built(s->eng)) return lb.finish(out);
+    const bool stream = s->unindexed == DBI_UNINDEXED_STREAM;
+    if (n_ranges == 0 || !s->eng || (!stream && !engine_built(s->eng))) return lb.finish(out);
     // every range is one window of the mass-sorted unique table (the engine
     // is built without buckets); their union, each sequence once
+    int rc;
+    if (stream) {  // cut the cached proteins through these ranges
+        if ((rc = dbi_set_windows(s->eng, mass, tol, n_ranges, 1)) || (rc = dbi_rebuild(s->eng))) return rc;
+    }
     std::vector<uint64_t> first(n_ranges), count(n_ranges);
-    int rc = dbi_query(s->eng, mass, tol, n_ranges, first.data(), count.data());
+    rc = dbi_query(s->eng, mass, tol, n_ranges, first.data(), count.data());
     if (rc) return rc;
     std::vector<std::pair<uint64_t, uint64_t>> iv;
     for (uint64_t i = 0; i < n_ranges; ++i)

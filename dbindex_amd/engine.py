@@ -190,6 +190,22 @@ class Engine:
         check(_native.lib().dbi_entry_keys(self.h, _p(keys), n.value, ctypes.byref(n)))
         return keys
 
+    def set_bucket_drop(self, on: bool) -> None:
+        """``dbi_set_bucket_drop``: off = MassRangeFilteringIndex semantics (no buckets)."""
+        check(_native.lib().dbi_set_bucket_drop(self.h, 1 if on else 0))
+
+    def set_windows(self, mass=None, tol=None, on: bool = True) -> None:
+        """``dbi_set_windows``: the next builds keep only peptides inside a window."""
+        m = np.ascontiguousarray(mass if mass is not None else [], np.float64)
+        t = np.ascontiguousarray(tol if tol is not None else [], np.float64)
+        check(_native.lib().dbi_set_windows(self.h, m.ctypes.data_as(ctypes.c_void_p),
+                                            t.ctypes.data_as(ctypes.c_void_p), m.shape[0], 1 if on else 0))
+
+    def rebuild(self) -> BuildStats:
+        """``dbi_rebuild``: build again over the resident inputs of the last build."""
+        check(_native.lib().dbi_rebuild(self.h))
+        return self.stats()
+
     def set_timing(self, on: bool, only: str = "") -> None:
         """Per-kernel HIP events carried by the dispatch packets (default: every
         stage); ``only`` restricts them to the stages of that name."""

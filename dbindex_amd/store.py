@@ -293,9 +293,15 @@ class MassRangeFilteringIndexHip(DBIndexStoreHip):
     own flanks.  Order is ascending mass (the reference's is THashMap order).
     """
 
-    def __init__(self, sparam, device: int = 0):
+    RESIDENT, STREAM = 1, 2  # DBI_UNINDEXED_*
+
+    def __init__(self, sparam, device: int = 0, mode: int = RESIDENT):
+        """``mode``: RESIDENT keeps one device index of every peptide (searches
+        are windows over it); STREAM keeps only the proteins in HBM and
+        re-digests them through each search's ranges (memory for the matches
+        only -- for proteomes or enzymes whose full index does not fit)."""
         super().__init__(sparam, device)
-        check(_native.lib().dbi_store_set_unindexed(self.s, 1))
+        check(_native.lib().dbi_store_set_unindexed(self.s, int(mode)))
 
     def cutAndSearch(self, massRanges: Sequence[MassRange]) -> List[IndexedSequence]:
         """``DBIndexer.cutAndSearch`` (DBIndexer.java:707-747)."""

@@ -139,6 +139,19 @@ int dbi_stats_get(dbi_handle* h, dbi_stats* out);
  * Clears the built index. */
 int dbi_set_bucket_drop(dbi_handle* h, int on);
 
+/* Mass-window filter for the next builds (needs the bucket drop off): with
+ * on = 1 a build keeps only the peptides with m - tol <= mass <= m + tol for
+ * some i (MassRangeFilteringIndex.filterSequence, :90-108; a NaN bound
+ * includes nothing, n = 0 includes nothing) and ends a start's walk once its
+ * mass passes every window (SKIP_PROTEIN_START, DBIndexer.java:351-354): the
+ * SEARCH_UNINDEXED cut-and-search without a resident full index.  on = 0
+ * removes the filter.  Clears the built index. */
+int dbi_set_windows(dbi_handle* h, const double* mass, const double* tol, uint64_t n, int on);
+
+/* Build again over the inputs of the last dbi_build (still resident in HBM),
+ * under the current windows / bucket setting. */
+int dbi_rebuild(dbi_handle* h);
+
 /* Batched single-range mass-window queries, getSequences(m, tol) semantics
  * (DBIndexStoreSQLiteMult.java:315-350 + IndexMerge.java:146-217,386-481):
  * for query i, the unique peptides with lo<=mass<=hi, lo=max(0,m-tol),
@@ -364,7 +377,7 @@ int dbi_store_set_device_digest(dbi_store* s, int on);
  * DBIndexer.java:522-527), and stopAddSeq() writes it (index + ProteinCache). */
 int dbi_store_set_persist(dbi_store* s, int on);
 
-/* SEARCH_UNINDEXED switch (before init; default off): the store becomes the
+/* SEARCH_UNINDEXED switch (before init; default 0 = off): the store becomes the
  * MassRangeFilteringIndex (DBIndexer.java:175-200, MassRangeFilteringIndex.java):
  * device digestion over the ProteinCache (addProteinDef) without buckets and
  * without the SQLite store's mandatory-residue filter; getSequences and
@@ -373,7 +386,11 @@ int dbi_store_set_persist(dbi_store* s, int on);
  * indexExists() is false, getNumberSequences() is the last result's size,
  * getEntryKeys() is not supported.  Needs non-negative residue masses and a
  * max precursor mass < 65536 Da. */
-int dbi_store_set_unindexed(dbi_store* s, int on);
+int dbi_store_set_unindexed(dbi_store* s, int mode);
+#define DBI_UNINDEXED_RESIDENT 1 /* one device index of every peptide; searches are windows over it  */
+#define DBI_UNINDEXED_STREAM   2 /* proteins resident; every search re-digests them through its       */
+                                 /* ranges (dbi_set_windows): memory for the matches only, for        */
+                                 /* proteomes/enzymes whose full index does not fit in HBM            */
 
 int dbi_store_init(dbi_store* s, const char* database_id);              /* init(String)      */
 int dbi_store_start_add_seq(dbi_store* s);                              /* startAddSeq()     */

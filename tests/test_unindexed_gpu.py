@@ -53,13 +53,17 @@ def _ranges(pp, prm, rng, k):
     return pick, tol
 
 
-def _indexer(prm, pp):
-    ix = DBIndexer(prm, IndexerMode.SEARCH_UNINDEXED)
+RESIDENT, STREAM = MassRangeFilteringIndexHip.RESIDENT, MassRangeFilteringIndexHip.STREAM
+
+
+def _indexer(prm, pp, mode=RESIDENT):
+    ix = DBIndexer(prm, IndexerMode.SEARCH_UNINDEXED, indexStore=MassRangeFilteringIndexHip(prm, mode=mode))
     ix.init()
     ix.run(pp)
     return ix
 
 
+@pytest.mark.parametrize("mode", [RESIDENT, STREAM], ids=["resident", "stream"])
 @pytest.mark.parametrize("name,prm,nprot", [
     ("tryp2", DBIndexSearchParams.trypsin(2), 1000),
     ("semi2", DBIndexSearchParams.semi_tryptic(2), 200),
@@ -67,9 +71,9 @@ def _indexer(prm, pp):
     ("mandK", DBIndexSearchParams.trypsin(2, mandatory_internal_aas="K"), 1000),
     ("no_drop", DBIndexSearchParams.trypsin(4, max_precursor_mass=9500.0), 500),
 ])
-def test_cut_and_search_parity(name, prm, nprot):
+def test_cut_and_search_parity(name, prm, nprot, mode):
     pp = fasta.config("1k").slice(0, nprot)
-    ix = _indexer(prm, pp)
+    ix = _indexer(prm, pp, mode)
     rng = np.random.default_rng(11)
     cp = prm.to_c()
     for k in (1, 4, 25):
@@ -91,10 +95,11 @@ def test_cut_and_search_parity(name, prm, nprot):
         _same(ix.getSequences([MassRange(8700.0, 800.0)]), exp, (name, "past 8000"))
 
 
-def test_cut_and_search_edges():
+@pytest.mark.parametrize("mode", [RESIDENT, STREAM], ids=["resident", "stream"])
+def test_cut_and_search_edges(mode):
     prm = DBIndexSearchParams.trypsin(2)
     pp = fasta.config("1k").slice(0, 300)
-    ix = _indexer(prm, pp)
+    ix = _indexer(prm, pp, mode)
     cp = prm.to_c()
     st = ix.indexStore
     assert not st.indexExists()
@@ -114,11 +119,12 @@ def test_cut_and_search_edges():
     assert (r.getResLeft(), r.getResRight()) == (s.getResLeft(), s.getResRight())
 
 
-def test_unindexed_duplicates_within_and_across_proteins():
+@pytest.mark.parametrize("mode", [RESIDENT, STREAM], ids=["resident", "stream"])
+def test_unindexed_duplicates_within_and_across_proteins(mode):
     prm = DBIndexSearchParams.trypsin(0, min_precursor_mass=300.0)
     seqs = ["MPEPTIDEKAAGGKPEPTIDEK", "GGGKPEPTIDEK", "PEPTIDEKW"] * 3
     pp = fasta.PackedProteins.from_sequences(seqs)
-    ix = _indexer(prm, pp)
+    ix = _indexer(prm, pp, mode)
     from dbindex_amd.params import calculate_mass
     mass = calculate_mass("PEPTIDEK", prm)
     res = ix.getSequencesUsingDaltonTolerance(mass, 0.0)
@@ -141,3 +147,44 @@ def test_unindexed_store_rules():
         _native.check(_native.lib().dbi_store_cut_and_search(other.s, None, None, 0, ctypes.byref(out)))
     other.close()
     st.close()
+
+
+@pytest.mark.parametrize("name,prm,nprot", [
+    ("tryp2", DBIndexSearchParams.trypsin(2), 1000),         # fused / count-emit digest (bounded is off)
+    ("semi2", DBIndexSearchParams.semi_tryptic(2), 300),
+    ("nonspec50", DBIndexSearchParams.non_specific(50), 300),
+])
+def test_window_filtered_build_is_the_full_index_restricted(name, prm, nprot):
+    """dbi_set_windows: the filtered build's unique table, occurrence lists
+    and order equal the unbucketed full build's rows whose mass lies in a
+    window -- and dbi_rebuild over the resident inputs gives the same."""
+    from dbindex_amd.engine import Engine
+    pp = fasta.config("1k").slice(0, nprot)
+    rng = np.random.default_rng(5)
+    with Engine(prm.to_c(), 0) as full, Engine(prm.to_c(), 0) as filt:
+        full.set_bucket_drop(False)
+        filt.set_bucket_drop(False)
+        full.build(pp)
+        g = full.export()
+        um = g["mass"]
+        for rep, k in enumerate((1, 7, 60)):
+            m = um[rng.integers(0, um.shape[0], k)] + rng.normal(0, 0.01, k)
+            t = rng.choice([0.0, 0.02, 0.5, 3.0], k)
+            filt.set_windows(m, t)
+            st = filt.build(pp) if rep == 0 else filt.rebuild()
+            f = filt.export()
+            sel = np.zeros(um.shape[0], bool)
+            for a, b in zip(m - t, m + t):
+                sel |= (um >= a) & (um <= b)
+            ids = np.nonzero(sel)[0]
+            assert st.n_unique == ids.shape[0], (name, k)
+            assert np.array_equal(f["mass"].view(np.uint64), um[ids].view(np.uint64)), (name, k)
+            for key in ("prot_id", "offset", "length"):
+                assert np.array_equal(f[key], g[key][ids]), (name, k, key)
+            occ = [g["occ_prot"][g["occ_off"][i]:g["occ_off"][i + 1]] for i in ids]
+            exp_occ = np.concatenate(occ) if occ else np.zeros(0, g["occ_prot"].dtype)
+            assert np.array_equal(f["occ_prot"], exp_occ), (name, k)
+        # the filter off again: the full index
+        filt.set_windows(on=False)
+        filt.rebuild()
+        assert np.array_equal(filt.export()["mass"].view(np.uint64), um.view(np.uint64))
