@@ -111,6 +111,42 @@ class DBIndexSearchParams:
         (SURVEY.md §8(a) A2)."""
         return cls(enzyme_residues=CANONICAL_AA, max_missed_cleavages=max_len - 1, **kw)
 
+    # --- static modifications (SearchParamReader.java:357-362, 401-583) --------
+    STATIC_MOD_ORDER = "GASPVTCLIXNOBDQKZEMHFRYW"  # the reader's add_<X>_<name> order
+
+    def with_static_mods(self, mods: Dict[str, float], n15_enrichment: float = 0.0,
+                         cterm: Optional[float] = None, nterm: Optional[float] = None) -> "DBIndexSearchParams":
+        """A copy with the params file's static modifications applied to the
+        residue table: ``add_<X>_<name> = f`` goes through
+        ``AssignMassToStaticParam.addMassAndStaticParam`` (model/AssignMassToStaticParam.java:7-14),
+        which ignores ``f <= 0`` and otherwise calls ``AssignMass.addMass(X, f)``
+        (external jar; restated as mass[X] += f -- parity unpinned).  With N15
+        enrichment e > 0, f becomes ``f * e``, except cysteine:
+        ``f + e * (f - 57.02146f)`` (:451-456, float literal).  ``add_C_terminus`` /
+        ``add_N_terminus`` SET cTerm / nTerm (``AssignMass.setcTerm``, :401-407)."""
+        import dataclasses
+        import numpy as np
+        unknown = set(mods) - set(self.STATIC_MOD_ORDER)
+        if unknown:
+            raise ValueError(f"no add_<X> parameter for residue(s) {sorted(unknown)}")
+        table = dict(self.residue_mass)
+        for ch in self.STATIC_MOD_ORDER:
+            f = float(mods.get(ch, 0.0))
+            if n15_enrichment > 0:
+                if ch == "C":
+                    f = f + n15_enrichment * (f - float(np.float32(57.02146)))
+                else:
+                    f = f * n15_enrichment
+            if f <= 0:
+                continue
+            table[ch] = table.get(ch, 0.0) + f
+        out = dataclasses.replace(self, residue_mass=table)
+        if cterm is not None:
+            out.cterm = float(cterm)
+        if nterm is not None:
+            out.nterm = float(nterm)
+        return out
+
     # --- helpers ---------------------------------------------------------------
     def mass_table(self):
         t = [0.0] * 256

@@ -78,6 +78,11 @@ def test_kat_proteins(Engine, name, prm):
     ("1k_tryp2", DBIndexSearchParams.trypsin(2), 1000),
     ("1k_semi2", DBIndexSearchParams.semi_tryptic(2), 1000),
     ("100_nonspec", DBIndexSearchParams.non_specific(50), 100),
+    # params-file static mods: carbamidomethyl C, oxidised M, TMT-like K + N-term
+    ("1k_static_mods", DBIndexSearchParams.trypsin(2).with_static_mods(
+        {"C": 57.02146, "M": 15.9949, "K": 229.162932}, nterm=229.162932), 1000),
+    ("300_semi_n15", DBIndexSearchParams.semi_tryptic(1).with_static_mods({"C": 57.02146}, n15_enrichment=0.98),
+     300),
 ])
 def test_synthetic(Engine, name, prm, nprot):
     pp = fasta.config("1k") if nprot == 1000 else fasta.config("1k").slice(0, nprot)

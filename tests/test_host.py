@@ -236,3 +236,21 @@ def test_index_file_matches_header(tmp_path):
     junk.write_bytes(b"NOTANIDX" + bytes(200))
     _native.check(_native.lib().dbi_index_file_matches(ctypes.byref(p), str(junk).encode(), ctypes.byref(v)))
     assert v.value == 0
+
+
+def test_static_mods_semantics():
+    """SearchParamReader.java:401-583 via AssignMassToStaticParam (:7-14):
+    f <= 0 ignored, otherwise added to the residue mass; N15 scales f, except
+    cysteine (f + e*(f - 57.02146f)); terminus parameters set cTerm/nTerm."""
+    base = DBIndexSearchParams.trypsin(2)
+    q = base.with_static_mods({"C": 57.02146, "M": 0.0, "K": -1.0}, cterm=1.5, nterm=2.5)
+    assert q.residue_mass["C"] == base.residue_mass["C"] + 57.02146
+    assert q.residue_mass["M"] == base.residue_mass["M"] and q.residue_mass["K"] == base.residue_mass["K"]
+    assert (q.cterm, q.nterm) == (1.5, 2.5) and (base.cterm, base.nterm) == (0.0, 0.0)
+    n = base.with_static_mods({"C": 57.02146, "S": 79.966331}, n15_enrichment=0.5)
+    assert n.residue_mass["S"] == base.residue_mass["S"] + 79.966331 * 0.5
+    assert n.residue_mass["C"] == base.residue_mass["C"] + (57.02146 + 0.5 * (57.02146 - float(np.float32(57.02146))))
+    # no C mod under N15: f = 0 + e*(0 - 57.02146f) < 0 -> ignored
+    assert base.with_static_mods({}, n15_enrichment=0.5).residue_mass["C"] == base.residue_mass["C"]
+    with pytest.raises(ValueError):
+        base.with_static_mods({"J": 1.0})
