@@ -2226,6 +2226,58 @@ __device__ __forceinline__ uint32_t upper_bound_d(const double* __restrict__ a, 
     }
     return lo;
 }
+// [lo, hi) variants: the result lies in [lo, hi]
+__device__ __forceinline__ uint32_t lower_bound_in(const double* __restrict__ a, uint32_t lo, uint32_t hi, double x) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ uint32_t upper_bound_in(const double* __restrict__ a, uint32_t lo, uint32_t hi, double x) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// Query directory over the unique masses: bucket(m) = clamp((m - lo) * scale)
+// is monotone in m, so dir[b] = first unique with bucket >= b brackets every
+// bound of a mass in bucket b: lower/upper_bound(x) lie in [dir[b], dir[b+1]].
+// The binary search then runs over ~4 uniques instead of all of them.
+__device__ __forceinline__ uint32_t qdir_bucket(const QueryDir& qd, double m) {
+    const double t = (m - qd.lo) * qd.scale;
+    if (!(t > 0.0)) return 0u;
+    if (t >= (double)(qd.nb - 1)) return qd.nb - 1;
+    return (uint32_t)t;
+}
+
+__global__ void k_qdir_params(const double* __restrict__ umass, uint32_t nu, uint32_t nb, QueryDir* qd) {
+    if (threadIdx.x != 0) return;
+    const double lo = nu ? umass[0] : 0.0, hi = nu ? umass[nu - 1] : 0.0;
+    qd->lo = lo;
+    qd->scale = hi > lo ? (double)nb / (hi - lo) : 0.0;
+    qd->nb = nb;
+}
+
+__global__ void k_qdir_fill(const double* __restrict__ umass, uint32_t nu, const QueryDir* __restrict__ qdp,
+                            uint32_t* __restrict__ dir) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > nu) return;
+    const QueryDir qd = *qdp;
+    const uint32_t bi = i < nu ? qdir_bucket(qd, umass[i]) : qd.nb;  // past the last unique: every bucket left
+    const uint32_t b0 = i == 0 ? 0u : qdir_bucket(qd, umass[i - 1]) + 1;
+    for (uint32_t k = b0; k <= bi; ++k) dir[k] = i;
+}
+
+hipError_t launch_qdir(const double* d_umass, uint32_t nu, uint32_t nb, QueryDir* d_qd, uint32_t* d_dir,
+                       hipStream_t s) {
+    DBI_LAUNCH(k_qdir_params, dim3(1), dim3(64), 0, s, d_umass, nu, nb, d_qd);
+    DBI_LAUNCH(k_qdir_fill, dim3((nu + 1 + 255) / 256), dim3(256), 0, s, d_umass, nu, d_qd, d_dir);
+    return hipGetLastError();
+}
+
 // first i with key(a[i]) > k   (key monotone in mass)
 __device__ __forceinline__ uint32_t key_upper(const double* __restrict__ a, uint32_t n, int32_t factor, int32_t k) {
     uint32_t lo = 0, hi = n;
@@ -2238,9 +2290,19 @@ __device__ __forceinline__ uint32_t key_upper(const double* __restrict__ a, uint
 
 __global__ void k_query(DevParams dp, int32_t factor, const double* __restrict__ umass, uint32_t nu,
                         const double* __restrict__ qm, const double* __restrict__ qt, uint64_t nq,
-                        uint64_t* __restrict__ first, uint64_t* __restrict__ count) {
+                        uint64_t* __restrict__ first, uint64_t* __restrict__ count,
+                        const QueryDir* __restrict__ qdp, const uint32_t* __restrict__ dir) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nq) return;
+    const QueryDir qd = *qdp;
+    auto lower_bound_d = [&](const double* a, uint32_t n, double x) {
+        const uint32_t b = qdir_bucket(qd, x);
+        return lower_bound_in(a, dir[b], dir[b + 1], x);
+    };
+    auto upper_bound_d = [&](const double* a, uint32_t n, double x) {
+        const uint32_t b = qdir_bucket(qd, x);
+        return upper_bound_in(a, dir[b], dir[b + 1], x);
+    };
     const double precMass = qm[i], tol = qt[i];
     double lo = precMass - tol;
     if (lo < 0) lo = 0;
@@ -2272,10 +2334,10 @@ __global__ void k_query(DevParams dp, int32_t factor, const double* __restrict__
 
 hipError_t launch_query(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,
                         const double* d_qmass, const double* d_qtol, uint64_t nq, uint64_t* d_first,
-                        uint64_t* d_count, hipStream_t s) {
+                        uint64_t* d_count, const QueryDir* d_qd, const uint32_t* d_dir, hipStream_t s) {
     if (nq == 0) return hipSuccess;
     DBI_LAUNCH(k_query, dim3((uint32_t)((nq + 255) / 256)), dim3(256), 0, s, dp, factor, d_umass,
-                       n_unique, d_qmass, d_qtol, nq, d_first, d_count);
+                       n_unique, d_qmass, d_qtol, nq, d_first, d_count, d_qd, d_dir);
     return hipGetLastError();
 }
 

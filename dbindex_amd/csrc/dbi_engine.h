@@ -135,6 +135,9 @@ struct dbi_handle {
 
     // query scratch
     DevBuf<double> win_lo, win_hi;      // dbi_set_windows: merged mass windows
+    DevBuf<uint32_t> qdir;              // query directory (launch_qdir), rebuilt per index
+    DevBuf<dbi::QueryDir> qdir_par;
+    uint64_t build_serial = 0, qdir_serial = 0;
     bool inputs_resident = false;       // res/poff hold the last host build's inputs (dbi_rebuild)
     DevBuf<double> q_mass, q_tol;
     DevBuf<uint64_t> q_first, q_count, q_row, q_ids;

@@ -229,6 +229,7 @@ int finish_build(dbi_handle* h) {
     bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes();
     st.device_bytes = bytes;
     h->built = true;
+    ++h->build_serial;
     return 0;
 }
 
@@ -498,7 +499,7 @@ void dbi_close(dbi_handle* h) {
     h->samp.release(); h->xcount.release();
     h->qcnt.release(); h->qpairA.release(); h->qpairB.release(); h->qsend.release(); h->qrecv.release();
     h->qres.release(); h->qback.release(); h->blk.release(); h->scan_tmp.release();
-    h->status.release(); h->win_lo.release(); h->win_hi.release();
+    h->status.release(); h->win_lo.release(); h->win_hi.release(); h->qdir.release(); h->qdir_par.release();
     h->thr.release(); h->tile_pf.release(); h->chunk_lo.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
     h->big_list.release(); h->giant_list.release(); h->segs.release(); h->synth_len.release(); h->synth_res.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
@@ -600,8 +601,19 @@ int dbi_query_device(dbi_handle* h, const double* d_mass, const double* d_tol, u
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
     DBI_HIP(hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    DBI_HIP(launch_query(h->dp, h->params.mass_group_factor, h->umass.p, (uint32_t)h->stats.n_unique, d_mass,
-                         d_tol, nq, d_first, d_count, s));
+    const uint32_t nu = (uint32_t)h->stats.n_unique;
+    if (h->qdir_serial != h->build_serial) {
+        // once per index: ~4 uniques per directory bucket (at most 2^22 buckets)
+        uint32_t nb = 16;
+        while (nb < nu / 4 && nb < (1u << 22)) nb <<= 1;
+        int rc;
+        if ((rc = h->qdir.ensure((size_t)nb + 1)) || (rc = h->qdir_par.ensure(1))) return rc;
+        DBI_HIP(launch_qdir(h->umass.p, nu, nb, h->qdir_par.p, h->qdir.p, s));
+        DBI_HIP(hipStreamSynchronize(s));  // later queries may come on other streams
+        h->qdir_serial = h->build_serial;
+    }
+    DBI_HIP(launch_query(h->dp, h->params.mass_group_factor, h->umass.p, nu, d_mass, d_tol, nq, d_first, d_count,
+                         h->qdir_par.p, h->qdir.p, s));
     return 0;
 }
 

@@ -284,9 +284,16 @@ hipError_t launch_gather(const uint64_t* d_ids, uint64_t n, const double* d_umas
                          uint64_t* o_e, hipStream_t s);
 hipError_t launch_write_keys(const double* d_umass, uint32_t n_unique, int32_t factor,
                              const uint32_t* d_pos, int32_t* d_keys, hipStream_t s);
+struct QueryDir {  // query directory over the unique masses (launch_qdir)
+    double lo, scale;
+    uint32_t nb;
+};
+hipError_t launch_qdir(const double* d_umass, uint32_t nu, uint32_t nb, QueryDir* d_qd, uint32_t* d_dir,
+                       hipStream_t s);
 hipError_t launch_query(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,
                         const double* d_qmass, const double* d_qtol, uint64_t nq,
-                        uint64_t* d_first, uint64_t* d_count, hipStream_t s);
+                        uint64_t* d_first, uint64_t* d_count, const QueryDir* d_qd, const uint32_t* d_dir,
+                        hipStream_t s);
 hipError_t launch_key_range(const double* d_umass, uint32_t n_unique, int32_t factor, int32_t klo,
                             int32_t khi, uint64_t* d_out2, hipStream_t s);
 hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const uint32_t* d_off,

@@ -187,6 +187,7 @@ int index_load(dbi_handle* h, const char* path, std::vector<uint8_t>* res_out, s
     st.n_unique = U;
     st.n_keys = hd.n_keys;
     h->built = true;
+    ++h->build_serial;
     if (res_out) res_out->swap(res);
     if (off_out) off_out->swap(off);
     if (defs_out) defs_out->swap(defs);

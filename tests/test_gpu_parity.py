@@ -301,3 +301,33 @@ def test_thresholds_on_exact_peptide_masses(Engine):
     for lo, hi in [(m[100], m[-100]), (m[7], m[8]), (np.nextafter(m[50], 0), np.nextafter(m[-50], 1e9))]:
         prm = DBIndexSearchParams.trypsin(2, min_precursor_mass=float(lo), max_precursor_mass=float(hi))
         _check(Engine, prm, pp, f"thresholds {lo} {hi}", nq=300)
+
+
+@pytest.mark.parametrize("seqs", [
+    [],                                    # empty index
+    ["PEPTIDEK"],                          # one unique
+    ["PEPTIDEK", "PEPTLDEK"],              # two uniques, bit-identical masses
+    ["PEPTIDEK", "WWWWWWWWK"],             # two uniques far apart
+])
+def test_query_directory_edges(Engine, seqs):
+    """The query directory (buckets over [first, last] unique mass) brackets
+    every bound: queries exactly at, just beside, below and above the uniques,
+    zero / huge / infinite tolerances and NaN give the oracle's answer."""
+    prm = DBIndexSearchParams.trypsin(0, min_precursor_mass=300.0)
+    pp = fasta.PackedProteins.from_sequences(seqs) if seqs else fasta.PackedProteins.from_sequences(["GGK"])
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    u = oix.unique()["mass"]
+    base = list(u) + [300.0, 499.9, 5999.0, 7999.0, 1e-3]
+    m, t = [], []
+    for x in base:
+        for dx in (0.0, -1e-9, 1e-9, np.nextafter(x, -np.inf) - x, np.nextafter(x, np.inf) - x):
+            for tol in (0.0, 1e-7, 0.5, 3000.0, np.inf):
+                m.append(x + dx)
+                t.append(tol)
+    m += [float("nan"), 900.0, float("inf"), -float("inf")]
+    t += [1.0, float("nan"), 1.0, 1.0]
+    m, t = np.array(m, np.float64), np.array(t, np.float64)
+    with Engine(cp) as eng:
+        eng.build(pp)
+        assert_queries_equal(eng, oix, m, t, f"dir {len(seqs)}")
