@@ -2552,9 +2552,19 @@ hipError_t launch_qpack(const Rec* d_pairs, uint64_t np, const double* d_qm, con
 }
 
 __global__ void k_query_pairs(DevParams dp, int32_t factor, const double* __restrict__ umass, uint32_t nu,
-                              const Rec* __restrict__ in, uint64_t n, uint64_t base, Rec* __restrict__ out) {
+                              const Rec* __restrict__ in, uint64_t n, uint64_t base, Rec* __restrict__ out,
+                              const QueryDir* __restrict__ qdp, const uint32_t* __restrict__ dir) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const QueryDir qd = *qdp;
+    auto lower_bound_d = [&](const double* a, uint32_t, double x) {
+        const uint32_t b = qdir_bucket(qd, x);
+        return lower_bound_in(a, dir[b], dir[b + 1], x);
+    };
+    auto upper_bound_d = [&](const double* a, uint32_t, double x) {
+        const uint32_t b = qdir_bucket(qd, x);
+        return upper_bound_in(a, dir[b], dir[b + 1], x);
+    };
     const Rec q = in[i];
     const double precMass = __longlong_as_double((long long)q.q0), tol = __longlong_as_double((long long)q.q1);
     double lo, hi;
@@ -2575,10 +2585,11 @@ __global__ void k_query_pairs(DevParams dp, int32_t factor, const double* __rest
 }
 
 hipError_t launch_query_pairs(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,
-                              const Rec* d_in, uint64_t n, uint64_t base, Rec* d_out, hipStream_t s) {
+                              const Rec* d_in, uint64_t n, uint64_t base, Rec* d_out, const QueryDir* d_qd,
+                              const uint32_t* d_dir, hipStream_t s) {
     if (n == 0) return hipSuccess;
     DBI_LAUNCH(k_query_pairs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, dp, factor, d_umass, n_unique,
-               d_in, n, base, d_out);
+               d_in, n, base, d_out, d_qd, d_dir);
     return hipGetLastError();
 }
 

@@ -224,6 +224,7 @@ int prepare_tiles(dbi_handle* h);
 // in the unused ones when *sparse)
 int run_digest(dbi_handle* h, uint64_t* n, uint64_t* n_in, bool* sparse);
 int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse);
+int ensure_qdir(dbi_handle* h, hipStream_t s);  // query directory of the current index
 int finish_build(dbi_handle* h);
 
 }  // namespace dbi

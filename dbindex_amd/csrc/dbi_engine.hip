@@ -595,6 +595,26 @@ int dbi_stats_get(dbi_handle* h, dbi_stats* out) {
     return 0;
 }
 
+}  // extern "C"
+
+namespace dbi {
+// the query directory of the current index, built on first use (once per build / load)
+int ensure_qdir(dbi_handle* h, hipStream_t s) {
+    if (h->qdir_serial == h->build_serial) return 0;
+    const uint32_t nu = (uint32_t)h->stats.n_unique;
+    uint32_t nb = 16;  // ~4 uniques per bucket, at most 2^22 buckets
+    while (nb < nu / 4 && nb < (1u << 22)) nb <<= 1;
+    int rc;
+    if ((rc = h->qdir.ensure((size_t)nb + 1)) || (rc = h->qdir_par.ensure(1))) return rc;
+    DBI_HIP(launch_qdir(h->umass.p, nu, nb, h->qdir_par.p, h->qdir.p, s));
+    DBI_HIP(hipStreamSynchronize(s));  // later queries may come on other streams
+    h->qdir_serial = h->build_serial;
+    return 0;
+}
+}  // namespace dbi
+
+extern "C" {
+
 int dbi_query_device(dbi_handle* h, const double* d_mass, const double* d_tol, uint64_t nq, uint64_t* d_first,
                      uint64_t* d_count, void* stream) {
     if (!h) return set_error(DBI_E_INVALID, "NULL handle");
@@ -602,16 +622,8 @@ int dbi_query_device(dbi_handle* h, const double* d_mass, const double* d_tol, u
     DBI_HIP(hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     const uint32_t nu = (uint32_t)h->stats.n_unique;
-    if (h->qdir_serial != h->build_serial) {
-        // once per index: ~4 uniques per directory bucket (at most 2^22 buckets)
-        uint32_t nb = 16;
-        while (nb < nu / 4 && nb < (1u << 22)) nb <<= 1;
-        int rc;
-        if ((rc = h->qdir.ensure((size_t)nb + 1)) || (rc = h->qdir_par.ensure(1))) return rc;
-        DBI_HIP(launch_qdir(h->umass.p, nu, nb, h->qdir_par.p, h->qdir.p, s));
-        DBI_HIP(hipStreamSynchronize(s));  // later queries may come on other streams
-        h->qdir_serial = h->build_serial;
-    }
+    int rc;
+    if ((rc = ensure_qdir(h, s))) return rc;
     DBI_HIP(launch_query(h->dp, h->params.mass_group_factor, h->umass.p, nu, d_mass, d_tol, nq, d_first, d_count,
                          h->qdir_par.p, h->qdir.p, s));
     return 0;

@@ -241,8 +241,13 @@ hipError_t launch_qroute_emit(const double* d_qm, const double* d_qt, uint64_t n
 hipError_t launch_qpack(const Rec* d_pairs, uint64_t np, const double* d_qm, const double* d_qt, Rec* d_out,
                         hipStream_t s);
 // owner side: (mass, tol) -> (base + first, count), first = ~0 when count = 0
+struct QueryDir {  // query directory over the unique masses (launch_qdir)
+    double lo, scale;
+    uint32_t nb;
+};
 hipError_t launch_query_pairs(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,
-                              const Rec* d_in, uint64_t n, uint64_t base, Rec* d_out, hipStream_t s);
+                              const Rec* d_in, uint64_t n, uint64_t base, Rec* d_out, const QueryDir* d_qd,
+                              const uint32_t* d_dir, hipStream_t s);
 // origin side: fold the owners' answers into per-query (first, count)
 hipError_t launch_qcombine(const Rec* d_pairs, const Rec* d_res, uint64_t np, uint64_t* d_first,
                            uint64_t* d_count, uint64_t nq, hipStream_t s);
@@ -284,10 +289,6 @@ hipError_t launch_gather(const uint64_t* d_ids, uint64_t n, const double* d_umas
                          uint64_t* o_e, hipStream_t s);
 hipError_t launch_write_keys(const double* d_umass, uint32_t n_unique, int32_t factor,
                              const uint32_t* d_pos, int32_t* d_keys, hipStream_t s);
-struct QueryDir {  // query directory over the unique masses (launch_qdir)
-    double lo, scale;
-    uint32_t nb;
-};
 hipError_t launch_qdir(const double* d_umass, uint32_t nu, uint32_t nb, QueryDir* d_qd, uint32_t* d_dir,
                        hipStream_t s);
 hipError_t launch_query(const DevParams& dp, int32_t factor, const double* d_umass, uint32_t n_unique,

@@ -186,9 +186,9 @@ int query_route(dbi_handle* h, const double* d_m, const double* d_t, uint64_t nq
 int query_answer(dbi_handle* h) {
     ShardState& sh = h->shard;
     int rc;
-    if ((rc = h->qres.ensure(sh.q_recv + 1))) return rc;
+    if ((rc = h->qres.ensure(sh.q_recv + 1)) || (rc = ensure_qdir(h, h->stream))) return rc;
     DBI_HIP(launch_query_pairs(h->dp, h->params.mass_group_factor, h->umass.p, (uint32_t)h->stats.n_unique,
-                               h->qrecv.p, sh.q_recv, sh.u_base, h->qres.p, h->stream));
+                               h->qrecv.p, sh.q_recv, sh.u_base, h->qres.p, h->qdir_par.p, h->qdir.p, h->stream));
     return 0;
 }
 
