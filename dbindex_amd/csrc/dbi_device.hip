@@ -2012,12 +2012,18 @@ k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32
         const uint32_t a = chunk_lo[c];
         const uint32_t m = chunk_lo[c + 1] - a;
         if (m > split_above) {
-            if (threadIdx.x == 0) giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
+            if (threadIdx.x == 0) {
+                giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
+                atomicAdd(&ctr->n_giant_recs, (unsigned long long)m);
+            }
             continue;
         }
         const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, rl, k0, k1, aux, s_u32, &s_bad);
         const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
-        if (threadIdx.x == 0) ucount[c] = tot;
+        if (threadIdx.x == 0) {
+            ucount[c] = tot;
+            atomicAdd(&ctr->n_big_recs, (unsigned long long)m);
+        }
         __syncthreads();
     }
 }

@@ -125,6 +125,7 @@ struct Counters {
     unsigned int n_giant;          // chunks above BIG_CAP (MSD split into LDS-sized leaves)
     unsigned int n_seg[GIANT_PASSES + 1];  // giant split: segments in work list p
     unsigned int n_leaf_small, n_leaf_big, n_fallback;
+    unsigned long long n_big_recs, n_giant_recs;  // records in chunks sorted by the big / giant paths
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads
     // (sharing the ticket's line cost the digest 30%)
