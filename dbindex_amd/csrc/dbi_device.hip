@@ -113,18 +113,17 @@ constexpr int WIN_PRE = 16;  // residues staged before the tile (N-terminal cont
 constexpr int WIN = WIN_PRE + DIGEST_TILE + DIGEST_HALO;
 constexpr int STARTS_PER_THREAD = DIGEST_TILE / DIGEST_THREADS;
 
-constexpr uint32_t PST_CAP = 512;  // protein starts of a tile kept in LDS (else searched in HBM)
+constexpr uint32_t PST_CAP = 192;  // protein starts of a tile kept in LDS (else searched in HBM)
 
 struct DigestSmem {
     double mass[256];
     uint64_t nokm[WIN / 64 + 2];  // bit p = N_ok at window position p (protein start, or a cut at p-1)
     uint64_t cutm[WIN / 64 + 2];  // bit p = F_CUT at p            (bounded digest: slot bounds)
     uint64_t clvm[WIN / 64 + 2];  // bit p = cleave residue at p
-    uint64_t stm[WIN / 64 + 2];   // bit p = a protein starts at p
+    uint64_t stm[WIN / 64 + 2];   // bit p = a protein starts at p (incl. one past the window)
     uint32_t pst[PST_CAP];      // poff[pf .. pl+1] (protein of a start: binary search)
     alignas(16) uint16_t win[WIN + 8];  // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST);
                                 // slack: walk_bounded reads one entry ahead without a clamp
-    alignas(4) uint8_t pbit[WIN + 4];  // 1 = a protein starts at this window position (incl. one past the window)
     uint8_t flags[256];
     uint16_t cand[DIGEST_TILE]; // compacted candidate starts (tile-local), in order
     uint32_t tmp[DIGEST_THREADS / 64 + 1];
@@ -330,10 +329,11 @@ struct TileCtx {
     uint32_t w;     // record field width (EMIT)
 };
 
+__device__ __forceinline__ bool bit_at(const uint64_t* m, uint32_t p) { return (m[p >> 6] >> (p & 63)) & 1ull; }
+
 // N_ok(s) for tile position i: protein N-terminus, or the previous position is a cut
 __device__ __forceinline__ bool n_ok_at(const DigestSmem& sm, const TileCtx& tc, uint32_t i) {
-    const uint32_t p = tc.t0 + i - tc.w0;
-    return sm.pbit[p] || (p > 0 && ((sm.win[p - 1] >> 8) & F_CUT));
+    return bit_at(sm.nokm, tc.t0 + i - tc.w0);
 }
 
 // Stage the tile's window (residues + class flags + cut / protein-end flags)
@@ -377,7 +377,8 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
     tc.pl = d_tile_pf[ntiles + 1 + tile];  // proteins overlapping [t0, w_end]: [pf, pl]
     sm.mass[tid] = d_mass_tab[tid];
     sm.flags[tid] = d_flags[tid];
-    for (uint32_t i = tid; i < (uint32_t)(WIN + 4) / 4; i += DIGEST_THREADS) reinterpret_cast<uint32_t*>(sm.pbit)[i] = 0;
+    if (tid < WIN / 64 + 2) sm.stm[tid] = 0;
+    static_assert(WIN / 64 + 2 <= DIGEST_THREADS, "one thread per protein-start word");
     const uint32_t np_all = tc.pl - tc.pf + 2;
     __syncthreads();
     // residue window -> LDS as (residue | flags << 8): a vector's 16 entries
@@ -407,7 +408,7 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
     tc.npst = np_all <= PST_CAP ? np_all : 0u;
     for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
         const uint32_t o = d_poff[tc.pf + i];
-        if (o >= w0 && o <= w_end) sm.pbit[o - w0] = 1;  // protein starts (and the end of the last one)
+        if (o >= w0 && o <= w_end) atomicOr(&sm.stm[(o - w0) >> 6], 1ull << ((o - w0) & 63));  // protein starts (and the end of the last one)
         if (i < PST_CAP) sm.pst[i] = o;
     }
     __syncthreads();
@@ -429,9 +430,9 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
                 const uint32_t e = sm.win[i];
                 const uint32_t en = sm.win[i + 1];
                 const uint32_t ep = i > 0 ? (uint32_t)sm.win[i - 1] : 0u;
-                first = sm.pbit[i] != 0;
+                first = bit_at(sm.stm, i);
                 clv = ((e >> 8) & F_CLEAVE) != 0;
-                const bool last = sm.pbit[i + 1] != 0;
+                const bool last = bit_at(sm.stm, i + 1);
                 const bool nocut_next = i + 1 < nbytes && ((en >> 8) & F_NOCUT);
                 const bool cut = last || (((e >> 8) & F_CLEAVE) && !nocut_next);
                 cf[k] = (cut ? F_CUT : 0u) | (last ? F_LAST : 0u);
@@ -442,12 +443,10 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
             const uint64_t m = __ballot(nok);
             const uint64_t mc = __ballot((cf[k] & F_CUT) != 0);
             const uint64_t ml = __ballot(clv);
-            const uint64_t ms = __ballot(first);
             if (lane_id() == 0 && i < nbytes) {  // lane 0: the word's first position
                 sm.nokm[i / 64] = m;
                 sm.cutm[i / 64] = mc;
                 sm.clvm[i / 64] = ml;
-                sm.stm[i / 64] = ms;
             }
         }
         __syncthreads();
