@@ -490,6 +490,11 @@ def run_trembl(args, world: int, rank: int, dev: int, dist) -> None:
                    sample=f"cutSeq digest (oracle/cpu_ref.cpp, occurrences materialised) of {sample.n_proteins} proteins / "
                           f"{sample.n_residues} residues of the same proteome ({dg.mass.shape[0]} peptides, "
                           f"{t1:.1f}s); host CPU: {cpu_model()}", seconds=t1)
+        # the same sample counted on the GPU: totalSeqCount parity at this scale
+        d_sr = DeviceBuffer.from_numpy(np.concatenate([sample.residues, np.zeros(16, np.uint8)]), dev)
+        d_so = DeviceBuffer.from_numpy(sample.offsets.astype(np.uint64), dev)
+        g = eng.count_device(d_sr.ptr, sample.n_residues, d_so.ptr, sample.n_proteins)[0]
+        cpu.update(gpu_count_same_sample=g, sample_parity=bool(g == dg.mass.shape[0]))
     if rank == 0:
         ms = 1000.0 * elapsed / max(args.steps, 1)
         alg = res_all + 8.0 * (P + 1)  # residues + offsets read once per step (count mode writes nothing)

@@ -330,6 +330,11 @@ struct TileCtx {
 };
 
 __device__ __forceinline__ bool bit_at(const uint64_t* m, uint32_t p) { return (m[p >> 6] >> (p & 63)) & 1ull; }
+// bits p, p+1, ... of a bit map (bit 0 = position p)
+__device__ __forceinline__ uint64_t bits_from(const uint64_t* m, uint32_t p) {
+    const uint32_t w = p >> 6, b = p & 63;
+    return b ? (m[w] >> b) | (m[w + 1] << (64 - b)) : m[w];
+}
 
 // N_ok(s) for tile position i: protein N-terminus, or the previous position is a cut
 __device__ __forceinline__ bool n_ok_at(const DigestSmem& sm, const TileCtx& tc, uint32_t i) {
@@ -575,29 +580,30 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
 
 
 // ---------------------------------------------------------------------------
-// COUNT for full-enzyme digestion without mandatory residues: decisions only
-// happen at cuts (checkCleavage is C_ok; the mass only grows), so a start
-// steps cut to cut: window-local fp64 prefix sums give the mass, prefix
-// counts of cleave residues give intMisCleavageCount, a next-cut table the
-// next cut.  ~4 steps per start instead of ~30 residues.  A start whose
-// approximate mass comes within CUT_EPS Da of minMH / maxMH / the bucket-drop
-// mass, or that would leave the window, is recounted by the exact walk, so the
-// counts equal the emit pass's exactly.  (Prefix error over a 2320-residue
-// window < 3e-7 Da; CUT_EPS = 1e-5.)
+// COUNT for full-enzyme digestion without mandatory residues.  Decisions only
+// happen at cuts and every limit is monotone along a walk (the mass only
+// grows; intMisCleavageCount only grows), so the peptides of a start are the
+// cuts e in [lo, hi]: hi = min(protein end, the position before the
+// (max_missed+2)-th cleave residue, the last position with m <= maxMH), lo =
+// max(start + MIN_PEP_LENGTH - 1, the first position with m >= minMH).  Over
+// a 64-position horizon the cut / cleave / protein-start bit maps of the
+// staged window give the first two by bit selects, window-local prefix masses
+// the mass limits by binary search, and a popcount the count: ~15 LDS reads
+// per start instead of one step per residue (non-specific 6-50: ~40).  A
+// start whose approximate mass lies within CUT_EPS Da of minMH / maxMH / the
+// bucket-drop mass at a boundary, or whose walk may leave the horizon, is
+// recounted by the exact walk, so the counts equal the emit pass's exactly.
+// (Prefix error over a window < 3e-7 Da.)
 // ---------------------------------------------------------------------------
 constexpr double CUT_EPS = 1e-4;  // > 2 x the fixed-point rounding of the prefix tables (7.6e-6 Da each)
-constexpr uint16_t NO_CUT = 0xFFFFu;
 constexpr uint32_t PM_BLOCK = 64;  // positions per fp64 prefix base
 
-// Window prefix tables for cut stepping.  Mass prefix of positions [0, i]:
-// base[i / 64] (fp64, prefix before the 64-position block) + off[i] / 2^16 Da
-// (fixed point; within a block < 64 residues x 1024 Da, DevParams::cut_count).
+// Window prefix masses of positions [0, i]: base[i / 64] (fp64, prefix before
+// the 64-position block) + off[i] / 2^16 Da (fixed point; within a block < 64
+// residues x 1024 Da, DevParams::cut_count).
 struct CutSmem {
     double base[WIN / PM_BLOCK + 1];
     uint32_t off[WIN];
-    uint16_t ccl[WIN];    // cleave residues in [0, i]
-    uint16_t ncut[WIN];   // first cut position >= i (the last position only if a protein ends there)
-    uint16_t first[DIGEST_THREADS];
 };
 
 __device__ __forceinline__ double cut_prefix(const CutSmem& cs, uint32_t i) {
@@ -609,64 +615,125 @@ struct CutCount {
     bool exact;  // false: recount with the residue walk
 };
 
-__device__ __forceinline__ CutCount count_by_cuts(const DevParams& dp, const DigestSmem& sm, const CutSmem& cs,
-                                                  uint32_t nbytes, uint32_t ps) {
-    CutCount r{0u, 0u, true};
-    if (!(dp.m0 <= dp.max_mh)) return r;
-    const double pb = ps > 0 ? cut_prefix(cs, ps - 1) : 0.0;
-    const int cb = ps > 0 ? (int)cs.ccl[ps - 1] : 0;
-    const bool can_drop = dp.drop_mass <= dp.max_mh;
-    uint32_t e = cs.ncut[ps];
-    for (;;) {
-        if (e == NO_CUT) {
-            // no cut before the window ends: only fine if the mass passes maxMH first
-            const double m_end = dp.m0 + (cut_prefix(cs, nbytes - 1) - pb);
-            r.exact = m_end > dp.max_mh + CUT_EPS;
-            return r;
+// position of the k-th (1-based) set bit of v, 64 when v has fewer
+__device__ __forceinline__ uint32_t select_bit(uint64_t v, uint32_t k) {
+    if ((uint32_t)__popcll(v) < k) return 64u;
+    uint32_t p = 0;
+#pragma unroll
+    for (uint32_t w = 32; w; w >>= 1) {
+        const uint32_t c = (uint32_t)__popcll(v & ((1ull << w) - 1));
+        if (c < k) {
+            k -= c;
+            v >>= w;
+            p += w;
         }
-        const double m = dp.m0 + (cut_prefix(cs, e) - pb);
-        if (fabs(m - dp.max_mh) <= CUT_EPS) { r.exact = false; return r; }
-        const int mc = (int)cs.ccl[e] - cb - 1;
-        if (mc > dp.max_missed || m > dp.max_mh) return r;  // break (:322-329)
-        if ((int)(e - ps + 1) >= dp.min_len) {
-            if (fabs(m - dp.min_mh) <= CUT_EPS || (can_drop && fabs(m - dp.drop_mass) <= CUT_EPS)) {
+    }
+    return p;
+}
+
+// bits lo..hi (lo <= hi <= 63)
+__device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi) {
+    return ((2ull << hi) - 1ull) & ~((1ull << lo) - 1ull);
+}
+
+__device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const DigestSmem& sm, const CutSmem& cs,
+                                                   uint32_t nbytes, uint32_t ps) {
+    CutCount r{0u, 0u, true};
+    if (!(dp.m0 <= dp.max_mh)) return r;  // while condition before the first residue (:284)
+    if (ps + 2 > nbytes) { r.exact = false; return r; }
+    // horizon: relative positions 0..h (the window's last position, whose cut is unknown, excluded)
+    const uint32_t h = min(63u, nbytes - 2 - ps);
+    const uint64_t hmask = bit_range(0, h);
+    const uint64_t C = bits_from(sm.cutm, ps) & hmask;   // cuts (checkCleavage, incl. protein ends)
+    const uint64_t V = bits_from(sm.clvm, ps) & hmask;   // cleave residues (intMisCleavageCount)
+    const uint64_t S = bits_from(sm.stm, ps + 1) & hmask;  // bit k: the next protein starts at ps+1+k
+    uint32_t H = h;
+    bool ends = false;  // the walk emits nothing past H
+    if (S) { H = (uint32_t)__ffsll((long long)S) - 1; ends = true; }  // protein end (:284 end < length)
+    const uint32_t xk = select_bit(V, (uint32_t)dp.max_missed + 2u);  // mc > max_missed at cuts from here (:322)
+    if (xk <= H) {  // xk >= 1
+        H = xk - 1;
+        ends = true;
+    }
+    const double pb = ps > 0 ? cut_prefix(cs, ps - 1) : 0.0;
+    auto M = [&](uint32_t e) { return dp.m0 + (cut_prefix(cs, ps + e) - pb); };
+    // last position with m <= maxMH (the walk stops past it: :284, :326)
+    int Y;
+    {
+        const double mH = M(H);
+        if (mH <= dp.max_mh) {
+            if (dp.max_mh - mH <= CUT_EPS || !ends) { r.exact = false; return r; }
+            Y = (int)H;
+        } else {
+            if (mH - dp.max_mh <= CUT_EPS) { r.exact = false; return r; }
+            uint32_t a = 0, b = H;  // first e with M(e) > maxMH
+            while (a < b) {
+                const uint32_t mid = (a + b) >> 1;
+                if (M(mid) > dp.max_mh) b = mid; else a = mid + 1;
+            }
+            if (a > 0 && dp.max_mh - M(a - 1) <= CUT_EPS) { r.exact = false; return r; }
+            if (M(a) - dp.max_mh <= CUT_EPS) { r.exact = false; return r; }
+            Y = (int)a - 1;
+        }
+    }
+    // first emittable position: pepSize >= MIN_PEP_LENGTH and m >= minMH (:331)
+    int lo = dp.min_len - 1;
+    if (Y < lo) return r;
+    {
+        const double ml = M((uint32_t)lo);
+        if (fabs(ml - dp.min_mh) <= CUT_EPS) { r.exact = false; return r; }
+        if (ml < dp.min_mh) {
+            const double my = M((uint32_t)Y);
+            if (fabs(my - dp.min_mh) <= CUT_EPS) { r.exact = false; return r; }
+            if (my < dp.min_mh) return r;
+            uint32_t a = (uint32_t)lo + 1, b = (uint32_t)Y;  // first e with M(e) >= minMH
+            while (a < b) {
+                const uint32_t mid = (a + b) >> 1;
+                if (M(mid) >= dp.min_mh) b = mid; else a = mid + 1;
+            }
+            if (fabs(M(a) - dp.min_mh) <= CUT_EPS || fabs(M(a - 1) - dp.min_mh) <= CUT_EPS) {
                 r.exact = false;
                 return r;
             }
-            if (m >= dp.min_mh) {
-                const bool drop = can_drop && m >= dp.drop_mass;
-                r.kept += !drop;
-                r.dropped += drop;
-            }
+            lo = (int)a;
         }
-        if ((sm.win[e] >> 8) & F_LAST) return r;
-        e = e + 1 < nbytes ? cs.ncut[e + 1] : NO_CUT;
     }
+    const uint64_t em = C & bit_range((uint32_t)lo, (uint32_t)Y);
+    const uint32_t n = (uint32_t)__popcll(em);
+    uint32_t nd = 0;
+    if (dp.drop_mass <= dp.max_mh && n) {  // bucket > NUM_BUCKETS-1 (:282-288): the cuts from m >= drop_mass on
+        const double my = M((uint32_t)Y), ml = M((uint32_t)lo);
+        if (fabs(my - dp.drop_mass) <= CUT_EPS || fabs(ml - dp.drop_mass) <= CUT_EPS) { r.exact = false; return r; }
+        if (my >= dp.drop_mass) {
+            uint32_t a = (uint32_t)lo, b = (uint32_t)Y;  // first e with M(e) >= drop_mass
+            while (a < b) {
+                const uint32_t mid = (a + b) >> 1;
+                if (M(mid) >= dp.drop_mass) b = mid; else a = mid + 1;
+            }
+            if (fabs(M(a) - dp.drop_mass) <= CUT_EPS || (a > 0 && fabs(M(a - 1) - dp.drop_mass) <= CUT_EPS)) {
+                r.exact = false;
+                return r;
+            }
+            nd = (uint32_t)__popcll(em & bit_range(a, (uint32_t)Y));
+        }
+    }
+    r.kept = n - nd;
+    r.dropped = nd;
+    return r;
 }
 
-// Build the cut tables from the staged window (all threads; ends with a barrier).
+// Build the prefix-mass tables from the staged window (all threads; ends with a barrier).
 __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nbytes, double* s_dtmp) {
     constexpr uint32_t E = (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS;
     const uint32_t lo = threadIdx.x * E;
     double msum = 0.0;
-    uint32_t csum = 0;
-    uint32_t fc = NO_CUT;  // first cut in my range
 #pragma unroll
     for (uint32_t k = 0; k < E; ++k) {
         const uint32_t i = lo + k;
-        if (i < nbytes) {
-            const uint32_t w = sm.win[i];
-            msum += sm.mass[w & 0xFFu];
-            csum += (w >> 8) & F_CLEAVE;
-            const bool cut = ((w >> 8) & F_CUT) && (i + 1 < nbytes || ((w >> 8) & F_LAST));
-            if (cut && fc == NO_CUT) fc = i;
-        }
+        if (i < nbytes) msum += sm.mass[sm.win[i] & 0xFFu];
     }
     double dtot;
-    uint32_t ctot;
     double mrun = block_excl_scan<DIGEST_THREADS, double>(msum, s_dtmp, dtot);
-    uint32_t crun = block_excl_scan<DIGEST_THREADS, uint32_t>(csum, reinterpret_cast<uint32_t*>(s_dtmp), ctot);
-    cs.first[threadIdx.x] = (uint16_t)fc;
     if (threadIdx.x == 0) cs.base[0] = 0.0;
     double pm[E];
 #pragma unroll
@@ -674,27 +741,16 @@ __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nby
         const uint32_t i = lo + k;
         pm[k] = 0.0;
         if (i < nbytes) {
-            const uint32_t w = sm.win[i];
-            mrun += sm.mass[w & 0xFFu];
-            crun += (w >> 8) & F_CLEAVE;
+            mrun += sm.mass[sm.win[i] & 0xFFu];
             pm[k] = mrun;
-            cs.ccl[i] = (uint16_t)crun;
             if (i % PM_BLOCK == PM_BLOCK - 1) cs.base[i / PM_BLOCK + 1] = mrun;
         }
     }
     __syncthreads();
-    uint32_t nxt = NO_CUT;  // first cut after my range
-    for (uint32_t t = threadIdx.x + 1; t < DIGEST_THREADS && nxt == NO_CUT; ++t) nxt = cs.first[t];
 #pragma unroll
-    for (int k = (int)E - 1; k >= 0; --k) {
-        const uint32_t i = lo + (uint32_t)k;
-        if (i < nbytes) {
-            cs.off[i] = (uint32_t)__double2ll_rn((pm[k] - cs.base[i / PM_BLOCK]) * 65536.0);
-            const uint32_t w = sm.win[i];
-            const bool cut = ((w >> 8) & F_CUT) && (i + 1 < nbytes || ((w >> 8) & F_LAST));
-            if (cut) nxt = i;
-            cs.ncut[i] = (uint16_t)nxt;
-        }
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint32_t i = lo + k;
+        if (i < nbytes) cs.off[i] = (uint32_t)__double2ll_rn((pm[k] - cs.base[i / PM_BLOCK]) * 65536.0);
     }
     __syncthreads();
 }
@@ -715,7 +771,7 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     thread_share(ncand, jb, je);
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
-        CutCount r = count_by_cuts(dp, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0);
+        CutCount r = count_by_masks(dp, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0);
         if (!r.exact) {
             const WalkOut w = walk_candidate<false, false, false>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr);
             r.kept = w.kept;
@@ -978,10 +1034,6 @@ __device__ __forceinline__ WalkOut walk_candidate_bounded(const DevParams& dp, c
 // protein start, whichever comes first; `cap` when neither lies within the 64
 // positions from p (or the window ends first: the walk may leave it).  Mass
 // filters only lower the real count.  Branch-free over 64-position slices.
-__device__ __forceinline__ uint64_t bits_from(const uint64_t* m, uint32_t p) {
-    const uint32_t w = p >> 6, b = p & 63;
-    return b ? (m[w] >> b) | (m[w + 1] << (64 - b)) : m[w];
-}
 
 __device__ __forceinline__ uint32_t slot_bound(const DigestSmem& sm, uint32_t p, uint32_t nbytes, uint32_t kcl,
                                                uint32_t min_len, uint32_t cap) {

@@ -399,7 +399,10 @@ int dbi_dev_free(int device, void* p) {
 
 int dbi_dev_copy_h2d(int device, void* dst, const void* src, uint64_t bytes) {
     DBI_HIP(hipSetDevice(device));
-    if (bytes) DBI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    if (bytes) {
+        DBI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+        DBI_HIP(hipDeviceSynchronize());  // pageable sources: the DMA may still be in flight on return
+    }
     return 0;
 }
 
@@ -411,7 +414,12 @@ int dbi_dev_copy_d2h(int device, void* dst, const void* src, uint64_t bytes) {
 
 int dbi_dev_copy_d2d(int device, void* dst, const void* src, uint64_t bytes) {
     DBI_HIP(hipSetDevice(device));
-    if (bytes) DBI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+    if (bytes) {
+        // a device-to-device hipMemcpy may return before the copy ran; the source
+        // may be an engine buffer its next (non-blocking-stream) call overwrites
+        DBI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+        DBI_HIP(hipDeviceSynchronize());
+    }
     return 0;
 }
 
@@ -489,7 +497,8 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
                 (params->mandatory[c] ? F_MAND : 0);
     if (hipMemcpy(h->mass_tab.p, params->mass, sizeof(double) * 256, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->flags_tab.p, fl, 256, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(h->ctr.p, 0, sizeof(Counters)) != hipSuccess)
+        hipMemset(h->ctr.p, 0, sizeof(Counters)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)  // null-stream work done before the engine's non-blocking stream runs
         return fail(set_error(DBI_E_HIP, "parameter upload failed"));
     *out = h;
     return 0;

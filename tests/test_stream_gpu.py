@@ -77,3 +77,24 @@ def test_count_empty(Engine):
         d_res, d_off, n_res = eng.synth_proteome(4, 0, 0, 0, TABLES)
         assert n_res == 0
         assert eng.count_device(d_res, 0, d_off, 0) == (0, 0)
+
+
+@pytest.mark.parametrize("shift", [1, 3, 8, 13])
+def test_count_and_build_misaligned_residues(shift):
+    """The C-ABI takes any device pointer: residues starting at an odd byte
+    (chunks packed back to back) must count and index exactly as aligned ones."""
+    from dbindex_amd import _native
+    from dbindex_amd.engine import Engine
+    pp = fasta.config("1k").slice(0, 120)
+    for prm in (DBIndexSearchParams.non_specific(50), DBIndexSearchParams.trypsin(2)):
+        cp = prm.to_c()
+        oix = cref.Index(cp, pp.residues, pp.offsets)
+        buf = np.full(pp.n_residues + shift + 64, ord("W"), np.uint8)  # heavy bytes around the data
+        buf[shift:shift + pp.n_residues] = pp.residues
+        d_res = _native.DeviceBuffer.from_numpy(buf, 0)
+        d_off = _native.DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), 0)
+        with Engine(cp, 0) as eng:
+            tot, drop = eng.count_device(d_res.ptr + shift, pp.n_residues, d_off.ptr, pp.n_proteins)
+            assert (tot, drop) == (oix.n_total, oix.n_dropped), (shift, prm)
+            st = eng.build_device(d_res.ptr + shift, pp.n_residues, d_off.ptr, pp.n_proteins)
+            assert st.n_total == oix.n_total and st.n_unique == oix.n_unique, (shift, prm)
