@@ -331,3 +331,26 @@ def test_query_directory_edges(Engine, seqs):
     with Engine(cp) as eng:
         eng.build(pp)
         assert_queries_equal(eng, oix, m, t, f"dir {len(seqs)}")
+
+
+def test_size_limits_fail_loudly(Engine):
+    """Limits of the 16-B record and the u32 device indices are errors, never
+    wrong answers: >= 2^32-1 residues or proteins per device, and a record
+    layout of 2 x bits(longest protein) + bits(protein count) > 56."""
+    from dbindex_amd import _native
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    with Engine(cp) as eng:
+        fake = 1 << 20  # never dereferenced: the sizes are rejected first
+        with pytest.raises(_native.DBIndexStoreException, match="2\\^32"):
+            eng.build_device(fake, (1 << 32) - 1, fake, 10)
+        with pytest.raises(_native.DBIndexStoreException, match="2\\^32"):
+            eng.build_device(fake, 100, fake, (1 << 32) - 1)
+        # longest protein 2^20 residues -> W = 21: at most 2^14 proteins
+        long = "AAAAAAK" * ((1 << 20) // 7 + 1)
+        seqs = [long] + ["GGGGGGK"] * (1 << 14)
+        pp = fasta.PackedProteins.from_sequences(seqs)
+        with pytest.raises(_native.DBIndexStoreException, match="56 bits"):
+            eng.build(pp)
+        ok = fasta.PackedProteins.from_sequences(seqs[:-1])  # 2^14 proteins: fits
+        st = eng.build(ok)
+        assert st.n_total > 0
