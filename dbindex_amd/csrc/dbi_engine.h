@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -134,6 +135,7 @@ struct dbi_handle {
     DevBuf<uint32_t> o_pid, o_off, o_len;
 
     // query scratch
+    std::recursive_mutex qmu;           // query-side calls share scratch buffers and the stream
     DevBuf<double> win_lo, win_hi;      // dbi_set_windows: merged mass windows
     DevBuf<uint32_t> qdir;              // query directory (launch_qdir), rebuilt per index
     DevBuf<dbi::QueryDir> qdir_par;

@@ -632,6 +632,7 @@ extern "C" {
 int dbi_query_device(dbi_handle* h, const double* d_mass, const double* d_tol, uint64_t nq, uint64_t* d_first,
                      uint64_t* d_count, void* stream) {
     if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
     DBI_HIP(hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
@@ -645,6 +646,7 @@ int dbi_query_device(dbi_handle* h, const double* d_mass, const double* d_tol, u
 
 int dbi_query(dbi_handle* h, const double* mass, const double* tol, uint64_t nq, uint64_t* first, uint64_t* count) {
     if (!h || (nq && (!mass || !tol || !first || !count))) return set_error(DBI_E_INVALID, "NULL argument");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
     if (nq == 0) return 0;
     DBI_HIP(hipSetDevice(h->device));
@@ -662,8 +664,9 @@ int dbi_query(dbi_handle* h, const double* mass, const double* tol, uint64_t nq,
 }
 
 int dbi_query_csr(dbi_handle* h, const double* mass, const double* tol, uint64_t nq, dbi_query_result** out) {
-    if (!out) return set_error(DBI_E_INVALID, "NULL argument");
+    if (!out || !h) return set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     std::vector<uint64_t> first(nq), count(nq);
     int rc = dbi_query(h, mass, tol, nq, first.data(), count.data());
     if (rc) return rc;
@@ -711,6 +714,7 @@ void dbi_query_result_free(dbi_query_result* r) {
 int dbi_peptides(dbi_handle* h, const uint64_t* ids, uint64_t n, double* mass, uint32_t* prot_id, uint32_t* offset,
                  uint32_t* length, uint64_t* occ_begin, uint64_t* occ_end) {
     if (!h || (n && !ids)) return set_error(DBI_E_INVALID, "NULL argument");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
     if (n == 0) return 0;
     for (uint64_t i = 0; i < n; ++i)
@@ -736,6 +740,7 @@ int dbi_peptides(dbi_handle* h, const uint64_t* ids, uint64_t n, double* mass, u
 
 int dbi_occurrences(dbi_handle* h, uint64_t begin, uint64_t end, uint32_t* prot_id) {
     if (!h || !prot_id) return set_error(DBI_E_INVALID, "NULL argument");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
     if (begin > end || end > h->stats.n_kept) return set_error(DBI_E_INVALID, "occurrence range out of bounds");
     if (end == begin) return 0;
@@ -748,6 +753,7 @@ int dbi_occurrences(dbi_handle* h, uint64_t begin, uint64_t end, uint32_t* prot_
 int dbi_export(dbi_handle* h, double* mass, uint32_t* prot_id, uint32_t* offset, uint32_t* length, uint64_t* occ_off,
                uint32_t* occ_prot) {
     if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
     DBI_HIP(hipSetDevice(h->device));
     const uint64_t U = h->stats.n_unique, K = h->stats.n_kept;
@@ -770,6 +776,7 @@ int dbi_export(dbi_handle* h, double* mass, uint32_t* prot_id, uint32_t* offset,
 
 int dbi_entry_keys(dbi_handle* h, int32_t* keys, uint64_t cap, uint64_t* n) {
     if (!h || !n) return set_error(DBI_E_INVALID, "NULL argument");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
     *n = h->stats.n_keys;
     if (!keys) return 0;

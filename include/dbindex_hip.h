@@ -152,6 +152,13 @@ int dbi_set_windows(dbi_handle* h, const double* mass, const double* tol, uint64
  * under the current windows / bucket setting. */
 int dbi_rebuild(dbi_handle* h);
 
+/* Threading: a build (dbi_build*, dbi_rebuild, dbi_count,
+ * dbi_index_load, the dbi_shard_* phases) is exclusive per handle.  Query-side
+ * calls (dbi_query*, dbi_peptides, dbi_occurrences, dbi_export,
+ * dbi_entry_keys) may come from several threads at once: they serialise on
+ * the handle's scratch buffers; dbi_query_device on caller buffers and its
+ * own stream only for the one-off query directory. */
+
 /* Batched single-range mass-window queries, getSequences(m, tol) semantics
  * (DBIndexStoreSQLiteMult.java:315-350 + IndexMerge.java:146-217,386-481):
  * for query i, the unique peptides with lo<=mass<=hi, lo=max(0,m-tol),

@@ -354,3 +354,35 @@ def test_size_limits_fail_loudly(Engine):
         ok = fasta.PackedProteins.from_sequences(seqs[:-1])  # 2^14 proteins: fits
         st = eng.build(ok)
         assert st.n_total > 0
+
+
+def test_concurrent_queries_from_threads(Engine):
+    """Query-side calls from several host threads on one handle (ctypes drops
+    the GIL): every answer equals the oracle's."""
+    import threading
+    pp = fasta.config("1k")
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    m, t = query_masses(oix, 4000)
+    of, oc = oix.query_batch(m, t)
+    errors = []
+    with Engine(cp) as eng:
+        eng.build(pp)
+
+        def worker(seed):
+            rng = np.random.default_rng(seed)
+            for _ in range(20):
+                sel = rng.integers(0, m.shape[0], 500)
+                f, c = eng.query(m[sel], t[sel])
+                hit = oc[sel] > 0
+                if not (np.array_equal(c, oc[sel]) and np.array_equal(f[hit], of[sel][hit])):
+                    errors.append(seed)
+                ids = np.unique(rng.integers(0, oix.n_unique, 50)).astype(np.uint64)
+                eng.peptides(ids)
+
+        th = [threading.Thread(target=worker, args=(s,)) for s in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    assert not errors
