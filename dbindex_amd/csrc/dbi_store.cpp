@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -38,6 +39,7 @@ struct dbi_store {
     bool inited = false, in_tx = false, device_digest = false, persist = false;
     int unindexed = 0;          // MassRangeFilteringIndex mode (SEARCH_UNINDEXED): 0 off, 1 resident, 2 stream
     uint64_t last_matches = 0;  // unindexed: size of the last cutAndSearch result
+    std::mutex search_mu;       // STREAM searches rebuild the engine's index: one at a time
     std::string db_id;
     // ProteinCache (ProteinCache.java:24-95): defs + sequences in id order
     std::vector<std::string> defs;
@@ -402,6 +404,7 @@ int dbi_store_cut_and_search(dbi_store* s, const double* mass, const double* tol
     *out = nullptr;
     if (!s->unindexed) return set_error(DBI_E_STATE, "Cut and search only supported for SEARCH_UNINDEXED mode !");
     if (!s->inited) return set_error(DBI_E_STATE, "Indexer is not initialized");
+    std::lock_guard<std::mutex> lock(s->search_mu);
     ListBuilder lb;
     s->last_matches = 0;
     const bool stream = s->unindexed == DBI_UNINDEXED_STREAM;
