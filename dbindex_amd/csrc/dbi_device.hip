@@ -1065,9 +1065,13 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
                  uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, unsigned long long* __restrict__ status,
                  uint32_t epoch, Rec* __restrict__ d_out, uint64_t cap, Counters* __restrict__ d_ctr) {
     __shared__ DigestSmem sm;
-    __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_tile, s_kept, s_waves;
     __shared__ unsigned long long s_base;
-    if (threadIdx.x == 0) s_tile = atomicAdd(&d_ctr->tile_ticket, 1u);
+    if (threadIdx.x == 0) {
+        s_tile = atomicAdd(&d_ctr->tile_ticket, 1u);
+        s_kept = 0;
+        s_waves = 0;
+    }
     __syncthreads();
     const uint32_t tile = s_tile;
     TileCtx tc;
@@ -1104,11 +1108,26 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     if (kept > lim) atomicOr(&d_ctr->err, ERR_SLOTS);  // slot_bound is an upper bound: never
     const Rec sent{REC_SENTINEL, REC_SENTINEL};
     for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
-    const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
-    const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
-    if (threadIdx.x == 0) {
-        if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
-        if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
+    if (DROP) {
+        const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
+        const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
+        if (threadIdx.x == 0) {
+            if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
+            if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
+        }
+    } else {
+        // nothing is dropped (drop_mass > maxMH, also in walk_global); the tile
+        // total without a barrier: each wave adds its sum in LDS, the last wave
+        // to arrive publishes it
+        const uint32_t wk = wave_sum(kept);
+        if (lane_id() == 0) {
+            atomicAdd(&s_kept, wk);
+            __threadfence_block();
+            if (atomicAdd(&s_waves, 1u) == DIGEST_THREADS / 64 - 1) {
+                const uint32_t tk = atomicAdd(&s_kept, 0u);
+                if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
+            }
+        }
     }
 }
 
