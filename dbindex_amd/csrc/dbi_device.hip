@@ -69,20 +69,18 @@ __device__ __forceinline__ T block_excl_scan(T v, T* s_tmp, T& total) {
     T inc = wave_incl_scan(v);
     if (lane_id() == 63) s_tmp[w] = inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        T acc = 0;
-        for (int i = 0; i < NW; ++i) {
-            T t = s_tmp[i];
-            s_tmp[i] = acc;
-            acc += t;
-        }
-        s_tmp[NW] = acc;
+    // every thread folds the (few) wave totals itself, in wave order: one
+    // barrier less than a serial pass by thread 0, same additions
+    T before = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const T t = s_tmp[i];
+        if (i < w) before += t;
+        all += t;
     }
-    __syncthreads();
-    T r = inc - v + s_tmp[w];
-    total = s_tmp[NW];
-    __syncthreads();
-    return r;
+    total = all;
+    __syncthreads();  // s_tmp reusable
+    return inc - v + before;
 }
 
 template <int NT, typename T>
