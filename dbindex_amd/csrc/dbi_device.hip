@@ -2146,17 +2146,24 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
     for (uint32_t t0 = 0; t0 < n; t0 += FIN_THREADS * FIN_ITEMS) {
         uint4 rv[FIN_ITEMS];
         uint32_t lpre[FIN_ITEMS];
+        // lane 0 also loads the record before its own (the rest take it from
+        // the lane below): every load of the round in flight together
+        const bool l0 = lane_id() == 0;
+        unsigned long long pq[FIN_ITEMS];
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
             const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
             rv[k] = i < n ? r4[i] : make_uint4(0, 0, 0, 0);  // low byte of q0 = head flag
+            pq[k] = (l0 && i < n && a + i > 0) ? recs[a + i - 1].q0 : 0ull;
         }
         // mass of the record before each head (= the previous unique's mass)
         double prevm[FIN_ITEMS];
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
             const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
-            prevm[k] = (i < n && a + i > 0 && (rv[k].x & 0xFFu)) ? q0_mass(recs[a + i - 1].q0) : 0.0;
+            const uint32_t px = __shfl_up((int)rv[k].x, 1, 64), py = __shfl_up((int)rv[k].y, 1, 64);
+            const unsigned long long prev = l0 ? pq[k] : (((unsigned long long)py << 32) | px);
+            prevm[k] = (i < n && a + i > 0 && (rv[k].x & 0xFFu)) ? q0_mass(prev) : 0.0;
         }
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
