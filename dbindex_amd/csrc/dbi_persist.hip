@@ -80,6 +80,10 @@ int read_header(FILE* f, dbi_index_header* hd, const char* path) {
 // engine index (+ optional ProteinCache definitions) -> file
 int index_save(dbi_handle* h, const char* path, const std::string* defs, const std::vector<uint64_t>* def_off) {
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    // the file is the bucketed store's index; unbucketed / window-filtered
+    // builds (SEARCH_UNINDEXED) are transient and carry other contents
+    if (!h->dp.buckets || h->dp.filter)
+        return set_error(DBI_E_STATE, "only a bucketed, unfiltered index can be saved");
     DBI_HIP(hipSetDevice(h->device));
     const uint64_t R = h->n_res, P = h->n_prot, U = h->stats.n_unique, K = h->stats.n_kept;
     std::vector<uint8_t> res(R);
@@ -134,6 +138,8 @@ int index_save(dbi_handle* h, const char* path, const std::string* defs, const s
 // file -> engine index; the proteome (and definitions) to the caller's vectors when given
 int index_load(dbi_handle* h, const char* path, std::vector<uint8_t>* res_out, std::vector<uint64_t>* off_out,
                std::string* defs_out, std::vector<uint64_t>* def_off_out) {
+    if (!h->dp.buckets || h->dp.filter)
+        return set_error(DBI_E_STATE, "a saved index loads into a bucketed, unfiltered engine only");
     File f;
     f.f = std::fopen(path, "rb");
     if (!f.f) return io_fail("cannot open index file", path);

@@ -82,3 +82,20 @@ def test_store_persist_and_reuse(tmp_path):
                       indexStore=DBIndexStoreHip(DBIndexSearchParams.trypsin(1), persist=True), database_name=name)
     other.init()
     assert not other.indexStore.indexExists()
+
+
+def test_unbucketed_or_filtered_index_is_not_saved(tmp_path):
+    from dbindex_amd import _native
+    from dbindex_amd.engine import Engine
+    pp = fasta.config("1k").slice(0, 50)
+    with Engine(DBIndexSearchParams.trypsin(2).to_c(), 0) as eng:
+        eng.set_bucket_drop(False)
+        eng.build(pp)
+        with pytest.raises(_native.DBIndexStoreException, match="bucketed"):
+            eng.save(str(tmp_path / "x.dbihip"))
+        eng.set_bucket_drop(True)
+        eng.build(pp)
+        eng.save(str(tmp_path / "x.dbihip"))
+        eng.set_bucket_drop(False)
+        with pytest.raises(_native.DBIndexStoreException, match="bucketed"):
+            eng.load(str(tmp_path / "x.dbihip"))
