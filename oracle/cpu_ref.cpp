@@ -4,7 +4,9 @@
 // written loop-for-loop from the Java sources under /root/reference
 // (paths below relative to src/main/java/edu/scripps/yates/dbindex/).
 // Used by tests/ as the parity checker, by bench.py as the `cpu_baseline`
-// ("port": single-threaded, like the reference), and by __graft_entry__.smoke().
+// ("port": single-threaded like the reference, and one thread per core over
+// protein ranges then row ranges — oref_set_threads), and by
+// __graft_entry__.smoke().
 //
 // Parity pinning: the reference is Java with no tests, no fixtures and no JDK
 // in this image, and its residue-mass table / cleavage rule live in the
@@ -29,8 +31,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
-#include <map>
 #include <string>
+#include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -140,19 +143,30 @@ void cut_seq(const dbi_params* p, const uint8_t* seq, int length, uint32_t prote
 // ---------------------------------------------------------------------------
 // Store: buckets -> rows keyed by (int)(mass*factor) -> merged peptide entries
 // ---------------------------------------------------------------------------
-struct Merged {
-    double mass;
-    uint32_t offset;
-    uint32_t length;
-    std::vector<uint32_t> pids;
-    uint64_t uid;  // position in the flattened (bucket, key, row-order) table
+// A row is one (bucket, key) pair: SQLiteMult routes a peptide to bucket
+// (int)m / BUCKET_MASS_RANGE (:215-217) and SQLiteByte appends it to the row
+// of key (int)(m*factor) in that bucket's database (Byte:185-226).  Both are
+// monotone in m, so (bucket, key) rows in lexicographic order are the rows of
+// bucket 0, 1, ... each in rowid (= key) order.  Merged entries are stored
+// flattened in that order: unique id = position (uid).
+struct RowRef {
+    int32_t bucket;
+    int32_t key;
+    uint64_t ub, ue;  // uids [ub, ue)
 };
 
-struct Row {
-    int32_t key;
-    std::vector<Occ> recs;        // insertion order (Byte.updateCachedData appends)
-    std::vector<Merged> merged;   // after getMergedData
-};
+int g_threads = 1;  // oref_set_threads: worker threads of build / query_batch
+
+template <typename F>
+void parallel_for(int nt, F&& f) {
+    if (nt <= 1) {
+        f(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&f, t] { f(t); });
+    for (auto& x : th) x.join();
+}
 
 }  // namespace
 
@@ -160,26 +174,23 @@ struct oref_index {
     dbi_params p;
     std::vector<uint8_t> residues;
     std::vector<uint64_t> off;
-    std::vector<Occ> occ;  // all INCLUDE'd occurrences, insertion order
     uint64_t n_total = 0, n_dropped = 0;
-    // buckets[b] : key -> row (std::map keeps ascending key = rowid order)
-    std::vector<std::map<int32_t, Row>> buckets;
-    std::vector<const Merged*> flat;  // uid -> entry
+    // unique table in (bucket, key, row) order + occurrence CSR
+    std::vector<double> umass;
+    std::vector<uint32_t> upid, uoff, ulen;
+    std::vector<uint64_t> occ_off;  // U + 1
+    std::vector<uint32_t> occ_pid;
+    std::vector<RowRef> rows;                // lexicographic (bucket, key)
+    std::vector<uint64_t> bucket_rows;       // rows of bucket b: [bucket_rows[b], bucket_rows[b+1])
     double build_seconds = 0;
 };
 
 namespace {
 
-std::string pep_string(const oref_index* ix, uint32_t pid, uint32_t off, uint32_t len) {
-    // ProteinCache.getPeptideSequence (ProteinCache.java:112-127)
-    const uint8_t* s = ix->residues.data() + ix->off[pid] + off;
-    return std::string((const char*)s, len);
-}
-
 // Pinned tie-break between different peptides of bit-identical mass
 // (semantics A7): the 32-bit FNV-1a of the peptide string folded
 // to 16 bits, then first appearance.
-uint16_t peptide_tag(const std::string& s) {
+uint16_t peptide_tag(std::string_view s) {
     uint32_t h = 2166136261u;
     for (unsigned char c : s) {
         h ^= c;
@@ -188,63 +199,168 @@ uint16_t peptide_tag(const std::string& s) {
     return (uint16_t)((h >> 16) ^ (h & 0xFFFFu));
 }
 
-// DBIndexStoreSQLiteByteIndexMerge.getMergedData (:620-719).  The reference
-// groups through a THashMap (iteration order unspecified) and then stable-sorts
-// by mass (IndexedSeqMerged.compareTo); we pin the order of equal-mass groups to
-// (16-bit FNV-1a tag of the string, first appearance) (semantics A7).
-void merge_row(const oref_index* ix, Row& row) {
-    std::unordered_map<std::string, size_t> where;
-    std::vector<Merged> groups;
-    std::vector<uint16_t> gtag;
-    where.reserve(row.recs.size() * 2);
-    for (const Occ& r : row.recs) {
-        std::string pep = pep_string(ix, r.pid, r.offset, r.length);
-        auto it = where.find(pep);
-        if (it == where.end()) {
-            gtag.push_back(peptide_tag(pep));
-            where.emplace(std::move(pep), groups.size());
-            // first occurrence keeps mass/offset/length; its protein id is first
-            groups.push_back(Merged{r.mass, r.offset, r.length, {r.pid}, 0});
-        } else {
-            groups[it->second].pids.push_back(r.pid);
-        }
-    }
-    // Collections.sort(sortedMerged) — stable, by mass (IndexedSeqMerged.compareTo),
-    // ties pinned to (tag, first appearance)
-    std::vector<size_t> ord(groups.size());
-    for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
-    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
-        if (groups[a].mass != groups[b].mass) return groups[a].mass < groups[b].mass;
-        return gtag[a] < gtag[b];
-    });
-    row.merged.clear();
-    row.merged.reserve(groups.size());
-    for (size_t i : ord) row.merged.push_back(std::move(groups[i]));
-    row.recs.clear();
-    row.recs.shrink_to_fit();
+int64_t row_of(const dbi_params* p, double mass) {
+    const int br = MAX_PRECURSOR_INT / p->index_factor;               // SQLiteMult:56
+    const int64_t bucket = java_d2i(mass) / br;                        // getBucketForMass :215-217
+    const int64_t key = java_d2i(mass * (double)p->mass_group_factor);  // Byte:187
+    return bucket * (int64_t(1) << 32) + key;
 }
 
-void build_store(oref_index* ix) {
+// One worker's slice of the store: every row whose (bucket, key) lies in
+// [lo, hi), merged, with uids local to the slice.
+struct Slice {
+    std::vector<double> umass;
+    std::vector<uint32_t> upid, uoff, ulen;
+    std::vector<uint64_t> ucnt;  // occurrences per merged entry
+    std::vector<uint32_t> occ_pid;
+    std::vector<RowRef> rows;
+};
+
+// DBIndexStoreSQLiteByteIndexMerge.getMergedData (:620-719) over the rows of
+// one slice.  Per row (records in insertion order, Byte.updateCachedData
+// appends): group by peptide string (ProteinCache.getPeptideSequence); the
+// first occurrence keeps mass/offset/length; proteinIds = every occurrence's
+// protein in insertion order, duplicates kept (:678-681); then
+// Collections.sort — stable, by mass (IndexedSeqMerged.compareTo) — with the
+// THashMap-order ties pinned to (tag, first appearance).
+void merge_slice(const oref_index* ix, const std::vector<Occ>& occ, int64_t lo, int64_t hi, Slice& out) {
     const dbi_params* p = &ix->p;
-    ix->buckets.assign(p->index_factor, {});
-    const int bucketRange = MAX_PRECURSOR_INT / p->index_factor;
-    for (const Occ& o : ix->occ) {
-        if (o.dropped) continue;
-        int bucket = java_d2i(o.mass) / bucketRange;
-        int32_t key = java_d2i(o.mass * (double)p->mass_group_factor);  // Byte:187
-        Row& row = ix->buckets[bucket][key];
-        row.key = key;
-        row.recs.push_back(o);
+    std::vector<std::pair<int64_t, uint32_t>> sel;  // (row, occurrence index)
+    for (uint32_t i = 0; i < (uint32_t)occ.size(); ++i) {
+        if (occ[i].dropped) continue;
+        const int64_t r = row_of(p, occ[i].mass);
+        if (r >= lo && r < hi) sel.push_back({r, i});
     }
-    for (auto& b : ix->buckets)
-        for (auto& kv : b) merge_row(ix, kv.second);
-    ix->flat.clear();
-    for (auto& b : ix->buckets)
-        for (auto& kv : b)
-            for (auto& m : kv.second.merged) {
-                m.uid = ix->flat.size();
-                ix->flat.push_back(&m);
+    std::sort(sel.begin(), sel.end());  // by row, insertion order inside
+    struct Group {
+        double mass;
+        uint32_t offset, length, first, n;
+        uint16_t tag;
+    };
+    std::unordered_map<std::string_view, uint32_t> where;
+    std::vector<std::string_view> gstr;
+    std::vector<Group> groups;
+    std::vector<uint32_t> gid, ord, gpos;
+    for (size_t a = 0; a < sel.size();) {
+        size_t b = a;
+        while (b < sel.size() && sel[b].first == sel[a].first) ++b;
+        // the THashMap of the row (a linear scan for short rows: same grouping)
+        const bool small = b - a <= 32;
+        if (!small) {
+            std::unordered_map<std::string_view, uint32_t>().swap(where);
+            where.reserve(2 * (b - a));
+        }
+        groups.clear();
+        gstr.clear();
+        gid.clear();
+        for (size_t k = a; k < b; ++k) {
+            const Occ& r = occ[sel[k].second];
+            const uint8_t* s = ix->residues.data() + ix->off[r.pid] + r.offset;
+            const std::string_view pep((const char*)s, r.length);
+            uint32_t g = (uint32_t)groups.size();
+            if (small) {
+                for (uint32_t q = 0; q < gstr.size(); ++q)
+                    if (gstr[q] == pep) { g = q; break; }
+            } else {
+                auto it = where.find(pep);
+                if (it != where.end()) g = it->second;
+                else where.emplace(pep, g);
             }
+            if (g == groups.size()) {
+                gstr.push_back(pep);
+                groups.push_back(Group{r.mass, r.offset, r.length, r.pid, 1, peptide_tag(pep)});
+            } else {
+                groups[g].n++;
+            }
+            gid.push_back(g);
+        }
+        ord.resize(groups.size());
+        for (size_t g = 0; g < ord.size(); ++g) ord[g] = (uint32_t)g;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+            if (groups[x].mass != groups[y].mass) return groups[x].mass < groups[y].mass;
+            return groups[x].tag < groups[y].tag;
+        });
+        // occurrence slots of each group in sorted order
+        gpos.assign(groups.size(), 0);
+        uint64_t base = out.occ_pid.size();
+        for (uint32_t g : ord) {
+            gpos[g] = (uint32_t)(base - out.occ_pid.size());
+            base += groups[g].n;
+        }
+        const uint64_t ob = out.occ_pid.size();
+        out.occ_pid.resize(base);
+        for (size_t k = a; k < b; ++k) out.occ_pid[ob + gpos[gid[k - a]]++] = occ[sel[k].second].pid;
+        RowRef row;
+        row.bucket = (int32_t)(sel[a].first >> 32);
+        row.key = (int32_t)(sel[a].first - ((int64_t)row.bucket << 32));
+        row.ub = out.umass.size();
+        for (uint32_t g : ord) {
+            out.umass.push_back(groups[g].mass);
+            out.upid.push_back(groups[g].first);
+            out.uoff.push_back(groups[g].offset);
+            out.ulen.push_back(groups[g].length);
+            out.ucnt.push_back(groups[g].n);
+        }
+        row.ue = out.umass.size();
+        out.rows.push_back(row);
+        a = b;
+    }
+}
+
+void build_store(oref_index* ix, const std::vector<Occ>& occ) {
+    const dbi_params* p = &ix->p;
+    const int nt = std::max(1, g_threads);
+    // row splitters: quantiles of a strided sample (rows never straddle slices)
+    std::vector<int64_t> samp;
+    const size_t stride = std::max<size_t>(1, occ.size() / 65536);
+    for (size_t i = 0; i < occ.size(); i += stride)
+        if (!occ[i].dropped) samp.push_back(row_of(p, occ[i].mass));
+    std::sort(samp.begin(), samp.end());
+    std::vector<int64_t> cut(nt + 1);
+    cut[0] = INT64_MIN;
+    cut[nt] = INT64_MAX;
+    for (int t = 1; t < nt; ++t) cut[t] = samp.empty() ? INT64_MAX : samp[samp.size() * t / nt];
+    std::vector<Slice> sl(nt);
+    parallel_for(nt, [&](int t) { merge_slice(ix, occ, cut[t], cut[t + 1], sl[t]); });
+    // concatenate the slices (rows ascend across them)
+    std::vector<uint64_t> ub(nt + 1, 0), ob(nt + 1, 0);
+    for (int t = 0; t < nt; ++t) {
+        ub[t + 1] = ub[t] + sl[t].umass.size();
+        ob[t + 1] = ob[t] + sl[t].occ_pid.size();
+    }
+    const uint64_t U = ub[nt];
+    ix->umass.resize(U);
+    ix->upid.resize(U);
+    ix->uoff.resize(U);
+    ix->ulen.resize(U);
+    ix->occ_off.resize(U + 1);
+    ix->occ_pid.resize(ob[nt]);
+    parallel_for(nt, [&](int t) {
+        const Slice& s = sl[t];
+        std::copy(s.umass.begin(), s.umass.end(), ix->umass.begin() + ub[t]);
+        std::copy(s.upid.begin(), s.upid.end(), ix->upid.begin() + ub[t]);
+        std::copy(s.uoff.begin(), s.uoff.end(), ix->uoff.begin() + ub[t]);
+        std::copy(s.ulen.begin(), s.ulen.end(), ix->ulen.begin() + ub[t]);
+        std::copy(s.occ_pid.begin(), s.occ_pid.end(), ix->occ_pid.begin() + ob[t]);
+        uint64_t pos = ob[t];
+        for (size_t u = 0; u < s.ucnt.size(); ++u) {
+            ix->occ_off[ub[t] + u] = pos;
+            pos += s.ucnt[u];
+        }
+    });
+    ix->occ_off[U] = ob[nt];
+    ix->rows.clear();
+    for (int t = 0; t < nt; ++t)
+        for (RowRef r : sl[t].rows) {
+            r.ub += ub[t];
+            r.ue += ub[t];
+            ix->rows.push_back(r);
+        }
+    ix->bucket_rows.assign(p->index_factor + 1, 0);
+    for (int b = 0, r = 0; b <= p->index_factor; ++b) {
+        while (r < (int)ix->rows.size() && ix->rows[r].bucket < b) ++r;
+        ix->bucket_rows[b] = r;
+    }
 }
 
 // IndexMerge.getSequences(precMass, tolerance) for one bucket (:146-217)
@@ -258,14 +374,54 @@ void bucket_query(const oref_index* ix, int b, double precMass, double tolerance
     if (minMass < 0) minMass = 0;
     int32_t maxMass = java_d2i(maxMassF * f);
     // SELECT ... WHERE precursor_mass_key BETWEEN minMass AND maxMass (rowid order)
-    const auto& rows = ix->buckets[b];
-    for (auto it = rows.lower_bound(minMass); it != rows.end() && it->first <= maxMass; ++it) {
+    auto rb = ix->rows.begin() + ix->bucket_rows[b], re = ix->rows.begin() + ix->bucket_rows[b + 1];
+    auto it = std::lower_bound(rb, re, minMass, [](const RowRef& r, int32_t k) { return r.key < k; });
+    for (; it != re && it->key <= maxMass; ++it) {
         // parseAddPeptideInfo (:386-481): sorted by mass; > max -> break; < min -> skip
-        for (const Merged& m : it->second.merged) {
-            if (m.mass > maxMassF) break;
-            if (m.mass < minMassF) continue;
-            out.push_back(m.uid);
+        for (uint64_t u = it->ub; u < it->ue; ++u) {
+            const double m = ix->umass[u];
+            if (m > maxMassF) break;
+            if (m < minMassF) continue;
+            out.push_back(u);
         }
+    }
+}
+
+// DBIndexStoreSQLiteMult.getSequences(precMass, tolerance) (:315-350)
+void query_one(const oref_index* ix, double precMass, double tolerance, std::vector<uint64_t>& out) {
+    const int nb = ix->p.index_factor;
+    const int br = MAX_PRECURSOR_INT / nb;
+    double minMass = precMass - tolerance;
+    if (minMass < 0) minMass = 0;
+    const double maxMass = precMass + tolerance;
+    int b0 = java_d2i(minMass) / br, b1 = java_d2i(maxMass) / br;  // :226-242
+    if (!(b0 > nb - 1 || b1 > nb - 1)) {
+        for (int b = b0; b <= b1; ++b) bucket_query(ix, b, precMass, tolerance, out);
+    }
+}
+
+// cutSeq over proteins [0, n_prot) with worker threads on residue-balanced
+// protein ranges, concatenated in protein order = the reference's insertion order
+void digest_all(const dbi_params* p, const uint8_t* res, const uint64_t* off, uint64_t n_prot,
+                std::vector<Occ>& occ) {
+    const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, g_threads), n_prot));
+    std::vector<uint64_t> pb(nt + 1, n_prot);
+    pb[0] = 0;
+    for (int t = 1; t < nt; ++t)
+        pb[t] = (uint64_t)(std::lower_bound(off, off + n_prot + 1, off[n_prot] / nt * t) - off);
+    for (int t = 1; t <= nt; ++t) pb[t] = std::max(pb[t], pb[t - 1]);
+    std::vector<std::vector<Occ>> part(nt);
+    parallel_for(nt, [&](int t) {
+        for (uint64_t i = pb[t]; i < pb[t + 1]; ++i)
+            cut_seq(p, res + off[i], (int)(off[i + 1] - off[i]), (uint32_t)i, part[t]);
+    });
+    size_t n = 0;
+    for (auto& v : part) n += v.size();
+    occ.clear();
+    occ.reserve(n);
+    for (auto& v : part) {
+        occ.insert(occ.end(), v.begin(), v.end());
+        std::vector<Occ>().swap(v);
     }
 }
 
@@ -273,14 +429,17 @@ void bucket_query(const oref_index* ix, int b, double precMass, double tolerance
 
 extern "C" {
 
+// Worker threads of oref_build*, oref_digest and oref_query_batch (default 1:
+// the reference's single-threaded path).
+void oref_set_threads(int n) { g_threads = std::max(1, n); }
+
 // Digestion only: every INCLUDE'd occurrence in insertion order.
 // Returns count via *n; arrays may be NULL to query the count.
 int oref_digest(const dbi_params* p, const uint8_t* res, const uint64_t* off, uint64_t n_prot,
                 double* mass, uint32_t* pid, uint32_t* offset, uint32_t* length,
                 uint8_t* dropped, uint64_t cap, uint64_t* n) {
     std::vector<Occ> occ;
-    for (uint64_t i = 0; i < n_prot; ++i)
-        cut_seq(p, res + off[i], (int)(off[i + 1] - off[i]), (uint32_t)i, occ);
+    digest_all(p, res, off, n_prot, occ);
     *n = occ.size();
     if (!mass) return 0;
     if (cap < occ.size()) return DBI_E_INVALID;
@@ -294,6 +453,29 @@ int oref_digest(const dbi_params* p, const uint8_t* res, const uint64_t* off, ui
     return 0;
 }
 
+// totalSeqCount and bucket drops of cutSeq over every protein, without
+// keeping the occurrences (count-only streaming, BASELINE configs[4]).
+int oref_count(const dbi_params* p, const uint8_t* res, const uint64_t* off, uint64_t n_prot,
+               uint64_t* total, uint64_t* dropped) {
+    const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_threads, n_prot));
+    std::vector<uint64_t> tot(nt, 0), drop(nt, 0);
+    parallel_for(nt, [&](int t) {
+        std::vector<Occ> occ;
+        for (uint64_t i = n_prot * t / nt; i < n_prot * (t + 1) / nt; ++i) {
+            occ.clear();
+            cut_seq(p, res + off[i], (int)(off[i + 1] - off[i]), (uint32_t)i, occ);
+            tot[t] += occ.size();
+            for (const Occ& o : occ) drop[t] += o.dropped;
+        }
+    });
+    *total = *dropped = 0;
+    for (int t = 0; t < nt; ++t) {
+        *total += tot[t];
+        *dropped += drop[t];
+    }
+    return 0;
+}
+
 int oref_build(const dbi_params* p, const uint8_t* res, const uint64_t* off, uint64_t n_prot,
                oref_index** out) {
     if (p->index_factor <= 0) return DBI_E_INVALID;
@@ -302,11 +484,11 @@ int oref_build(const dbi_params* p, const uint8_t* res, const uint64_t* off, uin
     ix->p = *p;
     ix->off.assign(off, off + n_prot + 1);
     ix->residues.assign(res, res + off[n_prot]);
-    for (uint64_t i = 0; i < n_prot; ++i)
-        cut_seq(p, ix->residues.data() + off[i], (int)(off[i + 1] - off[i]), (uint32_t)i, ix->occ);
-    ix->n_total = ix->occ.size();
-    for (const Occ& o : ix->occ) ix->n_dropped += o.dropped;
-    build_store(ix);
+    std::vector<Occ> occ;
+    digest_all(p, ix->residues.data(), off, n_prot, occ);
+    ix->n_total = occ.size();
+    for (const Occ& o : occ) ix->n_dropped += o.dropped;
+    build_store(ix, occ);
     auto t1 = std::chrono::steady_clock::now();
     ix->build_seconds = std::chrono::duration<double>(t1 - t0).count();
     *out = ix;
@@ -324,14 +506,15 @@ int oref_build_occurrences(const dbi_params* p, const uint8_t* res, const uint64
     ix->off.assign(off, off + n_prot + 1);
     ix->residues.assign(res, res + off[n_prot]);
     const int bucketRange = MAX_PRECURSOR_INT / p->index_factor;
+    std::vector<Occ> occ;
     for (uint64_t i = 0; i < n_occ; ++i) {
         int bucket = java_d2i(mass[i]) / bucketRange;
         Occ o{mass[i], pid[i], offset[i], length[i], (uint32_t)(bucket > p->index_factor - 1)};
-        ix->occ.push_back(o);
+        occ.push_back(o);
     }
-    ix->n_total = ix->occ.size();
-    for (const Occ& o : ix->occ) ix->n_dropped += o.dropped;
-    build_store(ix);
+    ix->n_total = occ.size();
+    for (const Occ& o : occ) ix->n_dropped += o.dropped;
+    build_store(ix, occ);
     *out = ix;
     return 0;
 }
@@ -341,41 +524,28 @@ void oref_free(oref_index* ix) { delete ix; }
 double oref_build_seconds(const oref_index* ix) { return ix->build_seconds; }
 uint64_t oref_n_total(const oref_index* ix) { return ix->n_total; }
 uint64_t oref_n_dropped(const oref_index* ix) { return ix->n_dropped; }
-uint64_t oref_n_unique(const oref_index* ix) { return ix->flat.size(); }
+uint64_t oref_n_unique(const oref_index* ix) { return ix->umass.size(); }
 uint64_t oref_n_kept(const oref_index* ix) { return ix->n_total - ix->n_dropped; }
 
 // getNumberSequences(): number of rows summed over buckets (SQLiteMult:182-192)
-uint64_t oref_n_keys(const oref_index* ix) {
-    uint64_t n = 0;
-    for (auto& b : ix->buckets) n += b.size();
-    return n;
-}
+uint64_t oref_n_keys(const oref_index* ix) { return ix->rows.size(); }
 
 // getEntryKeys(): rows of bucket 0, 1, ... in rowid order
 int oref_entry_keys(const oref_index* ix, int32_t* keys) {
-    uint64_t i = 0;
-    for (auto& b : ix->buckets)
-        for (auto& kv : b) keys[i++] = kv.first;
+    for (size_t i = 0; i < ix->rows.size(); ++i) keys[i] = ix->rows[i].key;
     return 0;
 }
 
 // Flattened unique table in (bucket, key, row) order + occurrence CSR.
 int oref_unique(const oref_index* ix, double* mass, uint32_t* pid, uint32_t* offset,
                 uint32_t* length, uint64_t* occ_off, uint32_t* occ_pid) {
-    uint64_t pos = 0;
-    for (size_t u = 0; u < ix->flat.size(); ++u) {
-        const Merged* m = ix->flat[u];
-        if (mass) mass[u] = m->mass;
-        if (pid) pid[u] = m->pids[0];
-        if (offset) offset[u] = m->offset;
-        if (length) length[u] = m->length;
-        if (occ_off) occ_off[u] = pos;
-        for (uint32_t q : m->pids) {
-            if (occ_pid) occ_pid[pos] = q;
-            ++pos;
-        }
-    }
-    if (occ_off) occ_off[ix->flat.size()] = pos;
+    const size_t U = ix->umass.size();
+    if (mass) std::copy(ix->umass.begin(), ix->umass.end(), mass);
+    if (pid) std::copy(ix->upid.begin(), ix->upid.end(), pid);
+    if (offset) std::copy(ix->uoff.begin(), ix->uoff.end(), offset);
+    if (length) std::copy(ix->ulen.begin(), ix->ulen.end(), length);
+    if (occ_off) std::copy(ix->occ_off.begin(), ix->occ_off.begin() + U + 1, occ_off);
+    if (occ_pid) std::copy(ix->occ_pid.begin(), ix->occ_pid.end(), occ_pid);
     return 0;
 }
 
@@ -384,20 +554,35 @@ int oref_unique(const oref_index* ix, double* mass, uint32_t* pid, uint32_t* off
 int oref_query(const oref_index* ix, double precMass, double tolerance, uint64_t* ids,
                uint64_t cap, uint64_t* n) {
     std::vector<uint64_t> out;
-    const int nb = ix->p.index_factor;
-    const int br = MAX_PRECURSOR_INT / nb;
-    double minMass = precMass - tolerance;
-    if (minMass < 0) minMass = 0;
-    const double maxMass = precMass + tolerance;
-    int b0 = java_d2i(minMass) / br, b1 = java_d2i(maxMass) / br;  // :226-242
-    if (!(b0 > nb - 1 || b1 > nb - 1)) {
-        for (int b = b0; b <= b1; ++b) bucket_query(ix, b, precMass, tolerance, out);
-    }
+    query_one(ix, precMass, tolerance, out);
     *n = out.size();
     if (ids) {
         if (cap < out.size()) return DBI_E_INVALID;
         std::copy(out.begin(), out.end(), ids);
     }
+    return 0;
+}
+
+// A batch of single-range queries as (first uid, count) per query — the
+// result of every query is a run of consecutive uids (rows ascend in uid
+// order and each row's entries are mass-sorted); DBI_E_STATE if one is not.
+int oref_query_batch(const oref_index* ix, const double* mass, const double* tol, uint64_t nq,
+                     uint64_t* first, uint64_t* count) {
+    const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_threads, nq / 4096 + 1));
+    std::vector<int> bad(nt, 0);
+    parallel_for(nt, [&](int t) {
+        std::vector<uint64_t> out;
+        for (uint64_t i = nq * t / nt; i < nq * (t + 1) / nt; ++i) {
+            out.clear();
+            query_one(ix, mass[i], tol[i], out);
+            count[i] = out.size();
+            first[i] = out.empty() ? 0 : out[0];
+            for (size_t k = 1; k < out.size(); ++k)
+                if (out[k] != out[0] + k) bad[t] = 1;
+        }
+    });
+    for (int b : bad)
+        if (b) return DBI_E_STATE;
     return 0;
 }
 
@@ -456,9 +641,9 @@ int oref_query_ranges(const oref_index* ix, const double* mass, const double* to
         // integer statements, more use an ad-hoc statement with double bounds.
         const size_t k = ranges.size();
         // rows selected by the OR of BETWEEN clauses over the integer key
-        const auto& rows = ix->buckets[b];
-        for (auto it = rows.begin(); it != rows.end(); ++it) {
-            const int32_t key = it->first;
+        for (uint64_t ri = ix->bucket_rows[b]; ri < ix->bucket_rows[b + 1]; ++ri) {
+            const RowRef& row = ix->rows[ri];
+            const int32_t key = row.key;
             bool sel = false;
             for (auto& r : ranges) {
                 if (k <= 24) {
@@ -471,16 +656,17 @@ int oref_query_ranges(const oref_index* ix, const double* mass, const double* to
             }
             if (!sel) continue;
             // parseAddPeptideInfo(data, ret, minMasses, maxMasses) (:494-600)
-            for (const Merged& m : it->second.merged) {
+            for (uint64_t u = row.ub; u < row.ue; ++u) {
+                const double m = ix->umass[u];
                 bool greaterThanMax = true, qualifies = false;
                 for (auto& r : ranges) {
-                    if (m.mass < r.second) greaterThanMax = false;
-                    if (m.mass >= r.first && m.mass <= r.second) qualifies = true;
+                    if (m < r.second) greaterThanMax = false;
+                    if (m >= r.first && m <= r.second) qualifies = true;
                     if (qualifies) break;
                 }
                 if (greaterThanMax && !qualifies) break;
                 if (!qualifies) continue;
-                out.push_back(m.uid);
+                out.push_back(u);
             }
         }
     }

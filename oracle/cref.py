@@ -50,8 +50,31 @@ def lib():
         L.oref_calculate_mass.restype = ctypes.c_double
         L.oref_tolerance_in_dalton.argtypes = [ctypes.c_double, ctypes.c_double]
         L.oref_tolerance_in_dalton.restype = ctypes.c_double
+        L.oref_set_threads.argtypes = [ctypes.c_int]
+        L.oref_count.argtypes = [P, P, P, ctypes.c_uint64, U64, U64]
+        L.oref_query_batch.argtypes = [P, P, P, ctypes.c_uint64, P, P]
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> None:
+    """Worker threads of the oracle's build, digest and batched query (1 = the
+    reference's single-threaded path; results do not depend on it)."""
+    lib().oref_set_threads(int(n))
+
+
+class threads:
+    """Context manager: ``with cref.threads(16): ...``, back to 1 afterwards."""
+
+    def __init__(self, n: int):
+        self.n = n
+
+    def __enter__(self):
+        set_threads(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        set_threads(1)
 
 
 def _ptr(a: np.ndarray):
@@ -84,6 +107,16 @@ def digest(cparams, residues: np.ndarray, offsets: np.ndarray) -> Digest:
                            _ptr(out.dropped), k, ctypes.byref(n))
         assert rc == 0
     return out
+
+
+def count(cparams, residues: np.ndarray, offsets: np.ndarray):
+    """(totalSeqCount, bucket drops) of cutSeq over every protein (oref_count)."""
+    residues = np.ascontiguousarray(residues, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    t, d = ctypes.c_uint64(), ctypes.c_uint64()
+    lib().oref_count(ctypes.byref(cparams), _ptr(residues), _ptr(offsets), offsets.shape[0] - 1,
+                     ctypes.byref(t), ctypes.byref(d))
+    return t.value, d.value
 
 
 class Index:
@@ -180,15 +213,14 @@ class Index:
         return ids
 
     def query_batch(self, masses, tols):
-        """(first, count) per query, as the engine reports them (contiguous ranges)."""
-        first = np.zeros(len(masses), np.uint64)
-        count = np.zeros(len(masses), np.uint64)
-        for i, (m, t) in enumerate(zip(masses, tols)):
-            ids = self.query(float(m), float(t))
-            count[i] = ids.shape[0]
-            if ids.shape[0]:
-                first[i] = ids[0]
-                assert np.all(np.diff(ids.astype(np.int64)) == 1), "non-contiguous oracle result"
+        """(first, count) per query, as the engine reports them (contiguous
+        ranges; first = 0 when count = 0), oref_query_batch."""
+        m = np.ascontiguousarray(masses, np.float64)
+        t = np.ascontiguousarray(tols, np.float64)
+        first = np.zeros(m.shape[0], np.uint64)
+        count = np.zeros(m.shape[0], np.uint64)
+        rc = lib().oref_query_batch(self.h, _ptr(m), _ptr(t), m.shape[0], _ptr(first), _ptr(count))
+        assert rc == 0, "non-contiguous oracle result"
         return first, count
 
 
