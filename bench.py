@@ -16,7 +16,7 @@ range.  The residues of every shard are all-gathered into each GPU's HBM once,
 before the timed region (input staging: the owner merge compares peptide
 strings of any shard).  --no-merge: independent shard-local indexes instead.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config swissprot|human|1k]
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config swissprot|human|1k|semi|trembl]
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -324,6 +324,9 @@ def main() -> None:
         dm, dt = DeviceBuffer.from_numpy(m, dev), DeviceBuffer.from_numpy(tol, dev)
         df, dc = DeviceBuffer(8 * nq, dev), DeviceBuffer(8 * nq, dev)
         synchronize(dev)
+        t_q = time.perf_counter()
+        eng.query_prepare()  # directory of the index of the last timed build
+        qdir_ms = 1e3 * (time.perf_counter() - t_q)
         for _ in range(3):
             eng.query_device(dm.ptr, dt.ptr, nq, df.ptr, dc.ptr)
         synchronize(dev)
@@ -334,22 +337,24 @@ def main() -> None:
         synchronize(dev)
         tq = time.perf_counter() - tq
         hits = int(dc.download(np.uint64, nq).sum())
-        qps = dict(value=nq * reps / tq, unit="queries/s", queries=nq, tol_ppm=20.0,
-                   avg_hits=hits / nq, index="the build above")
+        qps = dict(value=nq * reps / tq, unit="queries/s", queries=nq, tol_ppm=20.0, avg_hits=hits / nq,
+                   kind="range lookup: (first, count) of every window's run of unique ids (the complete "
+                        "answer over the mass-sorted unique table), device in/out",
+                   index="the build above", qdir_build_ms=qdir_ms)
+        # hit-producing leg: every hit's unique id and protein ids materialised in HBM
+        # (at most ~40 GB of hit buffers: semi-tryptic windows hold ~20x more hits)
+        nq_h = int(min(nq, nq * 40e9 / max(12.0 * hits, 1.0)))
+        hq = hits_leg(eng, dm, dt, max(nq_h, 1))
+        qps["materialised"] = hq
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # reference-semantics CPU restatement (oracle/cpu_ref.cpp), single thread
-        # like the reference; bounded sample of the same workload
-        from oracle import cref
+        # reference-semantics CPU restatement (oracle/cpu_ref.cpp) on a bounded
+        # sample of the same workload: one thread per host core (protein ranges,
+        # then row ranges) and single-threaded like the reference
         sample = pp.slice(0, min(cpu_sample, pp.n_proteins))
-        t1 = time.perf_counter()
-        oix = cref.Index(prm.to_c(), sample.residues, sample.offsets)
-        t1 = time.perf_counter() - t1
-        cpu = dict(value=oix.n_total / t1, unit="peptides indexed/s", cores=1, kind="port",
-                   sample=f"{sample.n_proteins} proteins / {sample.n_residues} residues of the same "
-                          f"workload ({oix.n_total} peptides, {t1:.1f}s); host CPU: {cpu_model()}",
-                   seconds=t1)
+        cpu = cpu_baseline_legs(prm, sample)
+        cpu["sample_parity"] = sample_parity(prm, sample, cpu.pop("_oix"), dev)
 
     traffic, traffic_src = pmc_traffic(dom["kernel"]) if dom else (None, None)
     if rank == 0:
@@ -407,6 +412,82 @@ def main() -> None:
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_threads() -> int:
+    """Host threads for the all-cores CPU leg: the cores this process may use
+    (OMP_NUM_THREADS caps it: the GPU box's CPU share), one per core."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else max(1, n)
+
+
+def cpu_baseline_legs(prm, sample) -> dict:
+    from oracle import cref
+    nthreads = host_threads()
+    cp = prm.to_c()
+    with cref.threads(nthreads):
+        t_all = time.perf_counter()
+        oix = cref.Index(cp, sample.residues, sample.offsets)
+        t_all = time.perf_counter() - t_all
+    t_one = time.perf_counter()
+    one = cref.Index(cp, sample.residues, sample.offsets)
+    t_one = time.perf_counter() - t_one
+    assert one.n_total == oix.n_total and one.n_unique == oix.n_unique
+    del one
+    desc = (f"{sample.n_proteins} proteins / {sample.n_residues} residues of the same workload "
+            f"({oix.n_total} peptides)")
+    return dict(value=oix.n_total / t_all, unit="peptides indexed/s", cores=nthreads, kind="port",
+                sample=f"{desc}: oracle/cpu_ref.cpp restatement, digest over protein ranges + merge over row "
+                       f"ranges, {nthreads} threads, {t_all:.2f}s",
+                seconds=t_all, nproc=os.cpu_count(), host_cpu=cpu_model(),
+                single_core=dict(value=oix.n_total / t_one, unit="peptides indexed/s", cores=1, kind="port",
+                                 seconds=t_one, sample=f"{desc}, one thread (the reference's threading)"),
+                _oix=oix)
+
+
+def sample_parity(prm, sample, oix, dev: int) -> dict:
+    """The CPU leg's sample built on the GPU too: counts and a digest of every
+    index array equal the oracle's (bit-exact)."""
+    import hashlib
+    from dbindex_amd.engine import Engine
+
+    def digest(d):
+        h = hashlib.sha256()
+        for k in ("mass", "prot_id", "offset", "length", "occ_off", "occ_prot"):
+            a = np.ascontiguousarray(d[k])
+            h.update(a.view(np.uint64).tobytes() if k == "mass" else a.astype(np.uint64).tobytes())
+        return h.hexdigest()[:16]
+
+    with Engine(prm, device=dev) as e2:
+        st = e2.build(sample)
+        g = digest(e2.export())
+    o = digest(oix.unique())
+    same = (st.n_total == oix.n_total and st.n_unique == oix.n_unique and st.n_keys == oix.n_keys and g == o)
+    return dict(ok=bool(same), gpu_sha=g, oracle_sha=o, n_total=st.n_total, n_unique=st.n_unique)
+
+
+def hits_leg(eng, dm, dt, nq: int, reps: int = 5) -> dict:
+    """1M +-20 ppm windows through dbi_query_hits_device: per query its unique
+    ids, per hit its protein ids (occurrence CSR), all written to HBM.
+    Algorithmic bytes: 32 Q (mass + tol in, two u64 offsets
+    out) + 12 H (id out, protein-list start out, occ_off read) + 8 Ho (protein
+    id read + written), Ho = protein ids of all hits."""
+    from dbindex_amd._native import synchronize
+    r = eng.query_hits_device(dm.ptr, dt.ptr, nq)  # warm: grows the buffers
+    synchronize(eng.device)
+    t = time.perf_counter()
+    for _ in range(reps):
+        r = eng.query_hits_device(dm.ptr, dt.ptr, nq)
+    synchronize(eng.device)
+    t = (time.perf_counter() - t) / reps
+    H, Ho = r.n_hits, r.n_prot_ids
+    alg = 32.0 * nq + 12.0 * H + 8.0 * Ho
+    return dict(value=nq / t, unit="queries/s", ms_per_batch=1e3 * t, queries=nq, hits=H, protein_ids=Ho,
+                kind="materialised: unique ids + protein ids of every hit in HBM (dbi_query_hits_device)",
+                roofline=dict(bound="hbm", alg_bytes=alg, formula="32Q + 12H + 8Ho",
+                              achieved=alg / t / 1e9, peak=HBM_PEAK_GBPS, unit="GB/s",
+                              frac=alg / t / 1e9 / HBM_PEAK_GBPS))
 
 
 def run_trembl(args, world: int, rank: int, dev: int, dist) -> None:
@@ -482,19 +563,29 @@ def run_trembl(args, world: int, rank: int, dev: int, dist) -> None:
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cref
-        sample = fasta.synth_proteome(seed, 0, 12000, 0, tables)
+        sample = fasta.synth_proteome(seed, 0, 120000, 0, tables)  # ~10 s of single-core count
+        cp = prm.to_c()
+        nthreads = host_threads()
+        with cref.threads(nthreads):
+            t_all = time.perf_counter()
+            want = cref.count(cp, sample.residues, sample.offsets)[0]
+            t_all = time.perf_counter() - t_all
         t1 = time.perf_counter()
-        dg = cref.digest(prm.to_c(), sample.residues, sample.offsets)
+        want1 = cref.count(cp, sample.residues, sample.offsets)[0]
         t1 = time.perf_counter() - t1
-        cpu = dict(value=dg.mass.shape[0] / t1, unit="peptides indexed/s", cores=1, kind="port",
-                   sample=f"cutSeq digest (oracle/cpu_ref.cpp, occurrences materialised) of {sample.n_proteins} proteins / "
-                          f"{sample.n_residues} residues of the same proteome ({dg.mass.shape[0]} peptides, "
-                          f"{t1:.1f}s); host CPU: {cpu_model()}", seconds=t1)
+        assert want1 == want
+        desc = (f"cutSeq count (oracle/cpu_ref.cpp) of {sample.n_proteins} proteins / {sample.n_residues} residues "
+                f"of the same proteome ({want} peptides)")
+        cpu = dict(value=want / t_all, unit="peptides indexed/s", cores=nthreads, kind="port",
+                   sample=f"{desc}, {nthreads} threads over protein ranges, {t_all:.2f}s", seconds=t_all,
+                   nproc=os.cpu_count(), host_cpu=cpu_model(),
+                   single_core=dict(value=want / t1, unit="peptides indexed/s", cores=1, kind="port", seconds=t1,
+                                    sample=f"{desc}, one thread"))
         # the same sample counted on the GPU: totalSeqCount parity at this scale
         d_sr = DeviceBuffer.from_numpy(np.concatenate([sample.residues, np.zeros(16, np.uint8)]), dev)
         d_so = DeviceBuffer.from_numpy(sample.offsets.astype(np.uint64), dev)
         g = eng.count_device(d_sr.ptr, sample.n_residues, d_so.ptr, sample.n_proteins)[0]
-        cpu.update(gpu_count_same_sample=g, sample_parity=bool(g == dg.mass.shape[0]))
+        cpu.update(gpu_count_same_sample=g, sample_parity=bool(g == want))
     if rank == 0:
         ms = 1000.0 * elapsed / max(args.steps, 1)
         alg = res_all + 8.0 * (P + 1)  # residues + offsets read once per step (count mode writes nothing)

@@ -70,6 +70,11 @@ class DbiDeviceIndex(ctypes.Structure):
                 ("n_kept", c_uint64)]
 
 
+class DbiDeviceHits(ctypes.Structure):
+    _fields_ = [("row", c_void_p), ("ids", c_void_p), ("occ_row", c_void_p), ("hit_occ", c_void_p),
+                ("prot", c_void_p), ("nq", c_uint64), ("n_hits", c_uint64), ("n_prot_ids", c_uint64)]
+
+
 class DbiSeqList(ctypes.Structure):
     _fields_ = [
         ("n", c_uint64), ("mass", POINTER(c_double)), ("seq_off", POINTER(c_uint64)),
@@ -93,6 +98,8 @@ SIGNATURES = [
     ("dbi_query_device", c_int, [P, P, P, c_uint64, P, P, P]),
     ("dbi_query_csr", c_int, [P, P, P, c_uint64, POINTER(POINTER(DbiQueryResult))]),
     ("dbi_query_result_free", None, [POINTER(DbiQueryResult)]),
+    ("dbi_query_prepare", c_int, [P]),
+    ("dbi_query_hits_device", c_int, [P, P, P, c_uint64, POINTER(DbiDeviceHits)]),
     ("dbi_peptides", c_int, [P, P, c_uint64, P, P, P, P, P, P]),
     ("dbi_occurrences", c_int, [P, c_uint64, c_uint64, P]),
     ("dbi_export", c_int, [P, P, P, P, P, P, P]),

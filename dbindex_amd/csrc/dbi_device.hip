@@ -2451,6 +2451,142 @@ hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, c
     return hipGetLastError();
 }
 
+// ---- hit materialisation (dbi_query_hits_device) ---------------------------------
+// The hits of one window are the consecutive unique ids [first, first+count)
+// (IndexMerge.parseAddPeptideInfo :386-481 walks them in mass order), and the
+// proteins of those peptides (the row blob's protein-id lists, :446-470) are
+// the consecutive occurrence slots [occ_off[first], occ_off[first+count]).
+// Per query: hits, proteins of its hits; per hit: its unique id and where its
+// protein list starts inside the query's.
+__global__ void k_hits_count(const uint64_t* __restrict__ first, const uint64_t* __restrict__ count,
+                             const uint32_t* __restrict__ occ_off, uint64_t nq, uint32_t* __restrict__ nh,
+                             uint32_t* __restrict__ no) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const uint64_t f = first[i], c = count[i];
+    nh[i] = (uint32_t)c;
+    no[i] = c ? occ_off[f + c] - occ_off[f] : 0u;
+}
+
+// exclusive scans of two u32 arrays into u64 offsets (+ totals), the same
+// three phases as launch_scan_u32
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan2_reduce(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint64_t n,
+               unsigned long long* __restrict__ sums) {
+    __shared__ unsigned long long tmp[SCAN_THREADS / 64 + 1];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK;
+    unsigned long long va = 0, vb = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * SCAN_THREADS + threadIdx.x;
+        if (i < n) { va += a[i]; vb += b[i]; }
+    }
+    const unsigned long long ta = block_sum<SCAN_THREADS, unsigned long long>(va, tmp);
+    __syncthreads();
+    const unsigned long long tb = block_sum<SCAN_THREADS, unsigned long long>(vb, tmp);
+    if (threadIdx.x == 0) {
+        sums[2 * blockIdx.x] = ta;
+        sums[2 * blockIdx.x + 1] = tb;
+    }
+}
+
+// one block: exclusive scan of the nb block sums (pairs) in place, totals to tot[0..1]
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan2_single(unsigned long long* __restrict__ sums, uint64_t nb, unsigned long long* __restrict__ tot) {
+    __shared__ unsigned long long tmp[SCAN_THREADS / 64 + 1];
+    for (int h = 0; h < 2; ++h) {
+        unsigned long long carry = 0;
+        for (uint64_t base = 0; base < nb; base += SCAN_THREADS) {
+            const uint64_t i = base + threadIdx.x;
+            const unsigned long long v = i < nb ? sums[2 * i + h] : 0ull;
+            unsigned long long t;
+            const unsigned long long e = block_excl_scan<SCAN_THREADS, unsigned long long>(v, tmp, t);
+            if (i < nb) sums[2 * i + h] = carry + e;
+            carry += t;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) tot[h] = carry;
+    }
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan2_down(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint64_t n,
+             const unsigned long long* __restrict__ sums, const unsigned long long* __restrict__ tot,
+             uint64_t* __restrict__ oa, uint64_t* __restrict__ ob) {
+    __shared__ unsigned long long tmp[SCAN_THREADS / 64 + 1];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK;
+    uint32_t va[SCAN_ITEMS], vb[SCAN_ITEMS];
+    unsigned long long la = 0, lb = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)threadIdx.x * SCAN_ITEMS + k;
+        va[k] = i < n ? a[i] : 0u;
+        vb[k] = i < n ? b[i] : 0u;
+        la += va[k];
+        lb += vb[k];
+    }
+    unsigned long long t;
+    unsigned long long ra = block_excl_scan<SCAN_THREADS, unsigned long long>(la, tmp, t) + sums[2 * blockIdx.x];
+    __syncthreads();
+    unsigned long long rb = block_excl_scan<SCAN_THREADS, unsigned long long>(lb, tmp, t) + sums[2 * blockIdx.x + 1];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)threadIdx.x * SCAN_ITEMS + k;
+        if (i < n) { oa[i] = ra; ob[i] = rb; }
+        ra += va[k];
+        rb += vb[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) { oa[n] = tot[0]; ob[n] = tot[1]; }
+}
+
+size_t scan2_tmp_elems(uint64_t n) { return 2 * (size_t)((n + SCAN_CHUNK - 1) / SCAN_CHUNK) + 2; }
+
+hipError_t launch_hits_offsets(const uint64_t* d_first, const uint64_t* d_count, const uint32_t* d_occ_off,
+                               uint64_t nq, uint32_t* d_nh, uint32_t* d_no, unsigned long long* d_sums,
+                               uint64_t* d_row, uint64_t* d_occ_row, unsigned long long* d_tot, hipStream_t s) {
+    const uint64_t nb = std::max<uint64_t>((nq + SCAN_CHUNK - 1) / SCAN_CHUNK, 1);
+    DBI_LAUNCH(k_hits_count, dim3((uint32_t)((nq + 255) / 256 + 1)), dim3(256), 0, s, d_first, d_count, d_occ_off,
+               nq, d_nh, d_no);
+    DBI_LAUNCH(k_scan2_reduce, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_nh, d_no, nq, d_sums);
+    DBI_LAUNCH(k_scan2_single, dim3(1), dim3(SCAN_THREADS), 0, s, d_sums, nb, d_tot);
+    DBI_LAUNCH(k_scan2_down, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_nh, d_no, nq, d_sums, d_tot, d_row,
+               d_occ_row);
+    return hipGetLastError();
+}
+
+// One block per query (grid-stride): the ids of its hits, each hit's protein
+// list start relative to the query's, and the protein ids themselves — all
+// three contiguous runs, written with consecutive lanes on consecutive words.
+constexpr uint32_t HITS_THREADS = 256;
+__global__ void __launch_bounds__(HITS_THREADS)
+k_hits_expand(const uint64_t* __restrict__ first, const uint64_t* __restrict__ count,
+              const uint64_t* __restrict__ row, const uint64_t* __restrict__ occ_row,
+              const uint32_t* __restrict__ occ_off, const uint32_t* __restrict__ occ_pid, uint64_t nq,
+              uint32_t* __restrict__ ids, uint32_t* __restrict__ hit_occ, uint32_t* __restrict__ prot) {
+    for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const uint64_t c = count[q];
+        if (c == 0) continue;
+        const uint32_t f = (uint32_t)first[q];
+        const uint64_t r = row[q], orow = occ_row[q];
+        const uint32_t o0 = occ_off[f], o1 = occ_off[f + c];
+        for (uint32_t k = threadIdx.x; k < c; k += HITS_THREADS) {
+            ids[r + k] = f + k;
+            hit_occ[r + k] = occ_off[f + k] - o0;
+        }
+        for (uint32_t k = threadIdx.x; k < o1 - o0; k += HITS_THREADS) prot[orow + k] = occ_pid[o0 + k];
+    }
+}
+
+hipError_t launch_hits_expand(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
+                              const uint64_t* d_occ_row, const uint32_t* d_occ_off, const uint32_t* d_occ_pid,
+                              uint64_t nq, uint32_t* d_ids, uint32_t* d_hit_occ, uint32_t* d_prot, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    const uint32_t g = (uint32_t)std::min<uint64_t>(nq, 256u * 64u);  // 64 blocks per CU, grid-stride
+    DBI_LAUNCH(k_hits_expand, dim3(g), dim3(HITS_THREADS), 0, s, d_first, d_count, d_row, d_occ_row, d_occ_off,
+               d_occ_pid, nq, d_ids, d_hit_occ, d_prot);
+    return hipGetLastError();
+}
+
 // host-supplied occurrences -> records (DBIndexStore.addSequence path; the
 // host checked 1 <= mass < 65536 and that every occurrence lies in its protein)
 __global__ void k_occ_to_recs(const double* __restrict__ mass, const uint32_t* __restrict__ pid,

@@ -143,6 +143,10 @@ struct dbi_handle {
     bool inputs_resident = false;       // res/poff hold the last host build's inputs (dbi_rebuild)
     DevBuf<double> q_mass, q_tol;
     DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
+    DevBuf<uint32_t> h_nh, h_no, h_ids, h_hocc, h_prot;  // dbi_query_hits_device
+    DevBuf<uint64_t> h_row, h_orow;
+    DevBuf<unsigned long long> h_sums;
+    DevBuf<uint64_t> kr_scratch;        // engine_key_range result (2 words)
     DevBuf<double> g_mass;
     DevBuf<uint32_t> g_pid, g_off, g_len;
     DevBuf<uint64_t> g_b, g_e;

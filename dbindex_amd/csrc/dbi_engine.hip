@@ -522,6 +522,8 @@ void dbi_close(dbi_handle* h) {
     h->q_mass.release(); h->q_tol.release(); h->q_first.release(); h->q_count.release(); h->q_row.release();
     h->q_ids.release(); h->g_mass.release(); h->g_pid.release(); h->g_off.release(); h->g_len.release();
     h->g_b.release(); h->g_e.release();
+    h->h_nh.release(); h->h_no.release(); h->h_ids.release(); h->h_hocc.release(); h->h_prot.release();
+    h->h_row.release(); h->h_orow.release(); h->h_sums.release(); h->kr_scratch.release();
     for (auto& ev : h->evpool)
         if (ev) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -663,6 +665,50 @@ int dbi_query(dbi_handle* h, const double* mass, const double* tol, uint64_t nq,
     return 0;
 }
 
+int dbi_query_prepare(dbi_handle* h) {
+    if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    DBI_HIP(hipSetDevice(h->device));
+    return ensure_qdir(h, h->stream);
+}
+
+int dbi_query_hits_device(dbi_handle* h, const double* d_mass, const double* d_tol, uint64_t nq,
+                          dbi_device_hits* out) {
+    if (!h || !out || (nq && (!d_mass || !d_tol))) return set_error(DBI_E_INVALID, "NULL argument");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
+    if (!h->built) return set_error(DBI_E_STATE, "index not built");
+    DBI_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    int rc;
+    if ((rc = h->q_first.ensure(std::max<uint64_t>(nq, 1))) || (rc = h->q_count.ensure(std::max<uint64_t>(nq, 1))) ||
+        (rc = h->h_nh.ensure(std::max<uint64_t>(nq, 1))) || (rc = h->h_no.ensure(std::max<uint64_t>(nq, 1))) ||
+        (rc = h->h_row.ensure(nq + 1)) || (rc = h->h_orow.ensure(nq + 1)) ||
+        (rc = h->h_sums.ensure(scan2_tmp_elems(nq))))
+        return rc;
+    if ((rc = dbi_query_device(h, d_mass, d_tol, nq, h->q_first.p, h->q_count.p, s))) return rc;
+    DBI_HIP(launch_hits_offsets(h->q_first.p, h->q_count.p, h->occ_off.p, nq, h->h_nh.p, h->h_no.p, h->h_sums.p,
+                                h->h_row.p, h->h_orow.p, h->h_sums.p + scan2_tmp_elems(nq) - 2, s));
+    unsigned long long tot[2];
+    DBI_HIP(hipMemcpyAsync(tot, h->h_sums.p + scan2_tmp_elems(nq) - 2, sizeof(tot), hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    if ((rc = h->h_ids.ensure(std::max<uint64_t>(tot[0], 1))) || (rc = h->h_hocc.ensure(std::max<uint64_t>(tot[0], 1))) ||
+        (rc = h->h_prot.ensure(std::max<uint64_t>(tot[1], 1))))
+        return rc;
+    DBI_HIP(launch_hits_expand(h->q_first.p, h->q_count.p, h->h_row.p, h->h_orow.p, h->occ_off.p, h->occ_pid.p, nq,
+                               h->h_ids.p, h->h_hocc.p, h->h_prot.p, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    out->row = h->h_row.p;
+    out->ids = h->h_ids.p;
+    out->occ_row = h->h_orow.p;
+    out->hit_occ = h->h_hocc.p;
+    out->prot = h->h_prot.p;
+    out->nq = nq;
+    out->n_hits = tot[0];
+    out->n_prot_ids = tot[1];
+    return 0;
+}
+
 int dbi_query_csr(dbi_handle* h, const double* mass, const double* tol, uint64_t nq, dbi_query_result** out) {
     if (!out || !h) return set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
@@ -674,6 +720,10 @@ int dbi_query_csr(dbi_handle* h, const double* mass, const double* tol, uint64_t
     if (!r) return set_error(DBI_E_OOM, "calloc");
     r->nq = nq;
     r->row_ptr = (uint64_t*)std::malloc(8 * (nq + 1));
+    if (!r->row_ptr) {
+        dbi_query_result_free(r);
+        return set_error(DBI_E_OOM, "malloc");
+    }
     uint64_t tot = 0;
     for (uint64_t i = 0; i < nq; ++i) {
         r->row_ptr[i] = tot;
@@ -913,14 +963,16 @@ int dbi_device_view(dbi_handle* h, dbi_device_index* out) {
 // ---- internal accessors used by the store mirror (dbi_store.cpp) ----------------
 namespace dbi {
 int engine_key_range(dbi_handle* h, int32_t klo, int32_t khi, uint64_t* b, uint64_t* e) {
+    // a query-side call: same lock as dbi_query* (shared stream), own scratch
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     if (!h->built) return set_error(DBI_E_STATE, "index not built");
     DBI_HIP(hipSetDevice(h->device));
     int rc;
-    if ((rc = h->q_first.ensure(2))) return rc;
+    if ((rc = h->kr_scratch.ensure(2))) return rc;
     DBI_HIP(launch_key_range(h->umass.p, (uint32_t)h->stats.n_unique, h->params.mass_group_factor, klo, khi,
-                             h->q_first.p, h->stream));
+                             h->kr_scratch.p, h->stream));
     uint64_t r[2];
-    DBI_HIP(hipMemcpyAsync(r, h->q_first.p, 16, hipMemcpyDeviceToHost, h->stream));
+    DBI_HIP(hipMemcpyAsync(r, h->kr_scratch.p, 16, hipMemcpyDeviceToHost, h->stream));
     DBI_HIP(hipStreamSynchronize(h->stream));
     *b = r[0];
     *e = r[1];

@@ -302,6 +302,15 @@ hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const
                               const uint32_t* d_len, const uint32_t* d_poff, const uint8_t* d_res, uint64_t n,
                               uint64_t n_prot, Rec* d_out, Counters* d_ctr, hipStream_t s);
 hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s);
+// query hits: per-query hit / protein-id counts -> u64 offsets (row, occ_row:
+// nq + 1 entries each, totals also at tot[0..1]); sums: scan2_tmp_elems(nq)
+size_t scan2_tmp_elems(uint64_t n);
+hipError_t launch_hits_offsets(const uint64_t* d_first, const uint64_t* d_count, const uint32_t* d_occ_off,
+                               uint64_t nq, uint32_t* d_nh, uint32_t* d_no, unsigned long long* d_sums,
+                               uint64_t* d_row, uint64_t* d_occ_row, unsigned long long* d_tot, hipStream_t s);
+hipError_t launch_hits_expand(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
+                              const uint64_t* d_occ_row, const uint32_t* d_occ_off, const uint32_t* d_occ_pid,
+                              uint64_t nq, uint32_t* d_ids, uint32_t* d_hit_occ, uint32_t* d_prot, hipStream_t s);
 hipError_t launch_expand_csr(const uint64_t* d_first, const uint64_t* d_count, const uint64_t* d_row,
                              uint64_t nq, uint64_t* d_ids, hipStream_t s);
 

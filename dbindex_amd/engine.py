@@ -14,7 +14,7 @@ from typing import Optional, Tuple
 import numpy as np
 
 from . import _native
-from ._native import DbiDeviceIndex, DbiQueryResult, DbiStats, check
+from ._native import DbiDeviceHits, DbiDeviceIndex, DbiQueryResult, DbiStats, check
 from .fasta import PackedProteins
 from .params import DBIndexSearchParams, DbiParams
 
@@ -143,6 +143,37 @@ class Engine:
         check(_native.lib().dbi_query_device(self.h, ctypes.c_void_p(d_mass), ctypes.c_void_p(d_tol), nq,
                                              ctypes.c_void_p(d_first), ctypes.c_void_p(d_count),
                                              ctypes.c_void_p(stream) if stream else None))
+
+    def query_prepare(self) -> None:
+        """Builds the query directory of the current index now (dbi_query_prepare)."""
+        check(_native.lib().dbi_query_prepare(self.h))
+
+    def query_hits_device(self, d_mass: int, d_tol: int, nq: int) -> DbiDeviceHits:
+        """Materialised hits in HBM (dbi_query_hits_device): per query its unique
+        ids and their protein ids; device pointers owned by the engine."""
+        out = DbiDeviceHits()
+        check(_native.lib().dbi_query_hits_device(self.h, ctypes.c_void_p(d_mass), ctypes.c_void_p(d_tol), nq,
+                                                  ctypes.byref(out)))
+        return out
+
+    def query_hits(self, mass, tol):
+        """Host copy of query_hits_device for numpy inputs: dict(row, ids, occ_row,
+        hit_occ, prot)."""
+        m = np.ascontiguousarray(np.atleast_1d(mass), np.float64)
+        t = np.ascontiguousarray(np.broadcast_to(np.atleast_1d(tol), m.shape), np.float64)
+        dm, dt = _native.DeviceBuffer.from_numpy(m, self.device), _native.DeviceBuffer.from_numpy(t, self.device)
+        r = self.query_hits_device(dm.ptr, dt.ptr, m.shape[0])
+        out = {}
+        for name, ptr, dt_, n in (("row", r.row, np.uint64, r.nq + 1), ("ids", r.ids, np.uint32, r.n_hits),
+                                  ("occ_row", r.occ_row, np.uint64, r.nq + 1),
+                                  ("hit_occ", r.hit_occ, np.uint32, r.n_hits),
+                                  ("prot", r.prot, np.uint32, r.n_prot_ids)):
+            a = np.zeros(n, dt_)
+            if n:
+                check(_native.lib().dbi_dev_copy_d2h(self.device, a.ctypes.data_as(ctypes.c_void_p),
+                                                     ctypes.c_void_p(ptr), a.nbytes))
+            out[name] = a
+        return out
 
     def query_csr(self, mass, tol) -> Tuple[np.ndarray, np.ndarray]:
         m = np.ascontiguousarray(np.atleast_1d(mass), np.float64)

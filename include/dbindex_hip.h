@@ -183,6 +183,32 @@ int dbi_query_csr(dbi_handle* h, const double* mass, const double* tol, uint64_t
                   dbi_query_result** out);
 void dbi_query_result_free(dbi_query_result* r);
 
+/* Builds the query directory of the current index now (otherwise the first
+ * query after a build or load does); lets a caller time or overlap it. */
+int dbi_query_prepare(dbi_handle* h);
+
+/* Materialised hits of a query batch, all in HBM (getSequences(m, tol) per
+ * query, DBIndexStoreSQLiteMult.java:315-350: every peptide with its protein
+ * ids, IndexMerge.parseAddPeptideInfo :386-481).  Hits of query i:
+ * ids[row[i] .. row[i+1]) (unique-peptide ids, ascending mass).  Protein ids
+ * of those hits: prot[occ_row[i] .. occ_row[i+1]), hit h's own list starting
+ * at prot[occ_row[i] + hit_occ[h]] and ending where the next hit's (or the
+ * query's) starts (insertion order, duplicates kept, IndexMerge.java:676-681).
+ * The buffers belong to the handle and stay valid until its next query-side
+ * call or build; the call returns once they are complete. */
+typedef struct dbi_device_hits {
+    const uint64_t* row;      /* nq + 1 */
+    const uint32_t* ids;      /* n_hits */
+    const uint64_t* occ_row;  /* nq + 1 */
+    const uint32_t* hit_occ;  /* n_hits */
+    const uint32_t* prot;     /* n_prot_ids */
+    uint64_t nq;
+    uint64_t n_hits;
+    uint64_t n_prot_ids;
+} dbi_device_hits;
+int dbi_query_hits_device(dbi_handle* h, const double* d_mass, const double* d_tol, uint64_t nq,
+                          dbi_device_hits* out);
+
 /* Gather per-unique-peptide data for ids[0..n): mass, representative
  * (first-occurrence) protein id + offset + length (IndexMerge.java:671-675),
  * and the occurrence range [occ_begin, occ_end) into dbi_occurrences().

@@ -386,3 +386,34 @@ def test_concurrent_queries_from_threads(Engine):
         for x in th:
             x.join()
     assert not errors
+
+
+@pytest.mark.parametrize("nprot,nq", [(300, 500), (1000, 3000)])
+def test_query_hits_device(Engine, nprot, nq):
+    """dbi_query_hits_device: every query's unique ids (getSequences(m, tol),
+    DBIndexStoreSQLiteMult.java:315-350) and every hit's protein ids
+    (insertion order, duplicates kept, IndexMerge.java:676-681), all
+    materialised in HBM, equal the oracle's."""
+    prm = DBIndexSearchParams.trypsin(2)
+    pp = fasta.config("1k").slice(0, nprot)
+    cp = prm.to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    o = oix.unique()
+    m, t = query_masses(oix, nq)
+    m[:5] = [float("nan"), 8000.0, -1.0, 0.0, 1e9]  # empty windows
+    with Engine(cp) as eng:
+        eng.build(pp)
+        for _ in range(2):  # second call reuses the grown buffers
+            r = eng.query_hits(m, t)
+            assert r["row"][0] == 0 and r["occ_row"][0] == 0
+            for i in range(nq):
+                exp = oix.query(float(m[i]), float(t[i]))
+                got = r["ids"][r["row"][i]:r["row"][i + 1]]
+                assert np.array_equal(got.astype(np.uint64), exp), i
+                prots = r["prot"][r["occ_row"][i]:r["occ_row"][i + 1]]
+                want = np.concatenate([o["occ_prot"][o["occ_off"][u]:o["occ_off"][u + 1]] for u in exp]) \
+                    if exp.shape[0] else np.zeros(0, np.uint32)
+                assert np.array_equal(prots, want), i
+                starts = r["hit_occ"][r["row"][i]:r["row"][i + 1]]
+                assert np.array_equal(starts.astype(np.uint64), (o["occ_off"][exp] - o["occ_off"][exp[0]])
+                                      if exp.shape[0] else np.zeros(0, np.uint64)), i
