@@ -122,6 +122,8 @@ struct dbi_handle {
     DevBuf<uint4> segs;                 // giant-chunk split: segment lists
     DevBuf<uint16_t> synth_len;         // dbi_synth_proteome: length quantile table
     DevBuf<uint8_t> synth_res;          //   residue table
+    DevBuf<uint8_t> synth_out;          //   generated residues (valid until the next dbi_synth_proteome)
+    DevBuf<uint64_t> synth_off;         //   generated offsets
     DevBuf<unsigned long long> ws_key;
     DevBuf<uint32_t> ws_k2;
 

@@ -516,7 +516,7 @@ void dbi_close(dbi_handle* h) {
     h->status.release(); h->win_lo.release(); h->win_hi.release(); h->qdir.release(); h->qdir_par.release();
     h->thr.release(); h->tile_pf.release(); h->chunk_lo.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
-    h->big_list.release(); h->giant_list.release(); h->segs.release(); h->synth_len.release(); h->synth_res.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
+    h->big_list.release(); h->giant_list.release(); h->segs.release(); h->synth_len.release(); h->synth_res.release(); h->synth_out.release(); h->synth_off.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
     h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release();
     h->o_mass.release(); h->o_pid.release(); h->o_off.release(); h->o_len.release();
     h->q_mass.release(); h->q_tol.release(); h->q_first.release(); h->q_count.release(); h->q_row.release();

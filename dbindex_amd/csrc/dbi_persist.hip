@@ -19,6 +19,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <vector>
 
@@ -151,17 +152,59 @@ int index_load(dbi_handle* h, const char* path, std::vector<uint8_t>* res_out, s
     const uint64_t R = hd.n_res, P = hd.n_prot, U = hd.n_unique, K = hd.n_kept;
     if (R >= (1ull << 32) - 1 || P >= (1ull << 32) - 1 || K >= (1ull << 32) - 1)
         return io_fail("index file too large for one device", path);
-    std::vector<uint8_t> res(R);
-    std::vector<uint64_t> off(P + 1), doff(P + 1);
-    std::string defs(hd.def_bytes, '\0');
-    std::vector<double> mass(U);
-    std::vector<uint32_t> pid(U), uoff(U), ulen(U), occ_off(U + 1), occ(K);
+    // the header must describe exactly this file (nothing allocated from an
+    // unchecked header: a damaged size would otherwise throw across the C-ABI)
+    if (U > K || hd.n_kept + hd.n_dropped != hd.n_total || hd.n_keys > U || hd.def_bytes >= (1ull << 40))
+        return io_fail("corrupt index file header", path);
+    if (std::fseek(f.f, 0, SEEK_END) != 0) return io_fail("cannot seek index file", path);
+    const long long fsize = std::ftell(f.f);
+    const unsigned long long want = sizeof(dbi_index_header) + R + 16ull * (P + 1) + hd.def_bytes + 8ull * U +
+                                    4ull * (3 * U + (U + 1) + K);
+    if (fsize < 0 || (unsigned long long)fsize != want) return io_fail("index file size does not match its header", path);
+    if (std::fseek(f.f, (long)sizeof(dbi_index_header), SEEK_SET) != 0) return io_fail("cannot seek index file", path);
+    std::vector<uint8_t> res;
+    std::vector<uint64_t> off, doff;
+    std::string defs;
+    std::vector<double> mass;
+    std::vector<uint32_t> pid, uoff, ulen, occ_off, occ;
+    try {
+        res.resize(R);
+        off.resize(P + 1);
+        doff.resize(P + 1);
+        defs.resize(hd.def_bytes);
+        mass.resize(U);
+        pid.resize(U);
+        uoff.resize(U);
+        ulen.resize(U);
+        occ_off.resize(U + 1);
+        occ.resize(K);
+    } catch (const std::exception&) {
+        return set_error(DBI_E_OOM, std::string("host memory for index file: ") + path);
+    }
     const bool ok = get(f.f, res.data(), R) && get(f.f, off.data(), P + 1) && get(f.f, doff.data(), P + 1) &&
                     (hd.def_bytes == 0 || get(f.f, &defs[0], hd.def_bytes)) && get(f.f, mass.data(), U) &&
                     get(f.f, pid.data(), U) && get(f.f, uoff.data(), U) && get(f.f, ulen.data(), U) &&
                     get(f.f, occ_off.data(), U + 1) && get(f.f, occ.data(), K);
     if (!ok) return io_fail("truncated index file", path);
     if (off[0] != 0 || off[P] != R) return io_fail("corrupt offsets in index file", path);
+    // contents: the invariants a build guarantees (dbi_build_occurrences checks
+    // the same of caller occurrences); a violation would mean out-of-range
+    // reads in queries and materialisation
+    for (uint64_t i = 0; i < P; ++i)
+        if (off[i + 1] < off[i]) return io_fail("corrupt offsets in index file", path);
+    if (hd.def_bytes && (doff[0] != 0 || doff[P] != hd.def_bytes)) return io_fail("corrupt definitions", path);
+    for (uint64_t i = 0; hd.def_bytes && i < P; ++i)
+        if (doff[i + 1] < doff[i]) return io_fail("corrupt definitions", path);
+    if (occ_off[0] != 0 || occ_off[U] != K) return io_fail("corrupt occurrence offsets in index file", path);
+    for (uint64_t u = 0; u < U; ++u) {
+        if (occ_off[u + 1] <= occ_off[u]) return io_fail("corrupt occurrence offsets in index file", path);
+        if (!(mass[u] >= 1.0 && mass[u] < 65536.0) || (u > 0 && mass[u] < mass[u - 1]))
+            return io_fail("corrupt peptide masses in index file (not finite, ascending, in [1, 65536))", path);
+        if (pid[u] >= P || ulen[u] == 0 || (uint64_t)uoff[u] + ulen[u] > off[pid[u] + 1] - off[pid[u]])
+            return io_fail("corrupt peptide location in index file", path);
+    }
+    for (uint64_t k = 0; k < K; ++k)
+        if (occ[k] >= P) return io_fail("corrupt occurrence protein id in index file", path);
 
     if ((rc = begin_build(h, R, P))) return rc;
     hipStream_t s = h->stream;

@@ -25,6 +25,7 @@
 #include <climits>
 #include <cmath>
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -39,6 +40,7 @@ struct dbi_comm {
     int nranks = 1;
     int rank = 0;
     int device = 0;
+    unsigned long long* d_flag = nullptr;  // failure agreement (agree())
 };
 
 namespace dbi {
@@ -112,19 +114,58 @@ int nccl_alltoallv(dbi_comm* c, const Rec* send, const std::vector<uint64_t>& so
     return 0;
 }
 
-// all[i * n + j] = mine_i[j] of every rank i (u64 all-gather through h->xcount)
-int nccl_count_matrix(dbi_handle* h, dbi_comm* c, const std::vector<uint64_t>& mine, std::vector<uint64_t>& all) {
-    const int n = c->nranks, me = c->rank;
+// Local failures must not strand the other ranks inside the next collective:
+// every rank reports its status with the data of a collective it would run
+// anyway (a status column in the count matrix and the totals, a status word
+// in the samples), or through agree() where no such collective comes first,
+// and all ranks return an error together.
+int peer_failed(const char* phase) {
+    return set_error(DBI_E_STATE, std::string("another rank failed (") + phase + "); see that rank's error");
+}
+
+// Test hook: DBI_TEST_FAIL="<phase>@<rank>" makes that rank fail locally at
+// that phase (digest, partition, buffers, merge, qroute, qbuffers), so the
+// agreement paths run without a real failure.
+int injected_failure(const char* phase, int rank) {
+    const char* e = std::getenv("DBI_TEST_FAIL");
+    if (!e || std::string(e) != std::string(phase) + "@" + std::to_string(rank)) return 0;
+    return set_error(DBI_E_STATE, std::string("injected failure (DBI_TEST_FAIL) in ") + phase);
+}
+
+// max over ranks of (rc != 0): 0 when every rank succeeded
+int agree(dbi_comm* c, int rc, hipStream_t s, bool* any) {
+    const unsigned long long mine = rc ? 1ull : 0ull;
+    unsigned long long all = 0;
+    DBI_HIP(hipMemcpyAsync(c->d_flag, &mine, sizeof(mine), hipMemcpyHostToDevice, s));
+    DBI_NCCL(ncclAllReduce(c->d_flag, c->d_flag + 1, 1, ncclUint64, ncclMax, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(&all, c->d_flag + 1, sizeof(all), hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    *any = all != 0;
+    return 0;
+}
+
+// all[i * n + j] = mine_i[j] of every rank i (u64 all-gather through h->xcount),
+// with each rank's status (rc != 0) in a last column: *any_failed
+int nccl_count_matrix(dbi_handle* h, dbi_comm* c, const std::vector<uint64_t>& mine, int status,
+                      std::vector<uint64_t>& all, bool* any_failed) {
+    const int n = c->nranks, me = c->rank, w = n + 1;
     hipStream_t s = h->stream;
     int rc;
-    if ((rc = h->xcount.ensure((size_t)n * n + 8))) return rc;
-    all.assign((size_t)n * n, 0);
-    for (int j = 0; j < n; ++j) all[(size_t)me * n + j] = mine[j];
-    DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * n, all.data() + (size_t)me * n, sizeof(uint64_t) * n,
+    if ((rc = h->xcount.ensure((size_t)n * w + 8))) return rc;
+    std::vector<uint64_t> full((size_t)n * w, 0);
+    for (int j = 0; j < n && j < (int)mine.size(); ++j) full[(size_t)me * w + j] = mine[j];
+    full[(size_t)me * w + n] = status ? 1u : 0u;
+    DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * w, full.data() + (size_t)me * w, sizeof(uint64_t) * w,
                            hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * n, h->xcount.p, n, ncclUint64, c->comm, s));
-    DBI_HIP(hipMemcpyAsync(all.data(), h->xcount.p, sizeof(uint64_t) * n * n, hipMemcpyDeviceToHost, s));
+    DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * w, h->xcount.p, w, ncclUint64, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(full.data(), h->xcount.p, sizeof(uint64_t) * n * w, hipMemcpyDeviceToHost, s));
     DBI_HIP(hipStreamSynchronize(s));
+    all.assign((size_t)n * n, 0);
+    *any_failed = false;
+    for (int i = 0; i < n; ++i) {
+        for (int j = 0; j < n; ++j) all[(size_t)i * n + j] = full[(size_t)i * w + j];
+        *any_failed |= full[(size_t)i * w + n] != 0;
+    }
     return 0;
 }
 
@@ -469,9 +510,13 @@ int dbi_query_sharded_local(dbi_handle* const* hs, int nshards, const double* co
         return set_error(DBI_E_INVALID, "NULL argument");
     int rc;
     uint64_t base = 0;
+    for (int i = 0; i < nshards; ++i)
+        if (!hs[i]) return set_error(DBI_E_INVALID, "NULL handle");
+    // every handle's query lock, in shard order (handles are distinct)
+    std::vector<std::unique_lock<std::recursive_mutex>> locks;
+    for (int i = 0; i < nshards; ++i) locks.emplace_back(hs[i]->qmu);
     for (int i = 0; i < nshards; ++i) {
         dbi_handle* h = hs[i];
-        if (!h) return set_error(DBI_E_INVALID, "NULL handle");
         if (h->shard.nshards != nshards || h->shard.rank != i)
             return set_error(DBI_E_INVALID, "hs[i] must be shard i of nshards");
         h->shard.u_base = base;  // owners' tables concatenate in shard order
@@ -517,22 +562,37 @@ int dbi_query_sharded_local(dbi_handle* const* hs, int nshards, const double* co
 int dbi_query_sharded(dbi_handle* h, dbi_comm* c, const double* d_mass, const double* d_tol, uint64_t nq,
                       uint64_t* d_first, uint64_t* d_count) {
     if (!h || !c || (nq && (!d_mass || !d_tol || !d_first || !d_count))) return set_error(DBI_E_INVALID, "NULL argument");
+    // argument and state errors are the same on every rank of a consistent job
+    // (same build, same communicator); the rest is agreed on below
     int rc;
     if ((rc = query_need(h))) return rc;
     if (h->shard.nshards != c->nranks || h->shard.rank != c->rank)
         return set_error(DBI_E_INVALID, "communicator does not match the sharded build");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
     DBI_HIP(hipSetDevice(h->device));
     ShardState& sh = h->shard;
     hipStream_t s = h->stream;
     const int n = c->nranks, me = c->rank;
-    if ((rc = query_route(h, d_mass, d_tol, nq))) return rc;
+    int rc_route = query_route(h, d_mass, d_tol, nq);
+    if (!rc_route) rc_route = injected_failure("qroute", me);
+    if (rc_route) sh.qsend_count.assign(n, 0);
     std::vector<uint64_t> counts;
-    if ((rc = nccl_count_matrix(h, c, sh.qsend_count, counts))) return rc;
+    bool failed = false;
+    if ((rc = nccl_count_matrix(h, c, sh.qsend_count, rc_route, counts, &failed))) return rc;
+    if (rc_route) return rc_route;
+    if (failed) return peer_failed("query routing");
     sh.qrecv_count.assign(n, 0);
     for (int i = 0; i < n; ++i) sh.qrecv_count[i] = counts[(size_t)i * n + me];
     offsets_of(sh.qrecv_count, sh.qrecv_off);
     sh.q_recv = sh.qrecv_off[n];
-    if ((rc = h->qrecv.ensure(sh.q_recv + 1))) return rc;
+    // every local allocation of the batch before the exchange, then agree
+    int rc_local = h->qrecv.ensure(sh.q_recv + 1);
+    if (!rc_local) rc_local = h->qres.ensure(sh.q_recv + 1);
+    if (!rc_local) rc_local = ensure_qdir(h, s);
+    if (!rc_local) rc_local = injected_failure("qbuffers", me);
+    if ((rc = agree(c, rc_local, s, &failed))) return rc;
+    if (rc_local) return rc_local;
+    if (failed) return peer_failed("query buffers");
     if ((rc = nccl_alltoallv(c, h->qsend.p, sh.qsend_off, sh.qsend_count, h->qrecv.p, sh.qrecv_off, sh.qrecv_count, s)))
         return rc;
     if ((rc = query_answer(h))) return rc;
@@ -566,8 +626,13 @@ int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_co
     c->nranks = nranks;
     c->rank = rank;
     c->device = device;
+    if (hipMalloc((void**)&c->d_flag, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        delete c;
+        return set_error(DBI_E_OOM, "hipMalloc (communicator status word)");
+    }
     const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
     if (r != ncclSuccess) {
+        (void)hipFree(c->d_flag);
         delete c;
         return nccl_fail(r, "ncclCommInitRank");
     }
@@ -579,6 +644,7 @@ void dbi_comm_destroy(dbi_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->d_flag) (void)hipFree(c->d_flag);
     delete c;
 }
 
@@ -610,28 +676,52 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     if (c->device != h->device) return set_error(DBI_E_INVALID, "communicator and engine on different devices");
     const int n = c->nranks, me = c->rank;
     int rc;
-    if ((rc = dbi_shard_digest(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n))) return rc;
+    // a rank that fails locally still takes part in the next collective, with
+    // its status, so that every rank returns an error (never a hang)
+    int rc_digest = dbi_shard_digest(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n);
+    if (!rc_digest) rc_digest = injected_failure("digest", me);
     ShardState& sh = h->shard;
     hipStream_t s = h->stream;
 
-    // samples of every shard -> the same owner splitters everywhere
-    const size_t blk = NS + 1;
-    std::vector<double> samples((size_t)n * blk);
-    if ((rc = dbi_shard_samples(h, samples.data() + (size_t)me * blk))) return rc;
+    // samples of every shard -> the same owner splitters everywhere; the word
+    // after the samples' weight carries the rank's status
+    const size_t blk = NS + 2;
+    std::vector<double> samples((size_t)n * blk, 0.0);
+    int rc_local = rc_digest ? rc_digest : dbi_shard_samples(h, samples.data() + (size_t)me * blk);
+    samples[(size_t)me * blk + NS + 1] = rc_local ? 1.0 : 0.0;
     if ((rc = h->samp.ensure((size_t)n * blk))) return rc;
     DBI_HIP(hipMemcpyAsync(h->samp.p + (size_t)me * blk, samples.data() + (size_t)me * blk, sizeof(double) * blk,
                            hipMemcpyHostToDevice, s));
     DBI_NCCL(ncclAllGather(h->samp.p + (size_t)me * blk, h->samp.p, blk, ncclFloat64, c->comm, s));
     DBI_HIP(hipMemcpyAsync(samples.data(), h->samp.p, sizeof(double) * n * blk, hipMemcpyDeviceToHost, s));
     DBI_HIP(hipStreamSynchronize(s));
+    if (rc_local) return rc_local;
+    std::vector<double> packed((size_t)n * (NS + 1));
+    for (int r = 0; r < n; ++r) {
+        if (samples[(size_t)r * blk + NS + 1] != 0.0) return peer_failed("shard digest");
+        std::copy(samples.begin() + (size_t)r * blk, samples.begin() + (size_t)r * blk + NS + 1,
+                  packed.begin() + (size_t)r * (NS + 1));
+    }
     int32_t split[MAX_SHARDS - 1] = {};
-    if ((rc = dbi_shard_splitters(samples.data(), n, h->params.mass_group_factor, split))) return rc;
-    if ((rc = dbi_shard_partition(h, split, nullptr))) return rc;
+    if ((rc = dbi_shard_splitters(packed.data(), n, h->params.mass_group_factor, split))) return rc;  // same everywhere
+    int rc_part = dbi_shard_partition(h, split, nullptr);
+    if (!rc_part) rc_part = injected_failure("partition", me);
+    if (rc_part) sh.send_count.assign(n, 0);
 
     // send counts of every shard: counts[i * n + j] = records shard i sends owner j
     const double t0 = now_ms();
     std::vector<uint64_t> counts;
-    if ((rc = nccl_count_matrix(h, c, sh.send_count, counts))) return rc;
+    bool failed = false;
+    if ((rc = nccl_count_matrix(h, c, sh.send_count, rc_part, counts, &failed))) return rc;
+    if (rc_part) return rc_part;
+    if (failed) return peer_failed("owner partition");
+    // checks on the whole matrix: every rank reaches the same verdict
+    for (int j = 0; j < n; ++j) {
+        uint64_t tot = 0;
+        for (int i = 0; i < n; ++i) tot += counts[(size_t)i * n + j];
+        if (tot >= (1ull << 32) - 1)
+            return set_error(DBI_E_INVALID, "more than 2^32-2 records for one owner: use more shards");
+    }
     sh.recv_count.assign(n, 0);
     uint64_t from_others = 0;
     for (int i = 0; i < n; ++i) {
@@ -641,9 +731,11 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     std::vector<uint64_t> roff;
     offsets_of(sh.recv_count, roff);
     if (sh.send_count[me] != sh.recv_count[me]) return set_error(DBI_E_STATE, "shard count exchange mismatch");
-    if (roff[n] >= (1ull << 32) - 1)
-        return set_error(DBI_E_INVALID, "more than 2^32-2 records for one owner: use more shards");
-    if ((rc = h->recA.ensure(std::max<uint64_t>(roff[n], 1)))) return rc;  // digest slots are free after partition
+    rc_local = h->recA.ensure(std::max<uint64_t>(roff[n], 1));  // digest slots are free after partition
+    if (!rc_local) rc_local = injected_failure("buffers", me);
+    if ((rc = agree(c, rc_local, s, &failed))) return rc;
+    if (rc_local) return rc_local;
+    if (failed) return peer_failed("owner buffers");
 
     // records to their owners: one group of point-to-point transfers over all peers
     {
@@ -656,22 +748,26 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     sh.n_recv = roff[n];
     sh.ms_exchange = now_ms() - t0;
     sh.phase = 3;
-    if ((rc = dbi_shard_merge(h))) return rc;
+    int rc_merge = dbi_shard_merge(h);
+    if (!rc_merge) rc_merge = injected_failure("merge", me);
 
-    // whole-index totals, and where this owner's rows start in the whole index
+    // whole-index totals (+ status), and where this owner's rows start in the whole index
     std::vector<uint64_t> tot(5, 0);
     {
-        const int w = 5;
+        const int w = 6;
         if ((rc = h->xcount.ensure((size_t)n * w + 8))) return rc;
         std::vector<unsigned long long> row(w, 0), rows((size_t)n * w);
         row[0] = sh.n_total; row[1] = sh.n_dropped; row[2] = sh.n_recv; row[3] = h->stats.n_unique;
         row[4] = h->stats.n_keys;
+        row[5] = rc_merge ? 1u : 0u;
         DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * w, row.data(), sizeof(uint64_t) * w, hipMemcpyHostToDevice, s));
         DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * w, h->xcount.p, w, ncclUint64, c->comm, s));
         DBI_HIP(hipMemcpyAsync(rows.data(), h->xcount.p, sizeof(uint64_t) * n * w, hipMemcpyDeviceToHost, s));
         DBI_HIP(hipStreamSynchronize(s));
+        if (rc_merge) return rc_merge;
         sh.u_base = 0;
         for (int i = 0; i < n; ++i) {
+            if (rows[(size_t)i * w + 5]) return peer_failed("owner merge");
             for (int k = 0; k < 5; ++k) tot[k] += rows[(size_t)i * w + k];
             if (i < me) sh.u_base += rows[(size_t)i * w + 3];
         }

@@ -87,7 +87,7 @@ int dbi_synth_proteome(dbi_handle* h, uint64_t seed, uint64_t p_begin, uint64_t 
     hipStream_t s = h->stream;
     int rc;
     if ((rc = h->synth_len.ensure(1u << SYNTH_LEN_BITS)) || (rc = h->synth_res.ensure(1u << SYNTH_RES_BITS)) ||
-        (rc = h->thr.ensure(n_prot + 1)) || (rc = h->poff64.ensure(n_prot + 1)) ||
+        (rc = h->thr.ensure(n_prot + 1)) || (rc = h->synth_off.ensure(n_prot + 1)) ||
         (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(n_prot + 1), h->scan_tmp.cap))) ||
         (rc = h->xcount.ensure(std::max<size_t>(h->xcount.cap, 8))))
         return rc;
@@ -103,19 +103,20 @@ int dbi_synth_proteome(dbi_handle* h, uint64_t seed, uint64_t p_begin, uint64_t 
         DBI_HIP(hipStreamSynchronize(s));
     }
     if (total >= (1ull << 32) - 16) return set_error(DBI_E_INVALID, "chunk above 2^32 residues: use smaller chunks");
-    if ((rc = h->res.ensure(total + 16))) return rc;
+    // the generator's own buffers: never the residues / offsets an index was built from
+    if ((rc = h->synth_out.ensure(total + 16))) return rc;
     DBI_LAUNCH(k_widen_offsets, dim3((n + 1 + 255) / 256), dim3(256), 0, s, h->thr.p, n, (uint32_t)total,
-               h->poff64.p);
+               h->synth_off.p);
     DBI_HIP(hipGetLastError());
     if (total) {
         const uint64_t nt = (total + 15) / 16;
         DBI_LAUNCH(k_synth_res, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, seed, res_base, total,
-                   h->synth_res.p, h->res.p);
+                   h->synth_res.p, h->synth_out.p);
         DBI_HIP(hipGetLastError());
     }
     DBI_HIP(hipStreamSynchronize(s));
-    *d_residues = h->res.p;
-    *d_prot_off = h->poff64.p;
+    *d_residues = h->synth_out.p;
+    *d_prot_off = h->synth_off.p;
     *n_res = total;
     return 0;
 }

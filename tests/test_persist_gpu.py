@@ -99,3 +99,49 @@ def test_unbucketed_or_filtered_index_is_not_saved(tmp_path):
         eng.set_bucket_drop(False)
         with pytest.raises(_native.DBIndexStoreException, match="bucketed"):
             eng.load(str(tmp_path / "x.dbihip"))
+
+
+@pytest.mark.parametrize("damage", ["truncate", "grow", "header_n_unique", "header_def_bytes", "occ_off",
+                                    "mass_order", "prot_id", "occ_prot", "offset"])
+def test_damaged_index_file_is_refused(Engine, tmp_path, damage):
+    """index_load checks the header against the file size before allocating and
+    every content invariant of a build (occ_off monotone ending at n_kept,
+    protein ids < P, peptide inside its protein, masses ascending, finite and in
+    [1, 65536)): a damaged file is an error, never an out-of-range read."""
+    import struct
+    from dbindex_amd import _native
+    pp = fasta.config("1k").slice(0, 100)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    path = str(tmp_path / "idx.dbihip")
+    with Engine(cp) as a:
+        st = a.build(pp)
+        a.save(path)
+    raw = bytearray(open(path, "rb").read())
+    R, P, U, K = st.n_residues, st.n_proteins, st.n_unique, st.n_kept
+    base = 128 + R + 16 * (P + 1)  # header, residues, offsets, def_off (no definitions)
+    mass0, pid0, off0, len0 = base, base + 8 * U, base + 12 * U, base + 16 * U
+    occ_off0, occ0 = base + 20 * U, base + 20 * U + 4 * (U + 1)
+    if damage == "truncate":
+        raw = raw[:-7]
+    elif damage == "grow":
+        raw += b"\0" * 8
+    elif damage == "header_n_unique":
+        struct.pack_into("<Q", raw, 8 + 8 + 8 + 16, 1 << 40)  # n_unique
+    elif damage == "header_def_bytes":
+        struct.pack_into("<Q", raw, 8 + 8 + 8 + 56, 1 << 50)  # def_bytes
+    elif damage == "occ_off":
+        struct.pack_into("<I", raw, occ_off0 + 4 * (U // 2), 0)
+    elif damage == "mass_order":
+        struct.pack_into("<d", raw, mass0 + 8 * (U // 2), 7000.0)
+    elif damage == "prot_id":
+        struct.pack_into("<I", raw, pid0 + 4 * 3, P + 5)
+    elif damage == "occ_prot":
+        struct.pack_into("<I", raw, occ0 + 4 * (K - 1), 0xFFFFFFF0)
+    elif damage == "offset":
+        struct.pack_into("<I", raw, off0 + 4 * 7, 1 << 20)
+    open(path, "wb").write(bytes(raw))
+    with Engine(cp) as b:
+        with pytest.raises(_native.DBIndexStoreException):
+            b.load(path)
+        b.build(pp)  # the engine stays usable
+        assert b.stats().n_unique == U

@@ -177,3 +177,41 @@ def test_shard_phase_order(native):
     with Engine(DBIndexSearchParams.trypsin(2).to_c(), 0) as eng:
         with pytest.raises(_native.DBIndexStoreException):
             _native.check(_native.lib().dbi_shard_merge(eng.h))
+
+
+@pytest.mark.parametrize("phase", ["digest", "partition", "buffers", "merge", "qroute", "qbuffers"])
+def test_sharded_rccl_local_failure_is_reported(native, phase, monkeypatch):
+    """A rank that fails locally still joins the next collective with its
+    status, so every rank returns an error instead of waiting in RCCL
+    (DBI_TEST_FAIL injects the failure; one rank here, the agreement
+    collectives are the same at N ranks).  The engine and the communicator
+    stay usable: the next build and query batch succeed."""
+    from dbindex_amd import _native
+    from dbindex_amd.engine import Engine
+    pp = fasta.config("1k").slice(0, 200)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    d_res, d_off = _inputs(native, pp)
+    m, t = query_masses(oix, 500)
+    dm, dt = native.DeviceBuffer.from_numpy(m, 0), native.DeviceBuffer.from_numpy(t, 0)
+    df, dc = native.DeviceBuffer(8 * m.shape[0], 0), native.DeviceBuffer(8 * m.shape[0], 0)
+    comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
+    try:
+        with Engine(cp, 0) as eng:
+            build = lambda: shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
+                                                0, pp.n_proteins)
+            query = lambda: shard.query_sharded(eng, comm, dm.ptr, dt.ptr, m.shape[0], df.ptr, dc.ptr)
+            if phase.startswith("q"):
+                build()
+            monkeypatch.setenv("DBI_TEST_FAIL", f"{phase}@0")
+            with pytest.raises(_native.DBIndexStoreException, match="injected failure"):
+                query() if phase.startswith("q") else build()
+            monkeypatch.delenv("DBI_TEST_FAIL")
+            st = build()
+            assert st.g_total == oix.n_total and st.g_unique == oix.n_unique
+            query()
+            of, oc = oix.query_batch(m, t)
+            f, c = df.download(np.uint64, m.shape[0]), dc.download(np.uint64, m.shape[0])
+            assert np.array_equal(c, oc) and np.array_equal(f[oc > 0], of[oc > 0])
+    finally:
+        comm.close()

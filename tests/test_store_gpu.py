@@ -162,3 +162,58 @@ def test_engine_matches_golden(fname, prm, nprot):
         first, count = eng.query(g["q_mass"], g["q_tol"])
         assert np.array_equal(first.astype(np.uint64), g["q_first"].astype(np.uint64))
         assert np.array_equal(count.astype(np.uint64), g["q_count"].astype(np.uint64))
+
+
+def test_concurrent_store_queries_mixed_ranges():
+    """Several host threads on one store: single-range getSequences(m, tol),
+    multi-range getSequences(List<MassRange>) (the key-range path) and engine
+    batch queries at once; every answer equals the oracle's (the query-side
+    calls serialise on the handle's query lock and scratch)."""
+    import threading
+    prm = DBIndexSearchParams.trypsin(2)
+    pp = fasta.config("1k").slice(0, 300)
+    seqs = pp.sequences()
+    oix = cref.Index(prm.to_c(), pp.residues, pp.offsets)
+    ix = _indexer(prm, pp)
+    st = ix.indexStore
+    u = oix.unique()
+    m, t = query_masses(oix, 400, seed=5)
+    single = [expected(oix, seqs, oix.query(float(a), float(b))) for a, b in zip(m[:40], t[:40])]
+    pairs = [(float(u["mass"][i]), float(u["mass"][(i * 7 + 3) % oix.n_unique]))
+             for i in range(0, oix.n_unique, max(1, oix.n_unique // 40))]
+    multi = [expected(oix, seqs, oix.query_ranges([a, b], [0.02, 0.5])) for a, b in pairs]
+    of, oc = oix.query_batch(m, t)
+    errors = []
+
+    def run_single():
+        for _ in range(5):
+            for (a, b), want in zip(zip(m[:40], t[:40]), single):
+                try:
+                    same(got(st.getSequences(float(a), float(b))), want)
+                except AssertionError:
+                    errors.append("single")
+
+    def run_multi():
+        for _ in range(5):
+            for (a, b), want in zip(pairs, multi):
+                try:
+                    same(got(st.getSequences([MassRange(a, 0.02), MassRange(b, 0.5)])), want)
+                except AssertionError:
+                    errors.append("multi")
+
+    def run_batch():
+        from dbindex_amd.engine import Engine
+        eng = Engine.__new__(Engine)  # a view of the store's engine handle (not owned)
+        eng.h, eng.device = st.engine_handle(), 0
+        for _ in range(20):
+            f, c = eng.query(m, t)
+            if not (np.array_equal(c, oc) and np.array_equal(f[oc > 0], of[oc > 0])):
+                errors.append("batch")
+        eng.h = None
+
+    th = [threading.Thread(target=f) for f in (run_single, run_multi, run_batch, run_single, run_multi)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
