@@ -1295,6 +1295,10 @@ struct BinDigit {  // LSD radix over the fine mass bin: (bin >> shift) & mask
     __device__ __forceinline__ uint32_t operator()(uint64_t q0) const {
         return (bin_of(q0_mass(q0), bm) >> shift) & mask;
     }
+    // the digit of the same record in the next pass (written next to it)
+    __device__ __forceinline__ uint32_t next(uint64_t q0, int nshift, uint32_t nmask) const {
+        return (bin_of(q0_mass(q0), bm) >> nshift) & nmask;
+    }
     __device__ __forceinline__ void xform(uint4&) const {}
 };
 struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor)
@@ -1305,6 +1309,7 @@ struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor
         for (uint32_t j = 0; j + 1 < om.nshards; ++j) d += k >= om.split[j] ? 1u : 0u;
         return d;
     }
+    __device__ __forceinline__ uint32_t next(uint64_t, int, uint32_t) const { return 0u; }
     __device__ __forceinline__ void xform(uint4& r) const {  // local -> global protein id
         const uint64_t q1 = u4_q1(r) + om.pid_add;
         r.z = (uint32_t)q1;
@@ -1313,6 +1318,7 @@ struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor
 };
 struct PairDigit {  // query routing pairs: q0 = owner shard, q1 = query index
     __device__ __forceinline__ uint32_t operator()(uint64_t q0) const { return (uint32_t)q0; }
+    __device__ __forceinline__ uint32_t next(uint64_t, int, uint32_t) const { return 0u; }
     __device__ __forceinline__ void xform(uint4&) const {}
 };
 
@@ -1361,10 +1367,47 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
     }
 }
 
+// The same counts from the digit bytes the previous pass wrote next to its
+// output (1 B per record instead of a 16-B record line): thread t of block b
+// counts records [b*RADIX_CHUNK + 8t, +8) (dense: every byte below n is a digit).
+__global__ void __launch_bounds__(RADIX_THREADS)
+k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
+    const uint32_t D = 1u << bits;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
+    wave_sync();
+    static_assert(RADIX_ITEMS == 8, "one 8-B load per thread");
+    const uint32_t i0 = blockIdx.x * RADIX_CHUNK + threadIdx.x * RADIX_ITEMS;
+    uint2 v = make_uint2(0u, 0u);
+    uint32_t nv = 0;  // digits of this thread below n
+    if (i0 + RADIX_ITEMS <= n) {
+        v = *reinterpret_cast<const uint2*>(dig + i0);
+        nv = RADIX_ITEMS;
+    } else if (i0 < n) {
+        uint32_t b[2] = {0u, 0u};
+        nv = n - i0;
+        for (uint32_t k = 0; k < nv; ++k) b[k >> 2] |= (uint32_t)dig[i0 + k] << (8 * (k & 3));
+        v = make_uint2(b[0], b[1]);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < RADIX_ITEMS; ++k) {
+        const uint32_t d = ((k < 4 ? v.x : v.y) >> (8 * (k & 3))) & 0xFFu;
+        if (k < nv) atomicAdd(&cnt[w][d], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int ww = 0; ww < RADIX_NW; ++ww) t += cnt[ww][d];
+        hist[(size_t)d * gridDim.x + blockIdx.x] = t;
+    }
+}
+
 template <bool SPARSE, typename Digit>
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, Digit dig, int bits,
-                const uint32_t* __restrict__ offs) {
+                const uint32_t* __restrict__ offs, uint8_t* __restrict__ nd_out, int nshift, uint32_t nmask) {
     static_assert(RADIX_D <= RADIX_THREADS, "one digit per thread");
     __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
     __shared__ uint4 stage[RADIX_CHUNK];  // the block's records in digit order
@@ -1432,6 +1475,7 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, D
     for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) {
         uint4 r = stage[t];
         const uint32_t dr = dig(u4_q0(r));
+        if (nd_out) nd_out[gofs[dr] + t] = (uint8_t)dig.next(u4_q0(r), nshift, nmask);
         dig.xform(r);
         out4[gofs[dr] + t] = r;
     }
@@ -1451,15 +1495,17 @@ static hipError_t radix_hist(const Rec* d_in, uint32_t n, const Digit& dig, int 
 
 template <typename Digit>
 static hipError_t radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const Digit& dig, int bits, bool sparse,
-                                const uint32_t* d_hist, hipStream_t s) {
+                                const uint32_t* d_hist, hipStream_t s, uint8_t* nd_out = nullptr, int nshift = 0,
+                                int nbits = 0) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    const uint32_t nmask = (1u << nbits) - 1;
     if (sparse)
         DBI_LAUNCH((k_radix_scatter<true, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, dig, bits,
-                   d_hist);
+                   d_hist, nd_out, nshift, nmask);
     else
         DBI_LAUNCH((k_radix_scatter<false, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, dig, bits,
-                   d_hist);
+                   d_hist, nd_out, nshift, nmask);
     return hipGetLastError();
 }
 
@@ -1468,9 +1514,18 @@ hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int 
     return radix_hist(d_in, n, BinDigit{bm, shift, (1u << bits) - 1}, bits, sparse, d_hist, s);
 }
 
+hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint32_t* d_hist, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    DBI_LAUNCH(k_radix_hist_u8, dim3(g), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist);
+    return hipGetLastError();
+}
+
 hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
-                                bool sparse, const uint32_t* d_hist, hipStream_t s) {
-    return radix_scatter(d_in, d_out, n, BinDigit{bm, shift, (1u << bits) - 1}, bits, sparse, d_hist, s);
+                                bool sparse, const uint32_t* d_hist, hipStream_t s, uint8_t* d_next_dig,
+                                int next_shift, int next_bits) {
+    return radix_scatter(d_in, d_out, n, BinDigit{bm, shift, (1u << bits) - 1}, bits, sparse, d_hist, s, d_next_dig,
+                         next_shift, next_bits);
 }
 
 // owner partition of a sharded build: the same stable pass with digit = owner

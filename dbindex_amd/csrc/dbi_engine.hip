@@ -92,6 +92,17 @@ DevParams make_dev_params(const dbi_params& p) {
     return d;
 }
 
+// LSD digit widths over log2(nbins) bits: the first (lowest) digit takes the
+// remainder, the others RADIX_BITS-wide digits; returns the number of passes
+int radix_plan(uint32_t nbins, bool sparse, int* width) {
+    int total = 0;
+    while ((1ull << total) < nbins) ++total;
+    const int passes = std::max((total + RADIX_BITS - 1) / RADIX_BITS, sparse ? 1 : 0);
+    const int per = total ? (total + passes - 1) / passes : 0;
+    for (int p = 0; p < passes; ++p) width[p] = p == 0 ? total - (passes - 1) * per : per;
+    return passes;
+}
+
 uint32_t choose_nbins(uint64_t n, int max_bits) {
     uint64_t want = n / BIN_AVG;  // fine mass bins; chunks group them to ~CHUNK_T records
     uint32_t b = 1;
@@ -120,13 +131,10 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     int rc;
     const uint32_t n32 = (uint32_t)n;
     const uint32_t nbins = choose_nbins(n, h->bin_bits_max);
-    BinMap bm;
-    bm.lo = lo;
-    bm.nbins = nbins;
-    bm.scale = (hi > lo) ? (double)nbins / (hi - lo) : 0.0;
-    const int total_bits = log2_ceil(nbins);
-    const int passes = std::max((total_bits + RADIX_BITS - 1) / RADIX_BITS, sparse ? 1 : 0);
-    const int bits_per = total_bits ? (total_bits + passes - 1) / passes : 0;
+    const BinMap bm = make_binmap(lo, hi, nbins);
+    int width[8] = {};
+    const int passes = radix_plan(nbins, sparse, width);
+    const int bits_per = passes ? width[passes - 1] : 0;  // the widest digit
     const uint32_t n_in32 = sparse ? (uint32_t)n_in : n32;
     const size_t hist_elems = passes ? radix_hist_elems(n_in32, bits_per) : 1;
 
@@ -146,23 +154,34 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
         (rc = h->ulen.ensure(n)) || (rc = h->occ_off.ensure(n + 1)) || (rc = h->occ_pid.ensure(n)))
         return rc;
 
-    // stable LSD passes over the bin id
+    // stable LSD passes over the bin id; every pass but the last writes the
+    // next pass's digit of each record (1 B) next to its output, so the next
+    // histogram reads bytes instead of records
+    if (passes > 1 && (rc = h->digits.ensure(std::max<uint64_t>(n, h->digits.cap)))) return rc;
     Rec* src = h->recA.p;
     Rec* dst = h->recB.p;
     int shift = 0;
     for (int ps = 0; ps < passes; ++ps) {
-        const int bits = std::min(bits_per, total_bits - shift);
+        const int bits = width[ps];
         const bool sp = sparse && ps == 0;
         const uint32_t nin = sp ? n_in32 : n32;
         const double hbytes = 8.0 * (double)radix_blocks(nin) * (double)(1u << bits);  // hist write + scan
-        // hist reads the 8-B mass of every record; scatter moves 16 B in + 16 B out
-        STAGE(h, "radix_hist", by(0, 8, 0, 0, 0), launch_radix_hist(src, nin, bm, shift, bits, sp, h->hist.p, s));
+        if (ps == 0) {                   // the 8-B mass of every record
+            STAGE(h, "radix_hist", by(0, 8, 0, 0, 0), launch_radix_hist(src, nin, bm, shift, bits, sp, h->hist.p, s));
+        } else {                         // the digit bytes of the previous pass
+            STAGE(h, "radix_hist", by(0, 1, 0, 0, 0),
+                  launch_radix_hist_u8(h->digits.p, nin, bits, h->hist.p, s));
+        }
         STAGE(h, "radix_scan", by(0, 0, 0, 0, 0),
               launch_scan_u32(h->hist.p, h->hist.p, (uint64_t)radix_blocks(nin) << bits, h->scan_tmp.p,
                               h->scan_tmp.cap, nullptr, s));
         h->stages[h->nstage - 1].cB = hbytes / std::max<double>(nbins, 1.0);
-        STAGE(h, "radix_scatter", by(0, 32, 0, 0, 0),
-              launch_radix_scatter(src, dst, nin, bm, shift, bits, sp, h->hist.p, s));
+        // scatter moves 16 B in + 16 B out (+ 1 B next digit)
+        const bool more = ps + 1 < passes;
+        const int nbits = more ? width[ps + 1] : 0;
+        STAGE(h, "radix_scatter", by(0, more ? 33 : 32, 0, 0, 0),
+              launch_radix_scatter(src, dst, nin, bm, shift, bits, sp, h->hist.p, s, more ? h->digits.p : nullptr,
+                                   shift + bits, nbits));
         std::swap(src, dst);
         shift += bits;
     }
@@ -515,7 +534,7 @@ void dbi_close(dbi_handle* h) {
     h->qres.release(); h->qback.release(); h->blk.release(); h->scan_tmp.release();
     h->status.release(); h->win_lo.release(); h->win_hi.release(); h->qdir.release(); h->qdir_par.release();
     h->thr.release(); h->tile_pf.release(); h->chunk_lo.release();
-    h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release();
+    h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release(); h->digits.release();
     h->big_list.release(); h->giant_list.release(); h->segs.release(); h->synth_len.release(); h->synth_res.release(); h->synth_out.release(); h->synth_off.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
     h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release();
     h->o_mass.release(); h->o_pid.release(); h->o_off.release(); h->o_len.release();

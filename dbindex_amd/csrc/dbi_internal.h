@@ -86,6 +86,12 @@ constexpr uint8_t F_MAND = 4;
 constexpr uint8_t F_CUT = 8;    // window only: checkCleavage C-side ok at this residue (or protein end)
 constexpr uint8_t F_LAST = 16;  // window only: last residue of its protein
 
+struct BinMap {
+    double lo;
+    double scale;     // nbins / (hi - lo)
+    uint32_t nbins;
+};
+
 // Device-side copy of the parameters the kernels need (kernel argument).
 struct DevParams {
     double min_mh, max_mh;
@@ -109,6 +115,15 @@ struct DevParams {
     const double* win_lo;     // device arrays, n_win each
     const double* win_hi;
 };
+
+// fine mass bins of a build: the one place the map's fields are computed
+inline BinMap make_binmap(double lo, double hi, uint32_t nbins) {
+    BinMap bm;
+    bm.lo = lo;
+    bm.nbins = nbins;
+    bm.scale = (hi > lo) ? (double)nbins / (hi - lo) : 0.0;
+    return bm;
+}
 
 constexpr int GIANT_PASSES = 3;  // MSD split passes over chunks above BIG_CAP (then the global-memory fallback)
 
@@ -188,11 +203,6 @@ hipError_t launch_scan_u32(const uint32_t* d_in, uint32_t* d_out, uint64_t n, ui
                            uint64_t tmp_elems, unsigned long long* d_total, hipStream_t s);
 size_t scan_u32_tmp_elems(uint64_t n);
 
-struct BinMap {
-    double lo;
-    double scale;     // nbins / (hi - lo)
-    uint32_t nbins;
-};
 // Owner map of a sharded build (dbi_shard_*): shard d owns the mass keys
 // (int)(m * factor) in [split[d-1], split[d]) (split[-1] = -inf, split[n-1] =
 // +inf), so a key, and every occurrence of a peptide, has exactly one owner.
@@ -220,8 +230,12 @@ struct RouteMap {
 // sparse: the input holds REC_SENTINEL slots (bounded digest), left out of the output
 hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,
                              uint32_t* d_hist, hipStream_t s);
+// d_next_dig (optional): the record's digit of the next pass, one byte per
+// output position, counted by launch_radix_hist_u8 instead of re-reading records
 hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
-                                bool sparse, const uint32_t* d_hist, hipStream_t s);
+                                bool sparse, const uint32_t* d_hist, hipStream_t s, uint8_t* d_next_dig = nullptr,
+                                int next_shift = 0, int next_bits = 0);
+hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint32_t* d_hist, hipStream_t s);
 uint64_t radix_blocks(uint32_t n);
 // stable partition pass by owner shard (digit = OwnerDigit), global protein ids out
 hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bool sparse, uint32_t* d_hist,
