@@ -7,14 +7,19 @@ HBM.  Default workload at N=1: the SwissProt-scale FASTA the metric is quoted
 on (BASELINE.json configs[2] "SwissProt (~560k proteins), trypsin, 2 missed
 cleavages", which fits one MI355X) as a seeded synthetic proteome (SURVEY.md
 §8(d), seed 3).  --config human is configs[1] (20k proteins, seed 2).
-N>1 (torchrun, one rank per GPU): every rank contributes its own protein shard
-of the same size (seed + 1000*rank) -> weak scaling.  One step builds ONE index
-over the proteins of all ranks (dbi_build_sharded): each rank digests its
-shard, routes every record to the rank owning its mass key over RCCL (grouped
-point-to-point sends over xGMI), and each owner sorts + de-duplicates its key
-range.  The residues of every shard are all-gathered into each GPU's HBM once,
-before the timed region (input staging: the owner merge compares peptide
-strings of any shard).  --no-merge: independent shard-local indexes instead.
+N>1 (torchrun, one rank per GPU), --scaling strong (default): the SAME
+proteome is split by residues into N protein ranges (configs[2]: "protein-
+sharded across 8xMI355X"); one step builds ONE index over all of it
+(dbi_build_sharded): each rank digests its range, routes every record to the
+rank owning its mass key over RCCL (grouped point-to-point sends over xGMI),
+and each owner sorts + de-duplicates its key range.  Every rank holds the whole
+proteome in HBM before the timed region (each rank reads the same FASTA: input
+staging; the owner merge compares peptide strings of any protein).  After the
+timed steps the owners' slices are all-gathered onto every rank
+(dbi_shard_replicate, north_star's all-gatherv; timed separately) and every
+rank answers its own 1M-query batch locally.  --scaling weak: each rank its own
+proteome of the same size (seed + 1000*rank), still one merged index.
+--no-merge: independent shard-local indexes instead.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config swissprot|human|1k|semi|trembl]
 Prints ONE JSON line on rank 0.
@@ -100,6 +105,8 @@ def main() -> None:
     ap.add_argument("--no-merge", action="store_true",
                     help="N>1: shard-local indexes (no exchange) instead of one merged index")
     ap.add_argument("--merge", action="store_true", help="N=1: run the sharded (RCCL) build with one rank")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="N>1 merged builds: split one proteome over the ranks (strong) or one proteome per rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,44 +133,57 @@ def main() -> None:
         return run_trembl(args, world, rank, dev, dist)
 
     desc, proteome, make_params, cpu_sample = WORKLOADS[args.config]
+    strong = merge and args.scaling == "strong"
     base = dict(fasta.CONFIGS[proteome])
-    base["seed"] = base["seed"] + 1000 * rank  # each rank its own shard of equal size
+    if not strong:
+        base["seed"] = base["seed"] + 1000 * rank  # weak: each rank its own proteome of equal size
     t0 = time.time()
     pp = fasta.synthetic(with_defs=False, **base)
     log(f"[rank {rank}] synthetic {args.config}: P={pp.n_proteins} R={pp.n_residues} ({time.time() - t0:.1f}s)")
     prm = make_params()
 
     eng = Engine(prm, device=dev)
+    t_ag = 0.0
     if merge:
         from dbindex_amd import shard
-        # global layout: every rank's residues and offsets, in rank order
-        sizes = [(pp.n_residues, pp.n_proteins, pp.offsets.astype(np.uint64))] * world
-        if world > 1:
-            dist.all_gather_object(sizes, sizes[0])
-        res_base = np.concatenate([[0], np.cumsum([x[0] for x in sizes])]).astype(np.uint64)
-        prot_base = np.concatenate([[0], np.cumsum([x[1] for x in sizes])]).astype(np.int64)
-        R_all, P_all = int(res_base[-1]), int(prot_base[-1])
-        off_all = np.concatenate([sizes[r][2][:-1] + res_base[r] for r in range(world)] +
-                                 [np.array([R_all], np.uint64)])
+        import ctypes
+        from dbindex_amd._native import lib as _lib
         uid = [stdout_to_stderr(shard.ShardComm.unique_id) if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
         comm = stdout_to_stderr(lambda: shard.ShardComm(uid[0], world, rank, dev))
-        # input staging (untimed): every shard's residues into every GPU's HBM
-        d_res = DeviceBuffer(R_all + 16, dev)
-        mine = d_res.ptr + int(res_base[rank])
-        from dbindex_amd._native import lib as _lib
-        import ctypes
-        _lib().dbi_dev_copy_h2d(dev, ctypes.c_void_p(mine), pp.residues.ctypes.data_as(ctypes.c_void_p),
-                                pp.n_residues)
-        t_ag = time.perf_counter()
-        comm.allgatherv(mine, d_res.ptr, [x[0] for x in sizes])
-        t_ag = time.perf_counter() - t_ag
-        d_off = DeviceBuffer.from_numpy(off_all, dev)
+        if strong:
+            # every rank holds the whole proteome (the same FASTA); rank r
+            # digests its residue-balanced protein range
+            R_all, P_all = pp.n_residues, pp.n_proteins
+            d_res = DeviceBuffer.from_numpy(np.concatenate([pp.residues, np.zeros(16, np.uint8)]), dev)
+            d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), dev)
+            p_begin, p_end = shard.protein_ranges(pp.offsets, world)[rank]
+        else:
+            # global layout: every rank's residues and offsets, in rank order
+            sizes = [(pp.n_residues, pp.n_proteins, pp.offsets.astype(np.uint64))] * world
+            if world > 1:
+                dist.all_gather_object(sizes, sizes[0])
+            res_base = np.concatenate([[0], np.cumsum([x[0] for x in sizes])]).astype(np.uint64)
+            prot_base = np.concatenate([[0], np.cumsum([x[1] for x in sizes])]).astype(np.int64)
+            R_all, P_all = int(res_base[-1]), int(prot_base[-1])
+            off_all = np.concatenate([sizes[r][2][:-1] + res_base[r] for r in range(world)] +
+                                     [np.array([R_all], np.uint64)])
+            # input staging (untimed): every shard's residues into every GPU's HBM
+            d_res = DeviceBuffer(R_all + 16, dev)
+            mine = d_res.ptr + int(res_base[rank])
+            _lib().dbi_dev_copy_h2d(dev, ctypes.c_void_p(mine), pp.residues.ctypes.data_as(ctypes.c_void_p),
+                                    pp.n_residues)
+            t_ag = time.perf_counter()
+            comm.allgatherv(mine, d_res.ptr, [x[0] for x in sizes])
+            t_ag = time.perf_counter() - t_ag
+            d_off = DeviceBuffer.from_numpy(off_all, dev)
+            p_begin, p_end = int(prot_base[rank]), int(prot_base[rank + 1])
         synchronize(dev)
-        p_begin, p_end = int(prot_base[rank]), int(prot_base[rank + 1])
-        log(f"[rank {rank}] merged index over {P_all} proteins / {R_all} residues; residue all-gather "
-            f"{t_ag * 1e3:.1f} ms")
+        my_res = int(pp.offsets[p_end] - pp.offsets[p_begin]) if strong else pp.n_residues
+        my_prot = p_end - p_begin
+        log(f"[rank {rank}] merged index over {P_all} proteins / {R_all} residues; this rank digests proteins "
+            f"[{p_begin}, {p_end}) ({my_res} residues)")
 
         def step():
             return shard.build_sharded(eng, comm, d_res.ptr, R_all, d_off.ptr, P_all, p_begin, p_end)
@@ -172,6 +192,7 @@ def main() -> None:
         d_res = DeviceBuffer.from_numpy(pp.residues, dev)
         d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), dev)
         synchronize(dev)
+        my_res, my_prot = pp.n_residues, pp.n_proteins
 
         def step():
             return eng.build_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins)
@@ -258,13 +279,14 @@ def main() -> None:
     kernels = kernel_table(warm_acc, n_warm - skip)
     timed = kernel_table(stage_acc, args.steps)
     dom = timed[0] if timed else None
-    build_alg = pp.n_residues + 8.0 * (pp.n_proteins + 1) + 48.0 * st.n_total  # SURVEY.md §8(d), this rank
+    build_alg = my_res + 8.0 * (my_prot + 1) + 48.0 * st.n_total  # SURVEY.md §8(d), this rank's share
     est = eng.stats()  # merged: this rank's owner slice
     if merge:
         unique_all, keys_all = st.g_unique, st.g_keys
         ph = np.mean(np.array(shard_acc), axis=0) if shard_acc else np.zeros(4)
         phases = dict(zip(("digest_ms", "partition_ms", "exchange_ms", "merge_ms"), map(float, ph)))
-        phases["residue_allgather_ms_untimed"] = t_ag * 1e3
+        if not strong:
+            phases["residue_allgather_ms_untimed"] = t_ag * 1e3
         phases["owner_records"] = st.n_received
         phases["records_sent"] = st.n_sent
     else:
@@ -273,33 +295,41 @@ def main() -> None:
     # secondary: mass-window queries/sec on the built index (1M queries, +-20 ppm)
     qps = None
     if args.queries > 0 and merge:
-        # routed queries on the one merged index: every rank brings its own 1M
-        # batch (90 % near indexed masses of ANY owner), windows go to their key
-        # owners over RCCL and the whole-index ids come back
+        # north_star's all-gatherv: every owner's slice onto every rank, then
+        # every rank answers its own 1M batch locally (no exchange per batch)
+        if world > 1:
+            dist.barrier()
+        synchronize(dev)
+        t_rep = time.perf_counter()
+        shard.replicate(eng, comm)
+        synchronize(dev)
+        t_rep = time.perf_counter() - t_rep
+        if world > 1:
+            t = torch.tensor([t_rep], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t_rep = float(t.item())
+        rst = eng.stats()
         ex = eng.export()["mass"]
         rng = np.random.Generator(np.random.PCG64(7 + rank))
-        pick = ex[rng.integers(0, ex.shape[0], min(ex.shape[0], args.queries // world + 1))] if ex.shape[0] else ex
-        pool = [pick] * world
-        if world > 1:
-            dist.all_gather_object(pool, pick)
-        pool = np.concatenate(pool) if sum(p.shape[0] for p in pool) else np.array([1000.0])
         nq = args.queries
         k = int(nq * 0.9)
         m = np.empty(nq)
-        m[:k] = pool[rng.integers(0, pool.shape[0], k)] * (1 + rng.normal(0, 5e-6, k))
+        m[:k] = ex[rng.integers(0, ex.shape[0], k)] * (1 + rng.normal(0, 5e-6, k)) if ex.shape[0] else 1000.0
         m[k:] = rng.uniform(500, 6000, nq - k)
         tol = m * (1 - 1 / (20.0 / 1e6 + 1))
         dm, dt = DeviceBuffer.from_numpy(m, dev), DeviceBuffer.from_numpy(tol, dev)
         df, dc = DeviceBuffer(8 * nq, dev), DeviceBuffer(8 * nq, dev)
         synchronize(dev)
+        eng.query_prepare()
         for _ in range(3):
-            shard.query_sharded(eng, comm, dm.ptr, dt.ptr, nq, df.ptr, dc.ptr)
+            eng.query_device(dm.ptr, dt.ptr, nq, df.ptr, dc.ptr)
+        synchronize(dev)
         reps = 20
         if world > 1:
             dist.barrier()
         tq = time.perf_counter()
         for _ in range(reps):
-            shard.query_sharded(eng, comm, dm.ptr, dt.ptr, nq, df.ptr, dc.ptr)
+            eng.query_device(dm.ptr, dt.ptr, nq, df.ptr, dc.ptr)
         synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -310,8 +340,11 @@ def main() -> None:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tq = float(t.item())
         qps = dict(value=world * nq * reps / tq, unit="queries/s", queries_per_rank=nq, tol_ppm=20.0,
-                   avg_hits=hits / nq, index=f"the merged index above, queries routed to key owners over RCCL "
-                                             f"({world} ranks)")
+                   avg_hits=hits / nq, kind="range lookup on each rank's replica of the whole index",
+                   index=f"the merged index above, replicated onto all {world} ranks "
+                         f"(dbi_shard_replicate: {rst.n_unique} unique peptides, {rst.n_kept} occurrences)",
+                   replicate_ms=1e3 * t_rep,
+                   replicate_bytes_per_rank=int(20 * rst.n_unique + 4 * rst.n_kept))
     if args.queries > 0 and not merge:
         ex = eng.export()["mass"]
         rng = np.random.Generator(np.random.PCG64(7 + rank))
@@ -367,18 +400,20 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded proteome, SwissProt residue frequencies; SURVEY.md §8(d))",
             "config": {
                 "workload": desc,
-                "proteins_per_gpu": pp.n_proteins,
-                "residues_per_gpu": pp.n_residues,
+                "proteins_per_gpu": my_prot,
+                "residues_per_gpu": my_res,
+                "proteins": pp.n_proteins * (world if merge and not strong else 1),
                 "peptides_per_step_per_gpu": st.n_total,
                 "unique_peptides": unique_all,
                 "mass_keys": keys_all,
-                "parallelism": (f"protein-sharded x{world}, one index: RCCL owner exchange by mass key" if merge
+                "parallelism": (f"protein-sharded x{world} ({'one proteome split' if strong else 'one proteome per rank'}), "
+                                f"one index: RCCL owner exchange by mass key" if merge
                                 else f"protein-sharded x{world}, shard-local indexes" if world > 1 else "single GPU"),
                 "n_bins": est.n_bins,
                 "n_big_bins": est.n_big_bins,

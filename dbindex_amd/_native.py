@@ -119,6 +119,8 @@ SIGNATURES = [
     ("dbi_shard_stats_get", c_int, [P, POINTER(DbiShardStats)]),
     ("dbi_query_sharded", c_int, [P, P, P, P, c_uint64, P, P]),
     ("dbi_query_sharded_local", c_int, [P, c_int, P, P, P, P, P]),
+    ("dbi_shard_replicate", c_int, [P, P]),
+    ("dbi_shard_replicate_local", c_int, [P, c_int]),
     ("dbi_synth_proteome", c_int, [P, c_uint64, c_uint64, c_uint64, c_uint64, P, P, POINTER(c_void_p),
                                    POINTER(c_void_p), POINTER(c_uint64)]),
     ("dbi_count", c_int, [P, P, c_uint64, P, c_uint64, POINTER(c_uint64), POINTER(c_uint64)]),

@@ -53,7 +53,7 @@ struct DevBuf {
 
 // State of a sharded build on this handle (dbi_shard_* phases, dbi_shard.hip).
 struct ShardState {
-    int phase = 0;  // 0 none, 1 digested, 2 partitioned, 3 exchanged, 4 merged
+    int phase = 0;  // 0 none, 1 digested, 2 partitioned, 3 exchanged, 4 merged, 5 replicated
     int rank = 0, nshards = 1;
     uint64_t p_begin = 0, p_end = 0;        // this shard's proteins (global ids)
     uint64_t n_res_global = 0, n_prot_global = 0;
@@ -150,6 +150,8 @@ struct dbi_handle {
     DevBuf<uint64_t> h_row, h_orow;
     DevBuf<unsigned long long> h_sums;
     DevBuf<uint64_t> kr_scratch;        // engine_key_range result (2 words)
+    DevBuf<double> r_mass;              // dbi_shard_replicate: the whole index being assembled
+    DevBuf<uint32_t> r_pid, r_off, r_len, r_occ_off, r_occ;
     DevBuf<double> g_mass;
     DevBuf<uint32_t> g_pid, g_off, g_len;
     DevBuf<uint64_t> g_b, g_e;

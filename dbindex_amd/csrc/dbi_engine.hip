@@ -543,6 +543,8 @@ void dbi_close(dbi_handle* h) {
     h->g_b.release(); h->g_e.release();
     h->h_nh.release(); h->h_no.release(); h->h_ids.release(); h->h_hocc.release(); h->h_prot.release();
     h->h_row.release(); h->h_orow.release(); h->h_sums.release(); h->kr_scratch.release();
+    h->r_mass.release(); h->r_pid.release(); h->r_off.release(); h->r_len.release(); h->r_occ_off.release();
+    h->r_occ.release();
     for (auto& ev : h->evpool)
         if (ev) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);

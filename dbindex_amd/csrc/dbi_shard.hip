@@ -233,6 +233,81 @@ int query_answer(dbi_handle* h) {
     return 0;
 }
 
+// ---- replicated index (every owner's slice on every rank) ----
+__global__ void k_add_u32(uint32_t* __restrict__ p, uint64_t n, uint32_t add) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] += add;
+}
+
+struct SliceSizes {
+    std::vector<uint64_t> u, k;  // per shard: unique peptides, occurrences
+    std::vector<uint64_t> ub, kb; // their bases in the whole index (nshards + 1)
+};
+
+void slice_bases(SliceSizes& z) {
+    const size_t n = z.u.size();
+    z.ub.assign(n + 1, 0);
+    z.kb.assign(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) {
+        z.ub[i + 1] = z.ub[i] + z.u[i];
+        z.kb[i + 1] = z.kb[i] + z.k[i];
+    }
+}
+
+int replica_check(const SliceSizes& z) {
+    if (z.kb.back() >= (1ull << 32) - 1 || z.ub.back() >= (1ull << 32) - 1)
+        return set_error(DBI_E_INVALID, "a replicated index holds at most 2^32-2 occurrences per device");
+    return 0;
+}
+
+int replica_alloc(dbi_handle* h, const SliceSizes& z) {
+    const uint64_t U = z.ub.back(), K = z.kb.back();
+    int rc;
+    if ((rc = h->r_mass.ensure(std::max<uint64_t>(U, 1))) || (rc = h->r_pid.ensure(std::max<uint64_t>(U, 1))) ||
+        (rc = h->r_off.ensure(std::max<uint64_t>(U, 1))) || (rc = h->r_len.ensure(std::max<uint64_t>(U, 1))) ||
+        (rc = h->r_occ_off.ensure(U + 1)) || (rc = h->r_occ.ensure(std::max<uint64_t>(K, 1))))
+        return rc;
+    return 0;
+}
+
+// slice i's occurrence offsets are local to it: add the occurrences of the
+// slices before it; the table ends at K
+int replica_rebase(dbi_handle* h, const SliceSizes& z, hipStream_t s) {
+    const size_t n = z.u.size();
+    for (size_t i = 0; i < n; ++i)
+        if (z.u[i] && z.kb[i]) {
+            hipLaunchKernelGGL(k_add_u32, dim3((uint32_t)((z.u[i] + 255) / 256)), dim3(256), 0, s,
+                               h->r_occ_off.p + z.ub[i], z.u[i], (uint32_t)z.kb[i]);
+            DBI_HIP(hipGetLastError());
+        }
+    const uint32_t K = (uint32_t)z.kb.back();
+    DBI_HIP(hipMemcpyAsync(h->r_occ_off.p + z.ub.back(), &K, 4, hipMemcpyHostToDevice, s));
+    DBI_HIP(hipStreamSynchronize(s));  // K is a stack value
+    return 0;
+}
+
+// the replica becomes the handle's index: the whole proteome, queried locally
+void replica_install(dbi_handle* h, const SliceSizes& z, uint64_t g_total, uint64_t g_dropped, uint64_t g_keys) {
+    std::swap(h->umass, h->r_mass);
+    std::swap(h->upid, h->r_pid);
+    std::swap(h->uoff, h->r_off);
+    std::swap(h->ulen, h->r_len);
+    std::swap(h->occ_off, h->r_occ_off);
+    std::swap(h->occ_pid, h->r_occ);
+    h->r_mass.release(); h->r_pid.release(); h->r_off.release(); h->r_len.release();
+    h->r_occ_off.release(); h->r_occ.release();
+    dbi_stats& st = h->stats;
+    st.n_unique = z.ub.back();
+    st.n_kept = z.kb.back();
+    st.n_total = g_total;
+    st.n_dropped = g_dropped;
+    st.n_keys = g_keys;
+    st.n_residues = h->n_res;
+    st.n_proteins = h->n_prot;
+    ++h->build_serial;  // a new query directory
+    h->shard.phase = 5;
+}
+
 int query_need(const dbi_handle* h) {
     if (h->shard.phase != 4 || !h->built || !h->shard.u_base_known)
         return set_error(DBI_E_STATE, "sharded queries need a finished sharded build (dbi_build_sharded, or the "
@@ -600,6 +675,108 @@ int dbi_query_sharded(dbi_handle* h, dbi_comm* c, const double* d_mass, const do
         return rc;
     DBI_HIP(launch_qcombine(h->qpairB.p, h->qback.p, sh.q_pairs, d_first, d_count, sh.q_n, s));
     DBI_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+int dbi_shard_replicate_local(dbi_handle* const* hs, int nshards) {
+    if (!hs || nshards < 1) return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    SliceSizes z;
+    uint64_t g_total = 0, g_dropped = 0, g_keys = 0;
+    for (int i = 0; i < nshards; ++i) {
+        if (!hs[i]) return set_error(DBI_E_INVALID, "NULL handle");
+        if (hs[i]->shard.phase != 4 || hs[i]->shard.nshards != nshards || hs[i]->shard.rank != i)
+            return set_error(DBI_E_STATE, "dbi_shard_replicate_local: hs[i] must be merged shard i of nshards");
+        z.u.push_back(hs[i]->stats.n_unique);
+        z.k.push_back(hs[i]->stats.n_kept);
+        g_total += hs[i]->shard.n_total;
+        g_dropped += hs[i]->shard.n_dropped;
+        g_keys += hs[i]->stats.n_keys;
+    }
+    slice_bases(z);
+    if ((rc = replica_check(z))) return rc;
+    std::vector<std::unique_lock<std::recursive_mutex>> locks;
+    for (int i = 0; i < nshards; ++i) locks.emplace_back(hs[i]->qmu);
+    for (int j = 0; j < nshards; ++j) {
+        dbi_handle* o = hs[j];
+        DBI_HIP(hipSetDevice(o->device));
+        if ((rc = replica_alloc(o, z))) return rc;
+        hipStream_t s = o->stream;
+        for (int i = 0; i < nshards; ++i) {
+            const dbi_handle* src = hs[i];
+            const uint64_t u = z.u[i], k = z.k[i], ub = z.ub[i];
+            if (u) {
+                DBI_HIP(hipMemcpyAsync(o->r_mass.p + ub, src->umass.p, 8 * u, hipMemcpyDeviceToDevice, s));
+                DBI_HIP(hipMemcpyAsync(o->r_pid.p + ub, src->upid.p, 4 * u, hipMemcpyDeviceToDevice, s));
+                DBI_HIP(hipMemcpyAsync(o->r_off.p + ub, src->uoff.p, 4 * u, hipMemcpyDeviceToDevice, s));
+                DBI_HIP(hipMemcpyAsync(o->r_len.p + ub, src->ulen.p, 4 * u, hipMemcpyDeviceToDevice, s));
+                DBI_HIP(hipMemcpyAsync(o->r_occ_off.p + ub, src->occ_off.p, 4 * u, hipMemcpyDeviceToDevice, s));
+            }
+            if (k) DBI_HIP(hipMemcpyAsync(o->r_occ.p + z.kb[i], src->occ_pid.p, 4 * k, hipMemcpyDeviceToDevice, s));
+        }
+        if ((rc = replica_rebase(o, z, s))) return rc;
+    }
+    for (int j = 0; j < nshards; ++j) replica_install(hs[j], z, g_total, g_dropped, g_keys);
+    return 0;
+}
+
+int dbi_shard_replicate(dbi_handle* h, dbi_comm* c) {
+    if (!h || !c) return set_error(DBI_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = query_need(h))) return rc;  // same verdict on every rank of a consistent job
+    if (h->shard.nshards != c->nranks || h->shard.rank != c->rank)
+        return set_error(DBI_E_INVALID, "communicator does not match the sharded build");
+    std::lock_guard<std::recursive_mutex> lock(h->qmu);
+    DBI_HIP(hipSetDevice(h->device));
+    ShardState& sh = h->shard;
+    hipStream_t s = h->stream;
+    const int n = c->nranks, me = c->rank;
+    // every slice's size (two columns of the count matrix)
+    std::vector<uint64_t> mine(n, 0), all;
+    mine[0] = h->stats.n_unique;
+    if (n > 1) mine[1] = h->stats.n_kept;
+    bool failed = false;
+    SliceSizes z;
+    if (n > 1) {
+        if ((rc = nccl_count_matrix(h, c, mine, 0, all, &failed))) return rc;
+        for (int i = 0; i < n; ++i) {
+            z.u.push_back(all[(size_t)i * n]);
+            z.k.push_back(all[(size_t)i * n + 1]);
+        }
+    } else {
+        z.u.push_back(h->stats.n_unique);
+        z.k.push_back(h->stats.n_kept);
+    }
+    slice_bases(z);
+    if ((rc = replica_check(z))) return rc;
+    const int rc_local = replica_alloc(h, z);
+    if ((rc = agree(c, rc_local, s, &failed))) return rc;
+    if (rc_local) return rc_local;
+    if (failed) return peer_failed("replica buffers");
+    // every array of every slice to every rank: one group of point-to-point
+    // transfers over all xGMI links; the own slice by a copy
+    struct Arr { void* src; uint8_t* dst; size_t esz; bool occ; };
+    const Arr arrs[] = {
+        {h->umass.p, (uint8_t*)h->r_mass.p, 8, false}, {h->upid.p, (uint8_t*)h->r_pid.p, 4, false},
+        {h->uoff.p, (uint8_t*)h->r_off.p, 4, false},   {h->ulen.p, (uint8_t*)h->r_len.p, 4, false},
+        {h->occ_off.p, (uint8_t*)h->r_occ_off.p, 4, false}, {h->occ_pid.p, (uint8_t*)h->r_occ.p, 4, true},
+    };
+    for (const Arr& a : arrs) {
+        const uint64_t cnt = a.occ ? z.k[me] : z.u[me], base = a.occ ? z.kb[me] : z.ub[me];
+        if (cnt) DBI_HIP(hipMemcpyAsync(a.dst + base * a.esz, a.src, cnt * a.esz, hipMemcpyDeviceToDevice, s));
+    }
+    DBI_NCCL(ncclGroupStart());
+    for (const Arr& a : arrs)
+        for (int p = 0; p < n; ++p) {
+            if (p == me) continue;
+            const uint64_t mc = a.occ ? z.k[me] : z.u[me];
+            const uint64_t pc = a.occ ? z.k[p] : z.u[p], pb = a.occ ? z.kb[p] : z.ub[p];
+            if (mc) DBI_NCCL(ncclSend(a.src, mc * a.esz, ncclUint8, p, c->comm, s));
+            if (pc) DBI_NCCL(ncclRecv(a.dst + pb * a.esz, pc * a.esz, ncclUint8, p, c->comm, s));
+        }
+    DBI_NCCL(ncclGroupEnd());
+    if ((rc = replica_rebase(h, z, s))) return rc;
+    replica_install(h, z, sh.global.g_total, sh.global.g_dropped, sh.global.g_keys);
     return 0;
 }
 

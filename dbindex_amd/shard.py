@@ -13,6 +13,9 @@ whole proteome, identical row for row to a single-device build.
   travels through any out-of-band channel (``torch.distributed`` gloo here).
 * ``build_sharded_local`` — every shard's handle in one process, exchange by
   device copies (tests; the same phases the RCCL driver runs).
+* ``replicate`` / ``replicate_local`` — the owners' slices all-gathered onto
+  every rank (north_star's all-gatherv): each handle then holds the whole
+  index and answers queries locally.
 * ``protein_ranges`` / ``owner_of`` / ``concat_exports`` — host logic shared by
   both drivers and the CPU tests.
 """
@@ -197,3 +200,16 @@ def query_sharded_local(engines: Sequence[Engine], batches: Sequence[Tuple[np.nd
     hs = (ctypes.c_void_p * n)(*[e.h.value for e in engines])
     check(_native.lib().dbi_query_sharded_local(hs, n, arr(0), arr(1), _p(nq), arr(2), arr(3)))
     return [(b[2].download(np.uint64, b[4]), b[3].download(np.uint64, b[4])) for b in bufs]
+
+
+def replicate(eng: Engine, comm: ShardComm) -> None:
+    """Every owner's slice onto every rank over RCCL (dbi_shard_replicate): the
+    engine then holds the index of the whole proteome and queries locally."""
+    check(_native.lib().dbi_shard_replicate(eng.h, comm.h))
+
+
+def replicate_local(engines: Sequence[Engine]) -> None:
+    """dbi_shard_replicate_local: the same between the handles of this process."""
+    n = len(engines)
+    hs = (ctypes.c_void_p * n)(*[e.h.value for e in engines])
+    check(_native.lib().dbi_shard_replicate_local(hs, n))

@@ -335,6 +335,19 @@ int dbi_shard_stats_get(dbi_handle* h, dbi_shard_stats* out);
  * index (the owners' unique tables concatenated in shard order). */
 int dbi_query_sharded(dbi_handle* h, dbi_comm* c, const double* d_mass, const double* d_tol, uint64_t nq,
                       uint64_t* d_first, uint64_t* d_count);
+/* Replicated index — BASELINE.json north_star's all-gatherv of the sorted
+ * mass index over xGMI: after a sharded build (phase 4 on every rank), every
+ * rank receives every owner's unique table and occurrence CSR (one group of
+ * point-to-point transfers over all peers).  The handle then holds the index
+ * of the whole proteome, identical to a single-device build, and answers every
+ * query locally (dbi_query*, dbi_query_hits_device, dbi_export, dbi_peptides,
+ * dbi_entry_keys) with no exchange per batch; routed queries
+ * (dbi_query_sharded) no longer apply.  At most 2^32-2 occurrences per device.
+ * Collective: every rank calls it.  _local: the shards' handles of one
+ * process, by device copies (tests). */
+int dbi_shard_replicate(dbi_handle* h, dbi_comm* c);
+int dbi_shard_replicate_local(dbi_handle* const* hs, int nshards);
+
 /* The same over the handles of one process: shard i's batch is
  * (d_mass[i], d_tol[i], nq[i]) with results in (d_first[i], d_count[i]). */
 int dbi_query_sharded_local(dbi_handle* const* hs, int nshards, const double* const* d_mass,

@@ -215,3 +215,55 @@ def test_sharded_rccl_local_failure_is_reported(native, phase, monkeypatch):
             assert np.array_equal(c, oc) and np.array_equal(f[oc > 0], of[oc > 0])
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("k,nprot", [(1, 300), (3, 1000), (5, 1000)])
+def test_replicated_index_local(native, k, nprot):
+    """North star's all-gatherv: after a sharded build, every shard's handle
+    receives every owner's slice (dbi_shard_replicate_local) and then IS the
+    single-device index of the whole proteome: the oracle's index bit for bit,
+    and local queries (range lookup and materialised hits) answer for it."""
+    from dbindex_amd.engine import Engine
+    from tests.helpers import assert_index_equal, assert_queries_equal
+    pp = fasta.config("1k").slice(0, nprot)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    d_res, d_off = _inputs(native, pp)
+    engines = [Engine(cp, 0) for _ in range(k)]
+    try:
+        for rep in ("cold", "warm"):
+            shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
+                                      shard.protein_ranges(pp.offsets, k))
+            shard.replicate_local(engines)
+            m, t = query_masses(oix, 800)
+            for r, e in enumerate(engines):
+                assert_index_equal(e, oix, f"replica {r}/{k} [{rep}]")
+                assert_queries_equal(e, oix, m, t, f"replica {r}/{k} [{rep}]")
+            h = engines[-1].query_hits(m[:50], t[:50])
+            o = oix.unique()
+            for i in range(50):
+                exp = oix.query(float(m[i]), float(t[i]))
+                assert np.array_equal(h["ids"][h["row"][i]:h["row"][i + 1]].astype(np.uint64), exp)
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_replicated_index_rccl_single_rank(native):
+    from dbindex_amd.engine import Engine
+    from tests.helpers import assert_index_equal, assert_queries_equal
+    pp = fasta.config("1k")
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    d_res, d_off = _inputs(native, pp)
+    comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
+    try:
+        with Engine(cp, 0) as eng:
+            for rep in ("cold", "warm"):
+                shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, 0, pp.n_proteins)
+                shard.replicate(eng, comm)
+                assert_index_equal(eng, oix, f"rccl replica [{rep}]")
+                m, t = query_masses(oix, 1000)
+                assert_queries_equal(eng, oix, m, t, f"rccl replica [{rep}]")
+    finally:
+        comm.close()

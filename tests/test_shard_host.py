@@ -119,22 +119,37 @@ def _rank_main(rank: int, world: int, port: int, cfg: str, nprot: int, missed: i
         keys = oix.entry_keys()
         sums = torch.tensor([n_total, n_dropped, oix.n_unique, oix.n_keys], dtype=torch.int64)
         dist.all_reduce(sums)
+        # 5. replicated index (dbi_shard_replicate): every owner's slice on
+        # every rank, which then holds the whole index and answers locally
         parts = [None] * world
         dist.all_gather_object(parts, (part, keys))
-        if rank == 0:
-            ref = cref.Index(cp, pp.residues, pp.offsets)
-            g = shard.concat_exports([p for p, _ in parts])
-            o = ref.unique()
-            assert sums.tolist() == [ref.n_total, ref.n_dropped, ref.n_unique, ref.n_keys]
-            assert np.array_equal(g["mass"].view(np.uint64), o["mass"].view(np.uint64))
-            for k in ("prot_id", "offset", "length", "occ_off", "occ_prot"):
-                assert np.array_equal(g[k].astype(np.uint64), o[k].astype(np.uint64)), k
-            assert np.array_equal(np.concatenate([k for _, k in parts]), ref.entry_keys())
+        ref = cref.Index(cp, pp.residues, pp.offsets)
+        g = shard.concat_exports([p for p, _ in parts])
+        o = ref.unique()
+        assert sums.tolist() == [ref.n_total, ref.n_dropped, ref.n_unique, ref.n_keys]
+        assert np.array_equal(g["mass"].view(np.uint64), o["mass"].view(np.uint64))
+        for k in ("prot_id", "offset", "length", "occ_off", "occ_prot"):
+            assert np.array_equal(g[k].astype(np.uint64), o[k].astype(np.uint64)), k
+        assert np.array_equal(np.concatenate([k for _, k in parts]), ref.entry_keys())
+        # this rank's own query batch, answered on its replica alone: a window's
+        # hits are the replica rows with lo <= mass <= hi (both ends inclusive)
+        rng = np.random.Generator(np.random.PCG64(17 + rank))
+        m = g["mass"][rng.integers(0, g["mass"].shape[0], 300)] * (1 + rng.normal(0, 5e-6, 300))
+        tol = m * (1 - 1 / (20.0 / 1e6 + 1))
+        of, oc = ref.query_batch(m, tol)
+        lo = np.searchsorted(g["mass"], m - tol, side="left")
+        hi = np.searchsorted(g["mass"], m + tol, side="right")
+        assert np.array_equal((hi - lo).astype(np.uint64), oc)
+        assert np.array_equal(lo[oc > 0].astype(np.uint64), of[oc > 0])
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg,nprot,missed,semi", [("1k", 1000, 2, False), ("1k", 200, 2, True)])
-def test_two_rank_gloo_plan_matches_single_store(cfg, nprot, missed, semi):
+@pytest.mark.parametrize("world,cfg,nprot,missed,semi", [(2, "1k", 1000, 2, False), (2, "1k", 200, 2, True),
+                                                        (3, "1k", 600, 1, False)])
+def test_gloo_strong_split_plan_matches_single_store(world, cfg, nprot, missed, semi):
+    """One proteome split by residues over `world` gloo ranks (bench.py
+    --scaling strong), owner exchange, owner merge, then the replicated index
+    on every rank answering its own queries."""
     import torch.multiprocessing as mp
-    mp.spawn(_rank_main, args=(2, _free_port(), cfg, nprot, missed, semi), nprocs=2, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), cfg, nprot, missed, semi), nprocs=world, join=True)
