@@ -4,18 +4,30 @@
 // left-to-right sum of DBIndexer.cutSeq (DBIndexer.java:265-308), i.e.
 // bit-identical to the reference's masses.
 //
-// Build pipeline (one stream):
-//   1. k_digest<COUNT>  — per 2048-start tile: residues + residue tables staged in
-//                          LDS, cleavage-site starts compacted with wave ballots,
-//                          one walk per site (cutSeq inner loop), per-tile count.
-//   2. scan of tile counts (insertion-order output offsets).
-//   3. k_digest<EMIT>   — same walk, block scan, 16-B records in insertion order.
-//   4. radix partition of records by mass bin (stable LSD passes, 8-bit digits).
-//   5. k_bin_sort       — per bin, bitonic sort by mass bits in LDS; equal-mass
-//                          runs grouped by peptide string (first appearance first),
-//                          unique-peptide heads flagged  (IndexMerge.getMergedData).
-//   6. scan of per-bin unique counts, k_finalize writes the unique table + the
-//                          occurrence CSR (protein ids, insertion order).
+// Build pipeline (one stream, dbi_engine.hip: run_digest + build_tail):
+//   0. k_tile_proteins    — first/last protein of every 4096-start digest tile,
+//                            longest protein (the record field width).
+//   1. k_digest_bounded   — (full enzyme, mc <= 2, warm builds) per tile: window
+//                            staged in LDS, cut / cleave / protein-start bit maps,
+//                            cleavage-site starts compacted, each start's slot
+//                            bound reserved by decoupled look-back, one cutSeq walk
+//                            per start writing 16-B records (Rec) straight into
+//                            them, sentinels in the unused slots.
+//      k_digest_fused     — (semi / mandatory residues / mc > 2) count walk,
+//                            look-back over exact tile totals, emit walk.
+//      k_digest<COUNT|EMIT> + scan — cold builds (no capacity known yet).
+//   2. LSD radix passes over the fine mass bin (k_radix_hist[_u8] + scan +
+//      k_radix_scatter): 3 passes of <= 8 bits at SwissProt scale; each pass
+//      but the last writes the next pass's digit bytes for the next histogram.
+//   3. k_chunk_bounds     — chunks of whole bins, ~CHUNK_T records each.
+//   4. k_chunk_sort (<= CHUNK_CAP records, LDS), k_chunk_sort_big (<= BIG_CAP),
+//      k_giant_* (MSD split) — sort by the 128-bit record key (mass, tag, first
+//      appearance), string-verify equal (mass, tag) neighbours, flag unique
+//      heads (IndexMerge.getMergedData).
+//   5. scan of per-chunk unique counts, k_finalize: unique table + occurrence
+//      CSR (protein ids, insertion order) + distinct mass-key count.
+// Queries: k_qdir_* (query directory), k_query (range per window),
+// k_hits_* (materialised hits), k_query_pairs / k_qroute_* (sharded index).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
