@@ -1416,9 +1416,11 @@ k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t*
     }
 }
 
-template <bool SPARSE, typename Digit>
+// NARROW: only the second word q1 of each record (after xform) is written, as
+// one u64 per record (the owner exchange of a sharded build: 8 B on the wire)
+template <bool SPARSE, typename Digit, bool NARROW = false>
 __global__ void __launch_bounds__(RADIX_THREADS)
-k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, Digit dig, int bits,
+k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, Digit dig, int bits,
                 const uint32_t* __restrict__ offs, uint8_t* __restrict__ nd_out, int nshift, uint32_t nmask) {
     static_assert(RADIX_D <= RADIX_THREADS, "one digit per thread");
     __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
@@ -1484,12 +1486,14 @@ k_radix_scatter(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t n, D
         if (vmask & (1u << k)) stage[cnt[w][dg[k]] + pos[k]] = rv[k];
     __syncthreads();
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
+    unsigned long long* __restrict__ out8 = reinterpret_cast<unsigned long long*>(out);
     for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) {
         uint4 r = stage[t];
         const uint32_t dr = dig(u4_q0(r));
         if (nd_out) nd_out[gofs[dr] + t] = (uint8_t)dig.next(u4_q0(r), nshift, nmask);
         dig.xform(r);
-        out4[gofs[dr] + t] = r;
+        if (NARROW) out8[gofs[dr] + t] = u4_q1(r);
+        else out4[gofs[dr] + t] = r;
     }
 }
 
@@ -1548,9 +1552,81 @@ hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bo
     return radix_hist(d_in, n, OwnerDigit{om}, owner_bits(om.nshards), sparse, d_hist, s);
 }
 
-hipError_t launch_owner_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const OwnerMap& om, bool sparse,
+hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, const OwnerMap& om, bool sparse,
                                 const uint32_t* d_hist, hipStream_t s) {
-    return radix_scatter(d_in, d_out, n, OwnerDigit{om}, owner_bits(om.nshards), sparse, d_hist, s);
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    const OwnerDigit dig{om};
+    const int bits = owner_bits(om.nshards);
+    if (sparse)
+        DBI_LAUNCH((k_radix_scatter<true, OwnerDigit, true>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, (void*)d_out,
+                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u);
+    else
+        DBI_LAUNCH((k_radix_scatter<false, OwnerDigit, true>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, (void*)d_out,
+                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u);
+    return hipGetLastError();
+}
+
+// Owner side of the exchange: the (global protein, offset, length) word of
+// each received occurrence -> its 16-B record, the mass and the tag
+// recomputed from the residues exactly as the digest walk sums them
+// (DBIndexer.java:265-308: m0, then one fp64 add per residue, left to right;
+// -ffp-contract=off), so the record is bit-identical to the sender's.
+constexpr uint32_t EXPAND_THREADS = 256;
+__global__ void __launch_bounds__(EXPAND_THREADS)
+k_expand_locs(const unsigned long long* __restrict__ locs, uint64_t n, const uint8_t* __restrict__ res,
+              const uint32_t* __restrict__ poff, const double* __restrict__ mass_tab, double m0, uint32_t w,
+              Rec* __restrict__ out) {
+    __shared__ double smass[256];
+    for (uint32_t c = threadIdx.x; c < 256; c += EXPAND_THREADS) smass[c] = mass_tab[c];
+    __syncthreads();
+    // dword view of the residues (a buffer not 4-B aligned is read from the dword holding its first byte)
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(res) & 3u);
+    const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(res - mis);
+    for (uint64_t i = (uint64_t)blockIdx.x * EXPAND_THREADS + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * EXPAND_THREADS) {
+        const uint64_t q1 = locs[i];
+        const uint32_t len = q1_len(q1, w);
+        // residues 16 at a time: the 5 dwords covering them loaded together
+        // (clamped to the peptide's last dword) and realigned, as seq_equal_at
+        const uint64_t ga = (uint64_t)poff[q1_pid(q1, w)] + q1_off(q1, w) + mis;
+        const uint64_t last = (ga + len - 1) >> 2;
+        double m = m0;
+        uint32_t h = FNV32_OFFSET;
+        for (uint32_t k0 = 0; k0 < len; k0 += 16) {
+            const uint64_t ia = (ga + k0) >> 2;
+            uint32_t wd[5];
+#pragma unroll
+            for (uint32_t j = 0; j < 5; ++j) wd[j] = w32[min(ia + j, last)];
+            const uint32_t sa = (uint32_t)((ga + k0) & 3u);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t x = __builtin_amdgcn_alignbyte(wd[j + 1], wd[j], sa);
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) {
+                    if (k0 + 4 * j + b < len) {  // sequential, left to right (DBIndexer.java:306-308)
+                        const uint32_t c = (x >> (8 * b)) & 0xFFu;
+                        m = m + smass[c];
+                        h = fnv32_step(h, c);
+                    }
+                }
+            }
+        }
+        const uint32_t tag = fold_tag(h);
+        Rec r;
+        r.q0 = rec_q0(m, tag);
+        r.q1 = ((uint64_t)(tag & 0xFFu) << 56) | (q1 & 0x00FFFFFFFFFFFFFFull);  // pid | off | len as sent
+        out[i] = r;
+    }
+}
+
+hipError_t launch_expand_locs(const uint64_t* d_locs, uint64_t n, const uint8_t* d_res, const uint32_t* d_poff,
+                              const double* d_mass_tab, double m0, uint32_t w, Rec* d_out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (uint32_t)std::min<uint64_t>((n + EXPAND_THREADS - 1) / EXPAND_THREADS, 256u * 16u);
+    DBI_LAUNCH(k_expand_locs, dim3(g), dim3(EXPAND_THREADS), 0, s, (const unsigned long long*)d_locs, n, d_res,
+               d_poff, d_mass_tab, m0, w, d_out);
+    return hipGetLastError();
 }
 
 hipError_t launch_pair_hist(const Rec* d_in, uint32_t n, uint32_t nshards, uint32_t* d_hist, hipStream_t s) {

@@ -158,6 +158,7 @@ struct dbi_handle {
 
     dbi_stats stats{};
     dbi::ShardState shard;
+    DevBuf<uint64_t> xsend, xrecv;      // sharded build: 8-B location words to / from the owners
     DevBuf<double> samp;                // sharded build: mass samples (splitters)
     DevBuf<unsigned long long> xcount;  // sharded build: send counts of every shard (RCCL all-gather)
     DevBuf<uint32_t> qcnt;              // sharded queries: owners per query -> pair offsets

@@ -529,7 +529,7 @@ void dbi_close(dbi_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
     h->res.release(); h->poff64.release(); h->poff.release(); h->poff_g.release();
-    h->samp.release(); h->xcount.release();
+    h->samp.release(); h->xcount.release(); h->xsend.release(); h->xrecv.release();
     h->qcnt.release(); h->qpairA.release(); h->qpairB.release(); h->qsend.release(); h->qrecv.release();
     h->qres.release(); h->qback.release(); h->blk.release(); h->scan_tmp.release();
     h->status.release(); h->win_lo.release(); h->win_hi.release(); h->qdir.release(); h->qdir_par.release();

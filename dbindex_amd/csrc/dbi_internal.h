@@ -240,8 +240,13 @@ uint64_t radix_blocks(uint32_t n);
 // stable partition pass by owner shard (digit = OwnerDigit), global protein ids out
 hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bool sparse, uint32_t* d_hist,
                              hipStream_t s);
-hipError_t launch_owner_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const OwnerMap& om, bool sparse,
+// writes the second record word only (global protein | offset | length), 8 B
+// per record: the owner recomputes mass and tag from the residues
+hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, const OwnerMap& om, bool sparse,
                                 const uint32_t* d_hist, hipStream_t s);
+// owner side: 8-B location words -> 16-B records (mass and tag from the residues)
+hipError_t launch_expand_locs(const uint64_t* d_locs, uint64_t n, const uint8_t* d_res, const uint32_t* d_poff,
+                              const double* d_mass_tab, double m0, uint32_t w, Rec* d_out, hipStream_t s);
 // stable partition of query routing pairs (q0 = owner, q1 = query index) by owner
 hipError_t launch_pair_hist(const Rec* d_in, uint32_t n, uint32_t nshards, uint32_t* d_hist, hipStream_t s);
 hipError_t launch_pair_scatter(const Rec* d_in, Rec* d_out, uint32_t n, uint32_t nshards, const uint32_t* d_hist,

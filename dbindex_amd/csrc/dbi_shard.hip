@@ -13,7 +13,9 @@
 // owner's result is a pure function of the set of records it receives, so the
 // order in which shards' records arrive does not matter.
 //
-// Exchange: RCCL point-to-point sends/receives grouped over all peers (each
+// Exchange: 8 B per record (global protein | offset | length; the owner
+// recomputes mass and tag from the residues, k_expand_locs), RCCL
+// point-to-point sends/receives grouped over all peers (each
 // pair of MI355X GPUs has its own xGMI link, so the grouped exchange drives
 // all links at once; a ring would serialise them), or device copies between
 // the handles of one process (dbi_shard_exchange_local).
@@ -96,19 +98,20 @@ void key_range(const int32_t* split, int nshards, int r, int32_t* lo, int32_t* h
     *hi = r == nshards - 1 ? INT32_MAX : split[r];
 }
 
-// 16-B items from every rank to every rank: item slices [soff[p], +scnt[p]) of
+// Items from every rank to every rank: item slices [soff[p], +scnt[p]) of
 // `send` go to rank p, which receives them at its roff[me]; one group of
 // point-to-point transfers over all peers, the rank's own slice by a copy
-int nccl_alltoallv(dbi_comm* c, const Rec* send, const std::vector<uint64_t>& soff, const std::vector<uint64_t>& scnt,
-                   Rec* recv, const std::vector<uint64_t>& roff, const std::vector<uint64_t>& rcnt, hipStream_t s) {
+template <typename T>
+int nccl_alltoallv(dbi_comm* c, const T* send, const std::vector<uint64_t>& soff, const std::vector<uint64_t>& scnt,
+                   T* recv, const std::vector<uint64_t>& roff, const std::vector<uint64_t>& rcnt, hipStream_t s) {
     const int me = c->rank;
     if (scnt[me])
-        DBI_HIP(hipMemcpyAsync(recv + roff[me], send + soff[me], scnt[me] * sizeof(Rec), hipMemcpyDeviceToDevice, s));
+        DBI_HIP(hipMemcpyAsync(recv + roff[me], send + soff[me], scnt[me] * sizeof(T), hipMemcpyDeviceToDevice, s));
     DBI_NCCL(ncclGroupStart());
     for (int p = 0; p < c->nranks; ++p) {
         if (p == me) continue;
-        if (scnt[p]) DBI_NCCL(ncclSend(send + soff[p], scnt[p] * sizeof(Rec), ncclUint8, p, c->comm, s));
-        if (rcnt[p]) DBI_NCCL(ncclRecv(recv + roff[p], rcnt[p] * sizeof(Rec), ncclUint8, p, c->comm, s));
+        if (scnt[p]) DBI_NCCL(ncclSend(send + soff[p], scnt[p] * sizeof(T), ncclUint8, p, c->comm, s));
+        if (rcnt[p]) DBI_NCCL(ncclRecv(recv + roff[p], rcnt[p] * sizeof(T), ncclUint8, p, c->comm, s));
     }
     DBI_NCCL(ncclGroupEnd());
     return 0;
@@ -452,7 +455,7 @@ int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_coun
     const uint32_t n_in = (uint32_t)sh.n_in;
     const uint64_t g = radix_blocks(n_in);
     const size_t hist_elems = std::max<size_t>(radix_hist_elems(n_in, bits), 1);
-    if ((rc = h->hist.ensure(hist_elems)) || (rc = h->recB.ensure(std::max<uint64_t>(sh.n_digest, 1))) ||
+    if ((rc = h->hist.ensure(hist_elems)) || (rc = h->xsend.ensure(std::max<uint64_t>(sh.n_digest, 1))) ||
         (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(hist_elems), h->scan_tmp.cap))))
         return rc;
     std::vector<uint32_t> start(ns + 1, 0);
@@ -462,8 +465,8 @@ int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_coun
         STAGE(h, "owner_scan", by(0, 0, 0, 0, 0),
               launch_scan_u32(h->hist.p, h->hist.p, g << bits, h->scan_tmp.p, h->scan_tmp.cap, nullptr, s));
         STAGE(h, "owner_scatter", by(0, 0, 0, 0, 0),
-              launch_owner_scatter(h->recA.p, h->recB.p, n_in, om, sh.sparse, h->hist.p, s));
-        h->stages[h->nstage - 1].c0 = 16.0 * (double)(sh.sparse ? n_in : sh.n_digest) + 16.0 * (double)sh.n_digest;
+              launch_owner_scatter(h->recA.p, h->xsend.p, n_in, om, sh.sparse, h->hist.p, s));
+        h->stages[h->nstage - 1].c0 = 16.0 * (double)(sh.sparse ? n_in : sh.n_digest) + 8.0 * (double)sh.n_digest;
         // first output position of every owner's run: hist[d * g] after the scan
         DBI_HIP(hipMemcpy2DAsync(start.data(), sizeof(uint32_t), h->hist.p, g * sizeof(uint32_t), sizeof(uint32_t),
                                  (size_t)ns, hipMemcpyDeviceToHost, s));
@@ -503,15 +506,15 @@ int dbi_shard_exchange_local(dbi_handle* const* hs, int nshards) {
             if (i != j) from_others += sh.recv_count[i];
         }
         DBI_HIP(hipSetDevice(o->device));
-        DBI_HIP(hipStreamSynchronize(o->stream));  // recA (the digest slots) is free: partition read it
-        if ((rc = o->recA.ensure(std::max<uint64_t>(tot, 1)))) return rc;
-        ManualStage ms(o, "exchange", 16.0 * (double)(from_others + (sh.n_digest - sh.send_count[j])));
+        DBI_HIP(hipStreamSynchronize(o->stream));
+        if ((rc = o->xrecv.ensure(std::max<uint64_t>(tot, 1)))) return rc;
+        ManualStage ms(o, "exchange", 8.0 * (double)(from_others + (sh.n_digest - sh.send_count[j])));
         uint64_t off = 0;
         for (int i = 0; i < nshards; ++i) {
             const uint64_t c = sh.recv_count[i];
             if (c)
-                DBI_HIP(hipMemcpyAsync(o->recA.p + off, hs[i]->recB.p + hs[i]->shard.send_off[j], c * sizeof(Rec),
-                                       hipMemcpyDeviceToDevice, o->stream));
+                DBI_HIP(hipMemcpyAsync(o->xrecv.p + off, hs[i]->xsend.p + hs[i]->shard.send_off[j],
+                                       c * sizeof(uint64_t), hipMemcpyDeviceToDevice, o->stream));
             off += c;
         }
         ms.end();
@@ -541,6 +544,11 @@ int dbi_shard_merge(dbi_handle* h) {
     DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
     const unsigned long long kept = sh.n_recv;
     DBI_HIP(hipMemcpyAsync(&h->ctr.p->n_kept, &kept, sizeof(kept), hipMemcpyHostToDevice, s));
+    // the received location words -> records (mass + tag from the residues)
+    if ((rc = h->recA.ensure(std::max<uint64_t>(sh.n_recv, 1)))) return rc;
+    STAGE(h, "owner_expand", by(0, 0, 0, 0, 0),
+          launch_expand_locs(h->xrecv.p, sh.n_recv, h->d_res, h->d_poff, h->mass_tab.p, h->dp.m0, sh.width, h->recA.p, s));
+    h->stages[h->nstage - 1].c0 = 24.0 * (double)sh.n_recv;  // 8 B in, 16 B out (+ the residues)
     DBI_HIP(hipStreamSynchronize(s));  // `kept` is a stack value
     int32_t klo, khi;
     key_range(sh.split, sh.nshards, sh.rank, &klo, &khi);
@@ -908,7 +916,7 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     std::vector<uint64_t> roff;
     offsets_of(sh.recv_count, roff);
     if (sh.send_count[me] != sh.recv_count[me]) return set_error(DBI_E_STATE, "shard count exchange mismatch");
-    rc_local = h->recA.ensure(std::max<uint64_t>(roff[n], 1));  // digest slots are free after partition
+    rc_local = h->xrecv.ensure(std::max<uint64_t>(roff[n], 1));
     if (!rc_local) rc_local = injected_failure("buffers", me);
     if ((rc = agree(c, rc_local, s, &failed))) return rc;
     if (rc_local) return rc_local;
@@ -916,8 +924,8 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
 
     // records to their owners: one group of point-to-point transfers over all peers
     {
-        ManualStage ms(h, "exchange", 16.0 * (double)(from_others + (sh.n_digest - sh.send_count[me])));
-        if ((rc = nccl_alltoallv(c, h->recB.p, sh.send_off, sh.send_count, h->recA.p, roff, sh.recv_count, s)))
+        ManualStage ms(h, "exchange", 8.0 * (double)(from_others + (sh.n_digest - sh.send_count[me])));
+        if ((rc = nccl_alltoallv(c, h->xsend.p, sh.send_off, sh.send_count, h->xrecv.p, roff, sh.recv_count, s)))
             return rc;
         ms.end();
     }
