@@ -63,7 +63,8 @@ struct ShardState {
     uint64_t n_total = 0, n_dropped = 0;    // this shard's digest: totalSeqCount, bucket drops
     uint32_t width = 0;                     // global record field width W
     int32_t split[MAX_SHARDS - 1] = {};
-    std::vector<uint64_t> send_count, send_off;  // per owner, records in recB
+    std::vector<uint64_t> send_count, send_off;  // per owner, location words in xsend
+    uint64_t part_blocks = 0;                    // radix blocks of the owner partition (hist stride)
     std::vector<uint64_t> recv_count;            // per source shard
     uint64_t n_recv = 0;
     double ms_digest = 0, ms_partition = 0, ms_exchange = 0, ms_merge = 0;

@@ -71,6 +71,21 @@ int need_phase(const dbi_handle* h, int phase, const char* what) {
     return 0;
 }
 
+__global__ void k_set_u64(unsigned long long* p, unsigned long long v) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *p = v;
+}
+
+// send counts of a partitioned shard, straight from the scanned owner
+// histogram (hist[d * g] = first output position of owner d's run)
+__global__ void k_owner_counts(const uint32_t* __restrict__ hist, uint64_t g, uint32_t ns, uint64_t n_total,
+                               unsigned long long* __restrict__ out) {
+    const uint32_t d = threadIdx.x;
+    if (d >= ns) return;
+    const uint64_t a = n_total ? hist[(uint64_t)d * g] : 0u;
+    const uint64_t b = (d + 1 < ns && n_total) ? hist[(uint64_t)(d + 1) * g] : n_total;
+    out[d] = b - a;
+}
+
 // Stage whose time comes from events recorded around non-kernel work (RCCL,
 // copies) rather than from a dispatch packet; `bytes` = bytes this rank moves.
 struct ManualStage {
@@ -436,15 +451,19 @@ int dbi_shard_splitters(const double* samples, int nshards, int32_t factor, int3
     return 0;
 }
 
-int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_count) {
-    if (!h || (!split && h->shard.nshards > 1)) return set_error(DBI_E_INVALID, "NULL argument");
+}  // extern "C"
+
+namespace dbi {
+namespace {
+// The partition's kernels (no host synchronisation): records routed to
+// xsend by owner; the scanned owner histogram is left in h->hist
+int partition_launch(dbi_handle* h, const int32_t* split) {
     int rc;
     if ((rc = need_phase(h, 1, "dbi_shard_partition"))) return rc;
     ShardState& sh = h->shard;
     const int ns = sh.nshards;
     for (int j = 0; j + 2 < ns; ++j)
         if (split[j] > split[j + 1]) return set_error(DBI_E_INVALID, "splitter keys must be non-decreasing");
-    const double t0 = now_ms();
     hipStream_t s = h->stream;
     OwnerMap om{};
     for (int j = 0; j + 1 < ns; ++j) om.split[j] = sh.split[j] = split[j];
@@ -458,7 +477,6 @@ int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_coun
     if ((rc = h->hist.ensure(hist_elems)) || (rc = h->xsend.ensure(std::max<uint64_t>(sh.n_digest, 1))) ||
         (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(hist_elems), h->scan_tmp.cap))))
         return rc;
-    std::vector<uint32_t> start(ns + 1, 0);
     if (n_in > 0) {
         STAGE(h, "owner_hist", by(0, 0, 0, 0, 0), launch_owner_hist(h->recA.p, n_in, om, sh.sparse, h->hist.p, s));
         h->stages[h->nstage - 1].c0 = 8.0 * (double)n_in;
@@ -467,6 +485,35 @@ int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_coun
         STAGE(h, "owner_scatter", by(0, 0, 0, 0, 0),
               launch_owner_scatter(h->recA.p, h->xsend.p, n_in, om, sh.sparse, h->hist.p, s));
         h->stages[h->nstage - 1].c0 = 16.0 * (double)(sh.sparse ? n_in : sh.n_digest) + 8.0 * (double)sh.n_digest;
+    }
+    sh.part_blocks = g;
+    return 0;
+}
+
+// send counts / offsets from the whole count matrix's row of this shard
+void send_plan(ShardState& sh, const std::vector<uint64_t>& counts) {
+    const int ns = sh.nshards;
+    sh.send_count.assign(ns, 0);
+    sh.send_off.assign(ns, 0);
+    for (int d = 0; d < ns; ++d) sh.send_count[d] = counts[(size_t)sh.rank * ns + d];
+    for (int d = 1; d < ns; ++d) sh.send_off[d] = sh.send_off[d - 1] + sh.send_count[d - 1];
+}
+}  // namespace
+}  // namespace dbi
+
+extern "C" {
+
+int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_count) {
+    if (!h || (!split && h->shard.nshards > 1)) return set_error(DBI_E_INVALID, "NULL argument");
+    const double t0 = now_ms();
+    int rc;
+    if ((rc = partition_launch(h, split))) return rc;
+    ShardState& sh = h->shard;
+    const int ns = sh.nshards;
+    hipStream_t s = h->stream;
+    const uint64_t g = sh.part_blocks;
+    std::vector<uint32_t> start(ns + 1, 0);
+    if (sh.n_in > 0) {
         // first output position of every owner's run: hist[d * g] after the scan
         DBI_HIP(hipMemcpy2DAsync(start.data(), sizeof(uint32_t), h->hist.p, g * sizeof(uint32_t), sizeof(uint32_t),
                                  (size_t)ns, hipMemcpyDeviceToHost, s));
@@ -542,14 +589,14 @@ int dbi_shard_merge(dbi_handle* h) {
     h->n_total_extra = 0;
     // counters back to zero (the layout word max_plen stays), n_kept = records received
     DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
-    const unsigned long long kept = sh.n_recv;
-    DBI_HIP(hipMemcpyAsync(&h->ctr.p->n_kept, &kept, sizeof(kept), hipMemcpyHostToDevice, s));
-    // the received location words -> records (mass + tag from the residues)
+    hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(64), 0, s, &h->ctr.p->n_kept, (unsigned long long)sh.n_recv);
+    DBI_HIP(hipGetLastError());
+    // the received location words -> records (mass + tag from the residues);
+    // recA is free (the partition read it before the exchange was enqueued)
     if ((rc = h->recA.ensure(std::max<uint64_t>(sh.n_recv, 1)))) return rc;
     STAGE(h, "owner_expand", by(0, 0, 0, 0, 0),
           launch_expand_locs(h->xrecv.p, sh.n_recv, h->d_res, h->d_poff, h->mass_tab.p, h->dp.m0, sh.width, h->recA.p, s));
     h->stages[h->nstage - 1].c0 = 24.0 * (double)sh.n_recv;  // 8 B in, 16 B out (+ the residues)
-    DBI_HIP(hipStreamSynchronize(s));  // `kept` is a stack value
     int32_t klo, khi;
     key_range(sh.split, sh.nshards, sh.rank, &klo, &khi);
     const double f = (double)h->params.mass_group_factor;
@@ -863,42 +910,75 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     int rc;
     // a rank that fails locally still takes part in the next collective, with
     // its status, so that every rank returns an error (never a hang)
+    const double t_digest = now_ms();
     int rc_digest = dbi_shard_digest(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n);
     if (!rc_digest) rc_digest = injected_failure("digest", me);
     ShardState& sh = h->shard;
     hipStream_t s = h->stream;
 
-    // samples of every shard -> the same owner splitters everywhere; the word
-    // after the samples' weight carries the rank's status
+    // samples of every shard -> the same owner splitters everywhere.  Block
+    // of rank r: NS record masses (written on the device), its record count,
+    // its status; the sample weight (records per valid sample) on the host
     const size_t blk = NS + 2;
-    std::vector<double> samples((size_t)n * blk, 0.0);
-    int rc_local = rc_digest ? rc_digest : dbi_shard_samples(h, samples.data() + (size_t)me * blk);
-    samples[(size_t)me * blk + NS + 1] = rc_local ? 1.0 : 0.0;
+    int rc_local = rc_digest;
     if ((rc = h->samp.ensure((size_t)n * blk))) return rc;
-    DBI_HIP(hipMemcpyAsync(h->samp.p + (size_t)me * blk, samples.data() + (size_t)me * blk, sizeof(double) * blk,
-                           hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllGather(h->samp.p + (size_t)me * blk, h->samp.p, blk, ncclFloat64, c->comm, s));
+    double* my_blk = h->samp.p + (size_t)me * blk;
+    if (!rc_local) {
+        if ((rc = launch_sample_masses(h->recA.p, sh.n_in, NS, my_blk, s)) != hipSuccess)
+            rc_local = hip_fail((hipError_t)rc, "launch_sample_masses");
+    }
+    std::vector<double> samples((size_t)n * blk, 0.0);
+    samples[(size_t)me * blk + NS] = rc_local ? 0.0 : (double)sh.n_digest;
+    samples[(size_t)me * blk + NS + 1] = rc_local ? 1.0 : 0.0;
+    DBI_HIP(hipMemcpyAsync(my_blk + NS, &samples[(size_t)me * blk + NS], 2 * sizeof(double), hipMemcpyHostToDevice,
+                           s));
+    DBI_NCCL(ncclAllGather(my_blk, h->samp.p, blk, ncclFloat64, c->comm, s));
     DBI_HIP(hipMemcpyAsync(samples.data(), h->samp.p, sizeof(double) * n * blk, hipMemcpyDeviceToHost, s));
     DBI_HIP(hipStreamSynchronize(s));
     if (rc_local) return rc_local;
     std::vector<double> packed((size_t)n * (NS + 1));
     for (int r = 0; r < n; ++r) {
-        if (samples[(size_t)r * blk + NS + 1] != 0.0) return peer_failed("shard digest");
-        std::copy(samples.begin() + (size_t)r * blk, samples.begin() + (size_t)r * blk + NS + 1,
-                  packed.begin() + (size_t)r * (NS + 1));
+        const double* b = samples.data() + (size_t)r * blk;
+        if (b[NS + 1] != 0.0) return peer_failed("shard digest");
+        uint64_t valid = 0;
+        for (uint32_t i = 0; i < NS; ++i) valid += b[i] == b[i];
+        std::copy(b, b + NS, packed.begin() + (size_t)r * (NS + 1));
+        packed[(size_t)r * (NS + 1) + NS] = valid ? b[NS] / (double)valid : 0.0;  // as dbi_shard_samples
     }
     int32_t split[MAX_SHARDS - 1] = {};
     if ((rc = dbi_shard_splitters(packed.data(), n, h->params.mass_group_factor, split))) return rc;  // same everywhere
-    int rc_part = dbi_shard_partition(h, split, nullptr);
+    sh.ms_digest = now_ms() - t_digest;
+    const double t_part = now_ms();
+    int rc_part = partition_launch(h, split);
     if (!rc_part) rc_part = injected_failure("partition", me);
-    if (rc_part) sh.send_count.assign(n, 0);
 
-    // send counts of every shard: counts[i * n + j] = records shard i sends owner j
+    // count matrix: row r = records shard r sends each owner (from its owner
+    // histogram, on the device) | its status | its receive capacity
     const double t0 = now_ms();
-    std::vector<uint64_t> counts;
-    bool failed = false;
-    if ((rc = nccl_count_matrix(h, c, sh.send_count, rc_part, counts, &failed))) return rc;
+    const int w = n + 2;
+    if ((rc = h->xcount.ensure((size_t)n * w + 8))) return rc;
+    unsigned long long* my_row = h->xcount.p + (size_t)me * w;
+    if (!rc_part && sh.n_in > 0) {
+        hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(64), 0, s, h->hist.p, sh.part_blocks, (uint32_t)n,
+                           sh.n_digest, my_row);
+        if ((rc = hipGetLastError()) != hipSuccess) rc_part = hip_fail((hipError_t)rc, "k_owner_counts");
+    } else if ((rc = hipMemsetAsync(my_row, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) {
+        return hip_fail((hipError_t)rc, "hipMemsetAsync");
+    }
+    std::vector<unsigned long long> full((size_t)n * w, 0);
+    full[(size_t)me * w + n] = rc_part ? 1u : 0u;
+    full[(size_t)me * w + n + 1] = h->xrecv.cap;
+    DBI_HIP(hipMemcpyAsync(my_row + n, &full[(size_t)me * w + n], 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+    DBI_NCCL(ncclAllGather(my_row, h->xcount.p, w, ncclUint64, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(full.data(), h->xcount.p, sizeof(unsigned long long) * n * w, hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
     if (rc_part) return rc_part;
+    std::vector<uint64_t> counts((size_t)n * n);
+    bool failed = false, grow = false;
+    for (int i = 0; i < n; ++i) {
+        failed |= full[(size_t)i * w + n] != 0;
+        for (int j = 0; j < n; ++j) counts[(size_t)i * n + j] = full[(size_t)i * w + j];
+    }
     if (failed) return peer_failed("owner partition");
     // checks on the whole matrix: every rank reaches the same verdict
     for (int j = 0; j < n; ++j) {
@@ -906,7 +986,10 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
         for (int i = 0; i < n; ++i) tot += counts[(size_t)i * n + j];
         if (tot >= (1ull << 32) - 1)
             return set_error(DBI_E_INVALID, "more than 2^32-2 records for one owner: use more shards");
+        grow |= std::max<uint64_t>(tot, 1) > full[(size_t)j * w + n + 1];
     }
+    send_plan(sh, counts);
+    sh.ms_partition = now_ms() - t_part;
     sh.recv_count.assign(n, 0);
     uint64_t from_others = 0;
     for (int i = 0; i < n; ++i) {
@@ -915,12 +998,15 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     }
     std::vector<uint64_t> roff;
     offsets_of(sh.recv_count, roff);
-    if (sh.send_count[me] != sh.recv_count[me]) return set_error(DBI_E_STATE, "shard count exchange mismatch");
-    rc_local = h->xrecv.ensure(std::max<uint64_t>(roff[n], 1));
-    if (!rc_local) rc_local = injected_failure("buffers", me);
-    if ((rc = agree(c, rc_local, s, &failed))) return rc;
-    if (rc_local) return rc_local;
-    if (failed) return peer_failed("owner buffers");
+    // an owner that must grow its receive buffer may fail to: then every rank
+    // learns it before the exchange (a collective only when someone grows)
+    if (grow) {
+        rc_local = h->xrecv.ensure(std::max<uint64_t>(roff[n], 1));
+        if (!rc_local) rc_local = injected_failure("buffers", me);
+        if ((rc = agree(c, rc_local, s, &failed))) return rc;
+        if (rc_local) return rc_local;
+        if (failed) return peer_failed("owner buffers");
+    }
 
     // records to their owners: one group of point-to-point transfers over all peers
     {
@@ -929,7 +1015,9 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
             return rc;
         ms.end();
     }
-    DBI_HIP(hipStreamSynchronize(s));
+    // the owner merge runs behind the exchange on the same stream; only a
+    // per-phase breakdown (every stage timed) waits for it here
+    if (h->timing && h->timing_only.empty()) DBI_HIP(hipStreamSynchronize(s));
     sh.n_recv = roff[n];
     sh.ms_exchange = now_ms() - t0;
     sh.phase = 3;
@@ -939,22 +1027,22 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // whole-index totals (+ status), and where this owner's rows start in the whole index
     std::vector<uint64_t> tot(5, 0);
     {
-        const int w = 6;
-        if ((rc = h->xcount.ensure((size_t)n * w + 8))) return rc;
-        std::vector<unsigned long long> row(w, 0), rows((size_t)n * w);
+        const int wt = 6;
+        if ((rc = h->xcount.ensure((size_t)n * wt + 8))) return rc;
+        std::vector<unsigned long long> row(wt, 0), rows((size_t)n * wt);
         row[0] = sh.n_total; row[1] = sh.n_dropped; row[2] = sh.n_recv; row[3] = h->stats.n_unique;
         row[4] = h->stats.n_keys;
         row[5] = rc_merge ? 1u : 0u;
-        DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * w, row.data(), sizeof(uint64_t) * w, hipMemcpyHostToDevice, s));
-        DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * w, h->xcount.p, w, ncclUint64, c->comm, s));
-        DBI_HIP(hipMemcpyAsync(rows.data(), h->xcount.p, sizeof(uint64_t) * n * w, hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * wt, row.data(), sizeof(uint64_t) * wt, hipMemcpyHostToDevice, s));
+        DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * wt, h->xcount.p, wt, ncclUint64, c->comm, s));
+        DBI_HIP(hipMemcpyAsync(rows.data(), h->xcount.p, sizeof(uint64_t) * n * wt, hipMemcpyDeviceToHost, s));
         DBI_HIP(hipStreamSynchronize(s));
         if (rc_merge) return rc_merge;
         sh.u_base = 0;
         for (int i = 0; i < n; ++i) {
-            if (rows[(size_t)i * w + 5]) return peer_failed("owner merge");
-            for (int k = 0; k < 5; ++k) tot[k] += rows[(size_t)i * w + k];
-            if (i < me) sh.u_base += rows[(size_t)i * w + 3];
+            if (rows[(size_t)i * wt + 5]) return peer_failed("owner merge");
+            for (int k = 0; k < 5; ++k) tot[k] += rows[(size_t)i * wt + k];
+            if (i < me) sh.u_base += rows[(size_t)i * wt + 3];
         }
         sh.u_base_known = true;
     }
