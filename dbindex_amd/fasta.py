@@ -265,3 +265,13 @@ def uniprot_accession(definition: str) -> Optional[str]:
     if len(parts) >= 3 and parts[0] in ("sp", "tr") and parts[1]:
         return parts[1]
     return None
+
+
+def fasta_accession(definition: str) -> str:
+    """What ``DBIndexer.run`` matches the decoy regexp against
+    (``fasta.getAccession()``, DBIndexer.java:608): the UniProt accession of a
+    ``db|ACC|NAME`` header, else the header's first word (decoy prefixes such as
+    ``Reverse_sp|...`` stay in it).  ``Fasta`` lives in the absent
+    edu.scripps.yates.utilities jar: parity unpinned."""
+    acc = uniprot_accession(definition)
+    return acc if acc is not None else definition.split(None, 1)[0] if definition.strip() else ""

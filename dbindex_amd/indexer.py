@@ -12,12 +12,14 @@ the store's ``getSequences``.
 from __future__ import annotations
 
 import os
+import re
 
 from typing import Iterable, List, Optional, Set, Tuple, Union
 
-from .fasta import PackedProteins, iter_fasta, uniprot_accession
+from .fasta import PackedProteins, fasta_accession, iter_fasta, uniprot_accession
 from .params import DBIndexSearchParams, calculate_mass, tolerance_in_dalton
-from .store import DBIndexStoreHip, IndexedProtein, IndexedSequence, MassRange, MassRangeFilteringIndexHip
+from .store import (DBIndexStoreHip, IndexedProtein, IndexedSequence, MassRange, MassRangeFilteringIndexHip,
+                    ProteinCache)
 
 PRECISION = 0.000001  # Constants.java:50
 
@@ -48,6 +50,7 @@ class DBIndexer:
         self.indexStore = indexStore
         self.indexStore.setDeviceDigest(True)
         self.protNum = -1
+        self.decoyDiscarded = 0
         self.inited = False
         self.database_name = database_name
         self._cache_populated = False
@@ -60,6 +63,13 @@ class DBIndexer:
         self.indexStore.init(self.database_name + "_dbindex_hip")
         if self.mode == IndexerMode.SEARCH_UNINDEXED and os.path.isfile(self.database_name):
             self._set_protein_cache(self.database_name)  # setProteinCache() (:443-444, :463-500)
+        elif (self.mode == IndexerMode.SEARCH_INDEXED and os.path.isfile(self.database_name)
+              and self.indexStore.indexExists()):
+            # a reused index: the cache holds every FASTA protein (:438-442, :483-489)
+            protCache = ProteinCache()
+            for d, s in _fasta_items(self.database_name):
+                protCache.addProtein(d, s)
+            self.indexStore.setProteinCache(protCache)
         self.inited = True
 
     def _set_protein_cache(self, fasta) -> None:
@@ -98,9 +108,17 @@ class DBIndexer:
         if not any(uniprot_accession(d) for d, _ in items):
             raise DBIndexerException("Reading FASTA file was not able to extract any single Uniprot "
                                      "protein accession.")  # :560-565
+        decoy = re.compile(self.sparam.discard_decoy_regexp) if self.sparam.discard_decoy_regexp else None
         self.indexStore.startAddSeq()
         try:
+            protCache = ProteinCache()  # :594-595
+            self.indexStore.setProteinCache(protCache)
+            self.decoyDiscarded = 0
             for d, s in items:
+                protCache.addProtein(d, s)  # every protein, decoys included (:605)
+                if decoy is not None and decoy.search(fasta_accession(d)):  # Matcher.find (:609-615)
+                    self.decoyDiscarded += 1
+                    continue
                 self.cutSeq(d, s)
         finally:
             self.indexStore.stopAddSeq()

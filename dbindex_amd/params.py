@@ -89,6 +89,7 @@ class DBIndexSearchParams:
     mass_group_factor: int = 10000
     index_factor: int = 8
     mandatory_internal_aas: Optional[str] = None
+    discard_decoy_regexp: Optional[str] = None  # getDiscardDecoyRegexp (DBIndexSearchParamsImpl.java:483)
     min_pep_length: int = MIN_PEP_LENGTH
     h2o_proton: float = H2O_PROTON
     cterm: float = 0.0

@@ -100,6 +100,43 @@ class MassRange:
         return self.tolerance
 
 
+class ProteinCache:
+    """``ProteinCache`` (ProteinCache.java:22-179): definitions and sequences by
+    insertion position.  ``DBIndexer.run`` fills it with EVERY FASTA protein
+    (DBIndexer.java:605) and hands it to the store (:595), which resolves
+    protein ids through it (SQLiteMult.java:297, :457; IndexMerge.java:452-461)."""
+
+    def __init__(self):
+        self.defs: List[str] = []
+        self.sequences: List[str] = []
+
+    def addProtein(self, definition: str, protein: Optional[str] = None) -> int:
+        self.defs.append(definition.replace("\t", " "))  # :87-89
+        if protein is not None:
+            self.sequences.append(protein)
+        return len(self.defs) - 1
+
+    def getNumberProteins(self) -> int:
+        return len(self.sequences)
+
+    def isPopulated(self) -> bool:
+        return bool(self.sequences)
+
+    def getProteinSequence(self, proteinId: int) -> Optional[str]:
+        return self.sequences[proteinId] if len(self.sequences) > proteinId else None  # :60-65
+
+    def getProteinDef(self, proteinId: int) -> str:
+        return self.defs[proteinId]
+
+    def getPeptideSequence(self, protId: int, seqOffset: int, seqLen: int) -> Optional[str]:
+        """String.substring's bounds; the reference logs the exception and
+        returns null (:112-127)."""
+        p = self.getProteinSequence(protId)
+        if p is None or seqOffset < 0 or seqLen < 0 or seqOffset + seqLen > len(p):
+            return None
+        return p[seqOffset:seqOffset + seqLen]
+
+
 def _seq_list(ptr) -> List[IndexedSequence]:
     l = ptr.contents
     n = l.n
@@ -138,6 +175,7 @@ class DBIndexStoreHip:
             cp = sparam
         assert isinstance(cp, DbiParams)
         self._cp = cp
+        self.proteinCache: Optional[ProteinCache] = None
         s = ctypes.c_void_p()
         check(_native.lib().dbi_store_create(ctypes.byref(cp), device, ctypes.byref(s)))
         self.s = s
@@ -203,9 +241,10 @@ class DBIndexStoreHip:
         else:
             check(L.dbi_store_get_sequences(self.s, float(precMass), float(tolerance), ctypes.byref(r)))
         try:
-            return _seq_list(r)
+            seqs = _seq_list(r)
         finally:
             L.dbi_seq_list_free(r)
+        return self._resolve(seqs)
 
     def getSequencesIterator(self, ranges: Sequence[MassRange]) -> Iterator[IndexedSequence]:
         return iter(self.getSequences(ranges))
@@ -217,15 +256,38 @@ class DBIndexStoreHip:
                                                       ctypes.byref(out)))
         return out.value
 
-    def setProteinCache(self, proteinCache) -> None:
-        # the store keeps its own ProteinCache, filled by addProteinDef
+    def setProteinCache(self, proteinCache: Optional[ProteinCache]) -> None:
+        """The store keeps its own copy of the proteins given to
+        ``addProteinDef``; a cache set here is where protein ids are RESOLVED,
+        as in every reference store (peptide text and flanks
+        IndexMerge.java:452-461, definitions SQLiteMult.java:457, residues
+        :297).  The two agree unless ``run()`` discarded decoys that precede a
+        target: the cache holds every protein (DBIndexer.java:605) while the
+        ids advance only for the non-decoys (:609-616), so the reference's
+        answers for later ids come from shifted cache entries -- reproduced."""
         self.proteinCache = proteinCache
+
+    def _resolve(self, seqs: List[IndexedSequence]) -> List[IndexedSequence]:
+        pc = getattr(self, "proteinCache", None)
+        if pc is None:
+            return seqs
+        for s in seqs:
+            pid, off, ln = s.proteinIds[0], s.sequenceOffset, s.sequenceLen
+            prot = pc.getProteinSequence(pid)
+            if prot is None or off > len(prot):  # Util.getResidues' substring throws (Util.java:132-138)
+                raise DBIndexStoreException(_native.DBI_E_INVALID, f"protein {pid} of the ProteinCache cannot hold "
+                                            f"offset {off} (String index out of range)")
+            s.sequence = pc.getPeptideSequence(pid, off, ln)
+            s.residues = get_residues(off, ln, prot)
+        return seqs
 
     def supportsProteinCache(self) -> bool:
         return True
 
     def getProteins(self, sequence: IndexedSequence) -> List[IndexedProtein]:
-        return [IndexedProtein(self.getProteinDef(pid), pid) for pid in sequence.getProteinIds()]
+        pc = getattr(self, "proteinCache", None)
+        name = pc.getProteinDef if pc is not None else self.getProteinDef
+        return [IndexedProtein(name(pid), pid) for pid in sequence.getProteinIds()]
 
     def getNumberSequences(self) -> int:
         v = ctypes.c_int64()
@@ -239,7 +301,8 @@ class DBIndexStoreHip:
 
     def getResidues(self, peptideSequence: IndexedSequence, protein: IndexedProtein) -> ResidueInfo:
         """SQLiteMult.getResidues (:294-312) -> Util.getResidues (Util.java:130-162)."""
-        prot = self.getProteinSequence(protein.getId())
+        pc = getattr(self, "proteinCache", None)
+        prot = (pc.getProteinSequence if pc is not None else self.getProteinSequence)(protein.getId())
         off = peptideSequence.getSequenceOffset()
         if off is None or off < 0:
             off = prot.find(peptideSequence.getSequence())

@@ -250,12 +250,14 @@ static jobject seq_list(JNIEnv* e, dbi_seq_list* l) {
     if (protOff) (*e)->SetIntArrayRegion(e, protOff, 0, n + 1, po);
     jintArray protIds = (*e)->NewIntArray(e, np);
     if (protIds) (*e)->SetIntArrayRegion(e, protIds, 0, np, (const jint*)l->prot_ids);
+    jintArray pepOff = (*e)->NewIntArray(e, n);
+    if (pepOff) (*e)->SetIntArrayRegion(e, pepOff, 0, n, (const jint*)l->offset);
     free(so);
     free(po);
     if (set_array(e, o, c, "mass", "[D", mass) || set_array(e, o, c, "seqOff", "[I", seqOff) ||
         set_array(e, o, c, "seqChars", "[B", chars) || set_array(e, o, c, "left", "[B", left) ||
         set_array(e, o, c, "right", "[B", right) || set_array(e, o, c, "protOff", "[I", protOff) ||
-        set_array(e, o, c, "protIds", "[I", protIds))
+        set_array(e, o, c, "protIds", "[I", protIds) || set_array(e, o, c, "pepOff", "[I", pepOff))
         return NULL;
     return o;
 }

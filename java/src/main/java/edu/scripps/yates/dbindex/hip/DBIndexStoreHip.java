@@ -44,6 +44,7 @@ public class DBIndexStoreHip implements DBIndexStore {
         byte[] right;
         int[] protOff;     // n + 1
         int[] protIds;
+        int[] pepOff;      // first occurrence's offset in protein protIds[protOff[i]]
     }
 
     protected long h;  // dbi_store*
@@ -151,7 +152,9 @@ public class DBIndexStoreHip implements DBIndexStore {
     public List<IndexedProtein> getProteins(IndexedSequence sequence) throws DBIndexStoreException {  // :171
         final List<IndexedProtein> ret = new ArrayList<IndexedProtein>();
         for (final Integer protId : sequence.getProteinIds()) {
-            ret.add(new IndexedProtein(proteinDef0(h, protId), protId));
+            // the cache's definition when one is set (SQLiteMult.java:457)
+            ret.add(new IndexedProtein(proteinCache != null ? proteinCache.getDef(protId) : proteinDef0(h, protId),
+                    protId));
         }
         return ret;
     }
@@ -166,7 +169,8 @@ public class DBIndexStoreHip implements DBIndexStore {
             throws DBIndexStoreException {                                      // :190
         // as DBIndexStoreSQLiteMult.getResidues (:294-312): the peptide's own
         // offset, else its first position in the protein
-        final String proteinSequence = proteinSequence0(h, protein.getId());
+        final String proteinSequence = proteinCache != null ? proteinCache.getProteinSequence(protein.getId())
+                : proteinSequence0(h, protein.getId());
         int seqOffset = peptideSequence.getSequenceOffset();
         if (seqOffset == IndexedSequence.OFFSET_UNKNOWN) {
             seqOffset = proteinSequence.indexOf(peptideSequence.getSequence());
@@ -220,21 +224,38 @@ public class DBIndexStoreHip implements DBIndexStore {
         }
     }
 
-    /** IndexMerge.parseAddPeptideInfo (:446-470): sequence, mass, protein ids, flanks. */
-    static List<IndexedSequence> toList(SeqList l) {
+    /**
+     * IndexMerge.parseAddPeptideInfo (:446-470): sequence, mass, protein ids,
+     * flanks.  With a ProteinCache set, text and flanks come from the cache
+     * entry of the first protein id, as the reference stores do
+     * (IndexMerge.java:452-461): that differs from the store's own copy only
+     * when DBIndexer.run discarded decoys ahead of targets (the cache holds
+     * every protein, DBIndexer.java:605; ids count non-decoys, :609-616), and
+     * the reference's shifted answers are then reproduced.
+     */
+    List<IndexedSequence> toList(SeqList l) {
         final int n = l.mass.length;
         final List<IndexedSequence> ret = new ArrayList<IndexedSequence>(n);
         for (int i = 0; i < n; i++) {
-            final String seq = new String(l.seqChars, l.seqOff[i], l.seqOff[i + 1] - l.seqOff[i],
-                    java.nio.charset.StandardCharsets.ISO_8859_1);
+            final int len = l.seqOff[i + 1] - l.seqOff[i];
+            final int pid0 = l.protIds[l.protOff[i]];
+            String seq;
+            ResidueInfo res;
+            if (proteinCache != null) {
+                seq = proteinCache.getPeptideSequence(pid0, l.pepOff[i], len);
+                res = Util.getResidues(null, l.pepOff[i], len, proteinCache.getProteinSequence(pid0));
+            } else {
+                seq = new String(l.seqChars, l.seqOff[i], len, java.nio.charset.StandardCharsets.ISO_8859_1);
+                res = new ResidueInfo(new String(l.left, 3 * i, 3, java.nio.charset.StandardCharsets.ISO_8859_1),
+                        new String(l.right, 3 * i, 3, java.nio.charset.StandardCharsets.ISO_8859_1));
+            }
             final IndexedSequence s = new IndexedSequence(0, l.mass[i], seq, "", "");
             final List<Integer> ids = new ArrayList<Integer>(l.protOff[i + 1] - l.protOff[i]);
             for (int k = l.protOff[i]; k < l.protOff[i + 1]; k++) {
                 ids.add(l.protIds[k]);
             }
             s.setProteinIds(ids);
-            s.setResidues(new ResidueInfo(new String(l.left, 3 * i, 3, java.nio.charset.StandardCharsets.ISO_8859_1),
-                    new String(l.right, 3 * i, 3, java.nio.charset.StandardCharsets.ISO_8859_1)));
+            s.setResidues(res);
             ret.add(s);
         }
         return ret;

@@ -254,3 +254,20 @@ def test_static_mods_semantics():
     assert base.with_static_mods({}, n15_enrichment=0.5).residue_mass["C"] == base.residue_mass["C"]
     with pytest.raises(ValueError):
         base.with_static_mods({"J": 1.0})
+
+
+def test_protein_cache_and_decoy_accession():
+    """ProteinCache (ProteinCache.java:60-127) and the string the decoy regexp
+    is matched against (DBIndexer.java:608-611)."""
+    from dbindex_amd.store import ProteinCache
+    pc = ProteinCache()
+    assert not pc.isPopulated()
+    assert pc.addProtein("sp|P1|A\tB", "PEPTIDEK") == 0
+    assert pc.addProtein("sp|P2|C", "MKR") == 1
+    assert pc.getProteinDef(0) == "sp|P1|A B" and pc.getNumberProteins() == 2
+    assert pc.getPeptideSequence(0, 2, 4) == "PTID"
+    assert pc.getPeptideSequence(1, 1, 5) is None  # substring out of range: logged, null
+    assert pc.getProteinSequence(5) is None
+    assert fasta.fasta_accession("sp|P12345|NAME_HUMAN desc") == "P12345"
+    assert fasta.fasta_accession("Reverse_sp|P12345|NAME_HUMAN desc") == "Reverse_sp|P12345|NAME_HUMAN"
+    assert fasta.fasta_accession("") == ""

@@ -217,3 +217,80 @@ def test_concurrent_store_queries_mixed_ranges():
     for x in th:
         x.join()
     assert not errors, errors[:5]
+
+
+def _with_decoys(pp, every):
+    """FASTA items with a reversed-sequence ``Reverse_`` decoy after every
+    ``every``-th target (every=0: all decoys at the end)."""
+    seqs = pp.sequences()
+    tg = [(pp.defs[i], s) for i, s in enumerate(seqs)]
+    dec = [("Reverse_" + d, s[::-1]) for d, s in tg]
+    if every == 0:
+        return tg + dec
+    out = []
+    for i, x in enumerate(tg):
+        out.append(x)
+        if i % every == 0:
+            out.append(dec[i])
+    return out
+
+
+def _pack(seqs):
+    lens = np.array([len(s) for s in seqs], np.uint64)
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    return np.frombuffer("".join(seqs).encode(), np.uint8).copy(), off
+
+
+@pytest.mark.parametrize("every", [0, 3])
+def test_decoy_regexp_protein_numbering(every):
+    """DBIndexer.run with discardDecoyRegexp (DBIndexer.java:594-616): every
+    protein enters the ProteinCache, only non-decoys are cut, so ids count the
+    non-decoys while the store resolves text, flanks and definitions through
+    the cache (IndexMerge.java:452-461, SQLiteMult.java:297/:457).  With
+    decoys interleaved the answers come from shifted cache entries, exactly as
+    the reference's; with decoys appended they are the target-only index."""
+    prm = DBIndexSearchParams.trypsin(2, discard_decoy_regexp="^Reverse_")
+    pp = fasta.config("1k").slice(0, 90)
+    items = _with_decoys(pp, every)
+    all_defs = [d for d, _ in items]
+    all_seqs = [s for _, s in items]
+    targets = [s for d, s in items if not d.startswith("Reverse_")]
+    res, off = _pack(targets)
+    oix = cref.Index(prm.to_c(), res, off)
+    ix = DBIndexer(prm)
+    ix.init()
+    ix.run(items)
+    assert ix.decoyDiscarded == len(items) - len(targets) > 0
+    st = ix.indexStore
+    assert st.getTotalSeqCount() == oix.n_total and st.getNumberSequences() == oix.n_keys
+    u = oix.unique()
+    m, t = query_masses(oix, 120, seed=17)
+    n_shifted = n_raised = 0
+    for mi, ti in zip(m, t):
+        ids = oix.query(float(mi), float(ti))
+        want, raises = [], False
+        for i in ids:
+            pids = [int(x) for x in u["occ_prot"][u["occ_off"][i]:u["occ_off"][i + 1]]]
+            p0, o, ln = int(u["prot_id"][i]), int(u["offset"][i]), int(u["length"][i])
+            cp = all_seqs[p0]
+            if o > len(cp):
+                raises = True
+                break
+            text = cp[o:o + ln] if o + ln <= len(cp) else None
+            n_shifted += text != targets[p0][o:o + ln]
+            left, right = pyref.get_residues(o, ln, cp)
+            want.append((text, float(u["mass"][i]), pids, left, right, o, ln))
+        if raises:
+            n_raised += 1
+            with pytest.raises(Exception, match="out of range"):
+                st.getSequences(float(mi), float(ti))
+            continue
+        res_q = st.getSequences(float(mi), float(ti))
+        same(got(res_q), want)
+        for s in res_q[:3]:
+            assert [p.getAccession() for p in st.getProteins(s)] == [all_defs[p] for p in s.getProteinIds()]
+    if every == 0:
+        assert n_shifted == 0 and n_raised == 0  # decoys after the targets: ids and cache agree
+    else:
+        assert n_shifted > 0  # the reference's shifted resolution is what is reproduced
