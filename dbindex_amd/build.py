@@ -38,7 +38,7 @@ def _newer(target: str, deps) -> bool:
 def build(force: bool = False, verbose: bool = False, lib_out: str = LIB, defines=()) -> str:
     """Compile + link the library (``defines``: extra -D flags for experiment variants)."""
     deps = [os.path.join(CSRC, s) for s in SOURCES]
-    deps += [os.path.join(CSRC, "dbi_internal.h"), os.path.join(CSRC, "dbi_engine.h"), os.path.join(ROOT, "include", "dbindex_hip.h")]
+    deps += [os.path.join(CSRC, "dbi_internal.h"), os.path.join(CSRC, "dbi_lane.h"), os.path.join(CSRC, "dbi_engine.h"), os.path.join(ROOT, "include", "dbindex_hip.h")]
     if not force and _newer(lib_out, deps):
         return lib_out
     objdir = os.path.join(HERE, "build") if lib_out == LIB else \

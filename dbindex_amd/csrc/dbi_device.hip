@@ -35,6 +35,7 @@
 #include <algorithm>
 
 #include "dbi_internal.h"
+#include "dbi_lane.h"
 
 namespace dbi {
 
@@ -1923,6 +1924,264 @@ __device__ void block_bitonic(unsigned long long* k0, unsigned long long* k1, ui
     }
 }
 
+// ---- compact-key register bitonic (the big bins) ---------------------------
+// Inside one fine bin the masses differ in ~32 low bits (bin width ~0.00066 Da
+// <= 2^32.4 ulps below 1024 Da), so with mb = mass bits (q0 >> 8) and mb0 the
+// run's minimum, one 64-bit key
+//   (mb - mb0) << 29 | tag high byte << 21 | tag low byte << 13 | arrival index
+// orders a run by (mass, tag), equal (mass, tag) by arrival.  For the device
+// digests arrival IS first appearance (records are emitted in protein/offset/
+// length order and the radix passes are stable); the order is checked after
+// the permutation, and a run that breaks either assumption (mb - mb0 >= 2^35,
+// arrival not ascending in q1) is re-sorted by the full 128-bit record key.
+// The keys live in registers, R per lane, element i = lane*R + r of the wave
+// (w*64R + lane*R + r of the block): the all-ascending flip network, register
+// pairs for distances < R, DPP / row swaps above (dbi_lane.h), LDS only across
+// waves.
+#ifdef DBI_X_CKSTAT
+__device__ unsigned int g_ck_stat[8];
+#endif
+constexpr int CK_IDX_BITS = 13;
+constexpr int CK_D_BITS = 64 - 16 - CK_IDX_BITS;
+
+__device__ __forceinline__ bool ck_make(uint64_t q0, uint64_t q1, uint64_t mb0, uint32_t idx, uint64_t& key) {
+    const uint64_t d = (q0 >> 8) - mb0;
+    key = (d << (16 + CK_IDX_BITS)) | ((q0 & 0xFFu) << (8 + CK_IDX_BITS)) | ((q1 >> 56) << CK_IDX_BITS) | idx;
+    return d < (1ull << CK_D_BITS);
+}
+
+__device__ __forceinline__ uint64_t ck_q0(uint64_t key, uint64_t mb0) {
+    return ((mb0 + (key >> (16 + CK_IDX_BITS))) << 8) | ((key >> (8 + CK_IDX_BITS)) & 0xFFu);
+}
+
+__device__ __forceinline__ uint32_t ck_idx(uint64_t key) { return (uint32_t)key & ((1u << CK_IDX_BITS) - 1u); }
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_xor(v, d, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void ck_cx(uint64_t& a, uint64_t& b) {  // a: the lower index
+    const bool gt = a > b;
+    const uint64_t lo = gt ? b : a, hi = gt ? a : b;
+    a = lo;
+    b = hi;
+}
+
+__device__ __forceinline__ uint64_t ck_pick(uint64_t a, uint64_t b, bool lower) {
+    return ((a > b) == lower) ? b : a;  // lower: min, else max
+}
+
+// flip step of the K-merge: partner i ^ (K-1)
+template <int R, int K>
+__device__ __forceinline__ void ck_flip(uint64_t (&key)[R]) {
+    if constexpr (K <= R) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r < (r ^ (K - 1))) ck_cx(key[r], key[r ^ (K - 1)]);
+    } else {
+        const bool lower = (lane_id() & (uint32_t)(K / (2 * R))) == 0;
+#pragma unroll
+        for (int r = 0; r < R / 2; ++r) {  // registers r and R-1-r trade with the partner lane
+            const int q = r ^ (R - 1);
+            const uint64_t br = lane_xor64<K / R - 1>(key[q]), bq = lane_xor64<K / R - 1>(key[r]);
+            key[r] = ck_pick(key[r], br, lower);
+            key[q] = ck_pick(key[q], bq, lower);
+        }
+    }
+}
+
+// half-cleaner step: partner i ^ J
+template <int R, int J>
+__device__ __forceinline__ void ck_half(uint64_t (&key)[R]) {
+    if constexpr (J < R) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r < (r ^ J)) ck_cx(key[r], key[r ^ J]);
+    } else {
+        const bool lower = (lane_id() & (uint32_t)(J / R)) == 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) key[r] = ck_pick(key[r], lane_xor64<J / R>(key[r]), lower);
+    }
+}
+
+template <int R, int J>
+__device__ __forceinline__ void ck_clean(uint64_t (&key)[R]) {
+    if constexpr (J >= 1) {
+        ck_half<R, J>(key);
+        ck_clean<R, J / 2>(key);
+    }
+}
+
+// sorts the wave's 64R keys ascending (K = 64R at the top)
+template <int R, int K>
+__device__ __forceinline__ void ck_sort_wave(uint64_t (&key)[R]) {
+    if constexpr (K > 2) ck_sort_wave<R, K / 2>(key);
+    ck_flip<R, K>(key);
+    ck_clean<R, K / 4>(key);
+}
+
+// equal (mass, tag) neighbours in [lo+1, lo+L) must ascend in q1 (first appearance)
+__device__ __forceinline__ bool ck_order_bad(const unsigned long long* k0, const unsigned long long* k1, uint32_t p) {
+    return k0[p] == k0[p - 1] && (k1[p] >> 56) == (k1[p - 1] >> 56) && k1[p] < k1[p - 1];
+}
+
+// One wave sorts k0/k1[lo, lo+L), L <= 64R, by the compact key; false: the
+// run is left a permutation of itself and needs the full-key sort.
+template <int R>
+__device__ bool ck_run_wave(unsigned long long* k0, unsigned long long* k1, uint32_t lo, uint32_t L) {
+    const uint32_t lane = lane_id();
+    uint64_t mb0 = ~0ull;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = lane * R + r;
+        if (i < L) {
+            const uint64_t o = k0[lo + i] >> 8;
+            mb0 = o < mb0 ? o : mb0;
+        }
+    }
+    mb0 = wave_min_u64(mb0);
+    uint64_t key[R];
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = lane * R + r;
+        key[r] = ~0ull;
+        if (i < L) ok &= ck_make(k0[lo + i], k1[lo + i], mb0, i, key[r]);
+    }
+#ifdef DBI_X_CKSTAT
+    if (lane == 0) atomicAdd(&g_ck_stat[0], 1u);
+    if (__ballot(!ok) && lane == 0) atomicAdd(&g_ck_stat[1], 1u);
+#endif
+    if (__ballot(!ok)) return false;
+    ck_sort_wave<R, 64 * R>(key);
+    // q0 comes back out of the key itself; q1 is gathered by the arrival index
+    uint64_t g1[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = lane * R + r;
+        if (i < L) g1[r] = k1[lo + ck_idx(key[r])];
+    }
+    wave_sync();  // every lane's gather before any write
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = lane * R + r;
+        if (i < L) {
+            k0[lo + i] = ck_q0(key[r], mb0);
+            k1[lo + i] = g1[r];
+        }
+    }
+    wave_sync();
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = lane * R + r;
+        if (i > 0 && i < L) bad |= ck_order_bad(k0, k1, lo + i);
+    }
+#ifdef DBI_X_CKSTAT
+    if (__ballot(bad) && lane == 0) atomicAdd(&g_ck_stat[2], 1u);
+#endif
+    return __ballot(bad) == 0;
+}
+
+// compare-exchange with partner i ^ m across waves, through LDS scratch sc[0, L)
+template <int R>
+__device__ __forceinline__ void ck_lds_step(unsigned long long* sc, uint64_t (&key)[R], uint32_t i0, uint32_t m,
+                                            uint32_t L) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (i0 + r < L) sc[i0 + r] = key[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = i0 + r, p = i ^ m;
+        const uint64_t b = p < L ? sc[p] : ~0ull;
+        key[r] = ck_pick(key[r], b, i < p);
+    }
+    __syncthreads();
+}
+
+// The whole block sorts k0/k1[lo, lo+L), L <= NT*R, by the compact key (block-
+// uniform result; false as in ck_run_wave).  k0[lo, lo+L) is the scratch of the
+// cross-wave steps; q0 is rebuilt from the keys.
+// s_min: NT/64 slots of scratch.
+template <int NT, int R>
+__device__ bool ck_run_block(unsigned long long* k0, unsigned long long* k1, uint32_t lo, uint32_t L,
+                             uint64_t* s_min) {
+    static_assert(NT * R <= (1 << CK_IDX_BITS), "arrival index bits");
+    constexpr uint32_t WE = 64 * R;
+    const uint32_t i0 = (threadIdx.x >> 6) * WE + lane_id() * R;
+    uint64_t mb0 = ~0ull;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (i0 + r < L) {
+            const uint64_t o = k0[lo + i0 + r] >> 8;
+            mb0 = o < mb0 ? o : mb0;
+        }
+    mb0 = wave_min_u64(mb0);
+    if (lane_id() == 0) s_min[threadIdx.x >> 6] = mb0;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const uint64_t o = s_min[w];
+        mb0 = o < mb0 ? o : mb0;
+    }
+    uint64_t key[R];
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        key[r] = ~0ull;
+        if (i0 + r < L) ok &= ck_make(k0[lo + i0 + r], k1[lo + i0 + r], mb0, i0 + r, key[r]);
+    }
+#ifdef DBI_X_CKSTAT
+    {
+        const int nok = __syncthreads_or(!ok);
+        if (threadIdx.x == 0) {
+            atomicAdd(&g_ck_stat[NT == 512 ? 3 : 6], 1u);
+            if (nok) atomicAdd(&g_ck_stat[NT == 512 ? 4 : 7], 1u);
+        }
+    }
+#endif
+    if (__syncthreads_or(!ok)) return false;
+    const bool live = (threadIdx.x >> 6) * WE < L;  // wave-uniform: waves past the run hold +inf only
+    if (live) ck_sort_wave<R, WE>(key);
+    uint32_t P2 = WE;
+    while (P2 < L) P2 <<= 1;
+    for (uint32_t k = 2 * WE; k <= P2; k <<= 1) {
+        ck_lds_step<R>(k0 + lo, key, i0, k - 1, L);
+        for (uint32_t j = k >> 2; j >= WE; j >>= 1) ck_lds_step<R>(k0 + lo, key, i0, j, L);
+        if (live) ck_clean<R, WE / 2>(key);
+    }
+    // q0 comes back out of the key (k0 was the scratch); q1 gathered by arrival index
+    uint64_t g1[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (i0 + r < L) g1[r] = k1[lo + ck_idx(key[r])];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (i0 + r < L) {
+            k0[lo + i0 + r] = ck_q0(key[r], mb0);
+            k1[lo + i0 + r] = g1[r];
+        }
+    }
+    __syncthreads();
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = i0 + r;
+        if (i > 0 && i < L) bad |= ck_order_bad(k0, k1, lo + i);
+    }
+#ifdef DBI_X_CKSTAT
+    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicAdd(&g_ck_stat[5], 1u);
+#endif
+    return !__syncthreads_or(bad);
+}
+
 // exclusive max of v over the block's lower threads (0 for thread 0)
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_max(uint32_t v, uint32_t* s_tmp) {
@@ -2046,44 +2305,48 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
 // order, independent of the order the records arrive in — then
 // finish_sorted().  Bins of <= RANK_MAX_RUN records: each record's rank inside
 // its bin from LDS compares (no barriers), scattered from registers; bigger
-// bins (equal-mass spikes at SwissProt scale) are sorted in place, one wave
-// each up to WAVE_SORT_MAX, else by the whole block.  A chunk above CAP goes
-// to k_chunk_sort_big.  LDS: 8+8+4 B per record, 39 KiB at CAP 1984 -> 4
-// blocks per CU.
+// bins (equal-mass spikes at SwissProt scale) are sorted in place by the
+// compact key in registers (ck_run_wave / ck_run_block), one wave each up to
+// WAVE_SORT_MAX, else by the whole block; the full-key bitonic only where the
+// compact key does not hold.  LDS: 8+8+4 B per record.
 constexpr uint32_t RANK_MAX_RUN = 64;
-constexpr uint32_t WAVE_SORT_MAX = 256;
-constexpr uint32_t MAX_BIG_RUNS = 64;
+#ifndef DBI_MID_WPE
+#define DBI_MID_WPE 7
+#endif
+constexpr uint32_t WAVE_SORT_MAX = WAVE_SORT_LIMIT;
 
 template <int NT, int CAP>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
-k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
-             const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
-             uint32_t* __restrict__ big_list, Counters* __restrict__ ctr) {
+struct ChunkSmem {
+    static constexpr uint32_t MAXB = CAP / (RANK_MAX_RUN + 1) + 1;  // runs above RANK_MAX_RUN
+    unsigned long long k0[CAP];
+    unsigned long long k1[CAP];
+    uint32_t aux[CAP];
+    uint32_t big[MAXB];  // lo | hi << 16
+    uint32_t u32[NT / 64 + 1];
+    uint64_t mins[NT / 64];
+    uint32_t nbig, wide, bad;
+};
+
+// The chunk in[0, m) -> out[0, m) in final order with head flags; *heads =
+// this thread's unique heads.  BLOCK off: a chunk with a run above
+// WAVE_SORT_MAX is left untouched and false returned (block-uniform) -- the
+// list kernel with the block-level sort takes it.
+template <int NT, int CAP, bool BLOCK>
+__device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const BinMap& bm,
+                           const RecLoc& rl, ChunkSmem<NT, CAP>& sm, uint32_t* heads_out) {
     static_assert(CAP <= 65535, "16-bit positions");
-    static_assert(CAP / (RANK_MAX_RUN + 1) <= MAX_BIG_RUNS, "big-run list");
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t E = (CAP + NT - 1) / NT;  // records per thread (contiguous) in the run pass
-    __shared__ unsigned long long k0[CAP];
-    __shared__ unsigned long long k1[CAP];
-    __shared__ uint32_t aux[CAP];
-    __shared__ uint32_t s_big[MAX_BIG_RUNS];  // runs above RANK_MAX_RUN: lo | hi << 16
-    __shared__ uint32_t s_u32[NW + 1];
-    __shared__ uint32_t s_nbig, s_bad;
-    const uint32_t c = blockIdx.x;
-    const uint32_t a = chunk_lo[c];
-    const uint32_t m = chunk_lo[c + 1] - a;
-    if (m == 0) {
-        if (threadIdx.x == 0) ucount[c] = 0;
-        return;
+    static_assert(E <= 32, "run-head bit mask");
+    unsigned long long* k0 = sm.k0;
+    unsigned long long* k1 = sm.k1;
+    if (threadIdx.x == 0) {
+        sm.nbig = 0;
+        sm.wide = 0;
     }
-    if (m > (uint32_t)CAP) {
-        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
-        return;
-    }
-    if (threadIdx.x == 0) s_nbig = 0;
     {
         // all loads in flight before the first use (a Rec as 4 dwords: q0, q1)
-        const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in + a);
+        const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
         uint4 rv[E];
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) {
@@ -2117,72 +2380,161 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
             }
         }
     }
-    uint32_t rlo[E], rhi[E];
     {
-        uint32_t cur = block_excl_max<NT>(heads ? lo0 + 31 - __clz(heads) : 0u, s_u32);
+        uint32_t rlo[E], rhi[E];
+        uint32_t cur = block_excl_max<NT>(heads ? lo0 + 31 - __clz(heads) : 0u, sm.u32);
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) {
             if (heads & (1u << k)) cur = lo0 + k;
             rlo[k] = cur;
         }
-        cur = block_excl_min_rev<NT>(heads ? lo0 + __ffs(heads) - 1 : m, m, s_u32);
+        cur = block_excl_min_rev<NT>(heads ? lo0 + __ffs(heads) - 1 : m, m, sm.u32);
 #pragma unroll
         for (int k = (int)E - 1; k >= 0; --k) {
             rhi[k] = cur;
             if (heads & (1u << k)) cur = lo0 + (uint32_t)k;
         }
-    }
 #pragma unroll
-    for (uint32_t k = 0; k < E; ++k) {
-        if ((heads & (1u << k)) && rhi[k] - rlo[k] > RANK_MAX_RUN)
-            s_big[atomicAdd(&s_nbig, 1u)] = rlo[k] | (rhi[k] << 16);
-        if (lo0 + k < m) aux[lo0 + k] = rlo[k] | (rhi[k] << 16);
+        for (uint32_t k = 0; k < E; ++k) {
+            if ((heads & (1u << k)) && rhi[k] - rlo[k] > RANK_MAX_RUN) {
+                sm.big[atomicAdd(&sm.nbig, 1u)] = rlo[k] | (rhi[k] << 16);
+                if (rhi[k] - rlo[k] > WAVE_SORT_MAX) sm.wide = 1;
+            }
+            if (lo0 + k < m) sm.aux[lo0 + k] = rlo[k] | (rhi[k] << 16);
+        }
     }
     __syncthreads();
+    if (!BLOCK && sm.wide) return false;
     // small bins: rank inside the bin (k-major: a wave's lanes share bins), kept in registers with the key
-    unsigned long long v0[E], v1[E];
-    uint32_t dst[E];
+    {
+        unsigned long long v0[E], v1[E];
+        uint32_t dst[E];
 #pragma unroll
-    for (uint32_t k = 0; k < E; ++k) {
-        const uint32_t i = threadIdx.x + k * NT;
-        dst[k] = ~0u;
-        const uint32_t bb = i < m ? aux[i] : 0u;
-        const uint32_t blo = bb & 0xFFFFu, bhi = bb >> 16;
-        if (i < m && bhi - blo <= RANK_MAX_RUN) {
-            const unsigned long long a0 = k0[i], a1 = k1[i];
-            uint32_t rank = 0;
-            for (uint32_t j = blo; j < bhi; ++j) rank += key_lt(k0[j], k1[j], a0, a1);
-            v0[k] = a0;
-            v1[k] = a1;
-            dst[k] = blo + rank;
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint32_t i = threadIdx.x + k * NT;
+            dst[k] = ~0u;
+            const uint32_t bb = i < m ? sm.aux[i] : 0u;
+            const uint32_t blo = bb & 0xFFFFu, bhi = bb >> 16;
+            if (i < m && bhi - blo <= RANK_MAX_RUN) {
+                const unsigned long long a0 = k0[i], a1 = k1[i];
+                uint32_t rank = 0;
+#ifdef DBI_X_RANKOLD
+                for (uint32_t j = blo; j < bhi; ++j) rank += key_lt(k0[j], k1[j], a0, a1);
+#else
+                for (uint32_t j = blo; j < bhi; ++j) {  // q1 only read on equal q0 (duplicates)
+                    const unsigned long long b0 = k0[j];
+                    rank += b0 < a0;
+                    if (b0 == a0) rank += k1[j] < a1;
+                }
+#endif
+                v0[k] = a0;
+                v1[k] = a1;
+                dst[k] = blo + rank;
+            }
+        }
+        __syncthreads();  // every rank read done: scatter the small bins
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            if (dst[k] != ~0u) {
+                k0[dst[k]] = v0[k];
+                k1[dst[k]] = v1[k];
+            }
         }
     }
-    // big bins, sorted in place (disjoint from the small bins): up to
-    // WAVE_SORT_MAX records one wave each
-    const uint32_t nbig = s_nbig;
+    // big bins, in place (disjoint from the small bins)
+    const uint32_t nbig = sm.nbig;
     for (uint32_t r = threadIdx.x >> 6; r < nbig; r += NW) {
-        const uint32_t b = s_big[r];
-        const uint32_t L = (b >> 16) - (b & 0xFFFFu);
-        if (L <= WAVE_SORT_MAX) wave_bitonic(k0, k1, b & 0xFFFFu, L);
-    }
-    __syncthreads();  // every rank read done: scatter the small bins
-#pragma unroll
-    for (uint32_t k = 0; k < E; ++k) {
-        if (dst[k] != ~0u) {
-            k0[dst[k]] = v0[k];
-            k1[dst[k]] = v1[k];
-        }
-    }
-    for (uint32_t r = 0; r < nbig; ++r) {  // above WAVE_SORT_MAX: the whole block
-        const uint32_t b = s_big[r];
-        const uint32_t L = (b >> 16) - (b & 0xFFFFu);
-        if (L > WAVE_SORT_MAX) block_bitonic<NT>(k0, k1, b & 0xFFFFu, L);
+        const uint32_t b = sm.big[r];
+        const uint32_t lo = b & 0xFFFFu, L = (b >> 16) - lo;
+        if (L > WAVE_SORT_MAX) continue;
+        bool done;
+        if constexpr (WAVE_SORT_MAX > 256)
+            done = L <= 128 ? ck_run_wave<2>(k0, k1, lo, L)
+                   : L <= 256 ? ck_run_wave<4>(k0, k1, lo, L) : ck_run_wave<8>(k0, k1, lo, L);
+        else
+            done = L <= 128 ? ck_run_wave<2>(k0, k1, lo, L) : ck_run_wave<4>(k0, k1, lo, L);
+        if (!done) wave_bitonic(k0, k1, lo, L);
     }
     __syncthreads();
+    if constexpr (BLOCK) {
+        constexpr int R = NT * 4 >= CAP ? 4 : 8;
+        static_assert(NT * R >= CAP, "compact-sort capacity");
+        for (uint32_t r = 0; r < nbig; ++r) {
+            const uint32_t b = sm.big[r];
+            const uint32_t lo = b & 0xFFFFu, L = (b >> 16) - lo;
+            if (L > WAVE_SORT_MAX && !ck_run_block<NT, R>(k0, k1, lo, L, sm.mins)) block_bitonic<NT>(k0, k1, lo, L);
+        }
+        __syncthreads();
+    }
+    *heads_out = finish_sorted<NT>(out, m, rl, k0, k1, sm.aux, sm.u32, &sm.bad);
+    return true;
+}
+
+// One block per chunk.  A chunk above CAP goes to big_list, one with a bin
+// above WAVE_SORT_MAX to mid_list (both sorted by k_chunk_sort_list).  LDS
+// 39 KiB at CAP 1984 and no block-level sort here: <= 64 VGPRs, 4 blocks per CU.
+template <int NT, int CAP>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
+             const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
+             uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, Counters* __restrict__ ctr) {
+    __shared__ ChunkSmem<NT, CAP> sm;
+    const uint32_t c = blockIdx.x;
+    const uint32_t a = chunk_lo[c];
+    const uint32_t m = chunk_lo[c + 1] - a;
+    if (m == 0) {
+        if (threadIdx.x == 0) ucount[c] = 0;
+        return;
+    }
+    if (m > (uint32_t)CAP) {
+        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
+        return;
+    }
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
-    const uint32_t h = finish_sorted<NT>(out + a, m, rl, k0, k1, aux, s_u32, &s_bad);
-    const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
+    uint32_t h = 0;
+    if (!sort_chunk<NT, CAP, false>(in + a, out + a, m, bm, rl, sm, &h)) {
+        if (threadIdx.x == 0) mid_list[atomicAdd(&ctr->n_mid, 1u)] = c;
+        return;
+    }
+    const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
     if (threadIdx.x == 0) ucount[c] = tot;
+}
+
+// The chunks k_chunk_sort listed: BIG off = mid_list (a bin above
+// WAVE_SORT_MAX: the block-level compact sort), BIG on = big_list (chunks of
+// (CHUNK_CAP, BIG_CAP] records, 1024 threads, 155 KiB LDS, one block per CU;
+// above split_above they go on to the giant path).  One block per listed
+// chunk, blocks past the list exit (a grid-stride loop around sort_chunk
+// doubled its registers).
+template <int NT, int CAP, bool BIG>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BIG ? 4 : DBI_MID_WPE, 8)))
+k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
+                  const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
+                  const uint32_t* __restrict__ list, uint32_t* __restrict__ giant_list, uint32_t split_above,
+                  Counters* __restrict__ ctr) {
+    __shared__ ChunkSmem<NT, CAP> sm;
+    const uint32_t n = BIG ? ctr->n_big : ctr->n_mid;
+    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
+    const uint32_t j = blockIdx.x;
+    if (j < n) {
+        const uint32_t c = list[j];
+        const uint32_t a = chunk_lo[c];
+        const uint32_t m = chunk_lo[c + 1] - a;
+        if (BIG && m > split_above) {
+            if (threadIdx.x == 0) {
+                giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
+                atomicAdd(&ctr->n_giant_recs, (unsigned long long)m);
+            }
+            return;
+        }
+        uint32_t h = 0;
+        sort_chunk<NT, CAP, true>(in + a, out + a, m, bm, rl, sm, &h);
+        const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
+        if (threadIdx.x == 0) {
+            ucount[c] = tot;
+            if (BIG) atomicAdd(&ctr->n_big_recs, (unsigned long long)m);
+        }
+    }
 }
 
 // One chunk of m <= CAP records sorted in LDS by the record key with the flip
@@ -2191,70 +2543,45 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
 template <int NT, int CAP>
 __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const RecLoc& rl,
                                   unsigned long long* k0, unsigned long long* k1, uint32_t* aux, uint32_t* s_u32,
-                                  uint32_t* s_bad) {
+                                  uint32_t* s_bad, uint64_t* s_min) {
     for (uint32_t i = threadIdx.x; i < m; i += NT) {
         const Rec r = in[i];
         k0[i] = r.q0;
         k1[i] = r.q1;
     }
     __syncthreads();
-    block_bitonic<NT>(k0, k1, 0, m);
+    constexpr int R = NT * 4 >= CAP ? 4 : 8;
+    static_assert(NT * R >= CAP, "compact-sort capacity");
+    if (!ck_run_block<NT, R>(k0, k1, 0, m, s_min)) block_bitonic<NT>(k0, k1, 0, m);
     return finish_sorted<NT>(out, m, rl, k0, k1, aux, s_u32, s_bad);
-}
-
-// chunks of (CHUNK_CAP, BIG_CAP] records (bins of very frequent masses at
-// SwissProt scale): 1024 threads, 155 KiB LDS, one block per CU; larger
-// chunks go on to the global-memory path.
-__global__ void __launch_bounds__(BIG_THREADS)
-k_chunk_sort_big(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
-                 const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
-                 const uint32_t* __restrict__ big_list, uint32_t* __restrict__ giant_list, uint32_t split_above,
-                 Counters* __restrict__ ctr) {
-    static_assert(BIG_CAP <= 65535, "16-bit positions");
-    __shared__ unsigned long long k0[BIG_CAP];
-    __shared__ unsigned long long k1[BIG_CAP];
-    __shared__ uint32_t aux[BIG_CAP];
-    __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
-    __shared__ uint32_t s_bad;
-    const uint32_t nbig = ctr->n_big;
-    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
-    for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {
-        const uint32_t c = big_list[j];
-        const uint32_t a = chunk_lo[c];
-        const uint32_t m = chunk_lo[c + 1] - a;
-        if (m > split_above) {
-            if (threadIdx.x == 0) {
-                giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
-                atomicAdd(&ctr->n_giant_recs, (unsigned long long)m);
-            }
-            continue;
-        }
-        const uint32_t h = bitonic_chunk<BIG_THREADS, BIG_CAP>(in + a, out + a, m, rl, k0, k1, aux, s_u32, &s_bad);
-        const uint32_t tot = block_sum<BIG_THREADS, uint32_t>(h, s_u32);
-        if (threadIdx.x == 0) {
-            ucount[c] = tot;
-            atomicAdd(&ctr->n_big_recs, (unsigned long long)m);
-        }
-        __syncthreads();
-    }
-}
-
-hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                                 const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list,
-                                 uint32_t* d_giant_list, uint32_t max_blocks, uint32_t split_above, Counters* d_ctr,
-                                 hipStream_t s) {
-    if (max_blocks == 0) return hipSuccess;
-    DBI_LAUNCH(k_chunk_sort_big, dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in, d_out, d_chunk_lo, d_res, d_poff,
-               d_ucount, d_big_list, d_giant_list, std::min<uint32_t>(split_above, (uint32_t)BIG_CAP), d_ctr);
-    return hipGetLastError();
 }
 
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
-                             uint32_t* d_big_list, Counters* d_ctr, hipStream_t s) {
+                             uint32_t* d_big_list, uint32_t* d_mid_list, Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
-                       d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_ctr);
+                       d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, d_ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
+                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
+                                 const uint32_t* d_mid_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s) {
+    if (max_blocks == 0) return hipSuccess;
+    DBI_LAUNCH((k_chunk_sort_list<CHUNK_THREADS, CHUNK_CAP, false>), dim3(max_blocks), dim3(CHUNK_THREADS), 0, s,
+               d_in, d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_mid_list, nullptr, 0u, d_ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
+                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
+                                 const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
+                                 uint32_t split_above, Counters* d_ctr, hipStream_t s) {
+    if (max_blocks == 0) return hipSuccess;
+    DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS, BIG_CAP, true>), dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in,
+               d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list,
+               std::min<uint32_t>(split_above, (uint32_t)BIG_CAP), d_ctr);
     return hipGetLastError();
 }
 
@@ -3160,13 +3487,14 @@ k_giant_leaf(const Rec* in, Rec* out, const uint4* __restrict__ list, const unsi
     __shared__ unsigned long long k1[CAP];
     __shared__ uint32_t aux[CAP];
     __shared__ uint32_t s_u32[NT / 64 + 1];
+    __shared__ uint64_t s_min[NT / 64];
     __shared__ uint32_t s_bad;
     const uint32_t nl = min(*n_list, cap);
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
         const uint4 lf = list[j];
         const Rec* from = (lf.w ? out : in) + lf.x;
-        const uint32_t h = bitonic_chunk<NT, CAP>(from, out + lf.x, lf.y, rl, k0, k1, aux, s_u32, &s_bad);
+        const uint32_t h = bitonic_chunk<NT, CAP>(from, out + lf.x, lf.y, rl, k0, k1, aux, s_u32, &s_bad, s_min);
         const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
         if (threadIdx.x == 0) atomicAdd(&ucount[lf.z], tot);
         __syncthreads();
@@ -3225,3 +3553,13 @@ hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_ch
 }
 
 }  // namespace dbi
+#ifdef DBI_X_CKSTAT
+namespace dbi {
+void ck_stat_read(unsigned int* v) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(v, HIP_SYMBOL(g_ck_stat), sizeof(unsigned int) * 8);
+    unsigned int z[8] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_ck_stat), z, sizeof(z));
+}
+}  // namespace dbi
+#endif

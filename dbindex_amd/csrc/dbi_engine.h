@@ -120,7 +120,7 @@ struct dbi_handle {
     DevBuf<Rec> recA, recB;
     DevBuf<uint32_t> hist;
     DevBuf<uint8_t> digits;             // radix: next pass's digit per record
-    DevBuf<uint32_t> ucount, big_list, giant_list, chunk_lo;
+    DevBuf<uint32_t> ucount, big_list, mid_list, giant_list, chunk_lo;
     DevBuf<uint4> segs;                 // giant-chunk split: segment lists
     DevBuf<uint16_t> synth_len;         // dbi_synth_proteome: length quantile table
     DevBuf<uint8_t> synth_res;          //   residue table

@@ -147,7 +147,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_need, h->scan_tmp.cap)))) return rc;
     if ((rc = h->recB.ensure(n)) || (rc = h->hist.ensure(hist_elems)) ||
         (rc = h->ucount.ensure(nchunks)) || (rc = h->chunk_lo.ensure((size_t)nchunks + 1)) ||
-        (rc = h->big_list.ensure(nchunks)) ||
+        (rc = h->big_list.ensure(nchunks)) || (rc = h->mid_list.ensure(nchunks)) ||
         (rc = h->giant_list.ensure(nchunks)) || (rc = h->segs.ensure((GIANT_PASSES + 4) * seg_cap)) ||
         (rc = h->ws_key.ensure(4 * n)) || (rc = h->ws_k2.ensure(4 * n)) ||
         (rc = h->umass.ensure(n)) || (rc = h->upid.ensure(n)) || (rc = h->uoff.ensure(n)) ||
@@ -191,10 +191,17 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
           launch_chunk_bounds(src, n32, bm, T, nchunks, h->chunk_lo.p, s));
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                            h->ctr.p, s));
+                            h->mid_list.p, h->ctr.p, s));
+    // one block per listed chunk: at most one chunk per bin above the wave
+    // sort's reach (the lists are filled on the device)
+    const uint32_t max_mid = (uint32_t)std::min<uint64_t>(nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
+    const uint32_t max_big = (uint32_t)std::min<uint64_t>(nchunks, n / (CHUNK_CAP + 1) + 1);
+    STAGE(h, "chunk_sort_mid", by(0, 0, 0, 0, 0),
+          launch_chunk_sort_mid(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->mid_list.p,
+                                max_mid, h->ctr.p, s));
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
-          launch_chunk_sort_big(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                                h->giant_list.p, std::min<uint32_t>(nchunks, 256u), h->split_above, h->ctr.p, s));
+          launch_chunk_sort_big(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
+                                h->giant_list.p, max_big, h->split_above, h->ctr.p, s));
     STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
           launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p, h->segs.p,
                               seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
@@ -229,6 +236,15 @@ int finish_build(dbi_handle* h) {
     st.n_keys = h->hc.n_keys;
     for (int i = 0; i < 8; ++i) st.n_keys += h->hc.n_keys_shard[i];
     st.n_big_bins = h->hc.n_big;  // chunks above CHUNK_CAP (of which n_giant above BIG_CAP)
+#ifdef DBI_X_CKSTAT
+    {
+        unsigned int v[8] = {};
+        extern void ck_stat_read(unsigned int*);
+        ck_stat_read(v);
+        fprintf(stderr, "ckstat wave runs=%u range=%u order=%u | block runs=%u range=%u order=%u | big=%u range=%u\n",
+                v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+    }
+#endif
     st.build_ms = ms;
     st.digest_ms = 0;
     for (int i = 0; i < h->nstage; ++i) {
@@ -249,7 +265,7 @@ int finish_build(dbi_handle* h) {
     bytes += h->res.bytes() + h->poff64.bytes() + h->poff.bytes() + h->poff_g.bytes() + h->blk.bytes() + h->scan_tmp.bytes();
     bytes += h->thr.bytes() + h->tile_pf.bytes() + h->chunk_lo.bytes();
     bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->ucount.bytes();
-    bytes += h->big_list.bytes() + h->giant_list.bytes() + h->segs.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
+    bytes += h->big_list.bytes() + h->mid_list.bytes() + h->giant_list.bytes() + h->segs.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
     bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes();
     st.device_bytes = bytes;
     h->built = true;
@@ -535,7 +551,7 @@ void dbi_close(dbi_handle* h) {
     h->status.release(); h->win_lo.release(); h->win_hi.release(); h->qdir.release(); h->qdir_par.release();
     h->thr.release(); h->tile_pf.release(); h->chunk_lo.release();
     h->recA.release(); h->recB.release(); h->hist.release(); h->ucount.release(); h->digits.release();
-    h->big_list.release(); h->giant_list.release(); h->segs.release(); h->synth_len.release(); h->synth_res.release(); h->synth_out.release(); h->synth_off.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
+    h->big_list.release(); h->mid_list.release(); h->giant_list.release(); h->segs.release(); h->synth_len.release(); h->synth_res.release(); h->synth_out.release(); h->synth_off.release(); h->ws_key.release(); h->ws_k2.release(); h->umass.release(); h->upid.release();
     h->uoff.release(); h->ulen.release(); h->occ_off.release(); h->occ_pid.release();
     h->o_mass.release(); h->o_pid.release(); h->o_off.release(); h->o_len.release();
     h->q_mass.release(); h->q_tol.release(); h->q_first.release(); h->q_count.release(); h->q_row.release();

@@ -136,11 +136,13 @@ struct Counters {
     unsigned long long n_keys_shard[8];  // per-XCD-group partial key counts (summed on readback)
     unsigned long long n_slots;    // bounded digest: record slots reserved (kept + sentinels)
     unsigned int n_big;            // chunks above CHUNK_CAP (sorted by the 1024-thread LDS kernel)
+    unsigned int n_mid;            // chunks with a bin above WAVE_SORT_MAX (block-level compact sort)
     unsigned int err;              // device error bits
     unsigned int n_giant;          // chunks above BIG_CAP (MSD split into LDS-sized leaves)
     unsigned int n_seg[GIANT_PASSES + 1];  // giant split: segments in work list p
     unsigned int n_leaf_small, n_leaf_big, n_fallback;
     unsigned long long n_big_recs, n_giant_recs;  // records in chunks sorted by the big / giant paths
+    unsigned int n_ck_stat[4];     // experiment builds (DBI_X_CKSTAT): compact-sort runs / range / order redo
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads
     // (sharing the ticket's line cost the digest 30%)
@@ -162,6 +164,10 @@ constexpr int CHUNK_THREADS = 512;
 constexpr int CHUNK_CAP = 1984;     // records per chunk sorted in LDS (20 B each: 4 blocks per CU)
 constexpr int CHUNK_T = 1280;       // target chunk size (whole mass bins, ~T..T+maxbin; tools/ab_knobs.sh: 768-1536 measured)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
+#ifndef DBI_WAVE_SORT_LIMIT
+#define DBI_WAVE_SORT_LIMIT 512
+#endif
+constexpr int WAVE_SORT_LIMIT = DBI_WAVE_SORT_LIMIT;  // bins up to this size: one wave in k_chunk_sort (more: chunk_sort_mid)
 constexpr int BIG_THREADS = 1024;
 constexpr int BIG_CAP = 7936;       // records per oversize chunk sorted in LDS (1 block per CU)
 
@@ -283,11 +289,14 @@ hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, 
                                uint32_t* d_chunk_lo, hipStream_t s);
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
-                             uint32_t* d_big_list, Counters* d_ctr, hipStream_t s);
-// chunks of (CHUNK_CAP, BIG_CAP] records listed in d_big_list: LDS bitonic, 1024 threads
-hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const uint32_t* d_chunk_lo, const uint8_t* d_res,
-                                 const uint32_t* d_poff, uint32_t* d_ucount, const uint32_t* d_big_list, uint32_t* d_giant_list,
-                                 uint32_t max_blocks, uint32_t split_above, Counters* d_ctr, hipStream_t s);
+                             uint32_t* d_big_list, uint32_t* d_mid_list, Counters* d_ctr, hipStream_t s);
+hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
+                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
+                                 const uint32_t* d_mid_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s);
+hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
+                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
+                                 const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
+                                 uint32_t split_above, Counters* d_ctr, hipStream_t s);
 // chunks above BIG_CAP listed in d_giant_list: MSD split on the (mass, tag)
 // key into leaves sorted in LDS; a segment of one (mass, tag) key above
 // BIG_CAP falls back to global-memory scratch (ws_key / ws_k2).  segs: 5 lists
