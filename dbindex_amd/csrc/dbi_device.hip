@@ -2240,11 +2240,18 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
     }
     __syncthreads();
     uint32_t heads = 0;
-    for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        const bool dup = p > 0 && same_tag_at(k0, k1, p);
-        if (dup) a16[2 * atomicAdd(&s_u32[NT / 64], 1u) + 1] = (uint16_t)p;
-        a16[2 * p] = (uint16_t)(dup ? 0u : p);
-        heads += !dup;
+    for (uint32_t p0 = 0; p0 < m; p0 += NT) {  // wave-uniform trip count: one LDS atomic per wave
+        const uint32_t p = p0 + threadIdx.x;
+        const bool dup = p < m && p > 0 && same_tag_at(k0, k1, p);
+        const uint64_t bal = __ballot(dup);
+        uint32_t base = 0;
+        if (bal && lane_id() == 0) base = atomicAdd(&s_u32[NT / 64], (uint32_t)__popcll(bal));
+        base = __shfl(base, 0, 64);
+        if (dup) a16[2 * (base + (uint32_t)__popcll(bal & lanemask_lt())) + 1] = (uint16_t)p;
+        if (p < m) {
+            a16[2 * p] = (uint16_t)(dup ? 0u : p);
+            heads += !dup;
+        }
     }
     __syncthreads();
     // string-verify every pair in one parallel round (each check is a chain
@@ -2406,6 +2413,8 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
     __syncthreads();
     if (!BLOCK && sm.wide) return false;
     // small bins: rank inside the bin (k-major: a wave's lanes share bins), kept in registers with the key
+    // (ranking by a 64-bit compact key instead measured slower: the extra
+    // barriers and the order check cost more than the cheaper compares save)
     {
         unsigned long long v0[E], v1[E];
         uint32_t dst[E];
@@ -2418,15 +2427,7 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
             if (i < m && bhi - blo <= RANK_MAX_RUN) {
                 const unsigned long long a0 = k0[i], a1 = k1[i];
                 uint32_t rank = 0;
-#ifdef DBI_X_RANKOLD
                 for (uint32_t j = blo; j < bhi; ++j) rank += key_lt(k0[j], k1[j], a0, a1);
-#else
-                for (uint32_t j = blo; j < bhi; ++j) {  // q1 only read on equal q0 (duplicates)
-                    const unsigned long long b0 = k0[j];
-                    rank += b0 < a0;
-                    if (b0 == a0) rank += k1[j] < a1;
-                }
-#endif
                 v0[k] = a0;
                 v1[k] = a1;
                 dst[k] = blo + rank;
@@ -2462,7 +2463,11 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         for (uint32_t r = 0; r < nbig; ++r) {
             const uint32_t b = sm.big[r];
             const uint32_t lo = b & 0xFFFFu, L = (b >> 16) - lo;
+#ifdef DBI_X_NOBLOCK
+            (void)L;
+#else
             if (L > WAVE_SORT_MAX && !ck_run_block<NT, R>(k0, k1, lo, L, sm.mins)) block_bitonic<NT>(k0, k1, lo, L);
+#endif
         }
         __syncthreads();
     }
