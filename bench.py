@@ -430,6 +430,10 @@ def main() -> None:
                 "alg_bytes_per_launch": dom["alg_bytes"],
                 "avg_launch_ms": dom["avg_ms"],
             },
+            # the chunk sort runs as three kernels (chunk_sort, chunk_sort_mid for
+            # chunks with a bin above the one-wave sort, chunk_sort_big above
+            # CHUNK_CAP); together: 16 B in + 16 B out per record per build
+            "chunk_sort_family": chunk_family(kernels, st.n_total),
             "build_roofline": {
                 "alg_bytes": build_alg,
                 "formula": "R + 8(P+1) + 48N (SURVEY.md §8(d))",
@@ -447,6 +451,18 @@ def main() -> None:
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def chunk_family(kernels, n_total):
+    """The chunk-sort stages combined (warmup events, per build): time, 32 B per
+    record, fraction of the HBM peak."""
+    ms = sum(k["ms_per_build"] for k in kernels if k["kernel"].startswith("chunk_sort"))
+    if ms <= 0:
+        return None
+    alg = 32.0 * n_total
+    return dict(stages=[k["kernel"] for k in kernels if k["kernel"].startswith("chunk_sort")],
+                ms_per_build=ms, alg_bytes=alg, achieved=alg / (ms * 1e-3) / 1e9, peak=HBM_PEAK_GBPS,
+                unit="GB/s", frac=alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS)
 
 
 def host_threads() -> int:

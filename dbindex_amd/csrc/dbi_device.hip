@@ -20,10 +20,12 @@
 //      k_radix_scatter): 3 passes of <= 8 bits at SwissProt scale; each pass
 //      but the last writes the next pass's digit bytes for the next histogram.
 //   3. k_chunk_bounds     — chunks of whole bins, ~CHUNK_T records each.
-//   4. k_chunk_sort (<= CHUNK_CAP records, LDS), k_chunk_sort_big (<= BIG_CAP),
+//   4. k_chunk_sort (<= CHUNK_CAP records, LDS, bins up to 512 records),
+//      k_chunk_sort_list (chunks with a bigger bin; chunks up to BIG_CAP),
 //      k_giant_* (MSD split) — sort by the 128-bit record key (mass, tag, first
-//      appearance), string-verify equal (mass, tag) neighbours, flag unique
-//      heads (IndexMerge.getMergedData).
+//      appearance): small bins by rank, big bins by a 64-bit compact key in
+//      registers (DPP bitonic, dbi_lane.h); string-verify equal (mass, tag)
+//      neighbours, flag unique heads (IndexMerge.getMergedData).
 //   5. scan of per-chunk unique counts, k_finalize: unique table + occurrence
 //      CSR (protein ids, insertion order) + distinct mass-key count.
 // Queries: k_qdir_* (query directory), k_query (range per window),
