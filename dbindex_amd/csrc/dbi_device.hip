@@ -1314,6 +1314,11 @@ struct BinDigit {  // LSD radix over the fine mass bin: (bin >> shift) & mask
     __device__ __forceinline__ uint32_t next(uint64_t q0, int nshift, uint32_t nmask) const {
         return (bin_of(q0_mass(q0), bm) >> nshift) & nmask;
     }
+    // this pass's digit | the next pass's << 8, from one bin computation
+    __device__ __forceinline__ uint32_t both(uint64_t q0, int nshift, uint32_t nmask) const {
+        const uint32_t b = bin_of(q0_mass(q0), bm);
+        return ((b >> shift) & mask) | (((b >> nshift) & nmask) << 8);
+    }
     __device__ __forceinline__ void xform(uint4&) const {}
 };
 struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor)
@@ -1325,6 +1330,7 @@ struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor
         return d;
     }
     __device__ __forceinline__ uint32_t next(uint64_t, int, uint32_t) const { return 0u; }
+    __device__ __forceinline__ uint32_t both(uint64_t q0, int, uint32_t) const { return (*this)(q0); }
     __device__ __forceinline__ void xform(uint4& r) const {  // local -> global protein id
         const uint64_t q1 = u4_q1(r) + om.pid_add;
         r.z = (uint32_t)q1;
@@ -1334,6 +1340,7 @@ struct OwnerDigit {  // owner shard: number of splitter keys <= (int)(m * factor
 struct PairDigit {  // query routing pairs: q0 = owner shard, q1 = query index
     __device__ __forceinline__ uint32_t operator()(uint64_t q0) const { return (uint32_t)q0; }
     __device__ __forceinline__ uint32_t next(uint64_t, int, uint32_t) const { return 0u; }
+    __device__ __forceinline__ uint32_t both(uint64_t q0, int, uint32_t) const { return (uint32_t)q0 & 0xFFu; }
     __device__ __forceinline__ void xform(uint4&) const {}
 };
 
@@ -1426,8 +1433,10 @@ __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, Digit dig, int bits,
                 const uint32_t* __restrict__ offs, uint8_t* __restrict__ nd_out, int nshift, uint32_t nmask) {
     static_assert(RADIX_D <= RADIX_THREADS, "one digit per thread");
-    __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
+    static_assert(RADIX_CHUNK <= 65535, "16-bit counts");
+    __shared__ uint16_t cnt[RADIX_NW][RADIX_D];
     __shared__ uint4 stage[RADIX_CHUNK];  // the block's records in digit order
+    __shared__ uint16_t sdig[RADIX_CHUNK];  // their digit | next pass's digit << 8 (computed once)
     __shared__ uint32_t gofs[RADIX_D];    // global position of digit d's first record - its local start
     __shared__ uint32_t s_tmp[RADIX_NW + 1];
     const uint32_t D = 1u << bits;
@@ -1450,14 +1459,15 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
         const uint32_t i = base + k * 64 + lane;
         const bool valid = i < n && (!SPARSE || (rv[k].x & rv[k].y) != 0xFFFFFFFFu);
         vmask |= (uint32_t)valid << k;
-        const uint32_t d = dig(u4_q0(rv[k]));
+        const uint32_t dd = dig.both(u4_q0(rv[k]), nshift, nmask);
+        const uint32_t d = dd & 0xFFu;
         const uint64_t peers = digit_peers(d, valid, bits);
         const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t before = cnt[w][d];
         wave_sync();
-        if (valid && rank == 0) cnt[w][d] = before + (uint32_t)__popcll(peers);
+        if (valid && rank == 0) cnt[w][d] = (uint16_t)(before + (uint32_t)__popcll(peers));
         wave_sync();
-        dg[k] = d;
+        dg[k] = dd;
         pos[k] = before + rank;
     }
     __syncthreads();
@@ -1476,7 +1486,7 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
 #pragma unroll
         for (int ww = 0; ww < RADIX_NW; ++ww) {
             const uint32_t t = cnt[ww][d];
-            cnt[ww][d] = acc;
+            cnt[ww][d] = (uint16_t)acc;
             acc += t;
         }
         gofs[d] = offs[(size_t)d * gridDim.x + blockIdx.x] - lstart;
@@ -1485,18 +1495,24 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
     // exchange through LDS, then write digit runs with consecutive lanes on
     // consecutive addresses
 #pragma unroll
-    for (int k = 0; k < RADIX_ITEMS; ++k)
-        if (vmask & (1u << k)) stage[cnt[w][dg[k]] + pos[k]] = rv[k];
+    for (int k = 0; k < RADIX_ITEMS; ++k) {
+        if (vmask & (1u << k)) {
+            const uint32_t at = cnt[w][dg[k] & 0xFFu] + pos[k];
+            stage[at] = rv[k];
+            sdig[at] = (uint16_t)dg[k];
+        }
+    }
     __syncthreads();
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
     unsigned long long* __restrict__ out8 = reinterpret_cast<unsigned long long*>(out);
     for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) {
         uint4 r = stage[t];
-        const uint32_t dr = dig(u4_q0(r));
-        if (nd_out) nd_out[gofs[dr] + t] = (uint8_t)dig.next(u4_q0(r), nshift, nmask);
+        const uint32_t dd = sdig[t];
+        const uint32_t at = gofs[dd & 0xFFu] + t;
+        if (nd_out) nd_out[at] = (uint8_t)(dd >> 8);
         dig.xform(r);
-        if (NARROW) out8[gofs[dr] + t] = u4_q1(r);
-        else out4[gofs[dr] + t] = r;
+        if (NARROW) out8[at] = u4_q1(r);
+        else out4[at] = r;
     }
 }
 
@@ -1943,6 +1959,9 @@ __device__ void block_bitonic(unsigned long long* k0, unsigned long long* k1, ui
 #ifdef DBI_X_CKSTAT
 __device__ unsigned int g_ck_stat[8];
 #endif
+#ifdef DBI_X_PHASE
+__device__ unsigned long long g_phase[24];  // sort_chunk phase clocks: [kernel*8 + phase]
+#endif
 constexpr int CK_IDX_BITS = 13;
 constexpr int CK_D_BITS = 64 - 16 - CK_IDX_BITS;
 
@@ -2349,6 +2368,19 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
     static_assert(E <= 32, "run-head bit mask");
     unsigned long long* k0 = sm.k0;
     unsigned long long* k1 = sm.k1;
+#ifdef DBI_X_PHASE
+    uint64_t ph_t = wall_clock64();
+#define DBI_PH(i)                                                                               \
+    do {                                                                                        \
+        const uint64_t t_ = wall_clock64();                                                     \
+        if (threadIdx.x == 0) atomicAdd(&g_phase[(BLOCK ? (NT == 512 ? 8 : 16) : 0) + (i)], t_ - ph_t); \
+        ph_t = t_;                                                                              \
+    } while (0)
+#else
+#define DBI_PH(i) \
+    do {          \
+    } while (0)
+#endif
     if (threadIdx.x == 0) {
         sm.nbig = 0;
         sm.wide = 0;
@@ -2372,6 +2404,7 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         }
     }
     __syncthreads();
+    DBI_PH(1);
     // bin runs: thread t owns records [t*E, t*E+E); run bounds of each record
     // from a block max-scan (last run start <= i) and a reverse min-scan
     // (first run start > i), kept in registers
@@ -2413,6 +2446,7 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         }
     }
     __syncthreads();
+    DBI_PH(2);
     if (!BLOCK && sm.wide) return false;
     // small bins: rank inside the bin (k-major: a wave's lanes share bins), kept in registers with the key
     // (ranking by a 64-bit compact key instead measured slower: the extra
@@ -2444,6 +2478,7 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
             }
         }
     }
+    DBI_PH(3);
     // big bins, in place (disjoint from the small bins)
     const uint32_t nbig = sm.nbig;
     for (uint32_t r = threadIdx.x >> 6; r < nbig; r += NW) {
@@ -2459,6 +2494,7 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         if (!done) wave_bitonic(k0, k1, lo, L);
     }
     __syncthreads();
+    DBI_PH(4);
     if constexpr (BLOCK) {
         constexpr int R = NT * 4 >= CAP ? 4 : 8;
         static_assert(NT * R >= CAP, "compact-sort capacity");
@@ -2472,8 +2508,10 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
 #endif
         }
         __syncthreads();
+        DBI_PH(5);
     }
     *heads_out = finish_sorted<NT>(out, m, rl, k0, k1, sm.aux, sm.u32, &sm.bad);
+    DBI_PH(6);
     return true;
 }
 
@@ -2589,6 +2627,128 @@ hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, 
     DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS, BIG_CAP, true>), dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in,
                d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list,
                std::min<uint32_t>(split_above, (uint32_t)BIG_CAP), d_ctr);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// inline '[formula]' PTMs (DBIndexer.java:288-303): the proteins that carry
+// them, one thread each, walked literally.  The first start whose walk reaches
+// a formula adds its mass as one more step (pepSize + 1, the residue before it
+// counted again by isEnzyme and checkCleavage, :295-318) and removes it from
+// the protein; every later start sees the protein without it.  Here the
+// protein is given stripped (sres) with its formulas as events (position in
+// the stripped protein = index of the residue that followed ']'; mass, NaN for
+// an unknown element: the exception ends the protein, :400-403), and the
+// pending events stand in for the '[' characters checkCleavage still sees.
+// Peptide identity (tag, later the string verification) is the protein as
+// stored in the ProteinCache -- with its formulas -- at the stripped offsets
+// (IndexMerge reads getPeptideSequence(protId, offset, length), :452).
+// COUNT: kept records per protein; EMIT: the records at base[i], counters.
+// ---------------------------------------------------------------------------
+template <bool EMIT>
+__global__ void __launch_bounds__(64)
+k_ptm_digest(DevParams dp, const double* __restrict__ mass_tab, const uint8_t* __restrict__ flags_tab,
+             const uint8_t* __restrict__ sres, const uint32_t* __restrict__ soff, const uint8_t* __restrict__ ores,
+             const uint32_t* __restrict__ ooff, const uint32_t* __restrict__ ptm_pid,
+             const uint32_t* __restrict__ ev_off, const uint32_t* __restrict__ ev_pos,
+             const double* __restrict__ ev_mass, uint32_t n_ptm, uint32_t* __restrict__ cnt,
+             Rec* __restrict__ out, Counters* __restrict__ ctr) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_ptm) return;
+    const uint8_t* __restrict__ T = sres + soff[i];
+    const uint32_t Ls = soff[i + 1] - soff[i];
+    const uint32_t pid = ptm_pid[i];
+    const uint8_t* __restrict__ O = ores + ooff[pid];
+    const uint32_t eb = ev_off[i], ee = ev_off[i + 1];
+    const uint32_t w = rec_width(ctr->max_plen);
+    Rec* __restrict__ o = EMIT ? out + cnt[i] : nullptr;  // EMIT: cnt holds the exclusive offsets
+    const bool can_drop = dp.drop_mass <= dp.max_mh;
+    uint32_t kept = 0, dropped = 0;
+    uint32_t k = eb;  // first formula not yet removed
+    bool dead = false;
+    for (uint32_t s = 0; s < Ls && !dead; ++s) {
+        double m = dp.m0;                  // :265-271
+        int mc = -1;                       // :280
+        uint32_t pep = 0;                  // pepSize
+        uint32_t p = s;                    // next residue
+        bool mand_all = false, mand_excl = false;  // mandatory residue in [s, p) / [s, p-1)
+        while (m <= dp.max_mh) {           // :284 (end < length below)
+            uint32_t q;                    // end: the peptide's last residue
+            if (k < ee && ev_pos[k] == p) {  // '[' at end (:288-303)
+                const double f = ev_mass[k];
+                if (!(f == f)) {
+                    dead = true;
+                    break;
+                }
+                ++pep;
+                m = m + f;
+                ++k;
+                q = p - 1;
+            } else {
+                if (p >= Ls) break;
+                ++pep;
+                m = m + mass_tab[T[p]];    // :306-308
+                q = p;
+                ++p;
+                mand_excl = mand_all;
+                mand_all = mand_all || (flags_tab[T[q]] & F_MAND) != 0;
+            }
+            const uint8_t fq = flags_tab[T[q]];
+            mc += (fq & F_CLEAVE) ? 1 : 0;  // isEnzyme(protSeq.charAt(end)) (:314-316)
+            // checkCleavage over the current protein: a pending formula right
+            // after end is a '[' (no cleave / no-cut residue), and end is the
+            // protein's last character only with no formula after it
+            const bool nxt_f = k < ee && ev_pos[k] == q + 1;
+            const bool n_ok = s == 0 || ((flags_tab[T[s - 1]] & F_CLEAVE) && !(flags_tab[T[s]] & F_NOCUT));
+            const bool c_ok = (q + 1 == Ls && !nxt_f) ||
+                              ((fq & F_CLEAVE) && (nxt_f || q + 1 >= Ls || !(flags_tab[T[q + 1]] & F_NOCUT)));
+            const bool cut = dp.semi ? (n_ok || c_ok) : (n_ok && c_ok);  // :318
+            if (!cut) continue;
+            if (mc > dp.max_missed) break;     // :322-324
+            if (m > dp.max_mh) break;          // :326-329
+            if (!(pep >= (uint32_t)dp.min_len && m >= dp.min_mh)) continue;  // :331
+            if (dp.mand_mode && !mand_all) break;  // :334-344
+            bool keep = !dp.mand_filter || mand_excl;  // filterSequence (SQLiteMult :245-268)
+            if (dp.filter) {                   // MassRangeFilteringIndex.filterSequence
+                if (m > dp.win_max) break;     // SKIP_PROTEIN_START (:351-354)
+                keep = keep && in_windows(dp, m);
+            }
+            if (!keep) continue;
+            if (can_drop && m >= dp.drop_mass) {  // bucket > NUM_BUCKETS-1 (SQLiteMult :282-288)
+                ++dropped;
+                continue;
+            }
+            if (EMIT) {
+                const uint32_t len = q - s + 1;  // curSeqI
+                uint32_t h = FNV32_OFFSET;
+                for (uint32_t j = 0; j < len; ++j) h = fnv32_step(h, O[s + j]);
+                const uint32_t tag = fold_tag(h);
+                o[kept] = Rec{rec_q0(m, tag), rec_q1(tag, rec_loc(pid, s, w), len)};
+            }
+            ++kept;
+        }
+    }
+    if (!EMIT) {
+        cnt[i] = kept;
+    } else {
+        if (kept) atomicAdd(&ctr->n_kept, (unsigned long long)kept);
+        if (dropped) atomicAdd(&ctr->n_dropped, (unsigned long long)dropped);
+    }
+}
+
+hipError_t launch_ptm_digest(bool emit, const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                             const uint8_t* d_sres, const uint32_t* d_soff, const uint8_t* d_ores,
+                             const uint32_t* d_ooff, const uint32_t* d_pid, const uint32_t* d_ev_off,
+                             const uint32_t* d_ev_pos, const double* d_ev_mass, uint32_t n_ptm, uint32_t* d_cnt,
+                             Rec* d_out, Counters* d_ctr, hipStream_t s) {
+    if (n_ptm == 0) return hipSuccess;
+    const dim3 g((n_ptm + 63) / 64);
+    if (emit)
+        DBI_LAUNCH(k_ptm_digest<true>, g, dim3(64), 0, s, dp, d_mass_tab, d_flags, d_sres, d_soff, d_ores, d_ooff,
+                   d_pid, d_ev_off, d_ev_pos, d_ev_mass, n_ptm, d_cnt, d_out, d_ctr);
+    else
+        DBI_LAUNCH(k_ptm_digest<false>, g, dim3(64), 0, s, dp, d_mass_tab, d_flags, d_sres, d_soff, d_ores, d_ooff,
+                   d_pid, d_ev_off, d_ev_pos, d_ev_mass, n_ptm, d_cnt, d_out, d_ctr);
     return hipGetLastError();
 }
 
@@ -3560,6 +3720,16 @@ hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_ch
 }
 
 }  // namespace dbi
+#ifdef DBI_X_PHASE
+namespace dbi {
+void phase_read(unsigned long long* v) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 24);
+    unsigned long long z[24] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z));
+}
+}  // namespace dbi
+#endif
 #ifdef DBI_X_CKSTAT
 namespace dbi {
 void ck_stat_read(unsigned int* v) {

@@ -120,6 +120,13 @@ struct dbi_handle {
     DevBuf<Rec> recA, recB;
     DevBuf<uint32_t> hist;
     DevBuf<uint8_t> digits;             // radix: next pass's digit per record
+    // inline '[formula]' PTM builds (dbi_build): the digest input (formulas
+    // stripped, PTM proteins masked), those proteins stripped, their formula
+    // events, and the mass table with the mask residue
+    DevBuf<uint8_t> res_dig, ptm_res;
+    DevBuf<uint32_t> poff_dig, ptm_soff, ptm_pid, ptm_evoff, ptm_evpos, ptm_cnt;
+    DevBuf<double> ptm_evmass, mass_tab_x;
+    DevBuf<unsigned long long> ptm_total;
     DevBuf<uint32_t> ucount, big_list, mid_list, giant_list, chunk_lo;
     DevBuf<uint4> segs;                 // giant-chunk split: segment lists
     DevBuf<uint16_t> synth_len;         // dbi_synth_proteome: length quantile table

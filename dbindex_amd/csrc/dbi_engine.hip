@@ -11,6 +11,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -236,6 +237,17 @@ int finish_build(dbi_handle* h) {
     st.n_keys = h->hc.n_keys;
     for (int i = 0; i < 8; ++i) st.n_keys += h->hc.n_keys_shard[i];
     st.n_big_bins = h->hc.n_big;  // chunks above CHUNK_CAP (of which n_giant above BIG_CAP)
+#ifdef DBI_X_PHASE
+    {
+        unsigned long long v[24] = {};
+        extern void phase_read(unsigned long long*);
+        phase_read(v);
+        for (int k = 0; k < 3; ++k)
+            fprintf(stderr, "phase %s: load %.1f runs %.1f rank %.1f wave %.1f block %.1f finish %.1f (Mclk summed over blocks)\n",
+                    k == 0 ? "chunk" : k == 1 ? "mid" : "big", v[8 * k + 1] / 1e6, v[8 * k + 2] / 1e6, v[8 * k + 3] / 1e6,
+                    v[8 * k + 4] / 1e6, v[8 * k + 5] / 1e6, v[8 * k + 6] / 1e6);
+    }
+#endif
 #ifdef DBI_X_CKSTAT
     {
         unsigned int v[8] = {};
@@ -392,10 +404,196 @@ int check_offsets_host(const uint64_t* off, uint64_t n_res, uint64_t n_prot) {
     return 0;
 }
 
-int check_residues_host(const uint8_t* res, uint64_t n) {
-    for (uint64_t i = 0; i < n; ++i)
-        if (res[i] == '[') return set_error(DBI_E_INVALID, "inline '[formula]' PTMs are not supported (DBIndexer.java:288-303)");
+// ---- inline '[formula]' PTMs (DBIndexer.java:288-303) ------------------------
+// FormulaCalculator.calculateMass lives in the un-vendored
+// edu.scripps.yates.utilities jar: restated as the left-to-right sum of
+// count x monoisotopic element mass (element = capital letter + lower-case
+// letters, count = optional [-]digits, default 1); an unknown element is NaN
+// (UnknownElementMassException).  Parity unpinned.
+double formula_mass(const std::string& f) {
+    static const std::pair<const char*, double> kEl[] = {
+        {"H", 1.00782503207}, {"D", 2.0141017778}, {"C", 12.0}, {"N", 14.0030740048}, {"O", 15.99491461956},
+        {"P", 30.97376163}, {"S", 31.97207100}, {"Se", 79.9165213}, {"Na", 22.9897692809}, {"K", 38.96370668},
+        {"Li", 7.01600455}, {"Mg", 23.9850417}, {"Ca", 39.96259098}, {"Fe", 55.9349375}, {"Zn", 63.9291422},
+        {"Cu", 62.9295975}, {"Cl", 34.96885268}, {"Br", 78.9183371}, {"I", 126.904473}, {"F", 18.99840322},
+        {"Si", 27.9769265325}, {"B", 11.0093054}, {"Hg", 201.970643}};
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    double mass = 0.0;
+    size_t i = 0;
+    while (i < f.size()) {
+        if (!(f[i] >= 'A' && f[i] <= 'Z')) return nan;
+        size_t j = i + 1;
+        while (j < f.size() && f[j] >= 'a' && f[j] <= 'z') ++j;
+        const std::string el = f.substr(i, j - i);
+        bool neg = false;
+        if (j < f.size() && f[j] == '-') {
+            neg = true;
+            ++j;
+        }
+        long cnt = 0;
+        size_t k = j;
+        while (k < f.size() && f[k] >= '0' && f[k] <= '9' && cnt < 100000000) cnt = cnt * 10 + (f[k++] - '0');
+        if (k == j) {
+            if (neg) return nan;
+            cnt = 1;
+        }
+        double em = nan;
+        for (const auto& e : kEl)
+            if (el == e.first) em = e.second;
+        if (!(em == em)) return nan;
+        mass = mass + (double)(neg ? -cnt : cnt) * em;
+        i = k;
+    }
+    return mass;
+}
+
+// Formulas out of every protein: the stripped proteome (digest input), and per
+// protein carrying formulas its events -- position in the stripped protein
+// (the residue that followed ']'), mass (NaN: unknown element).  A formula
+// string seen earlier in the same protein is dropped: String.replace removed
+// every copy when the first was reached (:298).
+struct PtmPlan {
+    std::vector<uint8_t> stripped;
+    std::vector<uint64_t> soff;
+    std::vector<uint32_t> pid, ev_off, ev_pos;
+    std::vector<double> ev_mass;
+};
+
+int plan_ptms(const uint8_t* res, const uint64_t* off, uint64_t n_prot, PtmPlan& pl) {
+    pl.stripped.reserve(off[n_prot]);
+    pl.soff.assign(1, 0);
+    pl.ev_off.assign(1, 0);
+    for (uint64_t i = 0; i < n_prot; ++i) {
+        const uint64_t b = off[i], e = off[i + 1];
+        if (!std::memchr(res + b, '[', e - b)) {
+            pl.stripped.insert(pl.stripped.end(), res + b, res + e);
+            pl.soff.push_back(pl.stripped.size());
+            continue;
+        }
+        const size_t p0 = pl.stripped.size();
+        std::vector<std::string> seen;
+        for (uint64_t x = b; x < e;) {
+            if (res[x] != '[') {
+                pl.stripped.push_back(res[x++]);
+                continue;
+            }
+            const uint8_t* close = (const uint8_t*)std::memchr(res + x + 1, ']', e - x - 1);
+            if (!close)
+                return set_error(DBI_E_INVALID, "protein " + std::to_string(i) +
+                                                    ": '[' without ']' (the reference reads past the protein: "
+                                                    "StringIndexOutOfBoundsException, DBIndexer.java:291)");
+            const std::string f((const char*)res + x + 1, (size_t)(close - res) - x - 1);
+            x = (uint64_t)(close - res) + 1;
+            if (std::find(seen.begin(), seen.end(), f) != seen.end()) continue;
+            seen.push_back(f);
+            const uint32_t pos = (uint32_t)(pl.stripped.size() - p0);
+            const double m = formula_mass(f);
+            if (pos == 0 && m == m)
+                return set_error(DBI_E_INVALID, "protein " + std::to_string(i) +
+                                                    ": a '[formula]' before its first residue (the reference reads "
+                                                    "charAt(-1): StringIndexOutOfBoundsException, DBIndexer.java:300-314)");
+            pl.ev_pos.push_back(pos);
+            pl.ev_mass.push_back(m);
+        }
+        pl.soff.push_back(pl.stripped.size());
+        pl.pid.push_back((uint32_t)i);
+        pl.ev_off.push_back((uint32_t)pl.ev_pos.size());
+    }
     return 0;
+}
+
+int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off, uint64_t n_prot);
+
+int build_with_ptms(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off,
+                    uint64_t n_prot) {
+    PtmPlan pl;
+    int rc;
+    if ((rc = plan_ptms(residues, prot_off, n_prot, pl))) return rc;
+    const uint64_t Rs = pl.stripped.size();
+    const uint32_t n_ptm = (uint32_t)pl.pid.size();
+    hipStream_t s = h->stream;
+    // the engine keeps the proteins as given (the ProteinCache's strings: tags,
+    // string verification and every later lookup read them at the stripped
+    // offsets, as IndexMerge does); the digest runs over the stripped proteome
+    // with the formula-carrying proteins masked (a residue above maxMH), and
+    // those proteins are walked literally by k_ptm_digest
+    if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
+    std::vector<uint8_t> masked = pl.stripped;
+    std::vector<uint8_t> sres;
+    std::vector<uint32_t> soff32(1, 0), off32(n_prot + 1);
+    for (uint32_t j = 0; j < n_ptm; ++j) {
+        const uint64_t b = pl.soff[pl.pid[j]], e = pl.soff[pl.pid[j] + 1];
+        sres.insert(sres.end(), pl.stripped.begin() + b, pl.stripped.begin() + e);
+        soff32.push_back((uint32_t)sres.size());
+        std::memset(masked.data() + b, 1, e - b);
+    }
+    for (uint64_t i = 0; i <= n_prot; ++i) off32[i] = (uint32_t)pl.soff[i];
+    double tab[256];
+    DBI_HIP(hipMemcpy(tab, h->mass_tab.p, sizeof(tab), hipMemcpyDeviceToHost));
+    tab[1] = 1e300;  // the mask residue: every walk over it ends at its first step
+    if ((rc = h->res_dig.ensure(Rs + 16)) || (rc = h->poff_dig.ensure(n_prot + 1)) ||
+        (rc = h->mass_tab_x.ensure(256)) || (rc = h->ptm_res.ensure(sres.size() + 16)) ||
+        (rc = h->ptm_soff.ensure(n_ptm + 1)) || (rc = h->ptm_pid.ensure(n_ptm)) ||
+        (rc = h->ptm_evoff.ensure(n_ptm + 1)) || (rc = h->ptm_evpos.ensure(pl.ev_pos.size())) ||
+        (rc = h->ptm_evmass.ensure(pl.ev_mass.size())) || (rc = h->ptm_cnt.ensure(n_ptm + 1)) ||
+        (rc = h->ptm_total.ensure(1)) ||
+        (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(n_ptm + 1), h->scan_tmp.cap))))
+        return rc;
+    if (Rs) DBI_HIP(hipMemcpyAsync(h->res_dig.p, masked.data(), Rs, hipMemcpyHostToDevice, s));
+    DBI_HIP(hipMemcpyAsync(h->poff_dig.p, off32.data(), 4 * (n_prot + 1), hipMemcpyHostToDevice, s));
+    DBI_HIP(hipMemcpyAsync(h->mass_tab_x.p, tab, sizeof(tab), hipMemcpyHostToDevice, s));
+    if (!sres.empty()) DBI_HIP(hipMemcpyAsync(h->ptm_res.p, sres.data(), sres.size(), hipMemcpyHostToDevice, s));
+    DBI_HIP(hipMemcpyAsync(h->ptm_soff.p, soff32.data(), 4 * (n_ptm + 1), hipMemcpyHostToDevice, s));
+    DBI_HIP(hipMemcpyAsync(h->ptm_pid.p, pl.pid.data(), 4 * n_ptm, hipMemcpyHostToDevice, s));
+    DBI_HIP(hipMemcpyAsync(h->ptm_evoff.p, pl.ev_off.data(), 4 * (n_ptm + 1), hipMemcpyHostToDevice, s));
+    if (!pl.ev_pos.empty()) {
+        DBI_HIP(hipMemcpyAsync(h->ptm_evpos.p, pl.ev_pos.data(), 4 * pl.ev_pos.size(), hipMemcpyHostToDevice, s));
+        DBI_HIP(hipMemcpyAsync(h->ptm_evmass.p, pl.ev_mass.data(), 8 * pl.ev_mass.size(), hipMemcpyHostToDevice, s));
+    }
+    DBI_HIP(hipStreamSynchronize(s));  // host staging vectors die here
+    // the digest over the masked stripped proteome (its own offsets, length,
+    // mass table; the cut-stepping count assumes residue masses < 1024 Da)
+    const uint8_t* o_res = h->d_res;
+    const uint32_t* o_off = h->d_poff;
+    const int cut_count = h->dp.cut_count;
+    h->d_res = h->res_dig.p;
+    h->d_poff = h->poff_dig.p;
+    h->n_res = Rs;
+    h->dp.cut_count = 0;
+    std::swap(h->mass_tab, h->mass_tab_x);
+    uint64_t n = 0, n_in = 0;
+    bool sparse = false;
+    rc = run_digest(h, &n, &n_in, &sparse);
+    std::swap(h->mass_tab, h->mass_tab_x);
+    h->dp.cut_count = cut_count;
+    h->d_res = o_res;
+    h->d_poff = o_off;
+    h->n_res = n_res;
+    if (rc) return rc;
+    // the formula-carrying proteins: count, offsets, emit after the digest's slots
+    DBI_HIP(launch_ptm_digest(false, h->dp, h->mass_tab.p, h->flags_tab.p, h->ptm_res.p, h->ptm_soff.p, h->d_res,
+                              h->d_poff, h->ptm_pid.p, h->ptm_evoff.p, h->ptm_evpos.p, h->ptm_evmass.p, n_ptm,
+                              h->ptm_cnt.p, nullptr, h->ctr.p, s));
+    DBI_HIP(launch_scan_u32(h->ptm_cnt.p, h->ptm_cnt.p, n_ptm, h->scan_tmp.p, h->scan_tmp.cap, h->ptm_total.p, s));
+    unsigned long long extra = 0;
+    DBI_HIP(hipMemcpyAsync(&extra, h->ptm_total.p, sizeof(extra), hipMemcpyDeviceToHost, s));
+    DBI_HIP(hipStreamSynchronize(s));
+    if (n_in + extra >= (1ull << 32) - 1)
+        return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences on one device: shard the FASTA");
+    if (h->recA.cap < n_in + extra) {  // grow, keeping the digest's records
+        DevBuf<Rec> grown;
+        if ((rc = grown.ensure(n_in + extra))) return rc;
+        if (n_in) DBI_HIP(hipMemcpyAsync(grown.p, h->recA.p, sizeof(Rec) * n_in, hipMemcpyDeviceToDevice, s));
+        DBI_HIP(hipStreamSynchronize(s));
+        std::swap(h->recA, grown);
+        grown.release();
+    }
+    DBI_HIP(launch_ptm_digest(true, h->dp, h->mass_tab.p, h->flags_tab.p, h->ptm_res.p, h->ptm_soff.p, h->d_res,
+                              h->d_poff, h->ptm_pid.p, h->ptm_evoff.p, h->ptm_evpos.p, h->ptm_evmass.p, n_ptm,
+                              h->ptm_cnt.p, h->recA.p + n_in, h->ctr.p, s));
+    if ((rc = read_counters(h))) return rc;
+    return build_tail(h, h->hc.n_kept, h->params.min_mh, h->params.max_mh, n_in + extra, sparse);
 }
 
 int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off, uint64_t n_prot) {
@@ -544,6 +742,9 @@ void dbi_close(dbi_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->mass_tab.release(); h->flags_tab.release(); h->ctr.release();
+    h->res_dig.release(); h->ptm_res.release(); h->poff_dig.release(); h->ptm_soff.release(); h->ptm_pid.release();
+    h->ptm_evoff.release(); h->ptm_evpos.release(); h->ptm_cnt.release(); h->ptm_evmass.release();
+    h->mass_tab_x.release(); h->ptm_total.release();
     h->res.release(); h->poff64.release(); h->poff.release(); h->poff_g.release();
     h->samp.release(); h->xcount.release(); h->xsend.release(); h->xrecv.release();
     h->qcnt.release(); h->qpairA.release(); h->qpairB.release(); h->qsend.release(); h->qrecv.release();
@@ -571,7 +772,10 @@ int dbi_build(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint
     if (!h || (!residues && n_res) || !prot_off) return set_error(DBI_E_INVALID, "NULL argument");
     int rc;
     if ((rc = check_offsets_host(prot_off, n_res, n_prot))) return rc;
-    if ((rc = check_residues_host(residues, n_res))) return rc;
+    if (n_res && std::memchr(residues, '[', n_res)) {  // inline '[formula]' PTMs
+        if ((rc = build_with_ptms(h, residues, n_res, prot_off, n_prot))) return rc;
+        return finish_build(h);
+    }
     if ((rc = begin_build(h, n_res, n_prot))) return rc;
     if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
     if ((rc = build_digest(h))) return rc;

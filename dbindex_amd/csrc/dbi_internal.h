@@ -208,6 +208,13 @@ hipError_t launch_digest_emit(const DevParams& dp, const double* d_mass_tab, con
 hipError_t launch_scan_u32(const uint32_t* d_in, uint32_t* d_out, uint64_t n, uint32_t* d_block_tmp,
                            uint64_t tmp_elems, unsigned long long* d_total, hipStream_t s);
 size_t scan_u32_tmp_elems(uint64_t n);
+// inline-PTM proteins, one thread each (COUNT: per-protein kept counts into
+// d_cnt; EMIT: d_cnt = exclusive offsets into d_out, counters updated)
+hipError_t launch_ptm_digest(bool emit, const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                             const uint8_t* d_sres, const uint32_t* d_soff, const uint8_t* d_ores,
+                             const uint32_t* d_ooff, const uint32_t* d_pid, const uint32_t* d_ev_off,
+                             const uint32_t* d_ev_pos, const double* d_ev_mass, uint32_t n_ptm, uint32_t* d_cnt,
+                             Rec* d_out, Counters* d_ctr, hipStream_t s);
 
 // Owner map of a sharded build (dbi_shard_*): shard d owns the mass keys
 // (int)(m * factor) in [split[d-1], split[d]) (split[-1] = -inf, split[n-1] =

@@ -267,6 +267,9 @@ int dbi_store_stop_add_seq(dbi_store* s) {
     const uint64_t P = s->defs.size();
     if (s->unindexed == DBI_UNINDEXED_STREAM) {
         // proteins to HBM once; each search digests them through its windows
+        if (!s->residues.empty() && std::memchr(s->residues.data(), '[', s->residues.size()))
+            return set_error(DBI_E_INVALID, "inline '[formula]' PTMs need the resident unindexed mode (the streaming "
+                                            "search re-digests the proteins as stored)");
         if ((rc = dbi_set_windows(s->eng, nullptr, nullptr, 0, 1))) return rc;
         rc = dbi_build(s->eng, s->residues.data(), s->residues.size(), s->off.data(), P);
     } else if (s->device_digest) {

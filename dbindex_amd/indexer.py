@@ -87,8 +87,8 @@ class DBIndexer:
 
     # DBIndexerHip.cutSeq: only hand the protein to the store (DBIndexer.java:251)
     def cutSeq(self, protAccession: str, protSeq: str) -> None:
-        if "[" in protSeq:
-            raise DBIndexerException("inline [formula] PTMs are not supported (DBIndexer.java:288-303)")
+        # inline '[formula]' PTMs (DBIndexer.java:288-303) are digested on the
+        # device as the reference does (dbi_build: k_ptm_digest)
         self.protNum += 1
         self.indexStore.addProteinDef(self.protNum, protAccession, protSeq)
 

@@ -29,9 +29,8 @@ public class DBIndexerHip extends DBIndexer {
 
     @Override
     protected void cutSeq(final String protAccession, String protSeq) throws IOException {
-        if (protSeq.indexOf('[') >= 0) {  // inline [formula] PTMs (DBIndexer.java:288-303): not supported
-            throw new IOException("inline [formula] PTMs are not supported by the MI355X store");
-        }
+        // inline [formula] PTMs (DBIndexer.java:288-303) go to the store as they
+        // are: the engine strips them and walks their proteins as cutSeq does
         try {
             indexStore.addProteinDef(++protNum, protAccession, protSeq);  // as cutSeq does (:251)
         } catch (final Exception e) {

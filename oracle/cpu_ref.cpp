@@ -26,6 +26,7 @@
 //   getNumberSequences ..... DBIndexStoreSQLiteByte.java:667-690 (rows, not peptides)
 //   Enzyme.checkCleavage ... external; pinned rule in DESIGN.md (semantics A3)
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -85,11 +86,137 @@ int filter_sequence(const dbi_params* p, double precMass, const uint8_t* pep, in
     return DBI_FILTER_INCLUDE;
 }
 
+// FormulaCalculator.calculateMass (external jar, not vendored): the restated
+// monoisotopic element sum the product uses too (dbi_engine.hip formula_mass);
+// NaN = unknown element (UnknownElementMassException).  Parity unpinned.
+double formula_mass(const std::string& f) {
+    static const std::pair<const char*, double> kEl[] = {
+        {"H", 1.00782503207}, {"D", 2.0141017778}, {"C", 12.0}, {"N", 14.0030740048}, {"O", 15.99491461956},
+        {"P", 30.97376163}, {"S", 31.97207100}, {"Se", 79.9165213}, {"Na", 22.9897692809}, {"K", 38.96370668},
+        {"Li", 7.01600455}, {"Mg", 23.9850417}, {"Ca", 39.96259098}, {"Fe", 55.9349375}, {"Zn", 63.9291422},
+        {"Cu", 62.9295975}, {"Cl", 34.96885268}, {"Br", 78.9183371}, {"I", 126.904473}, {"F", 18.99840322},
+        {"Si", 27.9769265325}, {"B", 11.0093054}, {"Hg", 201.970643}};
+    double mass = 0.0;
+    size_t i = 0;
+    while (i < f.size()) {
+        if (!(f[i] >= 'A' && f[i] <= 'Z')) return NAN;
+        size_t j = i + 1;
+        while (j < f.size() && f[j] >= 'a' && f[j] <= 'z') ++j;
+        const std::string el = f.substr(i, j - i);
+        bool neg = false;
+        if (j < f.size() && f[j] == '-') {
+            neg = true;
+            ++j;
+        }
+        long cnt = 0;
+        size_t k = j;
+        while (k < f.size() && f[k] >= '0' && f[k] <= '9' && cnt < 100000000) cnt = cnt * 10 + (f[k++] - '0');
+        if (k == j) {
+            if (neg) return NAN;
+            cnt = 1;
+        }
+        double em = NAN;
+        for (const auto& e : kEl)
+            if (el == e.first) em = e.second;
+        if (std::isnan(em)) return NAN;
+        mass = mass + (double)(neg ? -cnt : cnt) * em;
+        i = k;
+    }
+    return mass;
+}
+
+// Java String.replace(CharSequence, CharSequence): every non-overlapping copy, left to right
+void replace_all(std::string& s, const std::string& pat) {
+    std::string r;
+    size_t i = 0;
+    for (size_t at; (at = s.find(pat, i)) != std::string::npos; i = at + pat.size()) r.append(s, i, at - i);
+    r.append(s, i, std::string::npos);
+    s.swap(r);
+}
+
+// cutSeq over a protein carrying inline '[formula]' PTMs, literally: the
+// protein string is mutated as the reference does (:288-303).  Returns false
+// where the reference throws StringIndexOutOfBoundsException out of cutSeq
+// (a formula before the first residue, '[' without ']').
+bool cut_seq_literal(const dbi_params* p, std::string protSeq, uint32_t proteinId, std::vector<Occ>& out) {
+    Enzyme enz{p};
+    const int maxIntCleavage = p->max_missed;
+    const int bucketRange = MAX_PRECURSOR_INT / p->index_factor;
+    int length = (int)protSeq.size();
+    for (int start = 0; start < length; ++start) {
+        int end = start;
+        double precMass = 0;
+        if (p->add_h2o_proton) precMass += p->h2o_proton;
+        precMass += p->cterm;
+        precMass += p->nterm;
+        int pepSize = 0;
+        int intMisCleavageCount = -1;
+        std::string pepSeq;
+        while (precMass <= p->max_mh && end < length) {
+            pepSize++;
+            const char curIon = protSeq[end];
+            double aaMass;
+            if (curIon == '[') {
+                std::string formula;
+                for (;;) {
+                    if (++end >= length) return false;  // charAt past the end
+                    if (protSeq[end] == ']') break;
+                    formula += protSeq[end];
+                }
+                aaMass = formula_mass(formula);
+                if (std::isnan(aaMass)) return true;  // UnknownElementMassException: caught, cutSeq ends (:400-403)
+                replace_all(protSeq, "[" + formula + "]");
+                end -= (int)formula.size() + 2;
+                length = (int)protSeq.size();
+            } else {
+                pepSeq += curIon;
+                aaMass = p->mass[(uint8_t)curIon];
+            }
+            precMass = precMass + aaMass;
+            if (end < 0) return false;  // charAt(-1)
+            const uint8_t* seq = (const uint8_t*)protSeq.data();
+            if (enz.isEnzyme(seq[end])) intMisCleavageCount++;
+            if (enz.checkCleavage(seq, length, start, end)) {
+                if (intMisCleavageCount > maxIntCleavage) break;
+                if (precMass > p->max_mh) break;
+                const int curSeqI = (int)pepSeq.size();
+                if (pepSize >= p->min_len && precMass >= p->min_mh) {
+                    const uint8_t* pep = (const uint8_t*)pepSeq.data();
+                    if (p->mandatory_mode) {
+                        bool found = false;
+                        for (int c = 0; c < 256 && !found; ++c) {
+                            if (!p->mandatory[c]) continue;
+                            for (int i = 0; i < curSeqI; ++i)
+                                if (pep[i] == c) { found = true; break; }
+                        }
+                        if (!found) break;
+                    }
+                    int fr = filter_sequence(p, precMass, pep, curSeqI);
+                    if (fr == DBI_FILTER_SKIP_PROTEIN_START) break;
+                    if (fr == DBI_FILTER_INCLUDE) {
+                        int bucket = java_d2i(precMass) / bucketRange;
+                        out.push_back(Occ{precMass, proteinId, (uint32_t)start, (uint32_t)curSeqI,
+                                          (uint32_t)(bucket > p->index_factor - 1)});
+                    }
+                }
+            }
+            ++end;
+        }
+    }
+    return true;
+}
+
+std::atomic<bool> g_ptm_fatal{false};  // a protein the reference's cutSeq throws on
+
 // DBIndexer.cutSeq(String,String) (:237-405), with the SQLiteMult store behind it.
 // Appends every INCLUDE'd occurrence (incl. bucket-dropped ones, flagged) in
 // insertion order.
 void cut_seq(const dbi_params* p, const uint8_t* seq, int length, uint32_t proteinId,
              std::vector<Occ>& out) {
+    if (length > 0 && std::memchr(seq, '[', (size_t)length)) {
+        if (!cut_seq_literal(p, std::string((const char*)seq, (size_t)length), proteinId, out)) g_ptm_fatal = true;
+        return;
+    }
     Enzyme enz{p};
     const int maxIntCleavage = p->max_missed;
     const int bucketRange = MAX_PRECURSOR_INT / p->index_factor;  // SQLiteMult:56
@@ -411,6 +538,7 @@ void digest_all(const dbi_params* p, const uint8_t* res, const uint64_t* off, ui
         pb[t] = (uint64_t)(std::lower_bound(off, off + n_prot + 1, off[n_prot] / nt * t) - off);
     for (int t = 1; t <= nt; ++t) pb[t] = std::max(pb[t], pb[t - 1]);
     std::vector<std::vector<Occ>> part(nt);
+    g_ptm_fatal = false;
     parallel_for(nt, [&](int t) {
         for (uint64_t i = pb[t]; i < pb[t + 1]; ++i)
             cut_seq(p, res + off[i], (int)(off[i + 1] - off[i]), (uint32_t)i, part[t]);
@@ -440,6 +568,7 @@ int oref_digest(const dbi_params* p, const uint8_t* res, const uint64_t* off, ui
                 uint8_t* dropped, uint64_t cap, uint64_t* n) {
     std::vector<Occ> occ;
     digest_all(p, res, off, n_prot, occ);
+    if (g_ptm_fatal) return DBI_E_INVALID;
     *n = occ.size();
     if (!mass) return 0;
     if (cap < occ.size()) return DBI_E_INVALID;
@@ -459,6 +588,7 @@ int oref_count(const dbi_params* p, const uint8_t* res, const uint64_t* off, uin
                uint64_t* total, uint64_t* dropped) {
     const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_threads, n_prot));
     std::vector<uint64_t> tot(nt, 0), drop(nt, 0);
+    g_ptm_fatal = false;
     parallel_for(nt, [&](int t) {
         std::vector<Occ> occ;
         for (uint64_t i = n_prot * t / nt; i < n_prot * (t + 1) / nt; ++i) {
@@ -468,6 +598,7 @@ int oref_count(const dbi_params* p, const uint8_t* res, const uint64_t* off, uin
             for (const Occ& o : occ) drop[t] += o.dropped;
         }
     });
+    if (g_ptm_fatal) return DBI_E_INVALID;
     *total = *dropped = 0;
     for (int t = 0; t < nt; ++t) {
         *total += tot[t];
@@ -486,6 +617,10 @@ int oref_build(const dbi_params* p, const uint8_t* res, const uint64_t* off, uin
     ix->residues.assign(res, res + off[n_prot]);
     std::vector<Occ> occ;
     digest_all(p, ix->residues.data(), off, n_prot, occ);
+    if (g_ptm_fatal) {
+        delete ix;
+        return DBI_E_INVALID;
+    }
     ix->n_total = occ.size();
     for (const Occ& o : occ) ix->n_dropped += o.dropped;
     build_store(ix, occ);

@@ -96,8 +96,10 @@ def digest(cparams, residues: np.ndarray, offsets: np.ndarray) -> Digest:
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     n = ctypes.c_uint64()
     P = offsets.shape[0] - 1
-    L.oref_digest(ctypes.byref(cparams), _ptr(residues), _ptr(offsets), P,
-                  None, None, None, None, None, 0, ctypes.byref(n))
+    rc = L.oref_digest(ctypes.byref(cparams), _ptr(residues), _ptr(offsets), P,
+                       None, None, None, None, None, 0, ctypes.byref(n))
+    if rc != 0:  # a protein the reference's cutSeq throws on (inline PTM at its start, '[' without ']')
+        raise ValueError(f"oref_digest failed: {rc}")
     k = n.value
     out = Digest(np.zeros(k, np.float64), np.zeros(k, np.uint32), np.zeros(k, np.uint32),
                  np.zeros(k, np.uint32), np.zeros(k, np.uint8))
@@ -114,8 +116,10 @@ def count(cparams, residues: np.ndarray, offsets: np.ndarray):
     residues = np.ascontiguousarray(residues, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     t, d = ctypes.c_uint64(), ctypes.c_uint64()
-    lib().oref_count(ctypes.byref(cparams), _ptr(residues), _ptr(offsets), offsets.shape[0] - 1,
-                     ctypes.byref(t), ctypes.byref(d))
+    rc = lib().oref_count(ctypes.byref(cparams), _ptr(residues), _ptr(offsets), offsets.shape[0] - 1,
+                          ctypes.byref(t), ctypes.byref(d))
+    if rc != 0:
+        raise ValueError(f"oref_count failed: {rc}")
     return t.value, d.value
 
 

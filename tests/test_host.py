@@ -137,8 +137,6 @@ def test_indexer_host_checks():
         ix.init()
     with pytest.raises(DBIndexerException, match="Uniprot"):
         ix.run([("no accession here", "PEPTIDEK")])
-    with pytest.raises(DBIndexerException, match="formula"):
-        ix.cutSeq("sp|P1|X", "PEP[C2H2]TIDEK")
 
 
 # ------------------------------------------------------------- FASTA
