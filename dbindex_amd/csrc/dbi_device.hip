@@ -984,12 +984,22 @@ __device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const Diges
     const uint16_t* const wmin = wp + (dp.min_len - 1);          // pepSize >= MIN_PEP_LENGTH (:331)
     uint32_t len = 1;
     uint32_t cur = *wp;
+#ifndef DBI_X_NOPREFETCH
+    double cmass = sm.mass[cur & 0xFFu];
+#endif
     bool ovf;
     for (;;) {
         const uint32_t nxt = wp[1];
         const uint32_t c = cur & 0xFFu;
         const uint32_t fl = cur >> 8;
+#ifndef DBI_X_NOPREFETCH
+        // the next residue's mass is read one step ahead: the LDS round trip
+        // leaves the sequential fp64 chain
+        const double nmass = sm.mass[nxt & 0xFFu];
+        m = m + cmass;                                           // :306-308
+#else
         m = m + sm.mass[c];                                      // :306-308
+#endif
         mc += (int)(fl & F_CLEAVE);                              // :314-316
         hsh = fnv32_step(hsh, c);
         const bool last = (fl & F_LAST) != 0;
@@ -1016,6 +1026,9 @@ __device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const Diges
         ++wp;
         ++len;
         cur = nxt;
+#ifndef DBI_X_NOPREFETCH
+        cmass = nmass;
+#endif
     }
     r.kept = kept;
     r.dropped = dropped;

@@ -164,3 +164,37 @@ def test_engine_ptm_reference_exceptions(seq):
     with Engine(DBIndexSearchParams.trypsin(1).to_c()) as eng:
         with pytest.raises(_native.DBIndexStoreException, match="StringIndexOutOfBounds"):
             eng.build(fasta.PackedProteins(res, off))
+
+
+@pytest.mark.gpu
+def test_store_ptm_text_from_the_cache_strings():
+    """DBIndexer.run over proteins with formulas: the records come from the
+    stripped walks, the text and flanks from the ProteinCache's strings (with
+    their formulas) at those offsets, as IndexMerge.java:452-461 reads them."""
+    from dbindex_amd import _native
+    from dbindex_amd.indexer import DBIndexer
+    from oracle import pyref
+    from tests.helpers import query_masses
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    prm = DBIndexSearchParams.trypsin(2)
+    seqs = ptm_proteome(60)
+    items = [(fasta.uniprot_header(i), s) for i, s in enumerate(seqs)]
+    res, off = _pack(seqs)
+    oix = cref.Index(prm.to_c(), res, off)
+    ix = DBIndexer(prm)
+    ix.init()
+    ix.run(items)
+    st = ix.indexStore
+    assert st.getTotalSeqCount() == oix.n_total and st.getNumberSequences() == oix.n_keys
+    u = oix.unique()
+    m, t = query_masses(oix, 80, seed=9)
+    for mi, ti in zip(m, t):
+        got = st.getSequences(float(mi), float(ti))
+        ids = oix.query(float(mi), float(ti))
+        assert len(got) == len(ids)
+        for g, i in zip(got, ids):
+            p0, o, ln = int(u["prot_id"][i]), int(u["offset"][i]), int(u["length"][i])
+            assert g.getMass() == float(u["mass"][i]) and g.getProteinIds()[0] == p0
+            assert g.getSequence() == seqs[p0][o:o + ln]
+            assert (g.getResLeft(), g.getResRight()) == pyref.get_residues(o, ln, seqs[p0])
