@@ -2123,17 +2123,26 @@ __device__ bool ck_run_wave(unsigned long long* k0, unsigned long long* k1, uint
 }
 
 // compare-exchange with partner i ^ m across waves, through LDS scratch sc[0, L)
+// Element x sits at sig(x): its R-aligned group keeps its place and the low
+// bits are xored with bits 5.. of x, so a wave's R stores / loads of one
+// register hit 32 distinct 8-B bank pairs (plain lane*R + r strides put R
+// lanes on one pair); the group that reaches past L stays unpermuted.
+template <int R>
+__device__ __forceinline__ uint32_t ck_sig(uint32_t x, uint32_t L) {
+    return (x | (uint32_t)(R - 1)) < L ? x ^ ((x >> 5) & (uint32_t)(R - 1)) : x;
+}
+
 template <int R>
 __device__ __forceinline__ void ck_lds_step(unsigned long long* sc, uint64_t (&key)[R], uint32_t i0, uint32_t m,
                                             uint32_t L) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
-        if (i0 + r < L) sc[i0 + r] = key[r];
+        if (i0 + r < L) sc[ck_sig<R>(i0 + r, L)] = key[r];
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t i = i0 + r, p = i ^ m;
-        const uint64_t b = p < L ? sc[p] : ~0ull;
+        const uint64_t b = p < L ? sc[ck_sig<R>(p, L)] : ~0ull;
         key[r] = ck_pick(key[r], b, i < p);
     }
     __syncthreads();
