@@ -3563,6 +3563,8 @@ __global__ void __launch_bounds__(SPLIT_THREADS)
 k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__ ctr) {
     __shared__ uint32_t cnt[256];
     __shared__ uint32_t cur[256];
+    __shared__ uint32_t wcnt[SPLIT_THREADS / 64][256];  // per-wave digit counts of one scatter tile
+    for (uint32_t x = threadIdx.x; x < (SPLIT_THREADS / 64) * 256; x += SPLIT_THREADS) (&wcnt[0][0])[x] = 0;
     __shared__ unsigned long long s_lo0[SPLIT_THREADS / 64], s_hi0[SPLIT_THREADS / 64];
     __shared__ uint32_t s_lo1[SPLIT_THREADS / 64], s_hi1[SPLIT_THREADS / 64];
     __shared__ uint32_t s_shift, s_same;
@@ -3657,12 +3659,36 @@ k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__
             flush();
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < n; i += SPLIT_THREADS) {
-            const Rec r = from[lo + i];
-            const uint32_t d = (uint32_t)(key72(r) >> sh) & 0xFFu;
-            to[lo + atomicAdd(&cur[d], 1u)] = r;
+        // stable scatter, one block-wide tile at a time (per-wave ballot ranks,
+        // waves in order): the leaves keep the arrival order -- first
+        // appearance -- so the compact-key sort applies to them
+        for (uint32_t t0 = 0; t0 < n; t0 += SPLIT_THREADS) {
+            const uint32_t i = t0 + threadIdx.x;
+            const bool valid = i < n;
+            Rec r{0, 0};
+            uint32_t d = 0;
+            if (valid) {
+                r = from[lo + i];
+                d = (uint32_t)(key72(r) >> sh) & 0xFFu;
+            }
+            const uint64_t peers = digit_peers(d, valid, 8);
+            const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+            if (valid && rank == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
+            __syncthreads();
+            uint32_t at = cur[d] + rank;
+            for (uint32_t q = 0; q < w; ++q) at += wcnt[q][d];
+            __syncthreads();
+            if (valid) to[lo + at] = r;
+            if (threadIdx.x < 256) {
+                uint32_t add = 0;
+                for (uint32_t q = 0; q < SPLIT_THREADS / 64; ++q) {
+                    add += wcnt[q][threadIdx.x];
+                    wcnt[q][threadIdx.x] = 0;
+                }
+                cur[threadIdx.x] += add;
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 
