@@ -1464,6 +1464,8 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
         const uint32_t i = base + k * 64 + lane;
         rv[k] = i < n ? in4[i] : make_uint4(0, 0, 0, 0);
     }
+    // this block's global digit offsets, in flight with the records (one per thread)
+    const uint32_t goff = threadIdx.x < D ? offs[(size_t)threadIdx.x * gridDim.x + blockIdx.x] : 0u;
     // rank of every record among the wave's earlier records of its digit
     uint32_t dg[RADIX_ITEMS], pos[RADIX_ITEMS];
     uint32_t vmask = 0;
@@ -1502,7 +1504,7 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
             cnt[ww][d] = (uint16_t)acc;
             acc += t;
         }
-        gofs[d] = offs[(size_t)d * gridDim.x + blockIdx.x] - lstart;
+        gofs[d] = goff - lstart;
     }
     __syncthreads();
     // exchange through LDS, then write digit runs with consecutive lanes on
