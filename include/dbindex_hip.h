@@ -110,6 +110,10 @@ void dbi_close(dbi_handle* h);
  * sequences concatenated in FASTA order, prot_off[0..n_prot] = start offsets
  * (prot_off[0]=0, prot_off[n_prot]=n_res).  Protein id = 0-based position
  * (DBIndexer.java:251,418 + DBIndexStoreSQLiteMult.addProteinDef:446-450).
+ * Proteins may carry inline '[formula]' PTMs, digested as DBIndexer.cutSeq
+ * does (:288-303; offsets of the stripped protein, identity and text from the
+ * protein as given); a formula before a protein's first residue or a '['
+ * without ']' is DBI_E_INVALID (the reference throws out of cutSeq).
  * Host pointers; copied to HBM.  Replaces any previous index of the handle. */
 int dbi_build(dbi_handle* h, const uint8_t* residues, uint64_t n_res,
               const uint64_t* prot_off, uint64_t n_prot);
