@@ -49,6 +49,8 @@ public class DBIndexStoreHip implements DBIndexStore {
 
     protected long h;  // dbi_store*
     private ProteinCache proteinCache;
+    private int unindexedMode;     // dbi_store_set_unindexed mode (0: indexed store)
+    private boolean cacheLoaded;   // unindexed: cache proteins handed to the device
 
     public DBIndexStoreHip(DBIndexSearchParams p, int device) throws DBIndexStoreException {
         final char[] mand = p.getMandatoryInternalAAs();
@@ -141,6 +143,36 @@ public class DBIndexStoreHip implements DBIndexStore {
     @Override
     public void setProteinCache(ProteinCache protCache) {                      // :152
         proteinCache = protCache;
+        if (unindexedMode != 0 && protCache != null && !cacheLoaded) {
+            // SEARCH_UNINDEXED: DBIndexer.setProteinCache (:461-500) fills the cache
+            // from the FASTA; its proteins go to the device once, where the
+            // reference re-cuts them on every cutAndSearch (:707-747)
+            try {
+                startAddSeq0(h);
+                for (int i = 0; i < protCache.getNumberProteins(); i++) {
+                    addProteinDef0(h, i, protCache.getDef(i), protCache.getProteinSequence(i));
+                }
+                stopAddSeq0(h);
+            } catch (final DBIndexStoreException e) {
+                throw new RuntimeException(e);
+            }
+            cacheLoaded = true;
+        }
+    }
+
+    /**
+     * DBIndexer.cutAndSearch (DBIndexer.java:707-747) on the unindexed store: the
+     * MassRangeFilteringIndex init + cutSeq of every cached protein + getSequences
+     * in one device pass.  Errors propagate (the reference logs them and returns null).
+     */
+    public List<IndexedSequence> cutAndSearch(List<MassRange> ranges) throws DBIndexStoreException {
+        final double[] m = new double[ranges.size()];
+        final double[] t = new double[ranges.size()];
+        for (int i = 0; i < m.length; i++) {
+            m[i] = ranges.get(i).getPrecMass();
+            t[i] = ranges.get(i).getTolerance();
+        }
+        return toList(cutAndSearch0(h, m, t));
     }
 
     @Override
@@ -210,6 +242,7 @@ public class DBIndexStoreHip implements DBIndexStore {
     /** SEARCH_UNINDEXED store (dbi_store_set_unindexed: 1 resident, 2 stream), before init. */
     public void setUnindexed(int mode) throws DBIndexStoreException {
         setUnindexed0(h, mode);
+        unindexedMode = mode;
     }
 
     /** Total occurrences indexed (DBIndexStoreSQLiteMult.totalSeqCount, :277). */

@@ -98,3 +98,9 @@ def test_java_side_overrides_the_reference_interface():
     assert "implements DBIndexStore" in store
     idx = open(os.path.join(JAVA, "DBIndexerHip.java")).read()
     assert "extends DBIndexer" in idx and re.search(r"protected void cutSeq\(", idx)
+    # SEARCH_UNINDEXED queries bypass the private cutAndSearch (DBIndexer.java:707-747)
+    for meth in ("getSequencesUsingDaltonTolerance", "getSequencesUsingPPMTolerance", "getSequences"):
+        assert re.search(r"@Override\s+public List<IndexedSequence> " + meth + r"\(", idx), meth
+    assert re.search(r"public List<IndexedSequence> cutAndSearch\(List<MassRange>", store)
+    impl = open(os.path.join(JAVA, "DBIndexImplHip.java")).read()
+    assert "extends DBIndexImpl" in impl and "new DBIndexerHip(" in impl
