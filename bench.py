@@ -390,6 +390,7 @@ def main() -> None:
         cpu["sample_parity"] = sample_parity(prm, sample, cpu.pop("_oix"), dev)
 
     traffic, traffic_src = pmc_traffic(dom["kernel"]) if dom else (None, None)
+    copy_gbps = hbm_copy_gbps(dev) if rank == 0 else None
     if rank == 0:
         out = {
             "metric": BASELINE_METRIC,
@@ -429,6 +430,9 @@ def main() -> None:
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": dom["alg_bytes"],
                 "avg_launch_ms": dom["avg_ms"],
+                # STREAM-like copy on this GPU: the reachable ceiling
+                "measured_copy_gbps": copy_gbps,
+                "frac_of_measured_copy": dom["gbps"] / copy_gbps if copy_gbps else None,
             },
             # the chunk sort runs as three kernels (chunk_sort, chunk_sort_mid for
             # chunks with a bin above the one-wave sort, chunk_sort_big above
@@ -539,6 +543,15 @@ def hits_leg(eng, dm, dt, nq: int, reps: int = 5) -> dict:
                 roofline=dict(bound="hbm", alg_bytes=alg, formula="32Q + 12H + 8Ho",
                               achieved=alg / t / 1e9, peak=HBM_PEAK_GBPS, unit="GB/s",
                               frac=alg / t / 1e9 / HBM_PEAK_GBPS))
+
+
+def hbm_copy_gbps(dev: int, nbytes: int = 1 << 31, reps: int = 10):
+    """Measured device-copy bandwidth (read + write bytes / s, dbi_hbm_copy_bandwidth), GB/s."""
+    import ctypes
+    from dbindex_amd._native import lib as _lib
+    v = ctypes.c_double(0.0)
+    rc = _lib().dbi_hbm_copy_bandwidth(dev, nbytes, reps, ctypes.byref(v))
+    return v.value if rc == 0 else None
 
 
 def run_trembl(args, world: int, rank: int, dev: int, dist) -> None:

@@ -163,6 +163,7 @@ SIGNATURES = [
     ("dbi_dev_copy_h2d", c_int, [c_int, P, P, c_uint64]),
     ("dbi_dev_copy_d2h", c_int, [c_int, P, P, c_uint64]),
     ("dbi_dev_copy_d2d", c_int, [c_int, P, P, c_uint64]),
+    ("dbi_hbm_copy_bandwidth", c_int, [c_int, c_uint64, c_int, POINTER(c_double)]),
     ("dbi_dev_synchronize", c_int, [c_int]),
     ("dbi_last_error", c_char_p, []),
     ("dbi_abi_version", c_int, []),

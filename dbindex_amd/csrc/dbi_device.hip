@@ -119,6 +119,30 @@ __device__ __forceinline__ uint64_t u4_q0(const uint4& r) { return ((uint64_t)r.
 __device__ __forceinline__ uint64_t u4_q1(const uint4& r) { return ((uint64_t)r.w << 32) | r.z; }
 __device__ __forceinline__ double u4_mass(const uint4& r) { return q0_mass(u4_q0(r)); }
 
+// 16-B loads / stores with the streaming (nontemporal) cache policy.  Only the
+// copy probe uses them: on the record kernels they were no gain (chunk sort,
+// finalize) or a loss (radix scatter stores 1.65 vs 1.49 ms: its digit runs
+// rely on the L2 to merge partial lines)
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint4* p) {
+    if constexpr (NT) {
+        const v4u_t v = __builtin_nontemporal_load(reinterpret_cast<const v4u_t*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void st16(uint4* p, const uint4& r) {
+    if constexpr (NT) {
+        const v4u_t v = {r.x, r.y, r.z, r.w};
+        __builtin_nontemporal_store(v, reinterpret_cast<v4u_t*>(p));
+    } else {
+        *p = r;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // 1/3. digest: DBIndexer.cutSeq (:237-405) + SQLiteMult.filterSequence/addSequence
 // ---------------------------------------------------------------------------
@@ -2903,6 +2927,34 @@ __global__ void k_write_tail(uint32_t* __restrict__ occ_off, uint32_t n_kept, co
 
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s) {
     DBI_LAUNCH(k_write_tail, dim3(1), dim3(64), 0, s, d_occ_off, n_kept, d_ctr);
+    return hipGetLastError();
+}
+
+// STREAM-like copy (dbi_hbm_copy_bandwidth): the measured HBM ceiling printed
+// next to the 8 TB/s peak.  One-shot grid, four 16-B streaming loads in flight
+// per thread (tools/copy_probe.hip: 6.4 TB/s; a grid-stride loop 4.8, default
+// cache policy 5.9, eight per thread 4.4).
+constexpr uint32_t COPY_ITEMS = 4;
+__global__ void __launch_bounds__(256) k_hbm_copy(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n) {
+    const uint64_t base = (uint64_t)blockIdx.x * 256u * COPY_ITEMS + threadIdx.x;
+    uint4 v[COPY_ITEMS];
+#pragma unroll
+    for (uint32_t k = 0; k < COPY_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * 256u;
+        if (i < n) v[k] = ld16<true>(in + i);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < COPY_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * 256u;
+        if (i < n) st16<true>(out + i, v[k]);
+    }
+}
+
+hipError_t launch_hbm_copy(const void* d_in, void* d_out, uint64_t n16, hipStream_t s) {
+    const uint64_t blocks = (n16 + 256u * COPY_ITEMS - 1) / (256u * COPY_ITEMS);
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    DBI_LAUNCH(k_hbm_copy, dim3((uint32_t)blocks), dim3(256), 0, s, reinterpret_cast<const uint4*>(d_in),
+               reinterpret_cast<uint4*>(d_out), n16);
     return hipGetLastError();
 }
 

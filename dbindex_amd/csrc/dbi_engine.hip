@@ -661,6 +661,36 @@ int dbi_dev_synchronize(int device) {
     DBI_HIP(hipDeviceSynchronize());
     return 0;
 }
+
+int dbi_hbm_copy_bandwidth(int device, uint64_t bytes, int reps, double* gbps) {
+    if (!gbps || reps <= 0 || bytes < 16) return set_error(DBI_E_INVALID, "dbi_hbm_copy_bandwidth: bad argument");
+    DBI_HIP(hipSetDevice(device));
+    const uint64_t n16 = bytes / 16;
+    void *a = nullptr, *b = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipMalloc(&a, 16 * n16);
+    if (e == hipSuccess) e = hipMalloc(&b, 16 * n16);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipMemsetAsync(a, 1, 16 * n16, s);
+    if (e == hipSuccess) e = launch_hbm_copy(a, b, n16, s);  // warm
+    if (e == hipSuccess) e = hipEventRecord(e0, s);
+    for (int r = 0; r < reps && e == hipSuccess; ++r) e = launch_hbm_copy(r & 1 ? b : a, r & 1 ? a : b, n16, s);
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess) *gbps = ms > 0.f ? 2.0 * 16.0 * (double)n16 * reps / (ms * 1e-3) / 1e9 : 0.0;
+    if (e1) (void)hipEventDestroy(e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (s) (void)hipStreamDestroy(s);
+    if (b) (void)hipFree(b);
+    if (a) (void)hipFree(a);
+    DBI_HIP(e);
+    return 0;
+}
 int dbi_abi_version(void) { return DBI_ABI_VERSION; }
 
 int dbi_device_count(int* out) {

@@ -319,6 +319,7 @@ hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32
 hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t factor, uint32_t* d_flags,
                             hipStream_t s);
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s);
+hipError_t launch_hbm_copy(const void* d_in, void* d_out, uint64_t n16, hipStream_t s);
 hipError_t launch_gather(const uint64_t* d_ids, uint64_t n, const double* d_umass, const uint32_t* d_upid,
                          const uint32_t* d_uoff, const uint32_t* d_ulen, const uint32_t* d_occ_off,
                          double* o_mass, uint32_t* o_pid, uint32_t* o_off, uint32_t* o_len, uint64_t* o_b,

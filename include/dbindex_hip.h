@@ -524,6 +524,10 @@ int dbi_dev_copy_h2d(int device, void* dst, const void* src, uint64_t bytes);
 int dbi_dev_copy_d2h(int device, void* dst, const void* src, uint64_t bytes);
 int dbi_dev_copy_d2d(int device, void* dst, const void* src, uint64_t bytes);
 int dbi_dev_synchronize(int device);
+/* STREAM-like device copy of `bytes` (read + write counted: 2 x bytes per
+   pass), `reps` timed passes on a stream of its own: the measured HBM ceiling
+   the bench prints next to the 8 TB/s peak. */
+int dbi_hbm_copy_bandwidth(int device, uint64_t bytes, int reps, double* gbps);
 
 /* ------------------------------------------------------------------------ */
 /* Misc                                                                     */
