@@ -119,6 +119,16 @@ __device__ __forceinline__ uint64_t u4_q0(const uint4& r) { return ((uint64_t)r.
 __device__ __forceinline__ uint64_t u4_q1(const uint4& r) { return ((uint64_t)r.w << 32) | r.z; }
 __device__ __forceinline__ double u4_mass(const uint4& r) { return q0_mass(u4_q0(r)); }
 
+// p[min(i, n-1)], n >= 1: loads every lane issues, so a batch of them goes out
+// together.  "i < n ? p[i] : x" makes the compiler branch around each load and
+// wait for it before the next one (one memory round trip per element).
+__device__ uint4 g_zero16;  // load target of lanes with nothing to load (stays zero)
+
+template <typename T>
+__device__ __forceinline__ T ld_clamped(const T* __restrict__ p, uint32_t i, uint32_t n) {
+    return p[i < n ? i : n - 1u];
+}
+
 // 16-B loads / stores with the streaming (nontemporal) cache policy.  Only the
 // copy probe uses them: on the record kernels they were no gain (chunk sort,
 // finalize) or a loss (radix scatter stores 1.65 vs 1.49 ms: its digit runs
@@ -408,13 +418,13 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
 #pragma unroll
     for (uint32_t k = 0; k < NV; ++k) {
         const uint32_t i = tid + k * DIGEST_THREADS;
-        rv[k] = i < nvec ? vbase[i] : make_uint4(0, 0, 0, 0);
+        rv[k] = *(i < nvec ? vbase + i : &g_zero16);  // a select, not a branch: the loads go out together
     }
     // ragged ends: thread t < 16 the head byte t, 16 <= t < 32 the tail byte t-16
     uint32_t edge = 0;
     const uint32_t epos = tid < 16 ? tid : tail0 + (tid - 16);
     const bool has_edge = tid < 16 ? tid < hb : (tid < 32 && epos < nbytes);
-    if (has_edge) edge = d_res[w0 + epos];
+    edge = *(has_edge ? d_res + w0 + epos : reinterpret_cast<const uint8_t*>(&g_zero16));
     tc.pf = d_tile_pf[tile];
     tc.pl = d_tile_pf[ntiles + 1 + tile];  // proteins overlapping [t0, w_end]: [pf, pl]
     sm.mass[tid] = d_mass_tab[tid];
@@ -1408,7 +1418,7 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
-        qv[k] = i < n ? in[i].q0 : REC_SENTINEL;
+        qv[k] = ld_clamped(in, i, n).q0;  // records past n: not valid below
     }
     // counts only (no ranks): one LDS atomic per record into the wave's own row
 #pragma unroll
@@ -1486,7 +1496,7 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
         const uint32_t i = base + k * 64 + lane;
-        rv[k] = i < n ? in4[i] : make_uint4(0, 0, 0, 0);
+        rv[k] = ld_clamped(in4, i, n);  // records past n: not valid below
     }
     // this block's global digit offsets, in flight with the records (one per thread)
     const uint32_t goff = threadIdx.x < D ? offs[(size_t)threadIdx.x * gridDim.x + blockIdx.x] : 0u;
