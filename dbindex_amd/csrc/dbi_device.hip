@@ -1383,6 +1383,21 @@ struct PairDigit {  // query routing pairs: q0 = owner shard, q1 = query index
     __device__ __forceinline__ void xform(uint4&) const {}
 };
 
+// The record chunk of this block.  Workgroups go to the 8 XCDs round-robin
+// (block b on XCD b % 8), so each XCD takes one contiguous run of chunks: the
+// digit runs that consecutive chunks write next to each other (their (digit,
+// chunk) offsets are adjacent) meet in one L2, which merges the partial lines,
+// and the 32 chunks sharing a 128-B line of a histogram row are one XCD's.
+// SwissProt scatter 1.49 -> 1.24 ms per build (semi-tryptic 29.0 -> 27.3).
+__device__ __forceinline__ uint32_t xcd_contiguous_block() {
+    const uint32_t G = gridDim.x, b = blockIdx.x, x = b & 7u, q = G >> 3, r = G & 7u;
+    return x * q + min(x, r) + (b >> 3);
+}
+// (Not for the chunk sort or finalize: mass-adjacent chunks cost alike, and
+// one XCD per contiguous run of them loses the balance: 0.87 -> 1.10 ms and
+// 0.44 -> 0.47 ms.)
+__device__ __forceinline__ uint32_t radix_chunk() { return xcd_contiguous_block(); }
+
 // Digit of record r for this pass, and the wave's peers holding the same digit.
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits) {
     uint64_t peers = __ballot(valid);
@@ -1405,7 +1420,8 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
     wave_sync();
-    const uint32_t base = blockIdx.x * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
+    const uint32_t cb = radix_chunk();
+    const uint32_t base = cb * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
     uint64_t qv[RADIX_ITEMS];
 #pragma unroll
     for (int k = 0; k < RADIX_ITEMS; ++k) {
@@ -1424,7 +1440,7 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
         uint32_t t = 0;
 #pragma unroll
         for (int ww = 0; ww < RADIX_NW; ++ww) t += cnt[ww][d];
-        hist[(size_t)d * gridDim.x + blockIdx.x] = t;
+        hist[(size_t)d * gridDim.x + cb] = t;
     }
 }
 
@@ -1439,7 +1455,8 @@ k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t*
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
     wave_sync();
     static_assert(RADIX_ITEMS == 8, "one 8-B load per thread");
-    const uint32_t i0 = blockIdx.x * RADIX_CHUNK + threadIdx.x * RADIX_ITEMS;
+    const uint32_t cb = radix_chunk();
+    const uint32_t i0 = cb * RADIX_CHUNK + threadIdx.x * RADIX_ITEMS;
     uint2 v = make_uint2(0u, 0u);
     uint32_t nv = 0;  // digits of this thread below n
     if (i0 + RADIX_ITEMS <= n) {
@@ -1461,7 +1478,7 @@ k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t*
         uint32_t t = 0;
 #pragma unroll
         for (int ww = 0; ww < RADIX_NW; ++ww) t += cnt[ww][d];
-        hist[(size_t)d * gridDim.x + blockIdx.x] = t;
+        hist[(size_t)d * gridDim.x + cb] = t;
     }
 }
 
@@ -1482,7 +1499,8 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
     wave_sync();
-    const uint32_t base = blockIdx.x * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
+    const uint32_t cb = radix_chunk();
+    const uint32_t base = cb * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
     const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
     uint4 rv[RADIX_ITEMS];
 #pragma unroll
@@ -1494,7 +1512,7 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
         rv[k] = i < n ? in4[i] : make_uint4(0, 0, 0, 0);
     }
     // this block's global digit offsets, in flight with the records (one per thread)
-    const uint32_t goff = threadIdx.x < D ? offs[(size_t)threadIdx.x * gridDim.x + blockIdx.x] : 0u;
+    const uint32_t goff = threadIdx.x < D ? offs[(size_t)threadIdx.x * gridDim.x + cb] : 0u;
     // rank of every record among the wave's earlier records of its digit
     uint32_t dg[RADIX_ITEMS], pos[RADIX_ITEMS];
     uint32_t vmask = 0;
