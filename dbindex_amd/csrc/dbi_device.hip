@@ -3294,11 +3294,6 @@ hipError_t launch_hits_offsets(const uint64_t* d_first, const uint64_t* d_count,
 // list start relative to the query's, and the protein ids themselves — all
 // three contiguous runs, written with consecutive lanes on consecutive words.
 constexpr uint32_t HITS_THREADS = 256;
-#ifndef DBI_HITS_U
-#define DBI_HITS_U 4
-#endif
-constexpr uint32_t HITS_U = DBI_HITS_U;
-__device__ uint32_t g_hits_dummy[64 * HITS_THREADS];  // store sink for lanes past a run's end
 __global__ void __launch_bounds__(HITS_THREADS)
 k_hits_expand(const uint64_t* __restrict__ first, const uint64_t* __restrict__ count,
               const uint64_t* __restrict__ row, const uint64_t* __restrict__ occ_row,
@@ -3310,35 +3305,11 @@ k_hits_expand(const uint64_t* __restrict__ first, const uint64_t* __restrict__ c
         const uint32_t f = (uint32_t)first[q];
         const uint64_t r = row[q], orow = occ_row[q];
         const uint32_t o0 = occ_off[f], o1 = occ_off[f + c];
-        // HITS_U loads in flight per thread, then every store: straight-line
-        // code (loads clamped into the run, stores past it sent to a dummy
-        // slot), so no branch makes the compiler drain the memory counter
-        // between them (per-element bounds checks: 3-5 % slower)
-        uint32_t* const dummy = g_hits_dummy + (blockIdx.x & 63u) * HITS_THREADS + threadIdx.x;
-        for (uint32_t k0 = threadIdx.x; k0 < c; k0 += HITS_THREADS * HITS_U) {
-            uint32_t v[HITS_U];
-#pragma unroll
-            for (uint32_t u = 0; u < HITS_U; ++u)
-                v[u] = occ_off[f + min(k0 + u * HITS_THREADS, (uint32_t)c - 1u)];
-#pragma unroll
-            for (uint32_t u = 0; u < HITS_U; ++u) {
-                const uint32_t k = k0 + u * HITS_THREADS;
-                const bool in = k < c;
-                *(in ? ids + r + k : dummy) = f + k;
-                *(in ? hit_occ + r + k : dummy) = v[u] - o0;
-            }
+        for (uint32_t k = threadIdx.x; k < c; k += HITS_THREADS) {
+            ids[r + k] = f + k;
+            hit_occ[r + k] = occ_off[f + k] - o0;
         }
-        const uint32_t no = o1 - o0;
-        for (uint32_t k0 = threadIdx.x; k0 < no; k0 += HITS_THREADS * HITS_U) {
-            uint32_t v[HITS_U];
-#pragma unroll
-            for (uint32_t u = 0; u < HITS_U; ++u) v[u] = occ_pid[o0 + min(k0 + u * HITS_THREADS, no - 1u)];
-#pragma unroll
-            for (uint32_t u = 0; u < HITS_U; ++u) {
-                const uint32_t k = k0 + u * HITS_THREADS;
-                *(k < no ? prot + orow + k : dummy) = v[u];
-            }
-        }
+        for (uint32_t k = threadIdx.x; k < o1 - o0; k += HITS_THREADS) prot[orow + k] = occ_pid[o0 + k];
     }
 }
 
