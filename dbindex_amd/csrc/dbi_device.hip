@@ -18,7 +18,9 @@
 //      k_digest<COUNT|EMIT> + scan — cold builds (no capacity known yet).
 //   2. LSD radix passes over the fine mass bin (k_radix_hist[_u8] + scan +
 //      k_radix_scatter): 3 passes of <= 8 bits at SwissProt scale; each pass
-//      but the last writes the next pass's digit bytes for the next histogram.
+//      but the last writes the next pass's digit bytes for the next histogram;
+//      record chunks are XCD-contiguous (radix_chunk) so neighbouring digit
+//      runs meet in one L2.
 //   3. k_chunk_bounds     — chunks of whole bins, ~CHUNK_T records each.
 //   4. k_chunk_sort (<= CHUNK_CAP records, LDS, bins up to 512 records),
 //      k_chunk_sort_list (chunks with a bigger bin; chunks up to BIG_CAP),
@@ -30,6 +32,7 @@
 //      CSR (protein ids, insertion order) + distinct mass-key count.
 // Queries: k_qdir_* (query directory), k_query (range per window),
 // k_hits_* (materialised hits), k_query_pairs / k_qroute_* (sharded index).
+// k_hbm_copy: the measured copy ceiling the bench prints beside the peak.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
