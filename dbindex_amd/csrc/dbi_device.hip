@@ -165,9 +165,23 @@ struct DigestSmem {
     alignas(16) uint16_t win[WIN + 8];  // staged window: residue | flags << 8 (F_CLEAVE F_NOCUT F_MAND F_CUT F_LAST);
                                 // slack: walk_bounded reads one entry ahead without a clamp
     uint8_t flags[256];
-    uint16_t cand[DIGEST_TILE]; // compacted candidate starts (tile-local), in order
+    alignas(8) uint16_t cand[DIGEST_TILE]; // compacted candidate starts (tile-local), in order
     uint32_t tmp[DIGEST_THREADS / 64 + 1];
 };
+// digest_prepare's scratch bit maps live in sm.cand until the compaction
+// writes it (no LDS beyond the block's 22.8 KiB: 7 blocks per CU)
+constexpr int WIN_WORDS = WIN / 64 + 2;
+static_assert(2 * WIN_WORDS * 8 <= DIGEST_TILE * 2, "nocut / last maps inside sm.cand");
+__device__ __forceinline__ uint64_t* nocut_map(DigestSmem& sm) { return reinterpret_cast<uint64_t*>(sm.cand); }
+__device__ __forceinline__ uint64_t* last_map(DigestSmem& sm) { return reinterpret_cast<uint64_t*>(sm.cand) + WIN_WORDS; }
+
+// OR a 16-bit slice (bit b = window position p + b) into a bit map
+__device__ __forceinline__ void or_slice16(uint64_t* m, uint32_t p, uint32_t v) {
+    if (!v) return;
+    const uint32_t w = p >> 6, sh = p & 63u;
+    atomicOr(&m[w], (unsigned long long)v << sh);
+    if (sh > 48) atomicOr(&m[w + 1], (unsigned long long)v >> (64 - sh));
+}
 
 // largest p in [lo, hi) with poff[p] <= x   (poff ascending)
 __device__ __forceinline__ uint32_t find_le(const uint32_t* poff, uint32_t lo, uint32_t hi, uint32_t x) {
@@ -424,23 +438,35 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
     tc.pl = d_tile_pf[ntiles + 1 + tile];  // proteins overlapping [t0, w_end]: [pf, pl]
     sm.mass[tid] = d_mass_tab[tid];
     sm.flags[tid] = d_flags[tid];
-    if (tid < WIN / 64 + 2) sm.stm[tid] = 0;
-    static_assert(WIN / 64 + 2 <= DIGEST_THREADS, "one thread per protein-start word");
+    if (tid < WIN_WORDS) {
+        sm.stm[tid] = 0;
+        sm.clvm[tid] = 0;
+        nocut_map(sm)[tid] = 0;
+    }
+    static_assert(WIN_WORDS <= DIGEST_THREADS, "one thread per bit-map word");
     const uint32_t np_all = tc.pl - tc.pf + 2;
     __syncthreads();
     // residue window -> LDS as (residue | flags << 8): a vector's 16 entries
-    // leave as two 16-B LDS stores when the window is 8-entry aligned
+    // leave as two 16-B LDS stores when the window is 8-entry aligned; its
+    // cleave and no-cut flags as 16-bit slices of the two bit maps
 #pragma unroll
     for (uint32_t k = 0; k < NV; ++k) {
         const uint32_t i = tid + k * DIGEST_THREADS;
         if (i < nvec) {
             const uint32_t wv[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
             uint32_t e[16];
+            uint32_t clv16 = 0, noc16 = 0;
 #pragma unroll
             for (int b = 0; b < 16; ++b) {
                 const uint32_t c = (wv[b >> 2] >> (8 * (b & 3))) & 0xFFu;
-                e[b] = c | ((uint32_t)sm.flags[c] << 8);
+                const uint32_t f = sm.flags[c];
+                e[b] = c | (f << 8);
+                clv16 |= (f & F_CLEAVE) << b;
+                noc16 |= ((f >> 1) & 1u) << b;
             }
+            static_assert(F_CLEAVE == 1 && F_NOCUT == 2, "flag bits");
+            or_slice16(sm.clvm, hb + i * 16, clv16);
+            or_slice16(nocut_map(sm), hb + i * 16, noc16);
             if ((hb & 7u) == 0) {
                 uint4* dst = reinterpret_cast<uint4*>(&sm.win[hb + i * 16]);
                 dst[0] = make_uint4(e[0] | e[1] << 16, e[2] | e[3] << 16, e[4] | e[5] << 16, e[6] | e[7] << 16);
@@ -451,7 +477,12 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
             }
         }
     }
-    if (has_edge) sm.win[epos] = (uint16_t)(edge | ((uint32_t)sm.flags[edge] << 8));
+    if (has_edge) {
+        const uint32_t f = sm.flags[edge];
+        sm.win[epos] = (uint16_t)(edge | (f << 8));
+        or_slice16(sm.clvm, epos, f & F_CLEAVE);
+        or_slice16(nocut_map(sm), epos, (f >> 1) & 1u);
+    }
     tc.npst = np_all <= PST_CAP ? np_all : 0u;
     for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
         const uint32_t o = d_poff[tc.pf + i];
@@ -461,46 +492,51 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
     __syncthreads();
     // cleavage-cut and protein-end flags of every window position, and the
     // N_ok bit map (a protein start, or a cut just before: the candidate
-    // starts of a full enzyme).  At the window's last position (w_end < R) the
-    // next residue is unknown; a walk that reaches it without a protein end
+    // starts of a full enzyme), 64 positions per thread from the bit maps:
+    //   last     = a protein starts at p+1          (stm >> 1)
+    //   cut      = last || (cleave(p) && !nocut(p+1))
+    //   cut_prev = cleave(p-1) && !nocut(p)          (its protein-end case is a start)
+    //   N_ok     = start(p) || cut_prev
+    // At the window's last position (w_end < R) the next residue is unknown
+    // (no no-cut bit): a walk that reaches it without a protein end
     // overflows to walk_global first.
+    if (tid < WIN_WORDS) {
+        const uint32_t w = tid;
+        const uint64_t valid = nbytes >= 64 * w + 64 ? ~0ull
+                             : nbytes <= 64 * w  ? 0ull : ((1ull << (nbytes - 64 * w)) - 1);
+        const uint64_t* noc = nocut_map(sm);
+        const uint64_t st = sm.stm[w];
+        const uint64_t st_n = w + 1 < (uint32_t)WIN_WORDS ? sm.stm[w + 1] : 0ull;
+        const uint64_t cl = sm.clvm[w];
+        const uint64_t cl_p = w > 0 ? sm.clvm[w - 1] : 0ull;
+        const uint64_t nc = noc[w];
+        const uint64_t nc_n = w + 1 < (uint32_t)WIN_WORDS ? noc[w + 1] : 0ull;
+        const uint64_t last = ((st >> 1) | (st_n << 63)) & valid;
+        const uint64_t cut = (last | (cl & ~((nc >> 1) | (nc_n << 63)))) & valid;
+        const uint64_t cut_prev = ((cl << 1) | (cl_p >> 63)) & ~nc;
+        sm.cutm[w] = cut;
+        sm.nokm[w] = (st | cut_prev) & valid;
+        last_map(sm)[w] = last;
+    }
+    __syncthreads();
+    // F_CUT / F_LAST into the window entries, 16 aligned entries per step
     {
-        constexpr uint32_t K = (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS;
-        static_assert(DIGEST_THREADS % 64 == 0, "ballot words");
-        uint32_t cf[K];
+        static_assert(F_CUT == 8 && F_LAST == 16, "cut / last bits 11, 12 of an entry");
+        const uint16_t* cut16 = reinterpret_cast<const uint16_t*>(sm.cutm);
+        const uint16_t* last16 = reinterpret_cast<const uint16_t*>(last_map(sm));
+        for (uint32_t j = tid; j * 16 < nbytes; j += DIGEST_THREADS) {
+            const uint32_t cu = cut16[j], la = last16[j];
+            if ((cu | la) == 0) continue;
+            uint4* src = reinterpret_cast<uint4*>(&sm.win[j * 16]);
+            uint4 v[2] = {src[0], src[1]};
+            uint32_t* d = reinterpret_cast<uint32_t*>(v);
 #pragma unroll
-        for (uint32_t k = 0; k < K; ++k) {
-            const uint32_t i = tid + k * DIGEST_THREADS;
-            cf[k] = 0;
-            bool nok = false, clv = false, first = false;
-            if (i < nbytes) {
-                const uint32_t e = sm.win[i];
-                const uint32_t en = sm.win[i + 1];
-                const uint32_t ep = i > 0 ? (uint32_t)sm.win[i - 1] : 0u;
-                first = bit_at(sm.stm, i);
-                clv = ((e >> 8) & F_CLEAVE) != 0;
-                const bool last = bit_at(sm.stm, i + 1);
-                const bool nocut_next = i + 1 < nbytes && ((en >> 8) & F_NOCUT);
-                const bool cut = last || (((e >> 8) & F_CLEAVE) && !nocut_next);
-                cf[k] = (cut ? F_CUT : 0u) | (last ? F_LAST : 0u);
-                // cut at i-1 (its protein-end case is `first`)
-                const bool cut_prev = i > 0 && ((ep >> 8) & F_CLEAVE) && !((e >> 8) & F_NOCUT);
-                nok = first || cut_prev;
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t c2 = (cu >> (2 * q)) & 3u, l2 = (la >> (2 * q)) & 3u;
+                d[q] |= ((c2 & 1u) << 11) | ((l2 & 1u) << 12) | ((c2 >> 1) << 27) | ((l2 >> 1) << 28);
             }
-            const uint64_t m = __ballot(nok);
-            const uint64_t mc = __ballot((cf[k] & F_CUT) != 0);
-            const uint64_t ml = __ballot(clv);
-            if (lane_id() == 0 && i < nbytes) {  // lane 0: the word's first position
-                sm.nokm[i / 64] = m;
-                sm.cutm[i / 64] = mc;
-                sm.clvm[i / 64] = ml;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t k = 0; k < K; ++k) {
-            const uint32_t i = tid + k * DIGEST_THREADS;
-            if (i < nbytes) sm.win[i] |= (uint16_t)(cf[k] << 8);
+            src[0] = v[0];
+            src[1] = v[1];
         }
     }
     __syncthreads();
@@ -998,7 +1034,10 @@ __device__ void balance_candidates(DigestSmem& sm, uint32_t ncand, uint32_t B, u
 // max_missed + 2 records (its slots are reserved: no bound check), the bucket
 // drop is compiled in only when it can happen (DROP), and the window is read
 // through a running LDS pointer one entry ahead (the array has slack, and an
-// entry past the window is never used: that step overflows).
+// entry past the window is never used: that step overflows).  The per-step
+// tests are short-circuit conditions over one 2-bit cut field: the compiler
+// keeps them as lane masks in SGPRs and the length in an SGPR (18 VALU per
+// residue step, from 26 with branch-free `|` of the same tests).
 template <bool DROP>
 __device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const DigestSmem& sm, uint32_t i0,
                                                 uint32_t nbytes, uint64_t loc, Rec* __restrict__ out) {
@@ -1010,54 +1049,51 @@ __device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const Diges
     uint32_t kept = 0, dropped = 0;
     const uint16_t* wp = &sm.win[i0];
     const uint16_t* const wlast = &sm.win[nbytes - 1];          // last staged entry
-    const uint16_t* const wmin = wp + (dp.min_len - 1);          // pepSize >= MIN_PEP_LENGTH (:331)
-    uint32_t len = 1;
+    const uint32_t min_len = (uint32_t)dp.min_len;              // pepSize >= MIN_PEP_LENGTH (:331)
+    uint32_t len = 1;  // wave-uniform (every walk starts at 1 and steps with the wave): an SGPR
     uint32_t cur = *wp;
-#ifndef DBI_X_NOPREFETCH
     double cmass = sm.mass[cur & 0xFFu];
-#endif
     bool ovf;
     for (;;) {
         const uint32_t nxt = wp[1];
         const uint32_t c = cur & 0xFFu;
-        const uint32_t fl = cur >> 8;
-#ifndef DBI_X_NOPREFETCH
         // the next residue's mass is read one step ahead: the LDS round trip
         // leaves the sequential fp64 chain
         const double nmass = sm.mass[nxt & 0xFFu];
         m = m + cmass;                                           // :306-308
-#else
-        m = m + sm.mass[c];                                      // :306-308
-#endif
-        mc += (int)(fl & F_CLEAVE);                              // :314-316
+        mc += (int)((cur >> 8) & F_CLEAVE);                      // :314-316
         hsh = fnv32_step(hsh, c);
-        const bool last = (fl & F_LAST) != 0;
-        ovf = !last & (wp >= wlast);
-        const bool cut = (fl & F_CUT) != 0;                      // checkCleavage (:318)
+        // F_CUT (8) and F_LAST (16) are adjacent bits and F_LAST implies F_CUT:
+        // one field, 0 = no cut, 1 = cut, 3 = protein end
+        static_assert(F_CUT == 8 && F_LAST == 16, "cut / last field");
+        const uint32_t cl = (cur >> 11) & 3u;
+        const bool last = cl > 1u;
+        const bool cut = cl != 0u;                               // checkCleavage (:318)
         const bool over = m > dp.max_mh;
-        const bool brk = cut & ((mc > dp.max_missed) | over);   // :322-329
-        const bool emit = cut & !brk & !ovf & (wp >= wmin) & (m >= dp.min_mh);  // :331
-        bool keep = emit;
-        if (DROP) {
-            const bool drop = emit & (m >= dp.drop_mass);        // bucket > NUM_BUCKETS-1 (:282-288)
-            keep = emit & !drop;
-            dropped += drop;
+        ovf = !last && wp >= wlast;  // F_CUT of the window's last entry is unknown: redo from HBM
+        const bool mcb = mc > dp.max_missed;
+        // emit: a cut that does not break (:322-329), pepSize and minMH (:331)
+        if (cut && !mcb && !over && !ovf && len >= min_len && m >= dp.min_mh) {
+            bool keep = true;
+            if (DROP) {
+                const bool drop = m >= dp.drop_mass;             // bucket > NUM_BUCKETS-1 (:282-288)
+                keep = !drop;
+                dropped += drop;
+            }
+            if (keep) {
+                const uint32_t tag = fold_tag(hsh);
+                Rec rec;
+                rec.q0 = rec_q0(m, tag);
+                rec.q1 = rec_q1(tag, loc, len);
+                out[kept] = rec;
+                ++kept;
+            }
         }
-        if (keep) {
-            const uint32_t tag = fold_tag(hsh);
-            Rec rec;
-            rec.q0 = rec_q0(m, tag);
-            rec.q1 = rec_q1(tag, loc, len);
-            out[kept] = rec;
-        }
-        kept += keep;
-        if (brk | last | over | ovf) break;                      // breaks + while condition (:284)
+        if (over || ovf || last || (cut && mcb)) break;         // breaks + while condition (:284)
         ++wp;
         ++len;
         cur = nxt;
-#ifndef DBI_X_NOPREFETCH
         cmass = nmass;
-#endif
     }
     r.kept = kept;
     r.dropped = dropped;
