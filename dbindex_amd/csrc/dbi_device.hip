@@ -1038,17 +1038,40 @@ __device__ void balance_candidates(DigestSmem& sm, uint32_t ncand, uint32_t B, u
 // tests are short-circuit conditions over one 2-bit cut field: the compiler
 // keeps them as lane masks in SGPRs and the length in an SGPR (18 VALU per
 // residue step, from 26 with branch-free `|` of the same tests).
+// Offset of the k-th set bit (k >= 1) of the 128-bit map (lo, hi), 128 if
+// it has fewer than k.
+__device__ __forceinline__ uint32_t kth_bit_128(uint64_t lo, uint64_t hi, uint32_t k) {
+    const uint32_t nlo = (uint32_t)__popcll(lo);
+    uint64_t x = lo;
+    uint32_t base = 0;
+    if (nlo < k) {
+        k -= nlo;
+        x = hi;
+        base = 64;
+        if ((uint32_t)__popcll(hi) < k) return 128u;
+    }
+    for (uint32_t q = 1; q < k; ++q) x &= x - 1;  // drop the first k-1
+    return base + (uint32_t)__ffsll((long long)x) - 1;
+}
+
 template <bool DROP>
 __device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const DigestSmem& sm, uint32_t i0,
                                                 uint32_t nbytes, uint64_t loc, Rec* __restrict__ out) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;
     if (!(m <= dp.max_mh)) return r;
-    int mc = -1;
     uint32_t hsh = FNV32_OFFSET;
     uint32_t kept = 0, dropped = 0;
     const uint16_t* wp = &sm.win[i0];
-    const uint16_t* const wlast = &sm.win[nbytes - 1];          // last staged entry
+    // intMisCleavageCount (:280, :314-316) > maxMC  <=>  the walk has reached
+    // the (maxMC+2)-th cleave residue from the start: a pointer compare per
+    // step instead of a running count.  Found in the cleave bit map within
+    // 128 positions; a walk longer than that (no stop found) ends its LDS
+    // part there and is redone from HBM, which counts.
+    const uint32_t r_mc = kth_bit_128(bits_from(sm.clvm, i0), bits_from(sm.clvm, i0 + 64),
+                                      (uint32_t)dp.max_missed + 2u);
+    const uint16_t* const wmc = wp + r_mc;
+    const uint16_t* const wlast = &sm.win[min(nbytes - 1, i0 + 127)];  // last entry this walk reads
     const uint32_t min_len = (uint32_t)dp.min_len;              // pepSize >= MIN_PEP_LENGTH (:331)
     uint32_t len = 1;  // wave-uniform (every walk starts at 1 and steps with the wave): an SGPR
     uint32_t cur = *wp;
@@ -1061,7 +1084,6 @@ __device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const Diges
         // leaves the sequential fp64 chain
         const double nmass = sm.mass[nxt & 0xFFu];
         m = m + cmass;                                           // :306-308
-        mc += (int)((cur >> 8) & F_CLEAVE);                      // :314-316
         hsh = fnv32_step(hsh, c);
         // F_CUT (8) and F_LAST (16) are adjacent bits and F_LAST implies F_CUT:
         // one field, 0 = no cut, 1 = cut, 3 = protein end
@@ -1071,7 +1093,7 @@ __device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const Diges
         const bool cut = cl != 0u;                               // checkCleavage (:318)
         const bool over = m > dp.max_mh;
         ovf = !last && wp >= wlast;  // F_CUT of the window's last entry is unknown: redo from HBM
-        const bool mcb = mc > dp.max_missed;
+        const bool mcb = wp >= wmc;                              // :322-329
         // emit: a cut that does not break (:322-329), pepSize and minMH (:331)
         if (cut && !mcb && !over && !ovf && len >= min_len && m >= dp.min_mh) {
             bool keep = true;
