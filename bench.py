@@ -128,7 +128,12 @@ def main() -> None:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")
-    dev = local_rank
+    # one GPU per rank; with fewer visible GPUs than local ranks (a rehearsal of
+    # the N-rank driver on a small box) ranks share devices -- RCCL refuses
+    # that, so only --no-merge runs there
+    from dbindex_amd._native import device_count
+    ndev = device_count()
+    dev = local_rank % ndev if ndev else local_rank
     if args.config == "trembl":
         return run_trembl(args, world, rank, dev, dist)
 
