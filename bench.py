@@ -51,7 +51,7 @@ WORKLOADS = {
     "1k": ("1k-protein synthetic proteome (seed 1), trypsin, 0 missed cleavages (configs[0])", "1k",
            lambda: DBIndexSearchParams.trypsin(0), 1000),
     "swissprot": ("SwissProt-scale synthetic proteome (560,000 proteins, seed 3), trypsin, "
-                  "2 missed cleavages (configs[2], single GPU)", "swissprot",
+                  "2 missed cleavages (configs[2])", "swissprot",
                   lambda: DBIndexSearchParams.trypsin(2), 100000),
     "semi": ("SwissProt-scale synthetic proteome (560,000 proteins, seed 3), semi-tryptic, "
              "2 missed cleavages + 1M precursor-mass queries +-20 ppm (configs[3])", "swissprot",
@@ -118,16 +118,15 @@ def main() -> None:
     from dbindex_amd.engine import Engine
     from dbindex_amd.params import DBIndexSearchParams
 
-    dist = None
+    coord = None
     merge = (world > 1 and not args.no_merge) or args.merge
     if world > 1:
-        # gloo for coordination only (barrier, max time, sums, the RCCL id):
-        # the data path runs over RCCL inside the engine's library, and gloo
-        # keeps torch's own HIP runtime out of this process (dbindex_amd/_native.py)
-        import torch
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")
+        # host coordination (barrier, max time, sums, the RCCL id) over plain
+        # sockets (dbindex_amd/coord.py): no torch in this process, so the one
+        # HIP runtime and the one RCCL mapped are /opt/rocm's, the library's own
+        # (checked: _native.check_single_runtime); the data path runs over RCCL
+        from dbindex_amd.coord import Coordinator
+        coord = Coordinator(world, rank)
     # one GPU per rank; with fewer visible GPUs than local ranks (a rehearsal of
     # the N-rank driver on a small box) ranks share devices -- RCCL refuses
     # that, so only --no-merge runs there
@@ -135,7 +134,7 @@ def main() -> None:
     ndev = device_count()
     dev = local_rank % ndev if ndev else local_rank
     if args.config == "trembl":
-        return run_trembl(args, world, rank, dev, dist)
+        return run_trembl(args, world, rank, dev, coord)
 
     desc, proteome, make_params, cpu_sample = WORKLOADS[args.config]
     strong = merge and args.scaling == "strong"
@@ -153,10 +152,10 @@ def main() -> None:
         from dbindex_amd import shard
         import ctypes
         from dbindex_amd._native import lib as _lib
-        uid = [stdout_to_stderr(shard.ShardComm.unique_id) if rank == 0 else None]
+        uid = stdout_to_stderr(shard.ShardComm.unique_id) if rank == 0 else None
         if world > 1:
-            dist.broadcast_object_list(uid, src=0)
-        comm = stdout_to_stderr(lambda: shard.ShardComm(uid[0], world, rank, dev))
+            uid = bytes.fromhex(coord.broadcast(uid.hex() if uid else None))
+        comm = stdout_to_stderr(lambda: shard.ShardComm(uid, world, rank, dev))
         if strong:
             # every rank holds the whole proteome (the same FASTA); rank r
             # digests its residue-balanced protein range
@@ -166,14 +165,16 @@ def main() -> None:
             p_begin, p_end = shard.protein_ranges(pp.offsets, world)[rank]
         else:
             # global layout: every rank's residues and offsets, in rank order
-            sizes = [(pp.n_residues, pp.n_proteins, pp.offsets.astype(np.uint64))] * world
-            if world > 1:
-                dist.all_gather_object(sizes, sizes[0])
+            sizes = coord.allgather([pp.n_residues, pp.n_proteins]) if world > 1 else [[pp.n_residues, pp.n_proteins]]
             res_base = np.concatenate([[0], np.cumsum([x[0] for x in sizes])]).astype(np.uint64)
             prot_base = np.concatenate([[0], np.cumsum([x[1] for x in sizes])]).astype(np.int64)
             R_all, P_all = int(res_base[-1]), int(prot_base[-1])
-            off_all = np.concatenate([sizes[r][2][:-1] + res_base[r] for r in range(world)] +
-                                     [np.array([R_all], np.uint64)])
+            # every rank's protein offsets, rebased, all-gathered over RCCL
+            d_offs = DeviceBuffer(8 * P_all, dev)
+            mine_off = DeviceBuffer.from_numpy((pp.offsets[:-1].astype(np.uint64) + res_base[rank]), dev)
+            comm.allgatherv(mine_off.ptr, d_offs.ptr, [8 * int(x[1]) for x in sizes])
+            off_all = np.concatenate([d_offs.download(np.uint64, P_all), np.array([R_all], np.uint64)])
+            del d_offs, mine_off
             # input staging (untimed): every shard's residues into every GPU's HBM
             d_res = DeviceBuffer(R_all + 16, dev)
             mine = d_res.ptr + int(res_base[rank])
@@ -229,7 +230,7 @@ def main() -> None:
     eng.set_timing(True, only=dominant)
     stage_acc = {}
     if world > 1:
-        dist.barrier()
+        coord.barrier()
     synchronize(dev)
     t_start = time.perf_counter()
     n_total = 0
@@ -242,17 +243,14 @@ def main() -> None:
             shard_acc.append((st.digest_ms, st.partition_ms, st.exchange_ms, st.merge_ms))
     synchronize(dev)
     if world > 1:
-        dist.barrier()
+        coord.barrier()
     elapsed = time.perf_counter() - t_start
 
-    # whole-job: units of all ranks / max time over ranks
+    # whole-job: units of all ranks (each rank's digested occurrences; a
+    # strong-scaling step counts the proteome once) / max time over ranks
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        nt = torch.tensor([n_total], dtype=torch.float64)
-        dist.all_reduce(nt, op=dist.ReduceOp.SUM)
-        n_total_all = float(nt.item())
+        elapsed = coord.allreduce([elapsed], "max")[0]
+        n_total_all = coord.allreduce([n_total], "sum")[0]
     else:
         n_total_all = float(n_total)
     value = n_total_all / elapsed if elapsed > 0 else 0.0
@@ -303,16 +301,14 @@ def main() -> None:
         # north_star's all-gatherv: every owner's slice onto every rank, then
         # every rank answers its own 1M batch locally (no exchange per batch)
         if world > 1:
-            dist.barrier()
+            coord.barrier()
         synchronize(dev)
         t_rep = time.perf_counter()
         shard.replicate(eng, comm)
         synchronize(dev)
         t_rep = time.perf_counter() - t_rep
         if world > 1:
-            t = torch.tensor([t_rep], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            t_rep = float(t.item())
+            t_rep = coord.allreduce([t_rep], "max")[0]
         rst = eng.stats()
         ex = eng.export()["mass"]
         rng = np.random.Generator(np.random.PCG64(7 + rank))
@@ -331,19 +327,17 @@ def main() -> None:
         synchronize(dev)
         reps = 20
         if world > 1:
-            dist.barrier()
+            coord.barrier()
         tq = time.perf_counter()
         for _ in range(reps):
             eng.query_device(dm.ptr, dt.ptr, nq, df.ptr, dc.ptr)
         synchronize(dev)
         if world > 1:
-            dist.barrier()
+            coord.barrier()
         tq = time.perf_counter() - tq
         hits = int(dc.download(np.uint64, nq).sum())
         if world > 1:
-            t = torch.tensor([tq], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            tq = float(t.item())
+            tq = coord.allreduce([tq], "max")[0]
         qps = dict(value=world * nq * reps / tq, unit="queries/s", queries_per_rank=nq, tol_ppm=20.0,
                    avg_hits=hits / nq, kind="range lookup on each rank's replica of the whole index",
                    index=f"the merged index above, replicated onto all {world} ranks "
@@ -394,6 +388,8 @@ def main() -> None:
         cpu = cpu_baseline_legs(prm, sample)
         cpu["sample_parity"] = sample_parity(prm, sample, cpu.pop("_oix"), dev)
 
+    from dbindex_amd._native import runtime_info
+    runtime = runtime_info()  # raises if two HIP runtimes / RCCLs are mapped
     traffic, traffic_src = pmc_traffic(dom["kernel"]) if dom else (None, None)
     copy_gbps = hbm_copy_gbps(dev) if rank == 0 else None
     if rank == 0:
@@ -406,12 +402,18 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
+            # N>1 default: one proteome split over the ranks (total work fixed);
+            # --no-merge / --scaling weak: one proteome per rank
+            "scaling": "weak" if (args.no_merge or args.scaling == "weak") else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded proteome, SwissProt residue frequencies; SURVEY.md §8(d))",
             "config": {
-                "workload": desc,
+                "workload": desc + (
+                    ", single GPU" if world == 1 and not merge else
+                    f", {'one proteome split by residues over' if strong else 'one proteome per rank on'} {world} "
+                    f"GPU{'s' if world > 1 else ''}, " + ("one merged index (RCCL owner exchange)" if merge
+                                                          else "shard-local indexes")),
                 "proteins_per_gpu": my_prot,
                 "residues_per_gpu": my_res,
                 "proteins": pp.n_proteins * (world if merge and not strong else 1),
@@ -455,11 +457,13 @@ def main() -> None:
             "sharded_phases": phases,
             "queries": qps,
             "cpu_baseline": cpu,
+            # the HIP runtime and RCCL this process runs on (one of each: checked)
+            "runtime": runtime,
         }
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
-        dist.destroy_process_group()
+    if coord is not None:
+        coord.close()
 
 
 def chunk_family(kernels, n_total):
@@ -559,7 +563,7 @@ def hbm_copy_gbps(dev: int, nbytes: int = 1 << 31, reps: int = 10):
     return v.value if rc == 0 else None
 
 
-def run_trembl(args, world: int, rank: int, dev: int, dist) -> None:
+def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
     """BASELINE.json configs[4]: TrEMBL-scale synthetic proteome (50M proteins,
     ~1.8e10 residues), non-specific digestion 6-50, COUNT only: ~7e11 peptide
     occurrences (~12 TB of records) cannot be materialised, so a step digests
@@ -610,23 +614,19 @@ def run_trembl(args, world: int, rank: int, dev: int, dist) -> None:
     for _ in range(max(args.warmup, 1)):
         n_step = step()
     if world > 1:
-        dist.barrier()
+        coord.barrier()
     synchronize(dev)
     t = time.perf_counter()
     for _ in range(args.steps):
         n_step = step()
     synchronize(dev)
     if world > 1:
-        dist.barrier()
+        coord.barrier()
     elapsed = time.perf_counter() - t
     n_all = float(n_step * args.steps)
     if world > 1:
-        import torch
-        x = torch.tensor([elapsed, n_all, float(n_res_all)], dtype=torch.float64)
-        y = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(y, op=dist.ReduceOp.MAX)
-        dist.all_reduce(x)
-        elapsed, n_all, res_all = float(y.item()), float(x[1].item()), float(x[2].item())
+        elapsed = coord.allreduce([elapsed], "max")[0]
+        n_all, res_all = coord.allreduce([n_all, float(n_res_all)], "sum")
     else:
         res_all = float(n_res_all)
     cpu = None

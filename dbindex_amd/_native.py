@@ -75,6 +75,11 @@ class DbiDeviceHits(ctypes.Structure):
                 ("prot", c_void_p), ("nq", c_uint64), ("n_hits", c_uint64), ("n_prot_ids", c_uint64)]
 
 
+class DbiRuntimeInfo(ctypes.Structure):
+    _fields_ = [("hip_runtime_version", c_int), ("hip_driver_version", c_int), ("rccl_version", c_int),
+                ("libamdhip64", ctypes.c_char * 512), ("librccl", ctypes.c_char * 512)]
+
+
 class DbiSeqList(ctypes.Structure):
     _fields_ = [
         ("n", c_uint64), ("mass", POINTER(c_double)), ("seq_off", POINTER(c_uint64)),
@@ -128,6 +133,9 @@ SIGNATURES = [
     ("dbi_comm_init", c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
     ("dbi_comm_destroy", None, [P]),
     ("dbi_comm_allgatherv", c_int, [P, P, P, P, P]),
+    ("dbi_comm_allreduce_f64", c_int, [P, P, P, c_uint32, c_int]),
+    ("dbi_comm_allreduce_u64", c_int, [P, P, P, c_uint64, P]),
+    ("dbi_runtime_info_get", c_int, [POINTER(DbiRuntimeInfo)]),
     ("dbi_build_sharded", c_int, [P, P, P, c_uint64, P, c_uint64, c_uint64, c_uint64]),
     ("dbi_store_create", c_int, [POINTER(DbiParams), c_int, POINTER(c_void_p)]),
     ("dbi_store_close", None, [P]),
@@ -187,7 +195,51 @@ def lib():
             f.restype = res
             f.argtypes = args
         _lib = L
+        check_single_runtime()
     return _lib
+
+
+def mapped_runtimes() -> dict:
+    """Distinct files of the HIP runtime and of RCCL mapped into this process
+    (/proc/self/maps): {"libamdhip64": [...], "librccl": [...]}."""
+    found = {"libamdhip64": set(), "librccl": set()}
+    try:
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                parts = line.split(None, 5)
+                if len(parts) < 6:
+                    continue
+                path = parts[5].strip()
+                base = os.path.basename(path)
+                for key in found:
+                    if base.startswith(key + ".") or base.startswith(key + "-"):
+                        found[key].add(os.path.realpath(path))
+    except OSError:
+        pass
+    return {k: sorted(v) for k, v in found.items()}
+
+
+def check_single_runtime() -> dict:
+    """Raises when two HIP runtimes or two RCCLs are mapped into this process
+    (e.g. PyTorch's bundled copies next to /opt/rocm's): kernels, device
+    memory and communicators of one must never meet the other."""
+    m = mapped_runtimes()
+    for key, paths in m.items():
+        if len(paths) > 1:
+            raise ImportError(f"two {key} copies mapped into this process: {paths}; load dbindex_amd before "
+                              "anything that brings its own ROCm runtime (torch), or run without it")
+    return m
+
+
+def runtime_info() -> dict:
+    """The HIP runtime and RCCL the library is bound to (versions, providing files)."""
+    ri = DbiRuntimeInfo()
+    check(lib().dbi_runtime_info_get(ctypes.byref(ri)))
+    v = ri.rccl_version
+    return dict(hip_runtime_version=ri.hip_runtime_version, hip_driver_version=ri.hip_driver_version,
+                rccl_version=f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v else None,
+                libamdhip64=ri.libamdhip64.decode(errors="replace"), librccl=ri.librccl.decode(errors="replace"),
+                mapped=check_single_runtime())
 
 
 def last_error() -> str:

@@ -277,7 +277,11 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
     bool mand_excl = false;           // a mandatory residue in [s, e-1]
     const uint32_t e_min = s + (uint32_t)dp.min_len - 1;  // pepSize >= MIN_PEP_LENGTH (:331)
     const bool can_drop = dp.drop_mass <= dp.max_mh;     // uniform
-    uint32_t hsh = FNV32_OFFSET;      // peptide_tag of [s, e] (EMIT only)
+    uint32_t head = 0, tail = 0;      // peptide_tag of [s, e] (EMIT only)
+    if (EMIT) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) head |= (uint32_t)(sm.win[s - w0 + k] & 0xFFu) << (8 * k);  // slack: in bounds
+    }
     uint32_t kept = 0, dropped = 0;
     uint32_t e = s;
     uint32_t cur = sm.win[e - w0];
@@ -290,7 +294,7 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
         const uint32_t fl = cur >> 8;
         m = m + sm.mass[c];                                   // :306-308
         mc += (int)(fl & F_CLEAVE);                           // :314-316
-        if (EMIT) hsh = fnv32_step(hsh, c);
+        if (EMIT) tail = (tail << 8) | c;
         const bool last = (fl & F_LAST) != 0;
         ovf = !last & (e + 1 >= wlim);  // F_CUT of the window's last entry is unknown: redo from HBM
         const bool cut = SEMI ? (n_ok | ((fl & F_CUT) != 0)) : ((fl & F_CUT) != 0);  // checkCleavage (:318)
@@ -307,7 +311,7 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
         bool keep = emit & !drop;
         if (dp.filter && keep) keep = in_windows(dp, m);
         if (EMIT && keep) {
-            const uint32_t tag = fold_tag(hsh);
+            const uint32_t tag = peptide_tag(head, tail, e - s + 1);
             Rec rec;
             rec.q0 = rec_q0(m, tag);
             rec.q1 = rec_q1(tag, loc, e - s + 1);
@@ -330,7 +334,8 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
 // window, e.g. through zero-mass residues): flags from the residue tables,
 // the cut from the next residue and the protein end pe.
 template <bool EMIT, bool SEMI, bool MAND>
-__device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const uint8_t* __restrict__ g_res,
+__device__ WalkOut walk_global(const DevParams& dp, const double* __restrict__ s_mass,
+                               const uint8_t* __restrict__ s_flags, const uint8_t* __restrict__ g_res,
                                uint32_t s, uint32_t pe, bool n_ok, uint64_t loc, Rec* __restrict__ out,
                                const Rec* out_end) {
     WalkOut r{0u, 0u, false};
@@ -338,16 +343,18 @@ __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const 
     if (!(m <= dp.max_mh)) return r;
     int mc = -1;
     bool mand_excl = false;
-    uint32_t hsh = FNV32_OFFSET;
+    uint32_t head = 0, tail = 0;
+    if (EMIT)
+        for (uint32_t k = 0; k < 4 && s + k < pe; ++k) head |= (uint32_t)g_res[s + k] << (8 * k);
     uint32_t kept = 0, dropped = 0;
     for (uint32_t e = s; e < pe; ++e) {
         const uint32_t c = g_res[e];
-        const uint32_t fl = sm.flags[c];
-        m = m + sm.mass[c];
+        const uint32_t fl = s_flags[c];
+        m = m + s_mass[c];
         mc += (int)(fl & F_CLEAVE);
-        if (EMIT) hsh = fnv32_step(hsh, c);
+        if (EMIT) tail = (tail << 8) | c;
         const bool last = e + 1 == pe;
-        const bool c_ok = last || ((fl & F_CLEAVE) && !(sm.flags[g_res[e + 1]] & F_NOCUT));
+        const bool c_ok = last || ((fl & F_CLEAVE) && !(s_flags[g_res[e + 1]] & F_NOCUT));
         const bool cut = SEMI ? (n_ok || c_ok) : c_ok;
         const bool over = m > dp.max_mh;
         const bool brk = cut && (mc > dp.max_missed || over);
@@ -361,7 +368,7 @@ __device__ WalkOut walk_global(const DevParams& dp, const DigestSmem& sm, const 
         const bool drop = emit && m >= dp.drop_mass;
         const bool keep = emit && !drop && (!dp.filter || in_windows(dp, m));
         if (EMIT && keep) {
-            const uint32_t tag = fold_tag(hsh);
+            const uint32_t tag = peptide_tag(head, tail, e - s + 1);
             Rec rec;
             rec.q0 = rec_q0(m, tag);
             rec.q1 = rec_q1(tag, loc, e - s + 1);
@@ -396,6 +403,19 @@ __device__ __forceinline__ bool n_ok_at(const DigestSmem& sm, const TileCtx& tc,
 }
 
 __device__ uint4 g_zero16;  // load target of lanes with nothing to load (stays zero)
+#ifdef DBI_X_PHASE
+__device__ unsigned long long g_phase[32];  // experiment builds: phase clocks [kernel*8 + phase] (24..: digest)
+#define DBI_DPH(i)                                                               \
+    do {                                                                         \
+        const uint64_t t_ = wall_clock64();                                      \
+        if (threadIdx.x == 0) atomicAdd(&g_phase[24 + (i)], t_ - dph_t);         \
+        dph_t = t_;                                                              \
+    } while (0)
+#else
+#define DBI_DPH(i) \
+    do {           \
+    } while (0)
+#endif
 
 // Stage the tile's window (residues + class flags + cut / protein-end flags)
 // and the residue tables in LDS, and compact the candidate starts (every start
@@ -594,7 +614,7 @@ __device__ __forceinline__ WalkOut walk_candidate(const DevParams& dp, const Dig
     WalkOut w = walk_lds<EMIT, SEMI, MAND>(dp, sm, tc.w0, tc.w_end, s, n_ok, loc, o, o_end);
     if (w.overflow) {
         const uint32_t pe = d_poff[find_le(d_poff, tc.pf, tc.pl + 1, s) + 1];
-        w = walk_global<EMIT, SEMI, MAND>(dp, sm, d_res, s, pe, n_ok, loc, o, o_end);
+        w = walk_global<EMIT, SEMI, MAND>(dp, sm.mass, sm.flags, d_res, s, pe, n_ok, loc, o, o_end);
     }
     return w;
 }
@@ -876,14 +896,18 @@ __device__ __forceinline__ unsigned long long st_pack(uint32_t epoch, unsigned l
     return ((unsigned long long)epoch << 48) | (state << 46) | v;
 }
 
-// Wave 0 of tile `tile`: publish the tile's total, look back 64 tiles at a
-// time for the exclusive prefix (returned to every lane), publish the
-// inclusive prefix.
-__device__ unsigned long long tile_lookback(unsigned long long* __restrict__ status, uint32_t tile, uint32_t epoch,
-                                            unsigned long long total) {
-    if (threadIdx.x == 0)
-        __hip_atomic_store(&status[tile], st_pack(epoch, tile == 0 ? ST_PREFIX : ST_AGG, total), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+// Thread 0 of tile `tile`: publish the tile's total (the first tile its
+// inclusive prefix right away).
+__device__ __forceinline__ void tile_publish(unsigned long long* __restrict__ status, uint32_t tile, uint32_t epoch,
+                                             unsigned long long total) {
+    __hip_atomic_store(&status[tile], st_pack(epoch, tile == 0 ? ST_PREFIX : ST_AGG, total), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 of a tile that published its total: look back 64 tiles at a time
+// for the exclusive prefix (returned to every lane), publish the inclusive one.
+__device__ unsigned long long tile_lookback_wait(unsigned long long* __restrict__ status, uint32_t tile,
+                                                 uint32_t epoch, unsigned long long total) {
     unsigned long long excl = 0;
     int64_t t = (int64_t)tile - 1;
     const uint32_t lane = lane_id();
@@ -910,6 +934,13 @@ __device__ unsigned long long tile_lookback(unsigned long long* __restrict__ sta
         __hip_atomic_store(&status[tile], st_pack(epoch, ST_PREFIX, excl + total), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     return excl;
+}
+
+// Wave 0 of tile `tile`: publish the tile's total, then the look-back.
+__device__ unsigned long long tile_lookback(unsigned long long* __restrict__ status, uint32_t tile, uint32_t epoch,
+                                            unsigned long long total) {
+    if (threadIdx.x == 0) tile_publish(status, tile, epoch, total);
+    return tile_lookback_wait(status, tile, epoch, total);
 }
 
 template <bool SEMI, bool MAND>
@@ -980,16 +1011,15 @@ hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, co
 // the B-th next cleavage site, so cand[j+B] - cand[j] estimates its length; a
 // counting sort of the candidates by that estimate (in place, through
 // registers) gives each wave's lanes walks of about the same length, instead
-// of every wave waiting for its longest one.  Any order is valid: candidate j
-// (in the new order) fills slots [j*B, j*B + B).  Tiles of more than
-// BAL_MAX candidates keep their order.
+// of every wave waiting for its longest one.  Any order is valid: each
+// candidate's records go to the slots its thread reserved for it.  Tiles of
+// more than BAL_MAX candidates keep their order.  s_cnt: BAL_BUCKETS words.
 constexpr uint32_t BAL_ITEMS = 4;
 constexpr uint32_t BAL_MAX = BAL_ITEMS * DIGEST_THREADS;
 constexpr uint32_t BAL_BUCKETS = 128;
 
-__device__ void balance_candidates(DigestSmem& sm, uint32_t ncand, uint32_t B, uint32_t tile_len) {
+__device__ void balance_candidates(uint16_t* cand, uint32_t* s_cnt, uint32_t ncand, uint32_t B, uint32_t tile_len) {
     if (ncand > BAL_MAX || ncand < 2) return;  // block-uniform
-    __shared__ uint32_t s_cnt[BAL_BUCKETS];
     for (uint32_t b = threadIdx.x; b < BAL_BUCKETS; b += DIGEST_THREADS) s_cnt[b] = 0;
     __syncthreads();
     uint32_t cv[BAL_ITEMS], key[BAL_ITEMS], rk[BAL_ITEMS];
@@ -997,8 +1027,8 @@ __device__ void balance_candidates(DigestSmem& sm, uint32_t ncand, uint32_t B, u
     for (uint32_t k = 0; k < BAL_ITEMS; ++k) {
         const uint32_t j = threadIdx.x + k * DIGEST_THREADS;
         if (j < ncand) {
-            cv[k] = sm.cand[j];
-            const uint32_t nxt = j + B < ncand ? sm.cand[j + B] : tile_len + (uint32_t)DIGEST_HALO;
+            cv[k] = cand[j];
+            const uint32_t nxt = j + B < ncand ? cand[j + B] : tile_len + (uint32_t)DIGEST_HALO;
             key[k] = min(nxt - cv[k], BAL_BUCKETS - 1);
             rk[k] = atomicAdd(&s_cnt[key[k]], 1u);
         }
@@ -1023,21 +1053,11 @@ __device__ void balance_candidates(DigestSmem& sm, uint32_t ncand, uint32_t B, u
 #pragma unroll
     for (uint32_t k = 0; k < BAL_ITEMS; ++k) {
         const uint32_t j = threadIdx.x + k * DIGEST_THREADS;
-        if (j < ncand) sm.cand[s_cnt[key[k]] + rk[k]] = (uint16_t)cv[k];
+        if (j < ncand) cand[s_cnt[key[k]] + rk[k]] = (uint16_t)cv[k];
     }
     __syncthreads();
 }
 
-// The bounded digest's walk (full enzyme, no mandatory residues, <= 2 missed
-// cleavages): walk_lds<EMIT, !SEMI, !MAND> with what that mode makes
-// redundant taken out of the per-residue loop — a start emits at most
-// max_missed + 2 records (its slots are reserved: no bound check), the bucket
-// drop is compiled in only when it can happen (DROP), and the window is read
-// through a running LDS pointer one entry ahead (the array has slack, and an
-// entry past the window is never used: that step overflows).  The per-step
-// tests are short-circuit conditions over one 2-bit cut field: the compiler
-// keeps them as lane masks in SGPRs and the length in an SGPR (18 VALU per
-// residue step, from 26 with branch-free `|` of the same tests).
 // Offset of the k-th set bit (k >= 1) of the 128-bit map (lo, hi), 128 if
 // it has fewer than k.
 __device__ __forceinline__ uint32_t kth_bit_128(uint64_t lo, uint64_t hi, uint32_t k) {
@@ -1054,177 +1074,411 @@ __device__ __forceinline__ uint32_t kth_bit_128(uint64_t lo, uint64_t hi, uint32
     return base + (uint32_t)__ffsll((long long)x) - 1;
 }
 
-template <bool DROP>
-__device__ __forceinline__ WalkOut walk_bounded(const DevParams& dp, const DigestSmem& sm, uint32_t i0,
-                                                uint32_t nbytes, uint64_t loc, Rec* __restrict__ out) {
-    WalkOut r{0u, 0u, false};
-    double m = dp.m0;
-    if (!(m <= dp.max_mh)) return r;
-    uint32_t hsh = FNV32_OFFSET;
-    uint32_t kept = 0, dropped = 0;
-    const uint16_t* wp = &sm.win[i0];
-    // intMisCleavageCount (:280, :314-316) > maxMC  <=>  the walk has reached
-    // the (maxMC+2)-th cleave residue from the start: a pointer compare per
-    // step instead of a running count.  Found in the cleave bit map within
-    // 128 positions; a walk longer than that (no stop found) ends its LDS
-    // part there and is redone from HBM, which counts.
-    const uint32_t r_mc = kth_bit_128(bits_from(sm.clvm, i0), bits_from(sm.clvm, i0 + 64),
-                                      (uint32_t)dp.max_missed + 2u);
-    const uint16_t* const wmc = wp + r_mc;
-    const uint16_t* const wlast = &sm.win[min(nbytes - 1, i0 + 127)];  // last entry this walk reads
-    const uint32_t min_len = (uint32_t)dp.min_len;              // pepSize >= MIN_PEP_LENGTH (:331)
-    uint32_t len = 1;  // wave-uniform (every walk starts at 1 and steps with the wave): an SGPR
-    uint32_t cur = *wp;
-    double cmass = sm.mass[cur & 0xFFu];
-    bool ovf;
-    for (;;) {
-        const uint32_t nxt = wp[1];
-        const uint32_t c = cur & 0xFFu;
-        // the next residue's mass is read one step ahead: the LDS round trip
-        // leaves the sequential fp64 chain
-        const double nmass = sm.mass[nxt & 0xFFu];
-        m = m + cmass;                                           // :306-308
-        hsh = fnv32_step(hsh, c);
-        // F_CUT (8) and F_LAST (16) are adjacent bits and F_LAST implies F_CUT:
-        // one field, 0 = no cut, 1 = cut, 3 = protein end
-        static_assert(F_CUT == 8 && F_LAST == 16, "cut / last field");
-        const uint32_t cl = (cur >> 11) & 3u;
-        const bool last = cl > 1u;
-        const bool cut = cl != 0u;                               // checkCleavage (:318)
-        const bool over = m > dp.max_mh;
-        ovf = !last && wp >= wlast;  // F_CUT of the window's last entry is unknown: redo from HBM
-        const bool mcb = wp >= wmc;                              // :322-329
-        // emit: a cut that does not break (:322-329), pepSize and minMH (:331)
-        if (cut && !mcb && !over && !ovf && len >= min_len && m >= dp.min_mh) {
-            bool keep = true;
-            if (DROP) {
-                const bool drop = m >= dp.drop_mass;             // bucket > NUM_BUCKETS-1 (:282-288)
-                keep = !drop;
-                dropped += drop;
-            }
-            if (keep) {
-                const uint32_t tag = fold_tag(hsh);
-                Rec rec;
-                rec.q0 = rec_q0(m, tag);
-                rec.q1 = rec_q1(tag, loc, len);
-                out[kept] = rec;
-                ++kept;
-            }
-        }
-        if (over || ovf || last || (cut && mcb)) break;         // breaks + while condition (:284)
-        ++wp;
-        ++len;
-        cur = nxt;
-        cmass = nmass;
-    }
-    r.kept = kept;
-    r.dropped = dropped;
-    r.overflow = ovf;
-    return r;
+// first set bit of the 128-bit map (lo, hi), 128 if none
+__device__ __forceinline__ uint32_t first_bit_128(uint64_t lo, uint64_t hi) {
+    return lo ? (uint32_t)__ffsll((long long)lo) - 1u : hi ? 64u + (uint32_t)__ffsll((long long)hi) - 1u : 128u;
 }
 
-template <bool DROP>
-__device__ __forceinline__ WalkOut walk_candidate_bounded(const DevParams& dp, const DigestSmem& sm,
-                                                          const TileCtx& tc, const uint8_t* __restrict__ d_res,
-                                                          const uint32_t* __restrict__ d_poff, uint32_t j,
-                                                          Rec* __restrict__ o, const Rec* o_end) {
-    const uint32_t i = sm.cand[j];
-    const uint32_t s = tc.t0 + i;
-    uint32_t pstart;
-    const uint32_t p = tile_protein(sm, tc, d_poff, s, pstart);
-    const uint64_t loc = rec_loc(p, s - pstart, tc.w);
-    WalkOut w = walk_bounded<DROP>(dp, sm, s - tc.w0, tc.nbytes, loc, o);
-    if (w.overflow) {
-        const uint32_t pe = d_poff[find_le(d_poff, tc.pf, tc.pl + 1, s) + 1];
-        w = walk_global<true, false, false>(dp, sm, d_res, s, pe, true, loc, o, o_end);
+// bits [0, x) of a 64-bit word, x <= 64
+__device__ __forceinline__ uint64_t low_bits(uint32_t x) { return x >= 64 ? ~0ull : ((1ull << x) - 1ull); }
+
+// ---------------------------------------------------------------------------
+// Bounded digest (full enzyme, no mandatory residues, <= 2 missed cleavages;
+// warm builds): one walk per cleavage-site start, into slots reserved by a
+// decoupled look-back.  A full-enzyme walk emits only at cuts, and every
+// limit is monotone along it (the mass only grows, intMisCleavageCount only
+// grows), so the records of start s are the cuts e, in ascending order, with
+//   s + MIN_PEP_LENGTH - 1 <= e < stop  and  minMH <= m(e) <= maxMH,
+//   stop = the (maxMC+2)-th cleave residue from s (from there on every cut
+//          breaks, DBIndexer.java:322-324) or the first residue of the next
+//          protein (:284 end < length), whichever comes first
+// (the bucket drop, :282-288 of SQLiteMult, counts instead of keeping; the
+// filterSequence of a non-mandatory store is INCLUDE for every such mass).
+// The cut, cleave and protein-start bit maps of the staged window give those
+// candidate ends (<= maxMC + 2, within a 128-position horizon) before the walk
+// starts, so the residue loop is only the sequential fp64 sum (:306-308,
+// -ffp-contract=off) up to the last candidate end, with the mass at each end
+// parked in LDS; the records (mass filters, tag from the peptide's end bytes)
+// are written after the loop.  A start whose stop lies past the horizon (no
+// protein end and fewer than maxMC+2 cleave residues within 128 positions)
+// and whose mass is still <= maxMH there is redone from HBM (walk_global).
+// The window holds raw residue bytes (16-B LDS stores of the 16-B loads) at
+// LDS position q = global index - w0 + lb, lb = 16 + the misalignment of
+// d_res + w0, so every 16-B global vector lands on a 16-B LDS slot and the
+// cleave / no-cut bit maps are written as plain 16-bit slices.
+// ---------------------------------------------------------------------------
+constexpr int LD_PRE = 16;                          // residues staged before the tile (N_ok of its first start)
+constexpr int LD_HORIZON = 128;                     // positions a walk reads from LDS
+constexpr int LD_HALO = LD_HORIZON + 16;            // past the tile: the horizon + the residue after it
+constexpr int LD_WIN = 32 + LD_PRE + DIGEST_TILE + LD_HALO;  // + lb (16 + alignment pad)
+constexpr int LD_WORDS = LD_WIN / 64 + 2;
+constexpr int LD_ENDS = 4;                          // candidate ends of one start, at most (maxMC + 2)
+
+struct LeanSmem {
+    double mass[256];
+    uint64_t clvm[LD_WORDS];  // bit q: cleave residue at LDS position q
+    uint64_t cutm[LD_WORDS];  // bit q: checkCleavage's C side holds at q (protein ends included)
+    uint64_t stm[LD_WORDS];   // bit q: a protein starts at q (one past the window included)
+    uint32_t pst[PST_CAP];    // poff[pf .. pl+1] (protein of a start: binary search)
+    alignas(16) uint8_t win[LD_WIN + 16];
+    uint8_t flags[256];
+    alignas(8) uint16_t cand[DIGEST_TILE];  // candidate starts (tile-local), compacted, then balanced
+    // the masses at a walk's candidate ends, [end][thread]; before the walks:
+    // the no-cut and N_ok maps and the balance counts
+    double endm[LD_ENDS][DIGEST_THREADS];
+    uint32_t tmp[DIGEST_THREADS / 64 + 1];
+};
+static_assert((2 * LD_WORDS * 8 + 4 * BAL_BUCKETS) <= LD_ENDS * DIGEST_THREADS * 8, "scratch inside endm");
+static_assert(LD_ENDS * DIGEST_THREADS * 8 % 16 == 0, "endm layout");
+
+// Protein of start s: largest p in [pf, pl] with poff[p] <= s (LDS copy of
+// the tile's offsets, HBM when they did not fit), and its first residue.
+__device__ __forceinline__ uint32_t protein_of(const uint32_t* pst, uint32_t npst, uint32_t pf, uint32_t pl,
+                                               const uint32_t* __restrict__ d_poff, uint32_t s, uint32_t& pstart) {
+    if (npst) {
+        uint32_t lo = 0, hi = npst - 1;  // pst[hi] = poff[pl+1] > s
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pst[mid] <= s) lo = mid; else hi = mid;
+        }
+        pstart = pst[lo];
+        return pf + lo;
     }
+    const uint32_t p = find_le(d_poff, pf, pl + 1, s);
+    pstart = d_poff[p];
+    return p;
+}
+
+struct LeanEnds {
+    uint64_t lo, hi;   // candidate ends: bit r = LDS position p + r
+    uint32_t horizon;  // last position (relative) the walk may read from LDS
+    bool open;         // the walk may go on past the horizon (more ends there)
+};
+
+// known: last LDS position whose cut bit is known (the window's last one only
+// at the end of the residues)
+__device__ __forceinline__ LeanEnds lean_ends(const LeanSmem& sm, uint32_t p, uint32_t known, uint32_t kcl,
+                                              uint32_t min_len) {
+    const uint64_t cl0 = bits_from(sm.clvm, p), cl1 = bits_from(sm.clvm, p + 64);
+    const uint64_t st0 = bits_from(sm.stm, p) & ~1ull, st1 = bits_from(sm.stm, p + 64);
+    const uint32_t stop = min(kth_bit_128(cl0, cl1, kcl), first_bit_128(st0, st1));
+    LeanEnds e;
+    e.horizon = min((uint32_t)LD_HORIZON - 1u, known - p);
+    e.open = stop > e.horizon + 1u;
+    const uint32_t a = min_len > 0 ? min_len - 1u : 0u;  // pepSize >= MIN_PEP_LENGTH (:331)
+    const uint32_t b = min(stop, e.horizon + 1u);        // ends in [a, b)
+    e.lo = bits_from(sm.cutm, p) & low_bits(min(b, 64u)) & ~low_bits(min(a, 64u));
+    e.hi = bits_from(sm.cutm, p + 64) & low_bits(b > 64u ? b - 64u : 0u) & ~low_bits(a > 64u ? a - 64u : 0u);
+    return e;
+}
+
+// One start at LDS position p, in two halves: lean_masses runs the residue
+// loop and parks the mass at each candidate end in LDS; lean_emit writes the
+// records.  Between them the block may wait for its slot base (the first
+// walk of every thread overlaps the tile's look-back).
+struct LeanWalk {
+    uint32_t pk;     // candidate end positions, one byte each, ascending (0xFF: none)
+    uint32_t nreal;  // candidate ends (the horizon entry, if any, is not one)
+    uint32_t j;      // masses parked
+    bool overflow;   // the walk goes on past the horizon: redo it with walk_global
+};
+
+__device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, LeanSmem& sm, uint32_t p, const LeanEnds& en) {
+    LeanWalk w{~0u, 0u, 0u, false};
+    double m = dp.m0;
+    if (!(m <= dp.max_mh)) return w;  // while condition before the first residue (:284)
+    // a walk that may leave the horizon also parks the mass at the horizon
+    // (its last entry), which decides whether it is redone from HBM
+    uint32_t pk = ~0u, last = 0, nreal = 0;
+    {
+        uint64_t lo = en.lo, hi = en.hi;
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)LD_ENDS; ++k) {
+            const uint32_t b = first_bit_128(lo, hi);
+            if (b < 128u) {
+                pk = (pk & ~(0xFFu << (8 * k))) | (b << (8 * k));
+                last = b;
+                ++nreal;
+            }
+            if (lo) lo &= lo - 1; else hi &= hi - 1;
+        }
+    }
+    uint32_t nlist = nreal;
+    if (en.open) {  // nreal <= maxMC + 1 here: the horizon fits the list
+        if (nreal == 0 || last != en.horizon) {
+            pk = (pk & ~(0xFFu << (8 * nreal))) | (en.horizon << (8 * nreal));
+            ++nlist;
+        }
+        last = en.horizon;
+    }
+    w.pk = pk;
+    w.nreal = nreal;
+    if (nlist == 0) return w;  // no candidate end
+    // the residue loop, four positions per step: one dword pair of the window,
+    // four mass reads in flight, then the sequential fp64 adds (:306-308); the
+    // mass at each listed end goes to LDS.  Positions past `last` (at most 3)
+    // only add to a mass that is no longer used.
+    const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(sm.win);
+    double* __restrict__ em = &sm.endm[0][threadIdx.x];
+    uint32_t ne = pk & 0xFFu, rest = pk, j = 0;
+    for (uint32_t q = 0; q <= last; q += 4) {
+        const uint32_t a = p + q;
+        const uint32_t r4 = __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], a & 3u);
+        const double x0 = sm.mass[r4 & 0xFFu], x1 = sm.mass[(r4 >> 8) & 0xFFu];
+        const double x2 = sm.mass[(r4 >> 16) & 0xFFu], x3 = sm.mass[r4 >> 24];
+#define DBI_LEAN_STEP(K, X)                   \
+        m = m + X;                            \
+        if (q + K == ne) {                    \
+            em[j * DIGEST_THREADS] = m;       \
+            ++j;                              \
+            rest >>= 8;                       \
+            ne = rest & 0xFFu;                \
+        }
+        DBI_LEAN_STEP(0u, x0)
+        DBI_LEAN_STEP(1u, x1)
+        DBI_LEAN_STEP(2u, x2)
+        DBI_LEAN_STEP(3u, x3)
+#undef DBI_LEAN_STEP
+        if (m > dp.max_mh) break;  // no later end passes maxMH (:326-329, :284)
+    }
+    w.j = j;
+    // still <= maxMH at the horizon: the walk goes on past it
+    w.overflow = en.open && j == nlist && em[(nlist - 1) * DIGEST_THREADS] <= dp.max_mh;
     return w;
 }
 
-// Records a full-enzyme start at window position p can emit, at most: the
-// cuts at [p + min_len - 1, stop), stop = the kcl-th (max_missed + 2) cleave
-// residue at or after p (from there on every cut breaks, :322-329) or the next
-// protein start, whichever comes first; `cap` when neither lies within the 64
-// positions from p (or the window ends first: the walk may leave it).  Mass
-// filters only lower the real count.  Branch-free over 64-position slices.
-
-__device__ __forceinline__ uint32_t slot_bound(const DigestSmem& sm, uint32_t p, uint32_t nbytes, uint32_t kcl,
-                                               uint32_t min_len, uint32_t cap) {
-    uint64_t cl = bits_from(sm.clvm, p);               // bit r: cleave residue at p + r
-    const uint64_t st = bits_from(sm.stm, p) & ~1ull;  // protein starts after p
-    const uint64_t cu = bits_from(sm.cutm, p);
-    for (uint32_t q = 1; q < kcl; ++q) cl &= cl - 1;   // drop the first kcl-1 cleave residues
-    const uint32_t r_cl = cl ? (uint32_t)__ffsll((long long)cl) - 1 : 64u;
-    const uint32_t r_st = st ? (uint32_t)__ffsll((long long)st) - 1 : 64u;
-    const uint32_t r = min(r_cl, r_st);                // stop - p
-    if (r >= 64 || p + r >= nbytes) return cap;        // bits at or past nbytes are not this window's
-    const uint32_t a = min_len - 1;
-    if (a >= r) return 0;
-    const uint64_t keep = (~0ull << a) & ((1ull << r) - 1);  // r < 64
-    return min((uint32_t)__popcll(cu & keep), cap);
+// The records of a lean walk (not overflowed) into out[0, kept).
+template <bool DROP>
+__device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const LeanSmem& sm, uint32_t p, const LeanWalk& w,
+                                             uint64_t loc, Rec* __restrict__ out) {
+    WalkOut r{0u, 0u, false};
+    const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(sm.win);
+    const double* __restrict__ em = &sm.endm[0][threadIdx.x];
+    const uint32_t head = __builtin_amdgcn_alignbyte(w32[(p >> 2) + 1], w32[p >> 2], p & 3u);
+    uint32_t kept = 0, dropped = 0;
+    const uint32_t nk = min(w.j, w.nreal);
+    for (uint32_t k = 0; k < nk; ++k) {
+        const double mk = em[k * DIGEST_THREADS];
+        if (!(mk <= dp.max_mh)) break;
+        if (!(mk >= dp.min_mh)) continue;  // :331
+        if (DROP && mk >= dp.drop_mass) {  // bucket > NUM_BUCKETS-1
+            ++dropped;
+            continue;
+        }
+        const uint32_t e = (w.pk >> (8 * k)) & 0xFFu;
+        const uint32_t q = p + e - 3u;  // p >= 16
+        const uint32_t tail = __builtin_bswap32(__builtin_amdgcn_alignbyte(w32[(q >> 2) + 1], w32[q >> 2], q & 3u));
+        const uint32_t tag = peptide_tag(head, tail, e + 1u);
+        Rec rec;
+        rec.q0 = rec_q0(mk, tag);
+        rec.q1 = rec_q1(tag, loc, e + 1u);
+        out[kept++] = rec;
+    }
+    r.kept = kept;
+    r.dropped = dropped;
+    return r;
 }
 
-// One walk per start (see launch_digest_bounded): each thread's candidates
-// reserve their slot bounds (slot_bound), the tile's total by decoupled
-// look-back, then every walk emits into the thread's own slots and the rest
-// are sentinel-filled (~3 % of the slots at SwissProt scale; a flat
-// max_missed + 2 per start left 41 %).  (Bounds computed during the
-// compaction instead, so the look-back could start earlier: slower.)  (A persistent grid
-// taking tiles from the ticket measured slower: 2.25 vs 1.60 ms.)
 template <bool DROP>
 __global__ void __launch_bounds__(DIGEST_THREADS)
 k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                  const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
                  uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, unsigned long long* __restrict__ status,
                  uint32_t epoch, Rec* __restrict__ d_out, uint64_t cap, Counters* __restrict__ d_ctr) {
-    __shared__ DigestSmem sm;
+    __shared__ LeanSmem sm;
     __shared__ uint32_t s_tile, s_kept, s_waves;
     __shared__ unsigned long long s_base;
-    if (threadIdx.x == 0) {
+    const uint32_t tid = threadIdx.x;
+#ifdef DBI_X_PHASE
+    uint64_t dph_t = wall_clock64();
+#endif
+    if (tid == 0) {
         s_tile = atomicAdd(&d_ctr->tile_ticket, 1u);
         s_kept = 0;
         s_waves = 0;
     }
     __syncthreads();
-    const uint32_t tile = s_tile;
-    TileCtx tc;
-    const uint32_t ncand = digest_prepare<false>(sm, tc, tile, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot,
-                                                 n_res, d_tile_pf);
+    DBI_DPH(0);
+    const uint32_t tile = s_tile, ntiles = gridDim.x;
+    const uint32_t t0 = tile * (uint32_t)DIGEST_TILE;
+    const uint32_t t_end = min(t0 + (uint32_t)DIGEST_TILE, n_res);
+    const uint32_t w0 = t0 >= (uint32_t)LD_PRE ? t0 - (uint32_t)LD_PRE : 0u;
+    const uint32_t w_end = min(t0 + (uint32_t)(DIGEST_TILE + LD_HALO), n_res);
+    const uint32_t lb = 16u + (uint32_t)((reinterpret_cast<uintptr_t>(d_res) + w0) & 15u);  // LDS position of w0
+    const uint32_t lend = lb + (w_end - w0);
+    const uint32_t nvec = (lend + 15u) >> 4;
+    const uint8_t* __restrict__ gb = d_res + w0 - lb;  // LDS position q <- gb[q], q in [lb, lend)
+
+    // every independent global load first: the window's 16-B vectors (the
+    // ragged first / last one byte by byte), the tile's protein range, the tables
+    constexpr uint32_t NV = (LD_WIN / 16 + DIGEST_THREADS - 1) / DIGEST_THREADS;
+    uint4 rv[NV];
+#pragma unroll
+    for (uint32_t k = 0; k < NV; ++k) {
+        const uint32_t i = tid + k * DIGEST_THREADS;
+        const bool full = i < nvec && 16u * i >= lb && 16u * i + 16u <= lend;
+        rv[k] = *(full ? reinterpret_cast<const uint4*>(gb + 16u * i) : &g_zero16);
+    }
+    const uint32_t pf = d_tile_pf[tile], pl = d_tile_pf[ntiles + 1 + tile];
+    sm.mass[tid] = d_mass_tab[tid];
+    sm.flags[tid] = d_flags[tid];
+    static_assert(LD_WORDS <= DIGEST_THREADS, "one thread per bit-map word");
+    if (tid < (uint32_t)LD_WORDS) sm.stm[tid] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NV; ++k) {
+        const uint32_t i = tid + k * DIGEST_THREADS;
+        if (i < nvec && !(16u * i >= lb && 16u * i + 16u <= lend)) {  // ragged vector: bytes in [lb, lend)
+            uint32_t wv[4] = {0u, 0u, 0u, 0u};
+            for (uint32_t b = 0; b < 16; ++b) {
+                const uint32_t q = 16u * i + b;
+                if (q >= lb && q < lend) wv[b >> 2] |= (uint32_t)gb[q] << (8 * (b & 3u));
+            }
+            rv[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+    }
+    const uint32_t np_all = pl - pf + 2;
+    const uint32_t npst = np_all <= PST_CAP ? np_all : 0u;
+    uint64_t* nocm = reinterpret_cast<uint64_t*>(&sm.endm[0][0]);  // scratch until the walks
+    uint64_t* nokm = nocm + LD_WORDS;
+    uint32_t* s_cnt = reinterpret_cast<uint32_t*>(nokm + LD_WORDS);
+    __syncthreads();
+    // window -> LDS, cleave / no-cut flags -> 16-bit slices of the bit maps
+    // (every slice written: zeros past the window); protein starts
+    for (uint32_t i = tid; i < 4u * LD_WORDS; i += DIGEST_THREADS) {
+        uint32_t clv16 = 0, noc16 = 0;
+        const uint32_t k = (i - tid) / DIGEST_THREADS;
+        if (i < nvec) {
+            const uint4 v = k == 0 ? rv[0] : rv[NV - 1];
+            const uint32_t vlo = 16u * i >= lb ? 0u : lb - 16u * i;
+            const uint32_t vhi = 16u * i + 16u <= lend ? 16u : lend - 16u * i;
+            const uint32_t valid = (vhi > vlo) ? ((1u << vhi) - 1u) & ~((1u << vlo) - 1u) : 0u;
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+                const uint32_t f = sm.flags[(wv[b >> 2] >> (8 * (b & 3))) & 0xFFu];
+                clv16 |= (f & F_CLEAVE) << b;
+                noc16 |= ((f >> 1) & 1u) << b;
+            }
+            static_assert(F_CLEAVE == 1 && F_NOCUT == 2, "flag bits");
+            clv16 &= valid;
+            noc16 &= valid;
+            reinterpret_cast<uint4*>(sm.win)[i] = v;
+        }
+        reinterpret_cast<uint16_t*>(sm.clvm)[i] = (uint16_t)clv16;
+        reinterpret_cast<uint16_t*>(nocm)[i] = (uint16_t)noc16;
+    }
+    static_assert(NV == 2 && (4 * LD_WORDS) <= 2 * DIGEST_THREADS, "two vectors per thread");
+    for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
+        const uint32_t o = d_poff[pf + i];
+        if (o >= w0 && o <= w_end) {
+            const uint32_t q = o - w0 + lb;  // protein starts (and the end of the last one)
+            atomicOr(&sm.stm[q >> 6], 1ull << (q & 63));
+        }
+        if (i < PST_CAP) sm.pst[i] = o;
+    }
+    __syncthreads();
+    DBI_DPH(1);
+    // cut and N_ok maps, 64 positions per thread from the bit maps:
+    //   last     = a protein starts at q+1
+    //   cut      = last || (cleave(q) && !nocut(q+1))        (checkCleavage C side)
+    //   cut_prev = cleave(q-1) && !nocut(q)                   (its protein-end case is a start)
+    //   N_ok     = start(q) || cut_prev                       (the candidate starts)
+    // The window's last position (w_end < R): the next residue is unknown, its
+    // cut bit is never used (lean_ends' `known`).
+    if (tid < (uint32_t)LD_WORDS) {
+        const uint32_t w = tid;
+        const uint64_t valid = low_bits(lend > 64u * w ? min(lend - 64u * w, 64u) : 0u) &
+                               ~low_bits(lb > 64u * w ? min(lb - 64u * w, 64u) : 0u);
+        const uint64_t st = sm.stm[w];
+        const uint64_t st_n = w + 1 < (uint32_t)LD_WORDS ? sm.stm[w + 1] : 0ull;
+        const uint64_t cl = sm.clvm[w];
+        const uint64_t cl_p = w > 0 ? sm.clvm[w - 1] : 0ull;
+        const uint64_t nc = nocm[w];
+        const uint64_t nc_n = w + 1 < (uint32_t)LD_WORDS ? nocm[w + 1] : 0ull;
+        const uint64_t lastm = (st >> 1) | (st_n << 63);
+        sm.cutm[w] = (lastm | (cl & ~((nc >> 1) | (nc_n << 63)))) & valid;
+        nokm[w] = (st | (((cl << 1) | (cl_p >> 63)) & ~nc)) & valid;
+    }
+    __syncthreads();
+    DBI_DPH(2);
+    // cleavage-site compaction: thread t owns starts [16t, 16t+16) of the tile, in order
+    const uint32_t off = lb + (t0 - w0);  // LDS position of the tile's first start
+    const uint32_t n_here = t0 + tid * STARTS_PER_THREAD < t_end
+                                ? min((uint32_t)STARTS_PER_THREAD, t_end - t0 - tid * STARTS_PER_THREAD) : 0u;
+    const uint32_t mybits = (uint32_t)bits_from(nokm, off + tid * STARTS_PER_THREAD) &
+                            (n_here >= 16 ? 0xFFFFu : ((1u << n_here) - 1u));
+    uint32_t ncand;
+    uint32_t pos = block_excl_scan<DIGEST_THREADS, uint32_t>((uint32_t)__popc(mybits), sm.tmp, ncand);
+#pragma unroll
+    for (int k = 0; k < STARTS_PER_THREAD; ++k)
+        if (mybits & (1u << k)) sm.cand[pos++] = (uint16_t)(tid * STARTS_PER_THREAD + k);
+    __syncthreads();
+    DBI_DPH(3);
+
     const uint32_t B = (uint32_t)dp.max_missed + 2u;  // records per start, at most
-    tc.w = rec_width(d_ctr->max_plen);
-    if (tile == 0 && threadIdx.x == 0 && !rec_layout_ok(tc.w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
-    balance_candidates(sm, ncand, B, tc.t_end - tc.t0);
+    const uint32_t min_len = (uint32_t)dp.min_len;
+    const uint32_t known = w_end == n_res ? lend - 1u : lend - 2u;
+    const uint32_t w = rec_width(d_ctr->max_plen);
+    if (tile == 0 && tid == 0 && !rec_layout_ok(w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
+    balance_candidates(sm.cand, s_cnt, ncand, B, t_end - t0);
+    DBI_DPH(4);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
+    // slot bounds: the candidate ends (B for a walk that may leave the horizon)
     uint32_t lim = 0;
-    for (uint32_t j = jb; j < je; ++j)
-        lim += slot_bound(sm, tc.t0 - tc.w0 + sm.cand[j], tc.nbytes, B, (uint32_t)dp.min_len, B);
+    for (uint32_t j = jb; j < je; ++j) {
+        const LeanEnds en = lean_ends(sm, off + sm.cand[j], known, B, min_len);
+        lim += en.open ? B : (uint32_t)(__popcll(en.lo) + __popcll(en.hi));
+    }
     uint32_t tile_slots;
     const uint32_t excl_t = block_excl_scan<DIGEST_THREADS, uint32_t>(lim, sm.tmp, tile_slots);
-    if (threadIdx.x < 64) {
-        const unsigned long long excl = tile_lookback(status, tile, epoch, (unsigned long long)tile_slots);
-        if (threadIdx.x == 0) {
-            if (tile == gridDim.x - 1) d_ctr->n_slots = excl + tile_slots;
+    DBI_DPH(5);
+    // publish the tile's total, then walk every thread's first candidate
+    // (masses parked in LDS) while the predecessors' totals arrive
+    if (tid == 0) tile_publish(status, tile, epoch, (unsigned long long)tile_slots);
+    LeanWalk first{~0u, 0u, 0u, false};
+    if (jb < je) first = lean_masses(dp, sm, off + sm.cand[jb], lean_ends(sm, off + sm.cand[jb], known, B, min_len));
+    if (tid < 64) {
+        const unsigned long long excl = tile_lookback_wait(status, tile, epoch, (unsigned long long)tile_slots);
+        if (tid == 0) {
+            if (tile == ntiles - 1) d_ctr->n_slots = excl + tile_slots;
             s_base = excl;
         }
     }
     __syncthreads();
+    DBI_DPH(6);
     const unsigned long long base = s_base;
     if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
     Rec* __restrict__ o = d_out + base + excl_t;
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
-        const WalkOut w = walk_candidate_bounded<DROP>(dp, sm, tc, d_res, d_poff, j, o + kept, o + lim);
-        kept += w.kept;
-        dropped += w.dropped;
+        const uint32_t p = off + sm.cand[j];
+        const uint32_t s = w0 + (p - lb);
+        const LeanWalk lw = j == jb ? first : lean_masses(dp, sm, p, lean_ends(sm, p, known, B, min_len));
+        uint32_t pstart;
+        const uint32_t pid = protein_of(sm.pst, npst, pf, pl, d_poff, s, pstart);
+        const uint64_t loc = rec_loc(pid, s - pstart, w);
+        WalkOut wo;
+        if (lw.overflow) {
+            const uint32_t pe = d_poff[pid + 1];
+            wo = walk_global<true, false, false>(dp, sm.mass, sm.flags, d_res, s, pe, true, loc, o + kept, o + lim);
+        } else {
+            wo = lean_emit<DROP>(dp, sm, p, lw, loc, o + kept);
+        }
+        kept += wo.kept;
+        dropped += wo.dropped;
     }
-    if (kept > lim) atomicOr(&d_ctr->err, ERR_SLOTS);  // slot_bound is an upper bound: never
+    if (kept > lim) atomicOr(&d_ctr->err, ERR_SLOTS);  // the bound is an upper bound: never
     const Rec sent{REC_SENTINEL, REC_SENTINEL};
     for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
+#ifdef DBI_X_PHASE
+    __syncthreads();
+    DBI_DPH(7);
+#endif
     if (DROP) {
         const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
         const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
             if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
         }
@@ -1250,7 +1504,7 @@ hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, 
                                  Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s) {
     const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     if (nblk == 0) return hipSuccess;
-    if (dp.semi || dp.mand_mode) return hipErrorInvalidValue;
+    if (dp.semi || dp.mand_mode || dp.max_missed + 2 > LD_ENDS) return hipErrorInvalidValue;
     if (dp.drop_mass <= dp.max_mh)
         DBI_LAUNCH(k_digest_bounded<true>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
                    d_poff, n_prot, n_res, d_tile_pf, d_status, epoch, d_out, cap, d_ctr);
@@ -1734,7 +1988,7 @@ k_expand_locs(const unsigned long long* __restrict__ locs, uint64_t n, const uin
         const uint64_t ga = (uint64_t)poff[q1_pid(q1, w)] + q1_off(q1, w) + mis;
         const uint64_t last = (ga + len - 1) >> 2;
         double m = m0;
-        uint32_t h = FNV32_OFFSET;
+        uint32_t head = 0, tail = 0;
         for (uint32_t k0 = 0; k0 < len; k0 += 16) {
             const uint64_t ia = (ga + k0) >> 2;
             uint32_t wd[5];
@@ -1749,12 +2003,13 @@ k_expand_locs(const unsigned long long* __restrict__ locs, uint64_t n, const uin
                     if (k0 + 4 * j + b < len) {  // sequential, left to right (DBIndexer.java:306-308)
                         const uint32_t c = (x >> (8 * b)) & 0xFFu;
                         m = m + smass[c];
-                        h = fnv32_step(h, c);
+                        if (k0 == 0 && j == 0) head |= c << (8 * b);
+                        tail = (tail << 8) | c;
                     }
                 }
             }
         }
-        const uint32_t tag = fold_tag(h);
+        const uint32_t tag = peptide_tag(head, tail, len);
         Rec r;
         r.q0 = rec_q0(m, tag);
         r.q1 = ((uint64_t)(tag & 0xFFu) << 56) | (q1 & 0x00FFFFFFFFFFFFFFull);  // pid | off | len as sent
@@ -2081,9 +2336,6 @@ __device__ void block_bitonic(unsigned long long* k0, unsigned long long* k1, ui
 // waves.
 #ifdef DBI_X_CKSTAT
 __device__ unsigned int g_ck_stat[8];
-#endif
-#ifdef DBI_X_PHASE
-__device__ unsigned long long g_phase[24];  // sort_chunk phase clocks: [kernel*8 + phase]
 #endif
 constexpr int CK_IDX_BITS = 13;
 constexpr int CK_D_BITS = 64 - 16 - CK_IDX_BITS;
@@ -2852,9 +3104,7 @@ k_ptm_digest(DevParams dp, const double* __restrict__ mass_tab, const uint8_t* _
             }
             if (EMIT) {
                 const uint32_t len = q - s + 1;  // curSeqI
-                uint32_t h = FNV32_OFFSET;
-                for (uint32_t j = 0; j < len; ++j) h = fnv32_step(h, O[s + j]);
-                const uint32_t tag = fold_tag(h);
+                const uint32_t tag = peptide_tag_of(O + s, len);
                 o[kept] = Rec{rec_q0(m, tag), rec_q1(tag, rec_loc(pid, s, w), len)};
             }
             ++kept;
@@ -3395,10 +3645,7 @@ __global__ void k_occ_to_recs(const double* __restrict__ mass, const uint32_t* _
     if (i == 0 && !rec_layout_ok(W, n_prot)) atomicOr(&ctr->err, ERR_LAYOUT);
     if (i >= n) return;
     const uint32_t p = pid[i], o = off[i], l = len[i];
-    const uint8_t* __restrict__ g = res + poff[p] + o;
-    uint32_t h = FNV32_OFFSET;
-    for (uint32_t k = 0; k < l; ++k) h = fnv32_step(h, g[k]);
-    const uint32_t tag = fold_tag(h);
+    const uint32_t tag = peptide_tag_of(res + poff[p] + o, l);
     Rec r;
     r.q0 = rec_q0(mass[i], tag);
     r.q1 = rec_q1(tag, rec_loc(p, o, W), l);
@@ -3908,9 +4155,9 @@ hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_ch
 }  // namespace dbi
 #ifdef DBI_X_PHASE
 namespace dbi {
-void phase_read(unsigned long long* v) {
+void phase_read(unsigned long long* v) {  // 32 entries
     (void)hipDeviceSynchronize();
-    (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 24);
+    (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 32);
     unsigned long long z[24] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z));
 }

@@ -70,12 +70,31 @@ __host__ __device__ inline bool rec_layout_ok(uint32_t w, uint64_t n_prot) {
 }
 
 // Pinned order of different peptides with bit-identical mass:
-// (16-bit tag, first appearance), tag = 32-bit FNV-1a of the residue string
-// xor-folded to 16 bits.  The digest walk extends it one residue at a time.
-constexpr uint32_t FNV32_OFFSET = 2166136261u;
-constexpr uint32_t FNV32_PRIME = 16777619u;
-__host__ __device__ inline uint32_t fnv32_step(uint32_t h, uint32_t c) { return (h ^ c) * FNV32_PRIME; }
-__host__ __device__ inline uint16_t fold_tag(uint32_t h) { return (uint16_t)((h >> 16) ^ (h & 0xFFFFu)); }
+// (16-bit tag, first appearance).  The tag hashes the peptide's length and its
+// first and last (up to) four residues, so a digest walk reads residue bytes
+// only at the two ends of a peptide, never per residue step:
+//   head = s[0] | s[1] << 8 | s[2] << 16 | s[3] << 24        (bytes past the end: 0)
+//   tail = s[L-1] | s[L-2] << 8 | s[L-3] << 16 | s[L-4] << 24 (bytes before the start: 0)
+// (a walk keeps tail as tail << 8 | c).  oracle/cpu_ref.cpp peptide_tag and
+// oracle/pyref.py peptide_tag restate it over the string.
+__host__ __device__ inline uint32_t tag_keep(uint32_t len) { return len >= 4 ? ~0u : (1u << (8 * len)) - 1u; }
+__host__ __device__ inline uint16_t peptide_tag(uint32_t head, uint32_t tail, uint32_t len) {
+    const uint32_t k = tag_keep(len);
+    uint32_t x = ((head & k) * 0x9E3779B1u) ^ ((tail & k) * 0x85EBCA77u) ^ (len * 0xC2B2AE3Du);
+    x ^= x >> 15;
+    x *= 0x2C1B3C6Du;
+    x ^= x >> 12;
+    return (uint16_t)((x >> 16) ^ (x & 0xFFFFu));
+}
+// the tag of the len residues at s (reads s[0, len) only)
+__host__ __device__ inline uint16_t peptide_tag_of(const uint8_t* s, uint32_t len) {
+    uint32_t head = 0, tail = 0;
+    for (uint32_t k = 0; k < 4 && k < len; ++k) {
+        head |= (uint32_t)s[k] << (8 * k);
+        tail |= (uint32_t)s[len - 1 - k] << (8 * k);
+    }
+    return peptide_tag(head, tail, len);
+}
 
 constexpr int MAX_PRECURSOR_INT = 8000;  // (int) Constants.MAX_PRECURSOR_MASS
 

@@ -19,6 +19,7 @@
 // pair of MI355X GPUs has its own xGMI link, so the grouped exchange drives
 // all links at once; a ring would serialise them), or device copies between
 // the handles of one process (dbi_shard_exchange_local).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -43,7 +44,10 @@ struct dbi_comm {
     int rank = 0;
     int device = 0;
     unsigned long long* d_flag = nullptr;  // failure agreement (agree())
+    hipStream_t stream = nullptr;          // host-buffer collectives (dbi_comm_allreduce_*)
+    double* d_red = nullptr;               // their staging (COMM_RED_MAX values)
 };
+constexpr uint32_t COMM_RED_MAX = 4096;
 
 namespace dbi {
 namespace {
@@ -862,10 +866,15 @@ int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_co
         delete c;
         return set_error(DBI_E_OOM, "hipMalloc (communicator status word)");
     }
+    if (hipMalloc((void**)&c->d_red, COMM_RED_MAX * sizeof(double)) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        dbi_comm_destroy(c);
+        return set_error(DBI_E_HIP, "communicator stream / staging buffer");
+    }
     const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
     if (r != ncclSuccess) {
-        (void)hipFree(c->d_flag);
-        delete c;
+        c->comm = nullptr;
+        dbi_comm_destroy(c);
         return nccl_fail(r, "ncclCommInitRank");
     }
     *out = c;
@@ -875,9 +884,51 @@ int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_co
 void dbi_comm_destroy(dbi_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->d_flag) (void)hipFree(c->d_flag);
+    if (c->d_red) (void)hipFree(c->d_red);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+int dbi_comm_allreduce_f64(dbi_comm* c, const double* in, double* out, uint32_t n, int op) {
+    if (!c || (n && (!in || !out))) return set_error(DBI_E_INVALID, "NULL argument");
+    if (n > COMM_RED_MAX) return set_error(DBI_E_INVALID, "dbi_comm_allreduce_f64: at most 4096 values");
+    if (op != DBI_OP_SUM && op != DBI_OP_MAX && op != DBI_OP_MIN)
+        return set_error(DBI_E_INVALID, "dbi_comm_allreduce_f64: unknown op");
+    DBI_HIP(hipSetDevice(c->device));
+    const ncclRedOp_t rop = op == DBI_OP_SUM ? ncclSum : op == DBI_OP_MAX ? ncclMax : ncclMin;
+    const uint32_t m = n ? n : 1u;  // n = 0: a barrier (one value, ignored)
+    if (n) DBI_HIP(hipMemcpyAsync(c->d_red, in, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    else DBI_HIP(hipMemsetAsync(c->d_red, 0, sizeof(double), c->stream));
+    DBI_NCCL(ncclAllReduce(c->d_red, c->d_red, m, ncclFloat64, rop, c->comm, c->stream));
+    if (n) DBI_HIP(hipMemcpyAsync(out, c->d_red, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    DBI_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int dbi_comm_allreduce_u64(dbi_comm* c, const uint64_t* d_in, uint64_t* d_out, uint64_t n, void* stream) {
+    if (!c || (n && (!d_in || !d_out))) return set_error(DBI_E_INVALID, "NULL argument");
+    DBI_HIP(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (n) DBI_NCCL(ncclAllReduce(d_in, d_out, n, ncclUint64, ncclSum, c->comm, s));
+    if (!stream) DBI_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+int dbi_runtime_info_get(dbi_runtime_info* out) {
+    if (!out) return set_error(DBI_E_INVALID, "NULL argument");
+    std::memset(out, 0, sizeof(*out));
+    (void)hipRuntimeGetVersion(&out->hip_runtime_version);
+    (void)hipDriverGetVersion(&out->hip_driver_version);
+    (void)ncclGetVersion(&out->rccl_version);
+    Dl_info di;
+    if (dladdr(reinterpret_cast<void*>(static_cast<hipError_t (*)(void**, size_t)>(&hipMalloc)), &di) && di.dli_fname)
+        std::strncpy(out->libamdhip64, di.dli_fname, sizeof(out->libamdhip64) - 1);
+    if (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &di) && di.dli_fname)
+        std::strncpy(out->librccl, di.dli_fname, sizeof(out->librccl) - 1);
+    return 0;
 }
 
 int dbi_comm_allgatherv(dbi_comm* c, const void* d_send, void* d_recv, const uint64_t* rank_bytes, void* stream) {

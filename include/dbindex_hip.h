@@ -367,6 +367,17 @@ void dbi_comm_destroy(dbi_comm* c);
  * (rank_bytes[rank] bytes at d_send) lands at its offset (d_send may be that
  * spot).  Point-to-point sends/receives grouped over all peers. */
 int dbi_comm_allgatherv(dbi_comm* c, const void* d_send, void* d_recv, const uint64_t* rank_bytes, void* stream);
+/* Small host-buffer all-reduce over RCCL (bench / driver coordination: the
+ * barrier, max-over-ranks times, summed counts): out[i] = op over ranks of
+ * in[i], n <= 4096, op DBI_OP_SUM / DBI_OP_MAX / DBI_OP_MIN.  Blocking; a
+ * call with n = 0 is a barrier.  in may alias out. */
+#define DBI_OP_SUM 0
+#define DBI_OP_MAX 1
+#define DBI_OP_MIN 2
+int dbi_comm_allreduce_f64(dbi_comm* c, const double* in, double* out, uint32_t n, int op);
+/* Device-buffer sum all-reduce of n u64 values (a count histogram), in place
+ * allowed; stream NULL = the communicator's own stream (blocking). */
+int dbi_comm_allreduce_u64(dbi_comm* c, const uint64_t* d_in, uint64_t* d_out, uint64_t n, void* stream);
 /* All phases over RCCL: digest, sample all-gather, splitters, partition,
  * count all-gather, grouped send/recv exchange, owner merge, totals all-reduce. */
 int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_residues, uint64_t n_res,
@@ -534,6 +545,17 @@ int dbi_hbm_copy_bandwidth(int device, uint64_t bytes, int reps, double* gbps);
 /* ------------------------------------------------------------------------ */
 const char* dbi_last_error(void); /* thread-local; "" when no error */
 int dbi_abi_version(void);
+/* The HIP runtime and RCCL this library is bound to in this process: versions
+ * and the shared objects that provide hipMalloc / ncclGetVersion (dladdr), so
+ * a caller can check that one HIP runtime and one RCCL are in play. */
+typedef struct dbi_runtime_info {
+    int hip_runtime_version;  /* hipRuntimeGetVersion */
+    int hip_driver_version;   /* hipDriverGetVersion */
+    int rccl_version;         /* ncclGetVersion: major*10000 + minor*100 + patch */
+    char libamdhip64[512];
+    char librccl[512];
+} dbi_runtime_info;
+int dbi_runtime_info_get(dbi_runtime_info* out);
 int dbi_device_count(int* out);
 
 #ifdef __cplusplus

@@ -315,15 +315,20 @@ struct oref_index {
 namespace {
 
 // Pinned tie-break between different peptides of bit-identical mass
-// (semantics A7): the 32-bit FNV-1a of the peptide string folded
-// to 16 bits, then first appearance.
+// (semantics A7): a 16-bit hash of the length and the first and
+// last (up to) four residues, then first appearance.
 uint16_t peptide_tag(std::string_view s) {
-    uint32_t h = 2166136261u;
-    for (unsigned char c : s) {
-        h ^= c;
-        h *= 16777619u;
+    const uint32_t L = (uint32_t)s.size();
+    uint32_t head = 0, tail = 0;
+    for (uint32_t k = 0; k < 4 && k < L; ++k) {
+        head |= (uint32_t)(unsigned char)s[k] << (8 * k);
+        tail |= (uint32_t)(unsigned char)s[L - 1 - k] << (8 * k);
     }
-    return (uint16_t)((h >> 16) ^ (h & 0xFFFFu));
+    uint32_t x = (head * 0x9E3779B1u) ^ (tail * 0x85EBCA77u) ^ (L * 0xC2B2AE3Du);
+    x ^= x >> 15;
+    x *= 0x2C1B3C6Du;
+    x ^= x >> 12;
+    return (uint16_t)((x >> 16) ^ (x & 0xFFFFu));
 }
 
 int64_t row_of(const dbi_params* p, double mass) {

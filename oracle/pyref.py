@@ -131,12 +131,18 @@ def digest(params, proteins: Sequence[str]) -> list:
 
 def peptide_tag(s: str) -> int:
     """Pinned tie-break between different peptides of bit-identical mass
-    (DESIGN.md A7): 32-bit FNV-1a of the string folded to 16 bits."""
-    h = 2166136261
-    for ch in s.encode("ascii"):
-        h ^= ch
-        h = (h * 16777619) & 0xFFFFFFFF
-    return (h >> 16) ^ (h & 0xFFFF)
+    (DESIGN.md A7): a 16-bit hash of the length and the first and last (up
+    to) four residues."""
+    b = s.encode("ascii")
+    n = len(b)
+    head = sum(b[k] << (8 * k) for k in range(min(4, n)))
+    tail = sum(b[n - 1 - k] << (8 * k) for k in range(min(4, n)))
+    M = 0xFFFFFFFF
+    x = ((head * 0x9E3779B1) & M) ^ ((tail * 0x85EBCA77) & M) ^ ((n * 0xC2B2AE3D) & M)
+    x ^= x >> 15
+    x = (x * 0x2C1B3C6D) & M
+    x ^= x >> 12
+    return (x >> 16) ^ (x & 0xFFFF)
 
 
 def get_residues(offset: int, length: int, prot: str) -> Tuple[str, str]:
