@@ -21,28 +21,36 @@
 static const char* EXC = "edu/scripps/yates/utilities/fasta/dbindex/DBIndexStoreException";
 static const char* SEQLIST = "edu/scripps/yates/dbindex/hip/DBIndexStoreHip$SeqList";
 
-/* status -> pending checked exception; returns rc */
+/* status -> pending checked exception; returns rc.  An exception already
+ * pending (an OutOfMemoryError of a JNI call) is left as it is: JNI allows no
+ * further throw while one is pending. */
 static int fail(JNIEnv* e, int rc) {
-    if (rc) {
+    if (rc && !(*e)->ExceptionCheck(e)) {
         jclass c = (*e)->FindClass(e, EXC);
         if (c) (*e)->ThrowNew(e, c, dbi_last_error());
     }
     return rc;
 }
 
+/* a malloc of the shim failed (a failed JNI allocation has thrown already) */
 static int oom(JNIEnv* e) {
-    jclass c = (*e)->FindClass(e, "java/lang/OutOfMemoryError");
-    if (c) (*e)->ThrowNew(e, c, "dbindex_jni");
+    if (!(*e)->ExceptionCheck(e)) {
+        jclass c = (*e)->FindClass(e, "java/lang/OutOfMemoryError");
+        if (c) (*e)->ThrowNew(e, c, "dbindex_jni");
+    }
     return DBI_E_OOM;
 }
 
-/* chars of a Java string into flag table t (1 per residue present) */
-static void residue_flags(JNIEnv* e, jstring s, uint8_t* t) {
+/* chars of a Java string into flag table t (1 per residue present); -1 when
+ * the JVM could not copy the string (OutOfMemoryError pending) */
+static int residue_flags(JNIEnv* e, jstring s, uint8_t* t) {
     memset(t, 0, 256);
-    if (!s) return;
+    if (!s) return 0;
     const char* c = (*e)->GetStringUTFChars(e, s, NULL);
-    for (const char* p = c; p && *p; ++p) t[(unsigned char)*p] = 1;
+    if (!c) return -1;
+    for (const char* p = c; *p; ++p) t[(unsigned char)*p] = 1;
     (*e)->ReleaseStringUTFChars(e, s, c);
+    return 0;
 }
 
 JNIEXPORT jlong JNICALL JFN(create)(JNIEnv* e, jclass k, jdoubleArray mass, jstring cleave, jstring nocut,
@@ -58,9 +66,10 @@ JNIEXPORT jlong JNICALL JFN(create)(JNIEnv* e, jclass k, jdoubleArray mass, jstr
         return 0;
     }
     (*e)->GetDoubleArrayRegion(e, mass, 0, 256, p.mass);   /* AssignMass.getMass(c), every c */
-    residue_flags(e, cleave, p.cleave);                    /* Enzyme residues               */
-    residue_flags(e, nocut, p.nocut);                      /* getEnzymeNocutResidues()      */
-    residue_flags(e, mandatory, p.mandatory);              /* getMandatoryInternalAAs()     */
+    if (residue_flags(e, cleave, p.cleave) ||              /* Enzyme residues               */
+        residue_flags(e, nocut, p.nocut) ||                /* getEnzymeNocutResidues()      */
+        residue_flags(e, mandatory, p.mandatory))          /* getMandatoryInternalAAs()     */
+        return 0;
     p.mandatory_mode = mandatory != NULL;                  /* null vs empty (DBIndexer.java:334) */
     p.mandatory_count = 0;
     for (int c = 0; c < 256; ++c) p.mandatory_count += p.mandatory[c];
@@ -85,6 +94,7 @@ JNIEXPORT void JNICALL JFN(close0)(JNIEnv* e, jclass k, jlong h) {
 JNIEXPORT void JNICALL JFN(init0)(JNIEnv* e, jclass k, jlong h, jstring id) {
     (void)k;
     const char* s = id ? (*e)->GetStringUTFChars(e, id, NULL) : NULL;
+    if (id && !s) return; /* OutOfMemoryError pending */
     const int rc = dbi_store_init(STORE(h), s ? s : "");
     if (s) (*e)->ReleaseStringUTFChars(e, id, s);
     fail(e, rc);
@@ -111,6 +121,7 @@ JNIEXPORT jint JNICALL JFN(filterSequence0)(JNIEnv* e, jclass k, jlong h, jdoubl
     (void)k;
     const char* s = (*e)->GetStringUTFChars(e, seq, NULL);
     int out = DBI_FILTER_SKIP;
+    if (!s) return out; /* OutOfMemoryError pending */
     const int rc = dbi_store_filter_sequence(STORE(h), mass, s, strlen(s), &out);
     (*e)->ReleaseStringUTFChars(e, seq, s);
     fail(e, rc);  /* filterSequence declares no exception: an unchecked-style pending one */
@@ -126,7 +137,12 @@ JNIEXPORT void JNICALL JFN(addSequence0)(JNIEnv* e, jclass k, jlong h, jdouble m
 JNIEXPORT jlong JNICALL JFN(addProteinDef0)(JNIEnv* e, jclass k, jlong h, jlong num, jstring def, jstring seq) {
     (void)k;
     const char* d = (*e)->GetStringUTFChars(e, def, NULL);
+    if (!d) return -1; /* OutOfMemoryError pending */
     const char* q = (*e)->GetStringUTFChars(e, seq, NULL);
+    if (!q) {
+        (*e)->ReleaseStringUTFChars(e, def, d);
+        return -1;
+    }
     int64_t id = -1;
     const int rc = dbi_store_add_protein_def(STORE(h), num, d, q, strlen(q), &id);
     (*e)->ReleaseStringUTFChars(e, def, d);
@@ -210,7 +226,7 @@ JNIEXPORT void JNICALL JFN(setUnindexed0)(JNIEnv* e, jclass k, jlong h, jint mod
 /* dbi_seq_list -> DBIndexStoreHip.SeqList (flat arrays; Java builds the
  * IndexedSequence objects, DBIndexStoreHip.toList) */
 static int set_array(JNIEnv* e, jobject o, jclass c, const char* name, const char* sig, jobject arr) {
-    if (!arr) return oom(e);
+    if (!arr) return DBI_E_OOM; /* the failed New<Type>Array threw OutOfMemoryError */
     jfieldID f = (*e)->GetFieldID(e, c, name, sig);
     if (!f) return DBI_E_INVALID;
     (*e)->SetObjectField(e, o, f, arr);

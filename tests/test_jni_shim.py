@@ -104,3 +104,36 @@ def test_java_side_overrides_the_reference_interface():
     assert re.search(r"public List<IndexedSequence> cutAndSearch\(List<MassRange>", store)
     impl = open(os.path.join(JAVA, "DBIndexImplHip.java")).read()
     assert "extends DBIndexImpl" in impl and "new DBIndexerHip(" in impl
+
+
+STUB = os.path.join(ROOT, "tests", "jni_stub")
+
+
+def test_jni_shim_compiles_against_the_header():
+    """The shim passes a C compiler with every warning an error: each
+    dbi_store_* call is type-checked against include/dbindex_hip.h (types,
+    not just arity).  The JNI types come from a test-only header declaring
+    the specification's C signatures of the JNIEnv entries the shim uses
+    (tests/jni_stub/jni.h: no JDK in this image)."""
+    import subprocess
+    r = subprocess.run(["gcc", "-fsyntax-only", "-std=c11", "-Wall", "-Wextra", "-Werror", "-Wconversion",
+                        "-Wno-sign-conversion", "-Wstrict-prototypes", "-I", STUB, "-I", os.path.join(ROOT, "include"),
+                        JNI], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_jni_shim_links_against_the_library(tmp_path):
+    """Linked as the JNI library a JVM would load: every dbi_* symbol the
+    shim calls resolves in the built libdbindex_hip.so (--no-undefined)."""
+    import subprocess
+    import pytest
+    lib = os.path.join(ROOT, "dbindex_amd", "libdbindex_hip.so")
+    if not os.path.exists(lib):
+        pytest.skip("libdbindex_hip.so not built")
+    out = tmp_path / "libdbindex_jni.so"
+    r = subprocess.run(["gcc", "-shared", "-fPIC", "-std=c11", "-O2", "-I", STUB, "-I", os.path.join(ROOT, "include"),
+                        JNI, "-o", str(out), "-L", os.path.dirname(lib), "-l:libdbindex_hip.so",
+                        "-Wl,--no-undefined", f"-Wl,-rpath,{os.path.dirname(lib)}"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(out)], capture_output=True, text=True).stdout
+    assert "Java_edu_scripps_yates_dbindex_hip_DBIndexStoreHip_getSequences0" in nm
