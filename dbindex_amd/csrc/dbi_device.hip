@@ -425,7 +425,7 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
                                    const double* __restrict__ d_mass_tab,
                                    const uint8_t* __restrict__ d_flags, const uint8_t* __restrict__ d_res,
                                    const uint32_t* __restrict__ d_poff, uint32_t n_prot, uint32_t n_res,
-                                   const uint32_t* __restrict__ d_tile_pf) {
+                                   const uint32_t* __restrict__ d_tile_pf, Counters* __restrict__ d_ctr) {
     const uint32_t tid = threadIdx.x;
     tc.t0 = tile * (uint32_t)DIGEST_TILE;
     tc.t_end = min(tc.t0 + (uint32_t)DIGEST_TILE, n_res);
@@ -466,6 +466,7 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
     static_assert(WIN_WORDS <= DIGEST_THREADS, "one thread per bit-map word");
     const uint32_t np_all = tc.pl - tc.pf + 2;
     __syncthreads();
+    uint32_t anyf = 0;  // class flags of every residue staged (F_PTM: '[' in device input)
     // residue window -> LDS as (residue | flags << 8): a vector's 16 entries
     // leave as two 16-B LDS stores when the window is 8-entry aligned; its
     // cleave and no-cut flags as 16-bit slices of the two bit maps
@@ -480,6 +481,7 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
             for (int b = 0; b < 16; ++b) {
                 const uint32_t c = (wv[b >> 2] >> (8 * (b & 3))) & 0xFFu;
                 const uint32_t f = sm.flags[c];
+                anyf |= f;
                 e[b] = c | (f << 8);
                 clv16 |= (f & F_CLEAVE) << b;
                 noc16 |= ((f >> 1) & 1u) << b;
@@ -499,10 +501,12 @@ __device__ uint32_t digest_prepare(DigestSmem& sm, TileCtx& tc, uint32_t tile, u
     }
     if (has_edge) {
         const uint32_t f = sm.flags[edge];
+        anyf |= f;
         sm.win[epos] = (uint16_t)(edge | (f << 8));
         or_slice16(sm.clvm, epos, f & F_CLEAVE);
         or_slice16(nocut_map(sm), epos, (f >> 1) & 1u);
     }
+    if (anyf & F_PTM) atomicOr(&d_ctr->err, ERR_PTM);
     tc.npst = np_all <= PST_CAP ? np_all : 0u;
     for (uint32_t i = tid; i < np_all; i += DIGEST_THREADS) {
         const uint32_t o = d_poff[tc.pf + i];
@@ -653,7 +657,7 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     __shared__ DigestSmem sm;
     TileCtx tc;
     const uint32_t ncand = digest_prepare<SEMI>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
-                                                d_tile_pf);
+                                                d_tile_pf, d_ctr);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
     if (!EMIT) {
@@ -863,7 +867,7 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     __shared__ double s_dtmp[DIGEST_THREADS / 64 + 1];
     TileCtx tc;
     const uint32_t ncand = digest_prepare<false>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
-                                                 d_tile_pf);
+                                                 d_tile_pf, d_ctr);
     build_cut_tables(sm, cs, tc.nbytes, s_dtmp);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
@@ -904,31 +908,57 @@ __device__ __forceinline__ void tile_publish(unsigned long long* __restrict__ st
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave 0 of a tile that published its total: look back 64 tiles at a time
-// for the exclusive prefix (returned to every lane), publish the inclusive one.
+// Wave 0 of a tile that published its total: look back LB_SPAN tiles at a
+// time (LB_PER consecutive status words per lane, loaded together: the
+// frontier of published prefixes trails the tiles now looking back by a
+// few hundred tiles, and one round trip per 64 tiles made that lag feed
+// itself) for the exclusive prefix (returned to every lane); publish the
+// inclusive one.
+#ifndef DBI_X_LBPER
+#define DBI_X_LBPER 1
+#endif
+constexpr uint32_t LB_PER = DBI_X_LBPER;
+constexpr int64_t LB_SPAN = 64 * LB_PER;
+
 __device__ unsigned long long tile_lookback_wait(unsigned long long* __restrict__ status, uint32_t tile,
                                                  uint32_t epoch, unsigned long long total) {
     unsigned long long excl = 0;
     int64_t t = (int64_t)tile - 1;
     const uint32_t lane = lane_id();
     while (t >= 0) {
-        const int64_t q = t - (int64_t)lane;
-        unsigned long long v = 0;
-        bool ready = true;
-        if (q >= 0) {
-            v = __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ready = (uint32_t)(v >> 48) == epoch && ((v >> 46) & 3ull) != 0;
+        // entry k of this lane: tile t - (LB_PER * lane + k), nearest first
+        unsigned long long v[LB_PER];
+#pragma unroll
+        for (uint32_t k = 0; k < LB_PER; ++k) {
+            const int64_t q = t - (int64_t)(LB_PER * lane + k);
+            v[k] = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
         }
-        const uint64_t pref = __ballot(q >= 0 && ready && ((v >> 46) & 3ull) == ST_PREFIX);
-        const uint64_t notready = __ballot(!ready);
-        // lanes up to (and including) the nearest prefix, all ready -> sum them
+        uint32_t notready = 0, first_pref = LB_PER;
+#pragma unroll
+        for (int k = LB_PER - 1; k >= 0; --k) {
+            const int64_t q = t - (int64_t)(LB_PER * lane + k);
+            const unsigned long long st = (v[k] >> 46) & 3ull;
+            const bool ready = q < 0 || ((uint32_t)(v[k] >> 48) == epoch && st != 0);
+            notready |= (ready ? 0u : 1u) << k;
+            if (q >= 0 && ready && st == ST_PREFIX) first_pref = (uint32_t)k;
+        }
+        const uint64_t pref = __ballot(first_pref < LB_PER);
+        // entries up to (and including) the nearest prefix must all be ready
         const uint32_t upto = pref ? (uint32_t)__ffsll((long long)pref) - 1 : 64u;  // nearest prefix lane
-        const uint64_t need = upto >= 63 ? ~0ull : ((2ull << upto) - 1);
-        if (notready & need) continue;  // a predecessor has not published yet: poll again
-        const unsigned long long val = (lane <= upto && q >= 0) ? (v & ((1ull << 46) - 1)) : 0ull;
+        const uint32_t need = lane < upto ? (1u << LB_PER) - 1u : lane == upto ? (2u << first_pref) - 1u : 0u;
+        if (__ballot((notready & need) != 0)) {  // a predecessor has not published yet: poll again
+#ifdef DBI_X_LBSLEEP
+            __builtin_amdgcn_s_sleep(DBI_X_LBSLEEP);
+#endif
+            continue;
+        }
+        unsigned long long val = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < LB_PER; ++k)
+            if ((need >> k) & 1u) val += v[k] & ((1ull << 46) - 1);  // q < 0: v = 0
         excl += wave_sum(val);
         if (pref) break;
-        t -= 64;
+        t -= LB_SPAN;
     }
     if (threadIdx.x == 0 && tile != 0)
         __hip_atomic_store(&status[tile], st_pack(epoch, ST_PREFIX, excl + total), __ATOMIC_RELAXED,
@@ -957,7 +987,7 @@ k_digest_fused(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_
     const uint32_t tile = s_tile;
     TileCtx tc;
     const uint32_t ncand = digest_prepare<SEMI>(sm, tc, tile, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
-                                                d_tile_pf);
+                                                d_tile_pf, d_ctr);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
     // count (exact walk: the cut-stepping tables would cost this kernel its
@@ -1293,7 +1323,11 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     uint64_t dph_t = wall_clock64();
 #endif
     if (tid == 0) {
+#ifdef DBI_X_NOTICKET
+        s_tile = blockIdx.x;
+#else
         s_tile = atomicAdd(&d_ctr->tile_ticket, 1u);
+#endif
         s_kept = 0;
         s_waves = 0;
     }
@@ -1353,15 +1387,18 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
             const uint32_t vhi = 16u * i + 16u <= lend ? 16u : lend - 16u * i;
             const uint32_t valid = (vhi > vlo) ? ((1u << vhi) - 1u) & ~((1u << vlo) - 1u) : 0u;
             const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            uint32_t ptm16 = 0;
 #pragma unroll
             for (int b = 0; b < 16; ++b) {
                 const uint32_t f = sm.flags[(wv[b >> 2] >> (8 * (b & 3))) & 0xFFu];
                 clv16 |= (f & F_CLEAVE) << b;
                 noc16 |= ((f >> 1) & 1u) << b;
+                ptm16 |= ((f >> 5) & 1u) << b;
             }
-            static_assert(F_CLEAVE == 1 && F_NOCUT == 2, "flag bits");
+            static_assert(F_CLEAVE == 1 && F_NOCUT == 2 && F_PTM == 32, "flag bits");
             clv16 &= valid;
             noc16 &= valid;
+            if (ptm16 & valid) atomicOr(&d_ctr->err, ERR_PTM);  // '[' in device input
             reinterpret_cast<uint4*>(sm.win)[i] = v;
         }
         reinterpret_cast<uint16_t*>(sm.clvm)[i] = (uint16_t)clv16;

@@ -152,6 +152,7 @@ struct dbi_handle {
     DevBuf<dbi::QueryDir> qdir_par;
     uint64_t build_serial = 0, qdir_serial = 0;
     bool inputs_resident = false;       // res/poff hold the last host build's inputs (dbi_rebuild)
+    bool inputs_ptm = false;            // ... and they carry inline '[formula]' PTMs (no dbi_rebuild)
     DevBuf<double> q_mass, q_tol;
     DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
     DevBuf<uint32_t> h_nh, h_no, h_ids, h_hocc, h_prot;  // dbi_query_hits_device
@@ -238,6 +239,7 @@ inline Bytes by(double cR, double cN, double cU, double cP, double cB) {
 }
 
 int read_counters(dbi_handle* h);
+const char* ptm_device_msg();  // ERR_PTM's message
 int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot);
 int prepare_tiles(dbi_handle* h);
 // digest of h->d_res / h->d_poff into recA: *n records (*n_in slots, REC_SENTINEL

@@ -117,6 +117,11 @@ int log2_ceil(uint32_t x) {
     return r;
 }
 
+const char* ptm_device_msg() {
+    return "inline '[formula]' PTMs in device-resident residues: digested only from host input (dbi_build), "
+           "which strips and walks them (DBIndexer.java:288-303)";
+}
+
 int read_counters(dbi_handle* h) {
     DBI_HIP(hipMemcpyAsync(&h->hc, h->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, h->stream));
     DBI_HIP(hipStreamSynchronize(h->stream));
@@ -223,6 +228,7 @@ int finish_build(dbi_handle* h) {
     if (rc) return rc;
     if (h->hc.err & ERR_SEGS) return set_error(DBI_E_STATE, "internal: giant-chunk segment list overflow");
     if (h->hc.err & ERR_SLOTS) return set_error(DBI_E_STATE, "internal: digest slot bound exceeded");
+    if (h->hc.err & ERR_PTM) return set_error(DBI_E_INVALID, ptm_device_msg());
     if (h->hc.err & ERR_LAYOUT)
         return set_error(DBI_E_INVALID, "2 x bits(longest protein) + bits(protein count) exceeds the 56 bits of the "
                                         "16-B occurrence record: shard the FASTA");
@@ -521,6 +527,7 @@ int build_with_ptms(dbi_handle* h, const uint8_t* residues, uint64_t n_res, cons
     // those proteins are walked literally by k_ptm_digest
     if ((rc = begin_build(h, n_res, n_prot))) return rc;
     if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
+    h->inputs_ptm = true;  // dbi_rebuild cannot digest this text directly
     std::vector<uint8_t> masked = pl.stripped;
     std::vector<uint8_t> sres;
     std::vector<uint32_t> soff32(1, 0), off32(n_prot + 1);
@@ -610,6 +617,7 @@ int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const 
     h->d_res = h->res.p;
     h->d_poff = h->poff.p;
     h->inputs_resident = true;
+    h->inputs_ptm = false;
     return 0;
 }
 
@@ -759,7 +767,7 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     uint8_t fl[256];
     for (int c = 0; c < 256; ++c)
         fl[c] = (params->cleave[c] ? F_CLEAVE : 0) | (params->nocut[c] ? F_NOCUT : 0) |
-                (params->mandatory[c] ? F_MAND : 0);
+                (params->mandatory[c] ? F_MAND : 0) | (c == '[' ? F_PTM : 0);
     if (hipMemcpy(h->mass_tab.p, params->mass, sizeof(double) * 256, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->flags_tab.p, fl, 256, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(h->ctr.p, 0, sizeof(Counters)) != hipSuccess ||
@@ -1189,6 +1197,9 @@ int dbi_rebuild(dbi_handle* h) {
     if (!h) return set_error(DBI_E_INVALID, "NULL handle");
     if (!h->inputs_resident || h->d_res != h->res.p || h->d_poff != h->poff.p)
         return set_error(DBI_E_STATE, "no resident inputs: dbi_build from host arrays first");
+    if (h->inputs_ptm)
+        return set_error(DBI_E_INVALID, "dbi_rebuild after a build with inline '[formula]' PTMs: call dbi_build "
+                                        "again (the resident text still holds the formulas)");
     int rc;
     const uint64_t n_res = h->n_res, n_prot = h->n_prot;
     if ((rc = begin_build(h, n_res, n_prot))) return rc;

@@ -104,6 +104,7 @@ constexpr uint8_t F_NOCUT = 2;
 constexpr uint8_t F_MAND = 4;
 constexpr uint8_t F_CUT = 8;    // window only: checkCleavage C-side ok at this residue (or protein end)
 constexpr uint8_t F_LAST = 16;  // window only: last residue of its protein
+constexpr uint8_t F_PTM = 32;   // '[': an inline formula (DBIndexer.java:288-303) where none may be
 
 struct BinMap {
     double lo;
@@ -171,6 +172,7 @@ struct Counters {
 constexpr unsigned ERR_LAYOUT = 1;  // 2*bits(longest protein) + bits(proteins) > 56
 constexpr unsigned ERR_SEGS = 2;    // giant split: a segment list overflowed (internal)
 constexpr unsigned ERR_SLOTS = 4;   // bounded digest: a thread emitted more records than it reserved (internal)
+constexpr unsigned ERR_PTM = 8;     // a device digest met '[' (inline PTMs are only digested from host input)
 
 // Tunables
 constexpr int DIGEST_THREADS = 256;

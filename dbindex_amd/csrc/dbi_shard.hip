@@ -387,6 +387,7 @@ int dbi_shard_digest(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const 
         return rc;
     }
     if (h->hc.err & ERR_LAYOUT) return set_error(DBI_E_INVALID, "record layout overflow in the shard digest");
+    if (h->hc.err & ERR_PTM) return set_error(DBI_E_INVALID, ptm_device_msg());
     // the digest stages' algorithmic bytes are this shard's (the handle turns
     // into the owner of a slice of the whole proteome at the merge)
     for (int i = 0; i < h->nstage; ++i) {

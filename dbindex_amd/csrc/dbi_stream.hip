@@ -143,6 +143,7 @@ int dbi_count(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_
         DBI_HIP(launch_scan_u32(h->blk.p, h->blk.p, nblk, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_kept, s));
     }
     if ((rc = read_counters(h))) return rc;
+    if (h->hc.err & ERR_PTM) return set_error(DBI_E_INVALID, ptm_device_msg());
     *n_total = h->hc.n_kept + h->hc.n_dropped;
     if (n_dropped) *n_dropped = h->hc.n_dropped;
     return 0;

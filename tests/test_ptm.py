@@ -198,3 +198,40 @@ def test_store_ptm_text_from_the_cache_strings():
             assert g.getMass() == float(u["mass"][i]) and g.getProteinIds()[0] == p0
             assert g.getSequence() == seqs[p0][o:o + ln]
             assert (g.getResLeft(), g.getResRight()) == pyref.get_residues(o, ln, seqs[p0])
+
+
+@pytest.mark.gpu
+def test_engine_ptm_text_is_not_rebuilt_or_digested_on_device():
+    """A build with inline formulas leaves the unstripped text resident:
+    dbi_rebuild refuses it (it would digest the '[' characters as residues),
+    and the device-input paths (dbi_build_device, dbi_count) refuse residues
+    holding '[' instead of indexing them silently differently from dbi_build."""
+    from dbindex_amd import _native
+    from dbindex_amd._native import DeviceBuffer, synchronize
+    from dbindex_amd.engine import Engine
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    seqs = ptm_proteome(40)
+    res, off = _pack(seqs)
+    pp = fasta.PackedProteins(res, off)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, res, off)
+    from tests.helpers import assert_index_equal
+    with Engine(cp) as eng:
+        eng.build(pp)
+        with pytest.raises(_native.DBIndexStoreException, match="dbi_rebuild after a build with inline"):
+            eng.rebuild()
+        eng.build(pp)  # the refusal left the handle usable
+        assert_index_equal(eng, oix, "ptm build after refused rebuild")
+        d_res = DeviceBuffer.from_numpy(np.concatenate([res, np.zeros(16, np.uint8)]), 0)
+        d_off = DeviceBuffer.from_numpy(off.astype(np.uint64), 0)
+        synchronize(0)
+        for call in (lambda: eng.build_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins),
+                     lambda: eng.count_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins)):
+            with pytest.raises(_native.DBIndexStoreException, match="device-resident residues"):
+                call()
+        # plain text on the same paths still builds
+        plain = fasta.config("1k").slice(0, 50)
+        eng.build(plain)
+        st = eng.rebuild()
+        assert st.n_total == cref.Index(cp, plain.residues, plain.offsets).n_total
