@@ -908,57 +908,33 @@ __device__ __forceinline__ void tile_publish(unsigned long long* __restrict__ st
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave 0 of a tile that published its total: look back LB_SPAN tiles at a
-// time (LB_PER consecutive status words per lane, loaded together: the
-// frontier of published prefixes trails the tiles now looking back by a
-// few hundred tiles, and one round trip per 64 tiles made that lag feed
-// itself) for the exclusive prefix (returned to every lane); publish the
-// inclusive one.
-#ifndef DBI_X_LBPER
-#define DBI_X_LBPER 1
-#endif
-constexpr uint32_t LB_PER = DBI_X_LBPER;
-constexpr int64_t LB_SPAN = 64 * LB_PER;
-
+// Wave 0 of a tile that published its total: look back 64 tiles at a time
+// for the exclusive prefix (returned to every lane), publish the inclusive one.
+// (Four status words per lane per round trip measured slower: the pollers'
+// traffic, not the hops, is what the wait costs.)
 __device__ unsigned long long tile_lookback_wait(unsigned long long* __restrict__ status, uint32_t tile,
                                                  uint32_t epoch, unsigned long long total) {
     unsigned long long excl = 0;
     int64_t t = (int64_t)tile - 1;
     const uint32_t lane = lane_id();
     while (t >= 0) {
-        // entry k of this lane: tile t - (LB_PER * lane + k), nearest first
-        unsigned long long v[LB_PER];
-#pragma unroll
-        for (uint32_t k = 0; k < LB_PER; ++k) {
-            const int64_t q = t - (int64_t)(LB_PER * lane + k);
-            v[k] = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const int64_t q = t - (int64_t)lane;
+        unsigned long long v = 0;
+        bool ready = true;
+        if (q >= 0) {
+            v = __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ready = (uint32_t)(v >> 48) == epoch && ((v >> 46) & 3ull) != 0;
         }
-        uint32_t notready = 0, first_pref = LB_PER;
-#pragma unroll
-        for (int k = LB_PER - 1; k >= 0; --k) {
-            const int64_t q = t - (int64_t)(LB_PER * lane + k);
-            const unsigned long long st = (v[k] >> 46) & 3ull;
-            const bool ready = q < 0 || ((uint32_t)(v[k] >> 48) == epoch && st != 0);
-            notready |= (ready ? 0u : 1u) << k;
-            if (q >= 0 && ready && st == ST_PREFIX) first_pref = (uint32_t)k;
-        }
-        const uint64_t pref = __ballot(first_pref < LB_PER);
-        // entries up to (and including) the nearest prefix must all be ready
+        const uint64_t pref = __ballot(q >= 0 && ready && ((v >> 46) & 3ull) == ST_PREFIX);
+        const uint64_t notready = __ballot(!ready);
+        // lanes up to (and including) the nearest prefix, all ready -> sum them
         const uint32_t upto = pref ? (uint32_t)__ffsll((long long)pref) - 1 : 64u;  // nearest prefix lane
-        const uint32_t need = lane < upto ? (1u << LB_PER) - 1u : lane == upto ? (2u << first_pref) - 1u : 0u;
-        if (__ballot((notready & need) != 0)) {  // a predecessor has not published yet: poll again
-#ifdef DBI_X_LBSLEEP
-            __builtin_amdgcn_s_sleep(DBI_X_LBSLEEP);
-#endif
-            continue;
-        }
-        unsigned long long val = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < LB_PER; ++k)
-            if ((need >> k) & 1u) val += v[k] & ((1ull << 46) - 1);  // q < 0: v = 0
+        const uint64_t need = upto >= 63 ? ~0ull : ((2ull << upto) - 1);
+        if (notready & need) continue;  // a predecessor has not published yet: poll again
+        const unsigned long long val = (lane <= upto && q >= 0) ? (v & ((1ull << 46) - 1)) : 0ull;
         excl += wave_sum(val);
         if (pref) break;
-        t -= LB_SPAN;
+        t -= 64;
     }
     if (threadIdx.x == 0 && tile != 0)
         __hip_atomic_store(&status[tile], st_pack(epoch, ST_PREFIX, excl + total), __ATOMIC_RELAXED,
@@ -1313,27 +1289,21 @@ template <bool DROP>
 __global__ void __launch_bounds__(DIGEST_THREADS)
 k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                  const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
-                 uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, unsigned long long* __restrict__ status,
-                 uint32_t epoch, Rec* __restrict__ d_out, uint64_t cap, Counters* __restrict__ d_ctr) {
+                 uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, Rec* __restrict__ d_out, uint64_t cap,
+                 Counters* __restrict__ d_ctr) {
     __shared__ LeanSmem sm;
-    __shared__ uint32_t s_tile, s_kept, s_waves;
+    __shared__ uint32_t s_kept, s_waves;
     __shared__ unsigned long long s_base;
     const uint32_t tid = threadIdx.x;
 #ifdef DBI_X_PHASE
     uint64_t dph_t = wall_clock64();
 #endif
-    if (tid == 0) {
-#ifdef DBI_X_NOTICKET
-        s_tile = blockIdx.x;
-#else
-        s_tile = atomicAdd(&d_ctr->tile_ticket, 1u);
-#endif
+    if (tid == 0) {  // read at the end, behind many barriers
         s_kept = 0;
         s_waves = 0;
     }
-    __syncthreads();
     DBI_DPH(0);
-    const uint32_t tile = s_tile, ntiles = gridDim.x;
+    const uint32_t tile = blockIdx.x, ntiles = gridDim.x;
     const uint32_t t0 = tile * (uint32_t)DIGEST_TILE;
     const uint32_t t_end = min(t0 + (uint32_t)DIGEST_TILE, n_res);
     const uint32_t w0 = t0 >= (uint32_t)LD_PRE ? t0 - (uint32_t)LD_PRE : 0u;
@@ -1470,18 +1440,11 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     uint32_t tile_slots;
     const uint32_t excl_t = block_excl_scan<DIGEST_THREADS, uint32_t>(lim, sm.tmp, tile_slots);
     DBI_DPH(5);
-    // publish the tile's total, then walk every thread's first candidate
-    // (masses parked in LDS) while the predecessors' totals arrive
-    if (tid == 0) tile_publish(status, tile, epoch, (unsigned long long)tile_slots);
-    LeanWalk first{~0u, 0u, 0u, false};
-    if (jb < je) first = lean_masses(dp, sm, off + sm.cand[jb], lean_ends(sm, off + sm.cand[jb], known, B, min_len));
-    if (tid < 64) {
-        const unsigned long long excl = tile_lookback_wait(status, tile, epoch, (unsigned long long)tile_slots);
-        if (tid == 0) {
-            if (tile == ntiles - 1) d_ctr->n_slots = excl + tile_slots;
-            s_base = excl;
-        }
-    }
+    // the tile's output region: one atomic add, in whatever order the tiles
+    // get here (no tile waits for another; the chunk sort does not need
+    // records in first-appearance order, ck_fix_runs); ctr->n_slots ends as
+    // the total
+    if (tid == 0) s_base = atomicAdd(&d_ctr->n_slots, (unsigned long long)tile_slots);
     __syncthreads();
     DBI_DPH(6);
     const unsigned long long base = s_base;
@@ -1491,7 +1454,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     for (uint32_t j = jb; j < je; ++j) {
         const uint32_t p = off + sm.cand[j];
         const uint32_t s = w0 + (p - lb);
-        const LeanWalk lw = j == jb ? first : lean_masses(dp, sm, p, lean_ends(sm, p, known, B, min_len));
+        const LeanWalk lw = lean_masses(dp, sm, p, lean_ends(sm, p, known, B, min_len));
         uint32_t pstart;
         const uint32_t pid = protein_of(sm.pst, npst, pf, pl, d_poff, s, pstart);
         const uint64_t loc = rec_loc(pid, s - pstart, w);
@@ -1537,17 +1500,16 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
 
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
-                                 const uint32_t* d_tile_pf, unsigned long long* d_status, uint32_t epoch,
-                                 Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s) {
+                                 const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s) {
     const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     if (nblk == 0) return hipSuccess;
     if (dp.semi || dp.mand_mode || dp.max_missed + 2 > LD_ENDS) return hipErrorInvalidValue;
     if (dp.drop_mass <= dp.max_mh)
         DBI_LAUNCH(k_digest_bounded<true>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
-                   d_poff, n_prot, n_res, d_tile_pf, d_status, epoch, d_out, cap, d_ctr);
+                   d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr);
     else
         DBI_LAUNCH(k_digest_bounded<false>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
-                   d_poff, n_prot, n_res, d_tile_pf, d_status, epoch, d_out, cap, d_ctr);
+                   d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr);
     return hipGetLastError();
 }
 
@@ -2463,6 +2425,35 @@ __device__ __forceinline__ bool ck_order_bad(const unsigned long long* k0, const
     return k0[p] == k0[p - 1] && (k1[p] >> 56) == (k1[p - 1] >> 56) && k1[p] < k1[p - 1];
 }
 
+// Records need not arrive in first-appearance order (digest tiles take their
+// output regions in arrival order), so after the compact-key sort a run of
+// equal (mass, tag) -- the occurrences of one peptide, or a tag collision --
+// may be out of q1 order: each run is put in order by one thread (insertion
+// sort of q1; q0 is equal across the run).  Runs of [lo, lo+L) whose head
+// lies in this thread's share [i0, i1); false when a run is longer than
+// CK_RUN_MAX (the caller sorts the whole bin by the full key instead).
+constexpr uint32_t CK_RUN_MAX = 32;
+__device__ __forceinline__ bool ck_fix_runs(const unsigned long long* k0, unsigned long long* k1, uint32_t lo,
+                                            uint32_t L, uint32_t i, uint32_t step) {
+    bool ok = true;
+    for (; i < L; i += step) {
+        if (i > 0 && k0[lo + i] == k0[lo + i - 1] && (k1[lo + i] >> 56) == (k1[lo + i - 1] >> 56)) continue;
+        uint32_t e = i + 1;
+        while (e < L && k0[lo + e] == k0[lo + i] && (k1[lo + e] >> 56) == (k1[lo + i] >> 56)) ++e;
+        if (e - i > CK_RUN_MAX) {
+            ok = false;
+            continue;
+        }
+        for (uint32_t a = i + 1; a < e; ++a) {
+            const unsigned long long v = k1[lo + a];
+            uint32_t b = a;
+            for (; b > i && k1[lo + b - 1] > v; --b) k1[lo + b] = k1[lo + b - 1];
+            k1[lo + b] = v;
+        }
+    }
+    return ok;
+}
+
 // One wave sorts k0/k1[lo, lo+L), L <= 64R, by the compact key; false: the
 // run is left a permutation of itself and needs the full-key sort.
 template <int R>
@@ -2515,10 +2506,10 @@ __device__ bool ck_run_wave(unsigned long long* k0, unsigned long long* k1, uint
         const uint32_t i = lane * R + r;
         if (i > 0 && i < L) bad |= ck_order_bad(k0, k1, lo + i);
     }
-#ifdef DBI_X_CKSTAT
-    if (__ballot(bad) && lane == 0) atomicAdd(&g_ck_stat[2], 1u);
-#endif
-    return __ballot(bad) == 0;
+    if (__ballot(bad) == 0) return true;
+    const bool fixed = ck_fix_runs(k0, k1, lo, L, lane, 64);
+    wave_sync();
+    return __ballot(!fixed) == 0;
 }
 
 // compare-exchange with partner i ^ m across waves, through LDS scratch sc[0, L)
@@ -2618,10 +2609,9 @@ __device__ bool ck_run_block(unsigned long long* k0, unsigned long long* k1, uin
         const uint32_t i = i0 + r;
         if (i > 0 && i < L) bad |= ck_order_bad(k0, k1, lo + i);
     }
-#ifdef DBI_X_CKSTAT
-    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicAdd(&g_ck_stat[5], 1u);
-#endif
-    return !__syncthreads_or(bad);
+    if (!__syncthreads_or(bad)) return true;
+    const bool fixed = ck_fix_runs(k0, k1, lo, L, threadIdx.x, NT);
+    return !__syncthreads_or(!fixed);
 }
 
 // exclusive max of v over the block's lower threads (0 for thread 0)

@@ -332,8 +332,8 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
             if (bounded)
                 STAGE(h, "digest", by(1, 16, 0, 4, 0),
                       launch_digest_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
-                                            (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->status.p, h->epoch,
-                                            h->recA.p, cap, h->ctr.p, s));
+                                            (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->recA.p, cap, h->ctr.p,
+                                            s));
             else
                 STAGE(h, "digest", by(1, 16, 0, 4, 0),
                       launch_digest_fused(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,

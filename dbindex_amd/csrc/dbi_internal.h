@@ -154,7 +154,6 @@ struct Counters {
     unsigned long long n_unique;
     unsigned long long n_keys;
     unsigned long long n_keys_shard[8];  // per-XCD-group partial key counts (summed on readback)
-    unsigned long long n_slots;    // bounded digest: record slots reserved (kept + sentinels)
     unsigned int n_big;            // chunks above CHUNK_CAP (sorted by the 1024-thread LDS kernel)
     unsigned int n_mid;            // chunks with a bin above WAVE_SORT_MAX (block-level compact sort)
     unsigned int err;              // device error bits
@@ -166,7 +165,9 @@ struct Counters {
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads
     // (sharing the ticket's line cost the digest 30%)
-    alignas(256) unsigned int tile_ticket;  // k_digest_fused / k_digest_bounded: tiles in dispatch order
+    alignas(256) unsigned int tile_ticket;  // k_digest_fused: tiles in dispatch order
+    alignas(256) unsigned long long n_slots;  // k_digest_bounded: record slots reserved (kept + sentinels), the
+                                              // cursor every tile takes its output region from
     alignas(256) unsigned int max_plen;     // longest protein (k_tile_proteins): the record field width
 };
 constexpr unsigned ERR_LAYOUT = 1;  // 2*bits(longest protein) + bits(proteins) > 56
@@ -210,17 +211,17 @@ hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, co
                                const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                const uint32_t* d_tile_pf, unsigned long long* d_status, uint32_t epoch,
                                Rec* d_out, uint32_t cap, Counters* d_ctr, hipStream_t s);
-// Full-enzyme digest without mandatory residues in one walk: a start emits at
-// most max_missed + 2 records, so tile t reserves ncand_t * (max_missed + 2)
-// slots (decoupled look-back over the reservations), fills them in start order
-// and marks unused slots with REC_SENTINEL (q0 == ~0).  ctr->n_slots = slots
+// Full-enzyme digest without mandatory residues, <= 2 missed cleavages, in one
+// walk: each tile reserves the exact number of candidate ends of its starts
+// (mass filters only lower the real count) with one atomic add on
+// ctr->n_slots (tiles in arrival order), fills them in its own order and
+// marks unused slots with REC_SENTINEL (q0 == ~0).  ctr->n_slots = slots
 // reserved, ctr->n_kept = records kept; nothing is written when n_slots > cap
 // (the caller grows the buffer and runs it again).
 constexpr unsigned long long REC_SENTINEL = ~0ull;
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
-                                 const uint32_t* d_tile_pf, unsigned long long* d_status, uint32_t epoch,
-                                 Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s);
+                                 const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s);
 hipError_t launch_digest_emit(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                               const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
                               uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk_off, uint32_t* d_thr,

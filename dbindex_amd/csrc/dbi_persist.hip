@@ -192,8 +192,9 @@ int index_load(dbi_handle* h, const char* path, std::vector<uint8_t>* res_out, s
     // reads in queries and materialisation
     for (uint64_t i = 0; i < P; ++i)
         if (off[i + 1] < off[i]) return io_fail("corrupt offsets in index file", path);
-    if (hd.def_bytes && (doff[0] != 0 || doff[P] != hd.def_bytes)) return io_fail("corrupt definitions", path);
-    for (uint64_t i = 0; hd.def_bytes && i < P; ++i)
+    // definition offsets: monotone from 0 to def_bytes (all zero without definitions)
+    if (doff[0] != 0 || doff[P] != hd.def_bytes) return io_fail("corrupt definitions", path);
+    for (uint64_t i = 0; i < P; ++i)
         if (doff[i + 1] < doff[i]) return io_fail("corrupt definitions", path);
     if (occ_off[0] != 0 || occ_off[U] != K) return io_fail("corrupt occurrence offsets in index file", path);
     for (uint64_t u = 0; u < U; ++u) {

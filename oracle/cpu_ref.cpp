@@ -819,6 +819,9 @@ int oref_query_ranges(const oref_index* ix, const double* mass, const double* to
 }
 
 // IndexUtil.calculateMass(seq, h2o) (IndexUtil.java:197-208)
+// the formula mass the literal PTM walk adds (cut_seq_literal)
+double oref_formula_mass(const char* f, uint64_t len) { return formula_mass(std::string(f, len)); }
+
 double oref_calculate_mass(const dbi_params* p, const uint8_t* seq, uint64_t len) {
     double mass = 0;
     if (p->add_h2o_proton) mass += p->h2o_proton;

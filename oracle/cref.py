@@ -46,6 +46,8 @@ def lib():
         L.oref_unique.argtypes = [P, P, P, P, P, P, P]
         L.oref_query.argtypes = [P, ctypes.c_double, ctypes.c_double, P, ctypes.c_uint64, U64]
         L.oref_query_ranges.argtypes = [P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, U64]
+        L.oref_formula_mass.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+        L.oref_formula_mass.restype = ctypes.c_double
         L.oref_calculate_mass.argtypes = [P, P, ctypes.c_uint64]
         L.oref_calculate_mass.restype = ctypes.c_double
         L.oref_tolerance_in_dalton.argtypes = [ctypes.c_double, ctypes.c_double]
@@ -226,6 +228,12 @@ class Index:
         rc = lib().oref_query_batch(self.h, _ptr(m), _ptr(t), m.shape[0], _ptr(first), _ptr(count))
         assert rc == 0, "non-contiguous oracle result"
         return first, count
+
+
+def formula_mass(formula: str) -> float:
+    """The C++ oracle's FormulaCalculator restatement (NaN: unknown element)."""
+    b = formula.encode()
+    return lib().oref_formula_mass(b, len(b))
 
 
 def calculate_mass(cparams, seq: str) -> float:

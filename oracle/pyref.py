@@ -145,6 +145,38 @@ def peptide_tag(s: str) -> int:
     return (x >> 16) ^ (x & 0xFFFF)
 
 
+# FormulaCalculator.calculateMass (edu.scripps.yates.utilities, not vendored),
+# restated independently of oracle/cpu_ref.cpp and of the product: its own
+# element table (monoisotopic masses of the most abundant isotope, IUPAC /
+# NIST values), a regular-expression tokenizer, and the count x mass terms
+# summed left to right.  An element symbol without a mass, a sign without
+# digits or anything that is not "Symbol[-]digits*" is unknown: NaN.
+_ELEMENT_MONO = {
+    "H": 1.00782503207, "D": 2.0141017778, "B": 11.0093054, "C": 12.0, "N": 14.0030740048,
+    "O": 15.99491461956, "F": 18.99840322, "Na": 22.9897692809, "Mg": 23.9850417, "Si": 27.9769265325,
+    "P": 30.97376163, "S": 31.97207100, "Cl": 34.96885268, "K": 38.96370668, "Ca": 39.96259098,
+    "Li": 7.01600455, "Fe": 55.9349375, "Cu": 62.9295975, "Zn": 63.9291422, "Se": 79.9165213,
+    "Br": 78.9183371, "I": 126.904473, "Hg": 201.970643,
+}
+
+
+def formula_mass(formula: str) -> float:
+    import re
+    pos, mass = 0, 0.0
+    for m in re.finditer(r"([A-Z][a-z]*)(-?)([0-9]*)", formula):
+        if m.start() != pos:
+            return float("nan")
+        sym, neg, digits = m.groups()
+        if neg and not digits:
+            return float("nan")
+        if sym not in _ELEMENT_MONO:
+            return float("nan")
+        count = int(digits) if digits else 1
+        mass = mass + float(-count if neg else count) * _ELEMENT_MONO[sym]
+        pos = m.end()
+    return mass if pos == len(formula) else float("nan")
+
+
 def get_residues(offset: int, length: int, prot: str) -> Tuple[str, str]:
     """Util.getResidues (Util.java:130-162), including its right-flank quirk."""
     n = len(prot)

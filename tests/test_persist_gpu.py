@@ -60,15 +60,28 @@ def test_store_persist_and_reuse(tmp_path):
     def answers(ix):
         out = []
         for mm, tt in zip(m[:60], t[:60]):
-            out.append(sorted((s.getSequence(), tuple(sorted(p.getId() for p in ix.getProteins(s))))
+            out.append(sorted((s.getSequence(), tuple(sorted(set(p.getId() for p in ix.getProteins(s)))))
                               for s in ix.getSequencesUsingDaltonTolerance(float(mm), float(tt))))
         return out
+
+    # what the oracle answers: every unique peptide of the window, its proteins
+    u = oix.unique()
+    seqs = pp.sequences()
+    want = []
+    for mm, tt in zip(m[:60], t[:60]):
+        rows = []
+        for i in oix.query(float(mm), float(tt)):
+            p0, o, ln = int(u["prot_id"][i]), int(u["offset"][i]), int(u["length"][i])
+            prots = u["occ_prot"][u["occ_off"][i]:u["occ_off"][i + 1]]
+            rows.append((seqs[p0][o:o + ln], tuple(sorted(set(int(x) for x in prots)))))
+        want.append(sorted(rows))
+    assert sum(len(w) for w in want) > 0
 
     first = DBIndexer(prm, indexStore=DBIndexStoreHip(prm, persist=True), database_name=name)
     first.init()
     assert not first.indexStore.indexExists()
     first.run(pp)
-    want = answers(first)
+    assert answers(first) == want
     n_keys = first.getNumParentMasses()
     # a new process-like store with the same parameters finds the file and skips indexing
     second = DBIndexer(prm, indexStore=DBIndexStoreHip(prm, persist=True), database_name=name)
@@ -102,7 +115,7 @@ def test_unbucketed_or_filtered_index_is_not_saved(tmp_path):
 
 
 @pytest.mark.parametrize("damage", ["truncate", "grow", "header_n_unique", "header_def_bytes", "occ_off",
-                                    "mass_order", "prot_id", "occ_prot", "offset"])
+                                    "mass_order", "prot_id", "occ_prot", "offset", "def_off"])
 def test_damaged_index_file_is_refused(Engine, tmp_path, damage):
     """index_load checks the header against the file size before allocating and
     every content invariant of a build (occ_off monotone ending at n_kept,
@@ -139,6 +152,8 @@ def test_damaged_index_file_is_refused(Engine, tmp_path, damage):
         struct.pack_into("<I", raw, occ0 + 4 * (K - 1), 0xFFFFFFF0)
     elif damage == "offset":
         struct.pack_into("<I", raw, off0 + 4 * 7, 1 << 20)
+    elif damage == "def_off":  # definition offsets without definitions (def_bytes = 0)
+        struct.pack_into("<Q", raw, 128 + R + 8 * (P + 1) + 8 * (P // 2), 1000)
     open(path, "wb").write(bytes(raw))
     with Engine(cp) as b:
         with pytest.raises(_native.DBIndexStoreException):

@@ -235,3 +235,29 @@ def test_engine_ptm_text_is_not_rebuilt_or_digested_on_device():
         eng.build(plain)
         st = eng.rebuild()
         assert st.n_total == cref.Index(cp, plain.residues, plain.offsets).n_total
+
+
+def test_formula_mass_known_answers():
+    """The independent Python restatement of FormulaCalculator against sums
+    worked by hand (element masses written out), then the C++ oracle's
+    (which the device walk mirrors) against it: bit-identical."""
+    import math
+    from oracle import pyref
+    H, C, N, O, P = 1.00782503207, 12.0, 14.0030740048, 15.99491461956, 30.97376163
+    kat = {
+        "O": O,
+        "H2O": 2 * H + O,
+        "HPO3": ((H + P) + 3 * O),
+        "C2H3NO": (((2 * C) + 3 * H) + N) + O,
+        "H-2O-1": (-2 * H) + (-1 * O),
+        "CH2": C + 2 * H,
+        "C12": 12 * C,
+    }
+    for f, want in kat.items():
+        assert pyref.formula_mass(f) == want, f
+    for bad in ("Qx2", "2H", "O-", "h2o", "H2O]", "C2H3NO ", "Xx"):
+        assert math.isnan(pyref.formula_mass(bad)), bad
+    forms = list(kat) + ["Se", "NaCl", "C6H12O6", "C-2H-3", "Hg2Cl2", "SiO2", "H10", "D2O", "K1", "B4", "Zn0"]
+    for f in forms + ["Qx2", "2H", "O-"]:
+        a, b = pyref.formula_mass(f), cref.formula_mass(f)
+        assert (math.isnan(a) and math.isnan(b)) or np.float64(a).view(np.uint64) == np.float64(b).view(np.uint64), f
