@@ -183,7 +183,8 @@ def _fasta_items(fasta) -> List[Tuple[str, str]]:
         from .fasta import uniprot_header
         return [(fasta.defs[i] if fasta.defs else uniprot_header(i), fasta.sequence(i))
                 for i in range(fasta.n_proteins)]
-    if isinstance(fasta, str):
-        with open(fasta) as fh:
-            return list(iter_fasta(fh))
+    if isinstance(fasta, str):  # a FASTA file: the library's multi-threaded parser (dbi_fasta_read)
+        from .fasta import read_fasta
+        pp = read_fasta(fasta)
+        return [(pp.defs[i], pp.sequence(i)) for i in range(pp.n_proteins)]
     return list(fasta)
