@@ -1728,8 +1728,10 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits
 // the item loop.
 template <bool SPARSE, typename Digit>
 __global__ void __launch_bounds__(RADIX_THREADS)
-k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32_t* __restrict__ hist) {
+k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32_t* __restrict__ hist,
+             const unsigned long long* __restrict__ dn) {
     __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
+    if (dn) n = (uint32_t)min((unsigned long long)n, *dn);  // device-sized build: the count on the device
     const uint32_t D = 1u << bits;
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
@@ -1762,8 +1764,10 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
 // output (1 B per record instead of a 16-B record line): thread t of block b
 // counts records [b*RADIX_CHUNK + 8t, +8) (dense: every byte below n is a digit).
 __global__ void __launch_bounds__(RADIX_THREADS)
-k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t* __restrict__ hist) {
+k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t* __restrict__ hist,
+                const unsigned long long* __restrict__ dn) {
     __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
+    if (dn) n = (uint32_t)min((unsigned long long)n, *dn);
     const uint32_t D = 1u << bits;
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
@@ -1801,7 +1805,8 @@ k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t*
 template <bool SPARSE, typename Digit, bool NARROW = false>
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, Digit dig, int bits,
-                const uint32_t* __restrict__ offs, uint8_t* __restrict__ nd_out, int nshift, uint32_t nmask) {
+                const uint32_t* __restrict__ offs, uint8_t* __restrict__ nd_out, int nshift, uint32_t nmask,
+                const unsigned long long* __restrict__ dn) {
     static_assert(RADIX_D <= RADIX_THREADS, "one digit per thread");
     static_assert(RADIX_CHUNK <= 65535, "16-bit counts");
     __shared__ uint16_t cnt[RADIX_NW][RADIX_D];
@@ -1809,6 +1814,7 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
     __shared__ uint16_t sdig[RADIX_CHUNK];  // their digit | next pass's digit << 8 (computed once)
     __shared__ uint32_t gofs[RADIX_D];    // global position of digit d's first record - its local start
     __shared__ uint32_t s_tmp[RADIX_NW + 1];
+    if (dn) n = (uint32_t)min((unsigned long long)n, *dn);
     const uint32_t D = 1u << bits;
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
@@ -1894,49 +1900,50 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
 
 template <typename Digit>
 static hipError_t radix_hist(const Rec* d_in, uint32_t n, const Digit& dig, int bits, bool sparse, uint32_t* d_hist,
-                             hipStream_t s) {
+                             hipStream_t s, const unsigned long long* d_n = nullptr) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
     if (sparse)
-        DBI_LAUNCH((k_radix_hist<true, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, dig, bits, d_hist);
+        DBI_LAUNCH((k_radix_hist<true, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, dig, bits, d_hist, d_n);
     else
-        DBI_LAUNCH((k_radix_hist<false, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, dig, bits, d_hist);
+        DBI_LAUNCH((k_radix_hist<false, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, n, dig, bits, d_hist, d_n);
     return hipGetLastError();
 }
 
 template <typename Digit>
 static hipError_t radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const Digit& dig, int bits, bool sparse,
                                 const uint32_t* d_hist, hipStream_t s, uint8_t* nd_out = nullptr, int nshift = 0,
-                                int nbits = 0) {
+                                int nbits = 0, const unsigned long long* d_n = nullptr) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
     const uint32_t nmask = (1u << nbits) - 1;
     if (sparse)
         DBI_LAUNCH((k_radix_scatter<true, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, dig, bits,
-                   d_hist, nd_out, nshift, nmask);
+                   d_hist, nd_out, nshift, nmask, d_n);
     else
         DBI_LAUNCH((k_radix_scatter<false, Digit>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, d_out, n, dig, bits,
-                   d_hist, nd_out, nshift, nmask);
+                   d_hist, nd_out, nshift, nmask, d_n);
     return hipGetLastError();
 }
 
 hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,
-                             uint32_t* d_hist, hipStream_t s) {
-    return radix_hist(d_in, n, BinDigit{bm, shift, (1u << bits) - 1}, bits, sparse, d_hist, s);
+                             uint32_t* d_hist, hipStream_t s, const unsigned long long* d_n) {
+    return radix_hist(d_in, n, BinDigit{bm, shift, (1u << bits) - 1}, bits, sparse, d_hist, s, d_n);
 }
 
-hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint32_t* d_hist, hipStream_t s) {
+hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint32_t* d_hist, hipStream_t s,
+                                const unsigned long long* d_n) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
-    DBI_LAUNCH(k_radix_hist_u8, dim3(g), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist);
+    DBI_LAUNCH(k_radix_hist_u8, dim3(g), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist, d_n);
     return hipGetLastError();
 }
 
 hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
                                 bool sparse, const uint32_t* d_hist, hipStream_t s, uint8_t* d_next_dig,
-                                int next_shift, int next_bits) {
+                                int next_shift, int next_bits, const unsigned long long* d_n) {
     return radix_scatter(d_in, d_out, n, BinDigit{bm, shift, (1u << bits) - 1}, bits, sparse, d_hist, s, d_next_dig,
-                         next_shift, next_bits);
+                         next_shift, next_bits, d_n);
 }
 
 // owner partition of a sharded build: the same stable pass with digit = owner
@@ -1955,10 +1962,10 @@ hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, co
     const int bits = owner_bits(om.nshards);
     if (sparse)
         DBI_LAUNCH((k_radix_scatter<true, OwnerDigit, true>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, (void*)d_out,
-                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u);
+                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u, (const unsigned long long*)nullptr);
     else
         DBI_LAUNCH((k_radix_scatter<false, OwnerDigit, true>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, (void*)d_out,
-                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u);
+                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u, (const unsigned long long*)nullptr);
     return hipGetLastError();
 }
 
@@ -2226,9 +2233,10 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
 // thread per chunk: galloping, then binary search for the end of the bin that
 // straddles c*T — a few loads for ordinary bins, log steps for mass spikes).
 __global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap bm, uint32_t T, uint32_t nchunks,
-                               uint32_t* __restrict__ chunk_lo) {
+                               uint32_t* __restrict__ chunk_lo, const unsigned long long* __restrict__ dn) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c > nchunks) return;
+    if (dn) n = (uint32_t)min((unsigned long long)n, *dn);  // chunks past the records are empty
     const uint32_t x = c == nchunks ? n : min(c * T, n);
     if (x == 0 || x == n) {
         chunk_lo[c] = x;
@@ -2250,9 +2258,9 @@ __global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap 
 }
 
 hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,
-                               uint32_t* d_chunk_lo, hipStream_t s) {
+                               uint32_t* d_chunk_lo, hipStream_t s, const unsigned long long* d_n) {
     DBI_LAUNCH(k_chunk_bounds, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_recs, n, bm, T, nchunks,
-               d_chunk_lo);
+               d_chunk_lo, d_n);
     return hipGetLastError();
 }
 
@@ -3282,12 +3290,14 @@ hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t fa
 }
 
 // occ_off[U] = n_kept (U from the device counters)
-__global__ void k_write_tail(uint32_t* __restrict__ occ_off, uint32_t n_kept, const Counters* __restrict__ ctr) {
-    if (threadIdx.x == 0) occ_off[ctr->n_unique] = n_kept;
+__global__ void k_write_tail(uint32_t* __restrict__ occ_off, uint32_t n_kept, const Counters* __restrict__ ctr,
+                             const unsigned long long* __restrict__ dn) {
+    if (threadIdx.x == 0) occ_off[ctr->n_unique] = dn ? (uint32_t)*dn : n_kept;
 }
 
-hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s) {
-    DBI_LAUNCH(k_write_tail, dim3(1), dim3(64), 0, s, d_occ_off, n_kept, d_ctr);
+hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s,
+                             const unsigned long long* d_n) {
+    DBI_LAUNCH(k_write_tail, dim3(1), dim3(64), 0, s, d_occ_off, n_kept, d_ctr, d_n);
     return hipGetLastError();
 }
 

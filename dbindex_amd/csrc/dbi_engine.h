@@ -6,7 +6,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -15,6 +17,10 @@
 
 namespace dbi {
 
+// Bumped by every device (re)allocation: a captured build graph holds buffer
+// pointers, so it is replayed only while this has not moved.
+inline std::atomic<uint64_t> g_alloc_gen{0};
+
 // Growable device buffer.
 template <typename T>
 struct DevBuf {
@@ -22,6 +28,7 @@ struct DevBuf {
     size_t cap = 0;  // elements
     int ensure(size_t n) {
         if (n <= cap && p) return 0;
+        g_alloc_gen.fetch_add(1, std::memory_order_relaxed);
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -153,6 +160,8 @@ struct dbi_handle {
     uint64_t build_serial = 0, qdir_serial = 0;
     bool inputs_resident = false;       // res/poff hold the last host build's inputs (dbi_rebuild)
     bool inputs_ptm = false;            // ... and they carry inline '[formula]' PTMs (no dbi_rebuild)
+    bool hc_final = false;              // hc holds the counters after the build's last kernel
+    uint64_t last_kept = 0;             // the previous build's records (bins of a device-sized tail)
     DevBuf<double> q_mass, q_tol;
     DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
     DevBuf<uint32_t> h_nh, h_no, h_ids, h_hocc, h_prot;  // dbi_query_hits_device
@@ -190,6 +199,34 @@ struct dbi_handle {
     hipEvent_t evpool[2 * MAX_STAGES] = {};
     Stage stages[MAX_STAGES];
     int nstage = 0;
+
+    // The warm device-sized build (digest + tail, bounded digest) as one
+    // hipGraph: captured on the second warm build with the same key, replayed
+    // while the key holds.  The key is everything baked into the captured
+    // kernel arguments: inputs, sizes, buffers (g_alloc_gen), parameters,
+    // timing mode.
+    struct GraphKey {
+        const void* d_res = nullptr;
+        const void* d_poff = nullptr;
+        uint64_t n_res = 0, n_prot = 0, cap = 0, last_kept = 0, alloc_gen = 0, dp_gen = 0;
+        bool timing = false;
+        char timing_only[32] = {};
+        bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }
+    };
+    uint64_t dp_gen = 0;                  // bumped when dp changes (dbi_set_windows, bucket drop)
+    bool use_graph = true;                // DBI_BUILD_GRAPH=0: never
+    bool capturing = false;               // stage events become event nodes
+    GraphKey prev_key{};                  // the last plain warm build's key
+    bool prev_key_valid = false;
+    struct {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        GraphKey key{};
+        Stage stages[MAX_STAGES];
+        int nstage = 0;
+        uint64_t n_bins = 0, n_in = 0;
+        bool sparse = false;
+    } bgraph;
 };
 
 
@@ -211,16 +248,25 @@ inline int stage_begin(dbi_handle* h, const char* name, Bytes b) {
     st.c0 = 0;
     st.bytes = 0;
     st.launched = false;
-    if (h->timing && (h->timing_only.empty() || h->timing_only == name))
-        t_launch_ev = LaunchEvents{h->evpool[st.eb], h->evpool[st.ee]};
-    else
-        t_launch_ev = LaunchEvents{};
+    t_launch_ev = LaunchEvents{};
+    if (h->timing && (h->timing_only.empty() || h->timing_only == name)) {
+        if (h->capturing) {  // a graph: event-record nodes around the stage's kernels
+            st.launched = hipEventRecord(h->evpool[st.eb], h->stream) == hipSuccess;
+        } else {             // events in the kernels' own dispatch packets
+            t_launch_ev = LaunchEvents{h->evpool[st.eb], h->evpool[st.ee]};
+        }
+    }
     return i;
 }
 
 inline void stage_end(dbi_handle* h, int i) {
-    // the first launch of the stage consumed `start`: otherwise nothing ran
-    if (i >= 0) h->stages[i].launched = t_launch_ev.stop != nullptr && t_launch_ev.start == nullptr;
+    if (i >= 0 && h->capturing) {
+        auto& st = h->stages[i];
+        if (st.launched) st.launched = hipEventRecord(h->evpool[st.ee], h->stream) == hipSuccess;
+    } else if (i >= 0) {
+        // the first launch of the stage consumed `start`: otherwise nothing ran
+        h->stages[i].launched = t_launch_ev.stop != nullptr && t_launch_ev.start == nullptr;
+    }
     t_launch_ev = LaunchEvents{};
 }
 
@@ -244,8 +290,9 @@ int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot);
 int prepare_tiles(dbi_handle* h);
 // digest of h->d_res / h->d_poff into recA: *n records (*n_in slots, REC_SENTINEL
 // in the unused ones when *sparse)
-int run_digest(dbi_handle* h, uint64_t* n, uint64_t* n_in, bool* sparse);
-int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse);
+int run_digest(dbi_handle* h, uint64_t* n, uint64_t* n_in, bool* sparse, bool* dev_sized = nullptr);
+int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
+               const unsigned long long* d_n_in = nullptr, const unsigned long long* d_n = nullptr, uint64_t n_est = 0);
 int ensure_qdir(dbi_handle* h, hipStream_t s);  // query directory of the current index
 int finish_build(dbi_handle* h);
 

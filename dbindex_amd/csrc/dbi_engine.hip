@@ -125,18 +125,24 @@ const char* ptm_device_msg() {
 int read_counters(dbi_handle* h) {
     DBI_HIP(hipMemcpyAsync(&h->hc, h->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, h->stream));
     DBI_HIP(hipStreamSynchronize(h->stream));
+    h->hc_final = false;
     return 0;
 }
 
 // Steps 4-6 over n records in recA: partition by mass bin, per-bin sort +
 // dedup, finalize.  lo/hi bound every record mass.  sparse: recA holds n_in
 // slots, n of them records and the rest REC_SENTINEL (bounded digest); the
-// first radix pass leaves the sentinels behind.
-int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse) {
+// first radix pass leaves the sentinels behind.  Device-sized (d_n_in / d_n
+// set: the counts the digest left on the device): n_in and n are upper bounds
+// that size the grids and buffers, every kernel reads the real count itself,
+// and n_est (the previous build's count) chooses the bins -- no host sync
+// between the digest and the tail.
+int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
+               const unsigned long long* d_n_in, const unsigned long long* d_n, uint64_t n_est) {
     hipStream_t s = h->stream;
     int rc;
     const uint32_t n32 = (uint32_t)n;
-    const uint32_t nbins = choose_nbins(n, h->bin_bits_max);
+    const uint32_t nbins = choose_nbins(d_n && n_est ? std::min(n_est, n) : n, h->bin_bits_max);
     const BinMap bm = make_binmap(lo, hi, nbins);
     int width[8] = {};
     const int passes = radix_plan(nbins, sparse, width);
@@ -172,11 +178,13 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
         const bool sp = sparse && ps == 0;
         const uint32_t nin = sp ? n_in32 : n32;
         const double hbytes = 8.0 * (double)radix_blocks(nin) * (double)(1u << bits);  // hist write + scan
+        const unsigned long long* dn = sp ? d_n_in : d_n;
         if (ps == 0) {                   // the 8-B mass of every record
-            STAGE(h, "radix_hist", by(0, 8, 0, 0, 0), launch_radix_hist(src, nin, bm, shift, bits, sp, h->hist.p, s));
+            STAGE(h, "radix_hist", by(0, 8, 0, 0, 0),
+                  launch_radix_hist(src, nin, bm, shift, bits, sp, h->hist.p, s, dn));
         } else {                         // the digit bytes of the previous pass
             STAGE(h, "radix_hist", by(0, 1, 0, 0, 0),
-                  launch_radix_hist_u8(h->digits.p, nin, bits, h->hist.p, s));
+                  launch_radix_hist_u8(h->digits.p, nin, bits, h->hist.p, s, dn));
         }
         STAGE(h, "radix_scan", by(0, 0, 0, 0, 0),
               launch_scan_u32(h->hist.p, h->hist.p, (uint64_t)radix_blocks(nin) << bits, h->scan_tmp.p,
@@ -187,14 +195,14 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
         const int nbits = more ? width[ps + 1] : 0;
         STAGE(h, "radix_scatter", by(0, more ? 33 : 32, 0, 0, 0),
               launch_radix_scatter(src, dst, nin, bm, shift, bits, sp, h->hist.p, s, more ? h->digits.p : nullptr,
-                                   shift + bits, nbits));
+                                   shift + bits, nbits, dn));
         std::swap(src, dst);
         shift += bits;
     }
     // src: records grouped by bin, insertion order inside each bin
     // chunk sort: 16 B in + 16 B out per record (+ the residues of every peptide for its hash)
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
-          launch_chunk_bounds(src, n32, bm, T, nchunks, h->chunk_lo.p, s));
+          launch_chunk_bounds(src, n32, bm, T, nchunks, h->chunk_lo.p, s, d_n));
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                             h->mid_list.p, h->ctr.p, s));
@@ -218,13 +226,13 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     STAGE(h, "finalize", by(0, 20, 24, 0, 0),
           launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p,
                           h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor, h->ctr.p, s));
-    DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s));
+    DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s, d_n));
     h->stats.n_bins = nbins;
     return 0;
 }
 
 int finish_build(dbi_handle* h) {
-    int rc = read_counters(h);
+    int rc = h->hc_final ? 0 : read_counters(h);  // a device-sized build has read them after its last kernel
     if (rc) return rc;
     if (h->hc.err & ERR_SEGS) return set_error(DBI_E_STATE, "internal: giant-chunk segment list overflow");
     if (h->hc.err & ERR_SLOTS) return set_error(DBI_E_STATE, "internal: digest slot bound exceeded");
@@ -289,6 +297,7 @@ int finish_build(dbi_handle* h) {
     bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes();
     st.device_bytes = bytes;
     h->built = true;
+    h->last_kept = st.n_kept;
     ++h->build_serial;
     return 0;
 }
@@ -305,7 +314,10 @@ int prepare_tiles(dbi_handle* h) {
 }
 
 // Device digest over residues at d_res (n_res) with u32 offsets at h->d_poff.
-int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_out) {
+// Warm builds with dev_sized: the digest into the previous build's capacity,
+// and no host sync: *n = *n_in = that capacity (upper bounds), *dev_sized set;
+// the caller checks the real need once the whole build has run (build_digest).
+int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_out, bool* dev_sized) {
     hipStream_t s = h->stream;
     int rc;
     const uint64_t R = h->n_res;
@@ -316,15 +328,16 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
     if ((rc = prepare_tiles(h))) return rc;
     uint64_t n;
     // full enzyme, no mandatory residues, <= 2 missed cleavages: one walk into
-    // bounded per-tile reservations (<= 4 slots per cleavage-site start)
+    // per-tile reservations of exactly each start's candidate ends
     const bool bounded = !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2 && !h->dp.filter;
     if (h->recA.cap >= 1024) {
         // warm: one pass into the capacity of the previous build; the exact
         // need comes back with the counters, and a short buffer is grown and
         // the pass run again
-        if ((rc = h->status.ensure_zeroed(nblk, s))) return rc;
+        if (!bounded && (rc = h->status.ensure_zeroed(nblk, s))) return rc;
+        const bool dev = dev_sized != nullptr;
         for (int attempt = 0;; ++attempt) {
-            if (++h->epoch >= 0xFFFFu) {
+            if (!bounded && ++h->epoch >= 0xFFFFu) {
                 DBI_HIP(hipMemsetAsync(h->status.p, 0, sizeof(unsigned long long) * h->status.cap, s));
                 h->epoch = 1;
             }
@@ -339,6 +352,13 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
                       launch_digest_fused(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
                                           (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->status.p, h->epoch,
                                           h->recA.p, (uint32_t)cap, h->ctr.p, s));
+            if (dev) {  // no sync: the tail runs on device counts, checked after the build
+                *n_out = cap;
+                *n_in_out = cap;
+                *sparse_out = bounded;
+                *dev_sized = true;
+                return 0;
+            }
             if ((rc = read_counters(h))) return rc;
             n = h->hc.n_kept;
             const uint64_t need = bounded ? h->hc.n_slots : n;
@@ -380,12 +400,117 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
     return 0;
 }
 
-int build_digest(dbi_handle* h) {
-    uint64_t n = 0, n_in = 0;
-    bool sparse = false;
-    int rc = run_digest(h, &n, &n_in, &sparse);
+dbi_handle::GraphKey graph_key(const dbi_handle* h) {
+    dbi_handle::GraphKey k{};
+    k.d_res = h->d_res;
+    k.d_poff = h->d_poff;
+    k.n_res = h->n_res;
+    k.n_prot = h->n_prot;
+    k.cap = h->recA.cap;
+    k.last_kept = h->last_kept;
+    k.alloc_gen = g_alloc_gen.load(std::memory_order_relaxed);
+    k.dp_gen = h->dp_gen;
+    k.timing = h->timing;
+    std::strncpy(k.timing_only, h->timing_only.c_str(), sizeof(k.timing_only) - 1);
+    return k;
+}
+
+void drop_graph(dbi_handle* h) {
+    if (h->bgraph.exec) (void)hipGraphExecDestroy(h->bgraph.exec);
+    if (h->bgraph.graph) (void)hipGraphDestroy(h->bgraph.graph);
+    h->bgraph.exec = nullptr;
+    h->bgraph.graph = nullptr;
+}
+
+// digest + tail of a warm device-sized build, enqueued (or captured)
+int warm_body(dbi_handle* h, uint64_t* n_in, bool* sparse) {
+    uint64_t n = 0;
+    bool dev = false;
+    int rc = run_digest(h, &n, n_in, sparse, &dev);
     if (rc) return rc;
-    return build_tail(h, n, h->params.min_mh, h->params.max_mh, n_in, sparse);
+    if (!dev) return set_error(DBI_E_STATE, "internal: warm build without device sizing");
+    const unsigned long long* d_kept = &h->ctr.p->n_kept;
+    return build_tail(h, n, h->params.min_mh, h->params.max_mh, *n_in, *sparse,
+                      *sparse ? &h->ctr.p->n_slots : d_kept, d_kept, h->last_kept);
+}
+
+int build_digest(dbi_handle* h) {
+    for (int attempt = 0;; ++attempt) {
+        const bool warm = h->recA.cap >= 1024;
+        uint64_t n_in = 0;
+        bool sparse = false;
+        int rc;
+        if (!warm) {  // cold: the host-sized count / emit build
+            uint64_t n = 0;
+            if ((rc = run_digest(h, &n, &n_in, &sparse, nullptr))) return rc;
+            return build_tail(h, n, h->params.min_mh, h->params.max_mh, n_in, sparse);
+        }
+        // graphs for the bounded digest's builds, untimed or timing one stage
+        // (every stage timed: events in the dispatch packets, no graph)
+        const bool bounded = !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2 && !h->dp.filter &&
+                             !(h->timing && h->timing_only.empty());
+        const dbi_handle::GraphKey key = graph_key(h);
+        if (bounded && h->use_graph && attempt == 0 && h->bgraph.exec && h->bgraph.key == key) {
+            // replay the captured build; its host-side results come with it
+            DBI_HIP(hipGraphLaunch(h->bgraph.exec, h->stream));
+            h->nstage = h->bgraph.nstage;
+            std::copy(h->bgraph.stages, h->bgraph.stages + h->bgraph.nstage, h->stages);
+            h->stats.n_bins = h->bgraph.n_bins;
+            n_in = h->bgraph.n_in;
+            sparse = h->bgraph.sparse;
+        } else if (bounded && h->use_graph && attempt == 0 && h->prev_key_valid && h->prev_key == key) {
+            // the same build as last time: capture it, then run the graph
+            drop_graph(h);
+            DBI_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+            h->capturing = true;
+            rc = warm_body(h, &n_in, &sparse);
+            h->capturing = false;
+            hipGraph_t g = nullptr;
+            const hipError_t ec = hipStreamEndCapture(h->stream, &g);
+            if (rc || ec != hipSuccess) {
+                if (g) (void)hipGraphDestroy(g);
+                return rc ? rc : hip_fail(ec, "hipStreamEndCapture");
+            }
+            hipGraphExec_t ex = nullptr;
+            const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+            if (ei != hipSuccess) {
+                (void)hipGraphDestroy(g);
+                return hip_fail(ei, "hipGraphInstantiate");
+            }
+            DBI_HIP(hipGraphLaunch(ex, h->stream));
+            h->bgraph.graph = g;
+            h->bgraph.exec = ex;
+            h->bgraph.key = key;
+            h->bgraph.nstage = h->nstage;
+            std::copy(h->stages, h->stages + h->nstage, h->bgraph.stages);
+            h->bgraph.n_bins = h->stats.n_bins;
+            h->bgraph.n_in = n_in;
+            h->bgraph.sparse = sparse;
+            if (graph_key(h).alloc_gen != key.alloc_gen) drop_graph(h);  // buffers moved while capturing: once only
+        } else {
+            if ((rc = warm_body(h, &n_in, &sparse))) return rc;
+            h->prev_key = graph_key(h);
+            h->prev_key_valid = bounded;
+        }
+        // the one host sync of a warm build: did the digest fit the capacity?
+        if ((rc = read_counters(h))) return rc;
+        const uint64_t need = sparse ? h->hc.n_slots : h->hc.n_kept;
+        if (need >= (1ull << 32) - 1)
+            return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences (or bounded-digest slots) on "
+                                            "one device: shard the FASTA");
+        if (need <= n_in) {
+            h->hc_final = true;
+            return 0;
+        }
+        if (attempt > 0) return set_error(DBI_E_STATE, "digest output grew between identical passes");
+        // grown: everything again into the bigger buffer (counters back to
+        // zero, except the record layout; the stage table restarts)
+        drop_graph(h);
+        h->prev_key_valid = false;
+        if ((rc = h->recA.ensure(need + need / 8))) return rc;
+        DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), h->stream));
+        h->nstage = 0;
+    }
 }
 
 int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
@@ -399,6 +524,7 @@ int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
     h->n_total_extra = 0;
     std::memset(&h->stats, 0, sizeof(h->stats));
     h->nstage = 0;
+    h->hc_final = false;
     h->t0 = std::chrono::steady_clock::now();
     DBI_HIP(hipMemsetAsync(h->ctr.p, 0, sizeof(Counters), h->stream));
     return 0;
@@ -573,7 +699,7 @@ int build_with_ptms(dbi_handle* h, const uint8_t* residues, uint64_t n_res, cons
     std::swap(h->mass_tab, h->mass_tab_x);
     uint64_t n = 0, n_in = 0;
     bool sparse = false;
-    rc = run_digest(h, &n, &n_in, &sparse);
+    rc = run_digest(h, &n, &n_in, &sparse, nullptr);
     std::swap(h->mass_tab, h->mass_tab_x);
     h->dp.cut_count = cut_count;
     h->d_res = o_res;
@@ -754,6 +880,7 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     if (const char* ev = std::getenv("DBI_BIN_BITS_MAX")) h->bin_bits_max = std::max(1, std::min(32, std::atoi(ev)));
     if (const char* ev = std::getenv("DBI_SPLIT_ABOVE")) h->split_above = (uint32_t)std::max(1, std::atoi(ev));
     if (const char* ev = std::getenv("DBI_CHUNK_T")) h->chunk_t = (uint32_t)std::max(64, std::min(CHUNK_CAP, std::atoi(ev)));
+    if (const char* ev = std::getenv("DBI_BUILD_GRAPH")) h->use_graph = std::atoi(ev) != 0;
     auto fail = [&](int code) {
         dbi_close(h);
         return code;
@@ -802,6 +929,7 @@ void dbi_close(dbi_handle* h) {
     h->h_row.release(); h->h_orow.release(); h->h_sums.release(); h->kr_scratch.release();
     h->r_mass.release(); h->r_pid.release(); h->r_off.release(); h->r_len.release(); h->r_occ_off.release();
     h->r_occ.release();
+    drop_graph(h);
     for (auto& ev : h->evpool)
         if (ev) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1147,6 +1275,7 @@ int dbi_set_bucket_drop(dbi_handle* h, int on) {
                                         "max precursor mass must be < 65536 Da");
     h->dp.buckets = on ? 1 : 0;
     h->dp.drop_mass = on ? (double)(h->dp.nb * h->dp.br) : INFINITY;
+    ++h->dp_gen;
     h->built = false;  // an index built under the other setting no longer answers
     return 0;
 }
@@ -1155,6 +1284,7 @@ int dbi_set_windows(dbi_handle* h, const double* mass, const double* tol, uint64
     if (!h || (n && on && (!mass || !tol))) return set_error(DBI_E_INVALID, "NULL argument");
     if (on && h->dp.buckets) return set_error(DBI_E_STATE, "a window filter needs the bucket drop off");
     h->built = false;
+    ++h->dp_gen;
     if (!on) {
         h->dp.filter = 0;
         h->dp.n_win = 0;

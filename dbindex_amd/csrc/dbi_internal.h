@@ -263,14 +263,17 @@ struct RouteMap {
     int32_t nb, br;  // NUM_BUCKETS / BUCKET_MASS_RANGE: windows past the last bucket are empty
 };
 // sparse: the input holds REC_SENTINEL slots (bounded digest), left out of the output
+// d_n (optional, every launcher below): the real count on the device, n its
+// upper bound (a device-sized build sizes its grids by capacity)
 hipError_t launch_radix_hist(const Rec* d_in, uint32_t n, const BinMap& bm, int shift, int bits, bool sparse,
-                             uint32_t* d_hist, hipStream_t s);
+                             uint32_t* d_hist, hipStream_t s, const unsigned long long* d_n = nullptr);
 // d_next_dig (optional): the record's digit of the next pass, one byte per
 // output position, counted by launch_radix_hist_u8 instead of re-reading records
 hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const BinMap& bm, int shift, int bits,
                                 bool sparse, const uint32_t* d_hist, hipStream_t s, uint8_t* d_next_dig = nullptr,
-                                int next_shift = 0, int next_bits = 0);
-hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint32_t* d_hist, hipStream_t s);
+                                int next_shift = 0, int next_bits = 0, const unsigned long long* d_n = nullptr);
+hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint32_t* d_hist, hipStream_t s,
+                                const unsigned long long* d_n = nullptr);
 uint64_t radix_blocks(uint32_t n);
 // stable partition pass by owner shard (digit = OwnerDigit), global protein ids out
 hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bool sparse, uint32_t* d_hist,
@@ -315,7 +318,7 @@ hipError_t launch_max_plen(const uint32_t* d_poff, uint32_t n_prot, Counters* d_
 size_t radix_hist_elems(uint32_t n, int bits);
 // chunk_lo[c] = first bin start at or after c*T in the bin-sorted records (nchunks+1 entries)
 hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,
-                               uint32_t* d_chunk_lo, hipStream_t s);
+                               uint32_t* d_chunk_lo, hipStream_t s, const unsigned long long* d_n = nullptr);
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                              uint32_t* d_big_list, uint32_t* d_mid_list, Counters* d_ctr, hipStream_t s);
@@ -340,7 +343,8 @@ hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32
                            uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, Counters* d_ctr, hipStream_t s);
 hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t factor, uint32_t* d_flags,
                             hipStream_t s);
-hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s);
+hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s,
+                             const unsigned long long* d_n = nullptr);
 hipError_t launch_hbm_copy(const void* d_in, void* d_out, uint64_t n16, hipStream_t s);
 hipError_t launch_gather(const uint64_t* d_ids, uint64_t n, const double* d_umass, const uint32_t* d_upid,
                          const uint32_t* d_uoff, const uint32_t* d_ulen, const uint32_t* d_occ_off,

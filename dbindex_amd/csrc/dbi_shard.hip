@@ -382,7 +382,7 @@ int dbi_shard_digest(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const 
     uint64_t n = 0, n_in = 0;
     bool sparse = false;
     if (h->n_res > 0) {
-        if ((rc = run_digest(h, &n, &n_in, &sparse))) return rc;
+        if ((rc = run_digest(h, &n, &n_in, &sparse, nullptr))) return rc;
     } else if ((rc = read_counters(h))) {
         return rc;
     }

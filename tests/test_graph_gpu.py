@@ -1,0 +1,73 @@
+"""GPU: the warm device-sized build and its hipGraph replay.
+
+A warm build runs the digest and the whole tail on the counts the digest left
+on the device (one host sync, after the last kernel); the second identical
+warm build of a bounded digest is captured as a hipGraph and every later one
+replays it.  Every build of these sequences must equal the oracle: plain,
+capture, replays, a different proteome in between (new key: plain again), a
+bigger one (the reservation grows: the build is redone), timing of one stage
+(event nodes in the graph) and the graph switched off (DBI_BUILD_GRAPH=0 is
+read at dbi_open)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from dbindex_amd import fasta
+from dbindex_amd.params import DBIndexSearchParams
+from oracle import cref
+from tests.helpers import assert_index_equal, assert_queries_equal, query_masses
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    from dbindex_amd import _native
+    from dbindex_amd._native import DeviceBuffer, synchronize
+    from dbindex_amd.engine import Engine
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    return Engine, DeviceBuffer, synchronize
+
+
+def _dev(env, pp):
+    _, DeviceBuffer, synchronize = env
+    d_res = DeviceBuffer.from_numpy(np.concatenate([pp.residues, np.zeros(16, np.uint8)]), 0)
+    d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), 0)
+    synchronize(0)
+    return d_res, d_off
+
+
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_warm_builds_and_graph_replays_match_oracle(env, monkeypatch, graph):
+    monkeypatch.setenv("DBI_BUILD_GRAPH", graph)
+    Engine = env[0]
+    hum = fasta.config("human")
+    a, b = hum.slice(0, 6000), hum.slice(6000, 9000)
+    big = hum.slice(0, 14000)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oa, ob, obig = (cref.Index(cp, p.residues, p.offsets) for p in (a, b, big))
+    bufs = {id(p): _dev(env, p) for p in (a, b, big)}
+
+    def build(eng, p):
+        d_res, d_off = bufs[id(p)]
+        return eng.build_device(d_res.ptr, p.n_residues, d_off.ptr, p.n_proteins)
+
+    with Engine(cp) as eng:
+        eng.set_timing(False)
+        seq = [a, a, a, a, a, b, b, b, a, a, big, big, big, a]
+        want = {id(a): oa, id(b): ob, id(big): obig}
+        for k, p in enumerate(seq):
+            st = build(eng, p)
+            assert st.n_total == want[id(p)].n_total, k
+            assert_index_equal(eng, want[id(p)], f"graph={graph} build {k}")
+        m, t = query_masses(oa, 3000, seed=21)
+        assert_queries_equal(eng, oa, m, t, f"graph={graph} queries after replays")
+        # one stage timed: event nodes inside the graph
+        eng.set_timing(True, only="digest")
+        for k in range(4):
+            build(eng, a)
+            assert_index_equal(eng, oa, f"graph={graph} timed build {k}")
+            times = {name: ms for name, ms, _ in eng.stage_times()}
+            assert times.get("digest", 0.0) > 0.0 and times.get("radix_scatter", 0.0) == 0.0
