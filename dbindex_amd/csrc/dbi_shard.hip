@@ -46,6 +46,12 @@ struct dbi_comm {
     unsigned long long* d_flag = nullptr;  // failure agreement (agree())
     hipStream_t stream = nullptr;          // host-buffer collectives (dbi_comm_allreduce_*)
     double* d_red = nullptr;               // their staging (COMM_RED_MAX values)
+    // the sharded build's small collectives (sample blocks, count matrix,
+    // totals) stage through these, allocated with the communicator: a rank
+    // never fails an allocation between two collectives of a build
+    double* d_samp = nullptr;              // nranks x (DBI_SHARD_SAMPLES + 2)
+    unsigned long long* d_cnt = nullptr;   // nranks x cnt_row
+    int cnt_row = 0;                       // max(nranks + 2, 6)
 };
 constexpr uint32_t COMM_RED_MAX = 4096;
 
@@ -166,21 +172,19 @@ int agree(dbi_comm* c, int rc, hipStream_t s, bool* any) {
     return 0;
 }
 
-// all[i * n + j] = mine_i[j] of every rank i (u64 all-gather through h->xcount),
+// all[i * n + j] = mine_i[j] of every rank i (u64 all-gather through c->d_cnt),
 // with each rank's status (rc != 0) in a last column: *any_failed
 int nccl_count_matrix(dbi_handle* h, dbi_comm* c, const std::vector<uint64_t>& mine, int status,
                       std::vector<uint64_t>& all, bool* any_failed) {
     const int n = c->nranks, me = c->rank, w = n + 1;
     hipStream_t s = h->stream;
-    int rc;
-    if ((rc = h->xcount.ensure((size_t)n * w + 8))) return rc;
     std::vector<uint64_t> full((size_t)n * w, 0);
     for (int j = 0; j < n && j < (int)mine.size(); ++j) full[(size_t)me * w + j] = mine[j];
     full[(size_t)me * w + n] = status ? 1u : 0u;
-    DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * w, full.data() + (size_t)me * w, sizeof(uint64_t) * w,
+    DBI_HIP(hipMemcpyAsync(c->d_cnt + (size_t)me * w, full.data() + (size_t)me * w, sizeof(uint64_t) * w,
                            hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * w, h->xcount.p, w, ncclUint64, c->comm, s));
-    DBI_HIP(hipMemcpyAsync(full.data(), h->xcount.p, sizeof(uint64_t) * n * w, hipMemcpyDeviceToHost, s));
+    DBI_NCCL(ncclAllGather(c->d_cnt + (size_t)me * w, c->d_cnt, w, ncclUint64, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(full.data(), c->d_cnt, sizeof(uint64_t) * n * w, hipMemcpyDeviceToHost, s));
     DBI_HIP(hipStreamSynchronize(s));
     all.assign((size_t)n * n, 0);
     *any_failed = false;
@@ -867,7 +871,10 @@ int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_co
         delete c;
         return set_error(DBI_E_OOM, "hipMalloc (communicator status word)");
     }
+    c->cnt_row = std::max(nranks + 2, 6);
     if (hipMalloc((void**)&c->d_red, COMM_RED_MAX * sizeof(double)) != hipSuccess ||
+        hipMalloc((void**)&c->d_samp, sizeof(double) * (size_t)nranks * (NS + 2)) != hipSuccess ||
+        hipMalloc((void**)&c->d_cnt, sizeof(unsigned long long) * (size_t)nranks * c->cnt_row) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         dbi_comm_destroy(c);
         return set_error(DBI_E_HIP, "communicator stream / staging buffer");
@@ -889,6 +896,8 @@ void dbi_comm_destroy(dbi_comm* c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->d_flag) (void)hipFree(c->d_flag);
     if (c->d_red) (void)hipFree(c->d_red);
+    if (c->d_samp) (void)hipFree(c->d_samp);
+    if (c->d_cnt) (void)hipFree(c->d_cnt);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -954,11 +963,59 @@ int dbi_comm_allgatherv(dbi_comm* c, const void* d_send, void* d_recv, const uin
     return 0;
 }
 
+}  // extern "C"
+
+namespace dbi {
+namespace {
+// One rank owning the whole proteome: its owner slice is the whole index and
+// every record would be routed to itself, so the sharded build is the
+// single-device build (digest, one sort, finalise; no sample gather,
+// partition, exchange or second sort; warm builds replay its graph) plus the
+// shard bookkeeping the routed queries and the replica read.
+int build_single_owner(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_poff, uint64_t n_prot) {
+    const double t0 = now_ms();
+    int rc;
+    if ((rc = dbi_build_device(h, d_res, n_res, d_poff, n_prot, nullptr))) return rc;
+    ShardState& sh = h->shard;
+    sh = ShardState{};
+    sh.rank = 0;
+    sh.nshards = 1;
+    sh.p_end = n_prot;
+    sh.n_res_global = n_res;
+    sh.n_prot_global = n_prot;
+    sh.d_res_global = d_res;
+    sh.n_total = h->stats.n_total;
+    sh.n_dropped = h->stats.n_dropped;
+    sh.n_digest = sh.n_recv = h->stats.n_kept;
+    sh.send_count.assign(1, sh.n_recv);
+    sh.send_off.assign(1, 0);
+    sh.recv_count.assign(1, sh.n_recv);
+    sh.ms_merge = now_ms() - t0;
+    sh.u_base = 0;
+    sh.u_base_known = true;
+    sh.global.g_total = h->stats.n_total;
+    sh.global.g_dropped = h->stats.n_dropped;
+    sh.global.g_kept = h->stats.n_kept;
+    sh.global.g_unique = h->stats.n_unique;
+    sh.global.g_keys = h->stats.n_keys;
+    sh.phase = 4;
+    return 0;
+}
+}  // namespace
+}  // namespace dbi
+
+extern "C" {
+
 int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_poff,
                       uint64_t n_prot, uint64_t p_begin, uint64_t p_end) {
     if (!h || !c) return set_error(DBI_E_INVALID, "NULL argument");
     if (c->device != h->device) return set_error(DBI_E_INVALID, "communicator and engine on different devices");
     const int n = c->nranks, me = c->rank;
+    // DBI_SHARD_FULL_PATH=1: one rank takes the general path too (tests of the
+    // partition / exchange / agreement code at N=1)
+    const char* full_path = std::getenv("DBI_SHARD_FULL_PATH");
+    if (n == 1 && p_begin == 0 && p_end == n_prot && !(full_path && full_path[0] == '1'))
+        return build_single_owner(h, d_res, n_res, d_poff, n_prot);
     int rc;
     // a rank that fails locally still takes part in the next collective, with
     // its status, so that every rank returns an error (never a hang)
@@ -973,8 +1030,7 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // its status; the sample weight (records per valid sample) on the host
     const size_t blk = NS + 2;
     int rc_local = rc_digest;
-    if ((rc = h->samp.ensure((size_t)n * blk))) return rc;
-    double* my_blk = h->samp.p + (size_t)me * blk;
+    double* my_blk = c->d_samp + (size_t)me * blk;
     if (!rc_local) {
         if ((rc = launch_sample_masses(h->recA.p, sh.n_in, NS, my_blk, s)) != hipSuccess)
             rc_local = hip_fail((hipError_t)rc, "launch_sample_masses");
@@ -984,8 +1040,8 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     samples[(size_t)me * blk + NS + 1] = rc_local ? 1.0 : 0.0;
     DBI_HIP(hipMemcpyAsync(my_blk + NS, &samples[(size_t)me * blk + NS], 2 * sizeof(double), hipMemcpyHostToDevice,
                            s));
-    DBI_NCCL(ncclAllGather(my_blk, h->samp.p, blk, ncclFloat64, c->comm, s));
-    DBI_HIP(hipMemcpyAsync(samples.data(), h->samp.p, sizeof(double) * n * blk, hipMemcpyDeviceToHost, s));
+    DBI_NCCL(ncclAllGather(my_blk, c->d_samp, blk, ncclFloat64, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(samples.data(), c->d_samp, sizeof(double) * n * blk, hipMemcpyDeviceToHost, s));
     DBI_HIP(hipStreamSynchronize(s));
     if (rc_local) return rc_local;
     std::vector<double> packed((size_t)n * (NS + 1));
@@ -1008,21 +1064,20 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // histogram, on the device) | its status | its receive capacity
     const double t0 = now_ms();
     const int w = n + 2;
-    if ((rc = h->xcount.ensure((size_t)n * w + 8))) return rc;
-    unsigned long long* my_row = h->xcount.p + (size_t)me * w;
+    unsigned long long* my_row = c->d_cnt + (size_t)me * w;
     if (!rc_part && sh.n_in > 0) {
         hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(64), 0, s, h->hist.p, sh.part_blocks, (uint32_t)n,
                            sh.n_digest, my_row);
         if ((rc = hipGetLastError()) != hipSuccess) rc_part = hip_fail((hipError_t)rc, "k_owner_counts");
-    } else if ((rc = hipMemsetAsync(my_row, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) {
-        return hip_fail((hipError_t)rc, "hipMemsetAsync");
+    } else if ((rc = hipMemsetAsync(my_row, 0, sizeof(unsigned long long) * n, s)) != hipSuccess && !rc_part) {
+        rc_part = hip_fail((hipError_t)rc, "hipMemsetAsync");
     }
     std::vector<unsigned long long> full((size_t)n * w, 0);
     full[(size_t)me * w + n] = rc_part ? 1u : 0u;
     full[(size_t)me * w + n + 1] = h->xrecv.cap;
     DBI_HIP(hipMemcpyAsync(my_row + n, &full[(size_t)me * w + n], 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllGather(my_row, h->xcount.p, w, ncclUint64, c->comm, s));
-    DBI_HIP(hipMemcpyAsync(full.data(), h->xcount.p, sizeof(unsigned long long) * n * w, hipMemcpyDeviceToHost, s));
+    DBI_NCCL(ncclAllGather(my_row, c->d_cnt, w, ncclUint64, c->comm, s));
+    DBI_HIP(hipMemcpyAsync(full.data(), c->d_cnt, sizeof(unsigned long long) * n * w, hipMemcpyDeviceToHost, s));
     DBI_HIP(hipStreamSynchronize(s));
     if (rc_part) return rc_part;
     std::vector<uint64_t> counts((size_t)n * n);
@@ -1080,14 +1135,13 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     std::vector<uint64_t> tot(5, 0);
     {
         const int wt = 6;
-        if ((rc = h->xcount.ensure((size_t)n * wt + 8))) return rc;
         std::vector<unsigned long long> row(wt, 0), rows((size_t)n * wt);
         row[0] = sh.n_total; row[1] = sh.n_dropped; row[2] = sh.n_recv; row[3] = h->stats.n_unique;
         row[4] = h->stats.n_keys;
         row[5] = rc_merge ? 1u : 0u;
-        DBI_HIP(hipMemcpyAsync(h->xcount.p + (size_t)me * wt, row.data(), sizeof(uint64_t) * wt, hipMemcpyHostToDevice, s));
-        DBI_NCCL(ncclAllGather(h->xcount.p + (size_t)me * wt, h->xcount.p, wt, ncclUint64, c->comm, s));
-        DBI_HIP(hipMemcpyAsync(rows.data(), h->xcount.p, sizeof(uint64_t) * n * wt, hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipMemcpyAsync(c->d_cnt + (size_t)me * wt, row.data(), sizeof(uint64_t) * wt, hipMemcpyHostToDevice, s));
+        DBI_NCCL(ncclAllGather(c->d_cnt + (size_t)me * wt, c->d_cnt, wt, ncclUint64, c->comm, s));
+        DBI_HIP(hipMemcpyAsync(rows.data(), c->d_cnt, sizeof(uint64_t) * n * wt, hipMemcpyDeviceToHost, s));
         DBI_HIP(hipStreamSynchronize(s));
         if (rc_merge) return rc_merge;
         sh.u_base = 0;

@@ -49,12 +49,20 @@ def swissprot():
     return fasta.config("swissprot", with_defs=False)
 
 
-def test_swissprot_full_tryptic(Engine, swissprot):
+@pytest.fixture(scope="module")
+def swissprot_oix(swissprot):
+    """The oracle's index of configs[2] (built once for the tests below)."""
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    with cref.threads(THREADS):
+        return cref.Index(cp, swissprot.residues, swissprot.offsets)
+
+
+def test_swissprot_full_tryptic(Engine, swissprot, swissprot_oix):
     """configs[2] at full size: 560k proteins, 201M residues, 54M peptides."""
     pp = swissprot
     cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = swissprot_oix
     with cref.threads(THREADS):
-        oix = cref.Index(cp, pp.residues, pp.offsets)
         m, t = query_masses(oix, 1_000_000)
         with Engine(cp) as eng:
             st = eng.build(pp)
@@ -64,6 +72,49 @@ def test_swissprot_full_tryptic(Engine, swissprot):
             # a second (warm, bounded-digest) build of the same input
             eng.build(pp)
             assert_index_equal(eng, oix, "swissprot tryptic mc2 [warm]")
+
+
+def test_swissprot_sharded_8_shards(Engine, swissprot, swissprot_oix):
+    """configs[2] in its sharded form: the whole proteome split by residues
+    into 8 protein ranges (8 handles on this GPU, dbi_shard_exchange_local:
+    the phases of an 8-rank dbi_build_sharded), every record routed to the
+    owner of its mass key and merged there (IndexMerge.getMergedData,
+    DBIndexStoreSQLiteByteIndexMerge.java:620-719, across shards); the owners'
+    slices concatenated equal the oracle's single index array for array, then
+    the replicated index (north star's all-gatherv) on every handle equals it
+    too and answers 200k queries."""
+    from dbindex_amd import _native, shard
+    pp = swissprot
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = swissprot_oix
+    o = oix.unique()
+    k = 8
+    d_res = _native.DeviceBuffer.from_numpy(np.concatenate([pp.residues, np.zeros(16, np.uint8)]), 0)
+    d_off = _native.DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), 0)
+    engines = [Engine(cp, 0) for _ in range(k)]
+    try:
+        for rep in ("cold", "warm"):
+            shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
+                                      shard.protein_ranges(pp.offsets, k))
+            sts = [shard.shard_stats(e) for e in engines]
+            assert sum(s.n_total for s in sts) == oix.n_total
+            assert sum(s.n_received for s in sts) == oix.n_kept
+            assert sum(s.n_unique for s in sts) == oix.n_unique and sum(s.n_keys for s in sts) == oix.n_keys
+            assert min(s.n_received for s in sts) > oix.n_kept // (2 * k)  # owners balanced by the splitters
+            g = shard.concat_exports([e.export() for e in engines])
+            assert np.array_equal(g["mass"].view(np.uint64), o["mass"].view(np.uint64)), rep
+            for key in ("prot_id", "offset", "length", "occ_off", "occ_prot"):
+                assert np.array_equal(g[key].astype(np.uint64), o[key].astype(np.uint64)), (rep, key)
+            del g
+        shard.replicate_local(engines)
+        with cref.threads(THREADS):
+            m, t = query_masses(oix, 200_000, seed=13)
+            for r in (0, k - 1):
+                assert_index_equal(engines[r], oix, f"swissprot replica {r}/{k}")
+                assert_queries_equal(engines[r], oix, m, t, f"swissprot replica {r}/{k} queries")
+    finally:
+        for e in engines:
+            e.close()
 
 
 def test_swissprot_semi_slice(Engine, swissprot):

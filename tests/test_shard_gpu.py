@@ -139,8 +139,13 @@ def test_sharded_human_scale(native):
     _run_local(native, DBIndexSearchParams.trypsin(2), fasta.config("human"), 4, ctx="human")
 
 
-def test_sharded_rccl_single_rank(native):
+@pytest.mark.parametrize("full_path", ["0", "1"])
+def test_sharded_rccl_single_rank(native, full_path, monkeypatch):
+    """One rank: the single-owner build (the single-device build plus the
+    shard bookkeeping), and with DBI_SHARD_FULL_PATH=1 the general path
+    (samples, partition, exchange to itself, owner merge)."""
     from dbindex_amd.engine import Engine
+    monkeypatch.setenv("DBI_SHARD_FULL_PATH", full_path)
     pp = fasta.config("1k")
     prm = DBIndexSearchParams.trypsin(2)
     cp = prm.to_c()
@@ -188,6 +193,7 @@ def test_sharded_rccl_local_failure_is_reported(native, phase, monkeypatch):
     stay usable: the next build and query batch succeed."""
     from dbindex_amd import _native
     from dbindex_amd.engine import Engine
+    monkeypatch.setenv("DBI_SHARD_FULL_PATH", "1")  # one rank: the general path, not the single-owner build
     pp = fasta.config("1k").slice(0, 200)
     cp = DBIndexSearchParams.trypsin(2).to_c()
     oix = cref.Index(cp, pp.residues, pp.offsets)
@@ -249,8 +255,10 @@ def test_replicated_index_local(native, k, nprot):
             e.close()
 
 
-def test_replicated_index_rccl_single_rank(native):
+@pytest.mark.parametrize("full_path", ["0", "1"])
+def test_replicated_index_rccl_single_rank(native, full_path, monkeypatch):
     from dbindex_amd.engine import Engine
+    monkeypatch.setenv("DBI_SHARD_FULL_PATH", full_path)
     from tests.helpers import assert_index_equal, assert_queries_equal
     pp = fasta.config("1k")
     cp = DBIndexSearchParams.trypsin(2).to_c()

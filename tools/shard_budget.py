@@ -1,0 +1,104 @@
+"""Per-shard phase budget of an N-way sharded build, measured on ONE GPU.
+
+  python tools/shard_budget.py [--config swissprot] [--shards 8] [--reps 3]
+
+Builds the proteome as N local shards (N handles on this GPU, the phases of an
+N-rank dbi_build_sharded with dbi_shard_exchange_local copies in place of the
+RCCL exchange), every kernel timed by its HIP events, and prints one JSON
+object: for each shard its digest / partition / merge kernel time and the
+bytes it sends to other owners, and the model of the N-GPU build
+
+  T_N = max_r(digest_r + partition_r) + exchange + max_r(merge_r) + fixed
+
+where exchange = the largest per-GPU send or receive volume over one xGMI
+link per peer pair (MI355X: 7 links, ~64 GB/s achieved per direction each,
+i.e. bytes_to_peer / 64 GB/s for the slowest pair), and fixed = the
+collectives and host synchronisations of dbi_build_sharded (measured by the
+one-rank general path separately: bench.py --merge with DBI_SHARD_FULL_PATH=1).
+Shards run one after another here, so each shard's kernels have the whole GPU
+(on N GPUs each has its own).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+LINK_GBS = 64.0  # achieved GB/s per xGMI link per direction (one link per GPU pair)
+
+DIGEST = ("tile_proteins", "digest")
+PARTITION = ("owner_hist", "owner_scan", "owner_scatter")
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="swissprot")
+    ap.add_argument("--shards", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    from dbindex_amd import fasta, shard
+    from dbindex_amd._native import DeviceBuffer, synchronize
+    from dbindex_amd.engine import Engine
+    from dbindex_amd.params import DBIndexSearchParams
+    pp = fasta.config(a.config, with_defs=False)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    d_res = DeviceBuffer.from_numpy(np.concatenate([pp.residues, np.zeros(16, np.uint8)]), 0)
+    d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), 0)
+    synchronize(0)
+    k = a.shards
+    engines = [Engine(cp, 0) for _ in range(k)]
+    ranges = shard.protein_ranges(pp.offsets, k)
+    best = None
+    try:
+        for e in engines:
+            e.set_timing(True)
+        for _ in range(a.reps):
+            shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, ranges)
+            rows = []
+            for r, e in enumerate(engines):
+                st = shard.shard_stats(e)
+                dig = part = exch = merge = 0.0
+                stages = {}
+                for name, ms, _ in e.stage_times():
+                    stages[name] = round(stages.get(name, 0.0) + ms, 4)
+                    if name.startswith(DIGEST):
+                        dig += ms
+                    elif name in PARTITION:
+                        part += ms
+                    elif name == "exchange":
+                        exch += ms
+                    else:
+                        merge += ms
+                rows.append(dict(shard=r, proteins=int(ranges[r][1] - ranges[r][0]), digest_ms=dig,
+                                 partition_ms=part, local_exchange_ms=exch, merge_ms=merge,
+                                 n_total=int(st.n_total), n_dropped=int(st.n_dropped), n_sent=int(st.n_sent),
+                                 n_received=int(st.n_received),
+                                 wall_digest_ms=st.digest_ms, wall_merge_ms=st.merge_ms, stages=stages,
+                                 n_bins=int(e.stats().n_bins), n_big_bins=int(e.stats().n_big_bins)))
+            front = max(x["digest_ms"] + x["partition_ms"] for x in rows)
+            back = max(x["merge_ms"] for x in rows)
+            # pairwise volume: a shard's sends are spread over k-1 peers, one link each
+            def from_others(x):
+                return x["n_received"] - (x["n_total"] - x["n_dropped"] - x["n_sent"])
+            link_bytes = max(8.0 * max(x["n_sent"], from_others(x)) / max(k - 1, 1) for x in rows)
+            xch = link_bytes / (LINK_GBS * 1e6)
+            tot = front + xch + back
+            if best is None or tot < best["model_ms_without_fixed"]:
+                best = dict(config=a.config, shards=k, rows=rows, front_ms=front, exchange_model_ms=xch,
+                            merge_max_ms=back, model_ms_without_fixed=tot, link_gbs=LINK_GBS)
+    finally:
+        for e in engines:
+            e.close()
+    print(json.dumps(best))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
