@@ -2978,6 +2978,7 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
                   Counters* __restrict__ ctr) {
     __shared__ ChunkSmem<NT, CAP> sm;
     const uint32_t n = BIG ? ctr->n_big : ctr->n_mid;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x) atomicOr(&ctr->err, ERR_GRID);
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     const uint32_t j = blockIdx.x;
     if (j < n) {
@@ -2998,6 +2999,16 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
             ucount[c] = tot;
             if (BIG) atomicAdd(&ctr->n_big_recs, (unsigned long long)m);
         }
+    }
+    // entries past the grid (ERR_GRID: the build is redone with full grids):
+    // their records go to `out` unsorted and without unique heads, so the rest
+    // of this build stays inside its buffers
+    for (uint32_t e = j + gridDim.x; e < n; e += gridDim.x) {
+        const uint32_t c = list[e];
+        const uint32_t a = chunk_lo[c];
+        const uint32_t m = chunk_lo[c + 1] - a;
+        for (uint32_t i = threadIdx.x; i < m; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
+        if (threadIdx.x == 0) ucount[c] = 0;
     }
 }
 

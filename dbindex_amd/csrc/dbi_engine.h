@@ -162,6 +162,7 @@ struct dbi_handle {
     bool inputs_ptm = false;            // ... and they carry inline '[formula]' PTMs (no dbi_rebuild)
     bool hc_final = false;              // hc holds the counters after the build's last kernel
     uint64_t last_kept = 0;             // the previous build's records (bins of a device-sized tail)
+    uint32_t grid_mid = 0, grid_big = 0;  // list-kernel grids of a device-sized tail, from the previous build (0: one block per possible entry)
     DevBuf<double> q_mass, q_tol;
     DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
     DevBuf<uint32_t> h_nh, h_no, h_ids, h_hocc, h_prot;  // dbi_query_hits_device
@@ -209,6 +210,7 @@ struct dbi_handle {
         const void* d_res = nullptr;
         const void* d_poff = nullptr;
         uint64_t n_res = 0, n_prot = 0, cap = 0, last_kept = 0, alloc_gen = 0, dp_gen = 0;
+        uint32_t grid_mid = 0, grid_big = 0;
         bool timing = false;
         char timing_only[32] = {};
         bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }

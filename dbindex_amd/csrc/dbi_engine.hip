@@ -207,9 +207,15 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                             h->mid_list.p, h->ctr.p, s));
     // one block per listed chunk: at most one chunk per bin above the wave
-    // sort's reach (the lists are filled on the device)
-    const uint32_t max_mid = (uint32_t)std::min<uint64_t>(nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
-    const uint32_t max_big = (uint32_t)std::min<uint64_t>(nchunks, n / (CHUNK_CAP + 1) + 1);
+    // sort's reach (the lists are filled on the device).  A device-sized tail
+    // launches the previous build's list lengths plus a margin instead (a grid
+    // of every possible entry spent most of these launches dispatching blocks
+    // with nothing to do, the big tier's at one 155-KiB block per CU at a
+    // time); a longer list sets ERR_GRID and the build is redone with full grids.
+    uint32_t max_mid = (uint32_t)std::min<uint64_t>(nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
+    uint32_t max_big = (uint32_t)std::min<uint64_t>(nchunks, n / (CHUNK_CAP + 1) + 1);
+    if (d_n && h->grid_mid) max_mid = std::min(max_mid, h->grid_mid);
+    if (d_n && h->grid_big) max_big = std::min(max_big, h->grid_big);
     STAGE(h, "chunk_sort_mid", by(0, 0, 0, 0, 0),
           launch_chunk_sort_mid(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->mid_list.p,
                                 max_mid, h->ctr.p, s));
@@ -298,6 +304,9 @@ int finish_build(dbi_handle* h) {
     st.device_bytes = bytes;
     h->built = true;
     h->last_kept = st.n_kept;
+    // the next device-sized tail's list grids: this build's lists plus a margin
+    h->grid_mid = h->hc.n_mid + h->hc.n_mid / 8 + 32;
+    h->grid_big = h->hc.n_big + h->hc.n_big / 8 + 16;
     ++h->build_serial;
     return 0;
 }
@@ -408,6 +417,8 @@ dbi_handle::GraphKey graph_key(const dbi_handle* h) {
     k.n_prot = h->n_prot;
     k.cap = h->recA.cap;
     k.last_kept = h->last_kept;
+    k.grid_mid = h->grid_mid;
+    k.grid_big = h->grid_big;
     k.alloc_gen = g_alloc_gen.load(std::memory_order_relaxed);
     k.dp_gen = h->dp_gen;
     k.timing = h->timing;
@@ -492,22 +503,26 @@ int build_digest(dbi_handle* h) {
             h->prev_key = graph_key(h);
             h->prev_key_valid = bounded;
         }
-        // the one host sync of a warm build: did the digest fit the capacity?
+        // the one host sync of a warm build: did the digest fit the capacity,
+        // and the chunk lists their grids?
         if ((rc = read_counters(h))) return rc;
         const uint64_t need = sparse ? h->hc.n_slots : h->hc.n_kept;
         if (need >= (1ull << 32) - 1)
             return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences (or bounded-digest slots) on "
                                             "one device: shard the FASTA");
-        if (need <= n_in) {
+        const bool grid_short = (h->hc.err & ERR_GRID) != 0;
+        if (need <= n_in && !grid_short) {
             h->hc_final = true;
             return 0;
         }
-        if (attempt > 0) return set_error(DBI_E_STATE, "digest output grew between identical passes");
-        // grown: everything again into the bigger buffer (counters back to
-        // zero, except the record layout; the stage table restarts)
+        if (attempt > 1) return set_error(DBI_E_STATE, "digest output grew between identical passes");
+        // grown, or a chunk list longer than its grid: everything again (full
+        // list grids; counters back to zero, except the record layout; the
+        // stage table restarts)
         drop_graph(h);
         h->prev_key_valid = false;
-        if ((rc = h->recA.ensure(need + need / 8))) return rc;
+        h->grid_mid = h->grid_big = 0;
+        if (need > n_in && (rc = h->recA.ensure(need + need / 8))) return rc;
         DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), h->stream));
         h->nstage = 0;
     }

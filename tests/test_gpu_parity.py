@@ -116,6 +116,31 @@ def test_big_bins_and_duplicates(Engine, copies):
         assert_index_equal(eng, oix, f"bigbins x{copies}")
 
 
+def test_list_grids_outgrown(Engine):
+    """Warm builds size the mid / big chunk-list grids from the previous
+    build's lists; a build with far more big chunks than the last one
+    outgrows them (ERR_GRID) and is redone with full grids -- same index as
+    the oracle.  Then the first proteome again on the larger grids."""
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    plain = fasta.config("human").slice(0, 6000)
+    base = fasta.config("1k").sequence(5)
+    seqs = [base] * 3000 + [fasta.config("1k").sequence(i) for i in range(6, 40)]
+    big = fasta.PackedProteins.from_sequences(seqs)
+    assert big.residues.size < plain.residues.size  # the second build stays warm (no regrowth)
+    o_plain = cref.Index(cp, plain.residues, plain.offsets)
+    o_big = cref.Index(cp, big.residues, big.offsets)
+    with Engine(cp) as eng:
+        st = eng.build(plain)
+        assert st.n_big_bins == 0
+        assert_index_equal(eng, o_plain, "list grids: plain [cold]")
+        st = eng.build(big)
+        assert st.n_big_bins > 16
+        assert_index_equal(eng, o_big, "list grids: big chunks [warm, outgrown]")
+        for k in range(2):
+            eng.build(plain)
+            assert_index_equal(eng, o_plain, f"list grids: plain again [{k}]")
+
+
 def _giant_isobaric():
     """~12k proteins whose tryptic peptides are permutations of one
     composition: thousands of bit-identical fp64 masses with different strings
