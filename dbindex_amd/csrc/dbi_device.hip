@@ -1313,15 +1313,19 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     const uint32_t nvec = (lend + 15u) >> 4;
     const uint8_t* __restrict__ gb = d_res + w0 - lb;  // LDS position q <- gb[q], q in [lb, lend)
 
-    // every independent global load first: the window's 16-B vectors (the
-    // ragged first / last one byte by byte), the tile's protein range, the tables
+    // every independent global load first: the window's 16-B vectors, the
+    // tile's protein range, the tables.  The ragged first / last vector is
+    // loaded whole (an aligned 16-B vector holding a byte of the residues
+    // never leaves that byte's page) and the bytes outside [lb, lend) are
+    // cleared: byte loads in a branch cost one HBM round trip each, and the
+    // whole block waited for the wave that made them.
     constexpr uint32_t NV = (LD_WIN / 16 + DIGEST_THREADS - 1) / DIGEST_THREADS;
     uint4 rv[NV];
 #pragma unroll
     for (uint32_t k = 0; k < NV; ++k) {
         const uint32_t i = tid + k * DIGEST_THREADS;
-        const bool full = i < nvec && 16u * i >= lb && 16u * i + 16u <= lend;
-        rv[k] = *(full ? reinterpret_cast<const uint4*>(gb + 16u * i) : &g_zero16);
+        const bool any = i < nvec && 16u * i + 16u > lb;
+        rv[k] = *(any ? reinterpret_cast<const uint4*>(gb + 16u * i) : &g_zero16);
     }
     const uint32_t pf = d_tile_pf[tile], pl = d_tile_pf[ntiles + 1 + tile];
     sm.mass[tid] = d_mass_tab[tid];
@@ -1331,11 +1335,16 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
 #pragma unroll
     for (uint32_t k = 0; k < NV; ++k) {
         const uint32_t i = tid + k * DIGEST_THREADS;
-        if (i < nvec && !(16u * i >= lb && 16u * i + 16u <= lend)) {  // ragged vector: bytes in [lb, lend)
-            uint32_t wv[4] = {0u, 0u, 0u, 0u};
-            for (uint32_t b = 0; b < 16; ++b) {
-                const uint32_t q = 16u * i + b;
-                if (q >= lb && q < lend) wv[b >> 2] |= (uint32_t)gb[q] << (8 * (b & 3u));
+        const uint32_t vlo = 16u * i >= lb ? 0u : min(lb - 16u * i, 16u);
+        const uint32_t vhi = 16u * i + 16u <= lend ? 16u : (lend > 16u * i ? lend - 16u * i : 0u);
+        if (vlo > 0u || vhi < 16u) {  // ragged vector: keep the bytes in [lb, lend)
+            uint32_t wv[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+#pragma unroll
+            for (uint32_t d = 0; d < 4; ++d) {
+                uint32_t keep = 0;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) keep |= (4u * d + b >= vlo && 4u * d + b < vhi) ? 0xFFu << (8 * b) : 0u;
+                wv[d] &= keep;
             }
             rv[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         }
@@ -1739,10 +1748,15 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
     const uint32_t cb = radix_chunk();
     const uint32_t base = cb * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
     uint64_t qv[RADIX_ITEMS];
+    if (base + RADIX_ITEMS * 64 <= n) {  // wave-uniform: every load in flight together
 #pragma unroll
-    for (int k = 0; k < RADIX_ITEMS; ++k) {
-        const uint32_t i = base + k * 64 + lane;
-        qv[k] = i < n ? in[i].q0 : REC_SENTINEL;
+        for (int k = 0; k < RADIX_ITEMS; ++k) qv[k] = in[base + k * 64 + lane].q0;
+    } else {
+#pragma unroll
+        for (int k = 0; k < RADIX_ITEMS; ++k) {
+            const uint32_t i = base + k * 64 + lane;
+            qv[k] = i < n ? in[i].q0 : REC_SENTINEL;
+        }
     }
     // counts only (no ranks): one LDS atomic per record into the wave's own row
 #pragma unroll
@@ -1823,13 +1837,15 @@ k_radix_scatter(const Rec* __restrict__ in, void* __restrict__ out, uint32_t n, 
     const uint32_t base = cb * RADIX_CHUNK + w * (RADIX_ITEMS * 64);
     const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
     uint4 rv[RADIX_ITEMS];
+    if (base + RADIX_ITEMS * 64 <= n) {  // wave-uniform: every load in flight together
 #pragma unroll
-    for (int k = 0; k < RADIX_ITEMS; ++k) {
-        const uint32_t i = base + k * 64 + lane;
-        // (a per-load branch: the compiler issues these one round trip apart;
-        // issuing all eight together -- clamped index -- measured slower on
-        // semi-tryptic builds, 36.9 vs 31.2 ms for the three passes)
-        rv[k] = i < n ? in4[i] : make_uint4(0, 0, 0, 0);
+        for (int k = 0; k < RADIX_ITEMS; ++k) rv[k] = in4[base + k * 64 + lane];
+    } else {  // the last records (a load per branch: one round trip each)
+#pragma unroll
+        for (int k = 0; k < RADIX_ITEMS; ++k) {
+            const uint32_t i = base + k * 64 + lane;
+            rv[k] = i < n ? in4[i] : make_uint4(0, 0, 0, 0);
+        }
     }
     // this block's global digit offsets, in flight with the records (one per thread)
     const uint32_t goff = threadIdx.x < D ? offs[(size_t)threadIdx.x * gridDim.x + cb] : 0u;
@@ -3211,16 +3227,23 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
     for (uint32_t t0 = 0; t0 < n; t0 += FIN_THREADS * FIN_ITEMS) {
         uint4 rv[FIN_ITEMS];
         uint32_t lpre[FIN_ITEMS];
-        // lane 0 also loads the record before its own (the rest take it from
-        // the lane below): every load of the round in flight together
+        // lane 0 also needs the record before its own (the rest take it from
+        // the lane below).  Loads at clamped indices, no branches: every load
+        // of the round in flight together (a load per branch costs one round
+        // trip each); lanes past the chunk drop what they read.
         const bool l0 = lane_id() == 0;
         unsigned long long pq[FIN_ITEMS];
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
             const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
-            rv[k] = i < n ? r4[i] : make_uint4(0, 0, 0, 0);  // low byte of q0 = head flag
-            pq[k] = (l0 && i < n && a + i > 0) ? recs[a + i - 1].q0 : 0ull;
+            const uint32_t ic = min(i, n - 1);
+            const uint32_t ip = a + ic > 0 ? a + ic - 1 : 0u;
+            rv[k] = r4[ic];  // low byte of q0 = head flag (hd below: only below n)
+            pq[k] = recs[l0 ? ip : a + ic].q0;  // lanes > 0: the line they already read
         }
+        bool hd[FIN_ITEMS];
+#pragma unroll
+        for (uint32_t k = 0; k < FIN_ITEMS; ++k) hd[k] = t0 + k * FIN_THREADS + threadIdx.x < n && (rv[k].x & 0xFFu);
         // mass of the record before each head (= the previous unique's mass)
         double prevm[FIN_ITEMS];
 #pragma unroll
@@ -3228,11 +3251,11 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
             const uint32_t i = t0 + k * FIN_THREADS + threadIdx.x;
             const uint32_t px = __shfl_up((int)rv[k].x, 1, 64), py = __shfl_up((int)rv[k].y, 1, 64);
             const unsigned long long prev = l0 ? pq[k] : (((unsigned long long)py << 32) | px);
-            prevm[k] = (i < n && a + i > 0 && (rv[k].x & 0xFFu)) ? q0_mass(prev) : 0.0;
+            prevm[k] = (hd[k] && a + i > 0) ? q0_mass(prev) : 0.0;
         }
 #pragma unroll
         for (uint32_t k = 0; k < FIN_ITEMS; ++k) {
-            const uint64_t bal = __ballot((rv[k].x & 0xFFu) != 0);
+            const uint64_t bal = __ballot(hd[k]);
             lpre[k] = (uint32_t)__popcll(bal & lanemask_lt());
             if (lane_id() == 0) wc[k * NW + w] = (uint32_t)__popcll(bal);
         }
@@ -3254,7 +3277,7 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
                 const uint64_t q1 = u4_q1(rv[k]);
                 const uint32_t pid = q1_pid(q1, W);
                 occ_pid[a + i] = pid;
-                if (rv[k].x & 0xFFu) {
+                if (hd[k]) {
                     const uint32_t u = run + wc[k * NW + w] + lpre[k];
                     const double mu = u4_mass(rv[k]);
                     nkeys += (a + i == 0) || java_d2i(mu * (double)factor) != java_d2i(prevm[k] * (double)factor);
