@@ -382,11 +382,11 @@ def main() -> None:
                    kind="range lookup: (first, count) of every window's run of unique ids (the complete "
                         "answer over the mass-sorted unique table), device in/out",
                    index="the build above", qdir_build_ms=qdir_ms)
-        # hit-producing leg: every hit's unique id and protein ids materialised in HBM
-        # (at most ~40 GB of hit buffers: semi-tryptic windows hold ~20x more hits)
-        nq_h = int(min(nq, nq * 40e9 / max(12.0 * hits, 1.0)))
-        hq = hits_leg(eng, dm, dt, max(nq_h, 1))
-        qps["materialised"] = hq
+        # hit-producing leg: every hit's unique id and protein ids materialised in
+        # HBM, all nq windows, in consecutive batches of at most ~40 GB of hit
+        # buffers (semi-tryptic windows hold ~20x more hits than tryptic ones)
+        counts = dc.download(np.uint64, nq).astype(np.float64)
+        qps["materialised"] = hits_leg(eng, dm, dt, nq, counts)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -540,27 +540,55 @@ def sample_parity(prm, sample, oix, dev: int) -> dict:
     return dict(ok=bool(same), gpu_sha=g, oracle_sha=o, n_total=st.n_total, n_unique=st.n_unique)
 
 
-def hits_leg(eng, dm, dt, nq: int, reps: int = 5) -> dict:
-    """1M +-20 ppm windows through dbi_query_hits_device: per query its unique
-    ids, per hit its protein ids (occurrence CSR), all written to HBM.
-    Algorithmic bytes (DESIGN.md §6): 32 Q (mass + tol in, two u64 offsets
+def hit_batches(counts, cap_bytes: float = 40e9, per_hit: float = 12.0):
+    """Consecutive query ranges [a, b) whose hits (range-lookup counts) take at
+    most cap_bytes of hit buffers each (a single window above it: alone)."""
+    cum = np.concatenate([[0.0], np.cumsum(counts * per_hit)])
+    out, a, n = [], 0, len(counts)
+    while a < n:
+        b = int(np.searchsorted(cum, cum[a] + cap_bytes, side="right")) - 1
+        b = min(max(b, a + 1), n)
+        out.append((a, b))
+        a = b
+    return out
+
+
+def hits_leg(eng, dm, dt, nq: int, counts, reps: int = 3) -> dict:
+    """nq +-20 ppm windows through dbi_query_hits_device: per query its unique
+    ids, per hit its protein ids (occurrence CSR), all written to HBM, batch
+    by batch (hit_batches) when the hits of all windows exceed the buffer cap.
+    Algorithmic bytes (DESIGN.md §7): 32 Q (mass + tol in, two u64 offsets
     out) + 12 H (id out, protein-list start out, occ_off read) + 8 Ho (protein
-    id read + written), Ho = protein ids of all hits."""
+    id read + written), Ho = protein ids of all hits; also SURVEY.md §8(d)'s
+    16 Q + 16 H."""
     from dbindex_amd._native import synchronize
-    r = eng.query_hits_device(dm.ptr, dt.ptr, nq)  # warm: grows the buffers
+    batches = hit_batches(counts)
+    for a, b in batches[:1]:  # warm: grows the buffers
+        eng.query_hits_device(dm.ptr + 8 * a, dt.ptr + 8 * a, b - a)
     synchronize(eng.device)
-    t = time.perf_counter()
-    for _ in range(reps):
-        r = eng.query_hits_device(dm.ptr, dt.ptr, nq)
-    synchronize(eng.device)
-    t = (time.perf_counter() - t) / reps
-    H, Ho = r.n_hits, r.n_prot_ids
+    H = Ho = 0
+    t = 0.0
+    for a, b in batches:
+        eng.query_hits_device(dm.ptr + 8 * a, dt.ptr + 8 * a, b - a)  # this batch's buffer sizes
+        synchronize(eng.device)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = eng.query_hits_device(dm.ptr + 8 * a, dt.ptr + 8 * a, b - a)
+        synchronize(eng.device)
+        t += (time.perf_counter() - t0) / reps
+        H += r.n_hits
+        Ho += r.n_prot_ids
     alg = 32.0 * nq + 12.0 * H + 8.0 * Ho
+    alg_s = 16.0 * nq + 16.0 * H
     return dict(value=nq / t, unit="queries/s", ms_per_batch=1e3 * t, queries=nq, hits=H, protein_ids=Ho,
-                kind="materialised: unique ids + protein ids of every hit in HBM (dbi_query_hits_device)",
+                batches=len(batches),
+                kind="materialised: unique ids + protein ids of every hit in HBM (dbi_query_hits_device), all "
+                     "windows, in batches of at most ~40 GB of hit buffers",
                 roofline=dict(bound="hbm", alg_bytes=alg, formula="32Q + 12H + 8Ho",
                               achieved=alg / t / 1e9, peak=HBM_PEAK_GBPS, unit="GB/s",
-                              frac=alg / t / 1e9 / HBM_PEAK_GBPS))
+                              frac=alg / t / 1e9 / HBM_PEAK_GBPS,
+                              survey_formula="16Q + 16H (SURVEY.md §8(d))", survey_alg_bytes=alg_s,
+                              survey_frac=alg_s / t / 1e9 / HBM_PEAK_GBPS))
 
 
 def hbm_copy_gbps(dev: int, nbytes: int = 1 << 31, reps: int = 10):
