@@ -619,6 +619,16 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
     tables = fasta.synth_tables()
     prm = DBIndexSearchParams.non_specific(50)
     eng = Engine(prm, device=dev)
+    nb = int(prm.index_factor)  # SQLiteMult buckets (+1: past the last one)
+    comm = None
+    if world > 1:  # the per-bucket counts are summed over the ranks by RCCL (ncclAllReduce)
+        from dbindex_amd import shard
+        uid = stdout_to_stderr(shard.ShardComm.unique_id) if rank == 0 else None
+        uid = bytes.fromhex(coord.broadcast(uid.hex() if uid else None))
+        comm = stdout_to_stderr(lambda: shard.ShardComm(uid, world, rank, dev))
+    zeros = np.zeros(nb + 1, np.uint64)
+    d_hist = DeviceBuffer.from_numpy(zeros, dev)      # this rank's buckets, per step
+    d_hist_all = DeviceBuffer.from_numpy(zeros, dev)  # every rank's (allreduce)
     t0 = time.time()
     base = fasta.synth_residue_base(seed, p0, tables[0])
     CH = 1 << 20  # proteins per chunk (~3.8e8 residues)
@@ -648,6 +658,17 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
             tot += eng.count_device(*c)[0]
         return tot
 
+    def bucket_pass():
+        # the COUNT walk again with the SQLiteMult bucket of every occurrence
+        # (dbi_count_buckets), then the buckets of all ranks summed (RCCL)
+        d_hist.upload(zeros)
+        tot = 0
+        for c in chunks:
+            tot += eng.count_buckets_device(*c, d_hist.ptr)[0]
+        if comm is not None:
+            comm.allreduce_u64(d_hist.ptr, d_hist_all.ptr, nb + 1)
+        return tot
+
     for _ in range(max(args.warmup, 1)):
         n_step = step()
     if world > 1:
@@ -666,6 +687,20 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
         n_all, res_all = coord.allreduce([n_all, float(n_res_all)], "sum")
     else:
         res_all = float(n_res_all)
+    # per-bucket counts: one more pass, timed on its own (the step above is the count alone)
+    if world > 1:
+        coord.barrier()
+    t_b = time.perf_counter()
+    bucket_pass()
+    synchronize(dev)
+    if world > 1:
+        coord.barrier()
+    t_b = time.perf_counter() - t_b
+    if world > 1:
+        t_b = coord.allreduce([t_b], "max")[0]
+    hist = (d_hist_all if comm is not None else d_hist).download(np.uint64, nb + 1)
+    if int(hist.sum()) * args.steps != int(n_all):
+        raise RuntimeError(f"bucket counts {int(hist.sum())} do not add up to totalSeqCount {int(n_all) // args.steps}")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cref
@@ -692,6 +727,12 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
         d_so = DeviceBuffer.from_numpy(sample.offsets.astype(np.uint64), dev)
         g = eng.count_device(d_sr.ptr, sample.n_residues, d_so.ptr, sample.n_proteins)[0]
         cpu.update(gpu_count_same_sample=g, sample_parity=bool(g == want))
+        # and its per-bucket counts
+        with cref.threads(nthreads):
+            want_h = cref.count_buckets(cp, sample.residues, sample.offsets)
+        d_h = DeviceBuffer.from_numpy(zeros, dev)
+        eng.count_buckets_device(d_sr.ptr, sample.n_residues, d_so.ptr, sample.n_proteins, d_h.ptr)
+        cpu["sample_bucket_parity"] = bool(np.array_equal(d_h.download(np.uint64, nb + 1), want_h))
     if rank == 0:
         ms = 1000.0 * elapsed / max(args.steps, 1)
         alg = res_all + 8.0 * (P + 1)  # residues + offsets read once per step (count mode writes nothing)
@@ -704,7 +745,14 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
             "config": {"workload": f"TrEMBL-scale synthetic proteome ({P} proteins, seed {seed}), non-specific "
                                    f"6-50, count only (BASELINE.json configs[4])",
                        "proteins": P, "residues": res_all, "peptides_per_step": n_all / max(args.steps, 1),
-                       "parallelism": f"protein ranges x{world}, no exchange" if world > 1 else "single GPU"},
+                       "parallelism": (f"protein ranges x{world}, per-bucket counts summed by RCCL allreduce"
+                                       if world > 1 else "single GPU")},
+            # occurrences per SQLiteMult bucket, (int)m / BUCKET_MASS_RANGE (the last: past the last bucket)
+            "bucket_counts": {"bucket_mass_range_da": 8000 // nb, "counts": [int(x) for x in hist],
+                              "combined": "ncclAllReduce (dbi_comm_allreduce_u64)" if world > 1 else "one rank",
+                              "ms": 1e3 * t_b, "peptides_per_s": float(hist.sum()) / t_b,
+                              "kind": "dbi_count_buckets over every chunk (+ the allreduce), one pass after the "
+                                      "timed steps; the last entry is past the last bucket"},
             "roofline": {"bound": "hbm", "kernel": "digest_count",
                          "achieved": alg / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
@@ -714,6 +762,8 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
             "cpu_baseline": cpu,
         }), flush=True)
     eng.close()
+    if comm is not None:
+        comm.close()
 
 
 if __name__ == "__main__":

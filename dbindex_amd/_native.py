@@ -129,6 +129,7 @@ SIGNATURES = [
     ("dbi_synth_proteome", c_int, [P, c_uint64, c_uint64, c_uint64, c_uint64, P, P, POINTER(c_void_p),
                                    POINTER(c_void_p), POINTER(c_uint64)]),
     ("dbi_count", c_int, [P, P, c_uint64, P, c_uint64, POINTER(c_uint64), POINTER(c_uint64)]),
+    ("dbi_count_buckets", c_int, [P, P, c_uint64, P, c_uint64, P, POINTER(c_uint64), POINTER(c_uint64)]),
     ("dbi_comm_unique_id", c_int, [P]),
     ("dbi_comm_init", c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
     ("dbi_comm_destroy", None, [P]),

@@ -266,10 +266,16 @@ __device__ __forceinline__ bool in_windows(const DevParams& dp, double m) {
     return lo > 0 && m <= dp.win_hi[lo - 1];
 }
 
-template <bool EMIT, bool SEMI, bool MAND>
+// HIST (COUNT only): every INCLUDE'd occurrence also counted in its SQLiteMult
+// bucket, hist[min((int)m / BUCKET_MASS_RANGE, NUM_BUCKETS)] (LDS).
+__device__ __forceinline__ void hist_add(const DevParams& dp, uint32_t* hist, double m) {
+    atomicAdd(&hist[min(java_d2i(m) / dp.br, dp.nb)], 1u);
+}
+
+template <bool EMIT, bool SEMI, bool MAND, bool HIST = false>
 __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSmem& sm, uint32_t w0, uint32_t wlim,
                                             uint32_t s, bool n_ok, uint64_t loc, Rec* __restrict__ out,
-                                            const Rec* out_end) {
+                                            const Rec* out_end, uint32_t* hist = nullptr) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;                 // precMass after H2O+H+, cTerm, nTerm (:265-271)
     if (!(m <= dp.max_mh)) return r;  // while condition before the first residue (:284)
@@ -317,6 +323,7 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
             rec.q1 = rec_q1(tag, loc, e - s + 1);
             if (out + kept < out_end) out[kept] = rec;
         }
+        if (HIST && (keep | drop)) hist_add(dp, hist, m);
         kept += keep;
         dropped += drop;
         const bool past = m > dp.win_max;                     // SKIP_PROTEIN_START (:351-354)
@@ -333,11 +340,11 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
 // The same loop reading residues from HBM (walks that run past the staged
 // window, e.g. through zero-mass residues): flags from the residue tables,
 // the cut from the next residue and the protein end pe.
-template <bool EMIT, bool SEMI, bool MAND>
+template <bool EMIT, bool SEMI, bool MAND, bool HIST = false>
 __device__ WalkOut walk_global(const DevParams& dp, const double* __restrict__ s_mass,
                                const uint8_t* __restrict__ s_flags, const uint8_t* __restrict__ g_res,
                                uint32_t s, uint32_t pe, bool n_ok, uint64_t loc, Rec* __restrict__ out,
-                               const Rec* out_end) {
+                               const Rec* out_end, uint32_t* hist = nullptr, uint32_t hist_from = 0) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;
     if (!(m <= dp.max_mh)) return r;
@@ -374,6 +381,7 @@ __device__ WalkOut walk_global(const DevParams& dp, const double* __restrict__ s
             rec.q1 = rec_q1(tag, loc, e - s + 1);
             if (out + kept < out_end) out[kept] = rec;
         }
+        if (HIST && (keep || drop) && e >= hist_from) hist_add(dp, hist, m);
         kept += keep;
         dropped += drop;
         if (brk || mbrk || last || over || m > dp.win_max) break;
@@ -601,11 +609,11 @@ __device__ __forceinline__ uint32_t tile_protein(const DigestSmem& sm, const Til
 }
 
 // One candidate: LDS walk, or the HBM walk when it outruns the window
-template <bool EMIT, bool SEMI, bool MAND>
+template <bool EMIT, bool SEMI, bool MAND, bool HIST = false>
 __device__ __forceinline__ WalkOut walk_candidate(const DevParams& dp, const DigestSmem& sm, const TileCtx& tc,
                                                   const uint8_t* __restrict__ d_res,
                                                   const uint32_t* __restrict__ d_poff, uint32_t j,
-                                                  Rec* __restrict__ o, const Rec* o_end) {
+                                                  Rec* __restrict__ o, const Rec* o_end, uint32_t* hist = nullptr) {
     const uint32_t i = sm.cand[j];
     const uint32_t s = tc.t0 + i;
     const bool n_ok = SEMI ? n_ok_at(sm, tc, i) : true;
@@ -615,10 +623,11 @@ __device__ __forceinline__ WalkOut walk_candidate(const DevParams& dp, const Dig
         const uint32_t p = tile_protein(sm, tc, d_poff, s, pstart);
         loc = rec_loc(p, s - pstart, tc.w);
     }
-    WalkOut w = walk_lds<EMIT, SEMI, MAND>(dp, sm, tc.w0, tc.w_end, s, n_ok, loc, o, o_end);
-    if (w.overflow) {
+    WalkOut w = walk_lds<EMIT, SEMI, MAND, HIST>(dp, sm, tc.w0, tc.w_end, s, n_ok, loc, o, o_end, hist);
+    if (w.overflow) {  // (HIST: the LDS walk counted the ends before w_end - 1, the same as the HBM walk's)
         const uint32_t pe = d_poff[find_le(d_poff, tc.pf, tc.pl + 1, s) + 1];
-        w = walk_global<EMIT, SEMI, MAND>(dp, sm.mass, sm.flags, d_res, s, pe, n_ok, loc, o, o_end);
+        w = walk_global<EMIT, SEMI, MAND, HIST>(dp, sm.mass, sm.flags, d_res, s, pe, n_ok, loc, o, o_end, hist,
+                                                tc.w_end - 1);
     }
     return w;
 }
@@ -648,14 +657,27 @@ __device__ __forceinline__ void publish_counts(DigestSmem& sm, uint32_t kept, ui
 // EMIT : d_blk holds the exclusive per-tile offsets; a block scan of the
 //        per-thread counts places each thread's contiguous run of candidates:
 //        thread order == start order, so records land in insertion order.
-template <bool EMIT, bool SEMI, bool MAND>
+// The block's bucket counts (HIST) into the device histogram (one atomic per
+// non-empty bucket).
+__device__ __forceinline__ void hist_flush(const DevParams& dp, const uint32_t* s_hist,
+                                           unsigned long long* __restrict__ d_hist) {
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b <= (uint32_t)dp.nb; b += blockDim.x)
+        if (s_hist[b]) atomicAdd(&d_hist[b], (unsigned long long)s_hist[b]);
+}
+
+template <bool EMIT, bool SEMI, bool MAND, bool HIST = false>
 __global__ void __launch_bounds__(DIGEST_THREADS)
 k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
          const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
          uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, uint32_t* __restrict__ d_blk,
-         uint32_t* __restrict__ d_thr, Rec* __restrict__ d_out, Counters* __restrict__ d_ctr) {
+         uint32_t* __restrict__ d_thr, Rec* __restrict__ d_out, Counters* __restrict__ d_ctr,
+         unsigned long long* __restrict__ d_hist = nullptr) {
     __shared__ DigestSmem sm;
+    __shared__ uint32_t s_hist[HIST ? HIST_MAX_BUCKETS + 1 : 1];
     TileCtx tc;
+    if (HIST)  // (digest_prepare's barriers come before the first count)
+        for (uint32_t b = threadIdx.x; b <= (uint32_t)dp.nb; b += DIGEST_THREADS) s_hist[b] = 0;
     const uint32_t ncand = digest_prepare<SEMI>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
                                                 d_tile_pf, d_ctr);
     uint32_t jb, je;
@@ -663,11 +685,13 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
     if (!EMIT) {
         uint32_t kept = 0, dropped = 0;
         for (uint32_t j = jb; j < je; ++j) {
-            const WalkOut w = walk_candidate<false, SEMI, MAND>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr);
+            const WalkOut w = walk_candidate<false, SEMI, MAND, HIST>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr,
+                                                                      s_hist);
             kept += w.kept;
             dropped += w.dropped;
         }
         publish_counts(sm, kept, dropped, d_blk, d_thr, d_ctr);
+        if (HIST) hist_flush(dp, s_hist, d_hist);
         return;
     }
     tc.w = rec_width(d_ctr->max_plen);
@@ -738,8 +762,46 @@ __device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi) {
     return ((2ull << hi) - 1ull) & ~((1ull << lo) - 1ull);
 }
 
+// Bucket counts of one thread's starts (ascending) when NUM_BUCKETS <= 8: the
+// per-thread counts in registers, and for every bucket boundary B_k = (k+1) x
+// BUCKET_MASS_RANGE the first window position q whose prefix mass reaches it
+// for the current start (prefix(q) >= B_k - m0 + prefix(start - 1)).  That
+// position only moves forward from one start to the next (the threshold
+// grows with the start's prefix), so it is tracked, not searched: about one
+// LDS read per boundary and start instead of a binary search.
+constexpr int HIST_FAST_MAX = 8;
+struct HistTrack {
+    uint32_t t[HIST_FAST_MAX];  // the boundary's position (0: not yet found)
+    double p[HIST_FAST_MAX];    // prefix mass there
+    uint32_t c[HIST_FAST_MAX + 1];
+};
+
+// first q in [t, hi + 1] with prefix(q) >= x (prefix non-decreasing): gallop, then bisect
+__device__ __forceinline__ uint32_t prefix_seek(const CutSmem& cs, uint32_t t, uint32_t hi, double x) {
+    if (t > hi || cut_prefix(cs, t) >= x) return t;
+    uint32_t lo = t, step = 1;  // prefix(lo) < x
+    while (lo + step <= hi && cut_prefix(cs, lo + step) < x) {
+        lo += step;
+        step <<= 1;
+    }
+    uint32_t up = min(lo + step, hi + 1);  // prefix(up) >= x, or up = hi + 1
+    while (up - lo > 1) {
+        const uint32_t mid = (lo + up) >> 1;
+        if (cut_prefix(cs, mid) >= x) up = mid; else lo = mid;
+    }
+    return up;
+}
+
+// HIST: the ends' SQLiteMult buckets as well -- ht (NUM_BUCKETS <= 8): the
+// tracked boundaries above, counts in registers; otherwise the boundaries
+// k * BUCKET_MASS_RANGE located by binary search like the limits above,
+// counts into the LDS hist.  An end's mass within CUT_EPS of a boundary (or
+// more than 7 boundaries in one walk, binary-search path) and the start is
+// recounted by the exact walk.
+template <bool HIST = false>
 __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const DigestSmem& sm, const CutSmem& cs,
-                                                   uint32_t nbytes, uint32_t ps) {
+                                                   uint32_t nbytes, uint32_t ps, uint32_t* hist, HistTrack& ht,
+                                                   bool fast) {
     CutCount r{0u, 0u, true};
     if (!(dp.m0 <= dp.max_mh)) return r;  // while condition before the first residue (:284)
     if (ps + 2 > nbytes) { r.exact = false; return r; }
@@ -819,6 +881,99 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Di
             nd = (uint32_t)__popcll(em & bit_range(a, (uint32_t)Y));
         }
     }
+    if (HIST && n && fast) {
+        // absolute window positions of the first / last end; M(e) >= B <=> prefix(ps + e) >= B - m0 + pb
+        const uint32_t qlo = ps + (uint32_t)lo, qhi = ps + (uint32_t)Y;
+        const double plo = cut_prefix(cs, qlo), phi = cut_prefix(cs, qhi), xb = pb - dp.m0;
+        uint32_t pos[HIST_FAST_MAX];
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < HIST_FAST_MAX; ++k) {
+            pos[k] = qhi + 1u;
+            if (k < dp.nb) {
+                const double x = (double)((k + 1) * dp.br) + xb;
+                uint32_t t;
+                if (x > phi + CUT_EPS) t = qhi + 1u;        // past every end of this start
+                else if (x < plo - CUT_EPS) t = qlo;        // before every end
+                else {
+                    t = ht.t[k];
+                    double pt = ht.p[k];  // prefix(t), cached
+                    if (t < qlo || t > qhi + 1u) {  // first use, or left behind: search
+                        t = prefix_seek(cs, qlo, qhi, x);
+                        pt = cut_prefix(cs, t);
+                    } else {
+                        int steps = 0;  // usually one position per start
+                        while (t <= qhi && pt < x && steps < 4) {
+                            pt = cut_prefix(cs, ++t);
+                            ++steps;
+                        }
+                        if (t <= qhi && pt < x) {
+                            t = prefix_seek(cs, t, qhi, x);
+                            pt = cut_prefix(cs, t);
+                        }
+                    }
+                    ht.t[k] = t;
+                    ht.p[k] = pt;
+                    if (t <= qhi && pt - x <= CUT_EPS) bad = true;
+                    if (t > qlo && x - cut_prefix(cs, t - 1) <= CUT_EPS) bad = true;
+                }
+                pos[k] = t;
+            }
+        }
+        if (bad) { r.exact = false; return r; }
+        uint32_t from = qlo;
+#pragma unroll
+        for (int k = 0; k < HIST_FAST_MAX; ++k) {
+            if (k < dp.nb) {
+                if (pos[k] > from) ht.c[k] += (uint32_t)__popcll(em & bit_range(from - ps, pos[k] - 1u - ps));
+                from = max(from, pos[k]);
+            }
+        }
+        uint32_t last = 0;
+        if (from <= qhi) last = (uint32_t)__popcll(em & bit_range(from - ps, (uint32_t)Y));
+#pragma unroll
+        for (int k = 1; k <= HIST_FAST_MAX; ++k)
+            if (k == dp.nb) ht.c[k] += last;
+    } else if (HIST && n) {
+        const double ml = M((uint32_t)lo), my = M((uint32_t)Y);
+        auto near_edge = [&](double x) {
+            const int k = java_d2i(x) / dp.br;
+            return x - (double)(k * dp.br) <= CUT_EPS || (double)((k + 1) * dp.br) - x <= CUT_EPS;
+        };
+        if (near_edge(ml) || near_edge(my)) { r.exact = false; return r; }
+        const int b0 = java_d2i(ml) / dp.br, b1 = java_d2i(my) / dp.br;
+        if (b1 - b0 > 7) { r.exact = false; return r; }
+        uint32_t at[7];  // first position of bucket b0 + 1 + i
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            at[i] = (uint32_t)Y + 1u;
+            if (i < b1 - b0) {
+                const double B = (double)((b0 + 1 + i) * dp.br);
+                uint32_t a = (uint32_t)lo + 1u, b = (uint32_t)Y;  // M(lo) < B <= M(Y)
+                while (a < b) {
+                    const uint32_t mid = (a + b) >> 1;
+                    if (M(mid) >= B) b = mid; else a = mid + 1;
+                }
+                if (M(a) - B <= CUT_EPS || B - M(a - 1) <= CUT_EPS) { r.exact = false; return r; }
+                at[i] = a;
+            }
+        }
+        uint32_t from = (uint32_t)lo;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            if (i < b1 - b0) {
+                if (at[i] > from) {
+                    const uint32_t c = (uint32_t)__popcll(em & bit_range(from, at[i] - 1u));
+                    if (c) atomicAdd(&hist[min(b0 + i, dp.nb)], c);
+                }
+                from = max(from, at[i]);
+            }
+        }
+        if (from <= (uint32_t)Y) {
+            const uint32_t c = (uint32_t)__popcll(em & bit_range(from, (uint32_t)Y));
+            if (c) atomicAdd(&hist[min(b1, dp.nb)], c);
+        }
+    }
     r.kept = n - nd;
     r.dropped = nd;
     return r;
@@ -857,14 +1012,28 @@ __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nby
     __syncthreads();
 }
 
+template <bool HIST>
 __global__ void __launch_bounds__(DIGEST_THREADS)
 k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                     const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
                     uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, uint32_t* __restrict__ d_blk,
-                    uint32_t* __restrict__ d_thr, Counters* __restrict__ d_ctr) {
+                    uint32_t* __restrict__ d_thr, Counters* __restrict__ d_ctr,
+                    unsigned long long* __restrict__ d_hist) {
     __shared__ DigestSmem sm;
     __shared__ CutSmem cs;
     __shared__ double s_dtmp[DIGEST_THREADS / 64 + 1];
+    __shared__ uint32_t s_hist[HIST ? HIST_MAX_BUCKETS + 1 : 1];
+    if (HIST)  // (digest_prepare's barriers come before the first count)
+        for (uint32_t b = threadIdx.x; b <= (uint32_t)dp.nb; b += DIGEST_THREADS) s_hist[b] = 0;
+    HistTrack ht;
+    const bool fast = HIST && dp.nb <= HIST_FAST_MAX;
+#pragma unroll
+    for (int k = 0; k < HIST_FAST_MAX; ++k) {
+        ht.t[k] = 0;
+        ht.p[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k <= HIST_FAST_MAX; ++k) ht.c[k] = 0;
     TileCtx tc;
     const uint32_t ncand = digest_prepare<false>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
                                                  d_tile_pf, d_ctr);
@@ -873,16 +1042,25 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     thread_share(ncand, jb, je);
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
-        CutCount r = count_by_masks(dp, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0);
+        CutCount r = count_by_masks<HIST>(dp, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0, s_hist, ht, fast);
         if (!r.exact) {
-            const WalkOut w = walk_candidate<false, false, false>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr);
+            const WalkOut w = walk_candidate<false, false, false, HIST>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr,
+                                                                        s_hist);
             r.kept = w.kept;
             r.dropped = w.dropped;
         }
         kept += r.kept;
         dropped += r.dropped;
     }
+    if (fast) {  // the register counts into the block's (wave sums: one LDS atomic per wave and bucket)
+#pragma unroll
+        for (int k = 0; k <= HIST_FAST_MAX; ++k) {
+            const uint32_t v = wave_sum(ht.c[k]);
+            if (k <= dp.nb && lane_id() == 0 && v) atomicAdd(&s_hist[k], v);
+        }
+    }
     publish_counts(sm, kept, dropped, d_blk, d_thr, d_ctr);
+    if (HIST) hist_flush(dp, s_hist, d_hist);
 }
 
 // ---------------------------------------------------------------------------
@@ -1522,19 +1700,20 @@ hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, 
     return hipGetLastError();
 }
 
-template <bool EMIT>
+template <bool EMIT, bool HIST = false>
 static hipError_t launch_digest(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                 const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr, Rec* d_out,
-                                Counters* d_ctr, hipStream_t s) {
+                                Counters* d_ctr, hipStream_t s, unsigned long long* d_hist = nullptr) {
     const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     if (nblk == 0) return hipSuccess;
+    static_assert(!EMIT || !HIST, "bucket counts come from COUNT passes");
 #define DBI_DIGEST(SEMI, MAND)                                                                              \
-    DBI_LAUNCH((k_digest<EMIT, SEMI, MAND>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
-                       d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_out, d_ctr)
+    DBI_LAUNCH((k_digest<EMIT, SEMI, MAND, HIST>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
+                       d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_out, d_ctr, d_hist)
     if (!EMIT && !dp.semi && !dp.mand_mode && dp.cut_count) {
-        DBI_LAUNCH(k_digest_count_cuts, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
-                   d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr);
+        DBI_LAUNCH(k_digest_count_cuts<HIST>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags,
+                   d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr, d_hist);
         return hipGetLastError();
     }
     if (dp.semi) {
@@ -1552,6 +1731,15 @@ hipError_t launch_digest_count(const DevParams& dp, const double* d_mass_tab, co
                                Counters* d_ctr, hipStream_t s) {
     return launch_digest<false>(dp, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr,
                                 nullptr, d_ctr, s);
+}
+
+hipError_t launch_digest_count_hist(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                                    const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                                    const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr, Counters* d_ctr,
+                                    unsigned long long* d_hist, hipStream_t s) {
+    if (dp.nb < 1 || dp.nb > HIST_MAX_BUCKETS) return hipErrorInvalidValue;
+    return launch_digest<false, true>(dp, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr,
+                                      nullptr, d_ctr, s, d_hist);
 }
 
 hipError_t launch_digest_emit(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,

@@ -145,6 +145,7 @@ inline BinMap make_binmap(double lo, double hi, uint32_t nbins) {
     return bm;
 }
 
+constexpr int HIST_MAX_BUCKETS = 64;  // dbi_count_buckets: index_factor (NUM_BUCKETS) at most
 constexpr int GIANT_PASSES = 3;  // MSD split passes over chunks above BIG_CAP (then the global-memory fallback)
 
 // Device counters block (one per engine), read back once per build.
@@ -223,6 +224,12 @@ constexpr unsigned long long REC_SENTINEL = ~0ull;
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                  const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s);
+// COUNT with SQLiteMult bucket counts: d_hist[min((int)m / BUCKET_MASS_RANGE,
+// NUM_BUCKETS)] += each INCLUDE'd occurrence (NUM_BUCKETS <= HIST_MAX_BUCKETS)
+hipError_t launch_digest_count_hist(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                                    const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                                    const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr, Counters* d_ctr,
+                                    unsigned long long* d_hist, hipStream_t s);
 hipError_t launch_digest_emit(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                               const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
                               uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk_off, uint32_t* d_thr,

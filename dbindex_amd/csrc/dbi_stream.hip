@@ -121,8 +121,10 @@ int dbi_synth_proteome(dbi_handle* h, uint64_t seed, uint64_t p_begin, uint64_t 
     return 0;
 }
 
-int dbi_count(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_prot_off, uint64_t n_prot,
-              uint64_t* n_total, uint64_t* n_dropped) {
+namespace {
+// dbi_count / dbi_count_buckets (d_hist: accumulate bucket counts there)
+int count_impl(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_prot_off, uint64_t n_prot,
+               uint64_t* d_hist, uint64_t* n_total, uint64_t* n_dropped) {
     if (!h || (!d_res && n_res) || !d_prot_off || !n_total) return set_error(DBI_E_INVALID, "NULL argument");
     int rc;
     if ((rc = begin_build(h, n_res, n_prot))) return rc;
@@ -137,9 +139,15 @@ int dbi_count(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_
     h->d_poff = h->poff.p;
     if (n_res) {
         if ((rc = prepare_tiles(h))) return rc;
-        STAGE(h, "digest_count", by(1, 0, 0, 4, 0),
-              launch_digest_count(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff, (uint32_t)n_prot,
-                                  (uint32_t)n_res, h->tile_pf.p, h->blk.p, h->thr.p, h->ctr.p, s));
+        if (d_hist)
+            STAGE(h, "digest_count", by(1, 0, 0, 4, 0),
+                  launch_digest_count_hist(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
+                                           (uint32_t)n_prot, (uint32_t)n_res, h->tile_pf.p, h->blk.p, h->thr.p,
+                                           h->ctr.p, reinterpret_cast<unsigned long long*>(d_hist), s));
+        else
+            STAGE(h, "digest_count", by(1, 0, 0, 4, 0),
+                  launch_digest_count(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff, (uint32_t)n_prot,
+                                      (uint32_t)n_res, h->tile_pf.p, h->blk.p, h->thr.p, h->ctr.p, s));
         DBI_HIP(launch_scan_u32(h->blk.p, h->blk.p, nblk, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_kept, s));
     }
     if ((rc = read_counters(h))) return rc;
@@ -147,6 +155,20 @@ int dbi_count(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_
     *n_total = h->hc.n_kept + h->hc.n_dropped;
     if (n_dropped) *n_dropped = h->hc.n_dropped;
     return 0;
+}
+}  // namespace
+
+int dbi_count(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_prot_off, uint64_t n_prot,
+              uint64_t* n_total, uint64_t* n_dropped) {
+    return count_impl(h, d_res, n_res, d_prot_off, n_prot, nullptr, n_total, n_dropped);
+}
+
+int dbi_count_buckets(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_prot_off,
+                      uint64_t n_prot, uint64_t* d_bucket_counts, uint64_t* n_total, uint64_t* n_dropped) {
+    if (!h || !d_bucket_counts) return set_error(DBI_E_INVALID, "NULL argument");
+    if (h->dp.nb < 1 || h->dp.nb > HIST_MAX_BUCKETS)
+        return set_error(DBI_E_INVALID, "dbi_count_buckets: index_factor (NUM_BUCKETS) must be 1..64");
+    return count_impl(h, d_res, n_res, d_prot_off, n_prot, d_bucket_counts, n_total, n_dropped);
 }
 
 }  // extern "C"

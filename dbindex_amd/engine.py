@@ -113,6 +113,17 @@ class Engine:
                                       n_prot, ctypes.byref(t), ctypes.byref(d)))
         return t.value, d.value
 
+    def count_buckets_device(self, d_residues: int, n_res: int, d_offsets: int, n_prot: int,
+                             d_bucket_counts: int) -> Tuple[int, int]:
+        """COUNT-mode digest with the SQLiteMult bucket of every occurrence
+        (dbi_count_buckets): adds into the device array d_bucket_counts
+        (index_factor + 1 u64); returns (totalSeqCount, bucket drops)."""
+        t, d = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_native.lib().dbi_count_buckets(self.h, ctypes.c_void_p(d_residues), n_res, ctypes.c_void_p(d_offsets),
+                                              n_prot, ctypes.c_void_p(d_bucket_counts), ctypes.byref(t),
+                                              ctypes.byref(d)))
+        return t.value, d.value
+
     def save(self, path: str) -> None:
         """The built index + its proteome to one file (dbi_index_save)."""
         check(_native.lib().dbi_index_save(self.h, path.encode()))

@@ -126,6 +126,10 @@ class ShardComm:
         check(_native.lib().dbi_comm_allgatherv(self.h, ctypes.c_void_p(d_send) if d_send else None,
                                                 ctypes.c_void_p(d_recv), _p(rb), None))
 
+    def allreduce_u64(self, d_in: int, d_out: int, n: int) -> None:
+        """Sum of n u64 over every rank, device to device (ncclAllReduce)."""
+        check(_native.lib().dbi_comm_allreduce_u64(self.h, ctypes.c_void_p(d_in), ctypes.c_void_p(d_out), n, None))
+
     def close(self) -> None:
         if getattr(self, "h", None):
             _native.lib().dbi_comm_destroy(self.h)

@@ -403,6 +403,15 @@ int dbi_synth_proteome(dbi_handle* h, uint64_t seed, uint64_t p_begin, uint64_t 
  * drops.  Builds no index (the handle's index, if any, is discarded). */
 int dbi_count(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, const uint64_t* d_prot_off,
               uint64_t n_prot, uint64_t* n_total, uint64_t* n_dropped);
+/* dbi_count, and the occurrences per SQLiteMult bucket (getBucketForMass,
+ * DBIndexStoreSQLiteMult.java:215-217: (int)m / BUCKET_MASS_RANGE, the store
+ * each one goes to, :277-288): d_bucket_counts[b] += those of bucket b <
+ * NUM_BUCKETS, d_bucket_counts[NUM_BUCKETS] += those past the last bucket
+ * (the drops of :283-288).  d_bucket_counts: device array of index_factor + 1
+ * u64 (index_factor <= 64) on the handle's device, accumulated (+=) so
+ * chunks of one proteome add up; dbi_comm_allreduce_u64 sums it over ranks. */
+int dbi_count_buckets(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, const uint64_t* d_prot_off,
+                      uint64_t n_prot, uint64_t* d_bucket_counts, uint64_t* n_total, uint64_t* n_dropped);
 
 /* ------------------------------------------------------------------------ */
 /* Persisted index (the reference's SQLite index files + indexExists reuse)  */

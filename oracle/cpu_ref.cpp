@@ -612,6 +612,34 @@ int oref_count(const dbi_params* p, const uint8_t* res, const uint64_t* off, uin
     return 0;
 }
 
+// The same count split by SQLiteMult bucket (getBucketForMass, :215-217:
+// (int)precMass / BUCKET_MASS_RANGE): hist[b] += the INCLUDE'd occurrences of
+// bucket b < NUM_BUCKETS, hist[NUM_BUCKETS] += those past the last bucket
+// (addSequence's drops, :283-288).  hist has index_factor + 1 entries.
+int oref_count_buckets(const dbi_params* p, const uint8_t* res, const uint64_t* off, uint64_t n_prot,
+                       uint64_t* hist) {
+    if (p->index_factor <= 0) return DBI_E_INVALID;
+    const int nb = p->index_factor;
+    const int bucketRange = MAX_PRECURSOR_INT / nb;  // SQLiteMult:56
+    const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_threads, n_prot));
+    std::vector<std::vector<uint64_t>> part(nt, std::vector<uint64_t>(nb + 1, 0));
+    g_ptm_fatal = false;
+    parallel_for(nt, [&](int t) {
+        std::vector<Occ> occ;
+        for (uint64_t i = n_prot * t / nt; i < n_prot * (t + 1) / nt; ++i) {
+            occ.clear();
+            cut_seq(p, res + off[i], (int)(off[i + 1] - off[i]), (uint32_t)i, occ);
+            for (const Occ& o : occ) part[t][std::min(java_d2i(o.mass) / bucketRange, nb)]++;
+        }
+    });
+    if (g_ptm_fatal) return DBI_E_INVALID;
+    for (int b = 0; b <= nb; ++b) {
+        hist[b] = 0;
+        for (int t = 0; t < nt; ++t) hist[b] += part[t][b];
+    }
+    return 0;
+}
+
 int oref_build(const dbi_params* p, const uint8_t* res, const uint64_t* off, uint64_t n_prot,
                oref_index** out) {
     if (p->index_factor <= 0) return DBI_E_INVALID;

@@ -54,6 +54,7 @@ def lib():
         L.oref_tolerance_in_dalton.restype = ctypes.c_double
         L.oref_set_threads.argtypes = [ctypes.c_int]
         L.oref_count.argtypes = [P, P, P, ctypes.c_uint64, U64, U64]
+        L.oref_count_buckets.argtypes = [P, P, P, ctypes.c_uint64, P]
         L.oref_query_batch.argtypes = [P, P, P, ctypes.c_uint64, P, P]
         _lib = L
     return _lib
@@ -123,6 +124,19 @@ def count(cparams, residues: np.ndarray, offsets: np.ndarray):
     if rc != 0:
         raise ValueError(f"oref_count failed: {rc}")
     return t.value, d.value
+
+
+def count_buckets(cparams, residues: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    """Occurrences per SQLiteMult bucket ((int)m / BUCKET_MASS_RANGE), the last
+    entry = past the last bucket (oref_count_buckets): index_factor + 1 counts."""
+    residues = np.ascontiguousarray(residues, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    hist = np.zeros(int(cparams.index_factor) + 1, np.uint64)
+    rc = lib().oref_count_buckets(ctypes.byref(cparams), _ptr(residues), _ptr(offsets), offsets.shape[0] - 1,
+                                  _ptr(hist))
+    if rc != 0:
+        raise ValueError(f"oref_count_buckets failed: {rc}")
+    return hist
 
 
 class Index:

@@ -442,3 +442,46 @@ def test_query_hits_device(Engine, nprot, nq):
                 starts = r["hit_occ"][r["row"][i]:r["row"][i + 1]]
                 assert np.array_equal(starts.astype(np.uint64), (o["occ_off"][exp] - o["occ_off"][exp[0]])
                                       if exp.shape[0] else np.zeros(0, np.uint64)), i
+
+
+@pytest.mark.parametrize("name,prm", [
+    ("tryp2", DBIndexSearchParams.trypsin(2)),
+    ("nonspec", DBIndexSearchParams.non_specific(30)),
+    ("semi2", DBIndexSearchParams.semi_tryptic(2)),
+    ("mandK", DBIndexSearchParams.trypsin(2, mandatory_internal_aas="K")),
+    ("drop", DBIndexSearchParams.trypsin(4, index_factor=7, max_precursor_mass=7999.0)),
+    ("drop13", DBIndexSearchParams.trypsin(4, index_factor=13, max_precursor_mass=7999.0)),
+    ("fine", DBIndexSearchParams.trypsin(2, index_factor=64)),
+    ("nonspec9", DBIndexSearchParams.non_specific(50, index_factor=9)),
+    ("fine_nonspec", DBIndexSearchParams.non_specific(40, index_factor=64)),
+])
+def test_count_buckets(Engine, name, prm):
+    """dbi_count_buckets: occurrences per SQLiteMult bucket
+    (DBIndexStoreSQLiteMult.java:215-217; last entry: past the last bucket)
+    equal the oracle's, by the bit-map count (boundaries by binary search,
+    walks where one lies within CUT_EPS) and by the walk (semi / mandatory)."""
+    from dbindex_amd._native import DeviceBuffer
+    pp = fasta.config("1k").slice(0, 300)
+    cp = prm.to_c()
+    want = cref.count_buckets(cp, pp.residues, pp.offsets)
+    total = cref.count(cp, pp.residues, pp.offsets)
+    d_res = DeviceBuffer.from_numpy(np.concatenate([pp.residues, np.zeros(16, np.uint8)]))
+    d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64))
+    d_hist = DeviceBuffer.from_numpy(np.zeros(cp.index_factor + 1, np.uint64))
+    with Engine(cp) as eng:
+        assert eng.count_buckets_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, d_hist.ptr) == total
+    assert np.array_equal(d_hist.download(np.uint64, cp.index_factor + 1), want), name
+    if name.startswith("drop"):
+        assert want[-1] > 0  # occurrences past the last bucket (SQLiteMult's drops) are counted
+
+
+def test_count_buckets_rejects_large_index_factor(Engine):
+    from dbindex_amd._native import DBIndexStoreException, DeviceBuffer
+    pp = fasta.config("1k").slice(0, 10)
+    cp = DBIndexSearchParams.trypsin(2, index_factor=100).to_c()
+    d_res = DeviceBuffer.from_numpy(np.concatenate([pp.residues, np.zeros(16, np.uint8)]))
+    d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64))
+    d_hist = DeviceBuffer(8 * 101)
+    with Engine(cp) as eng:
+        with pytest.raises(DBIndexStoreException, match="index_factor"):
+            eng.count_buckets_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, d_hist.ptr)

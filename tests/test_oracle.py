@@ -182,6 +182,31 @@ def test_twin_restatements_agree(name, prm, n):
     assert st.number_sequences() == ix.n_keys and st.entry_keys() == list(ix.entry_keys())
 
 
+@pytest.mark.parametrize("name,prm,n", [
+    ("tryp2", DBIndexSearchParams.trypsin(2), 60),
+    ("nonspec", DBIndexSearchParams.non_specific(20), 8),
+    ("semi1", DBIndexSearchParams.semi_tryptic(1), 25),
+    ("drop", DBIndexSearchParams.trypsin(4, index_factor=3000, max_precursor_mass=7999.0), 40),
+    ("fine", DBIndexSearchParams.trypsin(2, index_factor=200), 60),
+])
+def test_count_buckets_twins(name, prm, n):
+    """oref_count_buckets (SQLiteMult bucket of every INCLUDE'd occurrence,
+    the last entry past the last bucket) against the pure-Python twin's
+    occurrences binned by java (int) / BUCKET_MASS_RANGE; it adds up to
+    totalSeqCount and its last entry to the bucket drops."""
+    pp = fasta.config("1k").slice(0, n)
+    cp = prm.to_c()
+    hist = cref.count_buckets(cp, pp.residues, pp.offsets)
+    nb = prm.index_factor
+    br = 8000 // nb
+    want = np.zeros(nb + 1, np.uint64)
+    for occ in pyref.digest(prm, pp.sequences()):
+        want[min(pyref.java_int(occ[0]) // br, nb)] += 1
+    assert np.array_equal(hist, want)
+    total, dropped = cref.count(cp, pp.residues, pp.offsets)
+    assert int(hist.sum()) == total and int(hist[nb]) == dropped
+
+
 def test_twin_tag_collisions():
     from tests.helpers import tag_collision_proteins
     seqs = tag_collision_proteins()

@@ -275,3 +275,27 @@ def test_replicated_index_rccl_single_rank(native, full_path, monkeypatch):
                 assert_queries_equal(eng, oix, m, t, f"rccl replica [{rep}]")
     finally:
         comm.close()
+
+
+def test_bucket_counts_rccl_allreduce_single_rank(native):
+    """TrEMBL-style per-bucket counts (dbi_count_buckets) of two protein ranges
+    of one proteome, summed by dbi_comm_allreduce_u64 (ncclAllReduce, one
+    rank), equal the oracle's buckets of the whole proteome."""
+    from dbindex_amd.engine import Engine
+    pp = fasta.config("1k").slice(0, 400)
+    cp = DBIndexSearchParams.non_specific(30).to_c()
+    want = cref.count_buckets(cp, pp.residues, pp.offsets)
+    nb = cp.index_factor
+    d_hist = native.DeviceBuffer.from_numpy(np.zeros(nb + 1, np.uint64))
+    d_sum = native.DeviceBuffer.from_numpy(np.zeros(nb + 1, np.uint64))
+    comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
+    try:
+        with Engine(cp, 0) as eng:
+            for a, b in ((0, 150), (150, 400)):
+                part = pp.slice(a, b)
+                d_res, d_off = _inputs(native, part)
+                eng.count_buckets_device(d_res.ptr, part.n_residues, d_off.ptr, part.n_proteins, d_hist.ptr)
+        comm.allreduce_u64(d_hist.ptr, d_sum.ptr, nb + 1)
+        assert np.array_equal(d_sum.download(np.uint64, nb + 1), want)
+    finally:
+        comm.close()
