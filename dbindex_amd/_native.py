@@ -45,7 +45,7 @@ class DbiShardStats(ctypes.Structure):
         ("n_sent", c_uint64), ("n_received", c_uint64), ("n_unique", c_uint64), ("n_keys", c_uint64),
         ("g_total", c_uint64), ("g_dropped", c_uint64), ("g_kept", c_uint64), ("g_unique", c_uint64),
         ("g_keys", c_uint64), ("digest_ms", c_double), ("partition_ms", c_double),
-        ("exchange_ms", c_double), ("merge_ms", c_double),
+        ("exchange_ms", c_double), ("merge_ms", c_double), ("merge_gpu_ms", c_double),
     ]
 
 
@@ -118,6 +118,9 @@ SIGNATURES = [
     ("dbi_shard_digest", c_int, [P, P, c_uint64, P, c_uint64, c_uint64, c_uint64, c_int, c_int]),
     ("dbi_shard_samples", c_int, [P, P]),
     ("dbi_shard_splitters", c_int, [P, c_int, c_int32, P]),
+    ("dbi_shard_splitters_cost", c_int, [P, c_int, c_int32, c_int, P, P, P]),
+    ("dbi_shard_cost_update", c_int, [P, c_int, P, P, P]),
+    ("dbi_shard_splitters_profiled", c_int, [P, P, c_int, P]),
     ("dbi_shard_partition", c_int, [P, P, P]),
     ("dbi_shard_exchange_local", c_int, [P, c_int]),
     ("dbi_shard_merge", c_int, [P]),

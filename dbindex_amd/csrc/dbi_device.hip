@@ -3189,19 +3189,26 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
         const uint32_t c = list[j];
         const uint32_t a = chunk_lo[c];
         const uint32_t m = chunk_lo[c + 1] - a;
-        if (BIG && m > split_above) {
+        if (BIG && m > split_above && giant_list) {
             if (threadIdx.x == 0) {
                 giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
                 atomicAdd(&ctr->n_giant_recs, (unsigned long long)m);
             }
-            return;
-        }
-        uint32_t h = 0;
-        sort_chunk<NT, CAP, true>(in + a, out + a, m, bm, rl, sm, &h);
-        const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
-        if (threadIdx.x == 0) {
-            ucount[c] = tot;
-            if (BIG) atomicAdd(&ctr->n_big_recs, (unsigned long long)m);
+        } else if (BIG && m > split_above) {
+            // no giant pass this build (none last time): through unsorted, redone (ERR_GRID)
+            for (uint32_t i = threadIdx.x; i < m; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
+            if (threadIdx.x == 0) {
+                ucount[c] = 0;
+                atomicOr(&ctr->err, ERR_GRID);
+            }
+        } else {
+            uint32_t h = 0;
+            sort_chunk<NT, CAP, true>(in + a, out + a, m, bm, rl, sm, &h);
+            const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
+            if (threadIdx.x == 0) {
+                ucount[c] = tot;
+                if (BIG) atomicAdd(&ctr->n_big_recs, (unsigned long long)m);
+            }
         }
     }
     // entries past the grid (ERR_GRID: the build is redone with full grids):
@@ -3400,7 +3407,7 @@ __global__ void __launch_bounds__(FIN_THREADS)
 k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
            double* __restrict__ umass, uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff,
            uint32_t* __restrict__ ulen, uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid,
-           int32_t factor, Counters* __restrict__ ctr) {
+           int32_t factor, uint32_t ucap, Counters* __restrict__ ctr) {
     constexpr uint32_t NW = FIN_THREADS / 64;
     __shared__ uint32_t wc[FIN_ITEMS * NW];  // heads per (round item k, wave), then exclusive bases
     __shared__ uint32_t s_tot;
@@ -3465,8 +3472,8 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
                 const uint64_t q1 = u4_q1(rv[k]);
                 const uint32_t pid = q1_pid(q1, W);
                 occ_pid[a + i] = pid;
-                if (hd[k]) {
-                    const uint32_t u = run + wc[k * NW + w] + lpre[k];
+                const uint32_t u = run + wc[k * NW + w] + lpre[k];
+                if (hd[k] && u < ucap) {  // (always below ucap; never a write past the table)
                     const double mu = u4_mass(rv[k]);
                     nkeys += (a + i == 0) || java_d2i(mu * (double)factor) != java_d2i(prevm[k] * (double)factor);
                     umass[u] = mu;
@@ -3487,10 +3494,10 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
 
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
-                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, Counters* d_ctr, hipStream_t s) {
+                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(FIN_THREADS), 0, s, d_recs, d_chunk_lo, d_ubase, d_umass, d_upid,
-               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, d_ctr);
+               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, d_ctr);
     return hipGetLastError();
 }
 
@@ -3512,9 +3519,23 @@ hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t fa
 }
 
 // occ_off[U] = n_kept (U from the device counters)
+__global__ void k_tail_counts(Counters* __restrict__ ctr, uint64_t cap, int sparse) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long need = sparse ? ctr->n_slots : ctr->n_kept;
+    const bool fit = need <= cap;
+    ctr->tail_in = fit ? need : 0ull;
+    ctr->tail_n = fit ? ctr->n_kept : 0ull;
+}
+
+hipError_t launch_tail_counts(Counters* d_ctr, uint64_t cap, bool sparse, hipStream_t s) {
+    DBI_LAUNCH(k_tail_counts, dim3(1), dim3(64), 0, s, d_ctr, cap, sparse ? 1 : 0);
+    return hipGetLastError();
+}
+
 __global__ void k_write_tail(uint32_t* __restrict__ occ_off, uint32_t n_kept, const Counters* __restrict__ ctr,
                              const unsigned long long* __restrict__ dn) {
-    if (threadIdx.x == 0) occ_off[ctr->n_unique] = dn ? (uint32_t)*dn : n_kept;
+    // (occ_off holds n_kept + 1 entries: a unique count past that is never written)
+    if (threadIdx.x == 0 && ctr->n_unique <= n_kept) occ_off[ctr->n_unique] = dn ? (uint32_t)*dn : n_kept;
 }
 
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s,

@@ -75,6 +75,7 @@ struct ShardState {
     std::vector<uint64_t> recv_count;            // per source shard
     uint64_t n_recv = 0;
     double ms_digest = 0, ms_partition = 0, ms_exchange = 0, ms_merge = 0;
+    double ms_merge_gpu = 0;                // device time of the owner merge's kernels
     dbi_shard_stats global{};               // filled by dbi_build_sharded (RCCL sums)
     uint64_t u_base = 0;                    // first global id of this owner's unique table
     bool u_base_known = false;
@@ -163,6 +164,7 @@ struct dbi_handle {
     bool hc_final = false;              // hc holds the counters after the build's last kernel
     uint64_t last_kept = 0;             // the previous build's records (bins of a device-sized tail)
     uint32_t grid_mid = 0, grid_big = 0;  // list-kernel grids of a device-sized tail, from the previous build (0: one block per possible entry)
+    bool giants_seen = true;              // the previous build had giant chunks (or none yet): run the giant pass
     DevBuf<double> q_mass, q_tol;
     DevBuf<uint64_t> q_first, q_count, q_row, q_ids;
     DevBuf<uint32_t> h_nh, h_no, h_ids, h_hocc, h_prot;  // dbi_query_hits_device
@@ -177,6 +179,15 @@ struct dbi_handle {
 
     dbi_stats stats{};
     dbi::ShardState shard;
+    // merge-cost profile kept across dbi_build_sharded calls (fixed key bands,
+    // smoothed over builds): the next build's splitters balance that cost
+    // instead of record counts
+    struct {
+        bool valid = false;
+        int32_t split[DBI_COST_BANDS - 1] = {};  // fixed key bands over [minMH, maxMH]
+        double cost[DBI_COST_BANDS] = {};        // smoothed merge time per record
+    } shard_prof;
+    hipEvent_t ev_merge[2] = {nullptr, nullptr};  // owner merge device time
     DevBuf<uint64_t> xsend, xrecv;      // sharded build: 8-B location words to / from the owners
     DevBuf<double> samp;                // sharded build: mass samples (splitters)
     DevBuf<unsigned long long> xcount;  // sharded build: send counts of every shard (RCCL all-gather)
@@ -211,6 +222,7 @@ struct dbi_handle {
         const void* d_poff = nullptr;
         uint64_t n_res = 0, n_prot = 0, cap = 0, last_kept = 0, alloc_gen = 0, dp_gen = 0;
         uint32_t grid_mid = 0, grid_big = 0;
+        bool giants = true;
         bool timing = false;
         char timing_only[32] = {};
         bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }
@@ -293,8 +305,9 @@ int prepare_tiles(dbi_handle* h);
 // digest of h->d_res / h->d_poff into recA: *n records (*n_in slots, REC_SENTINEL
 // in the unused ones when *sparse)
 int run_digest(dbi_handle* h, uint64_t* n, uint64_t* n_in, bool* sparse, bool* dev_sized = nullptr);
+int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse);  // build_tail's allocations, ahead
 int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
-               const unsigned long long* d_n_in = nullptr, const unsigned long long* d_n = nullptr, uint64_t n_est = 0);
+               const unsigned long long* d_n_in = nullptr, const unsigned long long* d_n = nullptr, uint64_t n_est = 0, bool est = false);
 int ensure_qdir(dbi_handle* h, hipStream_t s);  // query directory of the current index
 int finish_build(dbi_handle* h);
 

@@ -137,21 +137,13 @@ int read_counters(dbi_handle* h) {
 // that size the grids and buffers, every kernel reads the real count itself,
 // and n_est (the previous build's count) chooses the bins -- no host sync
 // between the digest and the tail.
-int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
-               const unsigned long long* d_n_in, const unsigned long long* d_n, uint64_t n_est) {
-    hipStream_t s = h->stream;
+// Every buffer the tail over n records (n_in slots) uses; build_tail calls it
+// before its first launch (a reallocation must never free a buffer that queued
+// kernels still use), callers that time the tail call it first.
+int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse, int passes, int bits_per) {
     int rc;
-    const uint32_t n32 = (uint32_t)n;
-    const uint32_t nbins = choose_nbins(d_n && n_est ? std::min(n_est, n) : n, h->bin_bits_max);
-    const BinMap bm = make_binmap(lo, hi, nbins);
-    int width[8] = {};
-    const int passes = radix_plan(nbins, sparse, width);
-    const int bits_per = passes ? width[passes - 1] : 0;  // the widest digit
-    const uint32_t n_in32 = sparse ? (uint32_t)n_in : n32;
+    const uint32_t n_in32 = sparse ? (uint32_t)n_in : (uint32_t)n;
     const size_t hist_elems = passes ? radix_hist_elems(n_in32, bits_per) : 1;
-
-    // every allocation before the first launch of this stage: a reallocation
-    // must never free a buffer that queued kernels still use
     const uint32_t T = h->chunk_t;
     const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + T - 1) / T, 1);
     const size_t seg_cap = giant_seg_cap(n);
@@ -165,11 +157,36 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
         (rc = h->umass.ensure(n)) || (rc = h->upid.ensure(n)) || (rc = h->uoff.ensure(n)) ||
         (rc = h->ulen.ensure(n)) || (rc = h->occ_off.ensure(n + 1)) || (rc = h->occ_pid.ensure(n)))
         return rc;
+    // stable LSD passes over the bin id write the next pass's digit of each record
+    if (passes > 1 && (rc = h->digits.ensure(std::max<uint64_t>(n, h->digits.cap)))) return rc;
+    return 0;
+}
+
+int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse) {
+    int width[8] = {};
+    const int passes = radix_plan(choose_nbins(n, h->bin_bits_max), sparse, width);
+    return tail_buffers(h, n, n_in, sparse, passes, passes ? width[passes - 1] : 0);
+}
+
+int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
+               const unsigned long long* d_n_in, const unsigned long long* d_n, uint64_t n_est, bool est) {
+    hipStream_t s = h->stream;
+    int rc;
+    const uint32_t n32 = (uint32_t)n;
+    const uint32_t nbins = choose_nbins(d_n && n_est ? std::min(n_est, n) : n, h->bin_bits_max);
+    const BinMap bm = make_binmap(lo, hi, nbins);
+    int width[8] = {};
+    const int passes = radix_plan(nbins, sparse, width);
+    const int bits_per = passes ? width[passes - 1] : 0;  // the widest digit
+    const uint32_t n_in32 = sparse ? (uint32_t)n_in : n32;
+    const uint32_t T = h->chunk_t;
+    const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + T - 1) / T, 1);
+    const size_t seg_cap = giant_seg_cap(n);
+    if ((rc = tail_buffers(h, n, n_in, sparse, passes, bits_per))) return rc;
 
     // stable LSD passes over the bin id; every pass but the last writes the
     // next pass's digit of each record (1 B) next to its output, so the next
     // histogram reads bytes instead of records
-    if (passes > 1 && (rc = h->digits.ensure(std::max<uint64_t>(n, h->digits.cap)))) return rc;
     Rec* src = h->recA.p;
     Rec* dst = h->recB.p;
     int shift = 0;
@@ -214,24 +231,30 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     // time); a longer list sets ERR_GRID and the build is redone with full grids.
     uint32_t max_mid = (uint32_t)std::min<uint64_t>(nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
     uint32_t max_big = (uint32_t)std::min<uint64_t>(nchunks, n / (CHUNK_CAP + 1) + 1);
-    if (d_n && h->grid_mid) max_mid = std::min(max_mid, h->grid_mid);
-    if (d_n && h->grid_big) max_big = std::min(max_big, h->grid_big);
+    est = est || d_n;
+    if (est && h->grid_mid) max_mid = std::min(max_mid, h->grid_mid);
+    if (est && h->grid_big) max_big = std::min(max_big, h->grid_big);
+    // the giant-chunk pass (seven launches) only when the last build had giant
+    // chunks: a giant chunk otherwise sets ERR_GRID and the build is redone
+    const bool giants = !est || h->giants_seen;
     STAGE(h, "chunk_sort_mid", by(0, 0, 0, 0, 0),
           launch_chunk_sort_mid(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->mid_list.p,
                                 max_mid, h->ctr.p, s));
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
           launch_chunk_sort_big(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                                h->giant_list.p, max_big, h->split_above, h->ctr.p, s));
-    STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
-          launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p, h->segs.p,
-                              seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
+                                giants ? h->giant_list.p : nullptr, max_big, h->split_above, h->ctr.p, s));
+    if (giants)
+        STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
+              launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,
+                                  h->segs.p, seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
     // unique offsets per chunk
     STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
           launch_scan_u32(h->ucount.p, h->ucount.p, nchunks, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_unique, s));
     // finalize: 16 B record in, 4 B occurrence protein id out, 24 B per unique out
     STAGE(h, "finalize", by(0, 20, 24, 0, 0),
           launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p,
-                          h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor, h->ctr.p, s));
+                          h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor,
+                          (uint32_t)std::min<size_t>(h->umass.cap, 0xFFFFFFFFu), h->ctr.p, s));
     DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s, d_n));
     h->stats.n_bins = nbins;
     return 0;
@@ -307,6 +330,7 @@ int finish_build(dbi_handle* h) {
     // the next device-sized tail's list grids: this build's lists plus a margin
     h->grid_mid = h->hc.n_mid + h->hc.n_mid / 8 + 32;
     h->grid_big = h->hc.n_big + h->hc.n_big / 8 + 16;
+    h->giants_seen = h->hc.n_giant > 0;
     ++h->build_serial;
     return 0;
 }
@@ -419,6 +443,7 @@ dbi_handle::GraphKey graph_key(const dbi_handle* h) {
     k.last_kept = h->last_kept;
     k.grid_mid = h->grid_mid;
     k.grid_big = h->grid_big;
+    k.giants = h->giants_seen;
     k.alloc_gen = g_alloc_gen.load(std::memory_order_relaxed);
     k.dp_gen = h->dp_gen;
     k.timing = h->timing;
@@ -440,9 +465,11 @@ int warm_body(dbi_handle* h, uint64_t* n_in, bool* sparse) {
     int rc = run_digest(h, &n, n_in, sparse, &dev);
     if (rc) return rc;
     if (!dev) return set_error(DBI_E_STATE, "internal: warm build without device sizing");
-    const unsigned long long* d_kept = &h->ctr.p->n_kept;
-    return build_tail(h, n, h->params.min_mh, h->params.max_mh, *n_in, *sparse,
-                      *sparse ? &h->ctr.p->n_slots : d_kept, d_kept, h->last_kept);
+    // the tail sorts what the digest wrote -- nothing when its slots did not
+    // fit (tiles that found no room left stale slots; build_digest redoes it)
+    DBI_HIP(launch_tail_counts(h->ctr.p, *n_in, *sparse, h->stream));
+    return build_tail(h, n, h->params.min_mh, h->params.max_mh, *n_in, *sparse, &h->ctr.p->tail_in,
+                      &h->ctr.p->tail_n, h->last_kept);
 }
 
 int build_digest(dbi_handle* h) {
@@ -522,6 +549,7 @@ int build_digest(dbi_handle* h) {
         drop_graph(h);
         h->prev_key_valid = false;
         h->grid_mid = h->grid_big = 0;
+        h->giants_seen = true;
         if (need > n_in && (rc = h->recA.ensure(need + need / 8))) return rc;
         DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), h->stream));
         h->nstage = 0;
@@ -946,6 +974,8 @@ void dbi_close(dbi_handle* h) {
     h->r_occ.release();
     drop_graph(h);
     for (auto& ev : h->evpool)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : h->ev_merge)
         if (ev) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;

@@ -163,6 +163,10 @@ struct Counters {
     unsigned int n_leaf_small, n_leaf_big, n_fallback;
     unsigned long long n_big_recs, n_giant_recs;  // records in chunks sorted by the big / giant paths
     unsigned int n_ck_stat[4];     // experiment builds (DBI_X_CKSTAT): compact-sort runs / range / order redo
+    // what the tail of a device-sized warm build sorts (k_tail_counts): the
+    // digest's slots / records, or 0 when they did not fit the buffer (the
+    // skipped tiles left stale slots behind; the build is redone)
+    unsigned long long tail_in, tail_n;
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads
     // (sharing the ticket's line cost the digest 30%)
@@ -224,6 +228,9 @@ constexpr unsigned long long REC_SENTINEL = ~0ull;
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                  const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s);
+// tail_in / tail_n of a device-sized build: the digest's slot and record
+// counts, or 0 / 0 when the slots needed exceed cap
+hipError_t launch_tail_counts(Counters* d_ctr, uint64_t cap, bool sparse, hipStream_t s);
 // COUNT with SQLiteMult bucket counts: d_hist[min((int)m / BUCKET_MASS_RANGE,
 // NUM_BUCKETS)] += each INCLUDE'd occurrence (NUM_BUCKETS <= HIST_MAX_BUCKETS)
 hipError_t launch_digest_count_hist(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
@@ -348,7 +355,8 @@ hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_ch
                                Counters* d_ctr, hipStream_t s);
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
-                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, Counters* d_ctr, hipStream_t s);
+                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, Counters* d_ctr,
+                           hipStream_t s);
 hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t factor, uint32_t* d_flags,
                             hipStream_t s);
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s,

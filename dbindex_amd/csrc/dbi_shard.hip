@@ -51,7 +51,7 @@ struct dbi_comm {
     // never fails an allocation between two collectives of a build
     double* d_samp = nullptr;              // nranks x (DBI_SHARD_SAMPLES + 2)
     unsigned long long* d_cnt = nullptr;   // nranks x cnt_row
-    int cnt_row = 0;                       // max(nranks + 2, 6)
+    int cnt_row = 0;                       // max(nranks + 2, 7)
 };
 constexpr uint32_t COMM_RED_MAX = 4096;
 
@@ -428,16 +428,35 @@ int dbi_shard_samples(dbi_handle* h, double* samples) {
 }
 
 int dbi_shard_splitters(const double* samples, int nshards, int32_t factor, int32_t* split) {
+    return dbi_shard_splitters_cost(samples, nshards, factor, 0, nullptr, nullptr, split);
+}
+
+int dbi_shard_splitters_cost(const double* samples, int nshards, int32_t factor, int nbands,
+                             const int32_t* band_split, const double* band_cost, int32_t* split) {
     if (!samples || (!split && nshards > 1)) return set_error(DBI_E_INVALID, "NULL argument");
     if (nshards < 1 || nshards > MAX_SHARDS) return set_error(DBI_E_INVALID, "1..64 shards");
     if (factor <= 0) return set_error(DBI_E_INVALID, "mass_group_factor must be > 0");
+    if (band_cost) {
+        if (nbands < 1 || (nbands > 1 && !band_split)) return set_error(DBI_E_INVALID, "bad band profile");
+        for (int r = 0; r < nbands; ++r)
+            if (!(band_cost[r] > 0.0) || !std::isfinite(band_cost[r]))
+                return set_error(DBI_E_INVALID, "band costs must be finite and > 0");
+        for (int r = 0; r + 2 < nbands; ++r)
+            if (band_split[r] > band_split[r + 1]) return set_error(DBI_E_INVALID, "band splits must ascend");
+    }
     std::vector<std::pair<int32_t, double>> ks;
     for (int r = 0; r < nshards; ++r) {
         const double* b = samples + (size_t)r * (NS + 1);
         const double w = b[NS];
         if (!(w > 0.0)) continue;
-        for (uint32_t i = 0; i < NS; ++i)
-            if (b[i] == b[i]) ks.emplace_back(java_d2i(b[i] * (double)factor), w);
+        for (uint32_t i = 0; i < NS; ++i) {
+            if (b[i] != b[i]) continue;
+            const int32_t k = java_d2i(b[i] * (double)factor);
+            double c = 1.0;
+            if (band_cost)  // band of k: the number of band boundaries <= k
+                c = band_cost[std::upper_bound(band_split, band_split + (nbands - 1), k) - band_split];
+            ks.emplace_back(k, w * c);
+        }
     }
     std::sort(ks.begin(), ks.end());
     double total = 0.0;
@@ -458,6 +477,49 @@ int dbi_shard_splitters(const double* samples, int nshards, int32_t factor, int3
         split[j - 1] = sp;
     }
     return 0;
+}
+
+namespace {
+constexpr int CB = DBI_COST_BANDS;
+// the fixed key bands of the cost profile: CB equal key ranges of [minMH, maxMH]
+void cost_bands(const dbi_handle* h, int32_t* bsplit) {
+    const double f = (double)h->params.mass_group_factor;
+    const double k0 = h->params.min_mh * f, k1 = h->params.max_mh * f;
+    for (int b = 1; b < CB; ++b) bsplit[b - 1] = (int32_t)std::floor(k0 + (k1 - k0) * (double)b / (double)CB);
+}
+}  // namespace
+
+int dbi_shard_cost_update(dbi_handle* h, int nshards, const int32_t* split, const double* merge_ms,
+                          const uint64_t* records) {
+    if (!h || !merge_ms || !records || (nshards > 1 && !split)) return set_error(DBI_E_INVALID, "NULL argument");
+    if (nshards < 2 || nshards > MAX_SHARDS) return 0;  // one owner: nothing to balance
+    for (int r = 0; r < nshards; ++r)
+        if (!(merge_ms[r] > 0.0) || records[r] == 0) return 0;  // an owner without a measurement: keep the profile
+    int32_t bs[CB - 1];
+    cost_bands(h, bs);
+    // each band takes the cost per record of the owner holding its middle key,
+    // averaged with what it had (the owners' ranges move between builds, so
+    // the bands see different owners: the average settles instead of swinging)
+    auto& pf = h->shard_prof;
+    const double f = (double)h->params.mass_group_factor;
+    const double k0 = h->params.min_mh * f, k1 = h->params.max_mh * f;
+    for (int b = 0; b < CB; ++b) {
+        const double mid = k0 + (k1 - k0) * ((double)b + 0.5) / (double)CB;
+        int r = 0;
+        while (r + 1 < nshards && (double)split[r] <= mid) ++r;
+        const double c = merge_ms[r] / (double)records[r];
+        pf.cost[b] = pf.valid ? 0.5 * pf.cost[b] + 0.5 * c : c;
+    }
+    std::copy(bs, bs + CB - 1, pf.split);
+    pf.valid = true;
+    return 0;
+}
+
+int dbi_shard_splitters_profiled(dbi_handle* h, const double* samples, int nshards, int32_t* split) {
+    if (!h) return set_error(DBI_E_INVALID, "NULL handle");
+    const auto& pf = h->shard_prof;
+    return dbi_shard_splitters_cost(samples, nshards, h->params.mass_group_factor, pf.valid ? CB : 0,
+                                    pf.valid ? pf.split : nullptr, pf.valid ? pf.cost : nullptr, split);
 }
 
 }  // extern "C"
@@ -596,23 +658,47 @@ int dbi_shard_merge(dbi_handle* h) {
     h->n_res = sh.n_res_global;
     h->n_prot = sh.n_prot_global;
     h->n_total_extra = 0;
-    // counters back to zero (the layout word max_plen stays), n_kept = records received
-    DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
-    hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(64), 0, s, &h->ctr.p->n_kept, (unsigned long long)sh.n_recv);
-    DBI_HIP(hipGetLastError());
-    // the received location words -> records (mass + tag from the residues);
-    // recA is free (the partition read it before the exchange was enqueued)
     if ((rc = h->recA.ensure(std::max<uint64_t>(sh.n_recv, 1)))) return rc;
-    STAGE(h, "owner_expand", by(0, 0, 0, 0, 0),
-          launch_expand_locs(h->xrecv.p, sh.n_recv, h->d_res, h->d_poff, h->mass_tab.p, h->dp.m0, sh.width, h->recA.p, s));
-    h->stages[h->nstage - 1].c0 = 24.0 * (double)sh.n_recv;  // 8 B in, 16 B out (+ the residues)
     int32_t klo, khi;
     key_range(sh.split, sh.nshards, sh.rank, &klo, &khi);
     const double f = (double)h->params.mass_group_factor;
     const double lo = klo == INT32_MIN ? h->params.min_mh : std::max(h->params.min_mh, (double)klo / f);
     const double hi = khi == INT32_MAX ? h->params.max_mh : std::min(h->params.max_mh, (double)khi / f);
-    if ((rc = build_tail(h, sh.n_recv, lo, std::max(hi, lo), sh.n_recv, false))) return rc;
-    if ((rc = finish_build(h))) return rc;
+    // the chunk-list grids (and whether to run the giant pass) from this
+    // owner's previous merge; lists that outgrow them (ERR_GRID) and the
+    // merge runs again from the received words, with this merge's lists
+    for (int e = 0; e < 2; ++e)
+        if (!h->ev_merge[e]) DBI_HIP(hipEventCreate(&h->ev_merge[e]));
+    // every buffer of the tail first: the merge's device time (the cost
+    // profile's measure) then has no host allocation inside it
+    if ((rc = tail_buffers(h, sh.n_recv, sh.n_recv, false))) return rc;
+    const bool first = h->build_serial == 0;  // the handle's first build also loads the code objects: not timed
+    for (int attempt = 0;; ++attempt) {
+        const int nstage0 = h->nstage;
+        DBI_HIP(hipEventRecord(h->ev_merge[0], s));
+        // counters back to zero (the layout word max_plen stays), n_kept = records received
+        DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
+        hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(64), 0, s, &h->ctr.p->n_kept, (unsigned long long)sh.n_recv);
+        DBI_HIP(hipGetLastError());
+        // the received location words -> records (mass + tag from the residues);
+        // recA is free (the partition read it before the exchange was enqueued)
+        STAGE(h, "owner_expand", by(0, 0, 0, 0, 0),
+              launch_expand_locs(h->xrecv.p, sh.n_recv, h->d_res, h->d_poff, h->mass_tab.p, h->dp.m0, sh.width,
+                                 h->recA.p, s));
+        h->stages[h->nstage - 1].c0 = 24.0 * (double)sh.n_recv;  // 8 B in, 16 B out (+ the residues)
+        if ((rc = build_tail(h, sh.n_recv, lo, std::max(hi, lo), sh.n_recv, false, nullptr, nullptr, 0,
+                             attempt == 0)))
+            return rc;
+        DBI_HIP(hipEventRecord(h->ev_merge[1], s));
+        if ((rc = finish_build(h))) return rc;  // (synchronises)
+        float mg = 0.f;
+        sh.ms_merge_gpu =
+            !first && hipEventElapsedTime(&mg, h->ev_merge[0], h->ev_merge[1]) == hipSuccess ? (double)mg : 0.0;
+        if (!(h->hc.err & ERR_GRID)) break;
+        if (attempt > 0) return set_error(DBI_E_STATE, "internal: chunk lists outgrew full grids");
+        h->nstage = nstage0;
+        h->giants_seen = true;
+    }
     sh.ms_merge = now_ms() - t0;
     sh.phase = 4;
     return 0;
@@ -623,6 +709,7 @@ int dbi_shard_stats_get(dbi_handle* h, dbi_shard_stats* out) {
     const ShardState& sh = h->shard;
     if (sh.phase < 1) return set_error(DBI_E_STATE, "no sharded build on this handle");
     dbi_shard_stats st = sh.global;
+    st.merge_gpu_ms = sh.ms_merge_gpu;
     st.rank = sh.rank;
     st.nshards = sh.nshards;
     st.p_begin = sh.p_begin;
@@ -871,7 +958,7 @@ int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_co
         delete c;
         return set_error(DBI_E_OOM, "hipMalloc (communicator status word)");
     }
-    c->cnt_row = std::max(nranks + 2, 6);
+    c->cnt_row = std::max(nranks + 2, 7);  // count matrix row | the totals row (7)
     if (hipMalloc((void**)&c->d_red, COMM_RED_MAX * sizeof(double)) != hipSuccess ||
         hipMalloc((void**)&c->d_samp, sizeof(double) * (size_t)nranks * (NS + 2)) != hipSuccess ||
         hipMalloc((void**)&c->d_cnt, sizeof(unsigned long long) * (size_t)nranks * c->cnt_row) != hipSuccess ||
@@ -1054,7 +1141,8 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
         packed[(size_t)r * (NS + 1) + NS] = valid ? b[NS] / (double)valid : 0.0;  // as dbi_shard_samples
     }
     int32_t split[MAX_SHARDS - 1] = {};
-    if ((rc = dbi_shard_splitters(packed.data(), n, h->params.mass_group_factor, split))) return rc;  // same everywhere
+    // the same everywhere: every rank holds the same samples and cost profile
+    if ((rc = dbi_shard_splitters_profiled(h, packed.data(), n, split))) return rc;
     sh.ms_digest = now_ms() - t_digest;
     const double t_part = now_ms();
     int rc_part = partition_launch(h, split);
@@ -1134,11 +1222,12 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // whole-index totals (+ status), and where this owner's rows start in the whole index
     std::vector<uint64_t> tot(5, 0);
     {
-        const int wt = 6;
+        const int wt = 7;
         std::vector<unsigned long long> row(wt, 0), rows((size_t)n * wt);
         row[0] = sh.n_total; row[1] = sh.n_dropped; row[2] = sh.n_recv; row[3] = h->stats.n_unique;
         row[4] = h->stats.n_keys;
         row[5] = rc_merge ? 1u : 0u;
+        row[6] = rc_merge ? 0u : (unsigned long long)(sh.ms_merge_gpu * 1e6);  // ns
         DBI_HIP(hipMemcpyAsync(c->d_cnt + (size_t)me * wt, row.data(), sizeof(uint64_t) * wt, hipMemcpyHostToDevice, s));
         DBI_NCCL(ncclAllGather(c->d_cnt + (size_t)me * wt, c->d_cnt, wt, ncclUint64, c->comm, s));
         DBI_HIP(hipMemcpyAsync(rows.data(), c->d_cnt, sizeof(uint64_t) * n * wt, hipMemcpyDeviceToHost, s));
@@ -1151,6 +1240,16 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
             if (i < me) sh.u_base += rows[(size_t)i * wt + 3];
         }
         sh.u_base_known = true;
+        // the cost profile for the next build: every owner's merge device time
+        // and records over its key range (the same numbers, hence the same
+        // profile, on every rank)
+        std::vector<double> mms(n);
+        std::vector<uint64_t> recs(n);
+        for (int i = 0; i < n; ++i) {
+            mms[i] = (double)rows[(size_t)i * wt + 6] * 1e-6;
+            recs[i] = rows[(size_t)i * wt + 2];
+        }
+        if ((rc = dbi_shard_cost_update(h, n, sh.split, mms.data(), recs.data()))) return rc;
     }
     sh.global.g_total = tot[0];
     sh.global.g_dropped = tot[1];

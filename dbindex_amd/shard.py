@@ -50,12 +50,19 @@ def protein_ranges(offsets: np.ndarray, nshards: int) -> List[Tuple[int, int]]:
     return [(bounds[r], bounds[r + 1]) for r in range(nshards)]
 
 
-def splitters(samples: np.ndarray, nshards: int, factor: int) -> np.ndarray:
+def splitters(samples: np.ndarray, nshards: int, factor: int, profile=None) -> np.ndarray:
     """Owner key splitters from every shard's samples (dbi_shard_splitters, host
-    only): ``samples`` = nshards blocks of SHARD_SAMPLES masses + 1 weight."""
+    only): ``samples`` = nshards blocks of SHARD_SAMPLES masses + 1 weight.
+    ``profile`` = (band_split, band_cost): balance records x the cost per
+    record of their key band instead of records (dbi_shard_splitters_cost)."""
     s = np.ascontiguousarray(samples, np.float64).reshape(nshards * (SHARD_SAMPLES + 1))
     out = np.zeros(max(nshards - 1, 1), np.int32)
-    check(_native.lib().dbi_shard_splitters(_p(s), nshards, factor, _p(out)))
+    if profile is None:
+        check(_native.lib().dbi_shard_splitters(_p(s), nshards, factor, _p(out)))
+    else:
+        bc = np.ascontiguousarray(profile[1], np.float64)
+        bs = np.ascontiguousarray(np.concatenate([np.asarray(profile[0], np.int32), np.zeros(1, np.int32)]), np.int32)
+        check(_native.lib().dbi_shard_splitters_cost(_p(s), nshards, factor, bc.shape[0], _p(bs), _p(bc), _p(out)))
     return out[: nshards - 1]
 
 
@@ -151,9 +158,12 @@ def build_sharded(eng: Engine, comm: ShardComm, d_res: int, n_res: int, d_off: i
 
 
 def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off: int, n_prot: int,
-                        ranges: Sequence[Tuple[int, int]]) -> np.ndarray:
+                        ranges: Sequence[Tuple[int, int]], profile=None, balance: bool = False) -> np.ndarray:
     """Every shard's handle in this process (exchange by device copies): the
-    phases of dbi_build_sharded one by one.  Returns the owner splitters."""
+    phases of dbi_build_sharded one by one.  ``profile`` = (band_split,
+    band_cost): cost-balanced splitters; ``balance``: the splitters follow the
+    merge-cost profile engines[0] keeps and this build updates, as
+    dbi_build_sharded does.  Returns the owner splitters."""
     n = len(engines)
     assert 1 <= n <= MAX_SHARDS and len(ranges) == n
     L = _native.lib()
@@ -163,7 +173,13 @@ def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off
         row = np.zeros(SHARD_SAMPLES + 1, np.float64)
         check(L.dbi_shard_samples(eng.h, _p(row)))
         samples[r] = row
-    split = splitters(samples, n, engines[0].cparams.mass_group_factor)
+    if balance:
+        s = np.ascontiguousarray(samples, np.float64).reshape(n * (SHARD_SAMPLES + 1))
+        out = np.zeros(max(n - 1, 1), np.int32)
+        check(L.dbi_shard_splitters_profiled(engines[0].h, _p(s), n, _p(out)))
+        split = out[: n - 1]
+    else:
+        split = splitters(samples, n, engines[0].cparams.mass_group_factor, profile)
     sp = np.ascontiguousarray(np.concatenate([split, np.zeros(1, np.int32)]), np.int32)
     for eng in engines:
         cnt = np.zeros(n, np.uint64)
@@ -172,6 +188,12 @@ def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off
     check(L.dbi_shard_exchange_local(hs, n))
     for eng in engines:
         check(L.dbi_shard_merge(eng.h))
+    if balance:
+        sts = [shard_stats(e) for e in engines]
+        mms = np.array([st.merge_gpu_ms for st in sts], np.float64)
+        recs = np.array([st.n_received for st in sts], np.uint64)
+        sp = np.ascontiguousarray(np.concatenate([split, np.zeros(1, np.int32)]), np.int32)
+        check(L.dbi_shard_cost_update(engines[0].h, n, _p(sp), _p(mms), _p(recs)))
     return split
 
 

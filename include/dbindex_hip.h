@@ -308,6 +308,7 @@ typedef struct dbi_shard_stats {
     /* whole-index totals (sums over shards; filled by dbi_build_sharded) */
     uint64_t g_total, g_dropped, g_kept, g_unique, g_keys;
     double digest_ms, partition_ms, exchange_ms, merge_ms; /* wall time of each phase      */
+    double merge_gpu_ms;          /* device time of this owner's merge kernels             */
 } dbi_shard_stats;
 
 /* Digest proteins [p_begin, p_end) of the global arrays (device pointers:
@@ -322,6 +323,22 @@ int dbi_shard_samples(dbi_handle* h, double* samples);
  * 1..nshards-1 (weighted quantiles: balanced record counts).  Deterministic: every
  * shard computes the same split from the same samples. */
 int dbi_shard_splitters(const double* samples, int nshards, int32_t factor, int32_t* split);
+/* The same with a cost profile: nbands key bands (band_split[0..nbands-1)
+ * their boundaries, ascending) of cost per record band_cost[0..nbands): the
+ * splitters balance sum(records x cost of their band) instead of records.
+ * band_cost NULL: dbi_shard_splitters. */
+int dbi_shard_splitters_cost(const double* samples, int nshards, int32_t factor, int nbands,
+                             const int32_t* band_split, const double* band_cost, int32_t* split);
+/* The handle's own merge-cost profile (the one dbi_build_sharded keeps): a
+ * smoothed cost per record over DBI_COST_BANDS fixed key bands of
+ * [minMH, maxMH], updated from one build's owners (their key ranges = split,
+ * their merge device time and records); dbi_shard_splitters_profiled then
+ * balances that cost.  A profile only steers the splitters: any split gives
+ * the same index. */
+#define DBI_COST_BANDS 256
+int dbi_shard_cost_update(dbi_handle* h, int nshards, const int32_t* split, const double* merge_ms,
+                          const uint64_t* records);
+int dbi_shard_splitters_profiled(dbi_handle* h, const double* samples, int nshards, int32_t* split);
 /* Route this shard's records by owner (stable; global protein ids);
  * send_count[0..nshards) = records for each owner. */
 int dbi_shard_partition(dbi_handle* h, const int32_t* split, uint64_t* send_count);

@@ -16,8 +16,8 @@ sources (paths relative to /root/reference/src/main/java/edu/scripps/yates/dbind
 
 Only for small inputs (pure-Python loops).  Agreement with the C++ oracle is
 bit-exact (masses compared as float64 bit patterns).  Ties between different
-peptides of identical mass inside one row are ordered by (16-bit FNV-1a tag of
-the string, first appearance): the reference's THashMap order is unspecified,
+peptides of identical mass inside one row are ordered by (16-bit tag of the
+string -- its length and first / last four residues hashed --, first appearance): the reference's THashMap order is unspecified,
 so this project pins it (DESIGN.md semantics A7).
 """
 from __future__ import annotations

@@ -116,15 +116,17 @@ def test_big_bins_and_duplicates(Engine, copies):
         assert_index_equal(eng, oix, f"bigbins x{copies}")
 
 
-def test_list_grids_outgrown(Engine):
+@pytest.mark.parametrize("copies", [3000, 9000])
+def test_list_grids_outgrown(Engine, copies):
     """Warm builds size the mid / big chunk-list grids from the previous
-    build's lists; a build with far more big chunks than the last one
-    outgrows them (ERR_GRID) and is redone with full grids -- same index as
-    the oracle.  Then the first proteome again on the larger grids."""
+    build's lists and skip the giant-chunk pass when it had no giant chunks; a
+    build with far more big chunks (3000 copies of one protein) or with giant
+    ones (9000) than the last one outgrows them (ERR_GRID) and is redone --
+    same index as the oracle.  Then the first proteome again."""
     cp = DBIndexSearchParams.trypsin(2).to_c()
-    plain = fasta.config("human").slice(0, 6000)
+    plain = fasta.config("human").slice(0, 12000)
     base = fasta.config("1k").sequence(5)
-    seqs = [base] * 3000 + [fasta.config("1k").sequence(i) for i in range(6, 40)]
+    seqs = [base] * copies + [fasta.config("1k").sequence(i) for i in range(6, 40)]
     big = fasta.PackedProteins.from_sequences(seqs)
     assert big.residues.size < plain.residues.size  # the second build stays warm (no regrowth)
     o_plain = cref.Index(cp, plain.residues, plain.offsets)
@@ -135,7 +137,7 @@ def test_list_grids_outgrown(Engine):
         assert_index_equal(eng, o_plain, "list grids: plain [cold]")
         st = eng.build(big)
         assert st.n_big_bins > 16
-        assert_index_equal(eng, o_big, "list grids: big chunks [warm, outgrown]")
+        assert_index_equal(eng, o_big, f"list grids: x{copies} [warm, outgrown]")
         for k in range(2):
             eng.build(plain)
             assert_index_equal(eng, o_plain, f"list grids: plain again [{k}]")

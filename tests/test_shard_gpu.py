@@ -299,3 +299,58 @@ def test_bucket_counts_rccl_allreduce_single_rank(native):
         assert np.array_equal(d_sum.download(np.uint64, nb + 1), want)
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("copies", [3000, 9000])
+def test_sharded_merge_grids_outgrown(native, copies):
+    """Owner merges size their chunk-list grids (and skip the giant pass) from
+    the previous merge on the same handle; a proteome with many more big or
+    with giant chunks outgrows them (ERR_GRID) and the merge runs again from
+    the received words -- equal to the oracle, then the first proteome again."""
+    from dbindex_amd.engine import Engine
+    prm = DBIndexSearchParams.trypsin(2)
+    cp = prm.to_c()
+    plain = fasta.config("human").slice(0, 4000)
+    base = fasta.config("1k").sequence(5)
+    big = fasta.PackedProteins.from_sequences([base] * copies + [fasta.config("1k").sequence(i) for i in range(6, 40)])
+    engines = [Engine(cp, 0) for _ in range(3)]
+    try:
+        for name, pp in (("plain", plain), (f"x{copies}", big), ("plain again", plain)):
+            oix = cref.Index(cp, pp.residues, pp.offsets)
+            d_res, d_off = _inputs(native, pp)
+            shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
+                                      shard.protein_ranges(pp.offsets, 3))
+            _assert_sharded_equal(engines, oix, f"merge grids: {name}")
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_sharded_cost_profile_splitters(native):
+    """Splitters balanced by the merge-cost profile a handle keeps (updated
+    by every build, as dbi_build_sharded does) or by an arbitrary skewed one
+    move the owner key ranges; the index, the queries and the routed queries
+    stay the oracle's."""
+    from dbindex_amd.engine import Engine
+    prm = DBIndexSearchParams.trypsin(2)
+    cp = prm.to_c()
+    pp = fasta.config("human").slice(0, 6000)
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    d_res, d_off = _inputs(native, pp)
+    ranges = shard.protein_ranges(pp.offsets, 4)
+    engines = [Engine(cp, 0) for _ in range(4)]
+    try:
+        sp0 = None
+        for rep in range(3):
+            sp = shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, ranges,
+                                           balance=True)
+            sp0 = sp if sp0 is None else sp0
+            _assert_sharded_equal(engines, oix, f"profile: measured merge cost [{rep}]")
+            assert all(shard.shard_stats(e).merge_gpu_ms > 0 for e in engines) or rep == 0  # (first: untimed)
+        sp2 = shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, ranges,
+                                        profile=(sp0, np.array([20.0, 1.0, 1.0, 5.0])))
+        assert sp2[0] < sp0[0]
+        _assert_sharded_equal(engines, oix, "profile: skewed")
+    finally:
+        for e in engines:
+            e.close()

@@ -50,6 +50,30 @@ def test_splitters_balance_and_determinism():
         assert counts.max() <= 1.1 * allm.shape[0] / k, counts
 
 
+def test_splitters_cost_profile():
+    """dbi_shard_splitters_cost: uniform band costs give the record-balanced
+    splitters; a costly band gets fewer records, so that records x cost
+    balance across owners (dbi_build_sharded's feedback between builds)."""
+    rng = np.random.Generator(np.random.PCG64(6))
+    blocks = [np.sort(rng.lognormal(7.3, 0.4, n)) for n in (60_000, 60_000, 60_000, 60_000)]
+    s = _samples_of(blocks)
+    k, f = 4, 10000
+    sp = shard.splitters(s, k, f)
+    assert np.array_equal(shard.splitters(s, k, f, profile=(sp, np.full(k, 2.5))), sp)
+    assert np.array_equal(shard.splitters(s, k, f, profile=(np.zeros(0, np.int32), np.full(1, 3.0))), sp)
+    cost = np.array([3.0, 1.0, 1.0, 1.0])
+    sp2 = shard.splitters(s, k, f, profile=(sp, cost))
+    assert sp2[0] < sp[0] and np.all(np.diff(sp2.astype(np.int64)) >= 0)
+    allm = np.concatenate(blocks)
+    band = shard.owner_of(allm, sp, f)
+    own = shard.owner_of(allm, sp2, f)
+    load = np.bincount(own, weights=cost[band], minlength=k)
+    assert load.max() <= 1.1 * load.sum() / k, load
+    assert np.array_equal(sp2, shard.splitters(s, k, f, profile=(sp, cost)))  # deterministic
+    with pytest.raises(Exception, match="band costs"):
+        shard.splitters(s, k, f, profile=(sp, np.array([1.0, 0.0, 1.0, 1.0])))
+
+
 def test_splitters_edge_cases():
     # no records anywhere: every key belongs to owner 0
     empty = _samples_of([[], []])

@@ -2,7 +2,9 @@
 
   python tools/shard_budget.py [--config swissprot] [--shards 8] [--reps 3]
 
-Builds the proteome as N local shards (N handles on this GPU, the phases of an
+Builds the proteome as N local shards (each build after the first with the
+splitters balanced by the previous build's owner merge costs, as
+dbi_build_sharded does; --no-balance: record-balanced splitters only) (N handles on this GPU, the phases of an
 N-rank dbi_build_sharded with dbi_shard_exchange_local copies in place of the
 RCCL exchange), every kernel timed by its HIP events, and prints one JSON
 object: for each shard its digest / partition / merge kernel time and the
@@ -42,6 +44,7 @@ def main() -> int:
     ap.add_argument("--config", default="swissprot")
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--no-balance", action="store_true", help="record-balanced splitters on every build")
     a = ap.parse_args()
     from dbindex_amd import fasta, shard
     from dbindex_amd._native import DeviceBuffer, synchronize
@@ -59,8 +62,11 @@ def main() -> int:
     try:
         for e in engines:
             e.set_timing(True)
+        history = []
         for _ in range(a.reps):
-            shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, ranges)
+            # each build balances the owners' merge cost measured so far (as dbi_build_sharded does)
+            split = shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, ranges,
+                                              balance=not a.no_balance)
             rows = []
             for r, e in enumerate(engines):
                 st = shard.shard_stats(e)
@@ -90,12 +96,15 @@ def main() -> int:
             link_bytes = max(8.0 * max(x["n_sent"], from_others(x)) / max(k - 1, 1) for x in rows)
             xch = link_bytes / (LINK_GBS * 1e6)
             tot = front + xch + back
+            history.append(dict(merge_max_ms=back, model_ms_without_fixed=tot,
+                                merge_ms=[round(x["merge_ms"], 3) for x in rows], split=[int(v) for v in split]))
             if best is None or tot < best["model_ms_without_fixed"]:
                 best = dict(config=a.config, shards=k, rows=rows, front_ms=front, exchange_model_ms=xch,
                             merge_max_ms=back, model_ms_without_fixed=tot, link_gbs=LINK_GBS)
     finally:
         for e in engines:
             e.close()
+    best["history"] = history
     print(json.dumps(best))
     return 0
 
