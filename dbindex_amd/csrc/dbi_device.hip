@@ -411,19 +411,6 @@ __device__ __forceinline__ bool n_ok_at(const DigestSmem& sm, const TileCtx& tc,
 }
 
 __device__ uint4 g_zero16;  // load target of lanes with nothing to load (stays zero)
-#ifdef DBI_X_PHASE
-__device__ unsigned long long g_phase[32];  // experiment builds: phase clocks [kernel*8 + phase] (24..: digest)
-#define DBI_DPH(i)                                                               \
-    do {                                                                         \
-        const uint64_t t_ = wall_clock64();                                      \
-        if (threadIdx.x == 0) atomicAdd(&g_phase[24 + (i)], t_ - dph_t);         \
-        dph_t = t_;                                                              \
-    } while (0)
-#else
-#define DBI_DPH(i) \
-    do {           \
-    } while (0)
-#endif
 
 // Stage the tile's window (residues + class flags + cut / protein-end flags)
 // and the residue tables in LDS, and compact the candidate starts (every start
@@ -1473,14 +1460,10 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     __shared__ uint32_t s_kept, s_waves;
     __shared__ unsigned long long s_base;
     const uint32_t tid = threadIdx.x;
-#ifdef DBI_X_PHASE
-    uint64_t dph_t = wall_clock64();
-#endif
     if (tid == 0) {  // read at the end, behind many barriers
         s_kept = 0;
         s_waves = 0;
     }
-    DBI_DPH(0);
     const uint32_t tile = blockIdx.x, ntiles = gridDim.x;
     const uint32_t t0 = tile * (uint32_t)DIGEST_TILE;
     const uint32_t t_end = min(t0 + (uint32_t)DIGEST_TILE, n_res);
@@ -1571,7 +1554,6 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
         if (i < PST_CAP) sm.pst[i] = o;
     }
     __syncthreads();
-    DBI_DPH(1);
     // cut and N_ok maps, 64 positions per thread from the bit maps:
     //   last     = a protein starts at q+1
     //   cut      = last || (cleave(q) && !nocut(q+1))        (checkCleavage C side)
@@ -1594,7 +1576,6 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
         nokm[w] = (st | (((cl << 1) | (cl_p >> 63)) & ~nc)) & valid;
     }
     __syncthreads();
-    DBI_DPH(2);
     // cleavage-site compaction: thread t owns starts [16t, 16t+16) of the tile, in order
     const uint32_t off = lb + (t0 - w0);  // LDS position of the tile's first start
     const uint32_t n_here = t0 + tid * STARTS_PER_THREAD < t_end
@@ -1607,7 +1588,6 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     for (int k = 0; k < STARTS_PER_THREAD; ++k)
         if (mybits & (1u << k)) sm.cand[pos++] = (uint16_t)(tid * STARTS_PER_THREAD + k);
     __syncthreads();
-    DBI_DPH(3);
 
     const uint32_t B = (uint32_t)dp.max_missed + 2u;  // records per start, at most
     const uint32_t min_len = (uint32_t)dp.min_len;
@@ -1615,7 +1595,6 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     const uint32_t w = rec_width(d_ctr->max_plen);
     if (tile == 0 && tid == 0 && !rec_layout_ok(w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
     balance_candidates(sm.cand, s_cnt, ncand, B, t_end - t0);
-    DBI_DPH(4);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
     // slot bounds: the candidate ends (B for a walk that may leave the horizon)
@@ -1626,14 +1605,12 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     }
     uint32_t tile_slots;
     const uint32_t excl_t = block_excl_scan<DIGEST_THREADS, uint32_t>(lim, sm.tmp, tile_slots);
-    DBI_DPH(5);
     // the tile's output region: one atomic add, in whatever order the tiles
     // get here (no tile waits for another; the chunk sort does not need
     // records in first-appearance order, ck_fix_runs); ctr->n_slots ends as
     // the total
     if (tid == 0) s_base = atomicAdd(&d_ctr->n_slots, (unsigned long long)tile_slots);
     __syncthreads();
-    DBI_DPH(6);
     const unsigned long long base = s_base;
     if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
     Rec* __restrict__ o = d_out + base + excl_t;
@@ -1658,10 +1635,6 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     if (kept > lim) atomicOr(&d_ctr->err, ERR_SLOTS);  // the bound is an upper bound: never
     const Rec sent{REC_SENTINEL, REC_SENTINEL};
     for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
-#ifdef DBI_X_PHASE
-    __syncthreads();
-    DBI_DPH(7);
-#endif
     if (DROP) {
         const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
         const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
@@ -2545,9 +2518,6 @@ __device__ void block_bitonic(unsigned long long* k0, unsigned long long* k1, ui
 // (w*64R + lane*R + r of the block): the all-ascending flip network, register
 // pairs for distances < R, DPP / row swaps above (dbi_lane.h), LDS only across
 // waves.
-#ifdef DBI_X_CKSTAT
-__device__ unsigned int g_ck_stat[8];
-#endif
 constexpr int CK_IDX_BITS = 13;
 constexpr int CK_D_BITS = 64 - 16 - CK_IDX_BITS;
 
@@ -2689,10 +2659,6 @@ __device__ bool ck_run_wave(unsigned long long* k0, unsigned long long* k1, uint
         key[r] = ~0ull;
         if (i < L) ok &= ck_make(k0[lo + i], k1[lo + i], mb0, i, key[r]);
     }
-#ifdef DBI_X_CKSTAT
-    if (lane == 0) atomicAdd(&g_ck_stat[0], 1u);
-    if (__ballot(!ok) && lane == 0) atomicAdd(&g_ck_stat[1], 1u);
-#endif
     if (__ballot(!ok)) return false;
     ck_sort_wave<R, 64 * R>(key);
     // q0 comes back out of the key itself; q1 is gathered by the arrival index
@@ -2782,15 +2748,6 @@ __device__ bool ck_run_block(unsigned long long* k0, unsigned long long* k1, uin
         key[r] = ~0ull;
         if (i0 + r < L) ok &= ck_make(k0[lo + i0 + r], k1[lo + i0 + r], mb0, i0 + r, key[r]);
     }
-#ifdef DBI_X_CKSTAT
-    {
-        const int nok = __syncthreads_or(!ok);
-        if (threadIdx.x == 0) {
-            atomicAdd(&g_ck_stat[NT == 512 ? 3 : 6], 1u);
-            if (nok) atomicAdd(&g_ck_stat[NT == 512 ? 4 : 7], 1u);
-        }
-    }
-#endif
     if (__syncthreads_or(!ok)) return false;
     const bool live = (threadIdx.x >> 6) * WE < L;  // wave-uniform: waves past the run hold +inf only
     if (live) ck_sort_wave<R, WE>(key);
@@ -2991,19 +2948,6 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
     static_assert(E <= 32, "run-head bit mask");
     unsigned long long* k0 = sm.k0;
     unsigned long long* k1 = sm.k1;
-#ifdef DBI_X_PHASE
-    uint64_t ph_t = wall_clock64();
-#define DBI_PH(i)                                                                               \
-    do {                                                                                        \
-        const uint64_t t_ = wall_clock64();                                                     \
-        if (threadIdx.x == 0) atomicAdd(&g_phase[(BLOCK ? (NT == 512 ? 8 : 16) : 0) + (i)], t_ - ph_t); \
-        ph_t = t_;                                                                              \
-    } while (0)
-#else
-#define DBI_PH(i) \
-    do {          \
-    } while (0)
-#endif
     if (threadIdx.x == 0) {
         sm.nbig = 0;
         sm.wide = 0;
@@ -3027,7 +2971,6 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         }
     }
     __syncthreads();
-    DBI_PH(1);
     // bin runs: thread t owns records [t*E, t*E+E); run bounds of each record
     // from a block max-scan (last run start <= i) and a reverse min-scan
     // (first run start > i), kept in registers
@@ -3069,7 +3012,6 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         }
     }
     __syncthreads();
-    DBI_PH(2);
     if (!BLOCK && sm.wide) return false;
     // small bins: rank inside the bin (k-major: a wave's lanes share bins), kept in registers with the key
     // (ranking by a 64-bit compact key instead measured slower: the extra
@@ -3101,7 +3043,6 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
             }
         }
     }
-    DBI_PH(3);
     // big bins, in place (disjoint from the small bins)
     const uint32_t nbig = sm.nbig;
     for (uint32_t r = threadIdx.x >> 6; r < nbig; r += NW) {
@@ -3117,24 +3058,17 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         if (!done) wave_bitonic(k0, k1, lo, L);
     }
     __syncthreads();
-    DBI_PH(4);
     if constexpr (BLOCK) {
         constexpr int R = NT * 4 >= CAP ? 4 : 8;
         static_assert(NT * R >= CAP, "compact-sort capacity");
         for (uint32_t r = 0; r < nbig; ++r) {
             const uint32_t b = sm.big[r];
             const uint32_t lo = b & 0xFFFFu, L = (b >> 16) - lo;
-#ifdef DBI_X_NOBLOCK
-            (void)L;
-#else
             if (L > WAVE_SORT_MAX && !ck_run_block<NT, R>(k0, k1, lo, L, sm.mins)) block_bitonic<NT>(k0, k1, lo, L);
-#endif
         }
         __syncthreads();
-        DBI_PH(5);
     }
     *heads_out = finish_sorted<NT>(out, m, rl, k0, k1, sm.aux, sm.u32, &sm.bad);
-    DBI_PH(6);
     return true;
 }
 
@@ -4433,23 +4367,3 @@ hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_ch
 }
 
 }  // namespace dbi
-#ifdef DBI_X_PHASE
-namespace dbi {
-void phase_read(unsigned long long* v) {  // 32 entries
-    (void)hipDeviceSynchronize();
-    (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 32);
-    unsigned long long z[24] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z));
-}
-}  // namespace dbi
-#endif
-#ifdef DBI_X_CKSTAT
-namespace dbi {
-void ck_stat_read(unsigned int* v) {
-    hipDeviceSynchronize();
-    hipMemcpyFromSymbol(v, HIP_SYMBOL(g_ck_stat), sizeof(unsigned int) * 8);
-    unsigned int z[8] = {};
-    hipMemcpyToSymbol(HIP_SYMBOL(g_ck_stat), z, sizeof(z));
-}
-}  // namespace dbi
-#endif

@@ -280,28 +280,6 @@ int finish_build(dbi_handle* h) {
     st.n_keys = h->hc.n_keys;
     for (int i = 0; i < 8; ++i) st.n_keys += h->hc.n_keys_shard[i];
     st.n_big_bins = h->hc.n_big;  // chunks above CHUNK_CAP (of which n_giant above BIG_CAP)
-#ifdef DBI_X_PHASE
-    {
-        unsigned long long v[32] = {};
-        extern void phase_read(unsigned long long*);
-        phase_read(v);
-        fprintf(stderr, "phase digest: ticket %.1f stage %.1f maps %.1f compact %.1f balance %.1f bounds %.1f lookback %.1f walks %.1f (x10ns summed over blocks, M)\n",
-                v[24] / 1e6, v[25] / 1e6, v[26] / 1e6, v[27] / 1e6, v[28] / 1e6, v[29] / 1e6, v[30] / 1e6, v[31] / 1e6);
-        for (int k = 0; k < 3; ++k)
-            fprintf(stderr, "phase %s: load %.1f runs %.1f rank %.1f wave %.1f block %.1f finish %.1f (Mclk summed over blocks)\n",
-                    k == 0 ? "chunk" : k == 1 ? "mid" : "big", v[8 * k + 1] / 1e6, v[8 * k + 2] / 1e6, v[8 * k + 3] / 1e6,
-                    v[8 * k + 4] / 1e6, v[8 * k + 5] / 1e6, v[8 * k + 6] / 1e6);
-    }
-#endif
-#ifdef DBI_X_CKSTAT
-    {
-        unsigned int v[8] = {};
-        extern void ck_stat_read(unsigned int*);
-        ck_stat_read(v);
-        fprintf(stderr, "ckstat wave runs=%u range=%u order=%u | block runs=%u range=%u order=%u | big=%u range=%u\n",
-                v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
-    }
-#endif
     st.build_ms = ms;
     st.digest_ms = 0;
     for (int i = 0; i < h->nstage; ++i) {
