@@ -9,10 +9,11 @@
 //                            longest protein (the record field width).
 //   1. k_digest_bounded   — (full enzyme, mc <= 2, warm builds) per tile: window
 //                            staged in LDS, cut / cleave / protein-start bit maps,
-//                            cleavage-site starts compacted, each start's slot
-//                            bound reserved by decoupled look-back, one cutSeq walk
-//                            per start writing 16-B records (Rec) straight into
-//                            them, sentinels in the unused slots.
+//                            cleavage-site starts compacted, each start's
+//                            candidate ends from the cut map, the tile's slots
+//                            reserved by one atomic add, one cutSeq mass walk per
+//                            start writing 16-B records (Rec) straight into them,
+//                            sentinels in the unused slots.
 //      k_digest_fused     — (semi / mandatory residues / mc > 2) count walk,
 //                            look-back over exact tile totals, emit walk.
 //      k_digest<COUNT|EMIT> + scan — cold builds (no capacity known yet).
@@ -1796,6 +1797,44 @@ k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_
     }
 }
 
+// Downsweep that finds its own block offset: the sum of the block sums before
+// it (nb <= SCAN_SELF_MAX, read by every block from L2), so the scan is two
+// launches instead of three.  The last block writes the total.
+constexpr uint64_t SCAN_SELF_MAX = SCAN_CHUNK;
+
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan_down_self(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t n,
+                 const uint32_t* __restrict__ sums, unsigned long long* __restrict__ d_total) {
+    __shared__ unsigned long long tmp[SCAN_THREADS / 64 + 1];
+    __shared__ uint32_t tmp32[SCAN_THREADS / 64 + 1];
+    const uint32_t b = blockIdx.x;
+    unsigned long long before = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t i = (uint32_t)k * SCAN_THREADS + threadIdx.x;
+        if (i < b) before += sums[i];
+    }
+    before = block_sum<SCAN_THREADS, unsigned long long>(before, tmp);
+    const uint64_t base = (uint64_t)b * SCAN_CHUNK;
+    uint32_t v[SCAN_ITEMS];
+    uint32_t loc = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)threadIdx.x * SCAN_ITEMS + k;
+        v[k] = i < n ? in[i] : 0u;
+        loc += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan<SCAN_THREADS, uint32_t>(loc, tmp32, tot) + (uint32_t)before;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)threadIdx.x * SCAN_ITEMS + k;
+        if (i < n) out[i] = run;
+        run += v[k];
+    }
+    if (d_total && b + 1 == gridDim.x && threadIdx.x == 0) *d_total = before + tot;
+}
+
 size_t scan_u32_tmp_elems(uint64_t n) { return (size_t)((n + SCAN_CHUNK - 1) / SCAN_CHUNK) + 1; }
 
 hipError_t launch_scan_u32(const uint32_t* d_in, uint32_t* d_out, uint64_t n, uint32_t* d_block_tmp,
@@ -1806,6 +1845,12 @@ hipError_t launch_scan_u32(const uint32_t* d_in, uint32_t* d_out, uint64_t n, ui
     }
     const uint64_t nb = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
     if (tmp_elems < nb) return hipErrorInvalidValue;
+    if (nb <= SCAN_SELF_MAX) {
+        DBI_LAUNCH(k_scan_reduce, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, n, d_block_tmp);
+        DBI_LAUNCH(k_scan_down_self, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, d_out, n, d_block_tmp,
+                   d_total);
+        return hipGetLastError();
+    }
     DBI_LAUNCH(k_scan_reduce, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, n, d_block_tmp);
     DBI_LAUNCH(k_scan_single, dim3(1), dim3(SCAN_THREADS), 0, s, d_block_tmp, d_block_tmp, nb, d_total);
     DBI_LAUNCH(k_scan_down, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, d_in, d_out, n, d_block_tmp);
@@ -2409,6 +2454,17 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
 // start at or after c*T, found on the bin-sorted records themselves (one
 // thread per chunk: galloping, then binary search for the end of the bin that
 // straddles c*T — a few loads for ordinary bins, log steps for mass spikes).
+// Chunk pairs: chunk 2c = [start(c), split(c)), chunk 2c+1 = [split(c),
+// start(c+1)), start(c) = the first bin start at or after c*T.  split(c) is
+// the start of the bin that straddles (c+1)*T when that bin holds more than
+// WAVE_SORT_LIMIT records and starts at or after c*T, else start(c+1): a big
+// bin that crosses a boundary becomes a chunk of its own instead of carrying
+// the chunk before it into the list kernels, and chunk 2c stays within
+// T + WAVE_SORT_LIMIT records unless it is one bin.  Thread c finds the end
+// of the bin straddling c*T (galloping, then binary search: a few loads for
+// ordinary bins, log steps for mass spikes) and, only when one probe says the
+// bin is big, its start; it writes chunk_lo[2c] and chunk_lo[2c-1].
+// chunk_lo has 2*nchunks + 1 entries.
 __global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap bm, uint32_t T, uint32_t nchunks,
                                uint32_t* __restrict__ chunk_lo, const unsigned long long* __restrict__ dn) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2416,7 +2472,8 @@ __global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap 
     if (dn) n = (uint32_t)min((unsigned long long)n, *dn);  // chunks past the records are empty
     const uint32_t x = c == nchunks ? n : min(c * T, n);
     if (x == 0 || x == n) {
-        chunk_lo[c] = x;
+        chunk_lo[2 * c] = x;
+        if (c > 0) chunk_lo[2 * c - 1] = x;
         return;
     }
     const uint32_t b = bin_of(q0_mass(recs[x - 1].q0), bm);
@@ -2431,7 +2488,24 @@ __global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap 
         const uint32_t mid = lo + ((hi - lo) >> 1);
         if (bin_of(q0_mass(recs[mid].q0), bm) <= b) lo = mid; else hi = mid;
     }
-    chunk_lo[c] = hi;
+    chunk_lo[2 * c] = hi;
+    constexpr uint32_t BIG = (uint32_t)WAVE_SORT_LIMIT;
+    uint32_t split = hi;
+    if (hi > BIG && bin_of(q0_mass(recs[hi - BIG - 1].q0), bm) == b) {  // more than BIG records: find its start
+        uint32_t up = hi - BIG - 1, dn2 = up;  // up: known in the bin
+        step = 1;
+        while (dn2 > 0 && bin_of(q0_mass(recs[dn2 - 1].q0), bm) == b) {
+            up = dn2 - 1;
+            dn2 = up > step ? up - step : 0u;
+            step <<= 1;
+        }
+        while (dn2 < up) {  // bin(dn2 - 1) < b or dn2 == 0: the first record of the bin in [dn2, up]
+            const uint32_t mid = dn2 + ((up - dn2) >> 1);
+            if (bin_of(q0_mass(recs[mid].q0), bm) == b) up = mid; else dn2 = mid + 1;
+        }
+        if (up >= (c - 1) * T) split = up;
+    }
+    chunk_lo[2 * c - 1] = split;
 }
 
 hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,
@@ -3081,9 +3155,15 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
              const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
              uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, Counters* __restrict__ ctr) {
     __shared__ ChunkSmem<NT, CAP> sm;
-    const uint32_t c = blockIdx.x;
+    const uint32_t c = 2 * blockIdx.x;  // chunk pair (k_chunk_bounds): this block sorts chunk c
     const uint32_t a = chunk_lo[c];
     const uint32_t m = chunk_lo[c + 1] - a;
+    if (threadIdx.x == 0) {  // chunk c+1: empty, or one big bin for the list kernels
+        const uint32_t mb = chunk_lo[c + 2] - chunk_lo[c + 1];
+        if (mb == 0) ucount[c + 1] = 0;
+        else if (mb > (uint32_t)CAP) big_list[atomicAdd(&ctr->n_big, 1u)] = c + 1;
+        else mid_list[atomicAdd(&ctr->n_mid, 1u)] = c + 1;
+    }
     if (m == 0) {
         if (threadIdx.x == 0) ucount[c] = 0;
         return;
@@ -3341,17 +3421,17 @@ __global__ void __launch_bounds__(FIN_THREADS)
 k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
            double* __restrict__ umass, uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff,
            uint32_t* __restrict__ ulen, uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid,
-           int32_t factor, uint32_t ucap, Counters* __restrict__ ctr) {
+           int32_t factor, uint32_t ucap, uint32_t cstride, Counters* __restrict__ ctr) {
     constexpr uint32_t NW = FIN_THREADS / 64;
     __shared__ uint32_t wc[FIN_ITEMS * NW];  // heads per (round item k, wave), then exclusive bases
     __shared__ uint32_t s_tot;
     const uint32_t c = blockIdx.x;
-    const uint32_t a = chunk_lo[c];
-    const uint32_t n = chunk_lo[c + 1] - a;
+    const uint32_t a = chunk_lo[cstride * c];  // a chunk pair (cstride 2) is one contiguous range
+    const uint32_t n = chunk_lo[cstride * (c + 1)] - a;
     const uint32_t W = rec_width(ctr->max_plen);
     const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(recs + a);
     const uint32_t w = threadIdx.x >> 6;
-    uint32_t run = ubase[c];
+    uint32_t run = ubase[cstride * c];
     uint32_t nkeys = 0;  // heads whose mass key differs from the previous unique's (SQLiteByte rows)
     for (uint32_t t0 = 0; t0 < n; t0 += FIN_THREADS * FIN_ITEMS) {
         uint4 rv[FIN_ITEMS];
@@ -3428,10 +3508,11 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
 
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
-                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, Counters* d_ctr, hipStream_t s) {
+                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, uint32_t cstride,
+                           Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(FIN_THREADS), 0, s, d_recs, d_chunk_lo, d_ubase, d_umass, d_upid,
-               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, d_ctr);
+               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, cstride, d_ctr);
     return hipGetLastError();
 }
 

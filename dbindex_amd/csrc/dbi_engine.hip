@@ -147,12 +147,12 @@ int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse, int pass
     const uint32_t T = h->chunk_t;
     const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + T - 1) / T, 1);
     const size_t seg_cap = giant_seg_cap(n);
-    const size_t scan_need = std::max(scan_u32_tmp_elems(hist_elems), scan_u32_tmp_elems(nchunks));
+    const size_t scan_need = std::max(scan_u32_tmp_elems(hist_elems), scan_u32_tmp_elems(2 * (uint64_t)nchunks));
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_need, h->scan_tmp.cap)))) return rc;
     if ((rc = h->recB.ensure(n)) || (rc = h->hist.ensure(hist_elems)) ||
-        (rc = h->ucount.ensure(nchunks)) || (rc = h->chunk_lo.ensure((size_t)nchunks + 1)) ||
-        (rc = h->big_list.ensure(nchunks)) || (rc = h->mid_list.ensure(nchunks)) ||
-        (rc = h->giant_list.ensure(nchunks)) || (rc = h->segs.ensure((GIANT_PASSES + 4) * seg_cap)) ||
+        (rc = h->ucount.ensure(2 * (size_t)nchunks)) || (rc = h->chunk_lo.ensure(2 * (size_t)nchunks + 1)) ||
+        (rc = h->big_list.ensure(2 * (size_t)nchunks)) || (rc = h->mid_list.ensure(2 * (size_t)nchunks)) ||
+        (rc = h->giant_list.ensure(2 * (size_t)nchunks)) || (rc = h->segs.ensure((GIANT_PASSES + 4) * seg_cap)) ||
         (rc = h->ws_key.ensure(4 * n)) || (rc = h->ws_k2.ensure(4 * n)) ||
         (rc = h->umass.ensure(n)) || (rc = h->upid.ensure(n)) || (rc = h->uoff.ensure(n)) ||
         (rc = h->ulen.ensure(n)) || (rc = h->occ_off.ensure(n + 1)) || (rc = h->occ_pid.ensure(n)))
@@ -229,8 +229,8 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     // of every possible entry spent most of these launches dispatching blocks
     // with nothing to do, the big tier's at one 155-KiB block per CU at a
     // time); a longer list sets ERR_GRID and the build is redone with full grids.
-    uint32_t max_mid = (uint32_t)std::min<uint64_t>(nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
-    uint32_t max_big = (uint32_t)std::min<uint64_t>(nchunks, n / (CHUNK_CAP + 1) + 1);
+    uint32_t max_mid = (uint32_t)std::min<uint64_t>(2 * (uint64_t)nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
+    uint32_t max_big = (uint32_t)std::min<uint64_t>(2 * (uint64_t)nchunks, n / (CHUNK_CAP + 1) + 1);
     est = est || d_n;
     if (est && h->grid_mid) max_mid = std::min(max_mid, h->grid_mid);
     if (est && h->grid_big) max_big = std::min(max_big, h->grid_big);
@@ -249,12 +249,13 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
                                   h->segs.p, seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
     // unique offsets per chunk
     STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
-          launch_scan_u32(h->ucount.p, h->ucount.p, nchunks, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->n_unique, s));
+          launch_scan_u32(h->ucount.p, h->ucount.p, 2 * (uint64_t)nchunks, h->scan_tmp.p, h->scan_tmp.cap,
+                          &h->ctr.p->n_unique, s));
     // finalize: 16 B record in, 4 B occurrence protein id out, 24 B per unique out
     STAGE(h, "finalize", by(0, 20, 24, 0, 0),
           launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p,
                           h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor,
-                          (uint32_t)std::min<size_t>(h->umass.cap, 0xFFFFFFFFu), h->ctr.p, s));
+                          (uint32_t)std::min<size_t>(h->umass.cap, 0xFFFFFFFFu), 2u, h->ctr.p, s));
     DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s, d_n));
     h->stats.n_bins = nbins;
     return 0;

@@ -330,7 +330,9 @@ hipError_t launch_off_rebase(const uint64_t* d_in, uint64_t base, uint32_t* d_ou
 // ctr->max_plen = max(ctr->max_plen, longest protein of poff[0..n_prot])
 hipError_t launch_max_plen(const uint32_t* d_poff, uint32_t n_prot, Counters* d_ctr, hipStream_t s);
 size_t radix_hist_elems(uint32_t n, int bits);
-// chunk_lo[c] = first bin start at or after c*T in the bin-sorted records (nchunks+1 entries)
+// chunk pairs over the bin-sorted records (2*nchunks+1 entries): chunk_lo[2c] =
+// first bin start at or after c*T, chunk_lo[2c+1] = the start of a big bin
+// straddling (c+1)*T (its own chunk), else chunk_lo[2c+2]
 hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,
                                uint32_t* d_chunk_lo, hipStream_t s, const unsigned long long* d_n = nullptr);
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
@@ -354,8 +356,8 @@ hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_ch
                                Counters* d_ctr, hipStream_t s);
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
-                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, Counters* d_ctr,
-                           hipStream_t s);
+                           uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, uint32_t cstride,
+                           Counters* d_ctr, hipStream_t s);
 hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t factor, uint32_t* d_flags,
                             hipStream_t s);
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s,
