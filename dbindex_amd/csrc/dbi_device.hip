@@ -1292,6 +1292,7 @@ struct LeanSmem {
     uint64_t cutm[LD_WORDS];  // bit q: checkCleavage's C side holds at q (protein ends included)
     uint64_t stm[LD_WORDS];   // bit q: a protein starts at q (one past the window included)
     uint32_t pst[PST_CAP];    // poff[pf .. pl+1] (protein of a start: binary search)
+    uint16_t wpre[LD_WORDS];  // protein starts marked in stm words before word w
     alignas(16) uint8_t win[LD_WIN + 16];
     uint8_t flags[256];
     alignas(8) uint16_t cand[DIGEST_TILE];  // candidate starts (tile-local), compacted, then balanced
@@ -1388,8 +1389,9 @@ __device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, LeanSmem& s
     if (nlist == 0) return w;  // no candidate end
     // the residue loop, four positions per step: one dword pair of the window,
     // four mass reads in flight, then the sequential fp64 adds (:306-308); the
-    // mass at each listed end goes to LDS.  Positions past `last` (at most 3)
-    // only add to a mass that is no longer used.
+    // mass at each listed end goes to LDS, tested once per step (an end in
+    // [q, q+4): the list is ascending and 0xFF-padded, q + 4 <= 132).
+    // Positions past `last` (at most 3) only add to a mass that is no longer used.
     const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(sm.win);
     double* __restrict__ em = &sm.endm[0][threadIdx.x];
     uint32_t ne = pk & 0xFFu, rest = pk, j = 0;
@@ -1398,19 +1400,15 @@ __device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, LeanSmem& s
         const uint32_t r4 = __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], a & 3u);
         const double x0 = sm.mass[r4 & 0xFFu], x1 = sm.mass[(r4 >> 8) & 0xFFu];
         const double x2 = sm.mass[(r4 >> 16) & 0xFFu], x3 = sm.mass[r4 >> 24];
-#define DBI_LEAN_STEP(K, X)                   \
-        m = m + X;                            \
-        if (q + K == ne) {                    \
-            em[j * DIGEST_THREADS] = m;       \
-            ++j;                              \
-            rest >>= 8;                       \
-            ne = rest & 0xFFu;                \
+        const double m0 = m + x0, m1 = m0 + x1, m2 = m1 + x2, m3 = m2 + x3;
+        while (ne < q + 4u) {
+            const uint32_t d = ne - q;
+            em[j * DIGEST_THREADS] = d == 0u ? m0 : d == 1u ? m1 : d == 2u ? m2 : m3;
+            ++j;
+            rest = (rest >> 8) | 0xFF000000u;  // 0xFF past the list
+            ne = rest & 0xFFu;
         }
-        DBI_LEAN_STEP(0u, x0)
-        DBI_LEAN_STEP(1u, x1)
-        DBI_LEAN_STEP(2u, x2)
-        DBI_LEAN_STEP(3u, x3)
-#undef DBI_LEAN_STEP
+        m = m3;
         if (m > dp.max_mh) break;  // no later end passes maxMH (:326-329, :284)
     }
     w.j = j;
@@ -1458,12 +1456,13 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
                  uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, Rec* __restrict__ d_out, uint64_t cap,
                  Counters* __restrict__ d_ctr) {
     __shared__ LeanSmem sm;
-    __shared__ uint32_t s_kept, s_waves;
+    __shared__ uint32_t s_kept, s_waves, s_dup;
     __shared__ unsigned long long s_base;
     const uint32_t tid = threadIdx.x;
     if (tid == 0) {  // read at the end, behind many barriers
         s_kept = 0;
         s_waves = 0;
+        s_dup = 0;
     }
     const uint32_t tile = blockIdx.x, ntiles = gridDim.x;
     const uint32_t t0 = tile * (uint32_t)DIGEST_TILE;
@@ -1550,11 +1549,26 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
         const uint32_t o = d_poff[pf + i];
         if (o >= w0 && o <= w_end) {
             const uint32_t q = o - w0 + lb;  // protein starts (and the end of the last one)
-            atomicOr(&sm.stm[q >> 6], 1ull << (q & 63));
+            const uint64_t bit = 1ull << (q & 63);
+            if (atomicOr(&sm.stm[q >> 6], bit) & bit) s_dup = 1;  // an empty protein: two starts at q
         }
         if (i < PST_CAP) sm.pst[i] = o;
     }
     __syncthreads();
+    // protein of a start from the start map: the marked starts before its word
+    // (one wave's scan) + those up to it in the word.  Not when two proteins
+    // start at one position (empty proteins) or the offsets did not fit pst.
+    const bool pid_map = npst != 0 && s_dup == 0;  // block-uniform
+    if (pid_map && tid < 64) {
+        static_assert(LD_WORDS <= 128, "two words per lane");
+        const uint32_t c0 = 2 * tid < (uint32_t)LD_WORDS ? (uint32_t)__popcll(sm.stm[2 * tid]) : 0u;
+        const uint32_t c1 = 2 * tid + 1 < (uint32_t)LD_WORDS ? (uint32_t)__popcll(sm.stm[2 * tid + 1]) : 0u;
+        const uint32_t ex = wave_incl_scan(c0 + c1) - (c0 + c1);
+        if (2 * tid < (uint32_t)LD_WORDS) sm.wpre[2 * tid] = (uint16_t)ex;
+        if (2 * tid + 1 < (uint32_t)LD_WORDS) sm.wpre[2 * tid + 1] = (uint16_t)(ex + c0);
+    }
+    // poff[pf] <= t0 always; it is marked unless it lies before the window
+    const uint32_t pid_base = pf + (npst != 0 && sm.pst[0] < w0 ? 1u : 0u) - 1u;
     // cut and N_ok maps, 64 positions per thread from the bit maps:
     //   last     = a protein starts at q+1
     //   cut      = last || (cleave(q) && !nocut(q+1))        (checkCleavage C side)
@@ -1598,10 +1612,15 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     balance_candidates(sm.cand, s_cnt, ncand, B, t_end - t0);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
-    // slot bounds: the candidate ends (B for a walk that may leave the horizon)
+    // slot bounds: the candidate ends (B for a walk that may leave the horizon);
+    // the first two starts' ends stay in registers for the walks (most threads
+    // have one or two: ncand ~ 450 per tile)
     uint32_t lim = 0;
+    LeanEnds en0{0ull, 0ull, 0u, false}, en1{0ull, 0ull, 0u, false};
     for (uint32_t j = jb; j < je; ++j) {
         const LeanEnds en = lean_ends(sm, off + sm.cand[j], known, B, min_len);
+        if (j == jb) en0 = en;
+        else if (j == jb + 1) en1 = en;
         lim += en.open ? B : (uint32_t)(__popcll(en.lo) + __popcll(en.hi));
     }
     uint32_t tile_slots;
@@ -1619,9 +1638,15 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     for (uint32_t j = jb; j < je; ++j) {
         const uint32_t p = off + sm.cand[j];
         const uint32_t s = w0 + (p - lb);
-        const LeanWalk lw = lean_masses(dp, sm, p, lean_ends(sm, p, known, B, min_len));
-        uint32_t pstart;
-        const uint32_t pid = protein_of(sm.pst, npst, pf, pl, d_poff, s, pstart);
+        const LeanWalk lw =
+            lean_masses(dp, sm, p, j == jb ? en0 : j == jb + 1 ? en1 : lean_ends(sm, p, known, B, min_len));
+        uint32_t pstart, pid;
+        if (pid_map) {
+            pid = pid_base + sm.wpre[p >> 6] + (uint32_t)__popcll(sm.stm[p >> 6] & low_bits((p & 63u) + 1u));
+            pstart = sm.pst[pid - pf];
+        } else {
+            pid = protein_of(sm.pst, npst, pf, pl, d_poff, s, pstart);
+        }
         const uint64_t loc = rec_loc(pid, s - pstart, w);
         WalkOut wo;
         if (lw.overflow) {
