@@ -3446,8 +3446,13 @@ __global__ void __launch_bounds__(FIN_THREADS)
 k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
            double* __restrict__ umass, uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff,
            uint32_t* __restrict__ ulen, uint32_t* __restrict__ occ_off, uint32_t* __restrict__ occ_pid,
-           int32_t factor, uint32_t ucap, uint32_t cstride, Counters* __restrict__ ctr) {
+           int32_t factor, uint32_t ucap, uint32_t cstride, uint32_t n_kept,
+           const unsigned long long* __restrict__ dn, Counters* __restrict__ ctr) {
     constexpr uint32_t NW = FIN_THREADS / 64;
+    // the CSR's closing offset (occ_off holds n_kept + 1 entries; a unique
+    // count past that is never written)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ctr->n_unique <= n_kept)
+        occ_off[ctr->n_unique] = dn ? (uint32_t)*dn : n_kept;
     __shared__ uint32_t wc[FIN_ITEMS * NW];  // heads per (round item k, wave), then exclusive bases
     __shared__ uint32_t s_tot;
     const uint32_t c = blockIdx.x;
@@ -3534,10 +3539,10 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
                            uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, uint32_t cstride,
-                           Counters* d_ctr, hipStream_t s) {
-    if (nchunks == 0) return hipSuccess;
+                           uint32_t n_kept, const unsigned long long* d_n, Counters* d_ctr, hipStream_t s) {
+    if (nchunks == 0) return launch_write_tail(d_occ_off, n_kept, d_ctr, s, d_n);
     DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(FIN_THREADS), 0, s, d_recs, d_chunk_lo, d_ubase, d_umass, d_upid,
-               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, cstride, d_ctr);
+               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, cstride, n_kept, d_n, d_ctr);
     return hipGetLastError();
 }
 

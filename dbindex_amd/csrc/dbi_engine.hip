@@ -255,8 +255,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     STAGE(h, "finalize", by(0, 20, 24, 0, 0),
           launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p,
                           h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor,
-                          (uint32_t)std::min<size_t>(h->umass.cap, 0xFFFFFFFFu), 2u, h->ctr.p, s));
-    DBI_HIP(launch_write_tail(h->occ_off.p, n32, h->ctr.p, s, d_n));
+                          (uint32_t)std::min<size_t>(h->umass.cap, 0xFFFFFFFFu), 2u, n32, d_n, h->ctr.p, s));
     h->stats.n_bins = nbins;
     return 0;
 }

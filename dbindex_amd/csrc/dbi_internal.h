@@ -357,7 +357,7 @@ hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_ch
 hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32_t nchunks, const uint32_t* d_ubase,
                            double* d_umass, uint32_t* d_upid, uint32_t* d_uoff, uint32_t* d_ulen,
                            uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, uint32_t cstride,
-                           Counters* d_ctr, hipStream_t s);
+                           uint32_t n_kept, const unsigned long long* d_n, Counters* d_ctr, hipStream_t s);
 hipError_t launch_key_flags(const double* d_umass, uint32_t n_unique, int32_t factor, uint32_t* d_flags,
                             hipStream_t s);
 hipError_t launch_write_tail(uint32_t* d_occ_off, uint32_t n_kept, const Counters* d_ctr, hipStream_t s,

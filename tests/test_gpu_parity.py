@@ -89,6 +89,30 @@ def test_synthetic(Engine, name, prm, nprot):
     _check(Engine, prm, pp, name)
 
 
+@pytest.mark.parametrize("layout", ["short", "empties", "mixed"])
+def test_protein_of_start(Engine, layout):
+    """The bounded digest finds a start's protein from the start bit map
+    (per-word prefix counts) unless two proteins start at one position (empty
+    proteins) or more than PST_CAP proteins touch a tile window (then a binary
+    search): short proteins (~200 per 4096-residue tile), empty proteins
+    between long ones, and both mixed across many tiles, cold and warm."""
+    rng = np.random.default_rng({"short": 11, "empties": 12, "mixed": 13}[layout])
+    base = fasta.config("1k")
+    seqs = []
+    for i in range(1500 if layout == "short" else 400):
+        s = base.sequence(i % 1000)
+        if layout == "short":
+            seqs.append(s[: int(rng.integers(4, 30))])
+        elif layout == "empties":
+            seqs.append(s)
+            if i % 25 == 0:  # some tiles hold empty proteins, most do not
+                seqs.extend([""] * int(rng.integers(1, 3)))
+        else:
+            seqs.append(s if i % 2 else s[: int(rng.integers(0, 25))])
+    pp = fasta.PackedProteins.from_sequences(seqs, [fasta.uniprot_header(i) for i in range(len(seqs))])
+    _check(Engine, DBIndexSearchParams.trypsin(2), pp, f"protein_of {layout}")
+
+
 @pytest.mark.parametrize("index_factor,maxmh,nprot", [(7, 7999.9, 1000), (3000, 7999.0, 300)])
 def test_bucket_drop(Engine, index_factor, maxmh, nprot):
     """BUCKET_MASS_RANGE = 8000 / index_factor (integer division): peptides whose
