@@ -196,25 +196,40 @@ __device__ __forceinline__ uint32_t find_le(const uint32_t* poff, uint32_t lo, u
 // tile_pf[t] = protein containing residue min(t*TILE, R-1), t in [0, ntiles];
 // tile_pf[ntiles + 1 + t] = protein containing the last residue of tile t's
 // staged window (t < ntiles), so a digest block starts with two independent
-// loads instead of a chain of dependent ones; threads < n_prot also fold their
-// protein's length into ctr->max_plen
+// loads instead of a chain of dependent ones.  One thread per protein writes
+// the entries of the positions it holds (a protein shorter than a tile holds
+// at most one of each kind; empty proteins hold none, which is find_le's
+// answer too: the last protein whose offset is <= the position) -- no
+// per-tile binary search over the offsets (20 dependent loads at SwissProt
+// scale).  Threads also fold their protein's length into ctr->max_plen.
 __global__ void k_tile_proteins(const uint32_t* __restrict__ poff, uint32_t n_prot, uint32_t n_res, uint32_t ntiles,
                                 uint32_t* __restrict__ tile_pf, Counters* __restrict__ ctr) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t <= ntiles) {
-        const uint32_t x = min(t * (uint32_t)DIGEST_TILE, n_res - 1);
-        const uint32_t pf = find_le(poff, 0, n_prot, x);
-        tile_pf[t] = pf;
-        if (t < ntiles) {
-            const uint32_t t0 = t * (uint32_t)DIGEST_TILE;
-            const uint32_t w0 = t0 >= (uint32_t)WIN_PRE ? t0 - WIN_PRE : 0u;
-            const uint32_t w_end = min(w0 + (uint32_t)WIN, n_res);
-            tile_pf[ntiles + 1 + t] = find_le(poff, pf, n_prot, w_end - 1);
+    constexpr int64_t TL = DIGEST_TILE;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t len = 0;
+    if (p < n_prot) {
+        const int64_t a = poff[p], e = poff[p + 1];
+        len = (uint32_t)(e - a);
+        if (e > a) {
+            // first protein: x_t = t*TILE (t < ntiles) in [a, e); the last protein also holds R-1 (t = ntiles)
+            for (int64_t t = (a + TL - 1) / TL; t * TL < e; ++t) tile_pf[t] = p;
+            if (e == (int64_t)n_res) tile_pf[ntiles] = p;
+            // last protein of the window: y_0 = min(WIN, R) - 1, y_t = min(t*TILE + K + 1, R) - 1 (t >= 1)
+            constexpr int64_t K = TL + DIGEST_HALO - 1;
+            const int64_t y0 = min((int64_t)WIN, (int64_t)n_res) - 1;
+            if (y0 >= a && y0 < e) tile_pf[ntiles + 1] = p;
+            int64_t t = max((int64_t)1, (a - K + TL - 1) / TL);
+            if (a - K < 0) t = 1;
+            for (; t < (int64_t)ntiles && t * TL + K < e; ++t)
+                if (t * TL + K >= a && t * TL + K < (int64_t)n_res) tile_pf[ntiles + 1 + t] = p;
+            if (e == (int64_t)n_res) {  // windows clipped at the end of the residues end in this protein
+                for (int64_t u = max((int64_t)1, ((int64_t)n_res - K + TL - 1) / TL); u < (int64_t)ntiles; ++u)
+                    if (u * TL + K >= (int64_t)n_res) tile_pf[ntiles + 1 + u] = p;
+            }
         }
     }
     // block max, then one atomic per block that can still raise the value
     __shared__ uint32_t s_max[4];
-    uint32_t len = t < n_prot ? poff[t + 1] - poff[t] : 0u;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) len = max(len, (uint32_t)__shfl_xor((int)len, d, 64));
     if (lane_id() == 0) s_max[threadIdx.x >> 6] = len;
@@ -230,8 +245,7 @@ hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_
                                 Counters* d_ctr, hipStream_t s) {
     if (n_res == 0 || n_prot == 0) return hipSuccess;
     const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
-    const uint32_t nthr = max(ntiles + 1, n_prot);
-    DBI_LAUNCH(k_tile_proteins, dim3((nthr + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
+    DBI_LAUNCH(k_tile_proteins, dim3((n_prot + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
                d_tile_pf, d_ctr);
     return hipGetLastError();
 }
@@ -2475,20 +2489,19 @@ __device__ uint32_t process_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
     return myheads;
 }
 
-// chunk c = records [chunk_lo[c], chunk_lo[c+1]): chunk_lo[c] = the first bin
-// start at or after c*T, found on the bin-sorted records themselves (one
-// thread per chunk: galloping, then binary search for the end of the bin that
-// straddles c*T — a few loads for ordinary bins, log steps for mass spikes).
-// Chunk pairs: chunk 2c = [start(c), split(c)), chunk 2c+1 = [split(c),
-// start(c+1)), start(c) = the first bin start at or after c*T.  split(c) is
-// the start of the bin that straddles (c+1)*T when that bin holds more than
-// WAVE_SORT_LIMIT records and starts at or after c*T, else start(c+1): a big
-// bin that crosses a boundary becomes a chunk of its own instead of carrying
-// the chunk before it into the list kernels, and chunk 2c stays within
-// T + WAVE_SORT_LIMIT records unless it is one bin.  Thread c finds the end
-// of the bin straddling c*T (galloping, then binary search: a few loads for
-// ordinary bins, log steps for mass spikes) and, only when one probe says the
-// bin is big, its start; it writes chunk_lo[2c] and chunk_lo[2c-1].
+// Chunk pairs over the bin-sorted records: chunk 2c = [start(c), split(c)),
+// chunk 2c+1 = [split(c), start(c+1)), start(c) = the first bin start at or
+// after c*T.  split(c) is the start of the bin that straddles (c+1)*T when
+// that bin holds more than WAVE_SORT_LIMIT records and starts at or after c*T,
+// else start(c+1): a big bin that crosses a boundary becomes a chunk of its
+// own instead of carrying the chunk before it into the list kernels, and chunk
+// 2c stays within T + WAVE_SORT_LIMIT records unless it is one bin.  Thread c
+// finds the end of the bin straddling c*T (galloping, then binary search: a
+// few loads for ordinary bins, log steps for mass spikes) and, only when one
+// probe says the bin is big and another that it starts after (c-1)*T, its
+// start by binary search inside that chunk width; it writes chunk_lo[2c] and
+// chunk_lo[2c-1].  (One wave per boundary with 64 probes per step: 42 vs
+// 35 us -- the probes' line traffic costs more than the shorter chains save.)
 // chunk_lo has 2*nchunks + 1 entries.
 __global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap bm, uint32_t T, uint32_t nchunks,
                                uint32_t* __restrict__ chunk_lo, const unsigned long long* __restrict__ dn) {
@@ -2515,20 +2528,17 @@ __global__ void k_chunk_bounds(const Rec* __restrict__ recs, uint32_t n, BinMap 
     }
     chunk_lo[2 * c] = hi;
     constexpr uint32_t BIG = (uint32_t)WAVE_SORT_LIMIT;
+    const uint32_t cm = (c - 1) * T;  // a split bin starts at or after (c-1)*T
     uint32_t split = hi;
-    if (hi > BIG && bin_of(q0_mass(recs[hi - BIG - 1].q0), bm) == b) {  // more than BIG records: find its start
-        uint32_t up = hi - BIG - 1, dn2 = up;  // up: known in the bin
-        step = 1;
-        while (dn2 > 0 && bin_of(q0_mass(recs[dn2 - 1].q0), bm) == b) {
-            up = dn2 - 1;
-            dn2 = up > step ? up - step : 0u;
-            step <<= 1;
+    if (hi > BIG && bin_of(q0_mass(recs[hi - BIG - 1].q0), bm) == b &&
+        bin_of(q0_mass(recs[cm].q0), bm) < b) {
+        // more than BIG records, starting after cm: its first record in (cm, hi - BIG - 1]
+        uint32_t l2 = cm, u2 = hi - BIG - 1;  // bin(l2) < b, bin(u2) == b
+        while (u2 - l2 > 1) {
+            const uint32_t mid = l2 + ((u2 - l2) >> 1);
+            if (bin_of(q0_mass(recs[mid].q0), bm) < b) l2 = mid; else u2 = mid;
         }
-        while (dn2 < up) {  // bin(dn2 - 1) < b or dn2 == 0: the first record of the bin in [dn2, up]
-            const uint32_t mid = dn2 + ((up - dn2) >> 1);
-            if (bin_of(q0_mass(recs[mid].q0), bm) == b) up = mid; else dn2 = mid + 1;
-        }
-        if (up >= (c - 1) * T) split = up;
+        split = u2;
     }
     chunk_lo[2 * c - 1] = split;
 }
