@@ -163,7 +163,9 @@ struct dbi_handle {
     bool inputs_ptm = false;            // ... and they carry inline '[formula]' PTMs (no dbi_rebuild)
     bool hc_final = false;              // hc holds the counters after the build's last kernel
     uint64_t last_kept = 0;             // the previous build's records (bins of a device-sized tail)
-    uint32_t grid_mid = 0, grid_big = 0;  // list-kernel grids of a device-sized tail, from the previous build (0: one block per possible entry)
+    uint32_t grid_mid = 0, grid_big = 0;  // list-kernel grids of a device-sized tail, from the previous build (0: one block per possible entry; GRID_NONE: that list was empty, the kernel is not launched)
+    bool skip_mid = false, skip_big = false;  // the last tail did not launch that list kernel (GRID_NONE)
+    bool lists_short = false;             // the last tail's chunk lists outgrew their grids (set by finish_build)
     bool giants_seen = true;              // the previous build had giant chunks (or none yet): run the giant pass
     DevBuf<double> q_mass, q_tol;
     DevBuf<uint64_t> q_first, q_count, q_row, q_ids;

@@ -232,8 +232,12 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     uint32_t max_mid = (uint32_t)std::min<uint64_t>(2 * (uint64_t)nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
     uint32_t max_big = (uint32_t)std::min<uint64_t>(2 * (uint64_t)nchunks, n / (CHUNK_CAP + 1) + 1);
     est = est || d_n;
-    if (est && h->grid_mid) max_mid = std::min(max_mid, h->grid_mid);
-    if (est && h->grid_big) max_big = std::min(max_big, h->grid_big);
+    // (a list that was empty last time is not launched at all: ~4 us of an
+    // empty grid plus its launch gap; entries there redo the build as above)
+    h->skip_mid = est && h->grid_mid == GRID_NONE;
+    h->skip_big = est && h->grid_big == GRID_NONE;
+    if (est && h->grid_mid) max_mid = h->skip_mid ? 0u : std::min(max_mid, h->grid_mid);
+    if (est && h->grid_big) max_big = h->skip_big ? 0u : std::min(max_big, h->grid_big);
     // the giant-chunk pass (seven launches) only when the last build had giant
     // chunks: a giant chunk otherwise sets ERR_GRID and the build is redone
     const bool giants = !est || h->giants_seen;
@@ -258,6 +262,13 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
                           (uint32_t)std::min<size_t>(h->umass.cap, 0xFFFFFFFFu), 2u, n32, d_n, h->ctr.p, s));
     h->stats.n_bins = nbins;
     return 0;
+}
+
+// did the last tail's chunk lists outgrow their grids (a launched list kernel
+// sets ERR_GRID; a list not launched because it was empty last time must be
+// empty again)?
+bool chunk_lists_short(const dbi_handle* h) {
+    return (h->hc.err & ERR_GRID) || (h->skip_mid && h->hc.n_mid) || (h->skip_big && h->hc.n_big);
 }
 
 int finish_build(dbi_handle* h) {
@@ -305,9 +316,11 @@ int finish_build(dbi_handle* h) {
     st.device_bytes = bytes;
     h->built = true;
     h->last_kept = st.n_kept;
-    // the next device-sized tail's list grids: this build's lists plus a margin
-    h->grid_mid = h->hc.n_mid + h->hc.n_mid / 8 + 32;
-    h->grid_big = h->hc.n_big + h->hc.n_big / 8 + 16;
+    // the next device-sized tail's list grids: this build's lists plus a
+    // margin, or no launch for an empty list
+    h->lists_short = chunk_lists_short(h);
+    h->grid_mid = h->hc.n_mid ? h->hc.n_mid + h->hc.n_mid / 8 + 32 : GRID_NONE;
+    h->grid_big = h->hc.n_big ? h->hc.n_big + h->hc.n_big / 8 + 16 : GRID_NONE;
     h->giants_seen = h->hc.n_giant > 0;
     ++h->build_serial;
     return 0;
@@ -472,6 +485,8 @@ int build_digest(dbi_handle* h) {
             h->nstage = h->bgraph.nstage;
             std::copy(h->bgraph.stages, h->bgraph.stages + h->bgraph.nstage, h->stages);
             h->stats.n_bins = h->bgraph.n_bins;
+            h->skip_mid = h->grid_mid == GRID_NONE;  // as when it was captured (the grids are in the key)
+            h->skip_big = h->grid_big == GRID_NONE;
             n_in = h->bgraph.n_in;
             sparse = h->bgraph.sparse;
         } else if (bounded && h->use_graph && attempt == 0 && h->prev_key_valid && h->prev_key == key) {
@@ -515,7 +530,7 @@ int build_digest(dbi_handle* h) {
         if (need >= (1ull << 32) - 1)
             return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences (or bounded-digest slots) on "
                                             "one device: shard the FASTA");
-        const bool grid_short = (h->hc.err & ERR_GRID) != 0;
+        const bool grid_short = chunk_lists_short(h);
         if (need <= n_in && !grid_short) {
             h->hc_final = true;
             return 0;

@@ -178,6 +178,7 @@ constexpr unsigned ERR_LAYOUT = 1;  // 2*bits(longest protein) + bits(proteins) 
 constexpr unsigned ERR_SEGS = 2;    // giant split: a segment list overflowed (internal)
 constexpr unsigned ERR_SLOTS = 4;   // bounded digest: a thread emitted more records than it reserved (internal)
 constexpr unsigned ERR_PTM = 8;     // a device digest met '[' (inline PTMs are only digested from host input)
+constexpr uint32_t GRID_NONE = 0xFFFFFFFFu;  // list grid: the previous build's list was empty (no launch)
 constexpr unsigned ERR_GRID = 16;   // a chunk list outgrew its kernel's grid (estimated from the previous build): redo
 
 // Tunables

@@ -694,7 +694,7 @@ int dbi_shard_merge(dbi_handle* h) {
         float mg = 0.f;
         sh.ms_merge_gpu =
             !first && hipEventElapsedTime(&mg, h->ev_merge[0], h->ev_merge[1]) == hipSuccess ? (double)mg : 0.0;
-        if (!(h->hc.err & ERR_GRID)) break;
+        if (!h->lists_short) break;
         if (attempt > 0) return set_error(DBI_E_STATE, "internal: chunk lists outgrew full grids");
         h->nstage = nstage0;
         h->giants_seen = true;
