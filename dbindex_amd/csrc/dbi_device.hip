@@ -1431,10 +1431,33 @@ __device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, LeanSmem& s
     return w;
 }
 
-// The records of a lean walk (not overflowed) into out[0, kept).
-template <bool DROP>
+// The first radix pass's histogram, counted where the records are written
+// (warm bounded builds): record slot s is in radix chunk s / RADIX_CHUNK_D;
+// the tile's first K chunks count in LDS (flushed by the last wave with one
+// global atomic per nonzero entry), later ones -- tiles above K-1 chunks of
+// slots, rare -- straight into the global histogram (zeroed before the digest).
+constexpr uint32_t RADIX_CHUNK_D = RADIX_THREADS * RADIX_ITEMS;
+constexpr uint32_t H1_LDS = 384;  // LDS counters: K = H1_LDS >> bits chunks of 2^bits digits
+struct Hist1 {
+    uint32_t* __restrict__ g;  // hist[d * G + chunk], nullptr: not counted here
+    BinMap bm;
+    uint32_t bits, G;
+};
+
+__device__ __forceinline__ void hist1_count(const Hist1& h1, uint32_t* s_h1, uint32_t c0, double m, uint32_t slot) {
+    const uint32_t d = bin_of(m, h1.bm) & ((1u << h1.bits) - 1u);
+    const uint32_t c = slot / RADIX_CHUNK_D;
+    const uint32_t k = c - c0;
+    if (k < (H1_LDS >> h1.bits)) atomicAdd(&s_h1[(k << h1.bits) + d], 1u);
+    else atomicAdd(&h1.g[(size_t)d * h1.G + c], 1u);
+}
+
+// The records of a lean walk (not overflowed) into out[0, kept); slot: the
+// global slot of out[0] (first-pass histogram, when h1.g is set).
+template <bool DROP, bool H1>
 __device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const LeanSmem& sm, uint32_t p, const LeanWalk& w,
-                                             uint64_t loc, Rec* __restrict__ out) {
+                                             uint64_t loc, Rec* __restrict__ out, const Hist1& h1, uint32_t* s_h1,
+                                             uint32_t c0, uint32_t slot) {
     WalkOut r{0u, 0u, false};
     const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(sm.win);
     const double* __restrict__ em = &sm.endm[0][threadIdx.x];
@@ -1456,6 +1479,7 @@ __device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const LeanSmem
         Rec rec;
         rec.q0 = rec_q0(mk, tag);
         rec.q1 = rec_q1(tag, loc, e + 1u);
+        if constexpr (H1) hist1_count(h1, s_h1, c0, mk, slot + kept);
         out[kept++] = rec;
     }
     r.kept = kept;
@@ -1463,16 +1487,21 @@ __device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const LeanSmem
     return r;
 }
 
-template <bool DROP>
-__global__ void __launch_bounds__(DIGEST_THREADS)
+// H1: with the first radix histogram (Hist1; 80 VGPRs kept for 6 waves per
+// SIMD, where the LDS puts the blocks)
+template <bool DROP, bool H1>
+__global__ void __launch_bounds__(DIGEST_THREADS) __attribute__((amdgpu_waves_per_eu(H1 ? 6 : 1, 8)))
 k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                  const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
                  uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, Rec* __restrict__ d_out, uint64_t cap,
-                 Counters* __restrict__ d_ctr) {
+                 Counters* __restrict__ d_ctr, Hist1 h1) {
     __shared__ LeanSmem sm;
     __shared__ uint32_t s_kept, s_waves, s_dup;
     __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_h1[H1 ? H1_LDS : 1];
     const uint32_t tid = threadIdx.x;
+    if constexpr (H1)
+        for (uint32_t i = tid; i < H1_LDS; i += DIGEST_THREADS) s_h1[i] = 0;
     if (tid == 0) {  // read at the end, behind many barriers
         s_kept = 0;
         s_waves = 0;
@@ -1648,6 +1677,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     const unsigned long long base = s_base;
     if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
     Rec* __restrict__ o = d_out + base + excl_t;
+    const uint32_t c0 = (uint32_t)(base / RADIX_CHUNK_D);
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
         const uint32_t p = off + sm.cand[j];
@@ -1666,8 +1696,11 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
         if (lw.overflow) {
             const uint32_t pe = d_poff[pid + 1];
             wo = walk_global<true, false, false>(dp, sm.mass, sm.flags, d_res, s, pe, true, loc, o + kept, o + lim);
+            if constexpr (H1)  // rare: the records it wrote, read back
+                for (uint32_t k = kept; k < kept + wo.kept; ++k)
+                    hist1_count(h1, s_h1, c0, q0_mass(o[k].q0), (uint32_t)base + excl_t + k);
         } else {
-            wo = lean_emit<DROP>(dp, sm, p, lw, loc, o + kept);
+            wo = lean_emit<DROP, H1>(dp, sm, p, lw, loc, o + kept, h1, s_h1, c0, (uint32_t)base + excl_t + kept);
         }
         kept += wo.kept;
         dropped += wo.dropped;
@@ -1675,6 +1708,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     if (kept > lim) atomicOr(&d_ctr->err, ERR_SLOTS);  // the bound is an upper bound: never
     const Rec sent{REC_SENTINEL, REC_SENTINEL};
     for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
+    bool flush;
     if (DROP) {
         const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
         const uint32_t td = block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp);
@@ -1682,34 +1716,57 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
             if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
             if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
         }
+        flush = tid < 64;  // behind the block sums' barriers
     } else {
         // nothing is dropped (drop_mass > maxMH, also in walk_global); the tile
         // total without a barrier: each wave adds its sum in LDS, the last wave
-        // to arrive publishes it
+        // to arrive publishes it (and flushes the histogram counters)
         const uint32_t wk = wave_sum(kept);
+        uint32_t last = 0;
         if (lane_id() == 0) {
             atomicAdd(&s_kept, wk);
             __threadfence_block();
             if (atomicAdd(&s_waves, 1u) == DIGEST_THREADS / 64 - 1) {
+                last = 1;
                 const uint32_t tk = atomicAdd(&s_kept, 0u);
                 if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
             }
+        }
+        flush = __shfl(last, 0, 64) != 0;
+    }
+    if (H1 && flush) {
+        __threadfence_block();
+        for (uint32_t i = lane_id(); i < H1_LDS; i += 64) {
+            const uint32_t v = atomicAdd(&s_h1[i], 0u), c = c0 + (i >> h1.bits);
+            if (v && c < h1.G) atomicAdd(&h1.g[(size_t)(i & ((1u << h1.bits) - 1u)) * h1.G + c], v);
         }
     }
 }
 
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
-                                 const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s) {
+                                 const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s,
+                                 const Hist1Plan* h1p) {
     const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     if (nblk == 0) return hipSuccess;
     if (dp.semi || dp.mand_mode || dp.max_missed + 2 > LD_ENDS) return hipErrorInvalidValue;
-    if (dp.drop_mass <= dp.max_mh)
-        DBI_LAUNCH(k_digest_bounded<true>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
-                   d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr);
-    else
-        DBI_LAUNCH(k_digest_bounded<false>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res,
-                   d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr);
+    Hist1 h1{nullptr, BinMap{}, 0u, 0u};
+    if (h1p) {
+        if (h1p->bits < 1 || h1p->bits > RADIX_BITS || (uint64_t)h1p->G * RADIX_CHUNK_D < cap) return hipErrorInvalidValue;
+        h1 = Hist1{h1p->hist, h1p->bm, (uint32_t)h1p->bits, h1p->G};
+    }
+#define DBI_DIGEST_B(DROP, H1)                                                                                    \
+    DBI_LAUNCH((k_digest_bounded<DROP, H1>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res, \
+               d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr, h1)
+    const bool drop = dp.drop_mass <= dp.max_mh;
+    if (h1p) {
+        if (drop) DBI_DIGEST_B(true, true);
+        else DBI_DIGEST_B(false, true);
+    } else {
+        if (drop) DBI_DIGEST_B(true, false);
+        else DBI_DIGEST_B(false, false);
+    }
+#undef DBI_DIGEST_B
     return hipGetLastError();
 }
 

@@ -225,9 +225,20 @@ hipError_t launch_digest_fused(const DevParams& dp, const double* d_mass_tab, co
 // reserved, ctr->n_kept = records kept; nothing is written when n_slots > cap
 // (the caller grows the buffer and runs it again).
 constexpr unsigned long long REC_SENTINEL = ~0ull;
+// h1p (warm device-sized builds): the digest also counts the first radix
+// pass's histogram -- hist[d * G + slot / RADIX_CHUNK] of every record it
+// writes, d = bin_of(mass, bm) & (2^bits - 1) -- into a zeroed `hist`, so the
+// tail skips that pass's histogram kernel (a read of every slot's mass)
+struct Hist1Plan {
+    uint32_t* hist;
+    BinMap bm;
+    int bits;
+    uint32_t G;  // radix blocks over cap slots
+};
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
-                                 const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s);
+                                 const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s,
+                                 const Hist1Plan* h1p = nullptr);
 // tail_in / tail_n of a device-sized build: the digest's slot and record
 // counts, or 0 / 0 when the slots needed exceed cap
 hipError_t launch_tail_counts(Counters* d_ctr, uint64_t cap, bool sparse, hipStream_t s);

@@ -140,6 +140,34 @@ def test_big_bins_and_duplicates(Engine, copies):
         assert_index_equal(eng, oix, f"bigbins x{copies}")
 
 
+@pytest.mark.parametrize("h1", ["1", "0"])
+def test_digest_counted_histogram(Engine, h1, monkeypatch):
+    """Warm bounded builds of small tails count the first radix pass's
+    histogram in the digest (DBI_DIGEST_HIST, default on below 16 M slots):
+    no histogram kernel for that pass, the same index.  ~400 k records: 2^16
+    bins, two 8-bit passes, so the LDS counters cover one radix chunk per tile
+    and every tile region that crosses a chunk boundary takes the global
+    atomic path; cleavage-dense proteins ("AK" repeats: ~8000 slots per
+    4096-start tile) span several chunks."""
+    monkeypatch.setenv("DBI_DIGEST_HIST", h1)
+    base = fasta.config("human")
+    seqs = [base.sequence(i) for i in range(4000)]
+    seqs[100:100] = ["AK" * 3000, "GAKR" * 1500, "AKK" * 2000]
+    pp = fasta.PackedProteins.from_sequences(seqs, [fasta.uniprot_header(i) for i in range(len(seqs))])
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    m, t = query_masses(oix, 1000)
+    with Engine(cp) as eng:
+        hists = []
+        for k in range(4):  # cold, warm, warm (captured), replay
+            eng.build(pp)
+            assert_index_equal(eng, oix, f"digest histogram={h1} [{k}]")
+            assert_queries_equal(eng, oix, m, t, f"digest histogram={h1} [{k}]")
+            hists.append(sum(1 for n, _, _ in eng.stage_times() if n == "radix_hist"))
+    passes = hists[0]  # the cold build: one histogram kernel per radix pass
+    assert hists[1] == (passes - 1 if h1 == "1" else passes), hists
+
+
 @pytest.mark.parametrize("copies", [3000, 9000])
 def test_list_grids_outgrown(Engine, copies):
     """Warm builds size the mid / big chunk-list grids from the previous
