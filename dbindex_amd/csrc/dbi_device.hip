@@ -2077,42 +2077,54 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
 }
 
 // The same counts from the digit bytes the previous pass wrote next to its
-// output (1 B per record instead of a 16-B record line): thread t of block b
-// counts records [b*RADIX_CHUNK + 8t, +8) (dense: every byte below n is a digit).
+// output (1 B per record instead of a 16-B record line).  A block counts PER
+// consecutive radix chunks (logical block XCD-contiguous, so a histogram row's
+// neighbouring chunks meet in one L2): thread t loads bytes [8t, 8t+8) of each
+// of them -- every load in flight together -- into LDS counters [digit][chunk].  One
+// chunk per block was 13 k blocks of 512 threads at SwissProt scale, ~51 us a
+// pass for 54 MB of digits: dispatch, not bytes.
+constexpr uint32_t HIST_U8_PER_MAX = 8;
 __global__ void __launch_bounds__(RADIX_THREADS)
-k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t* __restrict__ hist,
-                const unsigned long long* __restrict__ dn) {
-    __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
+k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t* __restrict__ hist, uint32_t G,
+                uint32_t per, const unsigned long long* __restrict__ dn) {
+    __shared__ uint32_t cnt[HIST_U8_PER_MAX * RADIX_D];
     if (dn) n = (uint32_t)min((unsigned long long)n, *dn);
     const uint32_t D = 1u << bits;
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-    for (uint32_t d = lane; d < D; d += 64) cnt[w][d] = 0;
-    wave_sync();
-    static_assert(RADIX_ITEMS == 8, "one 8-B load per thread");
-    const uint32_t cb = radix_chunk();
-    const uint32_t i0 = cb * RADIX_CHUNK + threadIdx.x * RADIX_ITEMS;
-    uint2 v = make_uint2(0u, 0u);
-    uint32_t nv = 0;  // digits of this thread below n
-    if (i0 + RADIX_ITEMS <= n) {
-        v = *reinterpret_cast<const uint2*>(dig + i0);
-        nv = RADIX_ITEMS;
-    } else if (i0 < n) {
-        uint32_t b[2] = {0u, 0u};
-        nv = n - i0;
-        for (uint32_t k = 0; k < nv; ++k) b[k >> 2] |= (uint32_t)dig[i0 + k] << (8 * (k & 3));
-        v = make_uint2(b[0], b[1]);
-    }
+    for (uint32_t i = threadIdx.x; i < per * D; i += RADIX_THREADS) cnt[i] = 0;
+    static_assert(RADIX_ITEMS == 8, "one 8-B load per thread and chunk");
+    const uint32_t c0 = xcd_contiguous_block() * per;
+    uint2 v[HIST_U8_PER_MAX];
+    uint32_t nv[HIST_U8_PER_MAX];  // digits of this thread below n, per chunk
 #pragma unroll
-    for (uint32_t k = 0; k < RADIX_ITEMS; ++k) {
-        const uint32_t d = ((k < 4 ? v.x : v.y) >> (8 * (k & 3))) & 0xFFu;
-        if (k < nv) atomicAdd(&cnt[w][d], 1u);
+    for (uint32_t j = 0; j < HIST_U8_PER_MAX; ++j) {
+        v[j] = make_uint2(0u, 0u);
+        nv[j] = 0;
+        const uint32_t i0 = (c0 + j) * RADIX_CHUNK + threadIdx.x * RADIX_ITEMS;
+        if (j < per && c0 + j < G) {
+            if (i0 + RADIX_ITEMS <= n) {
+                v[j] = *reinterpret_cast<const uint2*>(dig + i0);
+                nv[j] = RADIX_ITEMS;
+            } else if (i0 < n) {
+                uint32_t b[2] = {0u, 0u};
+                nv[j] = n - i0;
+                for (uint32_t k = 0; k < nv[j]; ++k) b[k >> 2] |= (uint32_t)dig[i0 + k] << (8 * (k & 3));
+                v[j] = make_uint2(b[0], b[1]);
+            }
+        }
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) {
-        uint32_t t = 0;
 #pragma unroll
-        for (int ww = 0; ww < RADIX_NW; ++ww) t += cnt[ww][d];
-        hist[(size_t)d * gridDim.x + cb] = t;
+    for (uint32_t j = 0; j < HIST_U8_PER_MAX; ++j) {
+#pragma unroll
+        for (uint32_t k = 0; k < RADIX_ITEMS; ++k) {
+            const uint32_t d = ((k < 4 ? v[j].x : v[j].y) >> (8 * (k & 3))) & 0xFFu;
+            if (k < nv[j]) atomicAdd(&cnt[d * per + j], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < per * D; i += RADIX_THREADS) {
+        const uint32_t d = i / per, j = i - d * per;  // consecutive threads: one row's consecutive chunks
+        if (c0 + j < G) hist[(size_t)d * G + c0 + j] = cnt[i];
     }
 }
 
@@ -2253,7 +2265,9 @@ hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint
                                 const unsigned long long* d_n) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
-    DBI_LAUNCH(k_radix_hist_u8, dim3(g), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist, d_n);
+    const uint32_t per = std::min<uint32_t>(HIST_U8_PER_MAX, std::max<uint32_t>(1u, g / 2048u));
+    DBI_LAUNCH(k_radix_hist_u8, dim3((g + per - 1) / per), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist, g, per,
+               d_n);
     return hipGetLastError();
 }
 
