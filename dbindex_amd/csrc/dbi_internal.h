@@ -190,7 +190,7 @@ constexpr int RADIX_THREADS = 512;
 constexpr int RADIX_ITEMS = 8;      // records per thread per radix block (4096: 64 KiB LDS exchange)
 constexpr int CHUNK_THREADS = 512;
 constexpr int CHUNK_CAP = 1984;     // records per chunk sorted in LDS (20 B each: 4 blocks per CU)
-constexpr int CHUNK_T = 1280;       // target chunk size (whole mass bins, ~T..T+maxbin; tools/ab_knobs.sh: 768-1536 measured)
+constexpr int CHUNK_T = 1536;       // target chunk size (whole mass bins; DBI_CHUNK_T A/B, round 3: 1024-1792 measured, 1536 best since the chunk pairs)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
 #ifndef DBI_WAVE_SORT_LIMIT
 #define DBI_WAVE_SORT_LIMIT 512
