@@ -100,7 +100,7 @@ struct dbi_handle {
     hipStream_t stream = nullptr;
     int bin_bits_max = 24;               // fine mass bins <= 2^bin_bits_max (radix passes of <= 8 bits)
     uint32_t split_above = dbi::BIG_CAP; // chunks above this many records take the MSD split path
-    uint32_t chunk_t = dbi::CHUNK_T;     // target records per chunk-sort block
+    uint32_t chunk_t = 0;                // target records per chunk-sort block (DBI_CHUNK_T; 0: chunk_target())
     bool timing = true;                  // per-stage kernel-attached events (dbi_set_timing)
     std::string timing_only;             // "" = every stage
     std::chrono::steady_clock::time_point t0;

@@ -140,11 +140,16 @@ int read_counters(dbi_handle* h) {
 // Every buffer the tail over n records (n_in slots) uses; build_tail calls it
 // before its first launch (a reallocation must never free a buffer that queued
 // kernels still use), callers that time the tail call it first.
+// records per chunk-sort block: DBI_CHUNK_T, else by the tail's size
+uint32_t chunk_target(const dbi_handle* h, uint64_t n) {
+    return h->chunk_t ? h->chunk_t : (uint32_t)(n >= CHUNK_T_MIN_RECS ? CHUNK_T : CHUNK_T_SMALL);
+}
+
 int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse, int passes, int bits_per) {
     int rc;
     const uint32_t n_in32 = sparse ? (uint32_t)n_in : (uint32_t)n;
     const size_t hist_elems = passes ? radix_hist_elems(n_in32, bits_per) : 1;
-    const uint32_t T = h->chunk_t;
+    const uint32_t T = chunk_target(h, n);
     const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + T - 1) / T, 1);
     const size_t seg_cap = giant_seg_cap(n);
     const size_t scan_need = std::max(scan_u32_tmp_elems(hist_elems), scan_u32_tmp_elems(2 * (uint64_t)nchunks));
@@ -179,7 +184,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     const int passes = radix_plan(nbins, sparse, width);
     const int bits_per = passes ? width[passes - 1] : 0;  // the widest digit
     const uint32_t n_in32 = sparse ? (uint32_t)n_in : n32;
-    const uint32_t T = h->chunk_t;
+    const uint32_t T = chunk_target(h, n);
     const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + T - 1) / T, 1);
     const size_t seg_cap = giant_seg_cap(n);
     if ((rc = tail_buffers(h, n, n_in, sparse, passes, bits_per))) return rc;
