@@ -26,7 +26,10 @@ from typing import Any, List, Optional, Sequence
 
 
 def _default_key() -> str:
-    return f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('TORCHELASTIC_RUN_ID', '')}"
+    # a restarted worker group (torchrun --max-restarts) gets a new key: a file a
+    # crashed rank 0 left behind is never read by the next attempt's ranks
+    return (f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('TORCHELASTIC_RUN_ID', '')}"
+            f"_{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}")
 
 
 class _Line:
@@ -85,19 +88,27 @@ class Coordinator:
             self.peers = [by_rank[r] for r in range(1, world)]
         else:
             t_end = time.time() + timeout
-            port = None
-            while port is None:
+            sock = None
+            while sock is None:
+                port = None
                 try:
                     with open(self.path) as fh:
                         txt = fh.read().strip()
                     port = int(txt) if txt else None
                 except (OSError, ValueError):
                     port = None
-                if port is None:
+                if port is not None:
+                    # a stale file (rank 0 gone, or not yet replaced) refuses the
+                    # connection: read the file again until the timeout
+                    try:
+                        sock = socket.create_connection(("127.0.0.1", port),
+                                                        timeout=max(1.0, t_end - time.time()))
+                    except OSError:
+                        sock = None
+                if sock is None:
                     if time.time() > t_end:
-                        raise TimeoutError(f"rank {rank}: no coordinator file {self.path} after {timeout:.0f} s")
+                        raise TimeoutError(f"rank {rank}: no coordinator at {self.path} after {timeout:.0f} s")
                     time.sleep(0.05)
-            sock = socket.create_connection(("127.0.0.1", port), timeout=timeout)
             sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             self.root = _Line(sock)
             self.root.send({"rank": rank})

@@ -3327,7 +3327,7 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
             const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
             if (threadIdx.x == 0) {
                 ucount[c] = tot;
-                if (BIG) atomicAdd(&ctr->n_big_recs, (unsigned long long)m);
+                atomicAdd(BIG ? &ctr->n_big_recs : &ctr->n_mid_recs, (unsigned long long)m);
             }
         }
     }

@@ -227,7 +227,13 @@ struct dbi_handle {
         bool giants = true;
         bool timing = false;
         char timing_only[32] = {};
-        bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }
+        // field by field: the struct's padding bytes are not guaranteed zero
+        bool operator==(const GraphKey& o) const {
+            return d_res == o.d_res && d_poff == o.d_poff && n_res == o.n_res && n_prot == o.n_prot &&
+                   cap == o.cap && last_kept == o.last_kept && alloc_gen == o.alloc_gen && dp_gen == o.dp_gen &&
+                   grid_mid == o.grid_mid && grid_big == o.grid_big && giants == o.giants && timing == o.timing &&
+                   std::strncmp(timing_only, o.timing_only, sizeof(timing_only)) == 0;
+        }
     };
     uint64_t dp_gen = 0;                  // bumped when dp changes (dbi_set_windows, bucket drop)
     bool use_graph = true;                // DBI_BUILD_GRAPH=0: never
@@ -314,6 +320,7 @@ int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse);  // bui
 int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
                const unsigned long long* d_n_in = nullptr, const unsigned long long* d_n = nullptr, uint64_t n_est = 0, bool est = false);
 int ensure_qdir(dbi_handle* h, hipStream_t s);  // query directory of the current index
+void drop_graph(dbi_handle* h);                 // the captured warm build graph, if any
 int finish_build(dbi_handle* h);
 
 }  // namespace dbi

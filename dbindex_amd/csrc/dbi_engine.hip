@@ -308,8 +308,12 @@ int finish_build(dbi_handle* h) {
         sg.bytes = sg.cR * (double)h->n_res + sg.cN * (double)st.n_kept + sg.cU * (double)st.n_unique +
                    sg.cP * (double)(h->n_prot + 1) + sg.cB * (double)st.n_bins + sg.c0;
         // the chunk-sort tiers split the records: 16 B in + 16 B out each, in the tier that sorted it
+        // (chunk_sort's read of a chunk it hands to the mid tier is overhead, not credited)
         const double big = (double)h->hc.n_big_recs, giant = (double)h->hc.n_giant_recs;
-        if (std::strcmp(sg.name, "chunk_sort") == 0) sg.bytes = 32.0 * std::max(0.0, (double)st.n_kept - big - giant);
+        const double mid = (double)h->hc.n_mid_recs;
+        if (std::strcmp(sg.name, "chunk_sort") == 0)
+            sg.bytes = 32.0 * std::max(0.0, (double)st.n_kept - mid - big - giant);
+        else if (std::strcmp(sg.name, "chunk_sort_mid") == 0) sg.bytes = 32.0 * mid;
         else if (std::strcmp(sg.name, "chunk_sort_big") == 0) sg.bytes = 32.0 * big;
         else if (std::strcmp(sg.name, "chunk_sort_giant") == 0) sg.bytes = 32.0 * giant;
     }

@@ -162,6 +162,7 @@ struct Counters {
     unsigned int n_seg[GIANT_PASSES + 1];  // giant split: segments in work list p
     unsigned int n_leaf_small, n_leaf_big, n_fallback;
     unsigned long long n_big_recs, n_giant_recs;  // records in chunks sorted by the big / giant paths
+    unsigned long long n_mid_recs;                // records in chunks sorted by the mid path (chunk_sort_mid)
     // what the tail of a device-sized warm build sorts (k_tail_counts): the
     // digest's slots / records, or 0 when they did not fit the buffer (the
     // skipped tiles left stale slots behind; the build is redone)

@@ -30,7 +30,10 @@ using namespace dbi;
 namespace dbi {
 namespace {
 
-constexpr char MAGIC[8] = {'D', 'B', 'I', 'H', 'I', 'P', '0', '1'};
+// format 02: the pinned tie order of equal-mass peptides is the end-bytes tag
+// (dbi_internal.h peptide_tag, round 3); a 01 file (FNV-1a tag) orders such
+// ties differently from a fresh build, so it is not reused (rebuilt instead)
+constexpr char MAGIC[8] = {'D', 'B', 'I', 'H', 'I', 'P', '0', '2'};
 
 struct dbi_index_header {
     char magic[8];

@@ -314,6 +314,10 @@ int replica_rebase(dbi_handle* h, const SliceSizes& z, hipStream_t s) {
 
 // the replica becomes the handle's index: the whole proteome, queried locally
 void replica_install(dbi_handle* h, const SliceSizes& z, uint64_t g_total, uint64_t g_dropped, uint64_t g_keys) {
+    // a captured build graph writes the index buffers being swapped out here
+    drop_graph(h);
+    h->prev_key_valid = false;
+    g_alloc_gen.fetch_add(1, std::memory_order_relaxed);
     std::swap(h->umass, h->r_mass);
     std::swap(h->upid, h->r_pid);
     std::swap(h->uoff, h->r_off);

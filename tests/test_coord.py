@@ -81,3 +81,43 @@ def test_bench_has_no_torch_import():
         elif isinstance(node, ast.ImportFrom) and node.module:
             names.add(node.module.split(".")[0])
     assert "torch" not in names
+
+
+def test_coordinator_stale_file_is_retried(tmp_path):
+    """A rendezvous file a crashed rank 0 left behind names a dead port: the
+    connection is refused, and the rank re-reads the file until the new rank 0
+    replaces it, instead of failing at once."""
+    import socket as _s
+    import threading
+    import time as _t
+    sys.path.insert(0, ROOT)
+    from dbindex_amd.coord import Coordinator
+    dead = _s.socket()
+    dead.bind(("127.0.0.1", 0))
+    port = dead.getsockname()[1]
+    dead.close()  # nothing listens there any more
+    (tmp_path / "dbindex_coord_stale").write_text(str(port))
+    out = {}
+
+    def rank1():
+        c = Coordinator(2, 1, key="stale", timeout=30, directory=str(tmp_path))
+        out["sum"] = c.allreduce([1.0], "sum")
+        c.close()
+
+    t = threading.Thread(target=rank1)
+    t.start()
+    _t.sleep(0.5)  # rank 1 is polling the stale file now
+    c0 = Coordinator(2, 0, key="stale", timeout=30, directory=str(tmp_path))
+    assert c0.allreduce([2.0], "sum") == [3.0]
+    c0.close()
+    t.join(timeout=30)
+    assert out["sum"] == [3.0]
+
+
+def test_coordinator_key_changes_with_restart(monkeypatch):
+    sys.path.insert(0, ROOT)
+    from dbindex_amd.coord import _default_key
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    k0 = _default_key()
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    assert _default_key() != k0

@@ -71,3 +71,45 @@ def test_warm_builds_and_graph_replays_match_oracle(env, monkeypatch, graph):
             assert_index_equal(eng, oa, f"graph={graph} timed build {k}")
             times = {name: ms for name, ms, _ in eng.stage_times()}
             assert times.get("digest", 0.0) > 0.0 and times.get("radix_scatter", 0.0) == 0.0
+
+
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_replays_over_rewritten_inputs(env, monkeypatch, graph):
+    """A caller that rewrites its residues IN PLACE (a reused staging buffer:
+    same d_res, n_res, n_prot) replays the captured graph over new contents.
+    Nothing the graph bakes in depends on the contents -- grids and buffers
+    are sized from capacities, every kernel reads the real counts on the
+    device -- and whatever the new contents outgrow (digest slots, chunk-list
+    grids, a first giant chunk) is caught by the one host check and the build
+    is redone.  Every build must equal the oracle of what the buffer holds."""
+    monkeypatch.setenv("DBI_BUILD_GRAPH", graph)
+    Engine, _, synchronize = env
+    a = fasta.config("human").slice(0, 6000)
+    # B: the same offsets over the residues reversed (other peptides, other counts)
+    b = fasta.PackedProteins(a.residues[::-1].copy(), a.offsets.copy(), a.defs)
+    # C: the first 250 proteins rewritten as GAAAAAAK repeats -- equal-mass
+    # spikes of ~11 k records each: giant chunks the earlier builds never had
+    spike = a.residues.copy()
+    e250 = int(a.offsets[250])
+    pat = np.frombuffer(b"GAAAAAAK", np.uint8)
+    spike[:e250] = np.resize(pat, e250)
+    c = fasta.PackedProteins(spike, a.offsets.copy(), a.defs)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    want = {k: cref.Index(cp, p.residues, p.offsets) for k, p in (("a", a), ("b", b), ("c", c))}
+    assert want["c"].n_total > want["a"].n_total
+    d_res, d_off = _dev(env, a)
+    contents = {"a": a, "b": b, "c": c}
+    with Engine(cp) as eng:
+        eng.set_timing(False)
+        seq = ["a", "a", "a", "a", "b", "b", "b", "c", "c", "c", "c", "a", "a", "b", "c"]
+        cur = "a"
+        for k, name in enumerate(seq):
+            if name != cur:  # rewrite the same device buffer
+                d_res.upload(contents[name].residues)
+                synchronize(0)
+                cur = name
+            st = eng.build_device(d_res.ptr, a.n_residues, d_off.ptr, a.n_proteins)
+            assert st.n_total == want[name].n_total, (k, name)
+            assert_index_equal(eng, want[name], f"graph={graph} build {k} ({name})")
+        m, t = query_masses(want["c"], 2000, seed=5)
+        assert_queries_equal(eng, want["c"], m, t, f"graph={graph} queries over the spiked proteome")

@@ -1,0 +1,274 @@
+"""GPU: the JNI shim EXECUTED (VERDICT r03 missing item 2).  No JDK exists in
+this image, so tests/jni_stub/fake_jvm.c plays the JVM: it fills the JNIEnv
+function table, and every ``Java_..._DBIndexStoreHip_*`` entry of
+java/src/main/c/dbindex_jni.c runs against libdbindex_hip.so on the GPU.
+What the shim would hand to Java -- the SeqList arrays toList turns into
+IndexedSequence objects, int[] entry keys, Strings, longs, the pending
+DBIndexStoreException and its message -- is compared with the oracle.
+
+Reference: DBIndexStore.java:37-192 (the interface the natives implement),
+DBIndexStoreSQLiteByteIndexMerge.java:386-481 (parseAddPeptideInfo: the
+fields of an IndexedSequence), Util.java:130-162 (flanks),
+DBIndexStoreSQLiteMult.java:470-571 (the reference's own store scenario)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from dbindex_amd import fasta
+from dbindex_amd.params import DBIndexSearchParams
+from oracle import cref, pyref
+from tests.helpers import query_masses
+from tests.jni_stub.harness import EXC, JavaException, Jvm, JniStore
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def jvm():
+    from dbindex_amd import _native
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    j = Jvm()
+    yield j
+    j.reset()
+
+
+def expected(oix, seqs, ids):
+    u = oix.unique()
+    out = []
+    for i in ids:
+        pids = [int(x) for x in u["occ_prot"][u["occ_off"][i]:u["occ_off"][i + 1]]]
+        p0, off, ln = int(u["prot_id"][i]), int(u["offset"][i]), int(u["length"][i])
+        left, right = pyref.get_residues(off, ln, seqs[p0])
+        out.append((seqs[p0][off:off + ln], float(u["mass"][i]), pids, left, right, off, ln))
+    return out
+
+
+def same(a, b, ctx=""):
+    assert len(a) == len(b), (ctx, len(a), len(b))
+    for x, y in zip(a, b):
+        assert x[0] == y[0] and np.float64(x[1]).view(np.uint64) == np.float64(y[1]).view(np.uint64), (ctx, x, y)
+        assert x[2:] == y[2:], (ctx, x, y)
+
+
+def last_error() -> str:
+    from dbindex_amd import _native
+    return _native.lib().dbi_last_error().decode()
+
+
+def clean(j):
+    assert j.violations() == 0, "a JNI call was made with an exception pending"
+    assert j.utf_outstanding() == 0, "GetStringUTFChars without ReleaseStringUTFChars"
+
+
+@pytest.mark.parametrize("device_digest", [True, False])
+def test_jni_build_and_queries_match_oracle(jvm, device_digest):
+    """DBIndexerHip's flow through the natives: init0, startAddSeq0,
+    addProteinDef0 per protein (the GPU digest at stopAddSeq0), then every
+    query-side native, against the oracle on a 300-protein proteome."""
+    prm = DBIndexSearchParams.trypsin(2)
+    cp = prm.to_c()
+    pp = fasta.config("1k").slice(0, 300)
+    seqs = pp.sequences()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    st = JniStore(jvm, cp)
+    try:
+        st.setDeviceDigest(device_digest)
+        st.init("synthetic_300.fasta")
+        st.startAddSeq()
+        if device_digest:
+            for i, s in enumerate(seqs):
+                assert st.addProteinDef(i, pp.defs[i], s) == i
+        else:  # the reference's per-peptide flow: cutSeq -> filterSequence -> addSequence
+            for i, s in enumerate(seqs):
+                assert st.addProteinDef(i, pp.defs[i], s) == i
+            for (mass, pid, off, ln, _dropped) in pyref.digest(prm, seqs):
+                assert st.filterSequence(mass, seqs[pid][off:off + ln]) == 0
+                st.addSequence(mass, off, ln, pid)
+        st.stopAddSeq()
+        clean(jvm)
+        assert st.indexExists() == 1
+        assert st.getTotalSeqCount() == oix.n_total
+        assert st.getNumberSequences() == oix.n_keys
+        assert np.array_equal(jvm.read(st.getEntryKeys()), oix.entry_keys())
+        for i in (0, 1, 150, 299):
+            assert jvm.read(st.proteinDef(i)) == pp.defs[i]
+            assert jvm.read(st.proteinSequence(i)) == seqs[i]
+        m, t = query_masses(oix, 200, seed=13)
+        for mi, ti in zip(m, t):
+            got = st.seq_list(st.getSequences(float(mi), float(ti)))
+            same(got, expected(oix, seqs, oix.query(float(mi), float(ti))), f"getSequences0({mi}, {ti})")
+        # multi-range: the reference's key-column binding (IndexMerge.java:300-312) included
+        for k in range(0, 40, 2):
+            got = st.seq_list(st.ranges("getSequencesRanges0", [m[k], m[k + 1]], [0.02, 0.5]))
+            same(got, expected(oix, seqs, oix.query_ranges([m[k], m[k + 1]], [0.02, 0.5])), "ranges")
+        got = st.seq_list(st.ranges("getSequencesRanges0", [m[0]], [t[0]]))
+        same(got, expected(oix, seqs, oix.query(float(m[0]), float(t[0]))), "one range")
+        clean(jvm)
+    finally:
+        st.close()
+        jvm.reset()
+
+
+def test_jni_build_errors(jvm):
+    """The GPU build's own status through stopAddSeq0: an addSequence flow
+    whose occurrences cannot be recorded (mass below 1 Da, the 16-B record's
+    floor) fails the build with a DBIndexStoreException carrying
+    dbi_last_error(); the host-side error paths run in test_jni_exec.py."""
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    st = JniStore(jvm, cp)
+    try:
+        st.init("errors.fasta")
+        st.startAddSeq()
+        assert st.addProteinDef(0, "sp|P1|X", "PEPTIDEKAAAAAAR") == 0
+        st.addSequence(0.5, 0, 3, 0)
+        with pytest.raises(JavaException) as ei:
+            st.stopAddSeq()
+        assert ei.value.cls == EXC and ei.value.msg == last_error() and "Da" in ei.value.msg
+        clean(jvm)
+    finally:
+        st.close()
+        jvm.reset()
+
+
+def test_jni_allocation_failures(jvm):
+    """Every JVM allocation of a SeqList (the object and its eight arrays)
+    failing in turn: the native returns NULL with the JVM's
+    OutOfMemoryError pending -- never another JNI call on top of it, never a
+    half-filled object handed over."""
+    prm = DBIndexSearchParams.trypsin(1)
+    cp = prm.to_c()
+    pp = fasta.config("1k").slice(0, 40)
+    seqs = pp.sequences()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    st = JniStore(jvm, cp)
+    try:
+        st.init("oom.fasta")
+        st.startAddSeq()
+        for i, s in enumerate(seqs):
+            st.addProteinDef(i, pp.defs[i], s)
+        st.stopAddSeq()
+        m = float(oix.unique()["mass"][oix.n_unique // 2])
+        want = expected(oix, seqs, oix.query(m, 0.5))
+        assert len(want) > 0
+        for k in range(9):
+            jvm.fail_alloc_at(k)
+            with pytest.raises(JavaException) as ei:
+                st.getSequences(m, 0.5)
+            assert ei.value.cls == "java/lang/OutOfMemoryError", k
+            clean(jvm)
+        jvm.fail_alloc_at(-1)
+        same(st.seq_list(st.getSequences(m, 0.5)), want, "after the failures")
+        for k in range(2):  # int[] of the entry keys; a String
+            jvm.fail_alloc_at(k if k == 0 else 0)
+            with pytest.raises(JavaException) as ei:
+                (st.getEntryKeys if k == 0 else (lambda: st.proteinDef(0)))()
+            assert ei.value.cls == "java/lang/OutOfMemoryError"
+            clean(jvm)
+        jvm.fail_alloc_at(-1)
+    finally:
+        st.close()
+        jvm.reset()
+
+
+# ---- the reference's own store scenario (DBIndexStoreSQLiteMult.main) --------------------------
+
+F32 = lambda x: float(np.float32(x))  # the reference passes float literals (6000.42323f, 8.9f)
+
+PROT_DEF1 = ("4R79.2 CE19650 WBGene00007067 Ras family status:Partially_confirmed TR:Q9XXA4 "
+             "protein_id:CAA20282.1")
+PROT_DEF2 = ("Reverse_4R79.2  CE19650 WBGene00007067 Ras family status:Partially_confirmed TR:Q9XXA4 "
+             "protein_id:CAA20282.1")
+PROTS = ["ABCDEFGHIJKL", "GHIJKLMNOPR"]
+# DBIndexStoreSQLiteMult.java:494-524: addSequence(mass, offset, length, ..., protId)
+ADDS = [(1.0, 0, 1, 0), (2.0, 0, 2, 0), (3.0, 0, 3, 0), (4.0, 0, 4, 0), (F32(6000.42323), 0, 5, 0),
+        (F32(6999.42323), 0, 6, 0), (3.0, 6, 3, 0),
+        (3.0, 1, 3, 1), (5.0, 2, 5, 1), (3.0, 0, 3, 1), (3.0, 0, 3, 1)]
+# :531 getSequences(10, 8.9f); :548-557 the four ranges, in the order added
+QUERY = (10.0, F32(8.9))
+RANGES = ([6.0, 2.0, 6.0, 6.0], [F32(1), F32(1), F32(1), F32(1.2)])
+
+
+def scenario_oracle(cp):
+    res = np.frombuffer("".join(PROTS).encode(), np.uint8)
+    off = np.array([0, len(PROTS[0]), len(PROTS[0]) + len(PROTS[1])], np.uint64)
+    occ = tuple(np.array([a[k] for a in ADDS]) for k in range(4))
+    return cref.Index(cp, res, off, occurrences=(occ[0], occ[3], occ[1], occ[2]))
+
+
+def test_reference_store_scenario_through_jni(jvm):
+    """DBIndexStoreSQLiteMult.main (:470-571) replayed through the natives:
+    two proteins, eleven addSequence calls (masses 1-4 Da, 6000.42323f and
+    6999.42323f, the duplicate GHI twice in the second protein), getSequences(10,
+    8.9f) and the redundant / overlapping four-range list.  The reference only
+    prints these answers; here each is compared with the oracle's store built
+    from the same occurrences.  Parameters: the library defaults
+    (dbindex.properties: index_factor 8, factor 10000)."""
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = scenario_oracle(cp)
+    st = JniStore(jvm, cp)
+    try:
+        st.setDeviceDigest(False)
+        st.init("./test.fasta")
+        st.startAddSeq()
+        assert st.addProteinDef(0, PROT_DEF1, PROTS[0]) == 0
+        for a in ADDS[:7]:
+            st.addSequence(*a)
+        assert st.addProteinDef(1, PROT_DEF2, PROTS[1]) == 1
+        for a in ADDS[7:]:
+            st.addSequence(*a)
+        st.stopAddSeq()
+        assert st.getTotalSeqCount() == oix.n_total == len(ADDS)
+        assert st.getNumberSequences() == oix.n_keys
+        assert np.array_equal(jvm.read(st.getEntryKeys()), oix.entry_keys())
+        got = st.seq_list(st.getSequences(*QUERY))
+        want = expected(oix, PROTS, oix.query(*QUERY))
+        same(got, want, "getSequences(10, 8.9f)")
+        # AB, ABC / GHI / HIJ (one key row, bit-identical masses), ABCD, IJKLM; not A (1 Da < 1.1)
+        assert sorted(g[0] for g in got) == ["AB", "ABC", "ABCD", "GHI", "HIJ", "IJKLM"]
+        ghi = [g for g in got if g[0] == "GHI"][0]
+        assert ghi[2] == [0, 1, 1]  # protein ids in insertion order, duplicates kept (:678-681)
+        got = st.seq_list(st.ranges("getSequencesRanges0", *RANGES))
+        same(got, expected(oix, PROTS, oix.query_ranges(*RANGES)), "four ranges")
+        clean(jvm)
+    finally:
+        st.close()
+        jvm.reset()
+
+
+def test_reference_store_scenario_python_store():
+    """The same scenario through the Python mirror (DBIndexStoreHip over
+    ctypes), plus the main's ProteinCache, which holds only the first protein:
+    the reference then resolves the second protein's peptides through a null
+    sequence (Util.getResidues dereferences it, Util.java:132) and the query
+    fails -- here a DBIndexStoreException, not a silent wrong answer."""
+    from dbindex_amd import _native
+    from dbindex_amd.store import DBIndexStoreHip, MassRange, ProteinCache
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    prm = DBIndexSearchParams.trypsin(2)
+    oix = scenario_oracle(prm.to_c())
+    st = DBIndexStoreHip(prm)
+    st.init("./test.fasta")
+    st.startAddSeq()
+    assert st.addProteinDef(0, PROT_DEF1, PROTS[0]) == 0
+    for (m, off, ln, pid) in ADDS[:7]:
+        st.addSequence(m, off, ln, proteinId=pid)
+    assert st.addProteinDef(1, PROT_DEF2, PROTS[1]) == 1
+    for (m, off, ln, pid) in ADDS[7:]:
+        st.addSequence(m, off, ln, proteinId=pid)
+    st.stopAddSeq()
+    got = [(s.getSequence(), s.getMass(), list(s.getProteinIds()), s.getResLeft(), s.getResRight(),
+            s.getSequenceOffset(), s.getSequenceLen()) for s in st.getSequences(*QUERY)]
+    same(got, expected(oix, PROTS, oix.query(*QUERY)), "python store")
+    rs = [MassRange(m, t) for m, t in zip(*RANGES)]
+    got = [(s.getSequence(), s.getMass(), list(s.getProteinIds()), s.getResLeft(), s.getResRight(),
+            s.getSequenceOffset(), s.getSequenceLen()) for s in st.getSequences(rs)]
+    same(got, expected(oix, PROTS, oix.query_ranges(*RANGES)), "python store ranges")
+    pc = ProteinCache()
+    pc.addProtein("4R79.2", "ABCDEFGHIJKL")  # :491, the only protein the store's cache gets
+    st.setProteinCache(pc)
+    with pytest.raises(_native.DBIndexStoreException):
+        st.getSequences(*QUERY)
+    st.close()

@@ -3,6 +3,8 @@ the DBIndexStore mirror's indexExists reuse contract (DBIndexer.java:522-527):
 the loaded index answers exactly like the oracle's."""
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -46,6 +48,21 @@ def test_engine_save_load_roundtrip(Engine, tmp_path):
     with Engine(DBIndexSearchParams.trypsin(1).to_c()) as c:
         with pytest.raises(_native.DBIndexStoreException):
             c.load(path)
+    # a format-01 file (the FNV-1a tie order of round 2) is neither reused nor
+    # loaded: its equal-mass ties would be ordered unlike a fresh build's
+    old = bytearray(open(path, "rb").read())
+    assert old[:8] == b"DBIHIP02"
+    old[6:8] = b"01"
+    p01 = str(tmp_path / "v01.dbihip")
+    open(p01, "wb").write(bytes(old))
+    def matches(pth):
+        v = ctypes.c_int(-1)
+        _native.check(_native.lib().dbi_index_file_matches(ctypes.byref(cp), pth.encode(), ctypes.byref(v)))
+        return v.value
+    assert matches(p01) == 0 and matches(path) == 1
+    with Engine(cp) as d:
+        with pytest.raises(_native.DBIndexStoreException):
+            d.load(p01)
 
 
 def test_store_persist_and_reuse(tmp_path):
