@@ -673,15 +673,17 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
     log(f"[rank {rank}] trembl proteins [{p0}, {p1}): {n_res_all} residues in {len(chunks)} chunks, "
         f"generated in HBM ({time.time() - t0:.1f}s)")
 
-    def step():
+    def count_only():
         tot = 0
         for c in chunks:
             tot += eng.count_device(*c)[0]
         return tot
 
-    def bucket_pass():
-        # the COUNT walk again with the SQLiteMult bucket of every occurrence
-        # (dbi_count_buckets), then the buckets of all ranks summed (RCCL)
+    def step():
+        # the configs[4] step: every occurrence counted into
+        # its SQLiteMult bucket ((int)m / BUCKET_MASS_RANGE,
+        # DBIndexStoreSQLiteMult.java:215-217), the per-bucket counts of all
+        # ranks summed by RCCL (ncclAllReduce); totalSeqCount = their sum
         d_hist.upload(zeros)
         tot = 0
         for c in chunks:
@@ -708,20 +710,24 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
         n_all, res_all = coord.allreduce([n_all, float(n_res_all)], "sum")
     else:
         res_all = float(n_res_all)
-    # per-bucket counts: one more pass, timed on its own (the step above is the count alone)
-    if world > 1:
-        coord.barrier()
-    t_b = time.perf_counter()
-    bucket_pass()
-    synchronize(dev)
-    if world > 1:
-        coord.barrier()
-    t_b = time.perf_counter() - t_b
-    if world > 1:
-        t_b = coord.allreduce([t_b], "max")[0]
     hist = (d_hist_all if comm is not None else d_hist).download(np.uint64, nb + 1)
     if int(hist.sum()) * args.steps != int(n_all):
         raise RuntimeError(f"bucket counts {int(hist.sum())} do not add up to totalSeqCount {int(n_all) // args.steps}")
+    # beside it: the plain count (totalSeqCount only, dbi_count), timed on its own
+    if world > 1:
+        coord.barrier()
+    synchronize(dev)
+    t_c = time.perf_counter()
+    n_c = count_only()
+    synchronize(dev)
+    if world > 1:
+        coord.barrier()
+    t_c = time.perf_counter() - t_c
+    if world > 1:
+        t_c = coord.allreduce([t_c], "max")[0]
+        n_c = coord.allreduce([float(n_c)], "sum")[0]
+    if int(n_c) != int(n_all) // args.steps:
+        raise RuntimeError(f"dbi_count {int(n_c)} != the bucket pass's totalSeqCount {int(n_all) // args.steps}")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cref
@@ -771,9 +777,11 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
             # occurrences per SQLiteMult bucket, (int)m / BUCKET_MASS_RANGE (the last: past the last bucket)
             "bucket_counts": {"bucket_mass_range_da": 8000 // nb, "counts": [int(x) for x in hist],
                               "combined": "ncclAllReduce (dbi_comm_allreduce_u64)" if world > 1 else "one rank",
-                              "ms": 1e3 * t_b, "peptides_per_s": float(hist.sum()) / t_b,
-                              "kind": "dbi_count_buckets over every chunk (+ the allreduce), one pass after the "
-                                      "timed steps; the last entry is past the last bucket"},
+                              "kind": "the timed step: dbi_count_buckets over every chunk + the allreduce; the "
+                                      "last entry is past the last bucket"},
+            "count_only": {"ms": 1e3 * t_c, "peptides_per_s": n_c / t_c,
+                           "kind": "dbi_count (totalSeqCount only, no buckets) over every chunk, one pass after "
+                                   "the timed steps"},
             "roofline": {"bound": "hbm", "kernel": "digest_count",
                          "achieved": alg / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,

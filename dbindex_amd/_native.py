@@ -46,6 +46,7 @@ class DbiShardStats(ctypes.Structure):
         ("g_total", c_uint64), ("g_dropped", c_uint64), ("g_kept", c_uint64), ("g_unique", c_uint64),
         ("g_keys", c_uint64), ("digest_ms", c_double), ("partition_ms", c_double),
         ("exchange_ms", c_double), ("merge_ms", c_double), ("merge_gpu_ms", c_double),
+        ("split_sampled", c_int32), ("split_rounds", c_int32),
     ]
 
 
@@ -135,6 +136,7 @@ SIGNATURES = [
     ("dbi_count_buckets", c_int, [P, P, c_uint64, P, c_uint64, P, POINTER(c_uint64), POINTER(c_uint64)]),
     ("dbi_comm_unique_id", c_int, [P]),
     ("dbi_comm_init", c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
+    ("dbi_comm_init_host", c_int, [c_char_p, c_int, c_int, c_int, c_uint64, POINTER(c_void_p)]),
     ("dbi_comm_destroy", None, [P]),
     ("dbi_comm_allgatherv", c_int, [P, P, P, P, P]),
     ("dbi_comm_allreduce_f64", c_int, [P, P, P, c_uint32, c_int]),

@@ -723,19 +723,47 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
 // recounted by the exact walk, so the counts equal the emit pass's exactly.
 // (Prefix error over a window < 3e-7 Da.)
 // ---------------------------------------------------------------------------
-constexpr double CUT_EPS = 1e-4;  // > 2 x the fixed-point rounding of the prefix tables (7.6e-6 Da each)
-constexpr uint32_t PM_BLOCK = 64;  // positions per fp64 prefix base
+// Window prefix masses in fixed point: p[i] = round(prefix of window
+// positions [0, i] x 2^9) as u32 (residue masses < 1024 Da, DevParams::
+// cut_count: a window's prefix < 4.5e6 Da < 2^32 / 512).  A peptide's mass
+// m0 + P(e) - P(s-1) compares with a limit X as the integer D = p[e] - p[s-1]
+// against T = floor((X - m0) x 2^9): |D - 512 (P(e) - P(s-1))| <= 1 (two
+// roundings; the fp64 sums behind them are exact to ~1e-9 Da), so D >= T + 3
+// is surely m >= X + 2^-9 and D <= T - 3 surely m < X; in between (within
+// ~0.006 Da of a limit: ~1e-4 of the starts) the start is recounted by the
+// exact walk.  One u32 LDS read per probe, integer compares.
+constexpr int64_t CUT_EPS_FX = 3;
+constexpr double CUT_SCALE = 512.0;
 
-// Window prefix masses of positions [0, i]: base[i / 64] (fp64, prefix before
-// the 64-position block) + off[i] / 2^16 Da (fixed point; within a block < 64
-// residues x 1024 Da, DevParams::cut_count).
 struct CutSmem {
-    double base[WIN / PM_BLOCK + 1];
-    uint32_t off[WIN];
+    uint32_t p[WIN];
 };
 
-__device__ __forceinline__ double cut_prefix(const CutSmem& cs, uint32_t i) {
-    return cs.base[i / PM_BLOCK] + (double)cs.off[i] * (1.0 / 65536.0);
+// T of a limit X (clamped: an infinite or huge limit is never reached)
+__device__ __forceinline__ int64_t cut_threshold(double x, double m0) {
+    const double t = floor((x - m0) * CUT_SCALE);
+    return t < -1e15 ? (int64_t)-1e15 : t > 1e15 ? (int64_t)1e15 : (int64_t)t;
+}
+
+// +1: surely m >= X; -1: surely m < X; 0: too close to tell
+__device__ __forceinline__ int cut_cmp(int64_t d, int64_t t) {
+    return d >= t + CUT_EPS_FX ? 1 : d <= t - CUT_EPS_FX ? -1 : 0;
+}
+
+// the limits of a count kernel, in window-prefix units
+struct CutLimits {
+    int64_t t_min, t_max, t_drop;
+    int64_t t_b[8];  // bucket boundaries (k + 1) x BUCKET_MASS_RANGE, k < min(NUM_BUCKETS, 8)
+};
+
+__device__ __forceinline__ CutLimits cut_limits(const DevParams& dp) {
+    CutLimits cl;
+    cl.t_min = cut_threshold(dp.min_mh, dp.m0);
+    cl.t_max = cut_threshold(dp.max_mh, dp.m0);
+    cl.t_drop = cut_threshold(dp.drop_mass, dp.m0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cl.t_b[k] = cut_threshold((double)((k + 1) * dp.br), dp.m0);
+    return cl;
 }
 
 struct CutCount {
@@ -765,45 +793,54 @@ __device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi) {
 }
 
 // Bucket counts of one thread's starts (ascending) when NUM_BUCKETS <= 8: the
-// per-thread counts in registers, and for every bucket boundary B_k = (k+1) x
-// BUCKET_MASS_RANGE the first window position q whose prefix mass reaches it
-// for the current start (prefix(q) >= B_k - m0 + prefix(start - 1)).  That
-// position only moves forward from one start to the next (the threshold
-// grows with the start's prefix), so it is tracked, not searched: about one
-// LDS read per boundary and start instead of a binary search.
+// per-thread counts in registers, and for every bucket boundary the first
+// window position whose prefix passes it for the current start (p[q] > p[s-1]
+// + T_k).  That position only moves forward from one start to the next (the
+// threshold grows with the start's prefix), so it is tracked, not searched:
+// about one LDS read per boundary and start.
 constexpr int HIST_FAST_MAX = 8;
 struct HistTrack {
     uint32_t t[HIST_FAST_MAX];  // the boundary's position (0: not yet found)
-    double p[HIST_FAST_MAX];    // prefix mass there
     uint32_t c[HIST_FAST_MAX + 1];
 };
 
-// first q in [t, hi + 1] with prefix(q) >= x (prefix non-decreasing): gallop, then bisect
-__device__ __forceinline__ uint32_t prefix_seek(const CutSmem& cs, uint32_t t, uint32_t hi, double x) {
-    if (t > hi || cut_prefix(cs, t) >= x) return t;
-    uint32_t lo = t, step = 1;  // prefix(lo) < x
-    while (lo + step <= hi && cut_prefix(cs, lo + step) < x) {
+// first q in [t, hi + 1] with p[q] > a (p non-decreasing): gallop, then bisect
+__device__ __forceinline__ uint32_t prefix_seek(const CutSmem& cs, uint32_t t, uint32_t hi, int64_t a) {
+    if (t > hi || (int64_t)cs.p[t] > a) return t;
+    uint32_t lo = t, step = 1;  // p[lo] <= a
+    while (lo + step <= hi && (int64_t)cs.p[lo + step] <= a) {
         lo += step;
         step <<= 1;
     }
-    uint32_t up = min(lo + step, hi + 1);  // prefix(up) >= x, or up = hi + 1
+    uint32_t up = min(lo + step, hi + 1);  // p[up] > a, or up = hi + 1
     while (up - lo > 1) {
         const uint32_t mid = (lo + up) >> 1;
-        if (cut_prefix(cs, mid) >= x) up = mid; else lo = mid;
+        if ((int64_t)cs.p[mid] > a) up = mid; else lo = mid;
     }
     return up;
+}
+
+// first e in [a, b] with D(e) > t (D non-decreasing; b + 1 when none)
+template <typename DF>
+__device__ __forceinline__ uint32_t first_above(DF D, uint32_t a, uint32_t b, int64_t t) {
+    uint32_t lo = a, hi = b + 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (D(mid) > t) hi = mid; else lo = mid + 1;
+    }
+    return lo;
 }
 
 // HIST: the ends' SQLiteMult buckets as well -- ht (NUM_BUCKETS <= 8): the
 // tracked boundaries above, counts in registers; otherwise the boundaries
 // k * BUCKET_MASS_RANGE located by binary search like the limits above,
-// counts into the LDS hist.  An end's mass within CUT_EPS of a boundary (or
-// more than 7 boundaries in one walk, binary-search path) and the start is
-// recounted by the exact walk.
+// counts into the LDS hist.  An end too close to a boundary (or more than 7
+// boundaries in one walk, binary-search path) and the start is recounted by
+// the exact walk.
 template <bool HIST = false>
-__device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const DigestSmem& sm, const CutSmem& cs,
-                                                   uint32_t nbytes, uint32_t ps, uint32_t* hist, HistTrack& ht,
-                                                   bool fast) {
+__device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const CutLimits& cl, const DigestSmem& sm,
+                                                   const CutSmem& cs, uint32_t nbytes, uint32_t ps, uint32_t* hist,
+                                                   HistTrack& ht, bool fast) {
     CutCount r{0u, 0u, true};
     if (!(dp.m0 <= dp.max_mh)) return r;  // while condition before the first residue (:284)
     if (ps + 2 > nbytes) { r.exact = false; return r; }
@@ -821,24 +858,22 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Di
         H = xk - 1;
         ends = true;
     }
-    const double pb = ps > 0 ? cut_prefix(cs, ps - 1) : 0.0;
-    auto M = [&](uint32_t e) { return dp.m0 + (cut_prefix(cs, ps + e) - pb); };
+    const int64_t pb = ps > 0 ? (int64_t)cs.p[ps - 1] : 0;
+    auto D = [&](uint32_t e) -> int64_t { return (int64_t)cs.p[ps + e] - pb; };
     // last position with m <= maxMH (the walk stops past it: :284, :326)
     int Y;
     {
-        const double mH = M(H);
-        if (mH <= dp.max_mh) {
-            if (dp.max_mh - mH <= CUT_EPS || !ends) { r.exact = false; return r; }
+        const int c = cut_cmp(D(H), cl.t_max);
+        if (c == 0) { r.exact = false; return r; }
+        if (c < 0) {
+            if (!ends) { r.exact = false; return r; }
             Y = (int)H;
         } else {
-            if (mH - dp.max_mh <= CUT_EPS) { r.exact = false; return r; }
-            uint32_t a = 0, b = H;  // first e with M(e) > maxMH
-            while (a < b) {
-                const uint32_t mid = (a + b) >> 1;
-                if (M(mid) > dp.max_mh) b = mid; else a = mid + 1;
+            const uint32_t a = first_above(D, 0u, H, cl.t_max);  // first e with m > maxMH
+            if (cut_cmp(D(a), cl.t_max) <= 0 || (a > 0 && cut_cmp(D(a - 1), cl.t_max) >= 0)) {
+                r.exact = false;
+                return r;
             }
-            if (a > 0 && dp.max_mh - M(a - 1) <= CUT_EPS) { r.exact = false; return r; }
-            if (M(a) - dp.max_mh <= CUT_EPS) { r.exact = false; return r; }
             Y = (int)a - 1;
         }
     }
@@ -846,21 +881,14 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Di
     int lo = dp.min_len - 1;
     if (Y < lo) return r;
     {
-        const double ml = M((uint32_t)lo);
-        if (fabs(ml - dp.min_mh) <= CUT_EPS) { r.exact = false; return r; }
-        if (ml < dp.min_mh) {
-            const double my = M((uint32_t)Y);
-            if (fabs(my - dp.min_mh) <= CUT_EPS) { r.exact = false; return r; }
-            if (my < dp.min_mh) return r;
-            uint32_t a = (uint32_t)lo + 1, b = (uint32_t)Y;  // first e with M(e) >= minMH
-            while (a < b) {
-                const uint32_t mid = (a + b) >> 1;
-                if (M(mid) >= dp.min_mh) b = mid; else a = mid + 1;
-            }
-            if (fabs(M(a) - dp.min_mh) <= CUT_EPS || fabs(M(a - 1) - dp.min_mh) <= CUT_EPS) {
-                r.exact = false;
-                return r;
-            }
+        const int c = cut_cmp(D((uint32_t)lo), cl.t_min);
+        if (c == 0) { r.exact = false; return r; }
+        if (c < 0) {
+            const int cy = cut_cmp(D((uint32_t)Y), cl.t_min);
+            if (cy == 0) { r.exact = false; return r; }
+            if (cy < 0) return r;
+            const uint32_t a = first_above(D, (uint32_t)lo + 1, (uint32_t)Y, cl.t_min);
+            if (cut_cmp(D(a), cl.t_min) <= 0 || cut_cmp(D(a - 1), cl.t_min) >= 0) { r.exact = false; return r; }
             lo = (int)a;
         }
     }
@@ -868,15 +896,11 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Di
     const uint32_t n = (uint32_t)__popcll(em);
     uint32_t nd = 0;
     if (dp.drop_mass <= dp.max_mh && n) {  // bucket > NUM_BUCKETS-1 (:282-288): the cuts from m >= drop_mass on
-        const double my = M((uint32_t)Y), ml = M((uint32_t)lo);
-        if (fabs(my - dp.drop_mass) <= CUT_EPS || fabs(ml - dp.drop_mass) <= CUT_EPS) { r.exact = false; return r; }
-        if (my >= dp.drop_mass) {
-            uint32_t a = (uint32_t)lo, b = (uint32_t)Y;  // first e with M(e) >= drop_mass
-            while (a < b) {
-                const uint32_t mid = (a + b) >> 1;
-                if (M(mid) >= dp.drop_mass) b = mid; else a = mid + 1;
-            }
-            if (fabs(M(a) - dp.drop_mass) <= CUT_EPS || (a > 0 && fabs(M(a - 1) - dp.drop_mass) <= CUT_EPS)) {
+        const int cy = cut_cmp(D((uint32_t)Y), cl.t_drop), cl0 = cut_cmp(D((uint32_t)lo), cl.t_drop);
+        if (cy == 0 || cl0 == 0) { r.exact = false; return r; }
+        if (cy > 0) {
+            const uint32_t a = first_above(D, (uint32_t)lo, (uint32_t)Y, cl.t_drop);
+            if (cut_cmp(D(a), cl.t_drop) <= 0 || (a > 0 && cut_cmp(D(a - 1), cl.t_drop) >= 0)) {
                 r.exact = false;
                 return r;
             }
@@ -884,42 +908,40 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Di
         }
     }
     if (HIST && n && fast) {
-        // absolute window positions of the first / last end; M(e) >= B <=> prefix(ps + e) >= B - m0 + pb
+        // absolute window positions of the first / last end; end q is past
+        // boundary k when p[q] > pb + T_k (the first such q tracked per k)
         const uint32_t qlo = ps + (uint32_t)lo, qhi = ps + (uint32_t)Y;
-        const double plo = cut_prefix(cs, qlo), phi = cut_prefix(cs, qhi), xb = pb - dp.m0;
+        const int64_t dlo = D((uint32_t)lo), dhi = D((uint32_t)Y);
         uint32_t pos[HIST_FAST_MAX];
         bool bad = false;
 #pragma unroll
         for (int k = 0; k < HIST_FAST_MAX; ++k) {
             pos[k] = qhi + 1u;
             if (k < dp.nb) {
-                const double x = (double)((k + 1) * dp.br) + xb;
-                uint32_t t;
-                if (x > phi + CUT_EPS) t = qhi + 1u;        // past every end of this start
-                else if (x < plo - CUT_EPS) t = qlo;        // before every end
-                else {
-                    t = ht.t[k];
-                    double pt = ht.p[k];  // prefix(t), cached
-                    if (t < qlo || t > qhi + 1u) {  // first use, or left behind: search
-                        t = prefix_seek(cs, qlo, qhi, x);
-                        pt = cut_prefix(cs, t);
+                const int64_t t = cl.t_b[k];
+                const int chi = cut_cmp(dhi, t), clo = cut_cmp(dlo, t);
+                if (chi < 0) {
+                    pos[k] = qhi + 1u;  // every end below the boundary
+                } else if (clo > 0) {
+                    pos[k] = qlo;       // every end past it
+                } else {
+                    const int64_t athr = pb + t;
+                    uint32_t q = ht.t[k];
+                    if (q < qlo || q > qhi + 1u) {  // first use, or left behind: search
+                        q = prefix_seek(cs, qlo, qhi, athr);
                     } else {
                         int steps = 0;  // usually one position per start
-                        while (t <= qhi && pt < x && steps < 4) {
-                            pt = cut_prefix(cs, ++t);
+                        while (q <= qhi && (int64_t)cs.p[q] <= athr && steps < 4) {
+                            ++q;
                             ++steps;
                         }
-                        if (t <= qhi && pt < x) {
-                            t = prefix_seek(cs, t, qhi, x);
-                            pt = cut_prefix(cs, t);
-                        }
+                        if (q <= qhi && (int64_t)cs.p[q] <= athr) q = prefix_seek(cs, q, qhi, athr);
                     }
-                    ht.t[k] = t;
-                    ht.p[k] = pt;
-                    if (t <= qhi && pt - x <= CUT_EPS) bad = true;
-                    if (t > qlo && x - cut_prefix(cs, t - 1) <= CUT_EPS) bad = true;
+                    ht.t[k] = q;
+                    if (q <= qhi && cut_cmp((int64_t)cs.p[q] - pb, t) <= 0) bad = true;
+                    if (q > qlo && cut_cmp((int64_t)cs.p[q - 1] - pb, t) >= 0) bad = true;
+                    pos[k] = q;
                 }
-                pos[k] = t;
             }
         }
         if (bad) { r.exact = false; return r; }
@@ -937,26 +959,24 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Di
         for (int k = 1; k <= HIST_FAST_MAX; ++k)
             if (k == dp.nb) ht.c[k] += last;
     } else if (HIST && n) {
-        const double ml = M((uint32_t)lo), my = M((uint32_t)Y);
-        auto near_edge = [&](double x) {
-            const int k = java_d2i(x) / dp.br;
-            return x - (double)(k * dp.br) <= CUT_EPS || (double)((k + 1) * dp.br) - x <= CUT_EPS;
-        };
-        if (near_edge(ml) || near_edge(my)) { r.exact = false; return r; }
+        // the buckets of the first and last end (exact ones: none within ~0.006 Da of a boundary)
+        const double ml = dp.m0 + (double)D((uint32_t)lo) / CUT_SCALE, my = dp.m0 + (double)D((uint32_t)Y) / CUT_SCALE;
         const int b0 = java_d2i(ml) / dp.br, b1 = java_d2i(my) / dp.br;
+        auto tb = [&](int k) { return cut_threshold((double)(k * dp.br), dp.m0); };  // boundary k x BR
+        if (cut_cmp(D((uint32_t)lo), tb(b0)) <= 0 || cut_cmp(D((uint32_t)lo), tb(b0 + 1)) >= 0 ||
+            cut_cmp(D((uint32_t)Y), tb(b1)) <= 0 || cut_cmp(D((uint32_t)Y), tb(b1 + 1)) >= 0) {
+            r.exact = false;
+            return r;
+        }
         if (b1 - b0 > 7) { r.exact = false; return r; }
         uint32_t at[7];  // first position of bucket b0 + 1 + i
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
             at[i] = (uint32_t)Y + 1u;
             if (i < b1 - b0) {
-                const double B = (double)((b0 + 1 + i) * dp.br);
-                uint32_t a = (uint32_t)lo + 1u, b = (uint32_t)Y;  // M(lo) < B <= M(Y)
-                while (a < b) {
-                    const uint32_t mid = (a + b) >> 1;
-                    if (M(mid) >= B) b = mid; else a = mid + 1;
-                }
-                if (M(a) - B <= CUT_EPS || B - M(a - 1) <= CUT_EPS) { r.exact = false; return r; }
+                const int64_t t = tb(b0 + 1 + i);
+                const uint32_t a = first_above(D, (uint32_t)lo + 1u, (uint32_t)Y, t);  // m(lo) < B <= m(Y)
+                if (cut_cmp(D(a), t) <= 0 || cut_cmp(D(a - 1), t) >= 0) { r.exact = false; return r; }
                 at[i] = a;
             }
         }
@@ -981,7 +1001,9 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Di
     return r;
 }
 
-// Build the prefix-mass tables from the staged window (all threads; ends with a barrier).
+// Build the fixed-point prefix table from the staged window (all threads;
+// ends with a barrier): fp64 sums per thread, a block scan, then each
+// position's prefix rounded to 2^-9 Da
 __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nbytes, double* s_dtmp) {
     constexpr uint32_t E = (WIN + DIGEST_THREADS - 1) / DIGEST_THREADS;
     const uint32_t lo = threadIdx.x * E;
@@ -993,23 +1015,13 @@ __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nby
     }
     double dtot;
     double mrun = block_excl_scan<DIGEST_THREADS, double>(msum, s_dtmp, dtot);
-    if (threadIdx.x == 0) cs.base[0] = 0.0;
-    double pm[E];
 #pragma unroll
     for (uint32_t k = 0; k < E; ++k) {
         const uint32_t i = lo + k;
-        pm[k] = 0.0;
         if (i < nbytes) {
             mrun += sm.mass[sm.win[i] & 0xFFu];
-            pm[k] = mrun;
-            if (i % PM_BLOCK == PM_BLOCK - 1) cs.base[i / PM_BLOCK + 1] = mrun;
+            cs.p[i] = (uint32_t)__double2ull_rn(mrun * CUT_SCALE);
         }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < E; ++k) {
-        const uint32_t i = lo + k;
-        if (i < nbytes) cs.off[i] = (uint32_t)__double2ll_rn((pm[k] - cs.base[i / PM_BLOCK]) * 65536.0);
     }
     __syncthreads();
 }
@@ -1030,21 +1042,19 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     HistTrack ht;
     const bool fast = HIST && dp.nb <= HIST_FAST_MAX;
 #pragma unroll
-    for (int k = 0; k < HIST_FAST_MAX; ++k) {
-        ht.t[k] = 0;
-        ht.p[k] = 0.0;
-    }
+    for (int k = 0; k < HIST_FAST_MAX; ++k) ht.t[k] = 0;
 #pragma unroll
     for (int k = 0; k <= HIST_FAST_MAX; ++k) ht.c[k] = 0;
     TileCtx tc;
     const uint32_t ncand = digest_prepare<false>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
                                                  d_tile_pf, d_ctr);
     build_cut_tables(sm, cs, tc.nbytes, s_dtmp);
+    const CutLimits cl = cut_limits(dp);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
-        CutCount r = count_by_masks<HIST>(dp, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0, s_hist, ht, fast);
+        CutCount r = count_by_masks<HIST>(dp, cl, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0, s_hist, ht, fast);
         if (!r.exact) {
             const WalkOut w = walk_candidate<false, false, false, HIST>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr,
                                                                         s_hist);
@@ -2307,6 +2317,43 @@ hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, co
 // (DBIndexer.java:265-308: m0, then one fp64 add per residue, left to right;
 // -ffp-contract=off), so the record is bit-identical to the sender's.
 constexpr uint32_t EXPAND_THREADS = 256;
+__device__ __forceinline__ Rec expand_loc(uint64_t q1, const uint32_t* __restrict__ w32, uint32_t mis,
+                                          const uint32_t* __restrict__ poff, const double* smass, double m0,
+                                          uint32_t w) {
+    const uint32_t len = q1_len(q1, w);
+    // residues 16 at a time: the 5 dwords covering them loaded together
+    // (clamped to the peptide's last dword) and realigned, as seq_equal_at
+    const uint64_t ga = (uint64_t)poff[q1_pid(q1, w)] + q1_off(q1, w) + mis;
+    const uint64_t last = (ga + len - 1) >> 2;
+    double m = m0;
+    uint32_t head = 0, tail = 0;
+    for (uint32_t k0 = 0; k0 < len; k0 += 16) {
+        const uint64_t ia = (ga + k0) >> 2;
+        uint32_t wd[5];
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) wd[j] = w32[min(ia + j, last)];
+        const uint32_t sa = (uint32_t)((ga + k0) & 3u);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t x = __builtin_amdgcn_alignbyte(wd[j + 1], wd[j], sa);
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b) {
+                if (k0 + 4 * j + b < len) {  // sequential, left to right (DBIndexer.java:306-308)
+                    const uint32_t c = (x >> (8 * b)) & 0xFFu;
+                    m = m + smass[c];
+                    if (k0 == 0 && j == 0) head |= c << (8 * b);
+                    tail = (tail << 8) | c;
+                }
+            }
+        }
+    }
+    const uint32_t tag = peptide_tag(head, tail, len);
+    Rec r;
+    r.q0 = rec_q0(m, tag);
+    r.q1 = ((uint64_t)(tag & 0xFFu) << 56) | (q1 & 0x00FFFFFFFFFFFFFFull);  // pid | off | len as sent
+    return r;
+}
+
 __global__ void __launch_bounds__(EXPAND_THREADS)
 k_expand_locs(const unsigned long long* __restrict__ locs, uint64_t n, const uint8_t* __restrict__ res,
               const uint32_t* __restrict__ poff, const double* __restrict__ mass_tab, double m0, uint32_t w,
@@ -2318,41 +2365,8 @@ k_expand_locs(const unsigned long long* __restrict__ locs, uint64_t n, const uin
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(res) & 3u);
     const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(res - mis);
     for (uint64_t i = (uint64_t)blockIdx.x * EXPAND_THREADS + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * EXPAND_THREADS) {
-        const uint64_t q1 = locs[i];
-        const uint32_t len = q1_len(q1, w);
-        // residues 16 at a time: the 5 dwords covering them loaded together
-        // (clamped to the peptide's last dword) and realigned, as seq_equal_at
-        const uint64_t ga = (uint64_t)poff[q1_pid(q1, w)] + q1_off(q1, w) + mis;
-        const uint64_t last = (ga + len - 1) >> 2;
-        double m = m0;
-        uint32_t head = 0, tail = 0;
-        for (uint32_t k0 = 0; k0 < len; k0 += 16) {
-            const uint64_t ia = (ga + k0) >> 2;
-            uint32_t wd[5];
-#pragma unroll
-            for (uint32_t j = 0; j < 5; ++j) wd[j] = w32[min(ia + j, last)];
-            const uint32_t sa = (uint32_t)((ga + k0) & 3u);
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t x = __builtin_amdgcn_alignbyte(wd[j + 1], wd[j], sa);
-#pragma unroll
-                for (uint32_t b = 0; b < 4; ++b) {
-                    if (k0 + 4 * j + b < len) {  // sequential, left to right (DBIndexer.java:306-308)
-                        const uint32_t c = (x >> (8 * b)) & 0xFFu;
-                        m = m + smass[c];
-                        if (k0 == 0 && j == 0) head |= c << (8 * b);
-                        tail = (tail << 8) | c;
-                    }
-                }
-            }
-        }
-        const uint32_t tag = peptide_tag(head, tail, len);
-        Rec r;
-        r.q0 = rec_q0(m, tag);
-        r.q1 = ((uint64_t)(tag & 0xFFu) << 56) | (q1 & 0x00FFFFFFFFFFFFFFull);  // pid | off | len as sent
-        out[i] = r;
-    }
+         i += (uint64_t)gridDim.x * EXPAND_THREADS)
+        out[i] = expand_loc(locs[i], w32, mis, poff, smass, m0, w);
 }
 
 hipError_t launch_expand_locs(const uint64_t* d_locs, uint64_t n, const uint8_t* d_res, const uint32_t* d_poff,
@@ -2361,6 +2375,48 @@ hipError_t launch_expand_locs(const uint64_t* d_locs, uint64_t n, const uint8_t*
     const uint32_t g = (uint32_t)std::min<uint64_t>((n + EXPAND_THREADS - 1) / EXPAND_THREADS, 256u * 16u);
     DBI_LAUNCH(k_expand_locs, dim3(g), dim3(EXPAND_THREADS), 0, s, (const unsigned long long*)d_locs, n, d_res,
                d_poff, d_mass_tab, m0, w, d_out);
+    return hipGetLastError();
+}
+
+// The same expansion with the owner merge's first radix pass histogram
+// counted on the way: one block per radix chunk (RADIX_CHUNK records, the
+// chunk of the scatter that follows: radix_chunk()), digit counts in LDS,
+// hist[d * G + chunk] written by the block -- the tail skips that pass's
+// histogram kernel, a read of every record's mass.
+__global__ void __launch_bounds__(RADIX_THREADS)
+k_expand_locs_hist(const unsigned long long* __restrict__ locs, uint32_t n, const uint8_t* __restrict__ res,
+                   const uint32_t* __restrict__ poff, const double* __restrict__ mass_tab, double m0, uint32_t w,
+                   Rec* __restrict__ out, BinMap bm, int bits, uint32_t* __restrict__ hist) {
+    __shared__ double smass[256];
+    __shared__ uint32_t cnt[RADIX_D];
+    const uint32_t D = 1u << bits;
+    for (uint32_t c = threadIdx.x; c < 256; c += RADIX_THREADS) smass[c] = mass_tab[c];
+    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) cnt[d] = 0;
+    __syncthreads();
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(res) & 3u);
+    const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(res - mis);
+    const uint32_t cb = radix_chunk();
+#pragma unroll 1
+    for (uint32_t k = 0; k < RADIX_ITEMS; ++k) {
+        const uint32_t i = cb * RADIX_CHUNK + k * RADIX_THREADS + threadIdx.x;
+        if (i < n) {
+            const Rec r = expand_loc(locs[i], w32, mis, poff, smass, m0, w);
+            out[i] = r;
+            atomicAdd(&cnt[bin_of(q0_mass(r.q0), bm) & (D - 1u)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < D; d += RADIX_THREADS) hist[(size_t)d * gridDim.x + cb] = cnt[d];
+}
+
+hipError_t launch_expand_locs_hist(const uint64_t* d_locs, uint32_t n, const uint8_t* d_res, const uint32_t* d_poff,
+                                   const double* d_mass_tab, double m0, uint32_t w, Rec* d_out, const BinMap& bm,
+                                   int bits, uint32_t* d_hist, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (bits < 1 || bits > RADIX_BITS) return hipErrorInvalidValue;
+    const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
+    DBI_LAUNCH(k_expand_locs_hist, dim3(g), dim3(RADIX_THREADS), 0, s, (const unsigned long long*)d_locs, n, d_res,
+               d_poff, d_mass_tab, m0, w, d_out, bm, bits, d_hist);
     return hipGetLastError();
 }
 

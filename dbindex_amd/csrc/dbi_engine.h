@@ -58,6 +58,12 @@ struct DevBuf {
     size_t bytes() const { return cap * sizeof(T); }
 };
 
+// Owner-splitter samples of a sharded build, sorted by mass key (dbi_shard.hip)
+struct SampleKeys {
+    std::vector<int32_t> key;
+    std::vector<double> w;  // records per sample of the shard it came from
+};
+
 // State of a sharded build on this handle (dbi_shard_* phases, dbi_shard.hip).
 struct ShardState {
     int phase = 0;  // 0 none, 1 digested, 2 partitioned, 3 exchanged, 4 merged, 5 replicated
@@ -76,6 +82,7 @@ struct ShardState {
     uint64_t n_recv = 0;
     double ms_digest = 0, ms_partition = 0, ms_exchange = 0, ms_merge = 0;
     double ms_merge_gpu = 0;                // device time of the owner merge's kernels
+    int split_sampled = 0, split_rounds = 0;  // dbi_build_sharded: the owner split's provenance
     dbi_shard_stats global{};               // filled by dbi_build_sharded (RCCL sums)
     uint64_t u_base = 0;                    // first global id of this owner's unique table
     bool u_base_known = false;
@@ -189,6 +196,23 @@ struct dbi_handle {
         int32_t split[DBI_COST_BANDS - 1] = {};  // fixed key bands over [minMH, maxMH]
         double cost[DBI_COST_BANDS] = {};        // smoothed merge time per record
     } shard_prof;
+    // what a warm dbi_build_sharded reuses: the sorted sample keys of the last
+    // sampled build (every rank's: all-gathered) and the split the previous
+    // build left for the next one (its cost profile applied); valid for a
+    // communicator of n ranks.  The count matrix carries a hash of each rank's
+    // split: ranks holding different ones sample again.
+    struct {
+        bool valid = false;
+        int n = 0;
+        int32_t split[DBI_MAX_SHARDS - 1] = {};
+        dbi::SampleKeys keys;
+        uint64_t sampled_kept = 0;  // whole-index records of the sampled build
+        // the last build's owner split, this owner's merge device time and records
+        // received: the next build's totals row carries them (the cost profile)
+        int32_t prev_split[DBI_MAX_SHARDS - 1] = {};
+        double prev_merge_ms = 0;
+        uint64_t prev_recv = 0;
+    } shard_warm;
     hipEvent_t ev_merge[2] = {nullptr, nullptr};  // owner merge device time
     DevBuf<uint64_t> xsend, xrecv;      // sharded build: 8-B location words to / from the owners
     DevBuf<double> samp;                // sharded build: mass samples (splitters)
@@ -321,6 +345,8 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
                const unsigned long long* d_n_in = nullptr, const unsigned long long* d_n = nullptr, uint64_t n_est = 0, bool est = false);
 int ensure_qdir(dbi_handle* h, hipStream_t s);  // query directory of the current index
 void drop_graph(dbi_handle* h);                 // the captured warm build graph, if any
+uint32_t choose_nbins(uint64_t n, int max_bits);  // fine mass bins of a tail over n records
+int radix_plan(uint32_t nbins, bool sparse, int* width);  // LSD digit widths; returns the passes
 int finish_build(dbi_handle* h);
 
 }  // namespace dbi

@@ -201,7 +201,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
         const uint32_t nin = sp ? n_in32 : n32;
         const double hbytes = 8.0 * (double)radix_blocks(nin) * (double)(1u << bits);  // hist write + scan
         const unsigned long long* dn = sp ? d_n_in : d_n;
-        if (ps == 0 && sp && h->h1_on) {  // counted by the digest (warm_body)
+        if (ps == 0 && h->h1_on) {  // counted by the digest (warm_body) or the owner's expansion (dbi_shard_merge)
         } else if (ps == 0) {            // the 8-B mass of every record
             STAGE(h, "radix_hist", by(0, 8, 0, 0, 0),
                   launch_radix_hist(src, nin, bm, shift, bits, sp, h->hist.p, s, dn));

@@ -314,6 +314,11 @@ hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, co
 // owner side: 8-B location words -> 16-B records (mass and tag from the residues)
 hipError_t launch_expand_locs(const uint64_t* d_locs, uint64_t n, const uint8_t* d_res, const uint32_t* d_poff,
                               const double* d_mass_tab, double m0, uint32_t w, Rec* d_out, hipStream_t s);
+// the same, counting the first radix pass's histogram (digit bin_of(m, bm) &
+// (2^bits - 1), hist[d * G + radix chunk], G = radix_blocks(n)) of the tail
+hipError_t launch_expand_locs_hist(const uint64_t* d_locs, uint32_t n, const uint8_t* d_res, const uint32_t* d_poff,
+                                   const double* d_mass_tab, double m0, uint32_t w, Rec* d_out, const BinMap& bm,
+                                   int bits, uint32_t* d_hist, hipStream_t s);
 // stable partition of query routing pairs (q0 = owner, q1 = query index) by owner
 hipError_t launch_pair_hist(const Rec* d_in, uint32_t n, uint32_t nshards, uint32_t* d_hist, hipStream_t s);
 hipError_t launch_pair_scatter(const Rec* d_in, Rec* d_out, uint32_t n, uint32_t nshards, const uint32_t* d_hist,

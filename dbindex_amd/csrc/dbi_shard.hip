@@ -31,15 +31,48 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
+#include <atomic>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "dbi_engine.h"
 
 using namespace dbi;
 
+namespace dbi {
+// Host-staged transport (dbi_comm_init_host, TESTS ONLY): the same collectives
+// through POSIX shared memory between the processes of one node -- device ->
+// host -> shm slot or mailbox -> host -> device, a barrier between -- so the
+// N-rank driver (warm splits, the count-matrix rounds, failure agreement, the
+// exchange, totals, replica, routed queries) runs with N processes on ONE GPU,
+// where RCCL refuses two ranks on one device.  Every product run is RCCL.
+struct ShmHeader {
+    std::atomic<uint32_t> ready, count, gen;
+    uint32_t nranks;
+    uint64_t slot;  // bytes per rank slot and per (src, dst) mailbox
+};
+struct HostXport {
+    int fd = -1;
+    uint8_t* base = nullptr;
+    size_t bytes = 0;
+    uint64_t slot = 0;
+    std::string name;
+    ShmHeader* hdr() const { return reinterpret_cast<ShmHeader*>(base); }
+    uint8_t* rank_slot(int r) const { return base + 4096 + (size_t)r * slot; }
+    uint8_t* mailbox(int src, int dst, int n) const {
+        return base + 4096 + (size_t)n * slot + ((size_t)src * n + dst) * slot;
+    }
+};
+}  // namespace dbi
+
 struct dbi_comm {
     ncclComm_t comm = nullptr;
+    dbi::HostXport* host = nullptr;        // the test transport instead of RCCL
     int nranks = 1;
     int rank = 0;
     int device = 0;
@@ -49,11 +82,14 @@ struct dbi_comm {
     // the sharded build's small collectives (sample blocks, count matrix,
     // totals) stage through these, allocated with the communicator: a rank
     // never fails an allocation between two collectives of a build
-    double* d_samp = nullptr;              // nranks x (DBI_SHARD_SAMPLES + 2)
+    double* d_samp = nullptr;              // nranks x (DBI_SHARD_SAMPLES + 3)
     unsigned long long* d_cnt = nullptr;   // nranks x cnt_row
-    int cnt_row = 0;                       // max(nranks + 2, 7)
+    int cnt_row = 0;                       // max(nranks + 3, TOTALS_W)
 };
 constexpr uint32_t COMM_RED_MAX = 4096;
+// totals row of a sharded build: n_total, n_dropped, n_recv, n_unique, n_keys,
+// status, the previous build's merge ns and records received, merge flags
+constexpr int TOTALS_W = 9;
 
 namespace dbi {
 namespace {
@@ -73,6 +109,131 @@ int nccl_fail(ncclResult_t r, const char* what) {
         ncclResult_t _r = (expr);                             \
         if (_r != ncclSuccess) return nccl_fail(_r, #expr);   \
     } while (0)
+
+// ---- collectives: RCCL, or the host-staged test transport ----
+int shm_barrier(dbi_comm* c) {
+    ShmHeader* h = c->host->hdr();
+    const uint32_t g = h->gen.load(std::memory_order_acquire);
+    if (h->count.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)c->nranks) {
+        h->count.store(0, std::memory_order_relaxed);
+        h->gen.fetch_add(1, std::memory_order_release);
+        return 0;
+    }
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+    while (h->gen.load(std::memory_order_acquire) == g) {
+        if (std::chrono::steady_clock::now() > t_end)
+            return set_error(DBI_E_RCCL, "host transport: barrier timed out (a peer process is gone)");
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    return 0;
+}
+
+int shm_check(const dbi_comm* c, uint64_t bytes) {
+    if (bytes > c->host->slot)
+        return set_error(DBI_E_INVALID, "host transport: a message of " + std::to_string(bytes) +
+                                            " B exceeds its mailbox (" + std::to_string(c->host->slot) + " B)");
+    return 0;
+}
+
+// every rank's `bytes` from send -> recv (rank order), device buffers
+int c_allgather(dbi_comm* c, const void* send, void* recv, uint64_t bytes, hipStream_t s) {
+    if (!c->host) {
+        DBI_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, c->comm, s));
+        return 0;
+    }
+    int rc;
+    if ((rc = shm_check(c, bytes))) return rc;
+    DBI_HIP(hipStreamSynchronize(s));
+    DBI_HIP(hipMemcpy(c->host->rank_slot(c->rank), send, bytes, hipMemcpyDeviceToHost));
+    if ((rc = shm_barrier(c))) return rc;
+    std::vector<uint8_t> all((size_t)bytes * c->nranks);
+    for (int r = 0; r < c->nranks; ++r) std::memcpy(all.data() + (size_t)r * bytes, c->host->rank_slot(r), bytes);
+    if ((rc = shm_barrier(c))) return rc;  // the slots are free again
+    DBI_HIP(hipMemcpy(recv, all.data(), all.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// element-wise reduction over the ranks (u64 sum / max, f64 sum / max / min)
+int c_allreduce(dbi_comm* c, const void* send, void* recv, uint64_t count, ncclDataType_t t, ncclRedOp_t op,
+                hipStream_t s) {
+    if (!c->host) {
+        DBI_NCCL(ncclAllReduce(send, recv, count, t, op, c->comm, s));
+        return 0;
+    }
+    if (t != ncclUint64 && t != ncclFloat64) return set_error(DBI_E_INVALID, "host transport: u64 / f64 only");
+    const uint64_t bytes = 8 * count;
+    std::vector<uint8_t> all((size_t)bytes * c->nranks);
+    int rc;
+    if ((rc = shm_check(c, bytes))) return rc;
+    DBI_HIP(hipStreamSynchronize(s));
+    DBI_HIP(hipMemcpy(c->host->rank_slot(c->rank), send, bytes, hipMemcpyDeviceToHost));
+    if ((rc = shm_barrier(c))) return rc;
+    for (int r = 0; r < c->nranks; ++r) std::memcpy(all.data() + (size_t)r * bytes, c->host->rank_slot(r), bytes);
+    if ((rc = shm_barrier(c))) return rc;
+    std::vector<uint8_t> out(bytes);
+    for (uint64_t i = 0; i < count; ++i) {
+        if (t == ncclUint64) {
+            uint64_t v;
+            std::memcpy(&v, all.data() + 8 * i, 8);
+            for (int r = 1; r < c->nranks; ++r) {
+                uint64_t x;
+                std::memcpy(&x, all.data() + (size_t)r * bytes + 8 * i, 8);
+                v = op == ncclSum ? v + x : op == ncclMax ? std::max(v, x) : std::min(v, x);
+            }
+            std::memcpy(out.data() + 8 * i, &v, 8);
+        } else {
+            double v;
+            std::memcpy(&v, all.data() + 8 * i, 8);
+            for (int r = 1; r < c->nranks; ++r) {
+                double x;
+                std::memcpy(&x, all.data() + (size_t)r * bytes + 8 * i, 8);
+                v = op == ncclSum ? v + x : op == ncclMax ? std::max(v, x) : std::min(v, x);
+            }
+            std::memcpy(out.data() + 8 * i, &v, 8);
+        }
+    }
+    DBI_HIP(hipMemcpy(recv, out.data(), bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// point-to-point transfers of one group: to peer p from the rank's device
+// buffers; matched by order per peer pair, as RCCL's grouped send / receive
+struct Xfer {
+    int peer;
+    void* ptr;
+    uint64_t bytes;
+};
+
+int c_group(dbi_comm* c, const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
+    if (!c->host) {
+        DBI_NCCL(ncclGroupStart());
+        for (const Xfer& x : sends)
+            if (x.bytes) DBI_NCCL(ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, s));
+        for (const Xfer& x : recvs)
+            if (x.bytes) DBI_NCCL(ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, s));
+        DBI_NCCL(ncclGroupEnd());
+        return 0;
+    }
+    const int n = c->nranks, me = c->rank;
+    int rc;
+    DBI_HIP(hipStreamSynchronize(s));
+    std::vector<uint64_t> cur(n, 0);
+    for (const Xfer& x : sends) {
+        if (!x.bytes) continue;
+        if ((rc = shm_check(c, cur[x.peer] + x.bytes))) return rc;
+        DBI_HIP(hipMemcpy(c->host->mailbox(me, x.peer, n) + cur[x.peer], x.ptr, x.bytes, hipMemcpyDeviceToHost));
+        cur[x.peer] += x.bytes;
+    }
+    if ((rc = shm_barrier(c))) return rc;
+    std::fill(cur.begin(), cur.end(), 0);
+    for (const Xfer& x : recvs) {
+        if (!x.bytes) continue;
+        if ((rc = shm_check(c, cur[x.peer] + x.bytes))) return rc;
+        DBI_HIP(hipMemcpy(x.ptr, c->host->mailbox(x.peer, me, n) + cur[x.peer], x.bytes, hipMemcpyHostToDevice));
+        cur[x.peer] += x.bytes;
+    }
+    return shm_barrier(c);  // the mailboxes are free again
+}
 
 int need_phase(const dbi_handle* h, int phase, const char* what) {
     if (h->shard.phase != phase)
@@ -132,14 +293,13 @@ int nccl_alltoallv(dbi_comm* c, const T* send, const std::vector<uint64_t>& soff
     const int me = c->rank;
     if (scnt[me])
         DBI_HIP(hipMemcpyAsync(recv + roff[me], send + soff[me], scnt[me] * sizeof(T), hipMemcpyDeviceToDevice, s));
-    DBI_NCCL(ncclGroupStart());
+    std::vector<Xfer> sends, recvs;
     for (int p = 0; p < c->nranks; ++p) {
         if (p == me) continue;
-        if (scnt[p]) DBI_NCCL(ncclSend(send + soff[p], scnt[p] * sizeof(T), ncclUint8, p, c->comm, s));
-        if (rcnt[p]) DBI_NCCL(ncclRecv(recv + roff[p], rcnt[p] * sizeof(T), ncclUint8, p, c->comm, s));
+        sends.push_back(Xfer{p, (void*)(send + soff[p]), scnt[p] * sizeof(T)});
+        recvs.push_back(Xfer{p, (void*)(recv + roff[p]), rcnt[p] * sizeof(T)});
     }
-    DBI_NCCL(ncclGroupEnd());
-    return 0;
+    return c_group(c, sends, recvs, s);
 }
 
 // Local failures must not strand the other ranks inside the next collective:
@@ -165,7 +325,8 @@ int agree(dbi_comm* c, int rc, hipStream_t s, bool* any) {
     const unsigned long long mine = rc ? 1ull : 0ull;
     unsigned long long all = 0;
     DBI_HIP(hipMemcpyAsync(c->d_flag, &mine, sizeof(mine), hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllReduce(c->d_flag, c->d_flag + 1, 1, ncclUint64, ncclMax, c->comm, s));
+    int rc_c;
+    if ((rc_c = c_allreduce(c, c->d_flag, c->d_flag + 1, 1, ncclUint64, ncclMax, s))) return rc_c;
     DBI_HIP(hipMemcpyAsync(&all, c->d_flag + 1, sizeof(all), hipMemcpyDeviceToHost, s));
     DBI_HIP(hipStreamSynchronize(s));
     *any = all != 0;
@@ -183,7 +344,8 @@ int nccl_count_matrix(dbi_handle* h, dbi_comm* c, const std::vector<uint64_t>& m
     full[(size_t)me * w + n] = status ? 1u : 0u;
     DBI_HIP(hipMemcpyAsync(c->d_cnt + (size_t)me * w, full.data() + (size_t)me * w, sizeof(uint64_t) * w,
                            hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllGather(c->d_cnt + (size_t)me * w, c->d_cnt, w, ncclUint64, c->comm, s));
+    int rc;
+    if ((rc = c_allgather(c, c->d_cnt + (size_t)me * w, c->d_cnt, 8ull * w, s))) return rc;
     DBI_HIP(hipMemcpyAsync(full.data(), c->d_cnt, sizeof(uint64_t) * n * w, hipMemcpyDeviceToHost, s));
     DBI_HIP(hipStreamSynchronize(s));
     all.assign((size_t)n * n, 0);
@@ -338,6 +500,68 @@ void replica_install(dbi_handle* h, const SliceSizes& z, uint64_t g_total, uint6
     h->shard.phase = 5;
 }
 
+// Sample keys of every shard, sorted (the sort happens once per sampled
+// build): key (int)(m * factor) of every valid sample and its weight (records
+// per valid sample of its shard)
+void sample_keys(const double* samples, int nshards, int32_t factor, SampleKeys& out) {
+    std::vector<std::pair<int32_t, double>> ks;
+    for (int r = 0; r < nshards; ++r) {
+        const double* b = samples + (size_t)r * (NS + 1);
+        const double w = b[NS];
+        if (!(w > 0.0)) continue;
+        for (uint32_t i = 0; i < NS; ++i)
+            if (b[i] == b[i]) ks.emplace_back(java_d2i(b[i] * (double)factor), w);
+    }
+    std::sort(ks.begin(), ks.end());
+    out.key.resize(ks.size());
+    out.w.resize(ks.size());
+    for (size_t i = 0; i < ks.size(); ++i) {
+        out.key[i] = ks[i].first;
+        out.w[i] = ks[i].second;
+    }
+}
+
+// split[j-1] = the first key whose preceding weight reaches j/n of the total;
+// a key's weight = its sample weight x the cost per record of its band (band
+// b: the band_split entries <= key; nbands = 0: 1).  Linear in the samples.
+void split_from_keys(const SampleKeys& sk, int nshards, int nbands, const int32_t* band_split,
+                     const double* band_cost, int32_t* split) {
+    const size_t m = sk.key.size();
+    std::vector<double> wt(m);
+    int b = 0;
+    double total = 0.0;
+    for (size_t i = 0; i < m; ++i) {
+        double c = 1.0;
+        if (nbands > 0) {
+            while (b < nbands - 1 && band_split[b] <= sk.key[i]) ++b;  // keys ascend: the band only moves up
+            c = band_cost[b];
+        }
+        wt[i] = sk.w[i] * c;
+        total += wt[i];
+    }
+    size_t i = 0;
+    double cum = 0.0;
+    for (int j = 1; j < nshards; ++j) {
+        const double target = total * (double)j / (double)nshards;
+        int32_t sp = INT32_MAX;
+        for (; i < m; ++i) {
+            if (cum >= target && (i == 0 || sk.key[i] != sk.key[i - 1])) {
+                sp = sk.key[i];
+                break;
+            }
+            cum += wt[i];
+        }
+        split[j - 1] = sp;
+    }
+}
+
+// FNV-1a 64 over bytes
+uint64_t fnv64(const void* p, size_t n, uint64_t h = 0xcbf29ce484222325ull) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+
 int query_need(const dbi_handle* h) {
     if (h->shard.phase != 4 || !h->built || !h->shard.u_base_known)
         return set_error(DBI_E_STATE, "sharded queries need a finished sharded build (dbi_build_sharded, or the "
@@ -448,38 +672,9 @@ int dbi_shard_splitters_cost(const double* samples, int nshards, int32_t factor,
         for (int r = 0; r + 2 < nbands; ++r)
             if (band_split[r] > band_split[r + 1]) return set_error(DBI_E_INVALID, "band splits must ascend");
     }
-    std::vector<std::pair<int32_t, double>> ks;
-    for (int r = 0; r < nshards; ++r) {
-        const double* b = samples + (size_t)r * (NS + 1);
-        const double w = b[NS];
-        if (!(w > 0.0)) continue;
-        for (uint32_t i = 0; i < NS; ++i) {
-            if (b[i] != b[i]) continue;
-            const int32_t k = java_d2i(b[i] * (double)factor);
-            double c = 1.0;
-            if (band_cost)  // band of k: the number of band boundaries <= k
-                c = band_cost[std::upper_bound(band_split, band_split + (nbands - 1), k) - band_split];
-            ks.emplace_back(k, w * c);
-        }
-    }
-    std::sort(ks.begin(), ks.end());
-    double total = 0.0;
-    for (const auto& k : ks) total += k.second;
-    // split[j-1] = first key whose preceding weight reaches j/n of the total
-    size_t i = 0;
-    double cum = 0.0;
-    for (int j = 1; j < nshards; ++j) {
-        const double target = total * (double)j / (double)nshards;
-        int32_t sp = INT32_MAX;
-        for (; i < ks.size(); ++i) {
-            if (cum >= target && (i == 0 || ks[i].first != ks[i - 1].first)) {
-                sp = ks[i].first;
-                break;
-            }
-            cum += ks[i].second;
-        }
-        split[j - 1] = sp;
-    }
+    SampleKeys sk;
+    sample_keys(samples, nshards, factor, sk);
+    split_from_keys(sk, nshards, band_cost ? nbands : 0, band_split, band_cost, split);
     return 0;
 }
 
@@ -648,60 +843,123 @@ int dbi_shard_exchange_local(dbi_handle* const* hs, int nshards) {
     return 0;
 }
 
+}  // extern "C"
+
+namespace dbi {
+namespace {
+// The owner merge in three parts, so that the RCCL driver can fold its
+// counters into the totals all-gather (one host sync for both):
+// merge_begin -- the handle turns into the owner of its key range of the
+// whole proteome, every buffer allocated (the merge's device time then holds
+// no host allocation); merge_enqueue -- its kernels, no host sync;
+// merge_done -- after the counters are on the host: stats, device time.
+struct MergeRange {
+    double lo = 0, hi = 0;
+    bool first = false;  // the handle's first build (code objects load): not timed
+};
+
+int merge_begin(dbi_handle* h, MergeRange& mr) {
+    ShardState& sh = h->shard;
+    DBI_HIP(hipSetDevice(h->device));
+    h->d_res = sh.d_res_global;
+    h->d_poff = h->poff_g.p;
+    h->n_res = sh.n_res_global;
+    h->n_prot = sh.n_prot_global;
+    h->n_total_extra = 0;
+    int rc;
+    if ((rc = h->recA.ensure(std::max<uint64_t>(sh.n_recv, 1)))) return rc;
+    int32_t klo, khi;
+    key_range(sh.split, sh.nshards, sh.rank, &klo, &khi);
+    const double f = (double)h->params.mass_group_factor;
+    mr.lo = klo == INT32_MIN ? h->params.min_mh : std::max(h->params.min_mh, (double)klo / f);
+    const double hi = khi == INT32_MAX ? h->params.max_mh : std::min(h->params.max_mh, (double)khi / f);
+    mr.hi = std::max(hi, mr.lo);
+    for (int e = 0; e < 2; ++e)
+        if (!h->ev_merge[e]) DBI_HIP(hipEventCreate(&h->ev_merge[e]));
+    if ((rc = tail_buffers(h, sh.n_recv, sh.n_recv, false))) return rc;
+    mr.first = h->build_serial == 0;
+    return 0;
+}
+
+// attempt 0: the chunk-list grids (and whether to run the giant pass) from
+// this owner's previous merge; attempt 1 (lists outgrew them, ERR_GRID): full
+// grids, from the received words again
+int merge_enqueue(dbi_handle* h, const MergeRange& mr, int attempt) {
+    ShardState& sh = h->shard;
+    hipStream_t s = h->stream;
+    if (attempt > 0) h->giants_seen = true;
+    DBI_HIP(hipEventRecord(h->ev_merge[0], s));
+    // counters back to zero (the layout word max_plen stays), n_kept = records received
+    DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
+    hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(64), 0, s, &h->ctr.p->n_kept, (unsigned long long)sh.n_recv);
+    DBI_HIP(hipGetLastError());
+    // the received location words -> records (mass + tag from the residues);
+    // recA is free (the partition read it before the exchange was enqueued).
+    // The expansion also counts the tail's first radix histogram (the same
+    // bins build_tail plans from n_recv and [lo, hi]): one kernel fewer
+    const uint32_t nbins = choose_nbins(sh.n_recv, h->bin_bits_max);
+    int width[8] = {};
+    const int passes = radix_plan(nbins, false, width);
+    h->h1_on = passes >= 1 && width[0] >= 1 && sh.n_recv > 0;
+    if (h->h1_on)
+        STAGE(h, "owner_expand", by(0, 0, 0, 0, 0),
+              launch_expand_locs_hist(h->xrecv.p, (uint32_t)sh.n_recv, h->d_res, h->d_poff, h->mass_tab.p, h->dp.m0,
+                                      sh.width, h->recA.p, make_binmap(mr.lo, mr.hi, nbins), width[0], h->hist.p, s));
+    else
+        STAGE(h, "owner_expand", by(0, 0, 0, 0, 0),
+              launch_expand_locs(h->xrecv.p, sh.n_recv, h->d_res, h->d_poff, h->mass_tab.p, h->dp.m0, sh.width,
+                                 h->recA.p, s));
+    h->stages[h->nstage - 1].c0 = 24.0 * (double)sh.n_recv;  // 8 B in, 16 B out (+ the residues)
+    const int rc = build_tail(h, sh.n_recv, mr.lo, mr.hi, sh.n_recv, false, nullptr, nullptr, 0, attempt == 0);
+    h->h1_on = false;
+    if (rc) return rc;
+    DBI_HIP(hipEventRecord(h->ev_merge[1], s));
+    return 0;
+}
+
+// h->hc holds the merge's counters (read_counters, or the totals round)
+int merge_done(dbi_handle* h, const MergeRange& mr) {
+    int rc;
+    if ((rc = finish_build(h))) return rc;
+    float mg = 0.f;
+    h->shard.ms_merge_gpu =
+        !mr.first && hipEventElapsedTime(&mg, h->ev_merge[0], h->ev_merge[1]) == hipSuccess ? (double)mg : 0.0;
+    return 0;
+}
+
+// the totals row's device columns: unique peptides, mass keys, and the
+// merge's flags (bit 0: chunk lists outgrew their grids -- merge again;
+// bits 8+: device error bits)
+__global__ void k_totals_row(const Counters* __restrict__ ctr, unsigned long long* __restrict__ row, int skip_mid,
+                             int skip_big) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    unsigned long long keys = ctr->n_keys;
+    for (int i = 0; i < 8; ++i) keys += ctr->n_keys_shard[i];
+    row[3] = ctr->n_unique;
+    row[4] = keys;
+    const bool redo = (ctr->err & ERR_GRID) || (skip_mid && ctr->n_mid) || (skip_big && ctr->n_big);
+    row[7] = (redo ? 1ull : 0ull) | ((unsigned long long)(ctr->err & ~ERR_GRID) << 8);
+}
+}  // namespace
+}  // namespace dbi
+
+extern "C" {
+
 int dbi_shard_merge(dbi_handle* h) {
     if (!h) return set_error(DBI_E_INVALID, "NULL handle");
     int rc;
     if ((rc = need_phase(h, 3, "dbi_shard_merge"))) return rc;
     ShardState& sh = h->shard;
     const double t0 = now_ms();
-    DBI_HIP(hipSetDevice(h->device));
-    hipStream_t s = h->stream;
-    // from here on the handle describes the owner's slice of the whole proteome
-    h->d_res = sh.d_res_global;
-    h->d_poff = h->poff_g.p;
-    h->n_res = sh.n_res_global;
-    h->n_prot = sh.n_prot_global;
-    h->n_total_extra = 0;
-    if ((rc = h->recA.ensure(std::max<uint64_t>(sh.n_recv, 1)))) return rc;
-    int32_t klo, khi;
-    key_range(sh.split, sh.nshards, sh.rank, &klo, &khi);
-    const double f = (double)h->params.mass_group_factor;
-    const double lo = klo == INT32_MIN ? h->params.min_mh : std::max(h->params.min_mh, (double)klo / f);
-    const double hi = khi == INT32_MAX ? h->params.max_mh : std::min(h->params.max_mh, (double)khi / f);
-    // the chunk-list grids (and whether to run the giant pass) from this
-    // owner's previous merge; lists that outgrow them (ERR_GRID) and the
-    // merge runs again from the received words, with this merge's lists
-    for (int e = 0; e < 2; ++e)
-        if (!h->ev_merge[e]) DBI_HIP(hipEventCreate(&h->ev_merge[e]));
-    // every buffer of the tail first: the merge's device time (the cost
-    // profile's measure) then has no host allocation inside it
-    if ((rc = tail_buffers(h, sh.n_recv, sh.n_recv, false))) return rc;
-    const bool first = h->build_serial == 0;  // the handle's first build also loads the code objects: not timed
+    MergeRange mr;
+    if ((rc = merge_begin(h, mr))) return rc;
     for (int attempt = 0;; ++attempt) {
         const int nstage0 = h->nstage;
-        DBI_HIP(hipEventRecord(h->ev_merge[0], s));
-        // counters back to zero (the layout word max_plen stays), n_kept = records received
-        DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
-        hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(64), 0, s, &h->ctr.p->n_kept, (unsigned long long)sh.n_recv);
-        DBI_HIP(hipGetLastError());
-        // the received location words -> records (mass + tag from the residues);
-        // recA is free (the partition read it before the exchange was enqueued)
-        STAGE(h, "owner_expand", by(0, 0, 0, 0, 0),
-              launch_expand_locs(h->xrecv.p, sh.n_recv, h->d_res, h->d_poff, h->mass_tab.p, h->dp.m0, sh.width,
-                                 h->recA.p, s));
-        h->stages[h->nstage - 1].c0 = 24.0 * (double)sh.n_recv;  // 8 B in, 16 B out (+ the residues)
-        if ((rc = build_tail(h, sh.n_recv, lo, std::max(hi, lo), sh.n_recv, false, nullptr, nullptr, 0,
-                             attempt == 0)))
-            return rc;
-        DBI_HIP(hipEventRecord(h->ev_merge[1], s));
-        if ((rc = finish_build(h))) return rc;  // (synchronises)
-        float mg = 0.f;
-        sh.ms_merge_gpu =
-            !first && hipEventElapsedTime(&mg, h->ev_merge[0], h->ev_merge[1]) == hipSuccess ? (double)mg : 0.0;
+        if ((rc = merge_enqueue(h, mr, attempt))) return rc;
+        if ((rc = merge_done(h, mr))) return rc;  // (synchronises)
         if (!h->lists_short) break;
         if (attempt > 0) return set_error(DBI_E_STATE, "internal: chunk lists outgrew full grids");
         h->nstage = nstage0;
-        h->giants_seen = true;
     }
     sh.ms_merge = now_ms() - t0;
     sh.phase = 4;
@@ -714,6 +972,8 @@ int dbi_shard_stats_get(dbi_handle* h, dbi_shard_stats* out) {
     if (sh.phase < 1) return set_error(DBI_E_STATE, "no sharded build on this handle");
     dbi_shard_stats st = sh.global;
     st.merge_gpu_ms = sh.ms_merge_gpu;
+    st.split_sampled = sh.split_sampled;
+    st.split_rounds = sh.split_rounds;
     st.rank = sh.rank;
     st.nshards = sh.nshards;
     st.p_begin = sh.p_begin;
@@ -920,16 +1180,16 @@ int dbi_shard_replicate(dbi_handle* h, dbi_comm* c) {
         const uint64_t cnt = a.occ ? z.k[me] : z.u[me], base = a.occ ? z.kb[me] : z.ub[me];
         if (cnt) DBI_HIP(hipMemcpyAsync(a.dst + base * a.esz, a.src, cnt * a.esz, hipMemcpyDeviceToDevice, s));
     }
-    DBI_NCCL(ncclGroupStart());
+    std::vector<Xfer> sends, recvs;
     for (const Arr& a : arrs)
         for (int p = 0; p < n; ++p) {
             if (p == me) continue;
             const uint64_t mc = a.occ ? z.k[me] : z.u[me];
             const uint64_t pc = a.occ ? z.k[p] : z.u[p], pb = a.occ ? z.kb[p] : z.ub[p];
-            if (mc) DBI_NCCL(ncclSend(a.src, mc * a.esz, ncclUint8, p, c->comm, s));
-            if (pc) DBI_NCCL(ncclRecv(a.dst + pb * a.esz, pc * a.esz, ncclUint8, p, c->comm, s));
+            sends.push_back(Xfer{p, a.src, mc * a.esz});
+            recvs.push_back(Xfer{p, a.dst + pb * a.esz, pc * a.esz});
         }
-    DBI_NCCL(ncclGroupEnd());
+    if ((rc = c_group(c, sends, recvs, s))) return rc;
     if ((rc = replica_rebase(h, z, s))) return rc;
     replica_install(h, z, sh.global.g_total, sh.global.g_dropped, sh.global.g_keys);
     return 0;
@@ -946,6 +1206,85 @@ int dbi_comm_unique_id(uint8_t* id128) {
     return 0;
 }
 
+namespace {
+// the communicator's device staging (status word, reduction buffer, sample
+// blocks, count matrix / totals rows) and its stream
+int comm_staging(dbi_comm* c) {
+    if (hipMalloc((void**)&c->d_flag, 2 * sizeof(unsigned long long)) != hipSuccess)
+        return set_error(DBI_E_OOM, "hipMalloc (communicator status word)");
+    c->cnt_row = std::max(c->nranks + 3, TOTALS_W);  // count matrix row | the totals row
+    if (hipMalloc((void**)&c->d_red, COMM_RED_MAX * sizeof(double)) != hipSuccess ||
+        hipMalloc((void**)&c->d_samp, sizeof(double) * (size_t)c->nranks * (NS + 3)) != hipSuccess ||
+        hipMalloc((void**)&c->d_cnt, sizeof(unsigned long long) * (size_t)c->nranks * c->cnt_row) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return set_error(DBI_E_HIP, "communicator stream / staging buffer");
+    return 0;
+}
+}  // namespace
+
+int dbi_comm_init_host(const char* name, int nranks, int rank, int device, uint64_t slot_bytes, dbi_comm** out) {
+    if (!name || !out || name[0] != '/') return set_error(DBI_E_INVALID, "host transport: a '/name' is needed");
+    *out = nullptr;
+    if (nranks < 1 || nranks > MAX_SHARDS || rank < 0 || rank >= nranks)
+        return set_error(DBI_E_INVALID, "rank / nranks out of range (1..64 ranks)");
+    if (slot_bytes < 4096) return set_error(DBI_E_INVALID, "host transport: slots of at least 4096 bytes");
+    DBI_HIP(hipSetDevice(device));
+    dbi_comm* c = new dbi_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    c->host = new HostXport();
+    HostXport& x = *c->host;
+    x.name = name;
+    x.slot = (slot_bytes + 63) & ~63ull;
+    x.bytes = 4096 + (size_t)nranks * x.slot + (size_t)nranks * nranks * x.slot;
+    auto fail = [&](int code, const std::string& msg) {
+        if (rank != 0) x.name.clear();  // only rank 0 unlinks
+        dbi_comm_destroy(c);
+        return set_error(code, "host transport: " + msg);
+    };
+    if (rank == 0) {
+        (void)shm_unlink(name);  // a segment a crashed run left behind
+        x.fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (x.fd < 0 || ftruncate(x.fd, (off_t)x.bytes) != 0) return fail(DBI_E_OOM, "shm_open / ftruncate");
+        void* m = mmap(nullptr, x.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, x.fd, 0);
+        if (m == MAP_FAILED) return fail(DBI_E_OOM, "mmap");
+        x.base = static_cast<uint8_t*>(m);
+        ShmHeader* h = new (x.base) ShmHeader();
+        h->count.store(0);
+        h->gen.store(0);
+        h->nranks = (uint32_t)nranks;
+        h->slot = x.slot;
+        h->ready.store(1, std::memory_order_release);
+    } else {
+        const auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+        for (;;) {
+            x.fd = shm_open(name, O_RDWR, 0600);
+            struct stat stt;
+            if (x.fd >= 0 && fstat(x.fd, &stt) == 0 && (size_t)stt.st_size == x.bytes) {
+                void* m = mmap(nullptr, x.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, x.fd, 0);
+                if (m != MAP_FAILED) {
+                    x.base = static_cast<uint8_t*>(m);
+                    if (x.hdr()->ready.load(std::memory_order_acquire) == 1) break;
+                    (void)munmap(x.base, x.bytes);
+                    x.base = nullptr;
+                }
+            }
+            if (x.fd >= 0) (void)close(x.fd);
+            x.fd = -1;
+            if (std::chrono::steady_clock::now() > t_end) return fail(DBI_E_RCCL, "rank 0's segment never appeared");
+            std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        }
+    }
+    int rc;
+    if ((rc = comm_staging(c)) || (rc = shm_barrier(c))) {
+        const std::string msg = dbi_last_error();
+        return fail(rc, msg);
+    }
+    *out = c;
+    return 0;
+}
+
 int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_comm** out) {
     if (!id128 || !out) return set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
@@ -958,17 +1297,10 @@ int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_co
     c->nranks = nranks;
     c->rank = rank;
     c->device = device;
-    if (hipMalloc((void**)&c->d_flag, 2 * sizeof(unsigned long long)) != hipSuccess) {
-        delete c;
-        return set_error(DBI_E_OOM, "hipMalloc (communicator status word)");
-    }
-    c->cnt_row = std::max(nranks + 2, 7);  // count matrix row | the totals row (7)
-    if (hipMalloc((void**)&c->d_red, COMM_RED_MAX * sizeof(double)) != hipSuccess ||
-        hipMalloc((void**)&c->d_samp, sizeof(double) * (size_t)nranks * (NS + 2)) != hipSuccess ||
-        hipMalloc((void**)&c->d_cnt, sizeof(unsigned long long) * (size_t)nranks * c->cnt_row) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    int rc;
+    if ((rc = comm_staging(c))) {
         dbi_comm_destroy(c);
-        return set_error(DBI_E_HIP, "communicator stream / staging buffer");
+        return rc;
     }
     const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
     if (r != ncclSuccess) {
@@ -985,6 +1317,12 @@ void dbi_comm_destroy(dbi_comm* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->host) {
+        if (c->host->base) (void)munmap(c->host->base, c->host->bytes);
+        if (c->host->fd >= 0) (void)close(c->host->fd);
+        if (c->rank == 0 && !c->host->name.empty()) (void)shm_unlink(c->host->name.c_str());
+        delete c->host;
+    }
     if (c->d_flag) (void)hipFree(c->d_flag);
     if (c->d_red) (void)hipFree(c->d_red);
     if (c->d_samp) (void)hipFree(c->d_samp);
@@ -1003,7 +1341,8 @@ int dbi_comm_allreduce_f64(dbi_comm* c, const double* in, double* out, uint32_t 
     const uint32_t m = n ? n : 1u;  // n = 0: a barrier (one value, ignored)
     if (n) DBI_HIP(hipMemcpyAsync(c->d_red, in, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
     else DBI_HIP(hipMemsetAsync(c->d_red, 0, sizeof(double), c->stream));
-    DBI_NCCL(ncclAllReduce(c->d_red, c->d_red, m, ncclFloat64, rop, c->comm, c->stream));
+    int rc;
+    if ((rc = c_allreduce(c, c->d_red, c->d_red, m, ncclFloat64, rop, c->stream))) return rc;
     if (n) DBI_HIP(hipMemcpyAsync(out, c->d_red, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     DBI_HIP(hipStreamSynchronize(c->stream));
     return 0;
@@ -1013,7 +1352,8 @@ int dbi_comm_allreduce_u64(dbi_comm* c, const uint64_t* d_in, uint64_t* d_out, u
     if (!c || (n && (!d_in || !d_out))) return set_error(DBI_E_INVALID, "NULL argument");
     DBI_HIP(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    if (n) DBI_NCCL(ncclAllReduce(d_in, d_out, n, ncclUint64, ncclSum, c->comm, s));
+    int rc;
+    if (n && (rc = c_allreduce(c, d_in, d_out, n, ncclUint64, ncclSum, s))) return rc;
     if (!stream) DBI_HIP(hipStreamSynchronize(s));
     return 0;
 }
@@ -1043,13 +1383,14 @@ int dbi_comm_allgatherv(dbi_comm* c, const void* d_send, void* d_recv, const uin
     const uint64_t my_bytes = rank_bytes[c->rank];
     if (d_send && d_send != mine && my_bytes)
         DBI_HIP(hipMemcpyAsync(mine, d_send, my_bytes, hipMemcpyDeviceToDevice, s));
-    DBI_NCCL(ncclGroupStart());
+    std::vector<Xfer> sends, recvs;
     for (int p = 0; p < c->nranks; ++p) {
         if (p == c->rank) continue;
-        if (my_bytes) DBI_NCCL(ncclSend(mine, my_bytes, ncclUint8, p, c->comm, s));
-        if (rank_bytes[p]) DBI_NCCL(ncclRecv(recv + off[p], rank_bytes[p], ncclUint8, p, c->comm, s));
+        sends.push_back(Xfer{p, mine, my_bytes});
+        recvs.push_back(Xfer{p, recv + off[p], rank_bytes[p]});
     }
-    DBI_NCCL(ncclGroupEnd());
+    int rc;
+    if ((rc = c_group(c, sends, recvs, s))) return rc;
     DBI_HIP(hipStreamSynchronize(s));
     return 0;
 }
@@ -1115,70 +1456,123 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     if (!rc_digest) rc_digest = injected_failure("digest", me);
     ShardState& sh = h->shard;
     hipStream_t s = h->stream;
+    auto& wm = h->shard_warm;
+    const auto& pf = h->shard_prof;
 
-    // samples of every shard -> the same owner splitters everywhere.  Block
-    // of rank r: NS record masses (written on the device), its record count,
-    // its status; the sample weight (records per valid sample) on the host
-    const size_t blk = NS + 2;
-    int rc_local = rc_digest;
-    double* my_blk = c->d_samp + (size_t)me * blk;
-    if (!rc_local) {
-        if ((rc = launch_sample_masses(h->recA.p, sh.n_in, NS, my_blk, s)) != hipSuccess)
-            rc_local = hip_fail((hipError_t)rc, "launch_sample_masses");
-    }
-    std::vector<double> samples((size_t)n * blk, 0.0);
-    samples[(size_t)me * blk + NS] = rc_local ? 0.0 : (double)sh.n_digest;
-    samples[(size_t)me * blk + NS + 1] = rc_local ? 1.0 : 0.0;
-    DBI_HIP(hipMemcpyAsync(my_blk + NS, &samples[(size_t)me * blk + NS], 2 * sizeof(double), hipMemcpyHostToDevice,
-                           s));
-    DBI_NCCL(ncclAllGather(my_blk, c->d_samp, blk, ncclFloat64, c->comm, s));
-    DBI_HIP(hipMemcpyAsync(samples.data(), c->d_samp, sizeof(double) * n * blk, hipMemcpyDeviceToHost, s));
-    DBI_HIP(hipStreamSynchronize(s));
-    if (rc_local) return rc_local;
-    std::vector<double> packed((size_t)n * (NS + 1));
-    for (int r = 0; r < n; ++r) {
-        const double* b = samples.data() + (size_t)r * blk;
-        if (b[NS + 1] != 0.0) return peer_failed("shard digest");
-        uint64_t valid = 0;
-        for (uint32_t i = 0; i < NS; ++i) valid += b[i] == b[i];
-        std::copy(b, b + NS, packed.begin() + (size_t)r * (NS + 1));
-        packed[(size_t)r * (NS + 1) + NS] = valid ? b[NS] / (double)valid : 0.0;  // as dbi_shard_samples
-    }
+    // Owner splitters.  A warm build reuses the split the previous build left
+    // (computed from the sorted samples of the last sampled build and the
+    // updated cost profile -- the same inputs, hence the same split, on every
+    // rank); the count matrix carries a hash of each rank's split.  A rank
+    // without one (a new handle, another communicator size, DBI_SHARD_RESAMPLE=1)
+    // or ranks that disagree: every rank samples (the samples all-gather, with
+    // a fingerprint of each rank's cost profile: profiles that differ are not
+    // used), and partitions again.  The decision is taken from the gathered
+    // matrix, so every rank takes the same collectives.
+    const char* resample = std::getenv("DBI_SHARD_RESAMPLE");
+    bool have_split = wm.valid && wm.n == n && !(resample && resample[0] == '1');
     int32_t split[MAX_SHARDS - 1] = {};
-    // the same everywhere: every rank holds the same samples and cost profile
-    if ((rc = dbi_shard_splitters_profiled(h, packed.data(), n, split))) return rc;
-    sh.ms_digest = now_ms() - t_digest;
-    const double t_part = now_ms();
-    int rc_part = partition_launch(h, split);
-    if (!rc_part) rc_part = injected_failure("partition", me);
+    if (have_split) std::copy(wm.split, wm.split + (n - 1), split);
+    bool sampled = false;
+    auto sample_split = [&]() -> int {
+        // block of rank r: NS record masses (written on the device), its record
+        // count, its status, its cost-profile fingerprint
+        const size_t blk = NS + 3;
+        int rc_s = rc_digest;
+        double* my_blk = c->d_samp + (size_t)me * blk;
+        if (!rc_s) {
+            const hipError_t e = launch_sample_masses(h->recA.p, sh.n_in, NS, my_blk, s);
+            if (e != hipSuccess) rc_s = hip_fail(e, "launch_sample_masses");
+        }
+        std::vector<double> samples((size_t)n * blk, 0.0);
+        double* mine = samples.data() + (size_t)me * blk;
+        mine[NS] = rc_s ? 0.0 : (double)sh.n_digest;
+        mine[NS + 1] = rc_s ? 1.0 : 0.0;
+        uint64_t fp = pf.valid ? fnv64(pf.cost, sizeof(pf.cost), fnv64(pf.split, sizeof(pf.split))) : 0ull;
+        std::memcpy(&mine[NS + 2], &fp, 8);
+        DBI_HIP(hipMemcpyAsync(my_blk + NS, mine + NS, 3 * sizeof(double), hipMemcpyHostToDevice, s));
+        int rc_c;
+        if ((rc_c = c_allgather(c, my_blk, c->d_samp, 8ull * blk, s))) return rc_c;
+        DBI_HIP(hipMemcpyAsync(samples.data(), c->d_samp, sizeof(double) * n * blk, hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipStreamSynchronize(s));
+        if (rc_s) return rc_s;
+        std::vector<double> packed((size_t)n * (NS + 1));
+        bool same_profile = true;
+        for (int r = 0; r < n; ++r) {
+            const double* b = samples.data() + (size_t)r * blk;
+            if (b[NS + 1] != 0.0) return peer_failed("shard digest");
+            uint64_t fr;
+            std::memcpy(&fr, &b[NS + 2], 8);
+            same_profile &= fr == fp;
+            uint64_t valid = 0;
+            for (uint32_t i = 0; i < NS; ++i) valid += b[i] == b[i];
+            std::copy(b, b + NS, packed.begin() + (size_t)r * (NS + 1));
+            packed[(size_t)r * (NS + 1) + NS] = valid ? b[NS] / (double)valid : 0.0;  // as dbi_shard_samples
+        }
+        sample_keys(packed.data(), n, h->params.mass_group_factor, wm.keys);
+        // the profile only where every rank holds the same one (a
+        // reopened handle or another build history must not split differently)
+        const bool prof = same_profile && pf.valid;
+        split_from_keys(wm.keys, n, prof ? CB : 0, prof ? pf.split : nullptr, prof ? pf.cost : nullptr, split);
+        sampled = true;
+        have_split = true;
+        return 0;
+    };
 
     // count matrix: row r = records shard r sends each owner (from its owner
-    // histogram, on the device) | its status | its receive capacity
-    const double t0 = now_ms();
-    const int w = n + 2;
-    unsigned long long* my_row = c->d_cnt + (size_t)me * w;
-    if (!rc_part && sh.n_in > 0) {
-        hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(64), 0, s, h->hist.p, sh.part_blocks, (uint32_t)n,
-                           sh.n_digest, my_row);
-        if ((rc = hipGetLastError()) != hipSuccess) rc_part = hip_fail((hipError_t)rc, "k_owner_counts");
-    } else if ((rc = hipMemsetAsync(my_row, 0, sizeof(unsigned long long) * n, s)) != hipSuccess && !rc_part) {
-        rc_part = hip_fail((hipError_t)rc, "hipMemsetAsync");
-    }
+    // histogram, on the device) | its status | its receive capacity | its split's hash
+    const int w = n + 3;
     std::vector<unsigned long long> full((size_t)n * w, 0);
-    full[(size_t)me * w + n] = rc_part ? 1u : 0u;
-    full[(size_t)me * w + n + 1] = h->xrecv.cap;
-    DBI_HIP(hipMemcpyAsync(my_row + n, &full[(size_t)me * w + n], 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
-    DBI_NCCL(ncclAllGather(my_row, c->d_cnt, w, ncclUint64, c->comm, s));
-    DBI_HIP(hipMemcpyAsync(full.data(), c->d_cnt, sizeof(unsigned long long) * n * w, hipMemcpyDeviceToHost, s));
-    DBI_HIP(hipStreamSynchronize(s));
-    if (rc_part) return rc_part;
     std::vector<uint64_t> counts((size_t)n * n);
     bool failed = false, grow = false;
-    for (int i = 0; i < n; ++i) {
-        failed |= full[(size_t)i * w + n] != 0;
-        for (int j = 0; j < n; ++j) counts[(size_t)i * n + j] = full[(size_t)i * w + j];
+    double t_part = now_ms();
+    for (int round = 0;; ++round) {
+        if (round > 0) {
+            if ((rc = sample_split())) return rc;
+            t_part = now_ms();
+        }
+        int rc_part = rc_digest;
+        if (round == 0 && have_split) {
+            // test hook: DBI_TEST_SPLIT_SKEW=<rank> -- that rank's reused split
+            // differs from its peers' (another build history): the count
+            // matrix's hashes disagree and every rank samples again
+            const char* sk = std::getenv("DBI_TEST_SPLIT_SKEW");
+            if (sk && std::atoi(sk) == me && n > 1) split[0] += 1;
+        }
+        if (!rc_part && have_split) rc_part = partition_launch(h, split);
+        if (!rc_part) rc_part = injected_failure("partition", me);
+        unsigned long long* my_row = c->d_cnt + (size_t)me * w;
+        if (!rc_part && have_split && sh.n_in > 0) {
+            hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(64), 0, s, h->hist.p, sh.part_blocks, (uint32_t)n,
+                               sh.n_digest, my_row);
+            if ((rc = hipGetLastError()) != hipSuccess) rc_part = hip_fail((hipError_t)rc, "k_owner_counts");
+        } else if ((rc = hipMemsetAsync(my_row, 0, sizeof(unsigned long long) * n, s)) != hipSuccess && !rc_part) {
+            rc_part = hip_fail((hipError_t)rc, "hipMemsetAsync");
+        }
+        unsigned long long* mine = &full[(size_t)me * w];
+        mine[n] = rc_part ? 1u : 0u;
+        mine[n + 1] = h->xrecv.cap;
+        mine[n + 2] = have_split ? (fnv64(split, sizeof(int32_t) * (n - 1)) | 1ull) : 0ull;
+        DBI_HIP(hipMemcpyAsync(my_row + n, mine + n, 3 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+        if ((rc = c_allgather(c, my_row, c->d_cnt, 8ull * w, s))) return rc;
+        DBI_HIP(hipMemcpyAsync(full.data(), c->d_cnt, sizeof(unsigned long long) * n * w, hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipStreamSynchronize(s));
+        if (rc_part) return rc_part;
+        bool agree_split = true;
+        for (int i = 0; i < n; ++i) {
+            failed |= full[(size_t)i * w + n] != 0;
+            agree_split &= full[(size_t)i * w + n + 2] != 0 && full[(size_t)i * w + n + 2] == mine[n + 2];
+        }
+        if (failed) return peer_failed(round == 0 ? "owner partition" : "owner partition (sampled split)");
+        sh.split_rounds = round + 1;
+        if (agree_split) break;
+        if (round > 0) return set_error(DBI_E_STATE, "internal: ranks computed different owner splits from the "
+                                                     "same samples");
+        have_split = false;  // every rank samples: the same verdict from the same matrix
     }
-    if (failed) return peer_failed("owner partition");
+    sh.ms_digest = t_part - t_digest;
+    sh.split_sampled = sampled ? 1 : 0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) counts[(size_t)i * n + j] = full[(size_t)i * w + j];
     // checks on the whole matrix: every rank reaches the same verdict
     for (int j = 0; j < n; ++j) {
         uint64_t tot = 0;
@@ -1197,10 +1591,11 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     }
     std::vector<uint64_t> roff;
     offsets_of(sh.recv_count, roff);
+    const double t0 = now_ms();
     // an owner that must grow its receive buffer may fail to: then every rank
     // learns it before the exchange (a collective only when someone grows)
     if (grow) {
-        rc_local = h->xrecv.ensure(std::max<uint64_t>(roff[n], 1));
+        int rc_local = h->xrecv.ensure(std::max<uint64_t>(roff[n], 1));
         if (!rc_local) rc_local = injected_failure("buffers", me);
         if ((rc = agree(c, rc_local, s, &failed))) return rc;
         if (rc_local) return rc_local;
@@ -1220,40 +1615,97 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     sh.n_recv = roff[n];
     sh.ms_exchange = now_ms() - t0;
     sh.phase = 3;
-    int rc_merge = dbi_shard_merge(h);
-    if (!rc_merge) rc_merge = injected_failure("merge", me);
 
-    // whole-index totals (+ status), and where this owner's rows start in the whole index
+    // owner merge, then the whole-index totals: the merge's counters reach the
+    // host with the totals all-gather (one host sync for both).  Row: n_total,
+    // n_dropped, n_recv, n_unique, n_keys, status, the previous build's merge
+    // device time (ns) and records received (the cost profile), merge flags
+    // (bit 0: this owner's chunk lists outgrew their grids -- it merges again
+    // and every rank gathers the totals again; bits 8+: device errors)
+    const double t_merge = now_ms();
+    MergeRange mr;
+    int rc_merge = merge_begin(h, mr);
+    std::vector<unsigned long long> rows((size_t)n * TOTALS_W);
     std::vector<uint64_t> tot(5, 0);
-    {
-        const int wt = 7;
-        std::vector<unsigned long long> row(wt, 0), rows((size_t)n * wt);
-        row[0] = sh.n_total; row[1] = sh.n_dropped; row[2] = sh.n_recv; row[3] = h->stats.n_unique;
-        row[4] = h->stats.n_keys;
+    bool redo_me = true;
+    const int nstage0 = h->nstage;
+    for (int attempt = 0;; ++attempt) {
+        if (!rc_merge && redo_me) {
+            if (attempt > 0) h->nstage = nstage0;
+            rc_merge = merge_enqueue(h, mr, attempt);
+        }
+        if (!rc_merge && attempt == 0) rc_merge = injected_failure("merge", me);
+        unsigned long long row[TOTALS_W] = {};
+        row[0] = sh.n_total;
+        row[1] = sh.n_dropped;
+        row[2] = sh.n_recv;
         row[5] = rc_merge ? 1u : 0u;
-        row[6] = rc_merge ? 0u : (unsigned long long)(sh.ms_merge_gpu * 1e6);  // ns
-        DBI_HIP(hipMemcpyAsync(c->d_cnt + (size_t)me * wt, row.data(), sizeof(uint64_t) * wt, hipMemcpyHostToDevice, s));
-        DBI_NCCL(ncclAllGather(c->d_cnt + (size_t)me * wt, c->d_cnt, wt, ncclUint64, c->comm, s));
-        DBI_HIP(hipMemcpyAsync(rows.data(), c->d_cnt, sizeof(uint64_t) * n * wt, hipMemcpyDeviceToHost, s));
+        row[6] = (unsigned long long)(wm.prev_merge_ms * 1e6);  // ns
+        row[8] = wm.prev_recv;
+        unsigned long long* my_row = c->d_cnt + (size_t)me * TOTALS_W;
+        DBI_HIP(hipMemcpyAsync(my_row, row, sizeof(row), hipMemcpyHostToDevice, s));
+        if (!rc_merge) {
+            hipLaunchKernelGGL(k_totals_row, dim3(1), dim3(64), 0, s, h->ctr.p, my_row, h->skip_mid ? 1 : 0,
+                               h->skip_big ? 1 : 0);
+            if ((rc = hipGetLastError()) != hipSuccess) rc_merge = hip_fail((hipError_t)rc, "k_totals_row");
+        }
+        if ((rc = c_allgather(c, my_row, c->d_cnt, 8ull * TOTALS_W, s))) return rc;
+        DBI_HIP(hipMemcpyAsync(rows.data(), c->d_cnt, sizeof(unsigned long long) * n * TOTALS_W,
+                               hipMemcpyDeviceToHost, s));
+        DBI_HIP(hipMemcpyAsync(&h->hc, h->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, s));
         DBI_HIP(hipStreamSynchronize(s));
         if (rc_merge) return rc_merge;
-        sh.u_base = 0;
+        bool any_redo = false;
         for (int i = 0; i < n; ++i) {
-            if (rows[(size_t)i * wt + 5]) return peer_failed("owner merge");
-            for (int k = 0; k < 5; ++k) tot[k] += rows[(size_t)i * wt + k];
-            if (i < me) sh.u_base += rows[(size_t)i * wt + 3];
+            const unsigned long long* r = rows.data() + (size_t)i * TOTALS_W;
+            if (r[5] || (r[7] >> 8)) {
+                if (i == me) {  // this owner's device error: finish_build names it
+                    h->hc_final = true;
+                    if ((rc = finish_build(h))) return rc;
+                }
+                return peer_failed("owner merge");
+            }
+            any_redo |= (r[7] & 1u) != 0;
         }
-        sh.u_base_known = true;
-        // the cost profile for the next build: every owner's merge device time
-        // and records over its key range (the same numbers, hence the same
-        // profile, on every rank)
-        std::vector<double> mms(n);
-        std::vector<uint64_t> recs(n);
-        for (int i = 0; i < n; ++i) {
-            mms[i] = (double)rows[(size_t)i * wt + 6] * 1e-6;
-            recs[i] = rows[(size_t)i * wt + 2];
-        }
-        if ((rc = dbi_shard_cost_update(h, n, sh.split, mms.data(), recs.data()))) return rc;
+        redo_me = (rows[(size_t)me * TOTALS_W + 7] & 1u) != 0;
+        if (!any_redo) break;
+        if (attempt > 0) return set_error(DBI_E_STATE, "internal: chunk lists outgrew full grids");
+    }
+    h->hc_final = true;  // the counters came with the totals
+    if ((rc = merge_done(h, mr))) return rc;
+    sh.ms_merge = now_ms() - t_merge;
+    sh.phase = 4;
+    sh.u_base = 0;
+    for (int i = 0; i < n; ++i) {
+        for (int k = 0; k < 5; ++k) tot[k] += rows[(size_t)i * TOTALS_W + k];
+        if (i < me) sh.u_base += rows[(size_t)i * TOTALS_W + 3];
+    }
+    sh.u_base_known = true;
+    // the cost profile from the PREVIOUS build's owners (merge device time and
+    // records, the same numbers on every rank; this build's merge time is
+    // known only after the totals round), then the split the next build uses
+    std::vector<double> mms(n);
+    std::vector<uint64_t> recs(n);
+    for (int i = 0; i < n; ++i) {
+        mms[i] = (double)rows[(size_t)i * TOTALS_W + 6] * 1e-6;
+        recs[i] = rows[(size_t)i * TOTALS_W + 8];
+    }
+    if (wm.valid && wm.n == n && (rc = dbi_shard_cost_update(h, n, wm.prev_split, mms.data(), recs.data())))
+        return rc;
+    std::copy(sh.split, sh.split + (n - 1), wm.prev_split);
+    wm.prev_merge_ms = sh.ms_merge_gpu;
+    wm.prev_recv = sh.n_recv;
+    if (sampled) wm.sampled_kept = tot[2];
+    // a proteome of another size than the sampled one: sample again next time
+    const bool stale = wm.sampled_kept == 0 || tot[2] > wm.sampled_kept + wm.sampled_kept / 20 ||
+                       tot[2] + wm.sampled_kept / 20 < wm.sampled_kept;
+    if (stale) {
+        wm.valid = false;
+    } else {
+        split_from_keys(wm.keys, n, pf.valid ? CB : 0, pf.valid ? pf.split : nullptr, pf.valid ? pf.cost : nullptr,
+                        wm.split);
+        wm.valid = true;
+        wm.n = n;
     }
     sh.global.g_total = tot[0];
     sh.global.g_dropped = tot[1];

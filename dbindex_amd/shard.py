@@ -121,6 +121,18 @@ class ShardComm:
         check(_native.lib().dbi_comm_init(buf, nranks, rank, device, ctypes.byref(h)))
         self.h = h
 
+    @classmethod
+    def host(cls, name: str, nranks: int, rank: int, device: int, slot_bytes: int = 64 << 20) -> "ShardComm":
+        """TESTS ONLY: the host-staged transport (dbi_comm_init_host): the same
+        collectives through POSIX shared memory ``name`` between the processes of
+        one node, so N processes on ONE GPU run the N-rank driver."""
+        self = cls.__new__(cls)
+        self.nranks, self.rank, self.device = nranks, rank, device
+        h = ctypes.c_void_p()
+        check(_native.lib().dbi_comm_init_host(name.encode(), nranks, rank, device, slot_bytes, ctypes.byref(h)))
+        self.h = h
+        return self
+
     @staticmethod
     def unique_id() -> bytes:
         buf = (ctypes.c_uint8 * 128)()

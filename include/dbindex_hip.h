@@ -309,6 +309,10 @@ typedef struct dbi_shard_stats {
     uint64_t g_total, g_dropped, g_kept, g_unique, g_keys;
     double digest_ms, partition_ms, exchange_ms, merge_ms; /* wall time of each phase      */
     double merge_gpu_ms;          /* device time of this owner's merge kernels             */
+    int32_t split_sampled;        /* dbi_build_sharded: 1 = this build gathered samples for its
+                                     owner split, 0 = it reused the previous build's split  */
+    int32_t split_rounds;         /* count-matrix rounds (2: a rank lacked or disagreed on the
+                                     split, every rank sampled and partitioned again)       */
 } dbi_shard_stats;
 
 /* Digest proteins [p_begin, p_end) of the global arrays (device pointers:
@@ -379,6 +383,13 @@ int dbi_query_sharded_local(dbi_handle* const* hs, int nshards, const double* co
  * rank 0's dbi_comm_unique_id and is passed to every rank out of band. */
 int dbi_comm_unique_id(uint8_t* id128);
 int dbi_comm_init(const uint8_t* id128, int nranks, int rank, int device, dbi_comm** out);
+/* TESTS ONLY: the same communicator over a host-staged transport -- POSIX
+ * shared memory `name` ("/..."; rank 0 creates it, the others attach) between
+ * the processes of one node, device -> host -> shared memory -> host ->
+ * device with a barrier between, slot_bytes per rank slot and per (source,
+ * destination) mailbox -- so that N processes on ONE GPU run the N-rank
+ * driver (RCCL refuses two ranks on one device).  Every product run is RCCL. */
+int dbi_comm_init_host(const char* name, int nranks, int rank, int device, uint64_t slot_bytes, dbi_comm** out);
 void dbi_comm_destroy(dbi_comm* c);
 /* d_recv = concatenation over ranks of rank_bytes[r] bytes; this rank's piece
  * (rank_bytes[rank] bytes at d_send) lands at its offset (d_send may be that

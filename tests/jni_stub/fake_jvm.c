@@ -85,8 +85,12 @@ static char* dup_str(const char* s) {
 static jclass FindClass(JNIEnv* env, const char* name) {
     (void)env;
     violation_if_pending("FindClass");
-    strncat(g_log, name, sizeof g_log - strlen(g_log) - 2);
-    strncat(g_log, ";", sizeof g_log - strlen(g_log) - 1);
+    const size_t used = strlen(g_log), len = strlen(name);
+    if (used + len + 2 <= sizeof g_log) {  /* the log keeps the first classes only */
+        memcpy(g_log + used, name, len);
+        g_log[used + len] = ';';
+        g_log[used + len + 1] = 0;
+    }
     struct _jobject* c = (struct _jobject*)calloc(1, sizeof(struct _jobject));
     c->kind = FJ_CLASS;
     c->name = dup_str(name);

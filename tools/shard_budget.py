@@ -34,6 +34,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 LINK_GBS = 64.0  # achieved GB/s per xGMI link per direction (one link per GPU pair)
+ALLGATHER_US = 20.0  # latency of one small RCCL all-gather over 8 GPUs (assumed, not measurable here)
 
 DIGEST = ("tile_proteins", "digest")
 PARTITION = ("owner_hist", "owner_scan", "owner_scatter")
@@ -45,6 +46,7 @@ def main() -> int:
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-balance", action="store_true", help="record-balanced splitters on every build")
+    ap.add_argument("--no-fixed", action="store_true", help="skip the one-rank fixed-cost measurement")
     a = ap.parse_args()
     from dbindex_amd import fasta, shard
     from dbindex_amd._native import DeviceBuffer, synchronize
@@ -105,6 +107,39 @@ def main() -> int:
         for e in engines:
             e.close()
     best["history"] = history
+    # fixed costs of the RCCL driver per build: dbi_build_sharded with one rank
+    # on the general path (DBI_SHARD_FULL_PATH=1: samples, partition, count
+    # matrix, exchange, owner merge, totals -- every host sync and launch gap
+    # of an N-rank build) over the whole proteome; wall time minus the summed
+    # kernel time.  At N ranks the collectives add their xGMI latency
+    # (ALLGATHER_US each: the count matrix and the totals round of a warm build).
+    if not a.no_fixed:
+        import time
+        os.environ["DBI_SHARD_FULL_PATH"] = "1"
+        comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
+        fixed = []
+        with Engine(cp, 0) as e1:
+            # kernel times from timed builds, wall times from untimed ones (a
+            # build with every stage timed also waits for the exchange)
+            for i in range(2 * a.reps + 4):
+                timed = i % 2 == 0
+                e1.set_timing(timed)
+                synchronize(0)
+                t0 = time.perf_counter()
+                shard.build_sharded(e1, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, 0, pp.n_proteins)
+                wall = 1e3 * (time.perf_counter() - t0)
+                if timed:
+                    dev = sum(ms for _, ms, _ in e1.stage_times())
+                elif i >= 4:
+                    fixed.append(dict(wall_ms=wall, kernels_ms=dev, fixed_ms=wall - dev))
+        comm.close()
+        os.environ.pop("DBI_SHARD_FULL_PATH", None)
+        f = sorted(x["fixed_ms"] for x in fixed)[len(fixed) // 2]
+        best["fixed_one_rank"] = fixed
+        best["fixed_ms"] = f + 2 * ALLGATHER_US * 1e-3
+        best["fixed_note"] = (f"median one-rank general-path wall - kernel time ({f:.3f} ms: host syncs, launch gaps, "
+                              f"host logic) + 2 x {ALLGATHER_US} us of multi-rank all-gather latency")
+        best["model_ms"] = best["model_ms_without_fixed"] + best["fixed_ms"]
     print(json.dumps(best))
     return 0
 
