@@ -3154,6 +3154,9 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
 // WAVE_SORT_MAX, else by the whole block; the full-key bitonic only where the
 // compact key does not hold.  LDS: 8+8+4 B per record.
 constexpr uint32_t RANK_MAX_RUN = 64;
+#ifndef DBI_TAG_SORT
+#define DBI_TAG_SORT 1  // single-mass bins above WAVE_SORT_MAX by the tag counting sort (tag_sort_block)
+#endif
 #ifndef DBI_MID_WPE
 #define DBI_MID_WPE 7
 #endif
@@ -3168,8 +3171,96 @@ struct ChunkSmem {
     uint32_t big[MAXB];  // lo | hi << 16
     uint32_t u32[NT / 64 + 1];
     uint64_t mins[NT / 64];
+    uint16_t tcnt[NT / 64 * 16];  // tag_sort_block: per-wave digit counts, then their scan
     uint32_t nbig, wide, bad;
 };
+
+// Single-mass bins -- equal-mass spikes, every record of the bin with the same
+// fp64 mass (isobaric permutations and repeated peptides; the semi-tryptic
+// scale's big bins): their order is (16-bit tag, first appearance), so the
+// bin is sorted by its tag with four stable 4-bit counting passes over an
+// index permutation (wave-ballot ranks in input order, the block's 16 x NW
+// digit counts scanned in LDS; O(L) per pass, against the compact-key
+// network's O(L log^2 L) with one barrier pair per cross-wave step), the
+// records gathered once into that order, then equal-tag runs put in q1
+// order (ck_fix_runs).  false (block-uniform): more than one mass in the bin,
+// or a run above CK_RUN_MAX (the bin is then a permutation of itself, for the
+// caller's compact-key sort).  pa / pb: 2 x L u16 of scratch.
+template <int NT, int CAP>
+__device__ bool tag_sort_block(unsigned long long* k0, unsigned long long* k1, uint32_t lo, uint32_t L, uint16_t* pa,
+                               uint16_t* pb, uint16_t* cnt, uint32_t* s_tmp) {
+    constexpr uint32_t NW = NT / 64;
+    constexpr uint32_t IT = (CAP + NT - 1) / NT;  // items per lane (a wave's share of L <= CAP)
+    static_assert(NW * 16 <= NT, "one scan entry per thread");
+    const uint64_t mb = k0[lo] >> 8;
+    bool diff = false;
+    for (uint32_t i = threadIdx.x; i < L; i += NT) diff |= (k0[lo + i] >> 8) != mb;
+    if (__syncthreads_or(diff)) return false;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t share = (L + NW - 1) / NW;  // wave w ranks positions [w*share, w*share + share)
+    const uint32_t wb = min(w * share, L), we = min(wb + share, L);
+    uint16_t* src = pa;
+    uint16_t* dst = pb;
+#pragma unroll 1
+    for (uint32_t pass = 0; pass < 4; ++pass) {
+        if (lane < 16) cnt[w * 16 + lane] = 0;
+        wave_sync();
+        // per item: index (13 b) | digit (4 b) << 13 | rank in the wave's digit (15 b) << 17; ~0: none
+        uint32_t it[IT];
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k) {
+            const uint32_t t = wb + k * 64 + lane;
+            const bool valid = t < we;
+            const uint32_t j = !valid ? 0u : pass == 0 ? t : (uint32_t)src[t];
+            const uint32_t tag = (uint32_t)((k0[lo + j] & 0xFFu) << 8) | (uint32_t)(k1[lo + j] >> 56);
+            const uint32_t d = (tag >> (4 * pass)) & 15u;
+            const uint64_t peers = digit_peers(d, valid, 4);
+            const uint32_t before = cnt[w * 16 + d];
+            wave_sync();
+            if (valid && (peers & lanemask_lt()) == 0) cnt[w * 16 + d] = (uint16_t)(before + (uint32_t)__popcll(peers));
+            wave_sync();
+            it[k] = valid ? j | (d << 13) | ((before + (uint32_t)__popcll(peers & lanemask_lt())) << 17) : ~0u;
+        }
+        __syncthreads();
+        // exclusive scan over (digit, wave), digit-major: the first position of
+        // wave w's records of digit d
+        const uint32_t e = threadIdx.x;  // e = d * NW + ww
+        const uint32_t v = e < NW * 16 ? (uint32_t)cnt[(e % NW) * 16 + e / NW] : 0u;
+        uint32_t tot;
+        const uint32_t base = block_excl_scan<NT, uint32_t>(v, s_tmp, tot);
+        if (e < NW * 16) cnt[(e % NW) * 16 + e / NW] = (uint16_t)base;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k)
+            if (it[k] != ~0u) dst[cnt[w * 16 + ((it[k] >> 13) & 15u)] + (it[k] >> 17)] = (uint16_t)(it[k] & 0x1FFFu);
+        __syncthreads();
+        uint16_t* x = src;
+        src = dst;
+        dst = x;
+    }
+    // the records into that order (every read before any write), then runs of equal tags by q1
+    // (one word at a time: half the registers; q0 differs only in its tag byte)
+    unsigned long long* const kw[2] = {k0, k1};
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+        unsigned long long* kk = kw[h];
+        unsigned long long v[IT];
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k) {
+            const uint32_t t = threadIdx.x + k * NT;
+            if (t < L) v[k] = kk[lo + src[t]];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k) {
+            const uint32_t t = threadIdx.x + k * NT;
+            if (t < L) kk[lo + t] = v[k];
+        }
+        __syncthreads();
+    }
+    const bool fixed = ck_fix_runs(k0, k1, lo, L, threadIdx.x, NT);
+    return !__syncthreads_or(!fixed);
+}
 
 // The chunk in[0, m) -> out[0, m) in final order with head flags; *heads =
 // this thread's unique heads.  BLOCK off: a chunk with a run above
@@ -3297,10 +3388,15 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
     if constexpr (BLOCK) {
         constexpr int R = NT * 4 >= CAP ? 4 : 8;
         static_assert(NT * R >= CAP, "compact-sort capacity");
+        uint16_t* a16 = reinterpret_cast<uint16_t*>(sm.aux);  // free until finish_sorted
         for (uint32_t r = 0; r < nbig; ++r) {
             const uint32_t b = sm.big[r];
             const uint32_t lo = b & 0xFFFFu, L = (b >> 16) - lo;
-            if (L > WAVE_SORT_MAX && !ck_run_block<NT, R>(k0, k1, lo, L, sm.mins)) block_bitonic<NT>(k0, k1, lo, L);
+            if (L <= WAVE_SORT_MAX) continue;
+            // (the big tier only: in the mid kernel its registers cost a block per CU)
+            if constexpr (DBI_TAG_SORT && CAP > 2048)
+                if (tag_sort_block<NT, CAP>(k0, k1, lo, L, a16, a16 + CAP, sm.tcnt, sm.u32)) continue;
+            if (!ck_run_block<NT, R>(k0, k1, lo, L, sm.mins)) block_bitonic<NT>(k0, k1, lo, L);
         }
         __syncthreads();
     }
@@ -3405,7 +3501,7 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
 template <int NT, int CAP>
 __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const RecLoc& rl,
                                   unsigned long long* k0, unsigned long long* k1, uint32_t* aux, uint32_t* s_u32,
-                                  uint32_t* s_bad, uint64_t* s_min) {
+                                  uint32_t* s_bad, uint64_t* s_min, uint16_t* s_tcnt) {
     for (uint32_t i = threadIdx.x; i < m; i += NT) {
         const Rec r = in[i];
         k0[i] = r.q0;
@@ -3414,7 +3510,10 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
     __syncthreads();
     constexpr int R = NT * 4 >= CAP ? 4 : 8;
     static_assert(NT * R >= CAP, "compact-sort capacity");
-    if (!ck_run_block<NT, R>(k0, k1, 0, m, s_min)) block_bitonic<NT>(k0, k1, 0, m);
+    // a giant chunk's leaves are mostly one mass (an isobaric spike split by tag bits)
+    uint16_t* a16 = reinterpret_cast<uint16_t*>(aux);
+    const bool tagged = DBI_TAG_SORT && m > 1 && tag_sort_block<NT, CAP>(k0, k1, 0, m, a16, a16 + CAP, s_tcnt, s_u32);
+    if (!tagged && !ck_run_block<NT, R>(k0, k1, 0, m, s_min)) block_bitonic<NT>(k0, k1, 0, m);
     return finish_sorted<NT>(out, m, rl, k0, k1, aux, s_u32, s_bad);
 }
 
@@ -4550,13 +4649,15 @@ k_giant_leaf(const Rec* in, Rec* out, const uint4* __restrict__ list, const unsi
     __shared__ uint32_t aux[CAP];
     __shared__ uint32_t s_u32[NT / 64 + 1];
     __shared__ uint64_t s_min[NT / 64];
+    __shared__ uint16_t s_tcnt[NT / 64 * 16];
     __shared__ uint32_t s_bad;
     const uint32_t nl = min(*n_list, cap);
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
         const uint4 lf = list[j];
         const Rec* from = (lf.w ? out : in) + lf.x;
-        const uint32_t h = bitonic_chunk<NT, CAP>(from, out + lf.x, lf.y, rl, k0, k1, aux, s_u32, &s_bad, s_min);
+        const uint32_t h =
+            bitonic_chunk<NT, CAP>(from, out + lf.x, lf.y, rl, k0, k1, aux, s_u32, &s_bad, s_min, s_tcnt);
         const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
         if (threadIdx.x == 0) atomicAdd(&ucount[lf.z], tot);
         __syncthreads();

@@ -276,6 +276,31 @@ struct dbi_handle {
         uint64_t n_bins = 0, n_in = 0;
         bool sparse = false;
     } bgraph;
+    // The owner merge of a warm sharded build (dbi_shard.hip merge_enqueue),
+    // captured the same way: the second identical merge is captured, later
+    // ones replay it.  Key: everything its kernels bake in.
+    struct MergeKey {
+        GraphKey g{};             // inputs, buffers, grids, parameters, timing
+        uint64_t n_recv = 0;
+        double lo = 0, hi = 0;
+        const void* xrecv = nullptr;
+        uint32_t width = 0;
+        int nstage0 = 0;          // stage slots (event pool) the merge's stages start at
+        bool operator==(const MergeKey& o) const {
+            return g == o.g && n_recv == o.n_recv && lo == o.lo && hi == o.hi && xrecv == o.xrecv &&
+                   width == o.width && nstage0 == o.nstage0;
+        }
+    };
+    struct {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        MergeKey key{};
+        Stage stages[MAX_STAGES];
+        int nstage = 0;
+        uint64_t n_bins = 0;
+    } mgraph;
+    MergeKey prev_mkey{};
+    bool prev_mkey_valid = false;
 };
 
 
@@ -344,7 +369,8 @@ int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse);  // bui
 int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
                const unsigned long long* d_n_in = nullptr, const unsigned long long* d_n = nullptr, uint64_t n_est = 0, bool est = false);
 int ensure_qdir(dbi_handle* h, hipStream_t s);  // query directory of the current index
-void drop_graph(dbi_handle* h);                 // the captured warm build graph, if any
+void drop_graph(dbi_handle* h);                 // the captured warm build graphs (build, owner merge), if any
+dbi_handle::GraphKey graph_key(const dbi_handle* h);
 uint32_t choose_nbins(uint64_t n, int max_bits);  // fine mass bins of a tail over n records
 int radix_plan(uint32_t nbins, bool sparse, int* width);  // LSD digit widths; returns the passes
 int finish_build(dbi_handle* h);

@@ -457,6 +457,11 @@ void drop_graph(dbi_handle* h) {
     if (h->bgraph.graph) (void)hipGraphDestroy(h->bgraph.graph);
     h->bgraph.exec = nullptr;
     h->bgraph.graph = nullptr;
+    if (h->mgraph.exec) (void)hipGraphExecDestroy(h->mgraph.exec);
+    if (h->mgraph.graph) (void)hipGraphDestroy(h->mgraph.graph);
+    h->mgraph.exec = nullptr;
+    h->mgraph.graph = nullptr;
+    h->prev_mkey_valid = false;
 }
 
 // digest + tail of a warm device-sized build, enqueued (or captured)

@@ -884,7 +884,7 @@ int merge_begin(dbi_handle* h, MergeRange& mr) {
 // attempt 0: the chunk-list grids (and whether to run the giant pass) from
 // this owner's previous merge; attempt 1 (lists outgrew them, ERR_GRID): full
 // grids, from the received words again
-int merge_enqueue(dbi_handle* h, const MergeRange& mr, int attempt) {
+int merge_body(dbi_handle* h, const MergeRange& mr, int attempt) {
     ShardState& sh = h->shard;
     hipStream_t s = h->stream;
     if (attempt > 0) h->giants_seen = true;
@@ -914,6 +914,79 @@ int merge_enqueue(dbi_handle* h, const MergeRange& mr, int attempt) {
     h->h1_on = false;
     if (rc) return rc;
     DBI_HIP(hipEventRecord(h->ev_merge[1], s));
+    return 0;
+}
+
+// The merge's kernels, enqueued -- or, for a warm merge identical to the
+// previous one (a repeated build of the same proteome: the same records
+// received, the same buffers, grids and key range), replayed as a hipGraph
+// captured on the second such merge (~30 launches: their gaps), as the
+// single-device warm build does (build_digest).  Not with every stage timed
+// (events in the dispatch packets) and not for a redo (attempt 1).
+int merge_enqueue(dbi_handle* h, const MergeRange& mr, int attempt) {
+    const bool graphable = attempt == 0 && h->use_graph && !(h->timing && h->timing_only.empty());
+    if (!graphable) return merge_body(h, mr, attempt);
+    dbi_handle::MergeKey k;
+    k.g = graph_key(h);
+    k.n_recv = h->shard.n_recv;
+    k.lo = mr.lo;
+    k.hi = mr.hi;
+    k.xrecv = h->xrecv.p;
+    k.width = h->shard.width;
+    k.nstage0 = h->nstage;
+    auto& mg = h->mgraph;
+    if (mg.exec && mg.key == k) {
+        DBI_HIP(hipGraphLaunch(mg.exec, h->stream));
+        std::copy(mg.stages, mg.stages + mg.nstage, h->stages + k.nstage0);
+        h->nstage = k.nstage0 + mg.nstage;
+        h->stats.n_bins = mg.n_bins;
+        h->skip_mid = h->grid_mid == GRID_NONE;  // as when it was captured (the grids are in the key)
+        h->skip_big = h->grid_big == GRID_NONE;
+        return 0;
+    }
+    if (!(h->prev_mkey_valid && h->prev_mkey == k)) {
+        const int rc = merge_body(h, mr, attempt);
+        h->prev_mkey = k;
+        h->prev_mkey_valid = rc == 0;
+        return rc;
+    }
+    // the same merge as last time: capture it, then run the graph
+    if (mg.exec) (void)hipGraphExecDestroy(mg.exec);
+    if (mg.graph) (void)hipGraphDestroy(mg.graph);
+    mg.exec = nullptr;
+    mg.graph = nullptr;
+    DBI_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+    h->capturing = true;
+    const int rc = merge_body(h, mr, attempt);
+    h->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(h->stream, &g);
+    if (rc || ec != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        h->prev_mkey_valid = false;
+        return rc ? rc : hip_fail(ec, "hipStreamEndCapture (owner merge)");
+    }
+    hipGraphExec_t ex = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        h->prev_mkey_valid = false;
+        return hip_fail(ei, "hipGraphInstantiate (owner merge)");
+    }
+    DBI_HIP(hipGraphLaunch(ex, h->stream));
+    mg.graph = g;
+    mg.exec = ex;
+    mg.key = k;
+    mg.nstage = h->nstage - k.nstage0;
+    std::copy(h->stages + k.nstage0, h->stages + h->nstage, mg.stages);
+    mg.n_bins = h->stats.n_bins;
+    if (graph_key(h).alloc_gen != k.g.alloc_gen) {  // buffers moved while capturing: once only
+        (void)hipGraphExecDestroy(mg.exec);
+        (void)hipGraphDestroy(mg.graph);
+        mg.exec = nullptr;
+        mg.graph = nullptr;
+        h->prev_mkey_valid = false;
+    }
     return 0;
 }
 

@@ -354,3 +354,27 @@ def test_sharded_cost_profile_splitters(native):
     finally:
         for e in engines:
             e.close()
+
+
+def test_sharded_local_merge_graph_replays(native):
+    """Untimed repeated builds: each owner's merge is enqueued (build 0),
+    captured as a hipGraph (build 1, the same merge again) and replayed (builds
+    2-4); a different proteome in between (new key: plain again), then the
+    first one again.  Every build equals the oracle."""
+    from dbindex_amd.engine import Engine
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    a, b = fasta.config("1k"), fasta.config("1k").slice(0, 700)
+    oa, ob = (cref.Index(cp, p.residues, p.offsets) for p in (a, b))
+    bufs = {id(p): _inputs(native, p) for p in (a, b)}
+    engines = [Engine(cp, 0) for _ in range(3)]
+    try:
+        for e in engines:
+            e.set_timing(False)
+        for k, (p, o) in enumerate([(a, oa)] * 5 + [(b, ob)] * 3 + [(a, oa)] * 3):
+            d_res, d_off = bufs[id(p)]
+            shard.build_sharded_local(engines, d_res.ptr, p.n_residues, d_off.ptr, p.n_proteins,
+                                      shard.protein_ranges(p.offsets, 3))
+            _assert_sharded_equal(engines, o, f"merge graph build {k}", nq=300)
+    finally:
+        for e in engines:
+            e.close()

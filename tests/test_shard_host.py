@@ -177,3 +177,54 @@ def test_gloo_strong_split_plan_matches_single_store(world, cfg, nprot, missed, 
     on every rank answering its own queries."""
     import torch.multiprocessing as mp
     mp.spawn(_rank_main, args=(world, _free_port(), cfg, nprot, missed, semi), nprocs=world, join=True)
+
+
+def _split_restated(samples, k, factor, band_split=None, band_cost=None):
+    """dbi_shard_splitters_cost restated: every valid sample's key (int)(m*f)
+    weighted by its shard's records per sample x its band's cost; split[j-1] =
+    the first key (at a key change) whose preceding weight reaches j/k of the
+    total; INT32_MAX when none."""
+    ks = []
+    for b in samples:
+        w = b[-1]
+        if not w > 0:
+            continue
+        for m in b[:-1]:
+            if m == m:
+                key = int(np.trunc(m * factor))
+                c = 1.0
+                if band_cost is not None:
+                    c = band_cost[int(np.searchsorted(band_split, key, side="right"))]
+                ks.append((key, w * c))
+    ks.sort(key=lambda x: x[0])
+    total = sum(w for _, w in ks)
+    out, i, cum = [], 0, 0.0
+    for j in range(1, k):
+        target = total * j / k
+        sp = 2**31 - 1
+        while i < len(ks):
+            if cum >= target and (i == 0 or ks[i][0] != ks[i - 1][0]):
+                sp = ks[i][0]
+                break
+            cum += ks[i][1]
+            i += 1
+        out.append(sp)
+    return np.array(out, np.int64)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_splitters_match_restatement(seed):
+    """The library's sorted-keys + linear quantile walk (sample keys sorted
+    once, band costs applied by a moving pointer) equals the weighted-quantile
+    definition -- ties of equal keys across shards included (a split lands on
+    a key change only)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k, f = 5, 10000
+    # coarse masses: many equal keys across shards
+    blocks = [np.sort(np.round(rng.lognormal(7.2, 0.35, n), 2)) for n in (30_000, 9_000, 45_000, 500, 20_000)]
+    s = _samples_of(blocks)
+    assert np.array_equal(shard.splitters(s, k, f).astype(np.int64), _split_restated(s, k, f))
+    band_split = np.sort(rng.integers(5_000_000, 30_000_000, 31)).astype(np.int32)
+    band_cost = rng.uniform(0.2, 4.0, 32)
+    got = shard.splitters(s, k, f, profile=(band_split, band_cost)).astype(np.int64)
+    assert np.array_equal(got, _split_restated(s, k, f, band_split, band_cost))
