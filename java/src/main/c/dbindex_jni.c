@@ -252,30 +252,38 @@ static jobject seq_list(JNIEnv* e, dbi_seq_list* l) {
         so[i] = (jint)l->seq_off[i];
         po[i] = (jint)l->prot_off[i];
     }
-    jdoubleArray mass = (*e)->NewDoubleArray(e, n);
-    if (mass) (*e)->SetDoubleArrayRegion(e, mass, 0, n, l->mass);
-    jintArray seqOff = (*e)->NewIntArray(e, n + 1);
-    if (seqOff) (*e)->SetIntArrayRegion(e, seqOff, 0, n + 1, so);
-    jbyteArray chars = (*e)->NewByteArray(e, nc);
-    if (chars) (*e)->SetByteArrayRegion(e, chars, 0, nc, (const jbyte*)l->seq_chars);
-    jbyteArray left = (*e)->NewByteArray(e, 3 * n);
-    if (left) (*e)->SetByteArrayRegion(e, left, 0, 3 * n, (const jbyte*)l->res_left);
-    jbyteArray right = (*e)->NewByteArray(e, 3 * n);
-    if (right) (*e)->SetByteArrayRegion(e, right, 0, 3 * n, (const jbyte*)l->res_right);
-    jintArray protOff = (*e)->NewIntArray(e, n + 1);
-    if (protOff) (*e)->SetIntArrayRegion(e, protOff, 0, n + 1, po);
-    jintArray protIds = (*e)->NewIntArray(e, np);
-    if (protIds) (*e)->SetIntArrayRegion(e, protIds, 0, np, (const jint*)l->prot_ids);
-    jintArray pepOff = (*e)->NewIntArray(e, n);
-    if (pepOff) (*e)->SetIntArrayRegion(e, pepOff, 0, n, (const jint*)l->offset);
-    free(so);
-    free(po);
+    /* one JVM allocation at a time: after a failed one (OutOfMemoryError
+     * pending) no further JNI call but the cleanup (JNI specification) */
+    jobject ret = NULL;
+    jdoubleArray mass = NULL;
+    jintArray seqOff = NULL, protOff = NULL, protIds = NULL, pepOff = NULL;
+    jbyteArray chars = NULL, left = NULL, right = NULL;
+    if (!(mass = (*e)->NewDoubleArray(e, n))) goto done;
+    (*e)->SetDoubleArrayRegion(e, mass, 0, n, l->mass);
+    if (!(seqOff = (*e)->NewIntArray(e, n + 1))) goto done;
+    (*e)->SetIntArrayRegion(e, seqOff, 0, n + 1, so);
+    if (!(chars = (*e)->NewByteArray(e, nc))) goto done;
+    (*e)->SetByteArrayRegion(e, chars, 0, nc, (const jbyte*)l->seq_chars);
+    if (!(left = (*e)->NewByteArray(e, 3 * n))) goto done;
+    (*e)->SetByteArrayRegion(e, left, 0, 3 * n, (const jbyte*)l->res_left);
+    if (!(right = (*e)->NewByteArray(e, 3 * n))) goto done;
+    (*e)->SetByteArrayRegion(e, right, 0, 3 * n, (const jbyte*)l->res_right);
+    if (!(protOff = (*e)->NewIntArray(e, n + 1))) goto done;
+    (*e)->SetIntArrayRegion(e, protOff, 0, n + 1, po);
+    if (!(protIds = (*e)->NewIntArray(e, np))) goto done;
+    (*e)->SetIntArrayRegion(e, protIds, 0, np, (const jint*)l->prot_ids);
+    if (!(pepOff = (*e)->NewIntArray(e, n))) goto done;
+    (*e)->SetIntArrayRegion(e, pepOff, 0, n, (const jint*)l->offset);
     if (set_array(e, o, c, "mass", "[D", mass) || set_array(e, o, c, "seqOff", "[I", seqOff) ||
         set_array(e, o, c, "seqChars", "[B", chars) || set_array(e, o, c, "left", "[B", left) ||
         set_array(e, o, c, "right", "[B", right) || set_array(e, o, c, "protOff", "[I", protOff) ||
         set_array(e, o, c, "protIds", "[I", protIds) || set_array(e, o, c, "pepOff", "[I", pepOff))
-        return NULL;
-    return o;
+        goto done;
+    ret = o;
+done:
+    free(so);
+    free(po);
+    return ret;
 }
 
 static jobject finish_list(JNIEnv* e, int rc, dbi_seq_list* l) {
