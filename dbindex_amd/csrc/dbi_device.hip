@@ -2874,6 +2874,8 @@ __device__ __forceinline__ bool ck_fix_runs(const unsigned long long* k0, unsign
 
 // One wave sorts k0/k1[lo, lo+L), L <= 64R, by the compact key; false: the
 // run is left a permutation of itself and needs the full-key sort.
+// (a call, not inlined: inlined into k_chunk_sort's 64 VGPRs it spills 132 B
+// per lane against the call's 28 B of callee-saved registers)
 template <int R>
 __device__ bool ck_run_wave(unsigned long long* k0, unsigned long long* k1, uint32_t lo, uint32_t L) {
     const uint32_t lane = lane_id();
@@ -3067,9 +3069,20 @@ __device__ __forceinline__ bool same_tag_at(const unsigned long long* k0, const 
 // by string (first appearance first), write the records in final order with
 // the head flag in the low byte of q0.  aux: scratch (a16[2p] = head info of
 // p, a16[2q+1] = q-th verification pair).  Returns this thread's head count.
+// p inside one of the nw ranges wr[i] = lo | hi << 16 (bins another kernel sorts)
+__device__ __forceinline__ bool in_ranges(const uint32_t* wr, uint32_t nw, uint32_t p) {
+    bool in = false;
+    for (uint32_t i = 0; i < nw; ++i) in |= p >= (wr[i] & 0xFFFFu) && p < (wr[i] >> 16);
+    return in;
+}
+
+// wr / nw: record ranges left out (neither written nor counted: the wide bins
+// chunk_sort_mid sorts); the record after such a range is in another bin, so
+// it is a head whatever the range holds.
 template <int NT>
 __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLoc& rl, const unsigned long long* k0,
-                                  const unsigned long long* k1, uint32_t* aux, uint32_t* s_u32, uint32_t* s_bad) {
+                                  const unsigned long long* k1, uint32_t* aux, uint32_t* s_u32, uint32_t* s_bad,
+                                  const uint32_t* wr = nullptr, uint32_t nw = 0) {
     uint16_t* a16 = reinterpret_cast<uint16_t*>(aux);
     if (threadIdx.x == 0) {
         *s_bad = 0;
@@ -3079,7 +3092,8 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
     uint32_t heads = 0;
     for (uint32_t p0 = 0; p0 < m; p0 += NT) {  // wave-uniform trip count: one LDS atomic per wave
         const uint32_t p = p0 + threadIdx.x;
-        const bool dup = p < m && p > 0 && same_tag_at(k0, k1, p);
+        const bool skip = nw && in_ranges(wr, nw, p);
+        const bool dup = p < m && p > 0 && !skip && same_tag_at(k0, k1, p);
         const uint64_t bal = __ballot(dup);
         uint32_t base = 0;
         if (bal && lane_id() == 0) base = atomicAdd(&s_u32[NT / 64], (uint32_t)__popcll(bal));
@@ -3087,7 +3101,7 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
         if (dup) a16[2 * (base + (uint32_t)__popcll(bal & lanemask_lt())) + 1] = (uint16_t)p;
         if (p < m) {
             a16[2 * p] = (uint16_t)(dup ? 0u : p);
-            heads += !dup;
+            heads += !dup && !skip;
         }
     }
     __syncthreads();
@@ -3101,7 +3115,8 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
     __syncthreads();
     if (*s_bad == 0) {
         for (uint32_t p = threadIdx.x; p < m; p += NT)
-            out[p] = Rec{(k0[p] & ~0xFFull) | (a16[2 * p] == p ? 1ull : 0ull), k1[p]};  // p == 0 always a head
+            if (!nw || !in_ranges(wr, nw, p))
+                out[p] = Rec{(k0[p] & ~0xFFull) | (a16[2 * p] == p ? 1ull : 0ull), k1[p]};  // p == 0 always a head
         return heads;
     }
     // 16-bit tag collision (rare, block-uniform): group start gs(p) = max head
@@ -3132,6 +3147,7 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
     __syncthreads();
     heads = 0;
     for (uint32_t p = threadIdx.x; p < m; p += NT) {
+        if (nw && in_ranges(wr, nw, p)) continue;  // a head of its own (one-record group), not written
         const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
         uint32_t np = gs;
         for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
@@ -3165,14 +3181,16 @@ constexpr uint32_t WAVE_SORT_MAX = WAVE_SORT_LIMIT;
 template <int NT, int CAP>
 struct ChunkSmem {
     static constexpr uint32_t MAXB = CAP / (RANK_MAX_RUN + 1) + 1;  // runs above RANK_MAX_RUN
+    static constexpr uint32_t MAXW = CAP / (WAVE_SORT_MAX + 1) + 1;  // runs above WAVE_SORT_MAX
     unsigned long long k0[CAP];
     unsigned long long k1[CAP];
     uint32_t aux[CAP];
     uint32_t big[MAXB];  // lo | hi << 16
+    uint32_t wr[MAXW];   // lo | hi << 16: bins left to chunk_sort_mid
     uint32_t u32[NT / 64 + 1];
     uint64_t mins[NT / 64];
     uint16_t tcnt[NT / 64 * 16];  // tag_sort_block: per-wave digit counts, then their scan
-    uint32_t nbig, wide, bad;
+    uint32_t nbig, nwide, bad;
 };
 
 // Single-mass bins -- equal-mass spikes, every record of the bin with the same
@@ -3263,11 +3281,12 @@ __device__ bool tag_sort_block(unsigned long long* k0, unsigned long long* k1, u
 }
 
 // The chunk in[0, m) -> out[0, m) in final order with head flags; *heads =
-// this thread's unique heads.  BLOCK off: a chunk with a run above
-// WAVE_SORT_MAX is left untouched and false returned (block-uniform) -- the
-// list kernel with the block-level sort takes it.
+// this thread's unique heads.  BLOCK off: the bins above WAVE_SORT_MAX are
+// left out (not written, not counted) and listed in sm.wr[0, sm.nwide) for
+// chunk_sort_mid, which sorts each of them on its own (round 3 listed the
+// whole chunk, and the mid kernel loaded and ranked it all again).
 template <int NT, int CAP, bool BLOCK>
-__device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const BinMap& bm,
+__device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const BinMap& bm,
                            const RecLoc& rl, ChunkSmem<NT, CAP>& sm, uint32_t* heads_out) {
     static_assert(CAP <= 65535, "16-bit positions");
     constexpr uint32_t NW = NT / 64;
@@ -3277,7 +3296,7 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
     unsigned long long* k1 = sm.k1;
     if (threadIdx.x == 0) {
         sm.nbig = 0;
-        sm.wide = 0;
+        sm.nwide = 0;
     }
     {
         // all loads in flight before the first use (a Rec as 4 dwords: q0, q1)
@@ -3332,14 +3351,13 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) {
             if ((heads & (1u << k)) && rhi[k] - rlo[k] > RANK_MAX_RUN) {
-                sm.big[atomicAdd(&sm.nbig, 1u)] = rlo[k] | (rhi[k] << 16);
-                if (rhi[k] - rlo[k] > WAVE_SORT_MAX) sm.wide = 1;
+                if (!BLOCK && rhi[k] - rlo[k] > WAVE_SORT_MAX) sm.wr[atomicAdd(&sm.nwide, 1u)] = rlo[k] | (rhi[k] << 16);
+                else sm.big[atomicAdd(&sm.nbig, 1u)] = rlo[k] | (rhi[k] << 16);
             }
             if (lo0 + k < m) sm.aux[lo0 + k] = rlo[k] | (rhi[k] << 16);
         }
     }
     __syncthreads();
-    if (!BLOCK && sm.wide) return false;
     // small bins: rank inside the bin (k-major: a wave's lanes share bins), kept in registers with the key
     // (ranking by a 64-bit compact key instead measured slower: the extra
     // barriers and the order check cost more than the cheaper compares save)
@@ -3400,99 +3418,7 @@ __device__ bool sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         }
         __syncthreads();
     }
-    *heads_out = finish_sorted<NT>(out, m, rl, k0, k1, sm.aux, sm.u32, &sm.bad);
-    return true;
-}
-
-// One block per chunk.  A chunk above CAP goes to big_list, one with a bin
-// above WAVE_SORT_MAX to mid_list (both sorted by k_chunk_sort_list).  LDS
-// 39 KiB at CAP 1984 and no block-level sort here: <= 64 VGPRs, 4 blocks per CU.
-template <int NT, int CAP>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
-k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
-             const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
-             uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, Counters* __restrict__ ctr) {
-    __shared__ ChunkSmem<NT, CAP> sm;
-    const uint32_t c = 2 * blockIdx.x;  // chunk pair (k_chunk_bounds): this block sorts chunk c
-    const uint32_t a = chunk_lo[c];
-    const uint32_t m = chunk_lo[c + 1] - a;
-    if (threadIdx.x == 0) {  // chunk c+1: empty, or one big bin for the list kernels
-        const uint32_t mb = chunk_lo[c + 2] - chunk_lo[c + 1];
-        if (mb == 0) ucount[c + 1] = 0;
-        else if (mb > (uint32_t)CAP) big_list[atomicAdd(&ctr->n_big, 1u)] = c + 1;
-        else mid_list[atomicAdd(&ctr->n_mid, 1u)] = c + 1;
-    }
-    if (m == 0) {
-        if (threadIdx.x == 0) ucount[c] = 0;
-        return;
-    }
-    if (m > (uint32_t)CAP) {
-        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
-        return;
-    }
-    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
-    uint32_t h = 0;
-    if (!sort_chunk<NT, CAP, false>(in + a, out + a, m, bm, rl, sm, &h)) {
-        if (threadIdx.x == 0) mid_list[atomicAdd(&ctr->n_mid, 1u)] = c;
-        return;
-    }
-    const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
-    if (threadIdx.x == 0) ucount[c] = tot;
-}
-
-// The chunks k_chunk_sort listed: BIG off = mid_list (a bin above
-// WAVE_SORT_MAX: the block-level compact sort), BIG on = big_list (chunks of
-// (CHUNK_CAP, BIG_CAP] records, 1024 threads, 155 KiB LDS, one block per CU;
-// above split_above they go on to the giant path).  One block per listed
-// chunk, blocks past the list exit (a grid-stride loop around sort_chunk
-// doubled its registers).
-template <int NT, int CAP, bool BIG>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BIG ? 4 : DBI_MID_WPE, 8)))
-k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
-                  const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
-                  const uint32_t* __restrict__ list, uint32_t* __restrict__ giant_list, uint32_t split_above,
-                  Counters* __restrict__ ctr) {
-    __shared__ ChunkSmem<NT, CAP> sm;
-    const uint32_t n = BIG ? ctr->n_big : ctr->n_mid;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x) atomicOr(&ctr->err, ERR_GRID);
-    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
-    const uint32_t j = blockIdx.x;
-    if (j < n) {
-        const uint32_t c = list[j];
-        const uint32_t a = chunk_lo[c];
-        const uint32_t m = chunk_lo[c + 1] - a;
-        if (BIG && m > split_above && giant_list) {
-            if (threadIdx.x == 0) {
-                giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
-                atomicAdd(&ctr->n_giant_recs, (unsigned long long)m);
-            }
-        } else if (BIG && m > split_above) {
-            // no giant pass this build (none last time): through unsorted, redone (ERR_GRID)
-            for (uint32_t i = threadIdx.x; i < m; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
-            if (threadIdx.x == 0) {
-                ucount[c] = 0;
-                atomicOr(&ctr->err, ERR_GRID);
-            }
-        } else {
-            uint32_t h = 0;
-            sort_chunk<NT, CAP, true>(in + a, out + a, m, bm, rl, sm, &h);
-            const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
-            if (threadIdx.x == 0) {
-                ucount[c] = tot;
-                atomicAdd(BIG ? &ctr->n_big_recs : &ctr->n_mid_recs, (unsigned long long)m);
-            }
-        }
-    }
-    // entries past the grid (ERR_GRID: the build is redone with full grids):
-    // their records go to `out` unsorted and without unique heads, so the rest
-    // of this build stays inside its buffers
-    for (uint32_t e = j + gridDim.x; e < n; e += gridDim.x) {
-        const uint32_t c = list[e];
-        const uint32_t a = chunk_lo[c];
-        const uint32_t m = chunk_lo[c + 1] - a;
-        for (uint32_t i = threadIdx.x; i < m; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
-        if (threadIdx.x == 0) ucount[c] = 0;
-    }
+    *heads_out = finish_sorted<NT>(out, m, rl, k0, k1, sm.aux, sm.u32, &sm.bad, sm.wr, BLOCK ? 0u : sm.nwide);
 }
 
 // One chunk of m <= CAP records sorted in LDS by the record key with the flip
@@ -3517,6 +3443,143 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
     return finish_sorted<NT>(out, m, rl, k0, k1, aux, s_u32, s_bad);
 }
 
+// One block per chunk.  A chunk above CAP goes to big_list (k_chunk_sort_list);
+// every bin above WAVE_SORT_MAX -- a wide bin inside the chunk, or the
+// straddling bin that is chunk c+1 -- to mid_list as (chunk, lo | hi << 16),
+// sorted by k_bin_sort_mid, which adds its heads to ucount[chunk].  LDS
+// 39 KiB at CAP 1984 and no block-level sort here: <= 64 VGPRs, 4 blocks per CU.
+template <int NT, int CAP>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
+             const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
+             uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, Counters* __restrict__ ctr) {
+    __shared__ ChunkSmem<NT, CAP> sm;
+    const uint32_t c = 2 * blockIdx.x;  // chunk pair (k_chunk_bounds): this block sorts chunk c
+    const uint32_t a = chunk_lo[c];
+    const uint32_t m = chunk_lo[c + 1] - a;
+    if (threadIdx.x == 0) {  // chunk c+1: empty, or one big bin for the list kernels
+        const uint32_t mb = chunk_lo[c + 2] - chunk_lo[c + 1];
+        if (mb == 0) ucount[c + 1] = 0;
+        else if (mb > (uint32_t)CAP) big_list[atomicAdd(&ctr->n_big, 1u)] = c + 1;
+        else {
+            ucount[c + 1] = 0;  // k_bin_sort_mid adds the bin's heads
+            const uint32_t e = atomicAdd(&ctr->n_mid, 1u);
+            mid_list[2 * e] = c + 1;
+            mid_list[2 * e + 1] = mb << 16;
+        }
+    }
+    if (m == 0) {
+        if (threadIdx.x == 0) ucount[c] = 0;
+        return;
+    }
+    if (m > (uint32_t)CAP) {
+        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
+        return;
+    }
+    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
+    uint32_t h = 0;
+    sort_chunk<NT, CAP, false>(in + a, out + a, m, bm, rl, sm, &h);
+    const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
+    if (threadIdx.x == 0) ucount[c] = tot;  // block_sum's barrier: before k_bin_sort_mid's adds (stream order)
+    if (threadIdx.x < sm.nwide) {
+        const uint32_t e = atomicAdd(&ctr->n_mid, 1u);
+        mid_list[2 * e] = c;
+        mid_list[2 * e + 1] = sm.wr[threadIdx.x];
+    }
+}
+
+// The big_list chunks k_chunk_sort listed: (CHUNK_CAP, BIG_CAP] records, 1024
+// threads, 155 KiB LDS, one block per CU; above split_above they go on to the
+// giant path.  One block per listed chunk, blocks past the list exit (a
+// grid-stride loop around sort_chunk doubled its registers).
+template <int NT, int CAP>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
+                  const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
+                  const uint32_t* __restrict__ list, uint32_t* __restrict__ giant_list, uint32_t split_above,
+                  Counters* __restrict__ ctr) {
+    __shared__ ChunkSmem<NT, CAP> sm;
+    const uint32_t n = ctr->n_big;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x) atomicOr(&ctr->err, ERR_GRID);
+    const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
+    const uint32_t j = blockIdx.x;
+    if (j < n) {
+        const uint32_t c = list[j];
+        const uint32_t a = chunk_lo[c];
+        const uint32_t m = chunk_lo[c + 1] - a;
+        if (m > split_above && giant_list) {
+            if (threadIdx.x == 0) {
+                giant_list[atomicAdd(&ctr->n_giant, 1u)] = c;
+                atomicAdd(&ctr->n_giant_recs, (unsigned long long)m);
+            }
+        } else if (m > split_above) {
+            // no giant pass this build (none last time): through unsorted, redone (ERR_GRID)
+            for (uint32_t i = threadIdx.x; i < m; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
+            if (threadIdx.x == 0) {
+                ucount[c] = 0;
+                atomicOr(&ctr->err, ERR_GRID);
+            }
+        } else {
+            uint32_t h = 0;
+            sort_chunk<NT, CAP, true>(in + a, out + a, m, bm, rl, sm, &h);
+            const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
+            if (threadIdx.x == 0) {
+                ucount[c] = tot;
+                atomicAdd(&ctr->n_big_recs, (unsigned long long)m);
+            }
+        }
+    }
+    // entries past the grid (ERR_GRID: the build is redone with full grids):
+    // their records go to `out` unsorted and without unique heads, so the rest
+    // of this build stays inside its buffers
+    for (uint32_t e = j + gridDim.x; e < n; e += gridDim.x) {
+        const uint32_t c = list[e];
+        const uint32_t a = chunk_lo[c];
+        const uint32_t m = chunk_lo[c + 1] - a;
+        for (uint32_t i = threadIdx.x; i < m; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
+        if (threadIdx.x == 0) ucount[c] = 0;
+    }
+}
+
+// The mid_list bins: one fine bin of (WAVE_SORT_MAX, CHUNK_CAP] records per
+// entry (chunk, lo | hi << 16), one block each: loaded alone, sorted as one
+// run (tag counting sort for a single-mass bin, else the block-level compact
+// sort), heads added to ucount[chunk].  No run detection, no small-bin pass:
+// the chunk's other records were finished by k_chunk_sort.
+template <int NT, int CAP>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DBI_MID_WPE, 8)))
+k_bin_sort_mid(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
+               const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
+               const uint32_t* __restrict__ list, Counters* __restrict__ ctr) {
+    __shared__ unsigned long long k0[CAP];
+    __shared__ unsigned long long k1[CAP];
+    __shared__ uint32_t aux[CAP];
+    __shared__ uint32_t s_u32[NT / 64 + 1];
+    __shared__ uint64_t s_min[NT / 64];
+    __shared__ uint16_t s_tcnt[NT / 64 * 16];
+    __shared__ uint32_t s_bad;
+    const uint32_t n = ctr->n_mid;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x) atomicOr(&ctr->err, ERR_GRID);
+    const uint32_t j = blockIdx.x;
+    if (j < n) {
+        const uint32_t c = list[2 * j], r = list[2 * j + 1];
+        const uint32_t a = chunk_lo[c] + (r & 0xFFFFu), L = (r >> 16) - (r & 0xFFFFu);
+        const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
+        const uint32_t h = bitonic_chunk<NT, CAP>(in + a, out + a, L, rl, k0, k1, aux, s_u32, &s_bad, s_min, s_tcnt);
+        const uint32_t tot = block_sum<NT, uint32_t>(h, s_u32);
+        if (threadIdx.x == 0) {
+            atomicAdd(&ucount[c], tot);
+            atomicAdd(&ctr->n_mid_recs, (unsigned long long)L);
+        }
+    }
+    // entries past the grid (ERR_GRID, redone): the bin unsorted, no heads
+    for (uint32_t e = j + gridDim.x; e < n; e += gridDim.x) {
+        const uint32_t c = list[2 * e], r = list[2 * e + 1];
+        const uint32_t a = chunk_lo[c] + (r & 0xFFFFu), L = (r >> 16) - (r & 0xFFFFu);
+        for (uint32_t i = threadIdx.x; i < L; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
+    }
+}
+
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                              uint32_t* d_big_list, uint32_t* d_mid_list, Counters* d_ctr, hipStream_t s) {
@@ -3530,8 +3593,9 @@ hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, 
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_mid_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s) {
     if (max_blocks == 0) return hipSuccess;
-    DBI_LAUNCH((k_chunk_sort_list<CHUNK_THREADS, CHUNK_CAP, false>), dim3(max_blocks), dim3(CHUNK_THREADS), 0, s,
-               d_in, d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_mid_list, nullptr, 0u, d_ctr);
+    (void)bm;
+    DBI_LAUNCH((k_bin_sort_mid<CHUNK_THREADS, CHUNK_CAP>), dim3(max_blocks), dim3(CHUNK_THREADS), 0, s, d_in, d_out,
+               d_chunk_lo, d_res, d_poff, d_ucount, d_mid_list, d_ctr);
     return hipGetLastError();
 }
 
@@ -3540,7 +3604,7 @@ hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, 
                                  const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
                                  uint32_t split_above, Counters* d_ctr, hipStream_t s) {
     if (max_blocks == 0) return hipSuccess;
-    DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS, BIG_CAP, true>), dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in,
+    DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS, BIG_CAP>), dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in,
                d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list,
                std::min<uint32_t>(split_above, (uint32_t)BIG_CAP), d_ctr);
     return hipGetLastError();

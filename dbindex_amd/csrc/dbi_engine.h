@@ -50,8 +50,11 @@ struct DevBuf {
         const hipError_t e = hipMemsetAsync(p, 0, cap * sizeof(T), s);
         return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
     }
-    void release() {
-        if (p) (void)hipFree(p);
+    void release() {  // (a freed pointer in a captured graph: the graph is stale too)
+        if (p) {
+            g_alloc_gen.fetch_add(1, std::memory_order_relaxed);
+            (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
     }

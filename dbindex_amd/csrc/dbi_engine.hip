@@ -156,7 +156,7 @@ int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse, int pass
     if ((rc = h->scan_tmp.ensure(std::max<size_t>(scan_need, h->scan_tmp.cap)))) return rc;
     if ((rc = h->recB.ensure(n)) || (rc = h->hist.ensure(hist_elems)) ||
         (rc = h->ucount.ensure(2 * (size_t)nchunks)) || (rc = h->chunk_lo.ensure(2 * (size_t)nchunks + 1)) ||
-        (rc = h->big_list.ensure(2 * (size_t)nchunks)) || (rc = h->mid_list.ensure(2 * (size_t)nchunks)) ||
+        (rc = h->big_list.ensure(2 * (size_t)nchunks)) || (rc = h->mid_list.ensure(2 * MID_PER_PAIR * (size_t)nchunks)) ||
         (rc = h->giant_list.ensure(2 * (size_t)nchunks)) || (rc = h->segs.ensure((GIANT_PASSES + 4) * seg_cap)) ||
         (rc = h->ws_key.ensure(4 * n)) || (rc = h->ws_k2.ensure(4 * n)) ||
         (rc = h->umass.ensure(n)) || (rc = h->upid.ensure(n)) || (rc = h->uoff.ensure(n)) ||
@@ -229,13 +229,13 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                             h->mid_list.p, h->ctr.p, s));
-    // one block per listed chunk: at most one chunk per bin above the wave
-    // sort's reach (the lists are filled on the device).  A device-sized tail
+    // one block per listed bin (mid: every bin above the wave sort's reach) or
+    // chunk (big: above CHUNK_CAP); the lists are filled on the device.  A device-sized tail
     // launches the previous build's list lengths plus a margin instead (a grid
     // of every possible entry spent most of these launches dispatching blocks
     // with nothing to do, the big tier's at one 155-KiB block per CU at a
     // time); a longer list sets ERR_GRID and the build is redone with full grids.
-    uint32_t max_mid = (uint32_t)std::min<uint64_t>(2 * (uint64_t)nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
+    uint32_t max_mid = (uint32_t)std::min<uint64_t>(MID_PER_PAIR * (uint64_t)nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
     uint32_t max_big = (uint32_t)std::min<uint64_t>(2 * (uint64_t)nchunks, n / (CHUNK_CAP + 1) + 1);
     est = est || d_n;
     // (a list that was empty last time is not launched at all: ~4 us of an

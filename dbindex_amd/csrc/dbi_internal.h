@@ -199,6 +199,9 @@ constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-so
 #define DBI_WAVE_SORT_LIMIT 512
 #endif
 constexpr int WAVE_SORT_LIMIT = DBI_WAVE_SORT_LIMIT;  // bins up to this size: one wave in k_chunk_sort (more: chunk_sort_mid)
+// chunk_sort_mid entries (single bins above WAVE_SORT_LIMIT) per chunk pair: the
+// wide bins of a chunk of <= CHUNK_CAP records plus the pair's straddling bin
+constexpr uint32_t MID_PER_PAIR = CHUNK_CAP / (WAVE_SORT_LIMIT + 1) + 1;
 constexpr int BIG_THREADS = 1024;
 constexpr int BIG_CAP = 7936;       // records per oversize chunk sorted in LDS (1 block per CU)
 

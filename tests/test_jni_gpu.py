@@ -152,6 +152,8 @@ def test_jni_allocation_failures(jvm):
         m = float(oix.unique()["mass"][oix.n_unique // 2])
         want = expected(oix, seqs, oix.query(m, 0.5))
         assert len(want) > 0
+        same(st.seq_list(st.getSequences(m, 0.5)), want, "before the failures")
+        clean(jvm)
         for k in range(9):
             jvm.fail_alloc_at(k)
             with pytest.raises(JavaException) as ei:

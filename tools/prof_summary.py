@@ -41,8 +41,9 @@ STAGES = [
     ("dbi::k_chunk_bounds", "chunk_bounds"),
     ("void dbi::k_chunk_sort<", "chunk_sort"),
     ("dbi::k_chunk_sort_big", "chunk_sort_big"),
-    ("void dbi::k_chunk_sort_list<512, 1984, false>", "chunk_sort_mid"),
-    ("void dbi::k_chunk_sort_list<1024, 7936, true>", "chunk_sort_big"),
+    ("void dbi::k_bin_sort_mid<", "chunk_sort_mid"),
+    ("void dbi::k_chunk_sort_list<512, 1984, false>", "chunk_sort_mid"),  # rounds 2-3
+    ("void dbi::k_chunk_sort_list<1024, 7936", "chunk_sort_big"),
     ("dbi::k_big_chunks", "chunk_sort_giant"),
     ("dbi::k_finalize", "finalize"),
     ("dbi::k_key_flags", "key_flags"),
