@@ -3285,9 +3285,11 @@ __device__ bool tag_sort_block(unsigned long long* k0, unsigned long long* k1, u
 // left out (not written, not counted) and listed in sm.wr[0, sm.nwide) for
 // chunk_sort_mid, which sorts each of them on its own (round 3 listed the
 // whole chunk, and the mid kernel loaded and ranked it all again).
+// ties: records may repeat exactly (host occurrences); ranks count equal keys
+// before the record too, so two copies never take one slot.
 template <int NT, int CAP, bool BLOCK>
 __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const BinMap& bm,
-                           const RecLoc& rl, ChunkSmem<NT, CAP>& sm, uint32_t* heads_out) {
+                           const RecLoc& rl, ChunkSmem<NT, CAP>& sm, uint32_t* heads_out, bool ties) {
     static_assert(CAP <= 65535, "16-bit positions");
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t E = (CAP + NT - 1) / NT;  // records per thread (contiguous) in the run pass
@@ -3373,7 +3375,12 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
             if (i < m && bhi - blo <= RANK_MAX_RUN) {
                 const unsigned long long a0 = k0[i], a1 = k1[i];
                 uint32_t rank = 0;
-                for (uint32_t j = blo; j < bhi; ++j) rank += key_lt(k0[j], k1[j], a0, a1);
+                if (!ties) {
+                    for (uint32_t j = blo; j < bhi; ++j) rank += key_lt(k0[j], k1[j], a0, a1);
+                } else {
+                    for (uint32_t j = blo; j < bhi; ++j)
+                        rank += key_lt(k0[j], k1[j], a0, a1) | ((j < i) & (k0[j] == a0) & (k1[j] == a1));
+                }
                 v0[k] = a0;
                 v1[k] = a1;
                 dst[k] = blo + rank;
@@ -3452,7 +3459,8 @@ template <int NT, int CAP>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
              const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
-             uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, Counters* __restrict__ ctr) {
+             uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, uint32_t ties,
+             Counters* __restrict__ ctr) {
     __shared__ ChunkSmem<NT, CAP> sm;
     const uint32_t c = 2 * blockIdx.x;  // chunk pair (k_chunk_bounds): this block sorts chunk c
     const uint32_t a = chunk_lo[c];
@@ -3478,7 +3486,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
     }
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     uint32_t h = 0;
-    sort_chunk<NT, CAP, false>(in + a, out + a, m, bm, rl, sm, &h);
+    sort_chunk<NT, CAP, false>(in + a, out + a, m, bm, rl, sm, &h, ties != 0);
     const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
     if (threadIdx.x == 0) ucount[c] = tot;  // block_sum's barrier: before k_bin_sort_mid's adds (stream order)
     if (threadIdx.x < sm.nwide) {
@@ -3497,7 +3505,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
                   const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
                   const uint32_t* __restrict__ list, uint32_t* __restrict__ giant_list, uint32_t split_above,
-                  Counters* __restrict__ ctr) {
+                  uint32_t ties, Counters* __restrict__ ctr) {
     __shared__ ChunkSmem<NT, CAP> sm;
     const uint32_t n = ctr->n_big;
     if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x) atomicOr(&ctr->err, ERR_GRID);
@@ -3521,7 +3529,7 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
             }
         } else {
             uint32_t h = 0;
-            sort_chunk<NT, CAP, true>(in + a, out + a, m, bm, rl, sm, &h);
+            sort_chunk<NT, CAP, true>(in + a, out + a, m, bm, rl, sm, &h, ties != 0);
             const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
             if (threadIdx.x == 0) {
                 ucount[c] = tot;
@@ -3582,10 +3590,10 @@ k_bin_sort_mid(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t
 
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
-                             uint32_t* d_big_list, uint32_t* d_mid_list, Counters* d_ctr, hipStream_t s) {
+                             uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
-                       d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, d_ctr);
+                       d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr);
     return hipGetLastError();
 }
 
@@ -3602,11 +3610,11 @@ hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, 
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
-                                 uint32_t split_above, Counters* d_ctr, hipStream_t s) {
+                                 uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s) {
     if (max_blocks == 0) return hipSuccess;
     DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS, BIG_CAP>), dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in,
                d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list,
-               std::min<uint32_t>(split_above, (uint32_t)BIG_CAP), d_ctr);
+               std::min<uint32_t>(split_above, (uint32_t)BIG_CAP), ties ? 1u : 0u, d_ctr);
     return hipGetLastError();
 }
 

@@ -175,6 +175,9 @@ struct dbi_handle {
     uint64_t last_kept = 0;             // the previous build's records (bins of a device-sized tail)
     uint32_t grid_mid = 0, grid_big = 0;  // list-kernel grids of a device-sized tail, from the previous build (0: one block per possible entry; GRID_NONE: that list was empty, the kernel is not launched)
     bool skip_mid = false, skip_big = false;  // the last tail did not launch that list kernel (GRID_NONE)
+    // records of this build may repeat exactly (the addSequence flow: the same occurrence added
+    // twice, DBIndexStoreSQLiteMult.java:521-523): the chunk sort's ranks break ties by position
+    bool exact_dups = false;
     bool lists_short = false;             // the last tail's chunk lists outgrew their grids (set by finish_build)
     bool giants_seen = true;              // the previous build had giant chunks (or none yet): run the giant pass
     DevBuf<double> q_mass, q_tol;

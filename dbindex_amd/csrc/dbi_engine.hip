@@ -228,7 +228,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
           launch_chunk_bounds(src, n32, bm, T, nchunks, h->chunk_lo.p, s, d_n));
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                            h->mid_list.p, h->ctr.p, s));
+                            h->mid_list.p, h->exact_dups, h->ctr.p, s));
     // one block per listed bin (mid: every bin above the wave sort's reach) or
     // chunk (big: above CHUNK_CAP); the lists are filled on the device.  A device-sized tail
     // launches the previous build's list lengths plus a margin instead (a grid
@@ -252,7 +252,8 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
                                 max_mid, h->ctr.p, s));
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
           launch_chunk_sort_big(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                                giants ? h->giant_list.p : nullptr, max_big, h->split_above, h->ctr.p, s));
+                                giants ? h->giant_list.p : nullptr, max_big, h->split_above, h->exact_dups, h->ctr.p,
+                                s));
     if (giants)
         STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
               launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,
@@ -603,6 +604,7 @@ int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
     h->n_res = n_res;
     h->n_prot = n_prot;
     h->n_total_extra = 0;
+    h->exact_dups = false;
     std::memset(&h->stats, 0, sizeof(h->stats));
     h->nstage = 0;
     h->hc_final = false;
@@ -1076,6 +1078,7 @@ int dbi_build_occurrences(dbi_handle* h, const uint8_t* residues, uint64_t n_res
         if (i == 0 || mass[i] > hi) hi = mass[i];
     }
     if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    h->exact_dups = true;
     if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
     if ((rc = h->o_mass.ensure(n_occ)) || (rc = h->o_pid.ensure(n_occ)) || (rc = h->o_off.ensure(n_occ)) ||
         (rc = h->o_len.ensure(n_occ)) || (rc = h->recA.ensure(n_occ)))

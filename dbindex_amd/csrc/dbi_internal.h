@@ -360,14 +360,14 @@ hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, 
                                uint32_t* d_chunk_lo, hipStream_t s, const unsigned long long* d_n = nullptr);
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
-                             uint32_t* d_big_list, uint32_t* d_mid_list, Counters* d_ctr, hipStream_t s);
+                             uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s);
 hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_mid_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s);
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
-                                 uint32_t split_above, Counters* d_ctr, hipStream_t s);
+                                 uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s);
 // chunks above BIG_CAP listed in d_giant_list: MSD split on the (mass, tag)
 // key into leaves sorted in LDS; a segment of one (mass, tag) key above
 // BIG_CAP falls back to global-memory scratch (ws_key / ws_k2).  segs: 5 lists

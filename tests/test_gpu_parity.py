@@ -375,6 +375,22 @@ def test_tag_collisions(Engine, copies):
     _check(Engine, DBIndexSearchParams.trypsin(2), pp, f"collisions mc2 x{copies}", nq=500)
 
 
+@pytest.mark.parametrize("spikes", [(("GGGAAAGGGAK", 600),),
+                                    (("GGGAAAGGGAK", 520), ("GGGAAAGGGSK", 530), ("GGGAAAGGGTK", 700))])
+def test_tag_collisions_beside_wide_bins(Engine, spikes):
+    """A chunk that holds tag-collision groups (regrouped by string in
+    k_chunk_sort) AND bins above 512 records, which k_chunk_sort leaves out
+    for k_bin_sort_mid (round 4): the left-out ranges must be neither written
+    nor counted by the collision path, and their heads come back through the
+    mid kernel's add to the chunk's unique count."""
+    seqs = list(tag_collision_proteins())
+    for pep, n in spikes:  # one tryptic peptide per protein: n identical records
+        seqs += [pep] * n
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    _check(Engine, DBIndexSearchParams.trypsin(0), pp, f"collisions + wide bins {spikes}", nq=300)
+    _check(Engine, DBIndexSearchParams.trypsin(2), pp, f"collisions + wide bins mc2 {spikes}", nq=300)
+
+
 def test_thresholds_on_exact_peptide_masses(Engine):
     """minMH / maxMH set exactly to indexed peptide masses: inclusive bounds
     (DBIndexer.java:284,331) decided on the bit-exact sequential sum, also in

@@ -144,6 +144,7 @@ def test_jni_allocation_failures(jvm):
     oix = cref.Index(cp, pp.residues, pp.offsets)
     st = JniStore(jvm, cp)
     try:
+        st.setDeviceDigest(True)  # DBIndexerHip's flow (DBIndexerHip.java:38)
         st.init("oom.fasta")
         st.startAddSeq()
         for i, s in enumerate(seqs):
