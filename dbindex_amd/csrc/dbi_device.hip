@@ -1279,6 +1279,102 @@ __device__ __forceinline__ uint32_t first_bit_128(uint64_t lo, uint64_t hi) {
 __device__ __forceinline__ uint64_t low_bits(uint32_t x) { return x >= 64 ? ~0ull : ((1ull << x) - 1ull); }
 
 // ---------------------------------------------------------------------------
+// Bounded semi-specific digest (no mandatory residues, no windows; warm
+// builds): one walk per start instead of the fused kernel's count walk +
+// look-back + emit walk.  Every start is a candidate (checkCleavage = N_ok ||
+// C_ok, DBIndexer.java:318), and a start's records are ends e, ascending, with
+//   s + MIN_PEP_LENGTH - 1 <= e < stop,  stop = the (maxMC+2)-th cleave residue
+//   from s (mc > maxMC from there on: every later cut breaks, :322-324, and no
+//   end after it emits) or the next protein's first residue (:284),
+// at every such position when N_ok(s) holds, else at the cuts only -- minus
+// the mass filters (minMH / maxMH / the bucket drop), which only remove
+// records.  So the bit maps bound a start's records before its walk; a start
+// whose stop lies past the 128-position horizon is counted by its exact walk
+// instead.  Tiles reserve the bound by one atomic add (any tile order: the
+// chunk sort restores first appearance, ck_fix_runs), each walk writes its
+// records into its slots, and the unused slots get REC_SENTINEL, which the
+// first radix pass drops -- as in k_digest_bounded.
+// ---------------------------------------------------------------------------
+template <bool DROP>
+__global__ void __launch_bounds__(DIGEST_THREADS)
+k_digest_semi_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
+                      const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
+                      uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, Rec* __restrict__ d_out, uint64_t cap,
+                      Counters* __restrict__ d_ctr) {
+    __shared__ DigestSmem sm;
+    __shared__ unsigned long long s_base;
+    TileCtx tc;
+    const uint32_t ncand = digest_prepare<true>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff,
+                                                n_prot, n_res, d_tile_pf, d_ctr);
+    uint32_t jb, je;
+    thread_share(ncand, jb, je);
+    const uint32_t kcl = (uint32_t)dp.max_missed + 2u;
+    const uint32_t a = dp.min_len > 0 ? (uint32_t)dp.min_len - 1u : 0u;  // first end, relative (:331)
+    const uint32_t known = tc.w_end == n_res ? tc.nbytes - 1u : tc.nbytes - 2u;  // last window position with its cut bit
+    // slot bounds (an open start: its exact count, the walk run twice)
+    uint32_t lim = 0;
+    for (uint32_t j = jb; j < je; ++j) {
+        const uint32_t i = sm.cand[j];
+        const uint32_t p = tc.t0 - tc.w0 + i;  // window position of the start
+        const uint64_t cl0 = bits_from(sm.clvm, p), cl1 = bits_from(sm.clvm, p + 64);
+        const uint64_t st0 = bits_from(sm.stm, p) & ~1ull, st1 = bits_from(sm.stm, p + 64);
+        const uint32_t stop = min(kth_bit_128(cl0, cl1, kcl), first_bit_128(st0, st1));
+        const uint32_t horizon = min(127u, known - p);
+        if (stop >= 128u || stop > horizon + 1u) {  // (128: no stop within the horizon)
+            lim += walk_candidate<false, true, false>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr).kept;
+        } else if (stop > a) {
+            if (n_ok_at(sm, tc, i)) {
+                lim += stop - a;
+            } else {
+                const uint64_t c0 = bits_from(sm.cutm, p), c1 = bits_from(sm.cutm, p + 64);
+                lim += (uint32_t)__popcll(c0 & low_bits(min(stop, 64u)) & ~low_bits(min(a, 64u))) +
+                       (uint32_t)__popcll(c1 & low_bits(stop > 64u ? stop - 64u : 0u) & ~low_bits(a > 64u ? a - 64u : 0u));
+            }
+        }
+    }
+    uint32_t tile_slots;
+    const uint32_t excl_t = block_excl_scan<DIGEST_THREADS, uint32_t>(lim, sm.tmp, tile_slots);
+    if (threadIdx.x == 0) s_base = atomicAdd(&d_ctr->n_slots, (unsigned long long)tile_slots);
+    __syncthreads();
+    const unsigned long long base = s_base;
+    if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
+    tc.w = rec_width(d_ctr->max_plen);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && !rec_layout_ok(tc.w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
+    Rec* __restrict__ o = d_out + base + excl_t;
+    uint32_t kept = 0, dropped = 0;
+    for (uint32_t j = jb; j < je; ++j) {
+        const WalkOut w = walk_candidate<true, true, false>(dp, sm, tc, d_res, d_poff, j, o + kept, o + lim);
+        kept += w.kept;
+        dropped += w.dropped;
+    }
+    if (kept > lim) atomicOr(&d_ctr->err, ERR_SLOTS);  // the bound is an upper bound: never
+    const Rec sent{REC_SENTINEL, REC_SENTINEL};
+    for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
+    const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
+    const uint32_t td = DROP ? block_sum<DIGEST_THREADS, uint32_t>(dropped, sm.tmp) : 0u;
+    if (threadIdx.x == 0) {
+        if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
+        if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
+    }
+}
+
+hipError_t launch_digest_semi_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                                      const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                                      const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr,
+                                      hipStream_t s) {
+    const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
+    if (nblk == 0) return hipSuccess;
+    if (!dp.semi || dp.mand_mode || dp.filter) return hipErrorInvalidValue;
+    if (dp.drop_mass <= dp.max_mh)
+        DBI_LAUNCH((k_digest_semi_bounded<true>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags,
+                   d_res, d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr);
+    else
+        DBI_LAUNCH((k_digest_semi_bounded<false>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags,
+                   d_res, d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Bounded digest (full enzyme, no mandatory residues, <= 2 missed cleavages;
 // warm builds): one walk per cleavage-site start, into slots reserved by a
 // decoupled look-back.  A full-enzyme walk emits only at cuts, and every
@@ -1361,7 +1457,10 @@ __device__ __forceinline__ LeanEnds lean_ends(const LeanSmem& sm, uint32_t p, ui
     const uint32_t stop = min(kth_bit_128(cl0, cl1, kcl), first_bit_128(st0, st1));
     LeanEnds e;
     e.horizon = min((uint32_t)LD_HORIZON - 1u, known - p);
-    e.open = stop > e.horizon + 1u;
+    // past the horizon: a stop beyond the window's known cut bits, or none
+    // within LD_HORIZON positions (kth / first_bit_128 return 128) -- a walk
+    // through residues light enough to stay <= maxMH over 128 positions
+    e.open = stop >= (uint32_t)LD_HORIZON || stop > e.horizon + 1u;
     const uint32_t a = min_len > 0 ? min_len - 1u : 0u;  // pepSize >= MIN_PEP_LENGTH (:331)
     const uint32_t b = min(stop, e.horizon + 1u);        // ends in [a, b)
     e.lo = bits_from(sm.cutm, p) & low_bits(min(b, 64u)) & ~low_bits(min(a, 64u));

@@ -268,6 +268,7 @@ struct dbi_handle {
     uint64_t dp_gen = 0;                  // bumped when dp changes (dbi_set_windows, bucket drop)
     bool use_graph = true;                // DBI_BUILD_GRAPH=0: never
     bool use_h1 = true;                   // DBI_DIGEST_HIST=0: the first radix histogram as its own kernel
+    bool use_semi_bounded = true;         // DBI_SEMI_BOUNDED=0: warm semi builds by the fused count + emit digest
     bool h1_on = false;                   // this warm build's digest counts the first radix histogram (h1plan)
     dbi::Hist1Plan h1plan{};
     bool capturing = false;               // stage events become event nodes

@@ -348,6 +348,16 @@ int prepare_tiles(dbi_handle* h) {
     return 0;
 }
 
+// Warm builds digest into bounded slots: the lean kernel (full enzyme, no
+// mandatory residues, <= 2 missed cleavages) or the semi-specific one (no
+// mandatory residues); both without the unindexed search's windows.
+bool lean_digest(const dbi_handle* h) {
+    return !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2 && !h->dp.filter;
+}
+bool bounded_digest(const dbi_handle* h) {
+    return lean_digest(h) || (h->dp.semi && !h->dp.mand_mode && !h->dp.filter && h->use_semi_bounded);
+}
+
 // Device digest over residues at d_res (n_res) with u32 offsets at h->d_poff.
 // Warm builds with dev_sized: the digest into the previous build's capacity,
 // and no host sync: *n = *n_in = that capacity (upper bounds), *dev_sized set;
@@ -364,7 +374,7 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
     uint64_t n;
     // full enzyme, no mandatory residues, <= 2 missed cleavages: one walk into
     // per-tile reservations of exactly each start's candidate ends
-    const bool bounded = !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2 && !h->dp.filter;
+    const bool lean = lean_digest(h), bounded = bounded_digest(h);
     if (h->recA.cap >= 1024) {
         // warm: one pass into the capacity of the previous build; the exact
         // need comes back with the counters, and a short buffer is grown and
@@ -377,7 +387,12 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
                 h->epoch = 1;
             }
             const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
-            if (bounded)
+            if (bounded && !lean)
+                STAGE(h, "digest", by(1, 16, 0, 4, 0),
+                      launch_digest_semi_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
+                                                 (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->recA.p, cap,
+                                                 h->ctr.p, s));
+            else if (bounded)
                 STAGE(h, "digest", by(1, 16, 0, 4, 0),
                       launch_digest_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
                                             (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->recA.p, cap, h->ctr.p,
@@ -475,9 +490,9 @@ int warm_body(dbi_handle* h, uint64_t* n_in, bool* sparse) {
     // tiles' flushes are ~200 global atomics each (SwissProt: 10 M, the digest
     // +0.1 ms against the 0.19 ms histogram kernel, measured: no gain).
     h->h1_on = false;
-    const bool bounded = !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2 && !h->dp.filter;
+    const bool lean = lean_digest(h);
     constexpr uint64_t H1_MAX_SLOTS = 16ull << 20;
-    if (bounded && h->use_h1 && std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull) <= H1_MAX_SLOTS) {
+    if (lean && h->use_h1 && std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull) <= H1_MAX_SLOTS) {
         const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
         const uint32_t nbins = choose_nbins(h->last_kept ? std::min<uint64_t>(h->last_kept, cap) : cap, h->bin_bits_max);
         int width[8] = {};
@@ -522,8 +537,7 @@ int build_digest(dbi_handle* h) {
         }
         // graphs for the bounded digest's builds, untimed or timing one stage
         // (every stage timed: events in the dispatch packets, no graph)
-        const bool bounded = !h->dp.semi && !h->dp.mand_mode && h->dp.max_missed <= 2 && !h->dp.filter &&
-                             !(h->timing && h->timing_only.empty());
+        const bool bounded = bounded_digest(h) && !(h->timing && h->timing_only.empty());
         const dbi_handle::GraphKey key = graph_key(h);
         if (bounded && h->use_graph && attempt == 0 && h->bgraph.exec && h->bgraph.key == key) {
             // replay the captured build; its host-side results come with it
@@ -965,6 +979,7 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     if (const char* ev = std::getenv("DBI_CHUNK_T")) h->chunk_t = (uint32_t)std::max(64, std::min(CHUNK_CAP, std::atoi(ev)));
     if (const char* ev = std::getenv("DBI_BUILD_GRAPH")) h->use_graph = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("DBI_DIGEST_HIST")) h->use_h1 = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("DBI_SEMI_BOUNDED")) h->use_semi_bounded = std::atoi(ev) != 0;
     auto fail = [&](int code) {
         dbi_close(h);
         return code;

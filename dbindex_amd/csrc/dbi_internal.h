@@ -245,6 +245,12 @@ hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, 
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                  const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s,
                                  const Hist1Plan* h1p = nullptr);
+// semi-specific enzymes (no mandatory residues, no windows): one walk per start
+// into slots bounded by the bit maps (REC_SENTINEL in the unused ones)
+hipError_t launch_digest_semi_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
+                                      const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
+                                      const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr,
+                                      hipStream_t s);
 // tail_in / tail_n of a device-sized build: the digest's slot and record
 // counts, or 0 / 0 when the slots needed exceed cap
 hipError_t launch_tail_counts(Counters* d_ctr, uint64_t cap, bool sparse, hipStream_t s);

@@ -83,10 +83,31 @@ def test_kat_proteins(Engine, name, prm):
         {"C": 57.02146, "M": 15.9949, "K": 229.162932}, nterm=229.162932), 1000),
     ("300_semi_n15", DBIndexSearchParams.semi_tryptic(1).with_static_mods({"C": 57.02146}, n15_enrichment=0.98),
      300),
+    # warm semi builds: the bounded semi digest (k_digest_semi_bounded), with the bucket drop too
+    ("1k_semi0", DBIndexSearchParams.semi_tryptic(0), 1000),
+    ("300_semi3", DBIndexSearchParams.semi_tryptic(3), 300),
+    ("300_semi_drop", DBIndexSearchParams.semi_tryptic(2, index_factor=7, max_precursor_mass=7999.0), 300),
 ])
 def test_synthetic(Engine, name, prm, nprot):
     pp = fasta.config("1k") if nprot == 1000 else fasta.config("1k").slice(0, nprot)
     _check(Engine, prm, pp, name)
+
+
+@pytest.mark.parametrize("prm", [DBIndexSearchParams.trypsin(2, max_precursor_mass=20000.0),
+                                 DBIndexSearchParams.trypsin(0, max_precursor_mass=20000.0),
+                                 DBIndexSearchParams.semi_tryptic(2, max_precursor_mass=20000.0)],
+                         ids=["tryp2", "tryp0", "semi2"])
+def test_long_light_walks(Engine, prm):
+    """Peptides longer than the bounded digests' 128-position horizon: runs of
+    glycine (57 Da) without K/R under a 20000-Da maxMH, so a walk finds no
+    stop within 128 positions and its mass is still below maxMH there -- it
+    goes on from HBM (walk_global) and its slot bound must cover the ends past
+    the horizon.  Mixed into the 1k proteome so the second build is warm."""
+    long = ["G" * 150 + "K" + "AAAAAAR", "M" + "G" * 140 + "R" + "GGGGGGGK", "GGGGGGK" + "G" * 200,
+            "A" * 129 + "KR" + "G" * 131, "PEPTIDEK" + "G" * 300 + "K"]
+    base = fasta.config("1k").slice(0, 300)
+    seqs = base.sequences()[:150] + long + base.sequences()[150:]
+    _check(Engine, prm, fasta.PackedProteins.from_sequences(seqs), "long light walks", nq=500)
 
 
 @pytest.mark.parametrize("layout", ["short", "empties", "mixed"])
