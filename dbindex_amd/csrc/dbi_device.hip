@@ -735,8 +735,14 @@ k_digest(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __r
 constexpr int64_t CUT_EPS_FX = 3;
 constexpr double CUT_SCALE = 512.0;
 
+// Stored with one pad word per 32 entries: the threads of a wave own
+// consecutive 16-start runs, so unpadded their reads p[ps + e] fell 16 words
+// apart -- two banks for 32 lanes (SQ: ~7 bank conflicts per LDS instruction
+// in the bucket count, 4.5 in the plain one).
 struct CutSmem {
-    uint32_t p[WIN];
+    uint32_t raw[WIN + WIN / 32 + 1];
+    __device__ __forceinline__ uint32_t& p(uint32_t i) { return raw[i + (i >> 5)]; }
+    __device__ __forceinline__ uint32_t p(uint32_t i) const { return raw[i + (i >> 5)]; }
 };
 
 // T of a limit X (clamped: an infinite or huge limit is never reached)
@@ -806,16 +812,16 @@ struct HistTrack {
 
 // first q in [t, hi + 1] with p[q] > a (p non-decreasing): gallop, then bisect
 __device__ __forceinline__ uint32_t prefix_seek(const CutSmem& cs, uint32_t t, uint32_t hi, int64_t a) {
-    if (t > hi || (int64_t)cs.p[t] > a) return t;
+    if (t > hi || (int64_t)cs.p(t) > a) return t;
     uint32_t lo = t, step = 1;  // p[lo] <= a
-    while (lo + step <= hi && (int64_t)cs.p[lo + step] <= a) {
+    while (lo + step <= hi && (int64_t)cs.p(lo + step) <= a) {
         lo += step;
         step <<= 1;
     }
     uint32_t up = min(lo + step, hi + 1);  // p[up] > a, or up = hi + 1
     while (up - lo > 1) {
         const uint32_t mid = (lo + up) >> 1;
-        if ((int64_t)cs.p[mid] > a) up = mid; else lo = mid;
+        if ((int64_t)cs.p(mid) > a) up = mid; else lo = mid;
     }
     return up;
 }
@@ -858,8 +864,8 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
         H = xk - 1;
         ends = true;
     }
-    const int64_t pb = ps > 0 ? (int64_t)cs.p[ps - 1] : 0;
-    auto D = [&](uint32_t e) -> int64_t { return (int64_t)cs.p[ps + e] - pb; };
+    const int64_t pb = ps > 0 ? (int64_t)cs.p(ps - 1) : 0;
+    auto D = [&](uint32_t e) -> int64_t { return (int64_t)cs.p(ps + e) - pb; };
     // last position with m <= maxMH (the walk stops past it: :284, :326)
     int Y;
     {
@@ -909,39 +915,66 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
     }
     if (HIST && n && fast) {
         // absolute window positions of the first / last end; end q is past
-        // boundary k when p[q] > pb + T_k (the first such q tracked per k)
+        // boundary k when p[q] > pb + T_k (the first such q tracked per k).
+        // u32 arithmetic (fast: 3 <= T_k < 2^31; a window's prefix + T_k < 2^32).  The
+        // tracked position moves ~one residue per start, so every boundary's
+        // next few prefixes are loaded together (p[q-1 .. q+2]: one LDS round
+        // trip for all boundaries instead of a chain of reads per boundary),
+        // and a search only when it moved further.
         const uint32_t qlo = ps + (uint32_t)lo, qhi = ps + (uint32_t)Y;
-        const int64_t dlo = D((uint32_t)lo), dhi = D((uint32_t)Y);
+        const uint32_t upb = (uint32_t)pb;
+        const uint32_t dlo = (uint32_t)D((uint32_t)lo), dhi = (uint32_t)D((uint32_t)Y);
         uint32_t pos[HIST_FAST_MAX];
+        uint32_t need = 0;  // bit k: boundary k falls among the ends (or too close to tell)
+#pragma unroll
+        for (int k = 0; k < HIST_FAST_MAX; ++k) {
+            pos[k] = qhi + 1u;  // every end below the boundary (k >= nb: unused)
+            if (k < dp.nb) {
+                const uint32_t t = (uint32_t)cl.t_b[k];
+                if (dhi + (uint32_t)CUT_EPS_FX <= t) {
+                    pos[k] = qhi + 1u;
+                } else if (dlo >= t + (uint32_t)CUT_EPS_FX) {
+                    pos[k] = qlo;  // every end past it
+                } else {
+                    uint32_t q = ht.t[k];
+                    if (q < qlo || q > qhi + 1u) q = qlo;  // first use, or left behind
+                    pos[k] = q;
+                    need |= 1u << k;
+                }
+            }
+        }
+        uint32_t v[HIST_FAST_MAX][4];  // p[q-1], p[q], p[q+1], p[q+2] (clamped into [qlo-1, qhi])
+#pragma unroll
+        for (int k = 0; k < HIST_FAST_MAX; ++k) {
+            if (need & (1u << k)) {
+                const uint32_t q = pos[k];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[k][i] = cs.p(max(min(q + (uint32_t)i, qhi + 1u), 1u) - 1u);
+            }
+        }
         bool bad = false;
 #pragma unroll
         for (int k = 0; k < HIST_FAST_MAX; ++k) {
-            pos[k] = qhi + 1u;
-            if (k < dp.nb) {
-                const int64_t t = cl.t_b[k];
-                const int chi = cut_cmp(dhi, t), clo = cut_cmp(dlo, t);
-                if (chi < 0) {
-                    pos[k] = qhi + 1u;  // every end below the boundary
-                } else if (clo > 0) {
-                    pos[k] = qlo;       // every end past it
+            if (need & (1u << k)) {
+                const uint32_t t = (uint32_t)cl.t_b[k], athr = upb + t;
+                uint32_t q = pos[k];
+                // first of q, q+1, q+2 (up to qhi) with p > athr: the prefixes ascend
+                const uint32_t a = (q <= qhi && v[k][1] <= athr ? 1u : 0u) + (q + 1u <= qhi && v[k][2] <= athr ? 1u : 0u) +
+                                   (q + 2u <= qhi && v[k][3] <= athr ? 1u : 0u);
+                uint32_t phi, plo;  // p[q'] (q' <= qhi) and p[q' - 1] (q' > qlo)
+                if (a == 3u && q + 3u <= qhi) {  // moved further: search (rare)
+                    q = prefix_seek(cs, q + 3u, qhi, (int64_t)athr);
+                    phi = q <= qhi ? cs.p(q) : 0u;
+                    plo = cs.p(q - 1u);
                 } else {
-                    const int64_t athr = pb + t;
-                    uint32_t q = ht.t[k];
-                    if (q < qlo || q > qhi + 1u) {  // first use, or left behind: search
-                        q = prefix_seek(cs, qlo, qhi, athr);
-                    } else {
-                        int steps = 0;  // usually one position per start
-                        while (q <= qhi && (int64_t)cs.p[q] <= athr && steps < 4) {
-                            ++q;
-                            ++steps;
-                        }
-                        if (q <= qhi && (int64_t)cs.p[q] <= athr) q = prefix_seek(cs, q, qhi, athr);
-                    }
-                    ht.t[k] = q;
-                    if (q <= qhi && cut_cmp((int64_t)cs.p[q] - pb, t) <= 0) bad = true;
-                    if (q > qlo && cut_cmp((int64_t)cs.p[q - 1] - pb, t) >= 0) bad = true;
-                    pos[k] = q;
+                    q += a;
+                    phi = a == 0u ? v[k][1] : a == 1u ? v[k][2] : v[k][3];
+                    plo = a == 0u ? v[k][0] : a == 1u ? v[k][1] : a == 2u ? v[k][2] : v[k][3];
                 }
+                ht.t[k] = q;
+                if (q <= qhi && phi - upb < t + (uint32_t)CUT_EPS_FX) bad = true;
+                if (q > qlo && plo - upb + (uint32_t)CUT_EPS_FX > t) bad = true;
+                pos[k] = q;
             }
         }
         if (bad) { r.exact = false; return r; }
@@ -1020,14 +1053,14 @@ __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nby
         const uint32_t i = lo + k;
         if (i < nbytes) {
             mrun += sm.mass[sm.win[i] & 0xFFu];
-            cs.p[i] = (uint32_t)__double2ull_rn(mrun * CUT_SCALE);
+            cs.p(i) = (uint32_t)__double2ull_rn(mrun * CUT_SCALE);
         }
     }
     __syncthreads();
 }
 
 template <bool HIST>
-__global__ void __launch_bounds__(DIGEST_THREADS)
+__global__ void __launch_bounds__(DIGEST_THREADS) __attribute__((amdgpu_waves_per_eu(HIST ? 4 : 1, 8)))
 k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                     const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
                     uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, uint32_t* __restrict__ d_blk,
@@ -1040,7 +1073,10 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     if (HIST)  // (digest_prepare's barriers come before the first count)
         for (uint32_t b = threadIdx.x; b <= (uint32_t)dp.nb; b += DIGEST_THREADS) s_hist[b] = 0;
     HistTrack ht;
-    const bool fast = HIST && dp.nb <= HIST_FAST_MAX;
+    const CutLimits cl = cut_limits(dp);
+    // (the tracked boundaries compare in u32: thresholds in [3, 2^31))
+    const bool fast = HIST && dp.nb <= HIST_FAST_MAX && cl.t_b[0] >= CUT_EPS_FX &&
+                      cut_threshold((double)(min(dp.nb, HIST_FAST_MAX) * dp.br), dp.m0) < (1ll << 31);
 #pragma unroll
     for (int k = 0; k < HIST_FAST_MAX; ++k) ht.t[k] = 0;
 #pragma unroll
@@ -1049,7 +1085,6 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     const uint32_t ncand = digest_prepare<false>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
                                                  d_tile_pf, d_ctr);
     build_cut_tables(sm, cs, tc.nbytes, s_dtmp);
-    const CutLimits cl = cut_limits(dp);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
     uint32_t kept = 0, dropped = 0;
