@@ -2426,22 +2426,22 @@ hipError_t launch_radix_scatter(const Rec* d_in, Rec* d_out, uint32_t n, const B
 // shard of the record's mass key, and the shard's first global protein id
 // folded into every record on the way out
 hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bool sparse, uint32_t* d_hist,
-                             hipStream_t s) {
-    return radix_hist(d_in, n, OwnerDigit{om}, owner_bits(om.nshards), sparse, d_hist, s);
+                             hipStream_t s, const unsigned long long* d_n) {
+    return radix_hist(d_in, n, OwnerDigit{om}, owner_bits(om.nshards), sparse, d_hist, s, d_n);
 }
 
 hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, const OwnerMap& om, bool sparse,
-                                const uint32_t* d_hist, hipStream_t s) {
+                                const uint32_t* d_hist, hipStream_t s, const unsigned long long* d_n) {
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
     const OwnerDigit dig{om};
     const int bits = owner_bits(om.nshards);
     if (sparse)
         DBI_LAUNCH((k_radix_scatter<true, OwnerDigit, true>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, (void*)d_out,
-                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u, (const unsigned long long*)nullptr);
+                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u, d_n);
     else
         DBI_LAUNCH((k_radix_scatter<false, OwnerDigit, true>), dim3(g), dim3(RADIX_THREADS), 0, s, d_in, (void*)d_out,
-                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u, (const unsigned long long*)nullptr);
+                   n, dig, bits, d_hist, (uint8_t*)nullptr, 0, 0u, d_n);
     return hipGetLastError();
 }
 
@@ -4461,14 +4461,19 @@ hipError_t launch_sample_masses(const Rec* d_recs, uint64_t n, uint32_t ns, doub
     return hipGetLastError();
 }
 
-__global__ void k_off_rebase(const uint64_t* __restrict__ in, uint64_t base, uint32_t* __restrict__ out, uint64_t n) {
+// clamped into [0, hi]: a device-sized shard digest rebases by the residue
+// range of the last build, which offsets rewritten since may leave (the build
+// is flagged and redone; meanwhile nothing reads outside the residues)
+__global__ void k_off_rebase(const uint64_t* __restrict__ in, uint64_t base, uint64_t hi, uint32_t* __restrict__ out,
+                             uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = (uint32_t)(in[i] - base);
+    if (i < n) out[i] = in[i] <= base ? 0u : (uint32_t)min(in[i] - base, hi);
 }
 
-hipError_t launch_off_rebase(const uint64_t* d_in, uint64_t base, uint32_t* d_out, uint64_t n, hipStream_t s) {
+hipError_t launch_off_rebase(const uint64_t* d_in, uint64_t base, uint64_t hi, uint32_t* d_out, uint64_t n,
+                             hipStream_t s) {
     if (n == 0) return hipSuccess;
-    DBI_LAUNCH(k_off_rebase, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, base, d_out, n);
+    DBI_LAUNCH(k_off_rebase, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, base, hi, d_out, n);
     return hipGetLastError();
 }
 

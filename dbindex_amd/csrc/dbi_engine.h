@@ -76,6 +76,7 @@ struct ShardState {
     const uint8_t* d_res_global = nullptr;  // every shard's residues (owner merge reads any peptide)
     uint64_t n_digest = 0, n_in = 0;        // digest records / slots in recA
     bool sparse = false;
+    bool dev = false;  // device-sized digest: n_digest / n_in are the capacity until the count-matrix sync
     uint64_t n_total = 0, n_dropped = 0;    // this shard's digest: totalSeqCount, bucket drops
     uint32_t width = 0;                     // global record field width W
     int32_t split[MAX_SHARDS - 1] = {};
@@ -219,6 +220,17 @@ struct dbi_handle {
         double prev_merge_ms = 0;
         uint64_t prev_recv = 0;
     } shard_warm;
+    // the shard the last dbi_build_sharded digested: a warm build of the same
+    // shard digests without a host round trip (residue range and record width
+    // from here; the device checks them against the offsets, k_shard_flags)
+    struct {
+        bool valid = false;
+        const void* d_res = nullptr;
+        const void* d_poff = nullptr;
+        uint64_t n_res = 0, n_prot = 0, p_begin = 0, p_end = 0;
+        uint64_t e0 = 0, e1 = 0;  // the shard's first / one-past-last residue
+        uint32_t width = 0;       // record field width W of the whole proteome
+    } shard_dev;
     hipEvent_t ev_merge[2] = {nullptr, nullptr};  // owner merge device time
     DevBuf<uint64_t> xsend, xrecv;      // sharded build: 8-B location words to / from the owners
     DevBuf<double> samp;                // sharded build: mass samples (splitters)
@@ -381,5 +393,6 @@ dbi_handle::GraphKey graph_key(const dbi_handle* h);
 uint32_t choose_nbins(uint64_t n, int max_bits);  // fine mass bins of a tail over n records
 int radix_plan(uint32_t nbins, bool sparse, int* width);  // LSD digit widths; returns the passes
 int finish_build(dbi_handle* h);
+bool bounded_digest(const dbi_handle* h);  // a warm build digests into bounded slots (device-sized)
 
 }  // namespace dbi

@@ -314,12 +314,13 @@ hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint
                                 const unsigned long long* d_n = nullptr);
 uint64_t radix_blocks(uint32_t n);
 // stable partition pass by owner shard (digit = OwnerDigit), global protein ids out
+// (d_n: the slot count on the device, n its upper bound -- a device-sized shard digest)
 hipError_t launch_owner_hist(const Rec* d_in, uint32_t n, const OwnerMap& om, bool sparse, uint32_t* d_hist,
-                             hipStream_t s);
+                             hipStream_t s, const unsigned long long* d_n = nullptr);
 // writes the second record word only (global protein | offset | length), 8 B
 // per record: the owner recomputes mass and tag from the residues
 hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, const OwnerMap& om, bool sparse,
-                                const uint32_t* d_hist, hipStream_t s);
+                                const uint32_t* d_hist, hipStream_t s, const unsigned long long* d_n = nullptr);
 // owner side: 8-B location words -> 16-B records (mass and tag from the residues)
 hipError_t launch_expand_locs(const uint64_t* d_locs, uint64_t n, const uint8_t* d_res, const uint32_t* d_poff,
                               const double* d_mass_tab, double m0, uint32_t w, Rec* d_out, hipStream_t s);
@@ -355,7 +356,8 @@ hipError_t launch_qcombine(const Rec* d_pairs, const Rec* d_res, uint64_t np, ui
 // out[i] = mass of slot i * n / ns (NaN for a sentinel slot), i < ns
 hipError_t launch_sample_masses(const Rec* d_recs, uint64_t n, uint32_t ns, double* d_out, hipStream_t s);
 // out[i] = in[i] - base (u64 -> u32 offsets of a protein range)
-hipError_t launch_off_rebase(const uint64_t* d_in, uint64_t base, uint32_t* d_out, uint64_t n, hipStream_t s);
+hipError_t launch_off_rebase(const uint64_t* d_in, uint64_t base, uint64_t hi, uint32_t* d_out, uint64_t n,
+                             hipStream_t s);  // out = clamp(in - base, 0, hi)
 // ctr->max_plen = max(ctr->max_plen, longest protein of poff[0..n_prot])
 hipError_t launch_max_plen(const uint32_t* d_poff, uint32_t n_prot, Counters* d_ctr, hipStream_t s);
 size_t radix_hist_elems(uint32_t n, int bits);

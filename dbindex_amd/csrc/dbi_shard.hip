@@ -84,7 +84,7 @@ struct dbi_comm {
     // never fails an allocation between two collectives of a build
     double* d_samp = nullptr;              // nranks x (DBI_SHARD_SAMPLES + 3)
     unsigned long long* d_cnt = nullptr;   // nranks x cnt_row
-    int cnt_row = 0;                       // max(nranks + 3, TOTALS_W)
+    int cnt_row = 0;                       // max(nranks + 4, TOTALS_W)
 };
 constexpr uint32_t COMM_RED_MAX = 4096;
 // totals row of a sharded build: n_total, n_dropped, n_recv, n_unique, n_keys,
@@ -248,13 +248,31 @@ __global__ void k_set_u64(unsigned long long* p, unsigned long long v) {
 
 // send counts of a partitioned shard, straight from the scanned owner
 // histogram (hist[d * g] = first output position of owner d's run)
+// d_total: the record count on the device (a device-sized digest), else n_total
 __global__ void k_owner_counts(const uint32_t* __restrict__ hist, uint64_t g, uint32_t ns, uint64_t n_total,
-                               unsigned long long* __restrict__ out) {
+                               const unsigned long long* __restrict__ d_total, unsigned long long* __restrict__ out) {
     const uint32_t d = threadIdx.x;
     if (d >= ns) return;
+    if (d_total) n_total = *d_total;
     const uint64_t a = n_total ? hist[(uint64_t)d * g] : 0u;
     const uint64_t b = (d + 1 < ns && n_total) ? hist[(uint64_t)(d + 1) * g] : n_total;
     out[d] = b - a;
+}
+
+// The count-matrix row's device flags of a device-sized shard digest: bit 0
+// its slots overflowed the buffer (nothing was partitioned: k_tail_counts),
+// bit 1 the offsets no longer give the shard's residue range or record width
+// the digest ran with, or the digest raised a layout / PTM error.  Either way
+// this rank digests again, synchronously (dbi_shard_digest).
+constexpr unsigned long long SHARD_REDO_SLOTS = 1, SHARD_REDO_RANGE = 2;
+__global__ void k_shard_flags(const uint64_t* __restrict__ poff, uint64_t p_begin, uint64_t p_end, uint64_t e0,
+                              uint64_t e1, uint32_t width, const Counters* __restrict__ ctr, uint64_t cap,
+                              unsigned long long* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    unsigned long long f = ctr->n_slots > cap ? SHARD_REDO_SLOTS : 0ull;
+    if (poff[p_begin] != e0 || poff[p_end] != e1 || rec_width(ctr->max_plen) != width) f |= SHARD_REDO_RANGE;
+    if (ctr->err & (ERR_LAYOUT | ERR_PTM)) f |= SHARD_REDO_RANGE;  // the synchronous digest reports it to every rank
+    *out = f;
 }
 
 // Stage whose time comes from events recorded around non-kernel work (RCCL,
@@ -592,8 +610,8 @@ int dbi_shard_digest(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const 
     const uint64_t np = p_end - p_begin;
     if ((rc = h->poff_g.ensure(n_prot + 1)) || (rc = h->poff.ensure(np + 1))) return rc;
     // global u32 offsets (owner merge) + this shard's offsets rebased to its first residue
-    DBI_HIP(launch_off_rebase(d_poff, 0, h->poff_g.p, n_prot + 1, s));
-    DBI_HIP(launch_off_rebase(d_poff + p_begin, ends[0], h->poff.p, np + 1, s));
+    DBI_HIP(launch_off_rebase(d_poff, 0, n_res, h->poff_g.p, n_prot + 1, s));
+    DBI_HIP(launch_off_rebase(d_poff + p_begin, ends[0], ends[1] - ends[0], h->poff.p, np + 1, s));
     // the record field width W comes from the longest protein of the WHOLE
     // proteome, so every shard packs records the same way
     DBI_HIP(launch_max_plen(h->poff_g.p, (uint32_t)n_prot, h->ctr.p, s));
@@ -638,6 +656,20 @@ int dbi_shard_digest(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const 
     sh.n_dropped = h->hc.n_dropped;
     sh.ms_digest = now_ms() - t0;
     sh.phase = 1;
+    // the next build of this shard may digest device-sized when this one
+    // was a bounded digest (its slots fit: a cold count + emit digest sizes
+    // the buffer by records, which the slots outgrow)
+    auto& dv = h->shard_dev;
+    dv.valid = sparse;
+    dv.d_res = d_res;
+    dv.d_poff = d_poff;
+    dv.n_res = n_res;
+    dv.n_prot = n_prot;
+    dv.p_begin = p_begin;
+    dv.p_end = p_end;
+    dv.e0 = ends[0];
+    dv.e1 = ends[1];
+    dv.width = sh.width;
     return 0;
 }
 
@@ -747,13 +779,15 @@ int partition_launch(dbi_handle* h, const int32_t* split) {
     if ((rc = h->hist.ensure(hist_elems)) || (rc = h->xsend.ensure(std::max<uint64_t>(sh.n_digest, 1))) ||
         (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(hist_elems), h->scan_tmp.cap))))
         return rc;
+    const unsigned long long* dn = sh.dev ? &h->ctr.p->tail_in : nullptr;  // slots written (0: overflowed)
     if (n_in > 0) {
-        STAGE(h, "owner_hist", by(0, 0, 0, 0, 0), launch_owner_hist(h->recA.p, n_in, om, sh.sparse, h->hist.p, s));
+        STAGE(h, "owner_hist", by(0, 0, 0, 0, 0),
+              launch_owner_hist(h->recA.p, n_in, om, sh.sparse, h->hist.p, s, dn));
         h->stages[h->nstage - 1].c0 = 8.0 * (double)n_in;
         STAGE(h, "owner_scan", by(0, 0, 0, 0, 0),
               launch_scan_u32(h->hist.p, h->hist.p, g << bits, h->scan_tmp.p, h->scan_tmp.cap, nullptr, s));
         STAGE(h, "owner_scatter", by(0, 0, 0, 0, 0),
-              launch_owner_scatter(h->recA.p, h->xsend.p, n_in, om, sh.sparse, h->hist.p, s));
+              launch_owner_scatter(h->recA.p, h->xsend.p, n_in, om, sh.sparse, h->hist.p, s, dn));
         h->stages[h->nstage - 1].c0 = 16.0 * (double)(sh.sparse ? n_in : sh.n_digest) + 8.0 * (double)sh.n_digest;
     }
     sh.part_blocks = g;
@@ -1285,7 +1319,7 @@ namespace {
 int comm_staging(dbi_comm* c) {
     if (hipMalloc((void**)&c->d_flag, 2 * sizeof(unsigned long long)) != hipSuccess)
         return set_error(DBI_E_OOM, "hipMalloc (communicator status word)");
-    c->cnt_row = std::max(c->nranks + 3, TOTALS_W);  // count matrix row | the totals row
+    c->cnt_row = std::max(c->nranks + 4, TOTALS_W);  // count matrix row | the totals row
     if (hipMalloc((void**)&c->d_red, COMM_RED_MAX * sizeof(double)) != hipSuccess ||
         hipMalloc((void**)&c->d_samp, sizeof(double) * (size_t)c->nranks * (NS + 3)) != hipSuccess ||
         hipMalloc((void**)&c->d_cnt, sizeof(unsigned long long) * (size_t)c->nranks * c->cnt_row) != hipSuccess ||
@@ -1506,6 +1540,84 @@ int build_single_owner(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, cons
     sh.phase = 4;
     return 0;
 }
+
+// Can this build digest its shard device-sized (shard_digest_dev)?  A warm
+// handle (bounded digest into the previous capacity) digesting the same
+// shard of the same inputs as its last sharded build.
+bool shard_dev_ok(const dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_poff, uint64_t n_prot,
+                  uint64_t p_begin, uint64_t p_end) {
+    const auto& dv = h->shard_dev;
+    const char* off = std::getenv("DBI_SHARD_DEV_DIGEST");
+    return dv.valid && !(off && off[0] == '0') && dv.d_res == d_res && dv.d_poff == d_poff && dv.n_res == n_res &&
+           dv.n_prot == n_prot && dv.p_begin == p_begin && dv.p_end == p_end && dv.e1 > dv.e0 &&
+           h->recA.cap >= 1024 && bounded_digest(h);
+}
+
+// dbi_shard_digest without its two host round trips (dbi_build_sharded, warm):
+// the residue range and record width of the last build (k_shard_flags checks
+// them on the device), the bounded digest into the previous capacity, and the
+// partition reading the slot count on the device (k_tail_counts: 0 when the
+// slots overflowed).  Host-side numbers (records, drops, errors) arrive with
+// the count matrix (shard_digest_dev_done); a flagged rank digests again
+// with dbi_shard_digest.
+int shard_digest_dev(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_poff, uint64_t n_prot,
+                     uint64_t p_begin, uint64_t p_end, int rank, int nshards) {
+    int rc;
+    if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    const double t0 = now_ms();
+    hipStream_t s = h->stream;
+    const auto& dv = h->shard_dev;
+    const uint64_t np = p_end - p_begin;
+    if ((rc = h->poff_g.ensure(n_prot + 1)) || (rc = h->poff.ensure(np + 1))) return rc;
+    DBI_HIP(launch_off_rebase(d_poff, 0, n_res, h->poff_g.p, n_prot + 1, s));
+    DBI_HIP(launch_off_rebase(d_poff + p_begin, dv.e0, dv.e1 - dv.e0, h->poff.p, np + 1, s));
+    DBI_HIP(launch_max_plen(h->poff_g.p, (uint32_t)n_prot, h->ctr.p, s));
+    ShardState& sh = h->shard;
+    sh = ShardState{};
+    sh.rank = rank;
+    sh.nshards = nshards;
+    sh.p_begin = p_begin;
+    sh.p_end = p_end;
+    sh.n_res_global = n_res;
+    sh.n_prot_global = n_prot;
+    sh.d_res_global = d_res;
+    h->d_res = d_res + dv.e0;
+    h->d_poff = h->poff.p;
+    h->n_res = dv.e1 - dv.e0;
+    h->n_prot = np;
+    uint64_t n = 0, n_in = 0;
+    bool sparse = false, dev = false;
+    if ((rc = run_digest(h, &n, &n_in, &sparse, &dev))) return rc;
+    if (!dev || !sparse) return set_error(DBI_E_STATE, "internal: device-sized shard digest without bounded slots");
+    DBI_HIP(launch_tail_counts(h->ctr.p, n_in, true, s));
+    sh.width = dv.width;
+    sh.n_digest = n;  // the capacity until the count matrix arrives
+    sh.n_in = n_in;
+    sh.sparse = true;
+    sh.dev = true;
+    sh.ms_digest = now_ms() - t0;
+    sh.phase = 1;
+    return 0;
+}
+
+// after the count-matrix sync (h->hc holds the digest's counters): the
+// numbers dbi_shard_digest reads at once
+int shard_digest_dev_done(dbi_handle* h) {
+    ShardState& sh = h->shard;
+    if (h->hc.err & ERR_LAYOUT) return set_error(DBI_E_INVALID, "record layout overflow in the shard digest");
+    if (h->hc.err & ERR_PTM) return set_error(DBI_E_INVALID, ptm_device_msg());
+    for (int i = 0; i < h->nstage; ++i) {  // the digest stages' bytes are this shard's
+        auto& st = h->stages[i];
+        st.c0 += st.cR * (double)h->n_res + st.cN * (double)h->hc.n_kept + st.cP * (double)(h->n_prot + 1);
+        st.cR = st.cN = st.cU = st.cP = st.cB = 0;
+    }
+    sh.n_digest = h->hc.n_kept;
+    sh.n_in = h->hc.n_slots;
+    sh.n_total = h->hc.n_kept + h->hc.n_dropped;
+    sh.n_dropped = h->hc.n_dropped;
+    sh.dev = false;
+    return 0;
+}
 }  // namespace
 }  // namespace dbi
 
@@ -1525,12 +1637,18 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // a rank that fails locally still takes part in the next collective, with
     // its status, so that every rank returns an error (never a hang)
     const double t_digest = now_ms();
-    int rc_digest = dbi_shard_digest(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n);
+    auto& wm = h->shard_warm;
+    const auto& pf = h->shard_prof;
+    const char* resample = std::getenv("DBI_SHARD_RESAMPLE");
+    // a warm build of the same shard with a reusable split digests
+    // device-sized: no host round trip before the count matrix
+    const bool dev_digest = wm.valid && wm.n == n && !(resample && resample[0] == '1') &&
+                            shard_dev_ok(h, d_res, n_res, d_poff, n_prot, p_begin, p_end);
+    int rc_digest = dev_digest ? shard_digest_dev(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n)
+                               : dbi_shard_digest(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n);
     if (!rc_digest) rc_digest = injected_failure("digest", me);
     ShardState& sh = h->shard;
     hipStream_t s = h->stream;
-    auto& wm = h->shard_warm;
-    const auto& pf = h->shard_prof;
 
     // Owner splitters.  A warm build reuses the split the previous build left
     // (computed from the sorted samples of the last sampled build and the
@@ -1541,7 +1659,6 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // a fingerprint of each rank's cost profile: profiles that differ are not
     // used), and partitions again.  The decision is taken from the gathered
     // matrix, so every rank takes the same collectives.
-    const char* resample = std::getenv("DBI_SHARD_RESAMPLE");
     bool have_split = wm.valid && wm.n == n && !(resample && resample[0] == '1');
     int32_t split[MAX_SHARDS - 1] = {};
     if (have_split) std::copy(wm.split, wm.split + (n - 1), split);
@@ -1592,14 +1709,15 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     };
 
     // count matrix: row r = records shard r sends each owner (from its owner
-    // histogram, on the device) | its status | its receive capacity | its split's hash
-    const int w = n + 3;
+    // histogram, on the device) | its status | its receive capacity | its
+    // split's hash | its device flags (a device-sized digest to redo, k_shard_flags)
+    const int w = n + 4;
     std::vector<unsigned long long> full((size_t)n * w, 0);
     std::vector<uint64_t> counts((size_t)n * n);
-    bool failed = false, grow = false;
+    bool failed = false, grow = false, sample_next = false;
     double t_part = now_ms();
     for (int round = 0;; ++round) {
-        if (round > 0) {
+        if (sample_next) {
             if ((rc = sample_split())) return rc;
             t_part = now_ms();
         }
@@ -1616,7 +1734,7 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
         unsigned long long* my_row = c->d_cnt + (size_t)me * w;
         if (!rc_part && have_split && sh.n_in > 0) {
             hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(64), 0, s, h->hist.p, sh.part_blocks, (uint32_t)n,
-                               sh.n_digest, my_row);
+                               sh.n_digest, sh.dev ? &h->ctr.p->tail_n : nullptr, my_row);
             if ((rc = hipGetLastError()) != hipSuccess) rc_part = hip_fail((hipError_t)rc, "k_owner_counts");
         } else if ((rc = hipMemsetAsync(my_row, 0, sizeof(unsigned long long) * n, s)) != hipSuccess && !rc_part) {
             rc_part = hip_fail((hipError_t)rc, "hipMemsetAsync");
@@ -1625,22 +1743,45 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
         mine[n] = rc_part ? 1u : 0u;
         mine[n + 1] = h->xrecv.cap;
         mine[n + 2] = have_split ? (fnv64(split, sizeof(int32_t) * (n - 1)) | 1ull) : 0ull;
-        DBI_HIP(hipMemcpyAsync(my_row + n, mine + n, 3 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+        mine[n + 3] = 0;
+        DBI_HIP(hipMemcpyAsync(my_row + n, mine + n, 4 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+        if (!rc_part && sh.dev) {
+            const auto& dv = h->shard_dev;
+            hipLaunchKernelGGL(k_shard_flags, dim3(1), dim3(64), 0, s, d_poff, p_begin, p_end, dv.e0, dv.e1, dv.width,
+                               h->ctr.p, sh.n_in, my_row + n + 3);
+            if ((rc = hipGetLastError()) != hipSuccess) rc_part = hip_fail((hipError_t)rc, "k_shard_flags");
+        }
         if ((rc = c_allgather(c, my_row, c->d_cnt, 8ull * w, s))) return rc;
         DBI_HIP(hipMemcpyAsync(full.data(), c->d_cnt, sizeof(unsigned long long) * n * w, hipMemcpyDeviceToHost, s));
+        if (sh.dev) DBI_HIP(hipMemcpyAsync(&h->hc, h->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, s));
         DBI_HIP(hipStreamSynchronize(s));
         if (rc_part) return rc_part;
-        bool agree_split = true;
+        bool agree_split = true, redo = false;
         for (int i = 0; i < n; ++i) {
             failed |= full[(size_t)i * w + n] != 0;
             agree_split &= full[(size_t)i * w + n + 2] != 0 && full[(size_t)i * w + n + 2] == mine[n + 2];
+            redo |= full[(size_t)i * w + n + 3] != 0;
         }
         if (failed) return peer_failed(round == 0 ? "owner partition" : "owner partition (sampled split)");
+        if (redo) {
+            // a device-sized digest did not fit its slots, or the offsets moved:
+            // that rank digests again with dbi_shard_digest (grows the buffer,
+            // reads the range), every rank partitions and gathers again (the
+            // same verdict everywhere: the same matrix)
+            if (round >= 2) return set_error(DBI_E_STATE, "internal: shard digest redone twice");
+            if (full[(size_t)me * w + n + 3] != 0) {
+                rc_digest = dbi_shard_digest(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n);
+                t_part = now_ms();
+            }
+            continue;
+        }
+        if (sh.dev && (rc = shard_digest_dev_done(h))) return rc;  // (a device error is a flag: never here)
         sh.split_rounds = round + 1;
         if (agree_split) break;
-        if (round > 0) return set_error(DBI_E_STATE, "internal: ranks computed different owner splits from the "
-                                                     "same samples");
-        have_split = false;  // every rank samples: the same verdict from the same matrix
+        if (sample_next) return set_error(DBI_E_STATE, "internal: ranks computed different owner splits from the "
+                                                       "same samples");
+        sample_next = true;  // every rank samples: the same verdict from the same matrix
+        have_split = false;
     }
     sh.ms_digest = t_part - t_digest;
     sh.split_sampled = sampled ? 1 : 0;

@@ -44,6 +44,12 @@ def _rank_main(world: int, rank: int, name: str, plan: dict, q) -> None:
         with Engine(cp, 0) as eng:
             eng.set_timing(False)
             for k in range(plan["builds"]):
+                kind = plan.get("mutate", {}).get(k)
+                if kind:  # new contents in the same device buffers (same pointers and sizes)
+                    res2, off2 = _mutated(pp, kind)
+                    d_res.upload(np.concatenate([res2, np.zeros(16, np.uint8)]))
+                    d_off.upload(off2.astype(np.uint64))
+                    synchronize(0)
                 env = plan.get("env", {}).get(k, {})
                 for key, val in env.items():
                     os.environ[key] = val.replace("{rank}", str(rank))
@@ -71,6 +77,24 @@ def _rank_main(world: int, rank: int, name: str, plan: dict, q) -> None:
         q.put((rank, out))
     except Exception:  # the parent reports it
         q.put((rank, {"crash": traceback.format_exc()}))
+
+
+def _mutated(pp, kind: str):
+    """The proteome rewritten in place between builds: 'dense' -- every third
+    residue of the first half a K (far more cleavage sites: more digest slots
+    than the last build reserved); 'offsets' -- the same residues with every
+    inner protein boundary moved three residues on (the shards' residue
+    ranges change under the same protein ranges)."""
+    res = pp.residues.copy()
+    off = pp.offsets.astype(np.int64).copy()
+    if kind == "dense":
+        res[np.arange(0, int(off[off.shape[0] // 2]), 3)] = ord("K")
+    elif kind == "offsets":
+        off[1:-1] += 3
+        assert np.all(np.diff(off) > 0)
+    else:
+        raise ValueError(kind)
+    return res, off.astype(np.uint64)
 
 
 def _run(world: int, plan: dict):
@@ -166,3 +190,26 @@ def test_ranks_failure_is_agreed(oracle, phase):
         assert not out["builds"][1]["ok"], (r, phase)
         assert ("injected" in out["builds"][1]["error"]) == (r == 1), (r, out["builds"][1]["error"])
     _assert_whole_index([out["builds"][2]["export"] for out in res], oracle, f"after a {phase} failure")
+
+
+@pytest.mark.parametrize("kind", ["dense", "offsets"])
+def test_ranks_device_sized_digest_redone(oracle, kind):
+    """Warm builds digest their shard device-sized (no host round trip before
+    the count matrix).  Build 2 rewrites the proteome in place: 'dense' makes
+    the digest outgrow the slots the last build reserved, 'offsets' moves the
+    shards' residue ranges; either way the device flags it in the count
+    matrix, that rank digests again synchronously, every rank gathers again
+    (two rounds), and builds 2-3 equal the oracle of the rewritten proteome."""
+    from dbindex_amd import fasta
+    from dbindex_amd.params import DBIndexSearchParams
+    from oracle import cref
+    res = _run(2, {"builds": 4, "mutate": {2: kind}})
+    pp = fasta.config("1k").slice(0, NPROT)
+    r2, o2 = _mutated(pp, kind)
+    oix2 = cref.Index(DBIndexSearchParams.trypsin(2).to_c(), r2, o2)
+    for k in range(4):
+        builds = [r["builds"][k] for r in res]
+        assert all(b["ok"] for b in builds), (k, [b.get("error") for b in builds])
+        _assert_whole_index([b["export"] for b in builds], oracle if k < 2 else oix2, f"{kind} build {k}")
+    assert {b["rounds"] for b in [r["builds"][1] for r in res]} == {1}
+    assert {b["rounds"] for b in [r["builds"][2] for r in res]} == {2}, [r["builds"][2]["rounds"] for r in res]

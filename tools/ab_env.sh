@@ -7,7 +7,7 @@ TAG=$1; CFG=$2; shift 2
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 for spec in "$@"; do
     name=${spec%%=*}; envs=${spec#*=}
-    env $envs timeout -k 10 300 python bench.py --config "$CFG" --steps 20 --warmup 3 --no-cpu-baseline --queries 0 > "$OUT/$name.json" 2> "$OUT/$name.err" \
+    env $envs timeout -k 10 300 python bench.py --config "$CFG" --steps ${AB_STEPS:-20} --warmup 5 --no-cpu-baseline --queries 0 > "$OUT/$name.json" 2> "$OUT/$name.err" \
         || { echo "$name failed"; tail -5 "$OUT/$name.err"; exit 1; }
     python3 -c "
 import json; d=json.loads(open('$OUT/$name.json').read().strip().splitlines()[-1])
