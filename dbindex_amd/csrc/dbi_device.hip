@@ -740,13 +740,13 @@ constexpr double CUT_SCALE = 512.0;
 // apart -- two banks for 32 lanes (SQ: ~7 bank conflicts per LDS instruction
 // in the bucket count, 4.5 in the plain one).
 struct CutSmem {
-    uint32_t raw[WIN + WIN / 32 + 1];
+    uint32_t raw[WIN + 4 + (WIN + 4) / 32 + 1];  // (+ slack: the bucket count reads up to p[q + 2] unclamped)
     __device__ __forceinline__ uint32_t& p(uint32_t i) { return raw[i + (i >> 5)]; }
     __device__ __forceinline__ uint32_t p(uint32_t i) const { return raw[i + (i >> 5)]; }
 };
 
 // T of a limit X (clamped: an infinite or huge limit is never reached)
-__device__ __forceinline__ int64_t cut_threshold(double x, double m0) {
+__host__ __device__ __forceinline__ int64_t cut_threshold(double x, double m0) {
     const double t = floor((x - m0) * CUT_SCALE);
     return t < -1e15 ? (int64_t)-1e15 : t > 1e15 ? (int64_t)1e15 : (int64_t)t;
 }
@@ -807,7 +807,7 @@ __device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi) {
 constexpr int HIST_FAST_MAX = 8;
 struct HistTrack {
     uint32_t t[HIST_FAST_MAX];  // the boundary's position (0: not yet found)
-    uint32_t c[HIST_FAST_MAX + 1];
+    uint32_t c[HIST_FAST_MAX + 1];  // c[k]: ends at or past boundary k (k < 8); c[8]: ends
 };
 
 // first q in [t, hi + 1] with p[q] > a (p non-decreasing): gallop, then bisect
@@ -843,10 +843,11 @@ __device__ __forceinline__ uint32_t first_above(DF D, uint32_t a, uint32_t b, in
 // counts into the LDS hist.  An end too close to a boundary (or more than 7
 // boundaries in one walk, binary-search path) and the start is recounted by
 // the exact walk.
-template <bool HIST = false>
+// FAST (a kernel of its own: the binary-search path's code is not in it)
+template <bool HIST = false, bool FAST = false>
 __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const CutLimits& cl, const DigestSmem& sm,
                                                    const CutSmem& cs, uint32_t nbytes, uint32_t ps, uint32_t* hist,
-                                                   HistTrack& ht, bool fast) {
+                                                   HistTrack& ht) {
     CutCount r{0u, 0u, true};
     if (!(dp.m0 <= dp.max_mh)) return r;  // while condition before the first residue (:284)
     if (ps + 2 > nbytes) { r.exact = false; return r; }
@@ -913,43 +914,37 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
             nd = (uint32_t)__popcll(em & bit_range(a, (uint32_t)Y));
         }
     }
-    if (HIST && n && fast) {
+    if constexpr (HIST && FAST) {
+      if (n) {
         // absolute window positions of the first / last end; end q is past
         // boundary k when p[q] > pb + T_k (the first such q tracked per k).
-        // u32 arithmetic (fast: 3 <= T_k < 2^31; a window's prefix + T_k < 2^32).  The
-        // tracked position moves ~one residue per start, so every boundary's
-        // next few prefixes are loaded together (p[q-1 .. q+2]: one LDS round
-        // trip for all boundaries instead of a chain of reads per boundary),
-        // and a search only when it moved further.
+        // u32 arithmetic (fast: 3 <= T_k < 2^31; a window's prefix + T_k < 2^32).
+        // The tracked position moves ~one residue per start, so every
+        // boundary's next prefixes are loaded together (p[q-1 .. q+2]: one LDS
+        // round trip for all boundaries) and a search runs only when it moved
+        // further.  ht.c[k] (k < 8) sums G_k, the ends at or past boundary k;
+        // ht.c[8] sums n (the bucket counts are their differences, at the flush).
         const uint32_t qlo = ps + (uint32_t)lo, qhi = ps + (uint32_t)Y;
         const uint32_t upb = (uint32_t)pb;
         const uint32_t dlo = (uint32_t)D((uint32_t)lo), dhi = (uint32_t)D((uint32_t)Y);
         uint32_t pos[HIST_FAST_MAX];
+        uint32_t v[HIST_FAST_MAX][4];  // p[q-1], p[q], p[q+1], p[q+2] (slack words past the window)
         uint32_t need = 0;  // bit k: boundary k falls among the ends (or too close to tell)
 #pragma unroll
         for (int k = 0; k < HIST_FAST_MAX; ++k) {
+            const uint32_t t = (uint32_t)cl.t_b[k];
             pos[k] = qhi + 1u;  // every end below the boundary (k >= nb: unused)
-            if (k < dp.nb) {
-                const uint32_t t = (uint32_t)cl.t_b[k];
-                if (dhi + (uint32_t)CUT_EPS_FX <= t) {
-                    pos[k] = qhi + 1u;
-                } else if (dlo >= t + (uint32_t)CUT_EPS_FX) {
+            if (k < dp.nb && dhi + (uint32_t)CUT_EPS_FX > t) {
+                if (dlo >= t + (uint32_t)CUT_EPS_FX) {
                     pos[k] = qlo;  // every end past it
                 } else {
                     uint32_t q = ht.t[k];
-                    if (q < qlo || q > qhi + 1u) q = qlo;  // first use, or left behind
+                    q = (q < qlo || q > qhi + 1u) ? qlo : q;  // first use, or left behind
                     pos[k] = q;
                     need |= 1u << k;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[k][i] = cs.p(q + (uint32_t)i - 1u);  // q >= qlo >= 1
                 }
-            }
-        }
-        uint32_t v[HIST_FAST_MAX][4];  // p[q-1], p[q], p[q+1], p[q+2] (clamped into [qlo-1, qhi])
-#pragma unroll
-        for (int k = 0; k < HIST_FAST_MAX; ++k) {
-            if (need & (1u << k)) {
-                const uint32_t q = pos[k];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[k][i] = cs.p(max(min(q + (uint32_t)i, qhi + 1u), 1u) - 1u);
             }
         }
         bool bad = false;
@@ -958,18 +953,19 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
             if (need & (1u << k)) {
                 const uint32_t t = (uint32_t)cl.t_b[k], athr = upb + t;
                 uint32_t q = pos[k];
-                // first of q, q+1, q+2 (up to qhi) with p > athr: the prefixes ascend
-                const uint32_t a = (q <= qhi && v[k][1] <= athr ? 1u : 0u) + (q + 1u <= qhi && v[k][2] <= athr ? 1u : 0u) +
-                                   (q + 2u <= qhi && v[k][3] <= athr ? 1u : 0u);
+                // how many of p[q], p[q+1], p[q+2] are <= athr (ascending prefixes;
+                // past qhi they only move q' to qhi + 1)
+                // (the first one above athr: the slack words past the window are not prefixes)
+                const uint32_t a = v[k][1] > athr ? 0u : v[k][2] > athr ? 1u : v[k][3] > athr ? 2u : 3u;
                 uint32_t phi, plo;  // p[q'] (q' <= qhi) and p[q' - 1] (q' > qlo)
                 if (a == 3u && q + 3u <= qhi) {  // moved further: search (rare)
                     q = prefix_seek(cs, q + 3u, qhi, (int64_t)athr);
-                    phi = q <= qhi ? cs.p(q) : 0u;
+                    phi = cs.p(q);
                     plo = cs.p(q - 1u);
                 } else {
-                    q += a;
                     phi = a == 0u ? v[k][1] : a == 1u ? v[k][2] : v[k][3];
                     plo = a == 0u ? v[k][0] : a == 1u ? v[k][1] : a == 2u ? v[k][2] : v[k][3];
+                    q = min(q + a, qhi + 1u);
                 }
                 ht.t[k] = q;
                 if (q <= qhi && phi - upb < t + (uint32_t)CUT_EPS_FX) bad = true;
@@ -978,19 +974,14 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
             }
         }
         if (bad) { r.exact = false; return r; }
-        uint32_t from = qlo;
+        // G_k = ends at or past boundary k's position (em: ends, bits from ps)
 #pragma unroll
         for (int k = 0; k < HIST_FAST_MAX; ++k) {
-            if (k < dp.nb) {
-                if (pos[k] > from) ht.c[k] += (uint32_t)__popcll(em & bit_range(from - ps, pos[k] - 1u - ps));
-                from = max(from, pos[k]);
-            }
+            const uint32_t sh = pos[k] - ps;  // <= Y + 1 <= 64
+            if (k < dp.nb) ht.c[k] += sh >= 64u ? 0u : (uint32_t)__popcll(em >> sh);
         }
-        uint32_t last = 0;
-        if (from <= qhi) last = (uint32_t)__popcll(em & bit_range(from - ps, (uint32_t)Y));
-#pragma unroll
-        for (int k = 1; k <= HIST_FAST_MAX; ++k)
-            if (k == dp.nb) ht.c[k] += last;
+        ht.c[HIST_FAST_MAX] += n;
+      }
     } else if (HIST && n) {
         // the buckets of the first and last end (exact ones: none within ~0.006 Da of a boundary)
         const double ml = dp.m0 + (double)D((uint32_t)lo) / CUT_SCALE, my = dp.m0 + (double)D((uint32_t)Y) / CUT_SCALE;
@@ -1059,7 +1050,7 @@ __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nby
     __syncthreads();
 }
 
-template <bool HIST>
+template <bool HIST, bool FAST = false>
 __global__ void __launch_bounds__(DIGEST_THREADS) __attribute__((amdgpu_waves_per_eu(HIST ? 4 : 1, 8)))
 k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                     const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
@@ -1074,9 +1065,7 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
         for (uint32_t b = threadIdx.x; b <= (uint32_t)dp.nb; b += DIGEST_THREADS) s_hist[b] = 0;
     HistTrack ht;
     const CutLimits cl = cut_limits(dp);
-    // (the tracked boundaries compare in u32: thresholds in [3, 2^31))
-    const bool fast = HIST && dp.nb <= HIST_FAST_MAX && cl.t_b[0] >= CUT_EPS_FX &&
-                      cut_threshold((double)(min(dp.nb, HIST_FAST_MAX) * dp.br), dp.m0) < (1ll << 31);
+    constexpr bool fast = HIST && FAST;  // (count_fast_ok on the host)
 #pragma unroll
     for (int k = 0; k < HIST_FAST_MAX; ++k) ht.t[k] = 0;
 #pragma unroll
@@ -1089,7 +1078,7 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     thread_share(ncand, jb, je);
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
-        CutCount r = count_by_masks<HIST>(dp, cl, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0, s_hist, ht, fast);
+        CutCount r = count_by_masks<HIST, FAST>(dp, cl, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0, s_hist, ht);
         if (!r.exact) {
             const WalkOut w = walk_candidate<false, false, false, HIST>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr,
                                                                         s_hist);
@@ -1100,10 +1089,14 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
         dropped += r.dropped;
     }
     if (fast) {  // the register counts into the block's (wave sums: one LDS atomic per wave and bucket)
+        // bucket k holds the ends past boundary k-1 and not past boundary k
+        uint32_t above = ht.c[HIST_FAST_MAX];  // every end is past "boundary -1"
 #pragma unroll
         for (int k = 0; k <= HIST_FAST_MAX; ++k) {
-            const uint32_t v = wave_sum(ht.c[k]);
+            const uint32_t past = k < dp.nb ? ht.c[k] : 0u;
+            const uint32_t v = k <= dp.nb ? wave_sum(above - past) : 0u;
             if (k <= dp.nb && lane_id() == 0 && v) atomicAdd(&s_hist[k], v);
+            if (k < dp.nb) above = past;
         }
     }
     publish_counts(sm, kept, dropped, d_blk, d_thr, d_ctr);
@@ -1914,6 +1907,14 @@ hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, 
     return hipGetLastError();
 }
 
+// the bucket count's tracked-boundary kernel applies: NUM_BUCKETS <= 8,
+// its thresholds compare in u32 ([3, 2^31)), and the first end of a start is
+// past window position 0 (MIN_PEP_LENGTH >= 2)
+static bool count_fast_ok(const DevParams& dp) {
+    return dp.nb >= 1 && dp.nb <= HIST_FAST_MAX && dp.min_len >= 2 && cut_threshold((double)dp.br, dp.m0) >= CUT_EPS_FX &&
+           cut_threshold((double)(dp.nb * dp.br), dp.m0) < (1ll << 31);
+}
+
 template <bool EMIT, bool HIST = false>
 static hipError_t launch_digest(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
@@ -1926,8 +1927,12 @@ static hipError_t launch_digest(const DevParams& dp, const double* d_mass_tab, c
     DBI_LAUNCH((k_digest<EMIT, SEMI, MAND, HIST>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
                        d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_out, d_ctr, d_hist)
     if (!EMIT && !dp.semi && !dp.mand_mode && dp.cut_count) {
-        DBI_LAUNCH(k_digest_count_cuts<HIST>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags,
-                   d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr, d_hist);
+        if (HIST && count_fast_ok(dp))
+            DBI_LAUNCH((k_digest_count_cuts<HIST, true>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab,
+                       d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr, d_hist);
+        else
+            DBI_LAUNCH(k_digest_count_cuts<HIST>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags,
+                       d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr, d_hist);
         return hipGetLastError();
     }
     if (dp.semi) {
