@@ -3693,7 +3693,11 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
 // run (tag counting sort for a single-mass bin, else the block-level compact
 // sort), heads added to ucount[chunk].  No run detection, no small-bin pass:
 // the chunk's other records were finished by k_chunk_sort.
-template <int NT, int CAP>
+// Two size classes over the one list (LMIN < L <= CAP each; a block whose
+// entry is the other class's returns at once): bins of up to 1024 records
+// in 256-thread blocks with half the LDS -- 7 blocks per CU instead of 4
+// (5 728 of SwissProt's 7 310 mid bins) -- the rest in 512-thread blocks.
+template <int NT, int CAP, uint32_t LMIN>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DBI_MID_WPE, 8)))
 k_bin_sort_mid(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
                const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
@@ -3708,7 +3712,8 @@ k_bin_sort_mid(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t
     const uint32_t n = ctr->n_mid;
     if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x) atomicOr(&ctr->err, ERR_GRID);
     const uint32_t j = blockIdx.x;
-    if (j < n) {
+    const uint32_t Lj = j < n ? (list[2 * j + 1] >> 16) - (list[2 * j + 1] & 0xFFFFu) : 0u;
+    if (j < n && Lj > LMIN && Lj <= (uint32_t)CAP) {  // else the other class's entry (block-uniform)
         const uint32_t c = list[2 * j], r = list[2 * j + 1];
         const uint32_t a = chunk_lo[c] + (r & 0xFFFFu), L = (r >> 16) - (r & 0xFFFFu);
         const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
@@ -3723,6 +3728,7 @@ k_bin_sort_mid(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t
     for (uint32_t e = j + gridDim.x; e < n; e += gridDim.x) {
         const uint32_t c = list[2 * e], r = list[2 * e + 1];
         const uint32_t a = chunk_lo[c] + (r & 0xFFFFu), L = (r >> 16) - (r & 0xFFFFu);
+        if (L <= LMIN || L > (uint32_t)CAP) continue;
         for (uint32_t i = threadIdx.x; i < L; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
     }
 }
@@ -3741,7 +3747,11 @@ hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, 
                                  const uint32_t* d_mid_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s) {
     if (max_blocks == 0) return hipSuccess;
     (void)bm;
-    DBI_LAUNCH((k_bin_sort_mid<CHUNK_THREADS, CHUNK_CAP>), dim3(max_blocks), dim3(CHUNK_THREADS), 0, s, d_in, d_out,
+    constexpr uint32_t MID_SPLIT = 1024;  // bins of (WAVE_SORT_MAX, MID_SPLIT] records: the small-block class
+    static_assert(MID_SPLIT > WAVE_SORT_MAX && MID_SPLIT < CHUNK_CAP, "mid size classes");
+    DBI_LAUNCH((k_bin_sort_mid<MID_SPLIT / 4, MID_SPLIT, WAVE_SORT_MAX>), dim3(max_blocks), dim3(MID_SPLIT / 4), 0, s,
+               d_in, d_out, d_chunk_lo, d_res, d_poff, d_ucount, d_mid_list, d_ctr);
+    DBI_LAUNCH((k_bin_sort_mid<CHUNK_THREADS, CHUNK_CAP, MID_SPLIT>), dim3(max_blocks), dim3(CHUNK_THREADS), 0, s, d_in, d_out,
                d_chunk_lo, d_res, d_poff, d_ucount, d_mid_list, d_ctr);
     return hipGetLastError();
 }
