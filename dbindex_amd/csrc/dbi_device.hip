@@ -3639,18 +3639,26 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
 // threads, 155 KiB LDS, one block per CU; above split_above they go on to the
 // giant path.  One block per listed chunk, blocks past the list exit (a
 // grid-stride loop around sort_chunk doubled its registers).
-template <int NT, int CAP>
+// Two size classes over the one list, as the mid tier: SMALL takes the
+// chunks of at most CAP records (and <= split_above) -- 512 threads and half
+// the LDS, two blocks per CU (SwissProt: 382 of 421 big chunks, semi-tryptic
+// most of them) -- the other class (SMALL false, BIG_CAP) every other entry;
+// a block whose entry is the other class's skips it.
+template <int NT, int CAP, bool SMALL = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
                   const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
                   const uint32_t* __restrict__ list, uint32_t* __restrict__ giant_list, uint32_t split_above,
-                  uint32_t ties, Counters* __restrict__ ctr) {
+                  uint32_t ties, Counters* __restrict__ ctr, uint32_t small_cap) {
     __shared__ ChunkSmem<NT, CAP> sm;
     const uint32_t n = ctr->n_big;
     if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x) atomicOr(&ctr->err, ERR_GRID);
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     const uint32_t j = blockIdx.x;
-    if (j < n) {
+    // the small class's entries: at most small_cap (<= its CAP) and split_above records
+    auto small_entry = [&](uint32_t m) { return m <= small_cap && m <= split_above; };
+    const uint32_t mj = j < n ? chunk_lo[list[j] + 1] - chunk_lo[list[j]] : 0u;
+    if (j < n && small_entry(mj) == SMALL) {
         const uint32_t c = list[j];
         const uint32_t a = chunk_lo[c];
         const uint32_t m = chunk_lo[c + 1] - a;
@@ -3683,6 +3691,7 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
         const uint32_t c = list[e];
         const uint32_t a = chunk_lo[c];
         const uint32_t m = chunk_lo[c + 1] - a;
+        if (small_entry(m) != SMALL) continue;
         for (uint32_t i = threadIdx.x; i < m; i += NT) out[a + i] = Rec{in[a + i].q0 & ~0xFFull, in[a + i].q1};
         if (threadIdx.x == 0) ucount[c] = 0;
     }
@@ -3694,7 +3703,7 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
 // sort), heads added to ucount[chunk].  No run detection, no small-bin pass:
 // the chunk's other records were finished by k_chunk_sort.
 // Two size classes over the one list (LMIN < L <= CAP each; a block whose
-// entry is the other class's returns at once): bins of up to 1024 records
+// entry is the other class's skips it): bins of up to 1024 records
 // in 256-thread blocks with half the LDS -- 7 blocks per CU instead of 4
 // (5 728 of SwissProt's 7 310 mid bins) -- the rest in 512-thread blocks.
 template <int NT, int CAP, uint32_t LMIN>
@@ -3756,14 +3765,27 @@ hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, 
     return hipGetLastError();
 }
 
+constexpr uint32_t BIG_SPLIT_CUS = 256;  // MI355X compute units
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
-                                 uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s) {
+                                 uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s, int split_mode) {
     if (max_blocks == 0) return hipSuccess;
+    constexpr int SMALL_BIG = BIG_CAP / 2;  // 3968 records: 512 threads, 2 blocks per CU
+    const uint32_t sa = std::min<uint32_t>(split_above, (uint32_t)BIG_CAP);
+    // the two classes only for long lists: a few hundred big chunks (SwissProt
+    // tryptic: 421) take two rounds of the 1024-thread blocks either way, and the
+    // second launch's skipping blocks cost more than the small class saves
+    // (0.15 -> 0.24 ms measured); semi-tryptic's ~70 k: 18.0 -> 15.4 ms
+    // (split_mode: DBI_BIG_SPLIT, 0 never / 1 always, for the tests; -1 by the list length)
+    const bool split = split_mode < 0 ? max_blocks > 4u * BIG_SPLIT_CUS : split_mode != 0;
+    if (split)
+        DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS / 2, SMALL_BIG, true>), dim3(max_blocks), dim3(BIG_THREADS / 2), 0,
+                   s, d_in, d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list, sa,
+                   ties ? 1u : 0u, d_ctr, (uint32_t)SMALL_BIG);
     DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS, BIG_CAP>), dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in,
-               d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list,
-               std::min<uint32_t>(split_above, (uint32_t)BIG_CAP), ties ? 1u : 0u, d_ctr);
+               d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list, sa, ties ? 1u : 0u, d_ctr,
+               split ? (uint32_t)SMALL_BIG : 0u);
     return hipGetLastError();
 }
 

@@ -281,6 +281,7 @@ struct dbi_handle {
     bool use_graph = true;                // DBI_BUILD_GRAPH=0: never
     bool use_h1 = true;                   // DBI_DIGEST_HIST=0: the first radix histogram as its own kernel
     bool use_semi_bounded = true;         // DBI_SEMI_BOUNDED=0: warm semi builds by the fused count + emit digest
+    int big_split = -1;                   // DBI_BIG_SPLIT: big tier in two size classes (1 always, 0 never, -1 long lists)
     bool h1_on = false;                   // this warm build's digest counts the first radix histogram (h1plan)
     dbi::Hist1Plan h1plan{};
     bool capturing = false;               // stage events become event nodes

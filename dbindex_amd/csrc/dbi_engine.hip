@@ -253,7 +253,7 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
           launch_chunk_sort_big(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                                 giants ? h->giant_list.p : nullptr, max_big, h->split_above, h->exact_dups, h->ctr.p,
-                                s));
+                                s, h->big_split));
     if (giants)
         STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
               launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,
@@ -980,6 +980,7 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     if (const char* ev = std::getenv("DBI_BUILD_GRAPH")) h->use_graph = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("DBI_DIGEST_HIST")) h->use_h1 = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("DBI_SEMI_BOUNDED")) h->use_semi_bounded = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("DBI_BIG_SPLIT")) h->big_split = std::atoi(ev) != 0 ? 1 : 0;
     auto fail = [&](int code) {
         dbi_close(h);
         return code;

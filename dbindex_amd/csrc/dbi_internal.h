@@ -375,7 +375,8 @@ hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, 
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
-                                 uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s);
+                                 uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s,
+                                 int split = -1);
 // chunks above BIG_CAP listed in d_giant_list: MSD split on the (mass, tag)
 // key into leaves sorted in LDS; a segment of one (mass, tag) key above
 // BIG_CAP falls back to global-memory scratch (ws_key / ws_k2).  segs: 5 lists
