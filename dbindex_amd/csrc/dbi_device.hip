@@ -4886,12 +4886,14 @@ k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__
     }
 }
 
-// leaves: sorted in LDS into out[lo, lo+n) (in place when they live in out)
+// leaves: sorted in LDS into out[lo, lo+n) (in place when they live in out);
+// this launch takes the leaves of more than lmin records (the big leaves in
+// two size classes, as the big tier: up to 3968 records two blocks per CU)
 template <int NT, int CAP>
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CAP <= CHUNK_CAP ? DBI_MID_WPE : 4, 8)))
 k_giant_leaf(const Rec* in, Rec* out, const uint4* __restrict__ list, const unsigned int* __restrict__ n_list,
              uint32_t cap, const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff,
-             uint32_t* __restrict__ ucount, Counters* __restrict__ ctr) {
+             uint32_t* __restrict__ ucount, Counters* __restrict__ ctr, uint32_t lmin) {
     __shared__ unsigned long long k0[CAP];
     __shared__ unsigned long long k1[CAP];
     __shared__ uint32_t aux[CAP];
@@ -4903,6 +4905,7 @@ k_giant_leaf(const Rec* in, Rec* out, const uint4* __restrict__ list, const unsi
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
         const uint4 lf = list[j];
+        if (lf.y <= lmin || lf.y > (uint32_t)CAP) continue;  // the other class's (block-uniform)
         const Rec* from = (lf.w ? out : in) + lf.x;
         const uint32_t h =
             bitonic_chunk<NT, CAP>(from, out + lf.x, lf.y, rl, k0, k1, aux, s_u32, &s_bad, s_min, s_tcnt);
@@ -4955,9 +4958,11 @@ hipError_t launch_giant_chunks(const Rec* d_in, Rec* d_out, const uint32_t* d_ch
     for (int p = 0; p < GIANT_PASSES; ++p)
         DBI_LAUNCH(k_giant_split, dim3(512), dim3(SPLIT_THREADS), 0, s, in, d_out, gl, p, d_ctr);
     DBI_LAUNCH((k_giant_leaf<CHUNK_THREADS, CHUNK_CAP>), dim3(2048), dim3(CHUNK_THREADS), 0, s, in, d_out,
-               gl.leaf_small, &d_ctr->n_leaf_small, gl.cap, d_res, d_poff, d_ucount, d_ctr);
+               gl.leaf_small, &d_ctr->n_leaf_small, gl.cap, d_res, d_poff, d_ucount, d_ctr, 0u);
+    DBI_LAUNCH((k_giant_leaf<BIG_THREADS / 2, BIG_CAP / 2>), dim3(512), dim3(BIG_THREADS / 2), 0, s, in, d_out,
+               gl.leaf_big, &d_ctr->n_leaf_big, gl.cap, d_res, d_poff, d_ucount, d_ctr, 0u);
     DBI_LAUNCH((k_giant_leaf<BIG_THREADS, BIG_CAP>), dim3(256), dim3(BIG_THREADS), 0, s, in, d_out, gl.leaf_big,
-               &d_ctr->n_leaf_big, gl.cap, d_res, d_poff, d_ucount, d_ctr);
+               &d_ctr->n_leaf_big, gl.cap, d_res, d_poff, d_ucount, d_ctr, (uint32_t)(BIG_CAP / 2));
     DBI_LAUNCH(k_giant_fallback, dim3(256), dim3(BIG_THREADS), 0, s, in, d_out, gl.fallback, gl.cap, d_res, d_poff,
                d_ucount, d_ws_key, d_ws_k2, d_ctr);
     return hipGetLastError();

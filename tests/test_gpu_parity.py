@@ -243,10 +243,23 @@ def _giant_near_isobaric(prm):
     return [f"MRGGGGGGGGGW{t}K" for t in tail]
 
 
-@pytest.mark.parametrize("kind", ["isobaric", "near_isobaric"])
+def _giant_duplicates():
+    """One isobaric spike of ~26k records made of six peptides repeated 3000
+    (four of them), 5000 and 9000 times: the split on the tag leaves
+    equal-(mass, tag) buckets of 3000 (big leaves of the 512-thread class),
+    5000 (the 1024-thread class) and 9000 (above BIG_CAP: the global-memory
+    fallback)."""
+    import itertools
+    perms = ["".join(p) for p in itertools.islice(itertools.permutations("ACDEFGHM"), 0, 40000, 6661)][:6]
+    counts = [3000, 3000, 3000, 3000, 5000, 9000]
+    return [f"MK{p}KWWR" for p, c in zip(perms, counts) for _ in range(c)]
+
+
+@pytest.mark.parametrize("kind", ["isobaric", "near_isobaric", "duplicates"])
 def test_giant_chunks(Engine, kind):
     prm = DBIndexSearchParams.trypsin(1)
-    seqs = _giant_isobaric() if kind == "isobaric" else _giant_near_isobaric(prm)
+    seqs = _giant_isobaric() if kind == "isobaric" else _giant_near_isobaric(prm) if kind == "near_isobaric" \
+        else _giant_duplicates()
     pp = fasta.PackedProteins.from_sequences(seqs)
     oix = _check(Engine, prm, pp, f"giant {kind}", nq=800)
     assert oix.n_kept > 8000
