@@ -3918,9 +3918,10 @@ hipError_t launch_ptm_digest(bool emit, const DevParams& dp, const double* d_mas
 // t0 + k*NT + tid), so every load/store instruction is coalesced and all loads
 // of a round are in flight together; unique slots come from per-(k, wave)
 // ballot counts.  Protein id, offset and length come out of the record itself.
-constexpr uint32_t FIN_THREADS = 256;
-constexpr uint32_t FIN_ITEMS = 4;  // one round = 1024 records ~ one chunk
-
+// 512 threads x 4 records a round: one round covers a whole chunk (1280-1536
+// records, pairs up to ~2000); 256 x 4 took two rounds for most chunks
+// (SwissProt finalize 0.44 -> 0.40 ms; DBI_FIN picks another shape for A/B)
+template <uint32_t FIN_THREADS, uint32_t FIN_ITEMS>
 __global__ void __launch_bounds__(FIN_THREADS)
 k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
            double* __restrict__ umass, uint32_t* __restrict__ upid, uint32_t* __restrict__ uoff,
@@ -3978,14 +3979,18 @@ k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, 
             if (lane_id() == 0) wc[k * NW + w] = (uint32_t)__popcll(bal);
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (uint32_t q = 0; q < FIN_ITEMS * NW; ++q) {
-                const uint32_t t = wc[q];
-                wc[q] = acc;
-                acc += t;
+        if (threadIdx.x < 64) {  // exclusive scan of the (k, wave) head counts in wave 0
+            constexpr uint32_t NQ = FIN_ITEMS * NW;
+            static_assert(NQ <= 64, "one lane per (k, wave)");
+            const uint32_t v = threadIdx.x < NQ ? wc[threadIdx.x] : 0u;
+            uint32_t incl = v;
+#pragma unroll
+            for (uint32_t d = 1; d < NQ; d <<= 1) {
+                const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+                if (threadIdx.x >= d) incl += o;
             }
-            s_tot = acc;
+            if (threadIdx.x < NQ) wc[threadIdx.x] = incl - v;
+            if (threadIdx.x == NQ - 1) s_tot = incl;
         }
         __syncthreads();
 #pragma unroll
@@ -4020,8 +4025,19 @@ hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32
                            uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, uint32_t cstride,
                            uint32_t n_kept, const unsigned long long* d_n, Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return launch_write_tail(d_occ_off, n_kept, d_ctr, s, d_n);
-    DBI_LAUNCH(k_finalize, dim3(nchunks), dim3(FIN_THREADS), 0, s, d_recs, d_chunk_lo, d_ubase, d_umass, d_upid,
-               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, cstride, n_kept, d_n, d_ctr);
+    static const int variant = [] {
+        const char* e = std::getenv("DBI_FIN");
+        return e ? std::atoi(e) : 0;
+    }();
+#define DBI_FIN_LAUNCH(NT, K)                                                                                  \
+    DBI_LAUNCH((k_finalize<NT, K>), dim3(nchunks), dim3(NT), 0, s, d_recs, d_chunk_lo, d_ubase, d_umass, d_upid, \
+               d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, cstride, n_kept, d_n, d_ctr)
+    switch (variant) {
+        case 1: DBI_FIN_LAUNCH(256, 4); break;  // round 3's shape
+        case 2: DBI_FIN_LAUNCH(256, 8); break;
+        default: DBI_FIN_LAUNCH(512, 4); break;
+    }
+#undef DBI_FIN_LAUNCH
     return hipGetLastError();
 }
 
