@@ -3918,9 +3918,11 @@ hipError_t launch_ptm_digest(bool emit, const DevParams& dp, const double* d_mas
 // t0 + k*NT + tid), so every load/store instruction is coalesced and all loads
 // of a round are in flight together; unique slots come from per-(k, wave)
 // ballot counts.  Protein id, offset and length come out of the record itself.
-// 512 threads x 4 records a round: one round covers a whole chunk (1280-1536
+// 256 threads x 8 records a round: one round covers a whole chunk (1280-1536
 // records, pairs up to ~2000); 256 x 4 took two rounds for most chunks
-// (SwissProt finalize 0.44 -> 0.40 ms; DBI_FIN picks another shape for A/B)
+// (SwissProt finalize 0.44 -> 0.40 ms, semi-tryptic 8.6 -> 7.8 ms; 512 x 4
+// is as fast at SwissProt scale but not at semi's; DBI_FIN picks another
+// shape for A/B)
 template <uint32_t FIN_THREADS, uint32_t FIN_ITEMS>
 __global__ void __launch_bounds__(FIN_THREADS)
 k_finalize(const Rec* __restrict__ recs, const uint32_t* __restrict__ chunk_lo, const uint32_t* __restrict__ ubase,
@@ -4034,8 +4036,8 @@ hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32
                d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, cstride, n_kept, d_n, d_ctr)
     switch (variant) {
         case 1: DBI_FIN_LAUNCH(256, 4); break;  // round 3's shape
-        case 2: DBI_FIN_LAUNCH(256, 8); break;
-        default: DBI_FIN_LAUNCH(512, 4); break;
+        case 2: DBI_FIN_LAUNCH(512, 4); break;
+        default: DBI_FIN_LAUNCH(256, 8); break;
     }
 #undef DBI_FIN_LAUNCH
     return hipGetLastError();

@@ -59,6 +59,8 @@ CONTAINS = [
     ("OwnerDigit", "owner_partition"),
     ("PairDigit", "query_route"),
     ("k_giant_", "chunk_sort_giant"),
+    ("k_finalize", "finalize"),  # k_finalize<NT, ITEMS> since round 4
+    ("k_chunk_sort_list<512, 3968", "chunk_sort_big"),  # the big tier's smaller size class
     ("k_digest_bounded", "digest"),
     ("k_digest_count_cuts", "digest_count"),
     ("k_synth_", "synth"),
