@@ -4933,13 +4933,148 @@ k_giant_leaf(const Rec* in, Rec* out, const uint4* __restrict__ list, const unsi
     }
 }
 
-// segments of one (mass, tag) key above BIG_CAP: global-memory scratch
+// segments of one (mass, tag) key above BIG_CAP.  Up to FB_LDS records: the
+// peptide repeated that often (semi-tryptic: one segment of ~9 000 records)
+// is ordered by q1 alone -- q0 and the tag byte are the segment's -- in LDS
+// (bitonic over the 8-B q1), its neighbours string-verified, and written with
+// the one head; a segment holding more than one string (a 16-bit tag
+// collision) or more records takes the global-memory path (process_chunk:
+// (key, q1, index) bitonic in scratch, regroup by string).  The global path
+// alone took 2.6 ms for the one 9 000-record segment (a single block, every
+// bitonic step an L2 round trip).
+constexpr uint32_t FB_LDS = 16384;
+constexpr uint32_t FB_GROUPS = 64;  // string groups of one segment (hash table slots; at most half used)
+
+// 64-bit hash of a peptide string (dword loads realigned to the string start,
+// as seq_equal_at): equal strings hash equal whatever their alignment
+__device__ __forceinline__ uint64_t seq_hash(const uint8_t* __restrict__ res, uint32_t g, uint32_t len) {
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(res) & 3u);
+    const uint32_t* __restrict__ w = reinterpret_cast<const uint32_t*>(res - mis);
+    const uint64_t ga = (uint64_t)g + mis;
+    const uint64_t first = ga >> 2, last = (ga + len - 1) >> 2;
+    const uint32_t sh = (uint32_t)(ga & 3u);
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ len;
+    for (uint32_t k = 0; k < len; k += 4) {
+        const uint64_t q = first + (k >> 2);
+        const uint32_t x = __builtin_amdgcn_alignbyte(w[min(q + 1, last)], w[q], sh);
+        const uint32_t rem = len - k;
+        h = (h ^ (rem >= 4 ? x : x & ((1u << (8 * rem)) - 1u))) * 0xFF51AFD7ED558CCDull;
+        h ^= h >> 32;
+    }
+    return h;
+}
+
+// see k_giant_fallback; true when the segment was written (block-uniform)
+__device__ bool fb_regroup(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t a, uint32_t m, uint64_t q0,
+                           const RecLoc& rl, const unsigned long long* s_q, uint8_t* s_gid, unsigned long long* s_gh,
+                           uint32_t* s_glead, uint32_t* s_gcnt, uint32_t* s_gbase, uint32_t* s_grun, uint32_t* s_gtile,
+                           uint16_t (*s_wc)[FB_GROUPS], uint32_t* s_ng, uint32_t* s_bad, uint32_t* ucount) {
+    constexpr uint32_t NT = BIG_THREADS, NW = NT / 64;
+    constexpr unsigned long long EMPTY = ~0ull;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    for (uint32_t x = tid; x < FB_GROUPS; x += NT) {
+        s_gh[x] = EMPTY;
+        s_glead[x] = ~0u;
+        s_gcnt[x] = 0;
+        s_grun[x] = 0;
+    }
+    if (tid == 0) {
+        *s_ng = 0;
+        *s_bad = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += NT) {
+        const uint64_t q1 = s_q[i];
+        const unsigned long long h = seq_hash(rl.res, rl.gstart(q1), q1_len(q1, rl.w)) & ~(1ull << 63);  // never EMPTY
+        uint32_t sl = (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> 58), p = 0;
+        for (; p < FB_GROUPS; ++p, sl = (sl + 1) & (FB_GROUPS - 1)) {
+            const unsigned long long cur = s_gh[sl];
+            if (cur == h) break;
+            if (cur == EMPTY) {
+                const unsigned long long prev = atomicCAS(&s_gh[sl], EMPTY, h);
+                if (prev == EMPTY) {
+                    atomicAdd(s_ng, 1u);
+                    break;
+                }
+                if (prev == h) break;
+            }
+        }
+        if (p == FB_GROUPS) {
+            *s_bad = 1;
+            sl = 0;
+        }
+        s_gid[i] = (uint8_t)sl;
+        atomicMin(&s_glead[sl], i);
+        atomicAdd(&s_gcnt[sl], 1u);
+    }
+    __syncthreads();
+    if (*s_bad == 0 && *s_ng <= FB_GROUPS / 2)
+        for (uint32_t i = tid; i < m; i += NT) {
+            const uint32_t ld = s_glead[s_gid[i]];
+            if (ld != i && !rl.same(Rec{q0, s_q[i]}, Rec{q0, s_q[ld]})) *s_bad = 1;  // a hash clash
+        }
+    __syncthreads();
+    const bool ok = *s_bad == 0 && *s_ng <= FB_GROUPS / 2;
+    if (!ok) {
+        __syncthreads();  // every thread read s_bad / s_ng before the global path reuses nothing of this
+        return false;
+    }
+    if (tid < FB_GROUPS) {  // groups in first-appearance order
+        uint32_t base = 0;
+        if (s_gcnt[tid])
+            for (uint32_t t = 0; t < FB_GROUPS; ++t) base += (s_gcnt[t] && s_glead[t] < s_glead[tid]) ? s_gcnt[t] : 0u;
+        s_gbase[tid] = base;
+    }
+    __syncthreads();
+    // stable placement by group, one NT-record tile at a time (wave ranks in order)
+    for (uint32_t t0 = 0; t0 < m; t0 += NT) {
+        const uint32_t i = t0 + tid;
+        const bool valid = i < m;
+        const uint32_t g = valid ? s_gid[i] : 0u;
+        s_wc[w][lane] = 0;
+        wave_sync();
+        const uint64_t peers = digit_peers(g, valid, 6);
+        const uint32_t r = (uint32_t)__popcll(peers & lanemask_lt());
+        if (valid && r == 0) s_wc[w][g] = (uint16_t)__popcll(peers);
+        __syncthreads();
+        if (tid < FB_GROUPS) {
+            uint32_t acc = 0;
+            for (uint32_t ww = 0; ww < NW; ++ww) {
+                const uint32_t c = s_wc[ww][tid];
+                s_wc[ww][tid] = (uint16_t)acc;
+                acc += c;
+            }
+            s_gtile[tid] = acc;
+        }
+        __syncthreads();
+        if (valid) {
+            const uint32_t pos = s_gbase[g] + s_grun[g] + s_wc[w][g] + r;
+            out[a + pos] = Rec{(q0 & ~0xFFull) | (pos == s_gbase[g] ? 1ull : 0ull), s_q[i]};
+        }
+        __syncthreads();
+        if (tid < FB_GROUPS) s_grun[tid] += s_gtile[tid];
+        __syncthreads();
+    }
+    if (tid == 0) atomicAdd(ucount, *s_ng);
+    __syncthreads();
+    (void)in;
+    return true;
+}
+
 __global__ void __launch_bounds__(BIG_THREADS)
 k_giant_fallback(Rec* in, Rec* out, const uint4* __restrict__ list, uint32_t cap, const uint8_t* __restrict__ res,
                  const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount, unsigned long long* ws_key,
                  uint32_t* ws_k2, Counters* __restrict__ ctr) {
     __shared__ uint32_t s_u32[BIG_THREADS / 64 + 1];
     __shared__ unsigned long long s_flag;
+    __shared__ unsigned long long s_q[FB_LDS];
+    // string regroup of a collision segment: group of each record, hash table,
+    // per-group leader (first position) / count / base / running count, per-(wave, group) tile counts
+    __shared__ uint8_t s_gid[FB_LDS];
+    __shared__ unsigned long long s_gh[FB_GROUPS];
+    __shared__ uint32_t s_glead[FB_GROUPS], s_gcnt[FB_GROUPS], s_gbase[FB_GROUPS], s_grun[FB_GROUPS], s_gtile[FB_GROUPS];
+    __shared__ uint16_t s_wc[BIG_THREADS / 64][FB_GROUPS];
+    __shared__ uint32_t s_ng, s_bad;
     const uint32_t nl = min(ctr->n_fallback, cap);
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
@@ -4948,6 +5083,59 @@ k_giant_fallback(Rec* in, Rec* out, const uint4* __restrict__ list, uint32_t cap
         if (sg.w) {  // lives in out: move it back to in (free there) so out is written once
             for (uint32_t i = threadIdx.x; i < m; i += BIG_THREADS) in[a + i] = out[a + i];
             __syncthreads();
+        }
+        if (m <= FB_LDS) {
+            const Rec r0 = in[a];
+            uint32_t P2 = 1;
+            while (P2 < m) P2 <<= 1;
+            bool diff = false;
+            for (uint32_t i = threadIdx.x; i < P2; i += BIG_THREADS) {
+                unsigned long long q = ~0ull;  // padding sorts last
+                if (i < m) {
+                    const Rec r = in[a + i];
+                    diff |= r.q0 != r0.q0 || (r.q1 >> 56) != (r0.q1 >> 56);
+                    q = r.q1;
+                }
+                s_q[i] = q;
+            }
+            if (threadIdx.x == 0) s_flag = 0;
+            if (!__syncthreads_or(diff)) {  // one (mass, tag) key (block-uniform)
+                for (uint32_t k = 2; k <= P2; k <<= 1) {
+                    for (uint32_t h = k >> 1; h > 0; h >>= 1) {
+                        for (uint32_t i = threadIdx.x; i < P2; i += BIG_THREADS) {
+                            const uint32_t ix = i ^ h;
+                            if (ix > i) {
+                                const unsigned long long x = s_q[i], y = s_q[ix];
+                                if (((i & k) == 0) ? x > y : x < y) {
+                                    s_q[i] = y;
+                                    s_q[ix] = x;
+                                }
+                            }
+                        }
+                        __syncthreads();
+                    }
+                }
+                for (uint32_t i = threadIdx.x + 1; i < m; i += BIG_THREADS)
+                    if (!rl.same(Rec{r0.q0, s_q[i]}, Rec{r0.q0, s_q[i - 1]})) s_flag = 1;
+                __syncthreads();
+                const bool one_string = s_flag == 0;
+                if (one_string) {
+                    for (uint32_t i = threadIdx.x; i < m; i += BIG_THREADS)
+                        out[a + i] = Rec{(r0.q0 & ~0xFFull) | (i == 0 ? 1ull : 0ull), s_q[i]};
+                    if (threadIdx.x == 0) atomicAdd(&ucount[sg.z], 1u);
+                }
+                __syncthreads();  // every thread read s_flag / s_q before the next use
+                if (one_string) continue;
+                // several strings (a tag collision): group by a string hash in
+                // LDS, verify every record against its group's first one,
+                // groups in first-appearance order, q1 order inside a group
+                // (what process_chunk's regroup computes with an O(n^2) leader
+                // search); more than FB_GROUPS / 2 strings or a hash clash
+                // between different strings: the global path
+                if (fb_regroup(in, out, a, m, r0.q0, rl, s_q, s_gid, s_gh, s_glead, s_gcnt, s_gbase, s_grun,
+                               s_gtile, s_wc, &s_ng, &s_bad, ucount + sg.z))
+                    continue;
+            }
         }
         unsigned long long* key = ws_key + 4ull * a;
         unsigned long long* hsh = key + 2ull * m;

@@ -146,7 +146,7 @@ inline BinMap make_binmap(double lo, double hi, uint32_t nbins) {
 }
 
 constexpr int HIST_MAX_BUCKETS = 64;  // dbi_count_buckets: index_factor (NUM_BUCKETS) at most
-constexpr int GIANT_PASSES = 3;  // MSD split passes over chunks above BIG_CAP (then the global-memory fallback)
+constexpr int GIANT_PASSES = 5;  // MSD split passes over chunks above BIG_CAP (then the global-memory fallback)
 
 // Device counters block (one per engine), read back once per build.
 struct Counters {

@@ -255,11 +255,38 @@ def _giant_duplicates():
     return [f"MK{p}KWWR" for p, c in zip(perms, counts) for _ in range(c)]
 
 
-@pytest.mark.parametrize("kind", ["isobaric", "near_isobaric", "duplicates"])
+def _giant_collision():
+    """Two different peptides with bit-identical mass AND equal 16-bit tag,
+    4 000 + 5 000 + 1 000 occurrences in mixed order: one equal-(mass, tag)
+    segment above BIG_CAP holding two strings -- the fallback's LDS path
+    finds the collision and hands the segment to the global-memory regroup."""
+    import collections
+    import itertools
+    from dbindex_amd.params import calculate_mass
+    from oracle.pyref import peptide_tag
+    prm = DBIndexSearchParams.trypsin(0)
+    groups = collections.defaultdict(list)
+    for perm in itertools.permutations("ACDEFGHM"):
+        pep = "".join(perm) + "K"
+        groups[(np.float64(calculate_mass(pep, prm)).view(np.uint64).item(), peptide_tag(pep))].append(pep)
+        if len(groups[next(reversed(groups))]) == 2:
+            break
+    a, b = next(v for v in groups.values() if len(v) == 2)
+    return [a] * 4000 + [b] * 5000 + [a] * 1000
+
+
+def _giant_one_peptide():
+    """One peptide 17 000 times (beyond the fallback's 16 384-record LDS
+    sort: the global-memory path) beside a 9 000-record one (the LDS path)."""
+    return ["ACDEFGHMK"] * 17000 + ["MHGFEDCAK"] * 9000
+
+
+@pytest.mark.parametrize("kind", ["isobaric", "near_isobaric", "duplicates", "collision", "one_peptide"])
 def test_giant_chunks(Engine, kind):
     prm = DBIndexSearchParams.trypsin(1)
     seqs = _giant_isobaric() if kind == "isobaric" else _giant_near_isobaric(prm) if kind == "near_isobaric" \
-        else _giant_duplicates()
+        else _giant_duplicates() if kind == "duplicates" else _giant_collision() if kind == "collision" \
+        else _giant_one_peptide()
     pp = fasta.PackedProteins.from_sequences(seqs)
     oix = _check(Engine, prm, pp, f"giant {kind}", nq=800)
     assert oix.n_kept > 8000

@@ -2,7 +2,7 @@
 # tools/gpu_round.sh TAG [what...] — one GPU-box session: parity tests, bench,
 # rocprofv3 kernel trace + stats, HBM counter passes.  Every GPU step has its
 # own time limit; the script stops at the first failure.
-#   what: tests smoke bench bench_h prof pmc pmc_sq (default: tests bench prof)
+#   what: tests smoke bench bench_h prof prof_semi pmc pmc_sq (default: tests bench prof)
 set -u -o pipefail
 TAG=${1:-r}
 shift || true
@@ -31,6 +31,9 @@ for w in $WHAT; do
     prof)  export TMPDIR=/tmp
            step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
                 -- python3 bench.py --steps 10 --warmup 2 --queries 0 --no-cpu-baseline ;;
+    prof_semi) export TMPDIR=/tmp
+           step prof_semi 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_semi" -o run \
+                -- python3 bench.py --config semi --steps 4 --warmup 5 --queries 0 --no-cpu-baseline ;;
     pmc)   export TMPDIR=/tmp
            step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
                 -- python3 bench.py --steps 3 --warmup 1 --queries 0 --no-cpu-baseline
