@@ -4770,6 +4770,7 @@ __global__ void k_giant_init(const uint32_t* __restrict__ giant_list, const uint
 }
 
 constexpr int SPLIT_THREADS = 1024;
+constexpr uint32_t SPLIT_ITEMS = 4;  // records per thread in a scatter tile
 
 __global__ void __launch_bounds__(SPLIT_THREADS)
 k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__ ctr) {
@@ -4780,6 +4781,9 @@ k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__
     __shared__ unsigned long long s_lo0[SPLIT_THREADS / 64], s_hi0[SPLIT_THREADS / 64];
     __shared__ uint32_t s_lo1[SPLIT_THREADS / 64], s_hi1[SPLIT_THREADS / 64];
     __shared__ uint32_t s_shift, s_same;
+    __shared__ uint4 s_ent[256];  // a segment's new list entries, their list (0 small leaf, 1 big leaf,
+    __shared__ uint8_t s_kind[256];  // 2 next pass, 3 fallback) and rank in it
+    __shared__ uint32_t s_rank[256], s_base[4], s_ne;
     const uint32_t nseg = ctr->n_seg[pass];
     const bool last = pass + 1 == GIANT_PASSES;
     for (uint32_t j = blockIdx.x; j < nseg; j += gridDim.x) {
@@ -4789,10 +4793,19 @@ k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__
         Rec* __restrict__ to = seg.w ? in : out;
         // min / max of the 72-bit key over the segment
         unsigned __int128 kmin = ~(unsigned __int128)0, kmax = 0;
-        for (uint32_t i = threadIdx.x; i < n; i += SPLIT_THREADS) {
-            const unsigned __int128 x = key72(from[lo + i]);
-            kmin = x < kmin ? x : kmin;
-            kmax = x > kmax ? x : kmax;
+        for (uint32_t t0 = 0; t0 < n; t0 += SPLIT_THREADS * SPLIT_ITEMS) {
+            Rec r[SPLIT_ITEMS];  // all loads of a round in flight together
+#pragma unroll
+            for (uint32_t k = 0; k < SPLIT_ITEMS; ++k) {
+                const uint32_t i = min(t0 + k * SPLIT_THREADS + threadIdx.x, n - 1);  // (a repeat is harmless)
+                r[k] = from[lo + i];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < SPLIT_ITEMS; ++k) {
+                const unsigned __int128 x = key72(r[k]);
+                kmin = x < kmin ? x : kmin;
+                kmax = x > kmax ? x : kmax;
+            }
         }
 #pragma unroll
         for (int d = 32; d > 0; d >>= 1) {
@@ -4834,17 +4847,37 @@ k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__
             continue;
         }
         const uint32_t sh = s_shift;
-        for (uint32_t i = threadIdx.x; i < n; i += SPLIT_THREADS)
-            atomicAdd(&cnt[(uint32_t)(key72(from[lo + i]) >> sh) & 0xFFu], 1u);
+        // digit counts: one LDS add per distinct digit of a wave (a spike's
+        // records share a few digits: per-record adds serialise on them)
+        for (uint32_t t0 = 0; t0 < n; t0 += SPLIT_THREADS * SPLIT_ITEMS) {
+            Rec r[SPLIT_ITEMS];
+#pragma unroll
+            for (uint32_t k = 0; k < SPLIT_ITEMS; ++k) {
+                const uint32_t i = t0 + k * SPLIT_THREADS + threadIdx.x;
+                r[k] = i < n ? from[lo + i] : Rec{0, 0};
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < SPLIT_ITEMS; ++k) {
+                const bool valid = t0 + k * SPLIT_THREADS + threadIdx.x < n;
+                const uint32_t d = valid ? (uint32_t)(key72(r[k]) >> sh) & 0xFFu : 0u;
+                const uint64_t peers = digit_peers(d, valid, 8);
+                if (valid && (peers & lanemask_lt()) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
+            }
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
-            // offsets + the next work list / leaves (adjacent small buckets packed)
-            uint32_t acc = 0, leaf_lo = 0, leaf_n = 0;
+            // offsets + the next work list / leaves (adjacent small buckets
+            // packed), collected in LDS; one reservation per list below (a
+            // global atomic per entry from this one thread cost ~0.1 ms a segment)
+            uint32_t acc = 0, leaf_lo = 0, leaf_n = 0, ne = 0;
+            auto emit = [&](uint4 e, uint32_t kind) {
+                s_ent[ne] = e;
+                s_kind[ne] = (uint8_t)kind;
+                ++ne;
+            };
             auto flush = [&]() {
                 if (leaf_n == 0) return;
-                const uint4 lf = make_uint4(lo + leaf_lo, leaf_n, seg.z, seg.w ^ 1u);
-                if (leaf_n <= (uint32_t)CHUNK_CAP) seg_push(gl.leaf_small, &ctr->n_leaf_small, gl.cap, lf, ctr);
-                else seg_push(gl.leaf_big, &ctr->n_leaf_big, gl.cap, lf, ctr);
+                emit(make_uint4(lo + leaf_lo, leaf_n, seg.z, seg.w ^ 1u), leaf_n <= (uint32_t)CHUNK_CAP ? 0u : 1u);
                 leaf_n = 0;
             };
             for (uint32_t d = 0; d < 256; ++d) {
@@ -4853,9 +4886,7 @@ k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__
                 if (c == 0) continue;
                 if (c > (uint32_t)BIG_CAP) {
                     flush();
-                    const uint4 ws = make_uint4(lo + acc, c, seg.z, seg.w ^ 1u);
-                    if (last) seg_push(gl.fallback, &ctr->n_fallback, gl.cap, ws, ctr);
-                    else seg_push(gl.work[pass + 1], &ctr->n_seg[pass + 1], gl.cap, ws, ctr);
+                    emit(make_uint4(lo + acc, c, seg.z, seg.w ^ 1u), last ? 3u : 2u);
                 } else if (c > (uint32_t)CHUNK_CAP) {
                     flush();
                     leaf_lo = acc;
@@ -4869,38 +4900,69 @@ k_giant_split(Rec* in, Rec* out, GiantLists gl, int pass, Counters* __restrict__
                 acc += c;
             }
             flush();
+            uint32_t nk[4] = {0, 0, 0, 0};
+            for (uint32_t e = 0; e < ne; ++e) s_rank[e] = nk[s_kind[e]]++;
+            unsigned int* const ctrs[4] = {&ctr->n_leaf_small, &ctr->n_leaf_big, &ctr->n_seg[min(pass + 1, GIANT_PASSES)],
+                                           &ctr->n_fallback};
+            for (uint32_t k = 0; k < 4; ++k) s_base[k] = nk[k] ? atomicAdd(ctrs[k], nk[k]) : 0u;
+            s_ne = ne;
         }
         __syncthreads();
-        // stable scatter, one block-wide tile at a time (per-wave ballot ranks,
-        // waves in order): the leaves keep the arrival order -- first
-        // appearance -- so the compact-key sort applies to them
-        for (uint32_t t0 = 0; t0 < n; t0 += SPLIT_THREADS) {
-            const uint32_t i = t0 + threadIdx.x;
-            const bool valid = i < n;
-            Rec r{0, 0};
-            uint32_t d = 0;
-            if (valid) {
-                r = from[lo + i];
-                d = (uint32_t)(key72(r) >> sh) & 0xFFu;
-            }
-            const uint64_t peers = digit_peers(d, valid, 8);
-            const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-            if (valid && rank == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
-            __syncthreads();
-            uint32_t at = cur[d] + rank;
-            for (uint32_t q = 0; q < w; ++q) at += wcnt[q][d];
-            __syncthreads();
-            if (valid) to[lo + at] = r;
-            if (threadIdx.x < 256) {
-                uint32_t add = 0;
-                for (uint32_t q = 0; q < SPLIT_THREADS / 64; ++q) {
-                    add += wcnt[q][threadIdx.x];
-                    wcnt[q][threadIdx.x] = 0;
-                }
-                cur[threadIdx.x] += add;
-            }
-            __syncthreads();
+        if (threadIdx.x < s_ne) {
+            const uint32_t e = threadIdx.x, k = s_kind[e], at = s_base[k] + s_rank[e];
+            uint4* const lists[4] = {gl.leaf_small, gl.leaf_big, gl.work[min(pass + 1, GIANT_PASSES)], gl.fallback};
+            if (at < gl.cap) lists[k][at] = s_ent[e];
+            else atomicOr(&ctr->err, ERR_SEGS);
         }
+        // stable scatter, SPLIT_ITEMS x SPLIT_THREADS records a tile: wave w
+        // ranks the contiguous records [w * 64 * SPLIT_ITEMS, +64 * SPLIT_ITEMS)
+        // of the tile in order (its digit counts in wcnt[w], no block barrier
+        // between items), one scan over the waves per digit, then the stores:
+        // the leaves keep the arrival order -- first appearance -- so the
+        // compact-key sort applies to them (two barriers per 4096 records; one
+        // tile of 1024 with three cost pass 0 of the semi-tryptic split 2.4 ms)
+        const uint32_t lane = lane_id();
+        for (uint32_t t0 = 0; t0 < n; t0 += SPLIT_THREADS * SPLIT_ITEMS) {
+            const uint32_t wb = t0 + w * 64 * SPLIT_ITEMS;
+            Rec r[SPLIT_ITEMS];
+            uint32_t dr[SPLIT_ITEMS];  // digit | rank in the wave's digit << 8
+#pragma unroll
+            for (uint32_t k = 0; k < SPLIT_ITEMS; ++k) {
+                const uint32_t i = wb + k * 64 + lane;
+                r[k] = i < n ? from[lo + i] : Rec{0, 0};
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < SPLIT_ITEMS; ++k) {
+                const uint32_t i = wb + k * 64 + lane;
+                const bool valid = i < n;
+                const uint32_t d = valid ? (uint32_t)(key72(r[k]) >> sh) & 0xFFu : 0u;
+                const uint64_t peers = digit_peers(d, valid, 8);
+                const uint32_t before = wcnt[w][d];
+                wave_sync();
+                if (valid && (peers & lanemask_lt()) == 0) wcnt[w][d] = before + (uint32_t)__popcll(peers);
+                wave_sync();
+                dr[k] = valid ? d | ((before + (uint32_t)__popcll(peers & lanemask_lt())) << 8) : ~0u;
+            }
+            __syncthreads();
+            if (threadIdx.x < 256) {  // per digit: the waves' bases in order, then the next tile's start
+                uint32_t acc = cur[threadIdx.x];
+                for (uint32_t q = 0; q < SPLIT_THREADS / 64; ++q) {
+                    const uint32_t c = wcnt[q][threadIdx.x];
+                    wcnt[q][threadIdx.x] = acc;
+                    acc += c;
+                }
+                cur[threadIdx.x] = acc;
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t k = 0; k < SPLIT_ITEMS; ++k)
+                if (dr[k] != ~0u) to[lo + wcnt[w][dr[k] & 0xFFu] + (dr[k] >> 8)] = r[k];
+            wave_sync();  // this wave's bases read: clear its row for the next tile
+#pragma unroll
+            for (uint32_t x = lane; x < 256; x += 64) wcnt[w][x] = 0;
+            wave_sync();
+        }
+        __syncthreads();  // cur / cnt / wcnt reused by the next segment
     }
 }
 
