@@ -2232,14 +2232,20 @@ k_radix_hist(const Rec* __restrict__ in, uint32_t n, Digit dig, int bits, uint32
 // of them -- every load in flight together -- into LDS counters [digit][chunk].  One
 // chunk per block was 13 k blocks of 512 threads at SwissProt scale, ~51 us a
 // pass for 54 MB of digits: dispatch, not bytes.
+// WAVE_ROWS: every wave counts into its own row of 16-bit counters (two per
+// word: a wave adds at most 64 x 8 to one (digit, chunk)), summed over the
+// waves at the end -- the block-shared counters took ~9 conflict cycles per
+// LDS instruction (SQ, r04y).
 constexpr uint32_t HIST_U8_PER_MAX = 8;
+template <bool WAVE_ROWS>
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t* __restrict__ hist, uint32_t G,
                 uint32_t per, const unsigned long long* __restrict__ dn) {
-    __shared__ uint32_t cnt[HIST_U8_PER_MAX * RADIX_D];
+    constexpr uint32_t ROW = HIST_U8_PER_MAX * RADIX_D / 2;  // words of one wave's packed row
+    __shared__ uint32_t cnt[WAVE_ROWS ? RADIX_NW * ROW : HIST_U8_PER_MAX * RADIX_D];
     if (dn) n = (uint32_t)min((unsigned long long)n, *dn);
     const uint32_t D = 1u << bits;
-    for (uint32_t i = threadIdx.x; i < per * D; i += RADIX_THREADS) cnt[i] = 0;
+    for (uint32_t i = threadIdx.x; i < (WAVE_ROWS ? RADIX_NW * ROW : per * D); i += RADIX_THREADS) cnt[i] = 0;
     static_assert(RADIX_ITEMS == 8, "one 8-B load per thread and chunk");
     const uint32_t c0 = xcd_contiguous_block() * per;
     uint2 v[HIST_U8_PER_MAX];
@@ -2262,18 +2268,34 @@ k_radix_hist_u8(const uint8_t* __restrict__ dig, uint32_t n, int bits, uint32_t*
         }
     }
     __syncthreads();
+    uint32_t* const row = cnt + (WAVE_ROWS ? (threadIdx.x >> 6) * ROW : 0u);
 #pragma unroll
     for (uint32_t j = 0; j < HIST_U8_PER_MAX; ++j) {
 #pragma unroll
         for (uint32_t k = 0; k < RADIX_ITEMS; ++k) {
             const uint32_t d = ((k < 4 ? v[j].x : v[j].y) >> (8 * (k & 3))) & 0xFFu;
-            if (k < nv[j]) atomicAdd(&cnt[d * per + j], 1u);
+            if (k < nv[j]) {
+                if constexpr (WAVE_ROWS) {
+                    const uint32_t x = d * per + j;
+                    atomicAdd(&row[x >> 1], 1u << (16 * (x & 1)));
+                } else {
+                    atomicAdd(&cnt[d * per + j], 1u);
+                }
+            }
         }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < per * D; i += RADIX_THREADS) {
         const uint32_t d = i / per, j = i - d * per;  // consecutive threads: one row's consecutive chunks
-        if (c0 + j < G) hist[(size_t)d * G + c0 + j] = cnt[i];
+        uint32_t t;
+        if constexpr (WAVE_ROWS) {
+            t = 0;
+#pragma unroll
+            for (uint32_t ww = 0; ww < RADIX_NW; ++ww) t += (cnt[ww * ROW + (i >> 1)] >> (16 * (i & 1))) & 0xFFFFu;
+        } else {
+            t = cnt[i];
+        }
+        if (c0 + j < G) hist[(size_t)d * G + c0 + j] = t;
     }
 }
 
@@ -2415,8 +2437,16 @@ hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
     const uint32_t per = std::min<uint32_t>(HIST_U8_PER_MAX, std::max<uint32_t>(1u, g / 2048u));
-    DBI_LAUNCH(k_radix_hist_u8, dim3((g + per - 1) / per), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist, g, per,
-               d_n);
+    static const bool rows = [] {
+        const char* e = std::getenv("DBI_HIST_ROWS");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    if (rows)
+        DBI_LAUNCH(k_radix_hist_u8<true>, dim3((g + per - 1) / per), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist,
+                   g, per, d_n);
+    else
+        DBI_LAUNCH(k_radix_hist_u8<false>, dim3((g + per - 1) / per), dim3(RADIX_THREADS), 0, s, d_dig, n, bits,
+                   d_hist, g, per, d_n);
     return hipGetLastError();
 }
 

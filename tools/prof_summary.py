@@ -60,6 +60,7 @@ CONTAINS = [
     ("PairDigit", "query_route"),
     ("k_giant_", "chunk_sort_giant"),
     ("k_finalize", "finalize"),  # k_finalize<NT, ITEMS> since round 4
+    ("k_radix_hist_u8", "radix_hist_u8"),
     ("k_chunk_sort_list<512, 3968", "chunk_sort_big"),  # the big tier's smaller size class
     ("k_digest_bounded", "digest"),
     ("k_digest_count_cuts", "digest_count"),
