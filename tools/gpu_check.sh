@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --t
 tail -1 "$OUT/t.log"
 for c in $CFGS; do
   steps=20; [ $c = semi ] && steps=5; [ $c = trembl ] && steps=3
-  timeout -k 10 600 python bench.py --config $c --steps $steps --warmup 3 > "$OUT/$c.json" 2> "$OUT/$c.err" || { tail -20 "$OUT/$c.err"; exit 1; }
+  timeout -k 10 600 python bench.py --config $c --steps $steps --warmup 5 > "$OUT/$c.json" 2> "$OUT/$c.err" || { tail -20 "$OUT/$c.err"; exit 1; }
   python3 -c "import json; d=json.load(open('$OUT/$c.json')); print('$c', round(d['ms_per_step'],3), '%.3g' % d['value'], [(k['kernel'], round(k['ms_per_build'],3)) for k in d['kernels']][:8])"
 done
 echo CHECK_DONE

@@ -25,9 +25,9 @@ for w in $WHAT; do
     case $w in
     tests) step tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) step bench 600 python bench.py --steps 20 --warmup 3
+    bench) step bench 600 python bench.py --steps 20 --warmup 5
            cp "$OUT/bench.log" "$OUT/bench.json" ;;
-    bench_h) step bench_h 600 python bench.py --config human --steps 20 --warmup 3 ;;
+    bench_h) step bench_h 600 python bench.py --config human --steps 20 --warmup 5 ;;
     prof)  export TMPDIR=/tmp
            step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
                 -- python3 bench.py --steps 10 --warmup 2 --queries 0 --no-cpu-baseline ;;
