@@ -102,6 +102,7 @@ def main() -> None:
                     help="--config trembl: proteins of the whole synthetic proteome (split over the ranks)")
     ap.add_argument("--queries", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold / end-to-end legs")
     ap.add_argument("--no-merge", action="store_true",
                     help="N>1: shard-local indexes (no exchange) instead of one merged index")
     ap.add_argument("--merge", action="store_true", help="N=1: run the sharded (RCCL) build with one rank")
@@ -395,6 +396,13 @@ def main() -> None:
         counts = dc.download(np.uint64, nq).astype(np.float64)
         qps["materialised"] = hits_leg(eng, dm, dt, nq, counts)
 
+    cold = None
+    if rank == 0 and world == 1 and not merge and not args.no_cold:
+        # the reference's real use is a one-off build (DBIndexer.run): the cold
+        # pipeline (no capacities, grids, map or graph from earlier builds),
+        # and FASTA file -> index end to end
+        cold = cold_legs(eng, prm, pp, d_res, d_off, dev, args.config)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # reference-semantics CPU restatement (oracle/cpu_ref.cpp) on a bounded
@@ -402,7 +410,9 @@ def main() -> None:
         # then row ranges) and single-threaded like the reference
         sample = pp.slice(0, min(cpu_sample, pp.n_proteins))
         cpu = cpu_baseline_legs(prm, sample)
-        cpu["sample_parity"] = sample_parity(prm, sample, cpu.pop("_oix"), dev)
+        oix = cpu.pop("_oix")
+        cpu["queries"] = cpu_query_legs(oix, args.queries or 1_000_000)
+        cpu["sample_parity"] = sample_parity(prm, sample, oix, dev)
 
     from dbindex_amd._native import runtime_info
     runtime = runtime_info()  # raises if two HIP runtimes / RCCLs are mapped
@@ -486,6 +496,8 @@ def main() -> None:
                             "roofline.kernel (the longest launch) is re-timed inside the timed region",
             "sharded_phases": phases,
             "queries": qps,
+            # the one-off build: cold pipeline, first build with allocations, FASTA file -> index
+            "cold": cold,
             "cpu_baseline": cpu,
             # the HIP runtime and RCCL this process runs on (one of each: checked)
             "runtime": runtime,
@@ -538,6 +550,100 @@ def cpu_baseline_legs(prm, sample) -> dict:
                 single_core=dict(value=oix.n_total / t_one, unit="peptides indexed/s", cores=1, kind="port",
                                  seconds=t_one, sample=f"{desc}, one thread (the reference's threading)"),
                 _oix=oix)
+
+
+def cold_legs(eng, prm, pp, d_res, d_off, dev: int, config: str) -> dict:
+    """The one-off build (DBIndexer.java:508-684) beside the warm steady state:
+    cold_ms -- this engine forced cold (dbi_set_cold: count + emit digest,
+    radix tail, full list grids; buffers kept), best of 3; first_build_ms -- a
+    fresh engine's first build (its allocations included); end_to_end -- a
+    FASTA file of the proteome written to a temporary directory (untimed),
+    then dbi_fasta_read (multi-threaded parser) + a fresh engine's dbi_build
+    (H2D of residues and offsets + the cold build), SURVEY.md §8(d)."""
+    import tempfile
+    from dbindex_amd import fasta
+    from dbindex_amd._native import synchronize
+    from dbindex_amd.engine import Engine
+
+    def build_dev(e):
+        return e.build_device(d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins)
+
+    eng.set_timing(False)
+    ts = []
+    for _ in range(3):
+        eng.set_cold()
+        synchronize(dev)
+        t = time.perf_counter()
+        st = build_dev(eng)
+        synchronize(dev)
+        ts.append(1e3 * (time.perf_counter() - t))
+    out = dict(cold_ms=min(ts), cold_ms_runs=ts, peptides=st.n_total,
+               cold_peptides_per_s=st.n_total / (min(ts) * 1e-3),
+               cold_kind="dbi_set_cold on the benched engine: count + emit digest, radix tail, full list grids "
+                         "(device buffers kept)")
+    if st.n_total > 200_000_000:  # (semi-tryptic: a second engine's ~100 GB would not fit beside this one)
+        out["first_build_ms"] = out["end_to_end"] = None
+        out["note"] = "fresh-engine legs skipped: a second index of this size does not fit beside the benched one"
+        return out
+    with Engine(prm, device=dev) as e2:
+        e2.set_timing(False)
+        synchronize(dev)
+        t = time.perf_counter()
+        build_dev(e2)
+        synchronize(dev)
+        out["first_build_ms"] = 1e3 * (time.perf_counter() - t)
+    # end to end: FASTA text -> packed proteome -> index
+    threads = host_threads()
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, f"{config}.fasta")
+        t = time.perf_counter()
+        with open(path, "w") as fh:
+            fasta.write_fasta(pp, fh)
+        write_s = time.perf_counter() - t
+        size = os.path.getsize(path)
+        t0 = time.perf_counter()
+        rp = fasta.read_fasta(path, threads=threads, with_defs=False)
+        t1 = time.perf_counter()
+        with Engine(prm, device=dev) as e3:
+            e3.set_timing(False)
+            st3 = e3.build(rp)
+            synchronize(dev)
+        t2 = time.perf_counter()
+    same = rp.n_proteins == pp.n_proteins and rp.n_residues == pp.n_residues and st3.n_total == st.n_total
+    out["end_to_end"] = dict(ms=1e3 * (t2 - t0), fasta_read_ms=1e3 * (t1 - t0), build_ms=1e3 * (t2 - t1),
+                             fasta_bytes=size, fasta_write_s_untimed=write_s, parser_threads=threads,
+                             peptides_per_s=st3.n_total / (t2 - t0), same_proteome=bool(same),
+                             kind="dbi_fasta_read of the written FASTA, then a fresh engine's dbi_build "
+                                  "(host residues: H2D + cold build, allocations included)")
+    return out
+
+
+def cpu_query_legs(oix, nq: int) -> dict:
+    """getSequences(m, tol) windows (DBIndexer.java:762-844 ->
+    IndexMerge.getSequences :146-217, as oracle/cpu_ref.cpp restates them) over
+    the CPU sample's index: the same +-20 ppm query mix, all cores and one."""
+    from oracle import cref
+    rng = np.random.Generator(np.random.PCG64(7))
+    ex = oix.unique()["mass"]
+    k = int(nq * 0.9)
+    m = np.empty(nq)
+    m[:k] = ex[rng.integers(0, ex.shape[0], k)] * (1 + rng.normal(0, 5e-6, k))
+    m[k:] = rng.uniform(500, 6000, nq - k)
+    tol = m * (1 - 1 / (20.0 / 1e6 + 1))
+    nthreads = host_threads()
+    with cref.threads(nthreads):
+        t = time.perf_counter()
+        _, cnt = oix.query_batch(m, tol)
+        t_all = time.perf_counter() - t
+    n1 = min(nq, 200_000)  # one thread: a bounded share of the same windows
+    t = time.perf_counter()
+    oix.query_batch(m[:n1], tol[:n1])
+    t_one = time.perf_counter() - t
+    return dict(value=nq / t_all, unit="queries/s", cores=nthreads, kind="port", queries=nq,
+                avg_hits=float(cnt.mean()), seconds=t_all,
+                sample=f"{nq} +-20 ppm windows over the sample's index ({oix.n_unique} unique peptides): "
+                       "oracle/cpu_ref.cpp getSequences restatement, (first, count) per window",
+                single_core=dict(value=n1 / t_one, unit="queries/s", cores=1, queries=n1, seconds=t_one))
 
 
 def sample_parity(prm, sample, oix, dev: int) -> dict:

@@ -112,6 +112,7 @@ SIGNATURES = [
     ("dbi_entry_keys", c_int, [P, P, c_uint64, POINTER(c_uint64)]),
     ("dbi_device_view", c_int, [P, POINTER(DbiDeviceIndex)]),
     ("dbi_set_timing", c_int, [P, c_int, c_char_p]),
+    ("dbi_set_cold", c_int, [P]),
     ("dbi_set_bucket_drop", c_int, [P, c_int]),
     ("dbi_set_windows", c_int, [P, P, P, c_uint64, c_int]),
     ("dbi_rebuild", c_int, [P]),

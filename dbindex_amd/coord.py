@@ -76,6 +76,7 @@ class Coordinator:
             try:
                 while len(by_rank) < world - 1:
                     conn, _ = srv.accept()
+                    conn.settimeout(None)
                     conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                     ln = _Line(conn)
                     by_rank[int(ln.recv()["rank"])] = ln
@@ -109,6 +110,9 @@ class Coordinator:
                     if time.time() > t_end:
                         raise TimeoutError(f"rank {rank}: no coordinator at {self.path} after {timeout:.0f} s")
                     time.sleep(0.05)
+            # the connect timeout must not carry over to the collectives: a rank
+            # that connected near the end of the wait would time out in them
+            sock.settimeout(None)
             sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             self.root = _Line(sock)
             self.root.send({"rank": rank})

@@ -963,9 +963,12 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
                     phi = cs.p(q);
                     plo = cs.p(q - 1u);
                 } else {
-                    phi = a == 0u ? v[k][1] : a == 1u ? v[k][2] : v[k][3];
-                    plo = a == 0u ? v[k][0] : a == 1u ? v[k][1] : a == 2u ? v[k][2] : v[k][3];
-                    q = min(q + a, qhi + 1u);
+                    // q' = q + d, clamped to qhi + 1: plo = p[q' - 1] = v[d], phi = p[q'] = v[d + 1]
+                    // (read only when q' <= qhi, where d = a <= 2)
+                    const uint32_t d = min(a, qhi + 1u - q);
+                    phi = d == 0u ? v[k][1] : d == 1u ? v[k][2] : v[k][3];
+                    plo = d == 0u ? v[k][0] : d == 1u ? v[k][1] : d == 2u ? v[k][2] : v[k][3];
+                    q += d;
                 }
                 ht.t[k] = q;
                 if (q <= qhi && phi - upb < t + (uint32_t)CUT_EPS_FX) bad = true;
@@ -1047,6 +1050,9 @@ __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nby
             cs.p(i) = (uint32_t)__double2ull_rn(mrun * CUT_SCALE);
         }
     }
+    // the slack words past the window read as "above every threshold" (the
+    // tracked bucket boundaries load p[q + 1], p[q + 2] unclamped)
+    if (threadIdx.x < 4) cs.p(nbytes + threadIdx.x) = 0xFFFFFFFFu;
     __syncthreads();
 }
 
@@ -1624,14 +1630,93 @@ __device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const LeanSmem
     return r;
 }
 
+// ---- depth bins: the digest's partition ------------------------------------
+__device__ __forceinline__ uint32_t depth_bin(double m, const DepthMap& dm) { return dm.tab[bin_of(m, dm.sub)]; }
+
+// the XCD this wave runs on (HW_REG_XCC_ID, bits 3:0; MI355X_MICROARCH.md: blockIdx % 8 only says
+// which blocks share one)
+__device__ __forceinline__ uint32_t xcc_id() {
+    return (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & (DEPTH_XCDS - 1u);
+}
+
+// The tile's records (slots [0, n) of src, just written by this block:
+// L2-resident) into the regions of their bins' high digits: 1024 slots a
+// round, each record's rank inside its digit from an LDS counter, one global
+// atomic per digit present reserves the tile's run in region (digit, this
+// block's XCD) -- the runs of one XCD's tiles are neighbours in its regions, so
+// its L2 merges their partial lines -- and the records go there with their
+// bins' low digits (pass 2 counts those bytes).  A region that would overflow
+// takes nothing and flags the build (ERR_PART: redone by the radix tail).
+// The records never go back through a full radix pass of their own: this is
+// the first pass, fused.
+constexpr uint32_t PART_ITEMS = 8;
+__device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32_t n, uint32_t* s_cnt,
+                          uint32_t* s_gof, Counters* __restrict__ ctr) {
+    const uint32_t tid = threadIdx.x, xcd = xcc_id(), D1 = 1u << po.b1;
+    const uint32_t b2 = po.dm.b2, m2 = (1u << b2) - 1u;
+    const uint4* __restrict__ src4 = reinterpret_cast<const uint4*>(src);
+    uint4* __restrict__ out4 = reinterpret_cast<uint4*>(po.recs);
+    // every record of the tile acknowledged by the L2 before the barrier: the
+    // other waves read the slots back (from the L2: the lines were never in
+    // this CU's L1).  (__threadfence() would write the L2 back to HBM per tile.)
+    __builtin_amdgcn_s_waitcnt(0);
+    for (uint32_t r0 = 0; r0 < n; r0 += DIGEST_THREADS * PART_ITEMS) {
+        __syncthreads();  // the tile's slots written (first round); the last round's counters read
+        if (tid < D1) s_cnt[tid] = 0;
+        uint4 rv[PART_ITEMS];
+#pragma unroll
+        for (uint32_t k = 0; k < PART_ITEMS; ++k)  // clamped: every load in flight together
+            rv[k] = src4[min(r0 + k * DIGEST_THREADS + tid, n - 1u)];
+        __syncthreads();
+        uint32_t bin[PART_ITEMS], rk[PART_ITEMS];
+#pragma unroll
+        for (uint32_t k = 0; k < PART_ITEMS; ++k) {
+            bin[k] = ~0u;
+            rk[k] = 0;
+            if (r0 + k * DIGEST_THREADS + tid < n && (rv[k].x & rv[k].y) != 0xFFFFFFFFu) {  // not a sentinel
+                bin[k] = depth_bin(u4_mass(rv[k]), po.dm);
+                rk[k] = atomicAdd(&s_cnt[bin[k] >> b2], 1u);
+            }
+        }
+        __syncthreads();
+        if (tid < D1) {
+            const uint32_t c = s_cnt[tid];
+            uint32_t g = ~0u;
+            if (c) {
+                const uint32_t r = tid * DEPTH_XCDS + xcd;
+                // the region's cursor is this XCD's alone (its own 1-KiB row, cur[xcd][digit]): the add runs
+                // in this XCD's L2 (workgroup scope: no trip to the memory-side atomics); the kernel's end
+                // writes it back.  A wrong XCD id would lose adds: k_part_plan checks the cursors' sum.
+                const uint32_t o = __hip_atomic_fetch_add(&po.cur[xcd * 256u + tid], c, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (o + c <= po.cap) g = r * po.cap + o;
+                else atomicOr(&ctr->err, ERR_PART);
+            }
+            s_gof[tid] = g;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < PART_ITEMS; ++k) {
+            if (bin[k] != ~0u) {
+                const uint32_t g = s_gof[bin[k] >> b2];
+                if (g != ~0u) {
+                    out4[g + rk[k]] = rv[k];
+                    po.dig[g + rk[k]] = (uint8_t)(bin[k] & m2);
+                }
+            }
+        }
+    }
+}
+
 // H1: with the first radix histogram (Hist1; 80 VGPRs kept for 6 waves per
-// SIMD, where the LDS puts the blocks)
-template <bool DROP, bool H1>
+// SIMD, where the LDS puts the blocks).  PART: the records are partitioned by
+// the depth bins' high digit afterwards (part_tile; the slots are scratch).
+template <bool DROP, bool H1, bool PART = false>
 __global__ void __launch_bounds__(DIGEST_THREADS) __attribute__((amdgpu_waves_per_eu(H1 ? 6 : 1, 8)))
 k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                  const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
                  uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, Rec* __restrict__ d_out, uint64_t cap,
-                 Counters* __restrict__ d_ctr, Hist1 h1) {
+                 Counters* __restrict__ d_ctr, Hist1 h1, PartOut po) {
     __shared__ LeanSmem sm;
     __shared__ uint32_t s_kept, s_waves, s_dup;
     __shared__ unsigned long long s_base;
@@ -1878,12 +1963,16 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
             if (v && c < h1.G) atomicAdd(&h1.g[(size_t)(i & ((1u << h1.bits) - 1u)) * h1.G + c], v);
         }
     }
+    if constexpr (PART) {  // the candidate list is dead: the partition's counters
+        uint32_t* p_cnt = reinterpret_cast<uint32_t*>(sm.cand);
+        part_tile(po, d_out + base, tile_slots, p_cnt, p_cnt + 256, d_ctr);
+    }
 }
 
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                  const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s,
-                                 const Hist1Plan* h1p) {
+                                 const Hist1Plan* h1p, const PartOut* part) {
     const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     if (nblk == 0) return hipSuccess;
     if (dp.semi || dp.mand_mode || dp.max_missed + 2 > LD_ENDS) return hipErrorInvalidValue;
@@ -1892,16 +1981,25 @@ hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, 
         if (h1p->bits < 1 || h1p->bits > RADIX_BITS || (uint64_t)h1p->G * RADIX_CHUNK_D < cap) return hipErrorInvalidValue;
         h1 = Hist1{h1p->hist, h1p->bm, (uint32_t)h1p->bits, h1p->G};
     }
-#define DBI_DIGEST_B(DROP, H1)                                                                                    \
-    DBI_LAUNCH((k_digest_bounded<DROP, H1>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, d_res, \
-               d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr, h1)
+    PartOut po{};
+    if (part) {
+        if (h1p || part->b1 < 1 || part->b1 > 8 || part->dm.b2 < 1 || part->dm.b2 > RADIX_BITS || part->cap % 64)
+            return hipErrorInvalidValue;
+        po = *part;
+    }
+#define DBI_DIGEST_B(DROP, H1, PART)                                                                                \
+    DBI_LAUNCH((k_digest_bounded<DROP, H1, PART>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, \
+               d_res, d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr, h1, po)
     const bool drop = dp.drop_mass <= dp.max_mh;
-    if (h1p) {
-        if (drop) DBI_DIGEST_B(true, true);
-        else DBI_DIGEST_B(false, true);
+    if (part) {
+        if (drop) DBI_DIGEST_B(true, false, true);
+        else DBI_DIGEST_B(false, false, true);
+    } else if (h1p) {
+        if (drop) DBI_DIGEST_B(true, true, false);
+        else DBI_DIGEST_B(false, true, false);
     } else {
-        if (drop) DBI_DIGEST_B(true, false);
-        else DBI_DIGEST_B(false, false);
+        if (drop) DBI_DIGEST_B(true, false, false);
+        else DBI_DIGEST_B(false, false, false);
     }
 #undef DBI_DIGEST_B
     return hipGetLastError();
@@ -2480,6 +2578,311 @@ hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, co
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// 4'. depth bins (warm lean builds): the map, the pass-2 plan, the pass over
+// the low digit, the chunk bounds.  See PartOut / part_tile.
+// ---------------------------------------------------------------------------
+// ns uniques of the previous index, evenly spaced, each weighted by its
+// occurrences, into the linear sub-bins (d_sub zeroed)
+__global__ void k_depth_sample(const double* __restrict__ umass, const uint32_t* __restrict__ occ_off, uint64_t nu,
+                               uint32_t ns, BinMap sub, uint32_t* __restrict__ d_sub) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ns) return;
+    const uint64_t j = (uint64_t)i * nu / ns;
+    const uint32_t w = occ_off[j + 1] - occ_off[j];
+    if (w && w <= (1u << 24)) atomicAdd(&d_sub[bin_of(umass[j], sub)], w);  // (a stale index: never a wild weight)
+}
+
+hipError_t launch_depth_sample(const double* d_umass, const uint32_t* d_occ_off, uint64_t n_unique, uint32_t ns,
+                               const BinMap& sub, uint32_t* d_sub, hipStream_t s) {
+    ns = (uint32_t)std::min<uint64_t>(ns, n_unique);
+    if (ns == 0) return hipSuccess;
+    DBI_LAUNCH(k_depth_sample, dim3((ns + 255) / 256), dim3(256), 0, s, d_umass, d_occ_off, n_unique, ns, sub, d_sub);
+    return hipGetLastError();
+}
+
+// tab[s] = floor(weight before sub-bin s * nbins / total): non-decreasing, so
+// bin order is mass order; each bin ~total / nbins of the sampled weight (a
+// sub-bin heavier than that spans several bins' worth alone).  No sample:
+// the linear map.
+__global__ void k_depth_table(const uint32_t* __restrict__ pre, const Counters* __restrict__ ctr, uint32_t nsub,
+                              uint32_t nbins, int sub_bits, uint16_t* __restrict__ tab) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nsub) return;
+    const unsigned long long tot = ctr->depth_w;
+    const uint64_t b = tot ? (uint64_t)pre[s] * nbins / tot : ((uint64_t)s * nbins) >> sub_bits;
+    tab[s] = (uint16_t)min(b, (uint64_t)nbins - 1u);
+}
+
+hipError_t launch_depth_table(const uint32_t* d_sub_scan, const Counters* d_ctr, uint32_t nsub, uint32_t nbins,
+                              uint16_t* d_tab, hipStream_t s) {
+    if (nbins == 0 || nbins > 65536u || (nsub & (nsub - 1))) return hipErrorInvalidValue;
+    int sb = 0;
+    while ((1u << sb) < nsub) ++sb;
+    DBI_LAUNCH(k_depth_table, dim3((nsub + 255) / 256), dim3(256), 0, s, d_sub_scan, d_ctr, nsub, nbins, sb, d_tab);
+    return hipGetLastError();
+}
+
+// One block: region counts -> pass-2 chunks (PART_CHUNK-record pieces of each
+// region, digit-major, XCD, piece), the first chunk and chunk count of every
+// high digit, ctr->part_chunks; the records to sort (ctr->tail_n), or 0 when
+// the digest's slots or a region overflowed.
+__global__ void __launch_bounds__(256)
+k_part_plan(const uint32_t* __restrict__ cur, uint32_t cap, uint32_t b1, uint64_t slot_cap,
+            uint32_t* __restrict__ desc, uint32_t* __restrict__ d1c, Counters* __restrict__ ctr) {
+    __shared__ uint32_t s_tmp[256 / 64 + 1];
+    const uint32_t d = threadIdx.x, D1 = 1u << b1;
+    // every cursor's adds accounted for: the regions hold exactly the kept records
+    uint32_t placed = 0;
+    if (d < D1) {
+#pragma unroll
+        for (uint32_t x = 0; x < DEPTH_XCDS; ++x) placed += cur[x * 256u + d];
+    }
+    uint32_t all_placed;
+    block_excl_scan<256, uint32_t>(placed, s_tmp, all_placed);
+    const bool ok = ctr->n_slots <= slot_cap && !(ctr->err & ERR_PART) && all_placed == ctr->n_kept;
+    if (d == 0 && !(ctr->err & ERR_PART) && ctr->n_slots <= slot_cap && all_placed != ctr->n_kept)
+        atomicOr(&ctr->err, ERR_PART);  // (lost cursor adds: redone by the radix tail)
+    uint32_t nch = 0;
+    if (ok && d < D1) {
+#pragma unroll
+        for (uint32_t x = 0; x < DEPTH_XCDS; ++x) nch += (cur[x * 256u + d] + PART_CHUNK - 1) / PART_CHUNK;
+    }
+    uint32_t total;
+    uint32_t first = block_excl_scan<256, uint32_t>(nch, s_tmp, total);
+    if (d < D1) {
+        d1c[d] = first;
+        d1c[D1 + d] = nch;
+    }
+    if (ok && d < D1) {
+        for (uint32_t x = 0; x < DEPTH_XCDS; ++x) {
+            const uint32_t r = d * DEPTH_XCDS + x, k1 = (cur[x * 256u + d] + PART_CHUNK - 1) / PART_CHUNK;
+            for (uint32_t k = 0; k < k1; ++k) desc[first++] = r << 16 | k;
+        }
+    }
+    if (d == 0) {
+        ctr->part_chunks = total;
+        ctr->tail_n = ok ? ctr->n_kept : 0ull;
+        ctr->tail_in = ok ? ctr->n_kept : 0ull;
+    }
+}
+
+hipError_t launch_part_plan(const uint32_t* d_cur, uint32_t cap, uint32_t b1, uint64_t slot_cap, uint32_t* d_desc,
+                            uint32_t* d_d1c, Counters* d_ctr, hipStream_t s) {
+    if (b1 < 1 || b1 > 8 || cap / PART_CHUNK >= 65536u) return hipErrorInvalidValue;
+    DBI_LAUNCH(k_part_plan, dim3(1), dim3(256), 0, s, d_cur, cap, b1, slot_cap, d_desc, d_d1c, d_ctr);
+    return hipGetLastError();
+}
+
+// pass-2 chunk c: its records [*lo, *lo + *n) of the region buffer, its high
+// digit's first chunk and chunk count
+struct PartChunk {
+    uint32_t lo, n, first, nch;
+};
+__device__ __forceinline__ PartChunk part_chunk(uint32_t c, const uint32_t* __restrict__ cur, uint32_t cap,
+                                                const uint32_t* __restrict__ desc,
+                                                const uint32_t* __restrict__ d1c, uint32_t b1) {
+    const uint32_t r = desc[c] >> 16, k = desc[c] & 0xFFFFu, d1 = r / DEPTH_XCDS;
+    PartChunk pc;
+    pc.lo = r * cap + k * PART_CHUNK;
+    pc.n = min(PART_CHUNK, cur[(r % DEPTH_XCDS) * 256u + d1] - k * PART_CHUNK);
+    pc.first = d1c[d1];
+    pc.nch = d1c[(1u << b1) + d1];
+    return pc;
+}
+
+__device__ __forceinline__ uint32_t part_hidx(const PartChunk& pc, uint32_t c, uint32_t d2, uint32_t b2) {
+    return (pc.first << b2) + d2 * pc.nch + (c - pc.first);
+}
+
+// the low digits (bytes) of one chunk counted in per-wave LDS rows
+__global__ void __launch_bounds__(RADIX_THREADS)
+k_part_hist(const uint8_t* __restrict__ dig, const uint32_t* __restrict__ cur, uint32_t cap,
+            const uint32_t* __restrict__ desc, const uint32_t* __restrict__ d1c, uint32_t b1, uint32_t b2,
+            uint32_t* __restrict__ hist, const Counters* __restrict__ ctr) {
+    __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
+    const uint32_t c = xcd_contiguous_block();
+    if (c >= ctr->part_chunks) return;
+    const uint32_t w = threadIdx.x >> 6, D2 = 1u << b2;
+    for (uint32_t d = lane_id(); d < D2; d += 64) cnt[w][d] = 0;
+    const PartChunk pc = part_chunk(c, cur, cap, desc, d1c, b1);
+    static_assert(PART_CHUNK == RADIX_THREADS * 8, "one 8-B load per thread");
+    const uint32_t i0 = threadIdx.x * 8;
+    uint2 v = make_uint2(0u, 0u);
+    if (i0 < pc.n) v = *reinterpret_cast<const uint2*>(dig + pc.lo + i0);  // (lo and cap: multiples of 64)
+    wave_sync();
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k)
+        if (i0 + k < pc.n) atomicAdd(&cnt[w][((k < 4 ? v.x : v.y) >> (8 * (k & 3))) & 0xFFu], 1u);
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < D2; d += RADIX_THREADS) {
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t ww = 0; ww < (uint32_t)RADIX_NW; ++ww) t += cnt[ww][d];
+        hist[part_hidx(pc, c, d, b2)] = t;
+    }
+}
+
+hipError_t launch_part_hist(const uint8_t* d_dig, const uint32_t* d_cur, uint32_t cap, const uint32_t* d_desc,
+                            const uint32_t* d_d1c, uint32_t b1, uint32_t b2, uint32_t max_chunks, uint32_t* d_hist,
+                            const Counters* d_ctr, hipStream_t s) {
+    if (max_chunks == 0) return hipSuccess;
+    if (b2 < 1 || b2 > (uint32_t)RADIX_BITS) return hipErrorInvalidValue;
+    DBI_LAUNCH(k_part_hist, dim3(max_chunks), dim3(RADIX_THREADS), 0, s, d_dig, d_cur, cap, d_desc, d_d1c, b1, b2,
+               d_hist, d_ctr);
+    return hipGetLastError();
+}
+
+// The pass over the low digit: a chunk's records ranked per digit in input
+// order (wave ballots, as k_radix_scatter), exchanged through LDS and written
+// as digit runs to their (high digit, low digit) = bin place.
+__global__ void __launch_bounds__(RADIX_THREADS)
+k_part_scatter(const Rec* __restrict__ recs, const uint8_t* __restrict__ dig, const uint32_t* __restrict__ cur,
+               uint32_t cap, const uint32_t* __restrict__ desc, const uint32_t* __restrict__ d1c, uint32_t b1,
+               uint32_t b2, const uint32_t* __restrict__ offs, Rec* __restrict__ out,
+               const Counters* __restrict__ ctr) {
+    __shared__ uint16_t cnt[RADIX_NW][RADIX_D];
+    __shared__ uint4 stage[RADIX_CHUNK];
+    __shared__ uint8_t sdig[RADIX_CHUNK];
+    __shared__ uint32_t gofs[RADIX_D];
+    __shared__ uint32_t s_tmp[RADIX_NW + 1];
+    const uint32_t c = xcd_contiguous_block();
+    if (c >= ctr->part_chunks) return;
+    const uint32_t D2 = 1u << b2;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (uint32_t d = lane; d < D2; d += 64) cnt[w][d] = 0;
+    wave_sync();
+    const PartChunk pc = part_chunk(c, cur, cap, desc, d1c, b1);
+    const uint32_t base = w * (RADIX_ITEMS * 64);  // this wave's records, chunk-relative
+    const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(recs + pc.lo);
+    uint4 rv[RADIX_ITEMS];
+    uint32_t dd[RADIX_ITEMS];
+    if (base + RADIX_ITEMS * 64 <= pc.n) {  // wave-uniform: every load in flight together
+#pragma unroll
+        for (int k = 0; k < RADIX_ITEMS; ++k) rv[k] = in4[base + k * 64 + lane];
+#pragma unroll
+        for (int k = 0; k < RADIX_ITEMS; ++k) dd[k] = dig[pc.lo + base + k * 64 + lane];
+    } else {
+#pragma unroll
+        for (int k = 0; k < RADIX_ITEMS; ++k) {
+            const uint32_t i = base + k * 64 + lane;
+            rv[k] = i < pc.n ? in4[i] : make_uint4(0, 0, 0, 0);
+            dd[k] = i < pc.n ? (uint32_t)dig[pc.lo + i] : 0u;
+        }
+    }
+    const uint32_t goff = threadIdx.x < D2 ? offs[part_hidx(pc, c, threadIdx.x, b2)] : 0u;
+    uint32_t pos[RADIX_ITEMS];
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int k = 0; k < RADIX_ITEMS; ++k) {
+        const bool valid = base + k * 64 + lane < pc.n;
+        vmask |= (uint32_t)valid << k;
+        const uint32_t d = dd[k];
+        const uint64_t peers = digit_peers(d, valid, (int)b2);
+        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+        const uint32_t before = cnt[w][d];
+        wave_sync();
+        if (valid && rank == 0) cnt[w][d] = (uint16_t)(before + (uint32_t)__popcll(peers));
+        wave_sync();
+        pos[k] = before + rank;
+    }
+    __syncthreads();
+    const uint32_t d = threadIdx.x;
+    uint32_t tot = 0;
+    if (d < D2) {
+#pragma unroll
+        for (int ww = 0; ww < RADIX_NW; ++ww) tot += cnt[ww][d];
+    }
+    uint32_t nvalid;
+    const uint32_t lstart = block_excl_scan<RADIX_THREADS, uint32_t>(tot, s_tmp, nvalid);
+    if (d < D2) {
+        uint32_t acc = lstart;
+#pragma unroll
+        for (int ww = 0; ww < RADIX_NW; ++ww) {
+            const uint32_t t = cnt[ww][d];
+            cnt[ww][d] = (uint16_t)acc;
+            acc += t;
+        }
+        gofs[d] = goff - lstart;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RADIX_ITEMS; ++k) {
+        if (vmask & (1u << k)) {
+            const uint32_t at = cnt[w][dd[k]] + pos[k];
+            stage[at] = rv[k];
+            sdig[at] = (uint8_t)dd[k];
+        }
+    }
+    __syncthreads();
+    uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
+    for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) out4[gofs[sdig[t]] + t] = stage[t];
+}
+
+hipError_t launch_part_scatter(const Rec* d_recs, const uint8_t* d_dig, const uint32_t* d_cur, uint32_t cap,
+                               const uint32_t* d_desc, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
+                               uint32_t max_chunks, const uint32_t* d_offs, Rec* d_out, const Counters* d_ctr,
+                               hipStream_t s) {
+    if (max_chunks == 0) return hipSuccess;
+    if (b2 < 1 || b2 > (uint32_t)RADIX_BITS) return hipErrorInvalidValue;
+    DBI_LAUNCH(k_part_scatter, dim3(max_chunks), dim3(RADIX_THREADS), 0, s, d_recs, d_dig, d_cur, cap, d_desc, d_d1c,
+               b1, b2, d_offs, d_out, d_ctr);
+    return hipGetLastError();
+}
+
+// bin b = (d1, d2) starts at the pass-2 offset of its first chunk's run
+// (an empty high digit: where the next one starts); bstart[nbins] = records
+__global__ void k_depth_starts(const uint32_t* __restrict__ offs, const uint32_t* __restrict__ d1c, uint32_t b1,
+                               uint32_t b2, uint32_t* __restrict__ bstart, const Counters* __restrict__ ctr) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x, NB = 1u << (b1 + b2);
+    if (b > NB) return;
+    const uint32_t n = (uint32_t)ctr->tail_n;
+    if (b == NB || n == 0) {
+        bstart[b] = b == NB ? n : 0u;
+        return;
+    }
+    const uint32_t d1 = b >> b2, d2 = b & ((1u << b2) - 1u);
+    const uint32_t pos = (d1c[d1] << b2) + d2 * d1c[(1u << b1) + d1];
+    bstart[b] = pos < (ctr->part_chunks << b2) ? offs[pos] : n;
+}
+
+// chunk pairs over the bins (k_chunk_bounds' layout): chunk 2c = the bins
+// starting in [c*T, (c+1)*T), its last bin split off as chunk 2c+1 when the
+// two together exceed CHUNK_CAP (a bin above it is a big chunk of its own)
+__global__ void k_depth_chunks(const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t T, uint32_t nchunks,
+                               uint32_t* __restrict__ chunk_lo, const Counters* __restrict__ ctr) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > nchunks) return;
+    const uint32_t n = (uint32_t)ctr->tail_n;
+    auto first_ge = [&](uint32_t x) {  // first b in [0, nb] with bstart[b] >= x (bstart[nb] = n >= x)
+        uint32_t lo = 0, hi = nb;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (bstart[mid] >= x) hi = mid; else lo = mid + 1;
+        }
+        return lo;
+    };
+    const uint32_t x = c == nchunks ? n : (uint32_t)min((uint64_t)c * T, (uint64_t)n);
+    const uint32_t s0 = bstart[first_ge(x)];
+    chunk_lo[2 * c] = s0;
+    if (c == nchunks) return;
+    const uint32_t j1 = first_ge((uint32_t)min((uint64_t)(c + 1) * T, (uint64_t)n));
+    const uint32_t s1 = bstart[j1];
+    uint32_t split = s1;
+    if (s1 - s0 > (uint32_t)CHUNK_CAP && j1 > 0 && bstart[j1 - 1] > s0) split = bstart[j1 - 1];
+    chunk_lo[2 * c + 1] = split;
+}
+
+hipError_t launch_depth_bounds(const uint32_t* d_offs, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
+                               uint32_t* d_bstart, uint32_t T, uint32_t nchunks, uint32_t* d_chunk_lo,
+                               const Counters* d_ctr, hipStream_t s) {
+    const uint32_t nb = 1u << (b1 + b2);
+    DBI_LAUNCH(k_depth_starts, dim3((nb + 1 + 255) / 256), dim3(256), 0, s, d_offs, d_d1c, b1, b2, d_bstart, d_ctr);
+    DBI_LAUNCH(k_depth_chunks, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_bstart, nb, T, nchunks, d_chunk_lo,
+               d_ctr);
+    return hipGetLastError();
+}
+
 // Owner side of the exchange: the (global protein, offset, length) word of
 // each received occurrence -> its 16-B record, the mass and the tag
 // recomputed from the residues exactly as the digest walk sums them
@@ -2947,6 +3350,15 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     return v;
 }
 
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_xor(v, d, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
 __device__ __forceinline__ void ck_cx(uint64_t& a, uint64_t& b) {  // a: the lower index
     const bool gt = a > b;
     const uint64_t lo = gt ? b : a, hi = gt ? a : b;
@@ -3251,8 +3663,12 @@ __device__ __forceinline__ bool in_ranges(const uint32_t* wr, uint32_t nw, uint3
 template <int NT>
 __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLoc& rl, const unsigned long long* k0,
                                   const unsigned long long* k1, uint32_t* aux, uint32_t* s_u32, uint32_t* s_bad,
-                                  const uint32_t* wr = nullptr, uint32_t nw = 0) {
+                                  const uint32_t* wr = nullptr, uint32_t nw = 0, bool raw_skipped = false) {
     uint16_t* a16 = reinterpret_cast<uint16_t*>(aux);
+    if (raw_skipped) {  // local bins: the skipped ranges exist only here -- out as they are (tags whole), chunk_sort_mid sorts them there
+        for (uint32_t p = threadIdx.x; p < m; p += NT)
+            if (in_ranges(wr, nw, p)) out[p] = Rec{k0[p], k1[p]};
+    }
     if (threadIdx.x == 0) {
         *s_bad = 0;
         s_u32[NT / 64] = 0;  // number of equal (mass, tag) neighbour pairs
@@ -3358,9 +3774,19 @@ struct ChunkSmem {
     uint32_t wr[MAXW];   // lo | hi << 16: bins left to chunk_sort_mid
     uint32_t u32[NT / 64 + 1];
     uint64_t mins[NT / 64];
+    uint64_t maxs[NT / 64];       // local bins: per-wave mass-bit range
     uint16_t tcnt[NT / 64 * 16];  // tag_sort_block: per-wave digit counts, then their scan
     uint32_t nbig, nwide, bad;
 };
+
+// local bins of a depth-bin chunk: a power of two >= CAP / 2 (about one
+// record per bin at the chunk target), two 16-bit counters per word
+template <int CAP>
+constexpr uint32_t local_bins() {
+    uint32_t nl = 1;
+    while (nl < (uint32_t)CAP / 2) nl <<= 1;
+    return nl;
+}
 
 // Single-mass bins -- equal-mass spikes, every record of the bin with the same
 // fp64 mass (isobaric permutations and repeated peptides; the semi-tryptic
@@ -3456,7 +3882,13 @@ __device__ bool tag_sort_block(unsigned long long* k0, unsigned long long* k1, u
 // whole chunk, and the mid kernel loaded and ranked it all again).
 // ties: records may repeat exactly (host occurrences); ranks count equal keys
 // before the record too, so two copies never take one slot.
-template <int NT, int CAP, bool BLOCK>
+// LOCAL (depth-bin chunks, whole coarse bins in any order): the bins are the
+// chunk's own -- local_bins<CAP>() linear bins over the chunk's mass range
+// (block min / max of the mass bits), filled by an LDS counting sort whose
+// counters' scan gives every record its place and its bin's bounds at once
+// (in place of the fine bins' run detection); the wide bins are written to
+// `out` unsorted for chunk_sort_mid.
+template <int NT, int CAP, bool BLOCK, bool LOCAL = false>
 __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const BinMap& bm,
                            const RecLoc& rl, ChunkSmem<NT, CAP>& sm, uint32_t* heads_out, bool ties) {
     static_assert(CAP <= 65535, "16-bit positions");
@@ -3469,6 +3901,90 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         sm.nbig = 0;
         sm.nwide = 0;
     }
+    if constexpr (LOCAL) {
+        constexpr uint32_t NL = local_bins<CAP>(), NLW = NL / 2, WPT = (NLW + NT - 1) / NT;
+        static_assert(NLW * 4 <= CAP * 8, "the counters inside k0");
+        uint32_t* lc = reinterpret_cast<uint32_t*>(k0);  // k0 is free until the records land
+        const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
+        const uint32_t w = threadIdx.x >> 6;
+        uint4 rv[E];
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) rv[k] = in4[min(threadIdx.x + k * NT, m - 1u)];  // m >= 1
+        for (uint32_t i = threadIdx.x; i < NLW; i += NT) lc[i] = 0;
+        uint64_t mn = ~0ull, mx = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint64_t x = u4_q0(rv[k]) >> 8;  // the clamped duplicates change nothing
+            mn = x < mn ? x : mn;
+            mx = x > mx ? x : mx;
+        }
+        mn = wave_min_u64(mn);
+        mx = wave_max_u64(mx);
+        if (lane_id() == 0) {
+            sm.mins[w] = mn;
+            sm.maxs[w] = mx;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < NW; ++q) {
+            mn = sm.mins[q] < mn ? sm.mins[q] : mn;
+            mx = sm.maxs[q] > mx ? sm.maxs[q] : mx;
+        }
+        // bin = floor((x - mn) * NL / (range + 1)): non-decreasing in the mass
+        const double scale = (double)NL / ((double)(mx - mn) + 1.0);
+        uint32_t lr[E];  // local bin << 16 | rank in it (any order)
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            lr[k] = 0;
+            if (threadIdx.x + k * NT < m) {
+                const uint32_t b = min((uint32_t)((double)((u4_q0(rv[k]) >> 8) - mn) * scale), NL - 1u);
+                const uint32_t sh = 16u * (b & 1u);
+                lr[k] = (b << 16) | ((atomicAdd(&lc[b >> 1], 1u << sh) >> sh) & 0xFFFFu);
+            }
+        }
+        __syncthreads();
+        // exclusive scan of the counters in bin order; each word becomes the
+        // starts of its two bins
+        uint32_t wd[WPT], part = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < WPT; ++j) {
+            const uint32_t i = threadIdx.x * WPT + j;
+            wd[j] = i < NLW ? lc[i] : 0u;
+            part += (wd[j] & 0xFFFFu) + (wd[j] >> 16);
+        }
+        uint32_t tot;
+        uint32_t run = block_excl_scan<NT, uint32_t>(part, sm.u32, tot);
+#pragma unroll
+        for (uint32_t j = 0; j < WPT; ++j) {
+            const uint32_t i = threadIdx.x * WPT + j;
+            const uint32_t lo = wd[j] & 0xFFFFu;
+            if (i < NLW) lc[i] = run | ((run + lo) << 16);
+            run += lo + (wd[j] >> 16);
+        }
+        __syncthreads();
+        uint32_t se[E];  // the bin's start | end << 16
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint32_t b = lr[k] >> 16, b1 = b + 1;
+            const uint32_t st = (lc[b >> 1] >> (16u * (b & 1u))) & 0xFFFFu;
+            const uint32_t en = b1 < NL ? (lc[b1 >> 1] >> (16u * (b1 & 1u))) & 0xFFFFu : m;
+            se[k] = st | (en << 16);
+        }
+        __syncthreads();  // every counter read: k0 takes the records
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            if (threadIdx.x + k * NT < m) {
+                const uint32_t st = se[k] & 0xFFFFu, len = (se[k] >> 16) - st, rk = lr[k] & 0xFFFFu;
+                k0[st + rk] = u4_q0(rv[k]);
+                k1[st + rk] = u4_q1(rv[k]);
+                sm.aux[st + rk] = se[k];
+                if (rk == 0 && len > RANK_MAX_RUN) {  // one record per bin lists it
+                    if (!BLOCK && len > WAVE_SORT_MAX) sm.wr[atomicAdd(&sm.nwide, 1u)] = se[k];
+                    else sm.big[atomicAdd(&sm.nbig, 1u)] = se[k];
+                }
+            }
+        }
+    } else {
     {
         // all loads in flight before the first use (a Rec as 4 dwords: q0, q1)
         const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
@@ -3528,6 +4044,7 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
             if (lo0 + k < m) sm.aux[lo0 + k] = rlo[k] | (rhi[k] << 16);
         }
     }
+    }  // !LOCAL
     __syncthreads();
     // small bins: rank inside the bin (k-major: a wave's lanes share bins), kept in registers with the key
     // (ranking by a 64-bit compact key instead measured slower: the extra
@@ -3594,14 +4111,15 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         }
         __syncthreads();
     }
-    *heads_out = finish_sorted<NT>(out, m, rl, k0, k1, sm.aux, sm.u32, &sm.bad, sm.wr, BLOCK ? 0u : sm.nwide);
+    *heads_out = finish_sorted<NT>(out, m, rl, k0, k1, sm.aux, sm.u32, &sm.bad, sm.wr, BLOCK ? 0u : sm.nwide,
+                                   LOCAL && !BLOCK);
 }
 
 // One chunk of m <= CAP records sorted in LDS by the record key with the flip
 // bitonic network (cost independent of how the masses cluster), then
 // finish_sorted.  k0/k1/aux: CAP entries each.  Returns this thread's head count.
 template <int NT, int CAP>
-__device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const RecLoc& rl,
+__device__ uint32_t bitonic_chunk(const Rec* in, Rec* out, uint32_t m, const RecLoc& rl,
                                   unsigned long long* k0, unsigned long long* k1, uint32_t* aux, uint32_t* s_u32,
                                   uint32_t* s_bad, uint64_t* s_min, uint16_t* s_tcnt) {
     for (uint32_t i = threadIdx.x; i < m; i += NT) {
@@ -3624,17 +4142,57 @@ __device__ uint32_t bitonic_chunk(const Rec* __restrict__ in, Rec* __restrict__ 
 // straddling bin that is chunk c+1 -- to mid_list as (chunk, lo | hi << 16),
 // sorted by k_bin_sort_mid, which adds its heads to ucount[chunk].  LDS
 // 39 KiB at CAP 1984 and no block-level sort here: <= 64 VGPRs, 4 blocks per CU.
-template <int NT, int CAP>
+
+// One chunk c of k_chunk_sort: empty (no heads), above CAP (big_list), or
+// sorted here with its wide bins listed for chunk_sort_mid.
+template <int NT, int CAP, bool LOCAL>
+__device__ void chunk_sort_one(uint32_t c, const Rec* __restrict__ in, Rec* __restrict__ out, const BinMap& bm,
+                               const uint32_t* __restrict__ chunk_lo, const RecLoc& rl, uint32_t* __restrict__ ucount,
+                               uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, uint32_t ties,
+                               Counters* __restrict__ ctr, ChunkSmem<NT, CAP>& sm) {
+    const uint32_t a = chunk_lo[c];
+    const uint32_t m = chunk_lo[c + 1] - a;
+    if (m == 0) {
+        if (threadIdx.x == 0) ucount[c] = 0;
+        return;
+    }
+    if (m > (uint32_t)CAP) {
+        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
+        return;
+    }
+    uint32_t h = 0;
+    sort_chunk<NT, CAP, false, LOCAL>(in + a, out + a, m, bm, rl, sm, &h, ties != 0);
+    const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
+    if (threadIdx.x == 0) ucount[c] = tot;  // block_sum's barrier: before k_bin_sort_mid's adds (stream order)
+    if (threadIdx.x < sm.nwide) {
+        const uint32_t e = atomicAdd(&ctr->n_mid, 1u);
+        mid_list[2 * e] = c;
+        mid_list[2 * e + 1] = sm.wr[threadIdx.x];
+    }
+}
+
+#ifdef DBI_CLOCK_CHUNKS  // experiment builds: per-block clocks of k_chunk_sort (dbi_debug_chunk_clock)
+__device__ unsigned long long g_chunk_clock[1u << 18][2];
+#endif
+
+// One block per chunk pair (k_chunk_bounds / launch_depth_bounds).  Radix
+// tail: chunk 2c here, chunk 2c+1 (one big bin) to the list kernels.  LOCAL
+// (depth bins): both chunks of the pair here, one after the other (2c+1 is
+// empty unless the pair was split) -- one block per chunk instead put every
+// non-empty block on every other XCD (blocks go to the XCDs round-robin):
+// half the chip idle, 1.76 vs 0.82 ms.
+template <int NT, int CAP, bool LOCAL = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
              const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
              uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, uint32_t ties,
              Counters* __restrict__ ctr) {
     __shared__ ChunkSmem<NT, CAP> sm;
-    const uint32_t c = 2 * blockIdx.x;  // chunk pair (k_chunk_bounds): this block sorts chunk c
-    const uint32_t a = chunk_lo[c];
-    const uint32_t m = chunk_lo[c + 1] - a;
-    if (threadIdx.x == 0) {  // chunk c+1: empty, or one big bin for the list kernels
+    const uint32_t c = 2 * blockIdx.x;
+#ifdef DBI_CLOCK_CHUNKS
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (!LOCAL && threadIdx.x == 0) {  // chunk c+1: empty, or one big bin for the list kernels
         const uint32_t mb = chunk_lo[c + 2] - chunk_lo[c + 1];
         if (mb == 0) ucount[c + 1] = 0;
         else if (mb > (uint32_t)CAP) big_list[atomicAdd(&ctr->n_big, 1u)] = c + 1;
@@ -3645,24 +4203,21 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
             mid_list[2 * e + 1] = mb << 16;
         }
     }
-    if (m == 0) {
-        if (threadIdx.x == 0) ucount[c] = 0;
-        return;
-    }
-    if (m > (uint32_t)CAP) {
-        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
-        return;
-    }
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
-    uint32_t h = 0;
-    sort_chunk<NT, CAP, false>(in + a, out + a, m, bm, rl, sm, &h, ties != 0);
-    const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
-    if (threadIdx.x == 0) ucount[c] = tot;  // block_sum's barrier: before k_bin_sort_mid's adds (stream order)
-    if (threadIdx.x < sm.nwide) {
-        const uint32_t e = atomicAdd(&ctr->n_mid, 1u);
-        mid_list[2 * e] = c;
-        mid_list[2 * e + 1] = sm.wr[threadIdx.x];
+    chunk_sort_one<NT, CAP, LOCAL>(c, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr, sm);
+    if constexpr (LOCAL) {
+        __syncthreads();  // the LDS is the next chunk's
+        chunk_sort_one<NT, CAP, LOCAL>(c + 1, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr, sm);
     }
+#ifdef DBI_CLOCK_CHUNKS
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 18)) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        g_chunk_clock[blockIdx.x][0] = t_start | ((t1 - t_start) << 40);
+        g_chunk_clock[blockIdx.x][1] = (unsigned long long)(chunk_lo[c + 1] - chunk_lo[c]) |
+                                       ((unsigned long long)(chunk_lo[c + 2] - chunk_lo[c + 1]) << 32);
+    }
+#endif
 }
 
 // The big_list chunks k_chunk_sort listed: (CHUNK_CAP, BIG_CAP] records, 1024
@@ -3674,7 +4229,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
 // the LDS, two blocks per CU (SwissProt: 382 of 421 big chunks, semi-tryptic
 // most of them) -- the other class (SMALL false, BIG_CAP) every other entry;
 // a block whose entry is the other class's skips it.
-template <int NT, int CAP, bool SMALL = false>
+template <int NT, int CAP, bool SMALL = false, bool LOCAL = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
                   const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
@@ -3706,7 +4261,7 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
             }
         } else {
             uint32_t h = 0;
-            sort_chunk<NT, CAP, true>(in + a, out + a, m, bm, rl, sm, &h, ties != 0);
+            sort_chunk<NT, CAP, true, LOCAL>(in + a, out + a, m, bm, rl, sm, &h, ties != 0);
             const uint32_t tot = block_sum<NT, uint32_t>(h, sm.u32);
             if (threadIdx.x == 0) {
                 ucount[c] = tot;
@@ -3738,7 +4293,7 @@ k_chunk_sort_list(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, 
 // (5 728 of SwissProt's 7 310 mid bins) -- the rest in 512-thread blocks.
 template <int NT, int CAP, uint32_t LMIN>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DBI_MID_WPE, 8)))
-k_bin_sort_mid(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t* __restrict__ chunk_lo,
+k_bin_sort_mid(const Rec* in, Rec* out, const uint32_t* __restrict__ chunk_lo,  // in == out: depth-bin builds
                const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
                const uint32_t* __restrict__ list, Counters* __restrict__ ctr) {
     __shared__ unsigned long long k0[CAP];
@@ -3764,7 +4319,7 @@ k_bin_sort_mid(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t
         }
     }
     // entries past the grid (ERR_GRID, redone): the bin unsorted, no heads
-    for (uint32_t e = j + gridDim.x; e < n; e += gridDim.x) {
+    for (uint32_t e = j + gridDim.x; e < n && in != out; e += gridDim.x) {
         const uint32_t c = list[2 * e], r = list[2 * e + 1];
         const uint32_t a = chunk_lo[c] + (r & 0xFFFFu), L = (r >> 16) - (r & 0xFFFFu);
         if (L <= LMIN || L > (uint32_t)CAP) continue;
@@ -3774,12 +4329,26 @@ k_bin_sort_mid(const Rec* __restrict__ in, Rec* __restrict__ out, const uint32_t
 
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
-                             uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s) {
+                             uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s,
+                             bool local) {
     if (nchunks == 0) return hipSuccess;
-    DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
-                       d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr);
+    if (local)
+        DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP, true>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
+                   d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr);
+    else
+        DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
+                   d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr);
     return hipGetLastError();
 }
+
+#ifdef DBI_CLOCK_CHUNKS
+}  // namespace dbi
+extern "C" int dbi_debug_chunk_clock(unsigned long long* out, unsigned long long n) {
+    if (n > (1ull << 18)) n = 1ull << 18;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dbi::g_chunk_clock), n * 16, 0, hipMemcpyDeviceToHost);
+}
+namespace dbi {
+#endif
 
 hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
@@ -3799,7 +4368,8 @@ constexpr uint32_t BIG_SPLIT_CUS = 256;  // MI355X compute units
 hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
-                                 uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s, int split_mode) {
+                                 uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s, int split_mode,
+                                 bool local) {
     if (max_blocks == 0) return hipSuccess;
     constexpr int SMALL_BIG = BIG_CAP / 2;  // 3968 records: 512 threads, 2 blocks per CU
     const uint32_t sa = std::min<uint32_t>(split_above, (uint32_t)BIG_CAP);
@@ -3809,13 +4379,19 @@ hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, 
     // (0.15 -> 0.24 ms measured); semi-tryptic's ~70 k: 18.0 -> 15.4 ms
     // (split_mode: DBI_BIG_SPLIT, 0 never / 1 always, for the tests; -1 by the list length)
     const bool split = split_mode < 0 ? max_blocks > 4u * BIG_SPLIT_CUS : split_mode != 0;
-    if (split)
-        DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS / 2, SMALL_BIG, true>), dim3(max_blocks), dim3(BIG_THREADS / 2), 0,
-                   s, d_in, d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list, sa,
-                   ties ? 1u : 0u, d_ctr, (uint32_t)SMALL_BIG);
-    DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS, BIG_CAP>), dim3(max_blocks), dim3(BIG_THREADS), 0, s, d_in,
-               d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list, sa, ties ? 1u : 0u, d_ctr,
-               split ? (uint32_t)SMALL_BIG : 0u);
+#define DBI_BIG_LAUNCH(LOC)                                                                                          \
+    do {                                                                                                             \
+        if (split)                                                                                                   \
+            DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS / 2, SMALL_BIG, true, LOC>), dim3(max_blocks),                 \
+                       dim3(BIG_THREADS / 2), 0, s, d_in, d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, \
+                       d_giant_list, sa, ties ? 1u : 0u, d_ctr, (uint32_t)SMALL_BIG);                                \
+        DBI_LAUNCH((k_chunk_sort_list<BIG_THREADS, BIG_CAP, false, LOC>), dim3(max_blocks), dim3(BIG_THREADS), 0, s, \
+                   d_in, d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_giant_list, sa,               \
+                   ties ? 1u : 0u, d_ctr, split ? (uint32_t)SMALL_BIG : 0u);                                         \
+    } while (0)
+    if (local) DBI_BIG_LAUNCH(true);
+    else DBI_BIG_LAUNCH(false);
+#undef DBI_BIG_LAUNCH
     return hipGetLastError();
 }
 

@@ -265,6 +265,9 @@ struct dbi_handle {
         const void* d_res = nullptr;
         const void* d_poff = nullptr;
         uint64_t n_res = 0, n_prot = 0, cap = 0, last_kept = 0, alloc_gen = 0, dp_gen = 0;
+        uint64_t prev_unique = 0;         // depth bins: the sampled index
+        uint32_t depth_cap = 0;           // depth bins: region capacity (0: the radix tail)
+        bool tail_local = false;          // the previous build's tail (its list grids)
         uint32_t grid_mid = 0, grid_big = 0;
         bool giants = true;
         bool timing = false;
@@ -273,6 +276,7 @@ struct dbi_handle {
         bool operator==(const GraphKey& o) const {
             return d_res == o.d_res && d_poff == o.d_poff && n_res == o.n_res && n_prot == o.n_prot &&
                    cap == o.cap && last_kept == o.last_kept && alloc_gen == o.alloc_gen && dp_gen == o.dp_gen &&
+                   prev_unique == o.prev_unique && depth_cap == o.depth_cap && tail_local == o.tail_local &&
                    grid_mid == o.grid_mid && grid_big == o.grid_big && giants == o.giants && timing == o.timing &&
                    std::strncmp(timing_only, o.timing_only, sizeof(timing_only)) == 0;
         }
@@ -283,6 +287,19 @@ struct dbi_handle {
     bool use_semi_bounded = true;         // DBI_SEMI_BOUNDED=0: warm semi builds by the fused count + emit digest
     int big_split = -1;                   // DBI_BIG_SPLIT: big tier in two size classes (1 always, 0 never, -1 long lists)
     bool h1_on = false;                   // this warm build's digest counts the first radix histogram (h1plan)
+    // depth bins (warm lean builds: dbi_engine.hip warm_body_depth)
+    bool use_depth = true;                // DBI_DEPTH=0: the radix tail always
+    bool depth_off = false;               // this build's retry takes the radix tail (a region overflowed)
+    bool depth_keep_map = false;          // this build's retry keeps the depth map it computed (dtab)
+    bool cur_local = false, tail_local = false;  // this / the last finished build's chunk sort took depth-bin chunks
+    bool force_cold = false;              // dbi_set_cold: the next build takes the cold path (buffers kept)
+    double depth_slack = 1.25;            // region capacity / its share of the previous build's records
+    uint64_t prev_unique = 0;             // uniques of the resident index (the depth map's sample)
+    DevBuf<Rec> recR;                     // the digest's regions
+    DevBuf<uint8_t> rdig;                 //   each record's low bin digit
+    DevBuf<uint32_t> rcur, dsub, desc, d1c, hist2, bstart;
+    DevBuf<uint16_t> dtab;                // sub-bin -> depth bin
+    const dbi::PartOut* part_now = nullptr;  // run_digest: partition the warm digest's records (warm_body_depth)
     dbi::Hist1Plan h1plan{};
     bool capturing = false;               // stage events become event nodes
     GraphKey prev_key{};                  // the last plain warm build's key

@@ -173,6 +173,9 @@ int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse) {
     return tail_buffers(h, n, n_in, sparse, passes, passes ? width[passes - 1] : 0);
 }
 
+int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nchunks, uint64_t n,
+                const unsigned long long* d_n, bool est, bool local);
+
 int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
                const unsigned long long* d_n_in, const unsigned long long* d_n, uint64_t n_est, bool est) {
     hipStream_t s = h->stream;
@@ -186,7 +189,6 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     const uint32_t n_in32 = sparse ? (uint32_t)n_in : n32;
     const uint32_t T = chunk_target(h, n);
     const uint32_t nchunks = (uint32_t)std::max<uint64_t>((n + T - 1) / T, 1);
-    const size_t seg_cap = giant_seg_cap(n);
     if ((rc = tail_buffers(h, n, n_in, sparse, passes, bits_per))) return rc;
 
     // stable LSD passes over the bin id; every pass but the last writes the
@@ -226,9 +228,22 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     // chunk sort: 16 B in + 16 B out per record (+ the residues of every peptide for its hash)
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
           launch_chunk_bounds(src, n32, bm, T, nchunks, h->chunk_lo.p, s, d_n));
+    if ((rc = sort_chunks(h, src, dst, bm, nchunks, n, d_n, est, false))) return rc;
+    h->stats.n_bins = nbins;
+    return 0;
+}
+
+// The chunk sort tiers, the unique counts' scan and finalize over the chunk
+// pairs in h->chunk_lo (src: records in bin order; the index from dst).
+// local: depth-bin chunks (sort_chunk LOCAL; chunk_sort_mid sorts dst in place).
+int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nchunks, uint64_t n,
+                const unsigned long long* d_n, bool est, bool local) {
+    hipStream_t s = h->stream;
+    const uint32_t n32 = (uint32_t)n;
+    const size_t seg_cap = giant_seg_cap(n);
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                            h->mid_list.p, h->exact_dups, h->ctr.p, s));
+                            h->mid_list.p, h->exact_dups, h->ctr.p, s, local));
     // one block per listed bin (mid: every bin above the wave sort's reach) or
     // chunk (big: above CHUNK_CAP); the lists are filled on the device.  A device-sized tail
     // launches the previous build's list lengths plus a margin instead (a grid
@@ -237,7 +252,10 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     // time); a longer list sets ERR_GRID and the build is redone with full grids.
     uint32_t max_mid = (uint32_t)std::min<uint64_t>(MID_PER_PAIR * (uint64_t)nchunks, n / (WAVE_SORT_LIMIT + 1) + 1);
     uint32_t max_big = (uint32_t)std::min<uint64_t>(2 * (uint64_t)nchunks, n / (CHUNK_CAP + 1) + 1);
-    est = est || d_n;
+    // the list grids of the previous build hold for the same tail only (the
+    // depth bins' chunks and lists differ from the radix tail's)
+    est = (est || d_n) && h->tail_local == local;
+    h->cur_local = local;
     // (a list that was empty last time is not launched at all: ~4 us of an
     // empty grid plus its launch gap; entries there redo the build as above)
     h->skip_mid = est && h->grid_mid == GRID_NONE;
@@ -248,12 +266,12 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
     // chunks: a giant chunk otherwise sets ERR_GRID and the build is redone
     const bool giants = !est || h->giants_seen;
     STAGE(h, "chunk_sort_mid", by(0, 0, 0, 0, 0),
-          launch_chunk_sort_mid(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->mid_list.p,
-                                max_mid, h->ctr.p, s));
+          launch_chunk_sort_mid(local ? dst : src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p,
+                                h->mid_list.p, max_mid, h->ctr.p, s));
     STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
           launch_chunk_sort_big(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                                 giants ? h->giant_list.p : nullptr, max_big, h->split_above, h->exact_dups, h->ctr.p,
-                                s, h->big_split));
+                                s, h->big_split, local));
     if (giants)
         STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
               launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,
@@ -267,7 +285,6 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
           launch_finalize(dst, h->chunk_lo.p, nchunks, h->ucount.p, h->umass.p, h->upid.p, h->uoff.p, h->ulen.p,
                           h->occ_off.p, h->occ_pid.p, h->params.mass_group_factor,
                           (uint32_t)std::min<size_t>(h->umass.cap, 0xFFFFFFFFu), 2u, n32, d_n, h->ctr.p, s));
-    h->stats.n_bins = nbins;
     return 0;
 }
 
@@ -327,12 +344,15 @@ int finish_build(dbi_handle* h) {
     st.device_bytes = bytes;
     h->built = true;
     h->last_kept = st.n_kept;
+    h->prev_unique = st.n_unique;
     // the next device-sized tail's list grids: this build's lists plus a
     // margin, or no launch for an empty list
     h->lists_short = chunk_lists_short(h);
     h->grid_mid = h->hc.n_mid ? h->hc.n_mid + h->hc.n_mid / 8 + 32 : GRID_NONE;
     h->grid_big = h->hc.n_big ? h->hc.n_big + h->hc.n_big / 8 + 16 : GRID_NONE;
     h->giants_seen = h->hc.n_giant > 0;
+    h->tail_local = h->cur_local;
+    h->force_cold = false;
     ++h->build_serial;
     return 0;
 }
@@ -375,7 +395,7 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
     // full enzyme, no mandatory residues, <= 2 missed cleavages: one walk into
     // per-tile reservations of exactly each start's candidate ends
     const bool lean = lean_digest(h), bounded = bounded_digest(h);
-    if (h->recA.cap >= 1024) {
+    if (h->recA.cap >= 1024 && !h->force_cold) {
         // warm: one pass into the capacity of the previous build; the exact
         // need comes back with the counters, and a short buffer is grown and
         // the pass run again
@@ -393,10 +413,11 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
                                                  (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->recA.p, cap,
                                                  h->ctr.p, s));
             else if (bounded)
-                STAGE(h, "digest", by(1, 16, 0, 4, 0),
+                STAGE(h, "digest", by(1, h->part_now ? 17 : 16, 0, 4, 0),
                       launch_digest_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
                                             (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->recA.p, cap, h->ctr.p,
-                                            s, dev_sized && h->h1_on ? &h->h1plan : nullptr));
+                                            s, dev_sized && h->h1_on ? &h->h1plan : nullptr,
+                                            dev_sized ? h->part_now : nullptr));
             else
                 STAGE(h, "digest", by(1, 16, 0, 4, 0),
                       launch_digest_fused(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
@@ -450,6 +471,40 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
     return 0;
 }
 
+// Depth bins of a warm lean build: 2^B bins of about
+// DEPTH_BIN_AVG records each -- the high b1 bits partitioned by the digest into
+// (digit, XCD) regions, the low b2 by one radix pass -- then chunks of whole
+// bins, binned again in LDS by the chunk sort.  Replaces the radix tail's
+// first histogram and two of its three full passes over the records.
+constexpr uint64_t DEPTH_BIN_AVG = 768;     // records per depth bin (~1 chunk-sort chunk per 2 bins)
+constexpr uint64_t DEPTH_MIN_RECS = 1u << 14;
+constexpr uint32_t DEPTH_SAMPLES = 1u << 19;  // uniques of the previous index sampled for the map
+struct DepthPlan {
+    bool on = false;
+    uint32_t b1 = 0, b2 = 0, nbins = 0, cap = 0, nreg = 0, max_chunks = 0;
+};
+
+DepthPlan depth_plan(const dbi_handle* h) {
+    DepthPlan p;
+    const uint64_t n = h->last_kept, slots = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
+    if (!h->use_depth || h->depth_off || !lean_digest(h) || h->prev_unique == 0 || n < DEPTH_MIN_RECS ||
+        slots < 1024)
+        return p;
+    int B = 9;
+    while (B < 16 && (DEPTH_BIN_AVG << (B + 1)) <= n) ++B;
+    p.b1 = (uint32_t)std::max(1, std::min(8, B - 8));  // the pass over the low digit: 8 bits when B >= 9
+    p.b2 = (uint32_t)B - p.b1;
+    p.nbins = 1u << B;
+    p.nreg = (1u << p.b1) * DEPTH_XCDS;
+    const double share = (double)n / (double)p.nreg * h->depth_slack;
+    p.cap = (uint32_t)std::min<double>((share + 256.0 + 63.0) / 64.0, (double)(1u << 26)) * 64u;
+    if ((uint64_t)p.nreg * p.cap >= (1ull << 32) - 1 || p.cap / PART_CHUNK >= 65536u) return DepthPlan{};
+    p.max_chunks = (uint32_t)std::min<uint64_t>((uint64_t)p.nreg * ((p.cap + PART_CHUNK - 1) / PART_CHUNK),
+                                                 slots / PART_CHUNK + p.nreg);
+    p.on = true;
+    return p;
+}
+
 dbi_handle::GraphKey graph_key(const dbi_handle* h) {
     dbi_handle::GraphKey k{};
     k.d_res = h->d_res;
@@ -460,6 +515,10 @@ dbi_handle::GraphKey graph_key(const dbi_handle* h) {
     k.last_kept = h->last_kept;
     k.grid_mid = h->grid_mid;
     k.grid_big = h->grid_big;
+    k.prev_unique = h->prev_unique;
+    k.tail_local = h->tail_local;
+    const DepthPlan dpl = depth_plan(h);
+    k.depth_cap = dpl.on ? dpl.cap : 0u;
     k.giants = h->giants_seen;
     k.alloc_gen = g_alloc_gen.load(std::memory_order_relaxed);
     k.dp_gen = h->dp_gen;
@@ -480,8 +539,89 @@ void drop_graph(dbi_handle* h) {
     h->prev_mkey_valid = false;
 }
 
+int warm_body_depth(dbi_handle* h, const DepthPlan& pl, uint64_t* n_in, bool* sparse) {
+    hipStream_t s = h->stream;
+    int rc;
+    const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
+    const uint32_t nsub = 1u << DEPTH_SUB_BITS;
+    const uint64_t nreg_slots = (uint64_t)pl.nreg * pl.cap;
+    const uint32_t T = chunk_target(h, cap);
+    const uint32_t nchunks = (uint32_t)std::max<uint64_t>((cap + T - 1) / T, 1);
+    const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
+    // every allocation before the first launch (a reallocation must never free
+    // a buffer that queued kernels use): the tail's (chunk sort, index), the
+    // depth bins', the digest's (run_digest finds them in place)
+    if ((rc = tail_buffers(h, cap, cap, true)) || (rc = h->recR.ensure(nreg_slots)) ||
+        (rc = h->rdig.ensure(nreg_slots + 16)) || (rc = h->rcur.ensure(DEPTH_XCDS * 256)) || (rc = h->dsub.ensure(nsub)) ||
+        (rc = h->dtab.ensure(nsub)) || (rc = h->desc.ensure(pl.max_chunks)) || (rc = h->d1c.ensure(512)) ||
+        (rc = h->hist2.ensure((size_t)pl.max_chunks << pl.b2)) || (rc = h->bstart.ensure(pl.nbins + 1)) ||
+        (rc = h->blk.ensure(std::max<uint32_t>(ntiles, 1))) ||
+        (rc = h->thr.ensure((size_t)ntiles * DIGEST_THREADS + 1)) || (rc = h->tile_pf.ensure(2 * ((size_t)ntiles + 2))) ||
+        (rc = h->scan_tmp.ensure(std::max({scan_u32_tmp_elems(nsub), scan_u32_tmp_elems((uint64_t)pl.max_chunks << pl.b2),
+                                           scan_u32_tmp_elems(ntiles), h->scan_tmp.cap}))))
+        return rc;
+    // the map, from a sample of the resident index (the previous build's)
+    const uint64_t U = std::min<uint64_t>({h->prev_unique, h->umass.cap, h->occ_off.cap ? h->occ_off.cap - 1 : 0});
+    const BinMap sub = make_binmap(h->params.min_mh, h->params.max_mh, nsub);
+    DBI_HIP(hipMemsetAsync(h->rcur.p, 0, sizeof(uint32_t) * DEPTH_XCDS * 256, s));
+    if (!h->depth_keep_map) {  // (a redo keeps the map: the failed attempt may have overwritten the index)
+        DBI_HIP(hipMemsetAsync(h->dsub.p, 0, sizeof(uint32_t) * nsub, s));
+        STAGE(h, "depth_map", by(0, 0, 0, 0, 0), ([&]() -> hipError_t {
+                  hipError_t e = launch_depth_sample(h->umass.p, h->occ_off.p, U, DEPTH_SAMPLES, sub, h->dsub.p, s);
+                  if (e == hipSuccess)
+                      e = launch_scan_u32(h->dsub.p, h->dsub.p, nsub, h->scan_tmp.p, h->scan_tmp.cap,
+                                          &h->ctr.p->depth_w, s);
+                  return e == hipSuccess ? launch_depth_table(h->dsub.p, h->ctr.p, nsub, pl.nbins, h->dtab.p, s) : e;
+              }()));
+    }
+    // the digest, partitioned into the regions
+    PartOut po{};
+    po.recs = h->recR.p;
+    po.dig = h->rdig.p;
+    po.cur = h->rcur.p;
+    po.dm = DepthMap{h->dtab.p, sub, pl.b2};
+    po.cap = pl.cap;
+    po.b1 = pl.b1;
+    h->part_now = &po;
+    uint64_t n = 0;
+    bool dev = false;
+    rc = run_digest(h, &n, n_in, sparse, &dev);
+    h->part_now = nullptr;
+    if (rc) return rc;
+    if (!dev) return set_error(DBI_E_STATE, "internal: warm build without device sizing");
+    // one radix pass over the low digit, region by region, into bin order (recA)
+    STAGE(h, "part_plan", by(0, 0, 0, 0, 0),
+          launch_part_plan(h->rcur.p, pl.cap, pl.b1, cap, h->desc.p, h->d1c.p, h->ctr.p, s));
+    STAGE(h, "part_hist", by(0, 1, 0, 0, 0),
+          launch_part_hist(h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2, pl.max_chunks, h->hist2.p,
+                           h->ctr.p, s));
+    STAGE(h, "part_scan", by(0, 0, 0, 0, 0),
+          launch_scan_u32(h->hist2.p, h->hist2.p, (uint64_t)pl.max_chunks << pl.b2, h->scan_tmp.p, h->scan_tmp.cap,
+                          nullptr, s));
+    STAGE(h, "bin_scatter", by(0, 33, 0, 0, 0),
+          launch_part_scatter(h->recR.p, h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2,
+                              pl.max_chunks, h->hist2.p, h->recA.p, h->ctr.p, s));
+    STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
+          launch_depth_bounds(h->hist2.p, h->d1c.p, pl.b1, pl.b2, h->bstart.p, T, nchunks, h->chunk_lo.p, h->ctr.p, s));
+    if ((rc = sort_chunks(h, h->recA.p, h->recB.p, sub, nchunks, cap, &h->ctr.p->tail_n, true, true))) return rc;
+    h->stats.n_bins = pl.nbins;
+    return 0;
+}
+
 // digest + tail of a warm device-sized build, enqueued (or captured)
 int warm_body(dbi_handle* h, uint64_t* n_in, bool* sparse) {
+    const DepthPlan dpl = depth_plan(h);
+    if (dpl.on) {
+        // (the map samples the resident index: a reallocation of it on the way
+        // here -- the tail's buffers grown -- and the radix tail runs instead)
+        const double* um = h->umass.p;
+        const uint32_t* oo = h->occ_off.p;
+        int rc0;
+        if ((rc0 = tail_buffers(h, std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull),
+                                std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull), true)))
+            return rc0;
+        if (um == h->umass.p && oo == h->occ_off.p) return warm_body_depth(h, dpl, n_in, sparse);
+    }
     // small tails: the bounded digest counts the first radix pass's histogram
     // as it writes the records (one kernel and its launch gap fewer, human
     // scale 0.33 -> 0.31 ms).  Bins and buffers planned here from what
@@ -526,7 +666,7 @@ int warm_body(dbi_handle* h, uint64_t* n_in, bool* sparse) {
 
 int build_digest(dbi_handle* h) {
     for (int attempt = 0;; ++attempt) {
-        const bool warm = h->recA.cap >= 1024;
+        const bool warm = h->recA.cap >= 1024 && !h->force_cold;
         uint64_t n_in = 0;
         bool sparse = false;
         int rc;
@@ -591,11 +731,30 @@ int build_digest(dbi_handle* h) {
             return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences (or bounded-digest slots) on "
                                             "one device: shard the FASTA");
         const bool grid_short = chunk_lists_short(h);
-        if (need <= n_in && !grid_short) {
+        const bool part_over = (h->hc.err & ERR_PART) != 0;
+        if (std::getenv("DBI_DEBUG_BUILD"))
+            fprintf(stderr, "[dbi] attempt %d: need %llu n_in %llu grid_short %d (err %u mid %u/%u big %u/%u) part_over %d "
+                            "kept %llu slots %llu tail_n %llu part_chunks %u depth_w %llu\n",
+                    attempt, (unsigned long long)need, (unsigned long long)n_in, (int)grid_short, h->hc.err, h->hc.n_mid,
+                    h->grid_mid, h->hc.n_big, h->grid_big, (int)part_over, h->hc.n_kept, h->hc.n_slots, h->hc.tail_n,
+                    h->hc.part_chunks, h->hc.depth_w);
+        if (need <= n_in && !grid_short && !part_over) {
             h->hc_final = true;
+            h->depth_off = false;
+            h->depth_keep_map = false;
             return 0;
         }
-        if (attempt > 1) return set_error(DBI_E_STATE, "digest output grew between identical passes");
+        if (part_over) {  // a depth-bin region overflowed: this build by the radix tail, the next with more room
+            h->depth_off = true;
+            h->depth_slack = std::min(8.0, 2.0 * h->depth_slack);
+        }
+        // a redo of a depth-bin build keeps its map (this attempt's finalize may have overwritten the index)
+        h->depth_keep_map = !part_over && !h->depth_off;
+        if (attempt > 2) {
+            h->depth_off = false;
+            h->depth_keep_map = false;
+            return set_error(DBI_E_STATE, "digest output grew between identical passes");
+        }
         // grown, or a chunk list longer than its grid: everything again (full
         // list grids; counters back to zero, except the record layout; the
         // stage table restarts)
@@ -619,6 +778,8 @@ int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
     h->n_prot = n_prot;
     h->n_total_extra = 0;
     h->exact_dups = false;
+    h->depth_off = false;  // (a depth-bin redo's state never outlives its build)
+    h->depth_keep_map = false;
     std::memset(&h->stats, 0, sizeof(h->stats));
     h->nstage = 0;
     h->hc_final = false;
@@ -981,6 +1142,7 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     if (const char* ev = std::getenv("DBI_DIGEST_HIST")) h->use_h1 = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("DBI_SEMI_BOUNDED")) h->use_semi_bounded = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("DBI_BIG_SPLIT")) h->big_split = std::atoi(ev) != 0 ? 1 : 0;
+    if (const char* ev = std::getenv("DBI_DEPTH")) h->use_depth = std::atoi(ev) != 0;
     auto fail = [&](int code) {
         dbi_close(h);
         return code;
@@ -1440,6 +1602,17 @@ int dbi_rebuild(dbi_handle* h) {
     h->d_poff = h->poff.p;
     if ((rc = build_digest(h))) return rc;
     return finish_build(h);
+}
+
+int dbi_set_cold(dbi_handle* h) {
+    if (!h) return set_error(DBI_E_INVALID, "null handle");
+    std::lock_guard<std::recursive_mutex> lk(h->qmu);
+    drop_graph(h);
+    h->force_cold = true;
+    h->prev_key_valid = false;
+    h->grid_mid = h->grid_big = 0;
+    h->giants_seen = true;
+    return 0;
 }
 
 int dbi_set_timing(dbi_handle* h, int on, const char* only) {

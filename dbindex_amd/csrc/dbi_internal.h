@@ -167,6 +167,8 @@ struct Counters {
     // digest's slots / records, or 0 when they did not fit the buffer (the
     // skipped tiles left stale slots behind; the build is redone)
     unsigned long long tail_in, tail_n;
+    unsigned long long depth_w;    // depth bins: the sampled occurrence weight (the map's total)
+    unsigned int part_chunks;      // depth bins: pass-2 chunks over the digest's regions (k_part_plan)
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads
     // (sharing the ticket's line cost the digest 30%)
@@ -181,6 +183,7 @@ constexpr unsigned ERR_SLOTS = 4;   // bounded digest: a thread emitted more rec
 constexpr unsigned ERR_PTM = 8;     // a device digest met '[' (inline PTMs are only digested from host input)
 constexpr uint32_t GRID_NONE = 0xFFFFFFFFu;  // list grid: the previous build's list was empty (no launch)
 constexpr unsigned ERR_GRID = 16;   // a chunk list outgrew its kernel's grid (estimated from the previous build): redo
+constexpr unsigned ERR_PART = 32;   // depth bins: a digest region outgrew its capacity: redo by the radix tail
 
 // Tunables
 constexpr int DIGEST_THREADS = 256;
@@ -241,10 +244,59 @@ struct Hist1Plan {
     int bits;
     uint32_t G;  // radix blocks over cap slots
 };
+// ---- depth bins (warm lean builds) ----------------------
+// 2^(b1 + b2) mass bins of about equal record counts: a monotone table over
+// 2^DEPTH_SUB_BITS linear sub-bins of [minMH, maxMH], built from a sample of the
+// previous build's index (occurrence-weighted; a heuristic: a stale or poor
+// map costs speed, never correctness).  The digest partitions its records by
+// the bin's high b1 bits into (digit, XCD) regions; one radix pass over the
+// low b2 bits orders them by bin; the chunk sort bins each chunk locally.
+constexpr int DEPTH_SUB_BITS = 20;
+constexpr uint32_t DEPTH_XCDS = 8;        // regions per high digit: one per XCD (block b on XCD b % 8)
+constexpr uint32_t PART_CHUNK = 4096;     // records per pass-2 block (RADIX_THREADS * RADIX_ITEMS)
+struct DepthMap {
+    const uint16_t* tab;  // sub-bin -> bin (non-decreasing)
+    BinMap sub;           // the linear sub-bins
+    uint32_t b2;          // low bits of a bin (the pass-2 digit); the high bits: the digest's partition
+};
+struct PartOut {          // the digest's partition (k_digest_bounded PART)
+    Rec* recs;            // region r = d1 * DEPTH_XCDS + xcd at [r * cap, r * cap + cur[r])
+    uint8_t* dig;         // the low b2 bits of each record's bin, same positions
+    uint32_t* cur;        // per region: records placed (zeroed before the digest)
+    DepthMap dm;
+    uint32_t cap;         // records per region (a multiple of 64)
+    uint32_t b1;
+};
+// the map: occurrence-weighted histogram of ns sampled uniques over the
+// sub-bins (zeroed d_sub), its scan (total -> ctr->depth_w), the table
+hipError_t launch_depth_sample(const double* d_umass, const uint32_t* d_occ_off, uint64_t n_unique, uint32_t ns,
+                               const BinMap& sub, uint32_t* d_sub, hipStream_t s);
+hipError_t launch_depth_table(const uint32_t* d_sub_scan, const Counters* d_ctr, uint32_t nsub, uint32_t nbins,
+                              uint16_t* d_tab, hipStream_t s);
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                  const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s,
-                                 const Hist1Plan* h1p = nullptr);
+                                 const Hist1Plan* h1p = nullptr, const PartOut* part = nullptr);
+// pass-2 plan over the regions: desc[c] = region << 16 | piece for every
+// PART_CHUNK-record piece, d1c[d] / d1c[D1 + d] = first chunk / chunks of high
+// digit d, ctr->part_chunks; ctr->tail_n = the records (0 when the digest's
+// slots or a region overflowed: nothing downstream runs, the host redoes it)
+hipError_t launch_part_plan(const uint32_t* d_cur, uint32_t cap, uint32_t b1, uint64_t slot_cap, uint32_t* d_desc,
+                            uint32_t* d_d1c, Counters* d_ctr, hipStream_t s);
+// hist[(first(d1) << b2) + d2 * nch(d1) + (c - first(d1))] = records of chunk c with digit d2
+hipError_t launch_part_hist(const uint8_t* d_dig, const uint32_t* d_cur, uint32_t cap, const uint32_t* d_desc,
+                            const uint32_t* d_d1c, uint32_t b1, uint32_t b2, uint32_t max_chunks, uint32_t* d_hist,
+                            const Counters* d_ctr, hipStream_t s);
+hipError_t launch_part_scatter(const Rec* d_recs, const uint8_t* d_dig, const uint32_t* d_cur, uint32_t cap,
+                               const uint32_t* d_desc, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
+                               uint32_t max_chunks, const uint32_t* d_offs, Rec* d_out, const Counters* d_ctr,
+                               hipStream_t s);
+// chunk pairs over the bin-ordered records from the pass-2 offsets: bin
+// starts (bstart: nbins + 1), then chunk_lo[2c] = first bin start at or after
+// c*T, chunk_lo[2c+1] = the last bin's start when the chunk exceeds CHUNK_CAP
+hipError_t launch_depth_bounds(const uint32_t* d_offs, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
+                               uint32_t* d_bstart, uint32_t T, uint32_t nchunks, uint32_t* d_chunk_lo,
+                               const Counters* d_ctr, hipStream_t s);
 // semi-specific enzymes (no mandatory residues, no windows): one walk per start
 // into slots bounded by the bit maps (REC_SENTINEL in the unused ones)
 hipError_t launch_digest_semi_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
@@ -366,9 +418,13 @@ size_t radix_hist_elems(uint32_t n, int bits);
 // straddling (c+1)*T (its own chunk), else chunk_lo[2c+2]
 hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, uint32_t T, uint32_t nchunks,
                                uint32_t* d_chunk_lo, hipStream_t s, const unsigned long long* d_n = nullptr);
+// local: depth-bin chunks (launch_depth_bounds), each binned in LDS by its own
+// mass range; one block per chunk (2 * nchunks), the wide local bins written
+// unsorted for chunk_sort_mid, which then sorts `out` in place (d_in == d_out)
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
-                             uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s);
+                             uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s,
+                             bool local = false);
 hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_mid_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s);
@@ -376,7 +432,7 @@ hipError_t launch_chunk_sort_big(const Rec* d_in, Rec* d_out, const BinMap& bm, 
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_big_list, uint32_t* d_giant_list, uint32_t max_blocks,
                                  uint32_t split_above, bool ties, Counters* d_ctr, hipStream_t s,
-                                 int split = -1);
+                                 int split = -1, bool local = false);
 // chunks above BIG_CAP listed in d_giant_list: MSD split on the (mass, tag)
 // key into leaves sorted in LDS; a segment of one (mass, tag) key above
 // BIG_CAP falls back to global-memory scratch (ws_key / ws_k2).  segs: 5 lists

@@ -248,6 +248,11 @@ class Engine:
         check(_native.lib().dbi_rebuild(self.h))
         return self.stats()
 
+    def set_cold(self) -> None:
+        """The next build takes the cold path (count + emit digest, radix tail,
+        full list grids) with the device buffers kept (dbi_set_cold)."""
+        check(_native.lib().dbi_set_cold(self.h))
+
     def set_timing(self, on: bool, only: str = "") -> None:
         """Per-kernel HIP events carried by the dispatch packets (default: every
         stage); ``only`` restricts them to the stages of that name."""

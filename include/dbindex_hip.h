@@ -257,6 +257,13 @@ int dbi_device_view(dbi_handle* h, dbi_device_index* out);
  * ms[i] = 0 for a stage that launched nothing or with timing off;
  * bytes[i] = algorithmic HBM bytes of that launch.
  * Arrays may be NULL to query *n. */
+/* The next build starts cold, as the one-off build of DBIndexer.run
+ * (DBIndexer.java:508-684) does: no capacity, chunk-list grids, depth-bin map
+ * or build graph carried over from earlier builds (count + emit digest, the
+ * radix tail), but the device buffers are kept -- the cold pipeline timed
+ * without its allocations (bench.py cold_ms). */
+int dbi_set_cold(dbi_handle* h);
+
 /* on = 0: no events (wall clock only); on = 1: time every stage, or only the
  * stages named `only` (NULL or "" = all) — each timed stage costs a few us. */
 int dbi_set_timing(dbi_handle* h, int on, const char* only);

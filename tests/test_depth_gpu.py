@@ -1,0 +1,105 @@
+"""GPU: depth bins (warm lean builds).
+
+A warm tryptic build partitions its records inside the digest by the high
+digit of an equal-depth mass-bin map (sampled from the previous index), sorts
+them into bins with one radix pass over the low digit, and bins every chunk
+again in LDS.  The map is only a heuristic: whatever it is -- the previous
+index of another proteome, a map that crowds one region past its capacity --
+every build must equal the oracle (reference: DBIndexer.java:237-405,
+DBIndexStoreSQLiteByteIndexMerge.java:620-719).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from dbindex_amd import fasta
+from dbindex_amd.params import DBIndexSearchParams
+from oracle import cref
+from tests.helpers import assert_index_equal, assert_queries_equal, query_masses
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def Engine():
+    from dbindex_amd import _native
+    from dbindex_amd.engine import Engine
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    return Engine
+
+
+def _stages(eng):
+    return {name for name, _, _ in eng.stage_times()}
+
+
+@pytest.mark.parametrize("depth", ["1", "0"])
+def test_depth_warm_builds_match_oracle(Engine, monkeypatch, depth):
+    """Human scale (configs[1], 1.9M records): cold, then warm builds -- every
+    stage timed (no graph), then untimed (captured, replayed) -- each equal to
+    the oracle; with DBI_DEPTH=0 the radix tail runs instead."""
+    monkeypatch.setenv("DBI_DEPTH", depth)
+    pp = fasta.config("human")
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    with Engine(cp) as eng:
+        eng.build(pp)
+        assert "bin_scatter" not in _stages(eng)  # cold: count + emit, the radix tail
+        assert_index_equal(eng, oix, "cold")
+        for k in range(2):
+            eng.build(pp)
+            names = _stages(eng)
+            assert ("bin_scatter" in names) == (depth == "1"), names
+            assert ("radix_scatter" in names) == (depth == "0"), names
+            assert_index_equal(eng, oix, f"warm timed {k}")
+        eng.set_timing(False)
+        for k in range(4):
+            eng.build(pp)
+            assert_index_equal(eng, oix, f"warm untimed {k}")
+        m, t = query_masses(oix, 5000, seed=3)
+        assert_queries_equal(eng, oix, m, t, "queries")
+
+
+def test_depth_map_of_another_proteome(Engine):
+    """The map comes from the resident index.  Proteome B (the same proteins
+    rewritten over G/A/S/K/R: light peptides) built after A uses A's map: its
+    records crowd the low high-digit regions past their capacity, the build
+    is redone by the radix tail (ERR_PART) and the next takes depth bins over
+    B's own map.  Then back to A.  Every build equals its oracle."""
+    hum = fasta.config("human")
+    a = hum.slice(0, 12000)
+    light = np.frombuffer(b"GASKR", np.uint8)
+    b_res = light[a.residues % 5].copy()
+    b = fasta.PackedProteins(b_res, a.offsets.copy(), a.defs)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oa, ob = cref.Index(cp, a.residues, a.offsets), cref.Index(cp, b.residues, b.offsets)
+    assert ob.n_total > 20000
+    with Engine(cp) as eng:
+        for k, (p, o) in enumerate([(a, oa), (a, oa), (b, ob), (b, ob), (b, ob), (a, oa), (a, oa)]):
+            eng.build(p)
+            assert_index_equal(eng, o, f"build {k}")
+            if k in (1, 3, 4, 6):  # the map of the same proteome: depth bins
+                assert "bin_scatter" in _stages(eng), (k, _stages(eng))
+            if k in (2, 5):  # the other proteome's map overflows a region: redone by the radix tail
+                assert "radix_scatter" in _stages(eng) and "bin_scatter" not in _stages(eng), (k, _stages(eng))
+        m, t = query_masses(oa, 3000, seed=9)
+        assert_queries_equal(eng, oa, m, t, "queries after the map changes")
+
+
+def test_depth_equal_mass_spikes(Engine):
+    """Equal-mass spikes (a protein block rewritten as GAAAAAAK repeats) land
+    whole in one depth bin: a chunk far above the LDS capacity, through the
+    big / giant tiers from the bin-ordered records, warm and replayed."""
+    a = fasta.config("human").slice(0, 6000)
+    spike = a.residues.copy()
+    e = int(a.offsets[400])
+    spike[:e] = np.resize(np.frombuffer(b"GAAAAAAK", np.uint8), e)
+    c = fasta.PackedProteins(spike, a.offsets.copy(), a.defs)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oc = cref.Index(cp, c.residues, c.offsets)
+    with Engine(cp) as eng:
+        eng.set_timing(False)
+        for k in range(5):
+            eng.build(c)
+            assert_index_equal(eng, oc, f"spiked build {k}")
