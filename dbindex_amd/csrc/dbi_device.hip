@@ -36,6 +36,7 @@
 // k_hbm_copy: the measured copy ceiling the bench prints beside the peak.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 #include <cstdlib>
 #include <algorithm>
@@ -1640,18 +1641,21 @@ __device__ __forceinline__ uint32_t xcc_id() {
 }
 
 // The tile's records (slots [0, n) of src, just written by this block:
-// L2-resident) into the regions of their bins' high digits: 1024 slots a
-// round, each record's rank inside its digit from an LDS counter, one global
-// atomic per digit present reserves the tile's run in region (digit, this
-// block's XCD) -- the runs of one XCD's tiles are neighbours in its regions, so
-// its L2 merges their partial lines -- and the records go there with their
-// bins' low digits (pass 2 counts those bytes).  A region that would overflow
-// takes nothing and flags the build (ERR_PART: redone by the radix tail).
-// The records never go back through a full radix pass of their own: this is
-// the first pass, fused.
-constexpr uint32_t PART_ITEMS = 8;
+// L2-resident) into the regions of their bins' high digits, PART_R slots a
+// round: each record's rank inside its digit from an LDS counter, the digit
+// counts scanned, one L2 atomic per digit present reserves the tile's run in
+// region (digit, this XCD) -- the runs of one XCD's tiles are neighbours in
+// its regions, so its L2 merges their partial lines -- the records staged in
+// LDS in digit order (the walks' LDS is dead) and written as digit runs by
+// consecutive lanes, with their bins' low digits (pass 2 counts those bytes).
+// A region that would overflow takes nothing and flags the build (ERR_PART:
+// redone by the radix tail).  The records never go through a full radix pass
+// of their own: this is the first pass, fused.
+// s_cnt / s_gof: 256 words each; stage: PART_R x 16 B, then PART_R x 2 B.
+template <uint32_t R>
 __device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32_t n, uint32_t* s_cnt,
-                          uint32_t* s_gof, Counters* __restrict__ ctr) {
+                          uint32_t* s_gof, uint32_t* s_tmp, uint4* stage, uint16_t* sdig, Counters* __restrict__ ctr) {
+    constexpr uint32_t KI = (R + DIGEST_THREADS - 1) / DIGEST_THREADS;
     const uint32_t tid = threadIdx.x, xcd = xcc_id(), D1 = 1u << po.b1;
     const uint32_t b2 = po.dm.b2, m2 = (1u << b2) - 1u;
     const uint4* __restrict__ src4 = reinterpret_cast<const uint4*>(src);
@@ -1660,49 +1664,60 @@ __device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32
     // other waves read the slots back (from the L2: the lines were never in
     // this CU's L1).  (__threadfence() would write the L2 back to HBM per tile.)
     __builtin_amdgcn_s_waitcnt(0);
-    for (uint32_t r0 = 0; r0 < n; r0 += DIGEST_THREADS * PART_ITEMS) {
-        __syncthreads();  // the tile's slots written (first round); the last round's counters read
-        if (tid < D1) s_cnt[tid] = 0;
-        uint4 rv[PART_ITEMS];
+    for (uint32_t r0 = 0; r0 < n; r0 += R) {
+        const uint32_t nr = min(R, n - r0);
+        __syncthreads();  // the tile's slots written (first round); the last round's stage and counters read
+        s_cnt[tid] = 0;
+        uint4 rv[KI];
 #pragma unroll
-        for (uint32_t k = 0; k < PART_ITEMS; ++k)  // clamped: every load in flight together
-            rv[k] = src4[min(r0 + k * DIGEST_THREADS + tid, n - 1u)];
+        for (uint32_t k = 0; k < KI; ++k)  // clamped: every load in flight together
+            rv[k] = src4[r0 + min(k * DIGEST_THREADS + tid, nr - 1u)];
         __syncthreads();
-        uint32_t bin[PART_ITEMS], rk[PART_ITEMS];
+        uint32_t bin[KI], rk[KI];
 #pragma unroll
-        for (uint32_t k = 0; k < PART_ITEMS; ++k) {
+        for (uint32_t k = 0; k < KI; ++k) {
             bin[k] = ~0u;
             rk[k] = 0;
-            if (r0 + k * DIGEST_THREADS + tid < n && (rv[k].x & rv[k].y) != 0xFFFFFFFFu) {  // not a sentinel
+            if (k * DIGEST_THREADS + tid < nr && (rv[k].x & rv[k].y) != 0xFFFFFFFFu) {  // not a sentinel
                 bin[k] = depth_bin(u4_mass(rv[k]), po.dm);
                 rk[k] = atomicAdd(&s_cnt[bin[k] >> b2], 1u);
             }
         }
         __syncthreads();
+        // digit d's run: stage[lstart, lstart + c), region cursor o -> out[region(d) + o + (t - lstart)]
+        const uint32_t c = tid < D1 ? s_cnt[tid] : 0u;
+        uint32_t nvalid;
+        const uint32_t lstart = block_excl_scan<DIGEST_THREADS, uint32_t>(c, s_tmp, nvalid);
         if (tid < D1) {
-            const uint32_t c = s_cnt[tid];
             uint32_t g = ~0u;
             if (c) {
-                const uint32_t r = tid * DEPTH_XCDS + xcd;
-                // the region's cursor is this XCD's alone (its own 1-KiB row, cur[xcd][digit]): the add runs
-                // in this XCD's L2 (workgroup scope: no trip to the memory-side atomics); the kernel's end
+                // the cursor is this XCD's alone (its own 1-KiB row, cur[xcd][digit]): the add runs in
+                // this XCD's L2 (workgroup scope: no trip to the memory-side atomics); the kernel's end
                 // writes it back.  A wrong XCD id would lose adds: k_part_plan checks the cursors' sum.
                 const uint32_t o = __hip_atomic_fetch_add(&po.cur[xcd * 256u + tid], c, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (o + c <= po.cap) g = r * po.cap + o;
+                if (o + c <= po.cap) g = (tid * DEPTH_XCDS + xcd) * po.cap + o - lstart;
                 else atomicOr(&ctr->err, ERR_PART);
             }
             s_gof[tid] = g;
+            s_cnt[tid] = lstart;
         }
         __syncthreads();
 #pragma unroll
-        for (uint32_t k = 0; k < PART_ITEMS; ++k) {
+        for (uint32_t k = 0; k < KI; ++k) {
             if (bin[k] != ~0u) {
-                const uint32_t g = s_gof[bin[k] >> b2];
-                if (g != ~0u) {
-                    out4[g + rk[k]] = rv[k];
-                    po.dig[g + rk[k]] = (uint8_t)(bin[k] & m2);
-                }
+                const uint32_t at = s_cnt[bin[k] >> b2] + rk[k];
+                stage[at] = rv[k];
+                sdig[at] = (uint16_t)bin[k];
+            }
+        }
+        __syncthreads();
+        for (uint32_t t = tid; t < nvalid; t += DIGEST_THREADS) {
+            const uint32_t bb = sdig[t];
+            const uint32_t g = s_gof[bb >> b2];
+            if (g != ~0u) {
+                out4[g + t] = stage[t];
+                po.dig[g + t] = (uint8_t)(bb & m2);
             }
         }
     }
@@ -1712,7 +1727,7 @@ __device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32
 // SIMD, where the LDS puts the blocks).  PART: the records are partitioned by
 // the depth bins' high digit afterwards (part_tile; the slots are scratch).
 template <bool DROP, bool H1, bool PART = false>
-__global__ void __launch_bounds__(DIGEST_THREADS) __attribute__((amdgpu_waves_per_eu(H1 ? 6 : 1, 8)))
+__global__ void __launch_bounds__(DIGEST_THREADS) __attribute__((amdgpu_waves_per_eu(H1 || PART ? 6 : 1, 8)))
 k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                  const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
                  uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, Rec* __restrict__ d_out, uint64_t cap,
@@ -1963,9 +1978,14 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
             if (v && c < h1.G) atomicAdd(&h1.g[(size_t)(i & ((1u << h1.bits) - 1u)) * h1.G + c], v);
         }
     }
-    if constexpr (PART) {  // the candidate list is dead: the partition's counters
-        uint32_t* p_cnt = reinterpret_cast<uint32_t*>(sm.cand);
-        part_tile(po, d_out + base, tile_slots, p_cnt, p_cnt + 256, d_ctr);
+    if constexpr (PART) {  // the walks' LDS is dead: the partition's counters and stage
+        constexpr size_t b0 = offsetof(LeanSmem, clvm), b1 = offsetof(LeanSmem, tmp);
+        constexpr uint32_t R = (uint32_t)((b1 - b0) / 18 / 64 * 64);  // 16 B + 2 B per staged record
+        static_assert(b0 % 16 == 0 && R >= 1024, "partition stage");
+        uint8_t* st = reinterpret_cast<uint8_t*>(&sm) + b0;
+        uint32_t* p_cnt = reinterpret_cast<uint32_t*>(sm.mass);
+        part_tile<R>(po, d_out + base, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
+                     reinterpret_cast<uint16_t*>(st + 16 * R), d_ctr);
     }
 }
 
@@ -4178,9 +4198,14 @@ __device__ unsigned long long g_chunk_clock[1u << 18][2];
 // One block per chunk pair (k_chunk_bounds / launch_depth_bounds).  Radix
 // tail: chunk 2c here, chunk 2c+1 (one big bin) to the list kernels.  LOCAL
 // (depth bins): both chunks of the pair here, one after the other (2c+1 is
-// empty unless the pair was split) -- one block per chunk instead put every
-// non-empty block on every other XCD (blocks go to the XCDs round-robin):
-// half the chip idle, 1.76 vs 0.82 ms.
+// empty unless the pair was split).  Measured against one block per chunk:
+// block b sorting chunk b put every non-empty chunk on every other XCD
+// (blocks go to the XCDs round-robin; half the chip idle, 1.76 vs 0.82 ms);
+// the even chunks in the grid's first half and the odd ones in its second
+// left the split chunks as the launch's tail (1.29-1.31 vs 1.21 ms).
+#ifndef DBI_LOCAL_PAIRS
+#define DBI_LOCAL_PAIRS 1
+#endif
 template <int NT, int CAP, bool LOCAL = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
@@ -4188,7 +4213,9 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
              uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, uint32_t ties,
              Counters* __restrict__ ctr) {
     __shared__ ChunkSmem<NT, CAP> sm;
-    const uint32_t c = 2 * blockIdx.x;
+    const uint32_t half = gridDim.x >> 1;
+    const uint32_t c = !LOCAL || DBI_LOCAL_PAIRS ? 2 * blockIdx.x
+                       : blockIdx.x < half ? 2 * blockIdx.x : 2 * (blockIdx.x - half) + 1;
 #ifdef DBI_CLOCK_CHUNKS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -4205,7 +4232,7 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
     }
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     chunk_sort_one<NT, CAP, LOCAL>(c, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr, sm);
-    if constexpr (LOCAL) {
+    if constexpr (LOCAL && DBI_LOCAL_PAIRS) {
         __syncthreads();  // the LDS is the next chunk's
         chunk_sort_one<NT, CAP, LOCAL>(c + 1, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr, sm);
     }
@@ -4333,7 +4360,8 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
                              bool local) {
     if (nchunks == 0) return hipSuccess;
     if (local)
-        DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP, true>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
+        DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP, true>), dim3(DBI_LOCAL_PAIRS ? nchunks : 2 * nchunks),
+                   dim3(CHUNK_THREADS), 0, s, d_in,
                    d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr);
     else
         DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,

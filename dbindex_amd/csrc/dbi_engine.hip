@@ -478,7 +478,10 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
 // first histogram and two of its three full passes over the records.
 constexpr uint64_t DEPTH_BIN_AVG = 768;     // records per depth bin (~1 chunk-sort chunk per 2 bins)
 constexpr uint64_t DEPTH_MIN_RECS = 1u << 14;
-constexpr uint32_t DEPTH_SAMPLES = 1u << 19;  // uniques of the previous index sampled for the map
+#ifndef DBI_DEPTH_SAMPLES
+#define DBI_DEPTH_SAMPLES (1u << 19)
+#endif
+constexpr uint32_t DEPTH_SAMPLES = DBI_DEPTH_SAMPLES;  // uniques of the previous index sampled for the map
 struct DepthPlan {
     bool on = false;
     uint32_t b1 = 0, b2 = 0, nbins = 0, cap = 0, nreg = 0, max_chunks = 0;

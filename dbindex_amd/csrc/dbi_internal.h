@@ -251,7 +251,10 @@ struct Hist1Plan {
 // map costs speed, never correctness).  The digest partitions its records by
 // the bin's high b1 bits into (digit, XCD) regions; one radix pass over the
 // low b2 bits orders them by bin; the chunk sort bins each chunk locally.
-constexpr int DEPTH_SUB_BITS = 20;
+#ifndef DBI_DEPTH_SUB_BITS
+#define DBI_DEPTH_SUB_BITS 20
+#endif
+constexpr int DEPTH_SUB_BITS = DBI_DEPTH_SUB_BITS;
 constexpr uint32_t DEPTH_XCDS = 8;        // regions per high digit: one per XCD (block b on XCD b % 8)
 constexpr uint32_t PART_CHUNK = 4096;     // records per pass-2 block (RADIX_THREADS * RADIX_ITEMS)
 struct DepthMap {

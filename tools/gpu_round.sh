@@ -30,19 +30,26 @@ for w in $WHAT; do
     bench_h) step bench_h 600 python bench.py --config human --steps 20 --warmup 5 ;;
     prof)  export TMPDIR=/tmp
            step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-                -- python3 bench.py --steps 10 --warmup 2 --queries 0 --no-cpu-baseline ;;
+                -- python3 bench.py --steps 10 --warmup 3 --queries 0 --no-cpu-baseline --no-cold ;;
     prof_semi) export TMPDIR=/tmp
            step prof_semi 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_semi" -o run \
-                -- python3 bench.py --config semi --steps 4 --warmup 5 --queries 0 --no-cpu-baseline ;;
+                -- python3 bench.py --config semi --steps 4 --warmup 5 --queries 0 --no-cpu-baseline --no-cold ;;
     pmc)   export TMPDIR=/tmp
            step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
-                -- python3 bench.py --steps 3 --warmup 1 --queries 0 --no-cpu-baseline
+                -- python3 bench.py --steps 5 --warmup 3 --queries 0 --no-cpu-baseline --no-cold
            step pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
-                -- python3 bench.py --steps 3 --warmup 1 --queries 0 --no-cpu-baseline ;;
+                -- python3 bench.py --steps 5 --warmup 3 --queries 0 --no-cpu-baseline --no-cold ;;
+    pmc_semi) export TMPDIR=/tmp
+           step pmc_semi_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/semi/pmc_fetch" -o run \
+                -- python3 bench.py --config semi --steps 2 --warmup 3 --queries 0 --no-cpu-baseline --no-cold
+           step pmc_semi_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/semi/pmc_write" -o run \
+                -- python3 bench.py --config semi --steps 2 --warmup 3 --queries 0 --no-cpu-baseline --no-cold
+           step prof_semi2 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/semi/prof" -o run \
+                -- python3 bench.py --config semi --steps 2 --warmup 3 --queries 0 --no-cpu-baseline --no-cold ;;
     pmc_sq) export TMPDIR=/tmp
            step pmc_sq 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
                 --output-format csv -d "$OUT/pmc_sq" -o run \
-                -- python3 bench.py --steps 3 --warmup 1 --queries 0 --no-cpu-baseline ;;
+                -- python3 bench.py --steps 5 --warmup 3 --queries 0 --no-cpu-baseline --no-cold ;;
     esac
 done
 echo ALLDONE

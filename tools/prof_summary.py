@@ -68,6 +68,13 @@ CONTAINS = [
     ("k_qroute", "query_route"),
     ("k_query_pairs", "query"),
     ("k_qcombine", "query"),
+    ("k_part_scatter", "bin_scatter"),  # depth bins (round 5)
+    ("k_part_hist", "part_hist"),
+    ("k_part_plan", "part_plan"),
+    ("k_depth_sample", "depth_map"),
+    ("k_depth_table", "depth_map"),
+    ("k_depth_starts", "chunk_bounds"),
+    ("k_depth_chunks", "chunk_bounds"),
 ]
 
 
@@ -151,12 +158,14 @@ def main(src: str, out: str, bench_json: str = "") -> None:
     for stage, st in summary["stages"].items():
         if any(stage.startswith(x) for x in NOT_BUILD):
             continue
+        # launches per build (0: a stage of the few builds that took another
+        # path -- the cold build, the first warm build -- not of the steady state)
         per = None
         if builds_trace and "launches" in st:
-            per = max(1, round((st["launches"] - st.get("dropped_launches", 0)) / builds_trace))
+            per = round((st["launches"] - st.get("dropped_launches", 0)) / builds_trace)
             build["device_ms"] += per * st["avg_us"] / 1e3
         if builds_pmc and "traffic_bytes" in st:
-            per_p = per if per is not None else max(1, round(st["pmc_launches"] / builds_pmc))
+            per_p = per if per is not None else round(st["pmc_launches"] / builds_pmc)
             build["traffic_bytes"] += per_p * st["traffic_bytes"]
             per = per if per is not None else per_p
         if per:
