@@ -103,6 +103,8 @@ def main() -> None:
     ap.add_argument("--queries", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold / end-to-end legs")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine option (dbi_set_option: tuning switches for experiments), repeatable")
     ap.add_argument("--no-merge", action="store_true",
                     help="N>1: shard-local indexes (no exchange) instead of one merged index")
     ap.add_argument("--merge", action="store_true", help="N=1: run the sharded (RCCL) build with one rank")
@@ -110,6 +112,10 @@ def main() -> None:
                     help="N>1 merged builds: split one proteome over the ranks (strong) or one proteome per rank")
     args = ap.parse_args()
 
+    options = {}
+    for o in args.option:
+        k, _, v = o.partition("=")
+        options[k] = int(v) if v.lstrip("-").isdigit() else v
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -135,7 +141,7 @@ def main() -> None:
     ndev = device_count()
     dev = local_rank % ndev if ndev else local_rank
     if args.config == "trembl":
-        return run_trembl(args, world, rank, dev, coord)
+        return run_trembl(args, world, rank, dev, coord, options)
 
     desc, proteome, make_params, cpu_sample = WORKLOADS[args.config]
     strong = merge and args.scaling == "strong"
@@ -147,7 +153,7 @@ def main() -> None:
     log(f"[rank {rank}] synthetic {args.config}: P={pp.n_proteins} R={pp.n_residues} ({time.time() - t0:.1f}s)")
     prm = make_params()
 
-    eng = Engine(prm, device=dev)
+    eng = Engine(prm, device=dev, options=options)
     t_ag = 0.0
     if merge:
         from dbindex_amd import shard
@@ -401,7 +407,7 @@ def main() -> None:
         # the reference's real use is a one-off build (DBIndexer.run): the cold
         # pipeline (no capacities, grids, map or graph from earlier builds),
         # and FASTA file -> index end to end
-        cold = cold_legs(eng, prm, pp, d_res, d_off, dev, args.config)
+        cold = cold_legs(eng, prm, pp, d_res, d_off, dev, args.config, options)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -552,7 +558,7 @@ def cpu_baseline_legs(prm, sample) -> dict:
                 _oix=oix)
 
 
-def cold_legs(eng, prm, pp, d_res, d_off, dev: int, config: str) -> dict:
+def cold_legs(eng, prm, pp, d_res, d_off, dev: int, config: str, options=None) -> dict:
     """The one-off build (DBIndexer.java:508-684) beside the warm steady state:
     cold_ms -- this engine forced cold (dbi_set_cold: count + emit digest,
     radix tail, full list grids; buffers kept), best of 3; first_build_ms -- a
@@ -585,7 +591,7 @@ def cold_legs(eng, prm, pp, d_res, d_off, dev: int, config: str) -> dict:
         out["first_build_ms"] = out["end_to_end"] = None
         out["note"] = "fresh-engine legs skipped: a second index of this size does not fit beside the benched one"
         return out
-    with Engine(prm, device=dev) as e2:
+    with Engine(prm, device=dev, options=options) as e2:
         e2.set_timing(False)
         synchronize(dev)
         t = time.perf_counter()
@@ -604,7 +610,7 @@ def cold_legs(eng, prm, pp, d_res, d_off, dev: int, config: str) -> dict:
         t0 = time.perf_counter()
         rp = fasta.read_fasta(path, threads=threads, with_defs=False)
         t1 = time.perf_counter()
-        with Engine(prm, device=dev) as e3:
+        with Engine(prm, device=dev, options=options) as e3:
             e3.set_timing(False)
             st3 = e3.build(rp)
             synchronize(dev)
@@ -659,7 +665,7 @@ def sample_parity(prm, sample, oix, dev: int) -> dict:
             h.update(a.view(np.uint64).tobytes() if k == "mass" else a.astype(np.uint64).tobytes())
         return h.hexdigest()[:16]
 
-    with Engine(prm, device=dev) as e2:
+    with Engine(prm, device=dev, options=options) as e2:
         st = e2.build(sample)
         g = digest(e2.export())
     o = digest(oix.unique())
@@ -727,7 +733,7 @@ def hbm_copy_gbps(dev: int, nbytes: int = 1 << 31, reps: int = 10):
     return v.value if rc == 0 else None
 
 
-def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
+def run_trembl(args, world: int, rank: int, dev: int, coord, options=None) -> None:
     """BASELINE.json configs[4]: TrEMBL-scale synthetic proteome (50M proteins,
     ~1.8e10 residues), non-specific digestion 6-50, COUNT only: ~7e11 peptide
     occurrences (~12 TB of records) cannot be materialised, so a step digests
@@ -745,7 +751,7 @@ def run_trembl(args, world: int, rank: int, dev: int, coord) -> None:
     p0, p1 = P * rank // world, P * (rank + 1) // world
     tables = fasta.synth_tables()
     prm = DBIndexSearchParams.non_specific(50)
-    eng = Engine(prm, device=dev)
+    eng = Engine(prm, device=dev, options=options)
     nb = int(prm.index_factor)  # SQLiteMult buckets (+1: past the last one)
     comm = None
     if world > 1:  # the per-bucket counts are summed over the ranks by RCCL (ncclAllReduce)

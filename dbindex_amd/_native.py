@@ -113,6 +113,8 @@ SIGNATURES = [
     ("dbi_device_view", c_int, [P, POINTER(DbiDeviceIndex)]),
     ("dbi_set_timing", c_int, [P, c_int, c_char_p]),
     ("dbi_set_cold", c_int, [P]),
+    ("dbi_set_option", c_int, [P, c_char_p, ctypes.c_int64]),
+    ("dbi_set_option_str", c_int, [P, c_char_p, c_char_p]),
     ("dbi_set_bucket_drop", c_int, [P, c_int]),
     ("dbi_set_windows", c_int, [P, P, P, c_uint64, c_int]),
     ("dbi_rebuild", c_int, [P]),

@@ -2555,16 +2555,8 @@ hipError_t launch_radix_hist_u8(const uint8_t* d_dig, uint32_t n, int bits, uint
     if (n == 0) return hipSuccess;
     const uint32_t g = (n + RADIX_CHUNK - 1) / RADIX_CHUNK;
     const uint32_t per = std::min<uint32_t>(HIST_U8_PER_MAX, std::max<uint32_t>(1u, g / 2048u));
-    static const bool rows = [] {
-        const char* e = std::getenv("DBI_HIST_ROWS");
-        return e ? std::atoi(e) != 0 : true;
-    }();
-    if (rows)
-        DBI_LAUNCH(k_radix_hist_u8<true>, dim3((g + per - 1) / per), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist,
-                   g, per, d_n);
-    else
-        DBI_LAUNCH(k_radix_hist_u8<false>, dim3((g + per - 1) / per), dim3(RADIX_THREADS), 0, s, d_dig, n, bits,
-                   d_hist, g, per, d_n);
+    DBI_LAUNCH(k_radix_hist_u8<true>, dim3((g + per - 1) / per), dim3(RADIX_THREADS), 0, s, d_dig, n, bits, d_hist,
+               g, per, d_n);
     return hipGetLastError();
 }
 
@@ -4661,18 +4653,10 @@ hipError_t launch_finalize(const Rec* d_recs, const uint32_t* d_chunk_lo, uint32
                            uint32_t* d_occ_off, uint32_t* d_occ_pid, int32_t factor, uint32_t ucap, uint32_t cstride,
                            uint32_t n_kept, const unsigned long long* d_n, Counters* d_ctr, hipStream_t s) {
     if (nchunks == 0) return launch_write_tail(d_occ_off, n_kept, d_ctr, s, d_n);
-    static const int variant = [] {
-        const char* e = std::getenv("DBI_FIN");
-        return e ? std::atoi(e) : 0;
-    }();
 #define DBI_FIN_LAUNCH(NT, K)                                                                                  \
     DBI_LAUNCH((k_finalize<NT, K>), dim3(nchunks), dim3(NT), 0, s, d_recs, d_chunk_lo, d_ubase, d_umass, d_upid, \
                d_uoff, d_ulen, d_occ_off, d_occ_pid, factor, ucap, cstride, n_kept, d_n, d_ctr)
-    switch (variant) {
-        case 1: DBI_FIN_LAUNCH(256, 4); break;  // round 3's shape
-        case 2: DBI_FIN_LAUNCH(512, 4); break;
-        default: DBI_FIN_LAUNCH(256, 8); break;
-    }
+    DBI_FIN_LAUNCH(256, 8);  // (256 x 4, round 3's shape, and 512 x 4 measured slower: DESIGN.md §6 round 4)
 #undef DBI_FIN_LAUNCH
     return hipGetLastError();
 }

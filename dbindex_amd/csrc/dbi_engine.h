@@ -293,6 +293,12 @@ struct dbi_handle {
     bool depth_keep_map = false;          // this build's retry keeps the depth map it computed (dtab)
     bool cur_local = false, tail_local = false;  // this / the last finished build's chunk sort took depth-bin chunks
     bool force_cold = false;              // dbi_set_cold: the next build takes the cold path (buffers kept)
+    // dbi_set_option: sharded-build switches and test hooks
+    bool opt_shard_full_path = false;     // one rank takes the general path (partition, exchange, agreement)
+    bool opt_shard_dev_digest = true;     // warm shard digests device-sized
+    bool opt_shard_resample = false;      // every sharded build samples its split again
+    int opt_test_split_skew = -1;         // this rank's reused split is skewed (a forced resample)
+    std::string opt_test_fail;            // "<phase>@<rank>": an injected local failure
     double depth_slack = 1.25;            // region capacity / its share of the previous build's records
     uint64_t prev_unique = 0;             // uniques of the resident index (the depth map's sample)
     DevBuf<Rec> recR;                     // the digest's regions

@@ -735,12 +735,6 @@ int build_digest(dbi_handle* h) {
                                             "one device: shard the FASTA");
         const bool grid_short = chunk_lists_short(h);
         const bool part_over = (h->hc.err & ERR_PART) != 0;
-        if (std::getenv("DBI_DEBUG_BUILD"))
-            fprintf(stderr, "[dbi] attempt %d: need %llu n_in %llu grid_short %d (err %u mid %u/%u big %u/%u) part_over %d "
-                            "kept %llu slots %llu tail_n %llu part_chunks %u depth_w %llu\n",
-                    attempt, (unsigned long long)need, (unsigned long long)n_in, (int)grid_short, h->hc.err, h->hc.n_mid,
-                    h->grid_mid, h->hc.n_big, h->grid_big, (int)part_over, h->hc.n_kept, h->hc.n_slots, h->hc.tail_n,
-                    h->hc.part_chunks, h->hc.depth_w);
         if (need <= n_in && !grid_short && !part_over) {
             h->hc_final = true;
             h->depth_off = false;
@@ -1137,15 +1131,7 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     h->params = *params;
     h->dp = make_dev_params(*params);
     h->device = device;
-    // tuning knobs (defaults are the measured best; environment overrides for experiments)
-    if (const char* ev = std::getenv("DBI_BIN_BITS_MAX")) h->bin_bits_max = std::max(1, std::min(32, std::atoi(ev)));
-    if (const char* ev = std::getenv("DBI_SPLIT_ABOVE")) h->split_above = (uint32_t)std::max(1, std::atoi(ev));
-    if (const char* ev = std::getenv("DBI_CHUNK_T")) h->chunk_t = (uint32_t)std::max(64, std::min(CHUNK_CAP, std::atoi(ev)));
-    if (const char* ev = std::getenv("DBI_BUILD_GRAPH")) h->use_graph = std::atoi(ev) != 0;
-    if (const char* ev = std::getenv("DBI_DIGEST_HIST")) h->use_h1 = std::atoi(ev) != 0;
-    if (const char* ev = std::getenv("DBI_SEMI_BOUNDED")) h->use_semi_bounded = std::atoi(ev) != 0;
-    if (const char* ev = std::getenv("DBI_BIG_SPLIT")) h->big_split = std::atoi(ev) != 0 ? 1 : 0;
-    if (const char* ev = std::getenv("DBI_DEPTH")) h->use_depth = std::atoi(ev) != 0;
+    // (tuning switches and test hooks: dbi_set_option; the defaults are the measured best)
     auto fail = [&](int code) {
         dbi_close(h);
         return code;
@@ -1605,6 +1591,40 @@ int dbi_rebuild(dbi_handle* h) {
     h->d_poff = h->poff.p;
     if ((rc = build_digest(h))) return rc;
     return finish_build(h);
+}
+
+int dbi_set_option(dbi_handle* h, const char* name, int64_t value) {
+    if (!h || !name) return set_error(DBI_E_INVALID, "NULL argument");
+    std::lock_guard<std::recursive_mutex> lk(h->qmu);
+    const std::string n(name);
+    const bool on = value != 0;
+    auto ranged = [&](int64_t lo, int64_t hi) { return value >= lo && value <= hi; };
+    if (n == "build_graph") h->use_graph = on;
+    else if (n == "digest_hist") h->use_h1 = on;
+    else if (n == "semi_bounded") h->use_semi_bounded = on;
+    else if (n == "depth_bins") h->use_depth = on;
+    else if (n == "big_split" && ranged(-1, 1)) h->big_split = (int)value;
+    else if (n == "bin_bits_max" && ranged(1, 32)) h->bin_bits_max = (int)value;
+    else if (n == "split_above" && ranged(1, 1ll << 31)) h->split_above = (uint32_t)value;
+    else if (n == "chunk_target" && (value == 0 || ranged(64, CHUNK_CAP))) h->chunk_t = (uint32_t)value;
+    else if (n == "shard_full_path") h->opt_shard_full_path = on;
+    else if (n == "shard_dev_digest") h->opt_shard_dev_digest = on;
+    else if (n == "shard_resample") h->opt_shard_resample = on;
+    else if (n == "test_split_skew" && ranged(-1, 1 << 20)) h->opt_test_split_skew = (int)value;
+    else return set_error(DBI_E_INVALID, "unknown option or value out of range: " + n);
+    drop_graph(h);  // a captured build bakes the old setting in
+    h->prev_key_valid = false;
+    return 0;
+}
+
+int dbi_set_option_str(dbi_handle* h, const char* name, const char* value) {
+    if (!h || !name || !value) return set_error(DBI_E_INVALID, "NULL argument");
+    std::lock_guard<std::recursive_mutex> lk(h->qmu);
+    if (std::string(name) == "test_fail") {
+        h->opt_test_fail = value;
+        return 0;
+    }
+    return set_error(DBI_E_INVALID, std::string("unknown string option: ") + name);
 }
 
 int dbi_set_cold(dbi_handle* h) {

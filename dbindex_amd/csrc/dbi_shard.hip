@@ -332,10 +332,9 @@ int peer_failed(const char* phase) {
 // Test hook: DBI_TEST_FAIL="<phase>@<rank>" makes that rank fail locally at
 // that phase (digest, partition, buffers, merge, qroute, qbuffers), so the
 // agreement paths run without a real failure.
-int injected_failure(const char* phase, int rank) {
-    const char* e = std::getenv("DBI_TEST_FAIL");
-    if (!e || std::string(e) != std::string(phase) + "@" + std::to_string(rank)) return 0;
-    return set_error(DBI_E_STATE, std::string("injected failure (DBI_TEST_FAIL) in ") + phase);
+int injected_failure(const dbi_handle* h, const char* phase, int rank) {
+    if (h->opt_test_fail.empty() || h->opt_test_fail != std::string(phase) + "@" + std::to_string(rank)) return 0;
+    return set_error(DBI_E_STATE, std::string("injected failure (option test_fail) in ") + phase);
 }
 
 // max over ranks of (rc != 0): 0 when every rank succeeded
@@ -1171,7 +1170,7 @@ int dbi_query_sharded(dbi_handle* h, dbi_comm* c, const double* d_mass, const do
     hipStream_t s = h->stream;
     const int n = c->nranks, me = c->rank;
     int rc_route = query_route(h, d_mass, d_tol, nq);
-    if (!rc_route) rc_route = injected_failure("qroute", me);
+    if (!rc_route) rc_route = injected_failure(h, "qroute", me);
     if (rc_route) sh.qsend_count.assign(n, 0);
     std::vector<uint64_t> counts;
     bool failed = false;
@@ -1186,7 +1185,7 @@ int dbi_query_sharded(dbi_handle* h, dbi_comm* c, const double* d_mass, const do
     int rc_local = h->qrecv.ensure(sh.q_recv + 1);
     if (!rc_local) rc_local = h->qres.ensure(sh.q_recv + 1);
     if (!rc_local) rc_local = ensure_qdir(h, s);
-    if (!rc_local) rc_local = injected_failure("qbuffers", me);
+    if (!rc_local) rc_local = injected_failure(h, "qbuffers", me);
     if ((rc = agree(c, rc_local, s, &failed))) return rc;
     if (rc_local) return rc_local;
     if (failed) return peer_failed("query buffers");
@@ -1547,8 +1546,7 @@ int build_single_owner(dbi_handle* h, const uint8_t* d_res, uint64_t n_res, cons
 bool shard_dev_ok(const dbi_handle* h, const uint8_t* d_res, uint64_t n_res, const uint64_t* d_poff, uint64_t n_prot,
                   uint64_t p_begin, uint64_t p_end) {
     const auto& dv = h->shard_dev;
-    const char* off = std::getenv("DBI_SHARD_DEV_DIGEST");
-    return dv.valid && !(off && off[0] == '0') && dv.d_res == d_res && dv.d_poff == d_poff && dv.n_res == n_res &&
+    return dv.valid && h->opt_shard_dev_digest && dv.d_res == d_res && dv.d_poff == d_poff && dv.n_res == n_res &&
            dv.n_prot == n_prot && dv.p_begin == p_begin && dv.p_end == p_end && dv.e1 > dv.e0 &&
            h->recA.cap >= 1024 && bounded_digest(h);
 }
@@ -1628,10 +1626,9 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     if (!h || !c) return set_error(DBI_E_INVALID, "NULL argument");
     if (c->device != h->device) return set_error(DBI_E_INVALID, "communicator and engine on different devices");
     const int n = c->nranks, me = c->rank;
-    // DBI_SHARD_FULL_PATH=1: one rank takes the general path too (tests of the
-    // partition / exchange / agreement code at N=1)
-    const char* full_path = std::getenv("DBI_SHARD_FULL_PATH");
-    if (n == 1 && p_begin == 0 && p_end == n_prot && !(full_path && full_path[0] == '1'))
+    // option shard_full_path: one rank takes the general path too (tests of
+    // the partition / exchange / agreement code at N=1)
+    if (n == 1 && p_begin == 0 && p_end == n_prot && !h->opt_shard_full_path)
         return build_single_owner(h, d_res, n_res, d_poff, n_prot);
     int rc;
     // a rank that fails locally still takes part in the next collective, with
@@ -1639,14 +1636,13 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     const double t_digest = now_ms();
     auto& wm = h->shard_warm;
     const auto& pf = h->shard_prof;
-    const char* resample = std::getenv("DBI_SHARD_RESAMPLE");
     // a warm build of the same shard with a reusable split digests
     // device-sized: no host round trip before the count matrix
-    const bool dev_digest = wm.valid && wm.n == n && !(resample && resample[0] == '1') &&
+    const bool dev_digest = wm.valid && wm.n == n && !h->opt_shard_resample &&
                             shard_dev_ok(h, d_res, n_res, d_poff, n_prot, p_begin, p_end);
     int rc_digest = dev_digest ? shard_digest_dev(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n)
                                : dbi_shard_digest(h, d_res, n_res, d_poff, n_prot, p_begin, p_end, me, n);
-    if (!rc_digest) rc_digest = injected_failure("digest", me);
+    if (!rc_digest) rc_digest = injected_failure(h, "digest", me);
     ShardState& sh = h->shard;
     hipStream_t s = h->stream;
 
@@ -1654,12 +1650,12 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // (computed from the sorted samples of the last sampled build and the
     // updated cost profile -- the same inputs, hence the same split, on every
     // rank); the count matrix carries a hash of each rank's split.  A rank
-    // without one (a new handle, another communicator size, DBI_SHARD_RESAMPLE=1)
+    // without one (a new handle, another communicator size, option shard_resample)
     // or ranks that disagree: every rank samples (the samples all-gather, with
     // a fingerprint of each rank's cost profile: profiles that differ are not
     // used), and partitions again.  The decision is taken from the gathered
     // matrix, so every rank takes the same collectives.
-    bool have_split = wm.valid && wm.n == n && !(resample && resample[0] == '1');
+    bool have_split = wm.valid && wm.n == n && !h->opt_shard_resample;
     int32_t split[MAX_SHARDS - 1] = {};
     if (have_split) std::copy(wm.split, wm.split + (n - 1), split);
     bool sampled = false;
@@ -1723,14 +1719,13 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
         }
         int rc_part = rc_digest;
         if (round == 0 && have_split) {
-            // test hook: DBI_TEST_SPLIT_SKEW=<rank> -- that rank's reused split
+            // test hook (option test_split_skew = this rank): its reused split
             // differs from its peers' (another build history): the count
             // matrix's hashes disagree and every rank samples again
-            const char* sk = std::getenv("DBI_TEST_SPLIT_SKEW");
-            if (sk && std::atoi(sk) == me && n > 1) split[0] += 1;
+            if (h->opt_test_split_skew == me && n > 1) split[0] += 1;
         }
         if (!rc_part && have_split) rc_part = partition_launch(h, split);
-        if (!rc_part) rc_part = injected_failure("partition", me);
+        if (!rc_part) rc_part = injected_failure(h, "partition", me);
         unsigned long long* my_row = c->d_cnt + (size_t)me * w;
         if (!rc_part && have_split && sh.n_in > 0) {
             hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(64), 0, s, h->hist.p, sh.part_blocks, (uint32_t)n,
@@ -1810,7 +1805,7 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // learns it before the exchange (a collective only when someone grows)
     if (grow) {
         int rc_local = h->xrecv.ensure(std::max<uint64_t>(roff[n], 1));
-        if (!rc_local) rc_local = injected_failure("buffers", me);
+        if (!rc_local) rc_local = injected_failure(h, "buffers", me);
         if ((rc = agree(c, rc_local, s, &failed))) return rc;
         if (rc_local) return rc_local;
         if (failed) return peer_failed("owner buffers");
@@ -1848,7 +1843,7 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
             if (attempt > 0) h->nstage = nstage0;
             rc_merge = merge_enqueue(h, mr, attempt);
         }
-        if (!rc_merge && attempt == 0) rc_merge = injected_failure("merge", me);
+        if (!rc_merge && attempt == 0) rc_merge = injected_failure(h, "merge", me);
         unsigned long long row[TOTALS_W] = {};
         row[0] = sh.n_total;
         row[1] = sh.n_dropped;

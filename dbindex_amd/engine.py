@@ -40,7 +40,9 @@ class BuildStats:
 
 
 class Engine:
-    def __init__(self, params, device: int = 0):
+    def __init__(self, params, device: int = 0, options=None):
+        """options: {name: value} for dbi_set_option / dbi_set_option_str
+        (tuning switches and test hooks, e.g. {"depth_bins": 0})."""
         if isinstance(params, DBIndexSearchParams):
             params = params.to_c()
         assert isinstance(params, DbiParams)
@@ -50,6 +52,15 @@ class Engine:
         check(_native.lib().dbi_open(ctypes.byref(params), device, ctypes.byref(h)))
         self.h = h
         self._keep = None
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
+
+    def set_option(self, name: str, value) -> None:
+        """dbi_set_option (int) or dbi_set_option_str (str)."""
+        if isinstance(value, str):
+            check(_native.lib().dbi_set_option_str(self.h, name.encode(), value.encode()))
+        else:
+            check(_native.lib().dbi_set_option(self.h, name.encode(), int(value)))
 
     def close(self) -> None:
         if getattr(self, "h", None):

@@ -257,6 +257,21 @@ int dbi_device_view(dbi_handle* h, dbi_device_index* out);
  * ms[i] = 0 for a stage that launched nothing or with timing off;
  * bytes[i] = algorithmic HBM bytes of that launch.
  * Arrays may be NULL to query *n. */
+/* Tuning switches and test hooks of one handle -- experiments and the test
+ * suite; the defaults are the measured best, and nothing is read from the
+ * environment.  Integer options: "build_graph", "digest_hist",
+ * "semi_bounded", "depth_bins" (0 / 1: the warm build's hipGraph, the
+ * digest-counted first radix histogram of small tails, the bounded
+ * semi-specific digest, depth bins); "big_split" (-1: by the list length, 0,
+ * 1: the big chunk tier's two size classes); "bin_bits_max", "split_above",
+ * "chunk_target" (0: by size); "shard_full_path", "shard_dev_digest",
+ * "shard_resample" (0 / 1, dbi_build_sharded); "test_split_skew" (a rank, -1
+ * off: that rank's reused owner split is skewed).  String option
+ * "test_fail" = "<phase>@<rank>" (or ""): an injected local failure of a
+ * sharded build or query.  DBI_E_INVALID for an unknown name or value. */
+int dbi_set_option(dbi_handle* h, const char* name, int64_t value);
+int dbi_set_option_str(dbi_handle* h, const char* name, const char* value);
+
 /* The next build starts cold, as the one-off build of DBIndexer.run
  * (DBIndexer.java:508-684) does: no capacity, chunk-list grids, depth-bin map
  * or build graph carried over from earlier builds (count + emit digest, the

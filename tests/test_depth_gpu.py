@@ -34,24 +34,23 @@ def _stages(eng):
     return {name for name, _, _ in eng.stage_times()}
 
 
-@pytest.mark.parametrize("depth", ["1", "0"])
-def test_depth_warm_builds_match_oracle(Engine, monkeypatch, depth):
+@pytest.mark.parametrize("depth", [1, 0])
+def test_depth_warm_builds_match_oracle(Engine, depth):
     """Human scale (configs[1], 1.9M records): cold, then warm builds -- every
     stage timed (no graph), then untimed (captured, replayed) -- each equal to
-    the oracle; with DBI_DEPTH=0 the radix tail runs instead."""
-    monkeypatch.setenv("DBI_DEPTH", depth)
+    the oracle; with option depth_bins=0 the radix tail runs instead."""
     pp = fasta.config("human")
     cp = DBIndexSearchParams.trypsin(2).to_c()
     oix = cref.Index(cp, pp.residues, pp.offsets)
-    with Engine(cp) as eng:
+    with Engine(cp, options={"depth_bins": depth}) as eng:
         eng.build(pp)
         assert "bin_scatter" not in _stages(eng)  # cold: count + emit, the radix tail
         assert_index_equal(eng, oix, "cold")
         for k in range(2):
             eng.build(pp)
             names = _stages(eng)
-            assert ("bin_scatter" in names) == (depth == "1"), names
-            assert ("radix_scatter" in names) == (depth == "0"), names
+            assert ("bin_scatter" in names) == (depth == 1), names
+            assert ("radix_scatter" in names) == (depth == 0), names
             assert_index_equal(eng, oix, f"warm timed {k}")
         eng.set_timing(False)
         for k in range(4):

@@ -161,16 +161,16 @@ def test_big_bins_and_duplicates(Engine, copies):
         assert_index_equal(eng, oix, f"bigbins x{copies}")
 
 
-@pytest.mark.parametrize("h1", ["1", "0"])
-def test_digest_counted_histogram(Engine, h1, monkeypatch):
+@pytest.mark.parametrize("h1", [1, 0])
+def test_digest_counted_histogram(Engine, h1):
     """Warm bounded builds of small tails count the first radix pass's
-    histogram in the digest (DBI_DIGEST_HIST, default on below 16 M slots):
+    histogram in the digest (option digest_hist, default on below 16 M slots;
+    the radix tail: depth bins off):
     no histogram kernel for that pass, the same index.  ~400 k records: 2^16
     bins, two 8-bit passes, so the LDS counters cover one radix chunk per tile
     and every tile region that crosses a chunk boundary takes the global
     atomic path; cleavage-dense proteins ("AK" repeats: ~8000 slots per
     4096-start tile) span several chunks."""
-    monkeypatch.setenv("DBI_DIGEST_HIST", h1)
     base = fasta.config("human")
     seqs = [base.sequence(i) for i in range(4000)]
     seqs[100:100] = ["AK" * 3000, "GAKR" * 1500, "AKK" * 2000]
@@ -178,7 +178,7 @@ def test_digest_counted_histogram(Engine, h1, monkeypatch):
     cp = DBIndexSearchParams.trypsin(2).to_c()
     oix = cref.Index(cp, pp.residues, pp.offsets)
     m, t = query_masses(oix, 1000)
-    with Engine(cp) as eng:
+    with Engine(cp, options={"digest_hist": h1, "depth_bins": 0}) as eng:
         hists = []
         for k in range(4):  # cold, warm, warm (captured), replay
             eng.build(pp)

@@ -6,8 +6,8 @@ warm build of a bounded digest is captured as a hipGraph and every later one
 replays it.  Every build of these sequences must equal the oracle: plain,
 capture, replays, a different proteome in between (new key: plain again), a
 bigger one (the reservation grows: the build is redone), timing of one stage
-(event nodes in the graph) and the graph switched off (DBI_BUILD_GRAPH=0 is
-read at dbi_open)."""
+(event nodes in the graph) and the graph switched off (option build_graph=0);
+with depth bins (the default for warm tryptic builds) and the radix tail."""
 from __future__ import annotations
 
 import numpy as np
@@ -39,9 +39,8 @@ def _dev(env, pp):
     return d_res, d_off
 
 
-@pytest.mark.parametrize("graph", ["1", "0"])
-def test_warm_builds_and_graph_replays_match_oracle(env, monkeypatch, graph):
-    monkeypatch.setenv("DBI_BUILD_GRAPH", graph)
+@pytest.mark.parametrize("graph,depth", [(1, 1), (0, 1), (1, 0)])
+def test_warm_builds_and_graph_replays_match_oracle(env, graph, depth):
     Engine = env[0]
     hum = fasta.config("human")
     a, b = hum.slice(0, 6000), hum.slice(6000, 9000)
@@ -54,14 +53,14 @@ def test_warm_builds_and_graph_replays_match_oracle(env, monkeypatch, graph):
         d_res, d_off = bufs[id(p)]
         return eng.build_device(d_res.ptr, p.n_residues, d_off.ptr, p.n_proteins)
 
-    with Engine(cp) as eng:
+    with Engine(cp, options={"build_graph": graph, "depth_bins": depth}) as eng:
         eng.set_timing(False)
         seq = [a, a, a, a, a, b, b, b, a, a, big, big, big, a]
         want = {id(a): oa, id(b): ob, id(big): obig}
         for k, p in enumerate(seq):
             st = build(eng, p)
             assert st.n_total == want[id(p)].n_total, k
-            assert_index_equal(eng, want[id(p)], f"graph={graph} build {k}")
+            assert_index_equal(eng, want[id(p)], f"graph={graph} depth={depth} build {k}")
         m, t = query_masses(oa, 3000, seed=21)
         assert_queries_equal(eng, oa, m, t, f"graph={graph} queries after replays")
         # one stage timed: event nodes inside the graph
@@ -73,8 +72,8 @@ def test_warm_builds_and_graph_replays_match_oracle(env, monkeypatch, graph):
             assert times.get("digest", 0.0) > 0.0 and times.get("radix_scatter", 0.0) == 0.0
 
 
-@pytest.mark.parametrize("graph", ["1", "0"])
-def test_replays_over_rewritten_inputs(env, monkeypatch, graph):
+@pytest.mark.parametrize("graph,depth", [(1, 1), (0, 1), (1, 0)])
+def test_replays_over_rewritten_inputs(env, graph, depth):
     """A caller that rewrites its residues IN PLACE (a reused staging buffer:
     same d_res, n_res, n_prot) replays the captured graph over new contents.
     Nothing the graph bakes in depends on the contents -- grids and buffers
@@ -82,7 +81,6 @@ def test_replays_over_rewritten_inputs(env, monkeypatch, graph):
     device -- and whatever the new contents outgrow (digest slots, chunk-list
     grids, a first giant chunk) is caught by the one host check and the build
     is redone.  Every build must equal the oracle of what the buffer holds."""
-    monkeypatch.setenv("DBI_BUILD_GRAPH", graph)
     Engine, _, synchronize = env
     a = fasta.config("human").slice(0, 6000)
     # B: the same offsets over the residues reversed (other peptides, other counts)
@@ -99,7 +97,7 @@ def test_replays_over_rewritten_inputs(env, monkeypatch, graph):
     assert want["c"].n_total > want["a"].n_total
     d_res, d_off = _dev(env, a)
     contents = {"a": a, "b": b, "c": c}
-    with Engine(cp) as eng:
+    with Engine(cp, options={"build_graph": graph, "depth_bins": depth}) as eng:
         eng.set_timing(False)
         seq = ["a", "a", "a", "a", "b", "b", "b", "c", "c", "c", "c", "a", "a", "b", "c"]
         cur = "a"
@@ -110,6 +108,6 @@ def test_replays_over_rewritten_inputs(env, monkeypatch, graph):
                 cur = name
             st = eng.build_device(d_res.ptr, a.n_residues, d_off.ptr, a.n_proteins)
             assert st.n_total == want[name].n_total, (k, name)
-            assert_index_equal(eng, want[name], f"graph={graph} build {k} ({name})")
+            assert_index_equal(eng, want[name], f"graph={graph} depth={depth} build {k} ({name})")
         m, t = query_masses(want["c"], 2000, seed=5)
         assert_queries_equal(eng, want["c"], m, t, f"graph={graph} queries over the spiked proteome")

@@ -52,7 +52,7 @@ comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
 try:
     with Engine(cp, 0) as eng:
         for full_path in ("0", "1"):
-            os.environ["DBI_SHARD_FULL_PATH"] = full_path
+            eng.set_option("shard_full_path", int(full_path))
             for rep in ("cold", "warm"):
                 st = shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
                                          0, pp.n_proteins)

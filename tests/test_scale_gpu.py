@@ -119,20 +119,18 @@ def test_swissprot_sharded_8_shards(Engine, swissprot, swissprot_oix):
 
 
 @pytest.mark.parametrize("big_split", ["auto", "1"])
-def test_swissprot_semi_slice(Engine, swissprot, big_split, monkeypatch):
+def test_swissprot_semi_slice(Engine, swissprot, big_split):
     """configs[3] parity on a 30k-protein slice (~55M semi-tryptic peptides),
     large enough to reach the 1024-thread big-chunk tier (equal-mass spikes).
-    DBI_BIG_SPLIT=1: the big tier in its two size classes (512-thread blocks
+    option big_split=1: the big tier in its two size classes (512-thread blocks
     for chunks of up to 3968 records, the rest 1024-thread), which the engine
     otherwise uses only for lists longer than 1024 chunks (full semi-tryptic)."""
-    if big_split != "auto":
-        monkeypatch.setenv("DBI_BIG_SPLIT", big_split)
     pp = swissprot.slice(0, 30000)
     cp = DBIndexSearchParams.semi_tryptic(2).to_c()
     with cref.threads(THREADS):
         oix = cref.Index(cp, pp.residues, pp.offsets)
         m, t = query_masses(oix, 1_000_000)
-        with Engine(cp) as eng:
+        with Engine(cp, options={} if big_split == "auto" else {"big_split": int(big_split)}) as eng:
             for phase in ("cold", "warm", "replay"):
                 st = eng.build(pp)
                 assert st.n_big_bins > 0, "slice too small to reach the big-chunk tier"

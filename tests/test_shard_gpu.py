@@ -140,12 +140,11 @@ def test_sharded_human_scale(native):
 
 
 @pytest.mark.parametrize("full_path", ["0", "1"])
-def test_sharded_rccl_single_rank(native, full_path, monkeypatch):
+def test_sharded_rccl_single_rank(native, full_path):
     """One rank: the single-owner build (the single-device build plus the
-    shard bookkeeping), and with DBI_SHARD_FULL_PATH=1 the general path
+    shard bookkeeping), and with option shard_full_path=1 the general path
     (samples, partition, exchange to itself, owner merge)."""
     from dbindex_amd.engine import Engine
-    monkeypatch.setenv("DBI_SHARD_FULL_PATH", full_path)
     pp = fasta.config("1k")
     prm = DBIndexSearchParams.trypsin(2)
     cp = prm.to_c()
@@ -153,7 +152,7 @@ def test_sharded_rccl_single_rank(native, full_path, monkeypatch):
     d_res, d_off = _inputs(native, pp)
     comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
     try:
-        with Engine(cp, 0) as eng:
+        with Engine(cp, 0, options={"shard_full_path": int(full_path)}) as eng:
             for rep in ("cold", "warm"):
                 st = shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
                                          0, pp.n_proteins)
@@ -185,15 +184,14 @@ def test_shard_phase_order(native):
 
 
 @pytest.mark.parametrize("phase", ["digest", "partition", "buffers", "merge", "qroute", "qbuffers"])
-def test_sharded_rccl_local_failure_is_reported(native, phase, monkeypatch):
+def test_sharded_rccl_local_failure_is_reported(native, phase):
     """A rank that fails locally still joins the next collective with its
     status, so every rank returns an error instead of waiting in RCCL
-    (DBI_TEST_FAIL injects the failure; one rank here, the agreement
+    (option test_fail injects the failure; one rank here, the agreement
     collectives are the same at N ranks).  The engine and the communicator
     stay usable: the next build and query batch succeed."""
     from dbindex_amd import _native
     from dbindex_amd.engine import Engine
-    monkeypatch.setenv("DBI_SHARD_FULL_PATH", "1")  # one rank: the general path, not the single-owner build
     pp = fasta.config("1k").slice(0, 200)
     cp = DBIndexSearchParams.trypsin(2).to_c()
     oix = cref.Index(cp, pp.residues, pp.offsets)
@@ -203,16 +201,16 @@ def test_sharded_rccl_local_failure_is_reported(native, phase, monkeypatch):
     df, dc = native.DeviceBuffer(8 * m.shape[0], 0), native.DeviceBuffer(8 * m.shape[0], 0)
     comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
     try:
-        with Engine(cp, 0) as eng:
+        with Engine(cp, 0, options={"shard_full_path": 1}) as eng:  # one rank: the general path, not the single-owner build
             build = lambda: shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
                                                 0, pp.n_proteins)
             query = lambda: shard.query_sharded(eng, comm, dm.ptr, dt.ptr, m.shape[0], df.ptr, dc.ptr)
             if phase.startswith("q"):
                 build()
-            monkeypatch.setenv("DBI_TEST_FAIL", f"{phase}@0")
+            eng.set_option("test_fail", f"{phase}@0")
             with pytest.raises(_native.DBIndexStoreException, match="injected failure"):
                 query() if phase.startswith("q") else build()
-            monkeypatch.delenv("DBI_TEST_FAIL")
+            eng.set_option("test_fail", "")
             st = build()
             assert st.g_total == oix.n_total and st.g_unique == oix.n_unique
             query()
@@ -256,9 +254,8 @@ def test_replicated_index_local(native, k, nprot):
 
 
 @pytest.mark.parametrize("full_path", ["0", "1"])
-def test_replicated_index_rccl_single_rank(native, full_path, monkeypatch):
+def test_replicated_index_rccl_single_rank(native, full_path):
     from dbindex_amd.engine import Engine
-    monkeypatch.setenv("DBI_SHARD_FULL_PATH", full_path)
     from tests.helpers import assert_index_equal, assert_queries_equal
     pp = fasta.config("1k")
     cp = DBIndexSearchParams.trypsin(2).to_c()
@@ -266,7 +263,7 @@ def test_replicated_index_rccl_single_rank(native, full_path, monkeypatch):
     d_res, d_off = _inputs(native, pp)
     comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
     try:
-        with Engine(cp, 0) as eng:
+        with Engine(cp, 0, options={"shard_full_path": int(full_path)}) as eng:
             for rep in ("cold", "warm"):
                 shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, 0, pp.n_proteins)
                 shard.replicate(eng, comm)

@@ -50,9 +50,9 @@ def _rank_main(world: int, rank: int, name: str, plan: dict, q) -> None:
                     d_res.upload(np.concatenate([res2, np.zeros(16, np.uint8)]))
                     d_off.upload(off2.astype(np.uint64))
                     synchronize(0)
-                env = plan.get("env", {}).get(k, {})
-                for key, val in env.items():
-                    os.environ[key] = val.replace("{rank}", str(rank))
+                opts = plan.get("options", {}).get(k, {})  # {name: (value, value after the build)}
+                for key, (val, _) in opts.items():
+                    eng.set_option(key, val)
                 try:
                     st = shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, b, e)
                     out["builds"].append(dict(ok=True, export=eng.export(), sampled=st.split_sampled,
@@ -60,8 +60,8 @@ def _rank_main(world: int, rank: int, name: str, plan: dict, q) -> None:
                                               g_keys=st.g_keys, key_lo=st.key_lo, key_hi=st.key_hi))
                 except DBIndexStoreException as ex:
                     out["builds"].append(dict(ok=False, error=str(ex)))
-                for key in env:
-                    os.environ.pop(key, None)
+                for key, (_, after) in opts.items():
+                    eng.set_option(key, after)
             if plan.get("queries"):
                 rng = np.random.Generator(np.random.PCG64(100 + rank))
                 m = rng.uniform(500.0, 3000.0, 400)
@@ -166,11 +166,11 @@ def test_ranks_warm_builds_queries_replica(oracle, world):
 
 
 def test_ranks_disagreeing_split_resamples(oracle):
-    """DBI_TEST_SPLIT_SKEW on rank 1 at build 2: its reused split differs from
+    """Option test_split_skew = rank 1 at build 2: its reused split differs from
     its peers' (what a reopened handle or another build history gives); the
     hashes in the count matrix disagree, every rank samples, and the index
     still equals the oracle -- no peptide split between two owners."""
-    res = _run(3, {"builds": 4, "env": {2: {"DBI_TEST_SPLIT_SKEW": "1"}}})
+    res = _run(3, {"builds": 4, "options": {2: {"test_split_skew": (1, -1)}}})
     for k in range(4):
         builds = [r["builds"][k] for r in res]
         assert all(b["ok"] for b in builds), [b.get("error") for b in builds]
@@ -181,10 +181,10 @@ def test_ranks_disagreeing_split_resamples(oracle):
 
 @pytest.mark.parametrize("phase", ["digest", "partition", "merge"])
 def test_ranks_failure_is_agreed(oracle, phase):
-    """A local failure on rank 1 (DBI_TEST_FAIL=<phase>@1) at build 1: every
+    """A local failure on rank 1 (option test_fail = <phase>@1) at build 1: every
     rank returns an error (no rank waits in a collective), and the next build
     of the same handles and communicator equals the oracle."""
-    res = _run(2, {"builds": 3, "env": {1: {"DBI_TEST_FAIL": phase + "@1"}}})
+    res = _run(2, {"builds": 3, "options": {1: {"test_fail": (phase + "@1", "")}}})
     for r, out in enumerate(res):
         assert out["builds"][0]["ok"] and out["builds"][2]["ok"], (r, out["builds"])
         assert not out["builds"][1]["ok"], (r, phase)

@@ -16,7 +16,7 @@ where exchange = the largest per-GPU send or receive volume over one xGMI
 link per peer pair (MI355X: 7 links, ~64 GB/s achieved per direction each,
 i.e. bytes_to_peer / 64 GB/s for the slowest pair), and fixed = the
 collectives and host synchronisations of dbi_build_sharded (measured by the
-one-rank general path separately: bench.py --merge with DBI_SHARD_FULL_PATH=1).
+one-rank general path separately: bench.py --merge --option shard_full_path=1).
 Shards run one after another here, so each shard's kernels have the whole GPU
 (on N GPUs each has its own).
 """
@@ -108,17 +108,16 @@ def main() -> int:
             e.close()
     best["history"] = history
     # fixed costs of the RCCL driver per build: dbi_build_sharded with one rank
-    # on the general path (DBI_SHARD_FULL_PATH=1: samples, partition, count
+    # on the general path (option shard_full_path=1: samples, partition, count
     # matrix, exchange, owner merge, totals -- every host sync and launch gap
     # of an N-rank build) over the whole proteome; wall time minus the summed
     # kernel time.  At N ranks the collectives add their xGMI latency
     # (ALLGATHER_US each: the count matrix and the totals round of a warm build).
     if not a.no_fixed:
         import time
-        os.environ["DBI_SHARD_FULL_PATH"] = "1"
         comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
         fixed = []
-        with Engine(cp, 0) as e1:
+        with Engine(cp, 0, options={"shard_full_path": 1}) as e1:
             # kernel times from timed builds, wall times from untimed ones (a
             # build with every stage timed also waits for the exchange)
             for i in range(2 * a.reps + 4):
@@ -133,7 +132,6 @@ def main() -> int:
                 elif i >= 4:
                     fixed.append(dict(wall_ms=wall, kernels_ms=dev, fixed_ms=wall - dev))
         comm.close()
-        os.environ.pop("DBI_SHARD_FULL_PATH", None)
         f = sorted(x["fixed_ms"] for x in fixed)[len(fixed) // 2]
         best["fixed_one_rank"] = fixed
         best["fixed_ms"] = f + 2 * ALLGATHER_US * 1e-3
