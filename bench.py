@@ -418,7 +418,7 @@ def main() -> None:
         cpu = cpu_baseline_legs(prm, sample)
         oix = cpu.pop("_oix")
         cpu["queries"] = cpu_query_legs(oix, args.queries or 1_000_000)
-        cpu["sample_parity"] = sample_parity(prm, sample, oix, dev)
+        cpu["sample_parity"] = sample_parity(prm, sample, oix, dev, options)
 
     from dbindex_amd._native import runtime_info
     runtime = runtime_info()  # raises if two HIP runtimes / RCCLs are mapped
@@ -652,7 +652,7 @@ def cpu_query_legs(oix, nq: int) -> dict:
                 single_core=dict(value=n1 / t_one, unit="queries/s", cores=1, queries=n1, seconds=t_one))
 
 
-def sample_parity(prm, sample, oix, dev: int) -> dict:
+def sample_parity(prm, sample, oix, dev: int, options=None) -> dict:
     """The CPU leg's sample built on the GPU too: counts and a digest of every
     index array equal the oracle's (bit-exact)."""
     import hashlib

@@ -46,7 +46,7 @@ class DbiShardStats(ctypes.Structure):
         ("g_total", c_uint64), ("g_dropped", c_uint64), ("g_kept", c_uint64), ("g_unique", c_uint64),
         ("g_keys", c_uint64), ("digest_ms", c_double), ("partition_ms", c_double),
         ("exchange_ms", c_double), ("merge_ms", c_double), ("merge_gpu_ms", c_double),
-        ("split_sampled", c_int32), ("split_rounds", c_int32),
+        ("split_sampled", c_int32), ("split_rounds", c_int32), ("split_held", c_int32), ("reserved0", c_int32),
     ]
 
 

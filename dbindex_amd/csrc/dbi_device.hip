@@ -1632,7 +1632,13 @@ __device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const LeanSmem
 }
 
 // ---- depth bins: the digest's partition ------------------------------------
-__device__ __forceinline__ uint32_t depth_bin(double m, const DepthMap& dm) { return dm.tab[bin_of(m, dm.sub)]; }
+__device__ __forceinline__ uint32_t depth_bin(double m, const DepthMap& dm) {
+    const uint32_t sb = bin_of(m, dm.sub);
+    const uint4 e = dm.map[sb >> 6];
+    const uint64_t mask = (uint64_t)e.y << 32 | e.x;
+    const uint32_t b = e.z + (uint32_t)__popcll(mask & (~0ull >> (63u - (sb & 63u))));
+    return min(b, dm.last);  // (a map whose starts outnumber the bins: the top ones share the last)
+}
 
 // the XCD this wave runs on (HW_REG_XCC_ID, bits 3:0; MI355X_MICROARCH.md: blockIdx % 8 only says
 // which blocks share one)
@@ -2594,44 +2600,109 @@ hipError_t launch_owner_scatter(const Rec* d_in, uint64_t* d_out, uint32_t n, co
 // 4'. depth bins (warm lean builds): the map, the pass-2 plan, the pass over
 // the low digit, the chunk bounds.  See PartOut / part_tile.
 // ---------------------------------------------------------------------------
-// ns uniques of the previous index, evenly spaced, each weighted by its
-// occurrences, into the linear sub-bins (d_sub zeroed)
+// ns uniques of the previous index, evenly spaced (so in mass order): each
+// one's sub-bin and occurrence weight (capped at 4096: the weights' scan stays
+// in 32 bits; a heavier spike is heavy either way)
 __global__ void k_depth_sample(const double* __restrict__ umass, const uint32_t* __restrict__ occ_off, uint64_t nu,
-                               uint32_t ns, BinMap sub, uint32_t* __restrict__ d_sub) {
+                               uint32_t ns, BinMap sub, uint32_t* __restrict__ ss, uint32_t* __restrict__ sw) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ns) return;
     const uint64_t j = (uint64_t)i * nu / ns;
     const uint32_t w = occ_off[j + 1] - occ_off[j];
-    if (w && w <= (1u << 24)) atomicAdd(&d_sub[bin_of(umass[j], sub)], w);  // (a stale index: never a wild weight)
+    ss[i] = bin_of(umass[j], sub);
+    sw[i] = w <= (1u << 24) ? min(w, 4096u) : 0u;  // (a stale index: never a wild weight)
 }
 
 hipError_t launch_depth_sample(const double* d_umass, const uint32_t* d_occ_off, uint64_t n_unique, uint32_t ns,
-                               const BinMap& sub, uint32_t* d_sub, hipStream_t s) {
-    ns = (uint32_t)std::min<uint64_t>(ns, n_unique);
+                               const BinMap& sub, uint32_t* d_ss, uint32_t* d_sw, hipStream_t s) {
+    if (n_unique < ns) return hipErrorInvalidValue;
     if (ns == 0) return hipSuccess;
-    DBI_LAUNCH(k_depth_sample, dim3((ns + 255) / 256), dim3(256), 0, s, d_umass, d_occ_off, n_unique, ns, sub, d_sub);
+    DBI_LAUNCH(k_depth_sample, dim3((ns + 255) / 256), dim3(256), 0, s, d_umass, d_occ_off, n_unique, ns, sub, d_ss,
+               d_sw);
     return hipGetLastError();
 }
 
-// tab[s] = floor(weight before sub-bin s * nbins / total): non-decreasing, so
-// bin order is mass order; each bin ~total / nbins of the sampled weight (a
-// sub-bin heavier than that spans several bins' worth alone).  No sample:
-// the linear map.
-__global__ void k_depth_table(const uint32_t* __restrict__ pre, const Counters* __restrict__ ctr, uint32_t nsub,
-                              uint32_t nbins, int sub_bits, uint16_t* __restrict__ tab) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nsub) return;
+// Bin starts.  Sample i starts a bin at its sub-bin when its weight quantile
+// pre * nq / total differs from its predecessor's (equal depth); a heavy
+// sub-bin -- sampled weight above one mean bin, an isobaric cluster or a
+// spike -- gets a bin of its own (starts at it and after it), so a bin never
+// holds a heavy sub-bin plus its quantile's share (SwissProt: 787 -> ~420
+// depth bins above the 1 984-record chunk capacity, tools/depth_sim.py).
+// nq leaves room for the previous map's heavy sub-bins (2 starts each): the
+// bins stay <= nbins; more heavies than that only merge the top bins.
+__global__ void k_depth_mark(const uint32_t* __restrict__ ss, const uint32_t* __restrict__ pre, uint32_t ns,
+                             uint32_t nbins, uint32_t nsub, const uint32_t* __restrict__ prev_h,
+                             uint4* __restrict__ map, Counters* __restrict__ ctr) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ns) return;
     const unsigned long long tot = ctr->depth_w;
-    const uint64_t b = tot ? (uint64_t)pre[s] * nbins / tot : ((uint64_t)s * nbins) >> sub_bits;
-    tab[s] = (uint16_t)min(b, (uint64_t)nbins - 1u);
+    if (tot == 0) return;
+    const uint32_t hp = *prev_h;
+    const uint64_t nq = 4ull * hp <= nbins ? nbins - 2ull * hp : nbins / 2u;
+    const uint32_t s = ss[i];
+    auto start = [&](uint32_t b) {
+        if (b > 0 && b < nsub) atomicOr(reinterpret_cast<unsigned long long*>(&map[b >> 6]), 1ull << (b & 63u));
+    };
+    if (i > 0 && (uint64_t)pre[i] * nq / tot != (uint64_t)pre[i - 1] * nq / tot) start(s);
+    if (i > 0 && ss[i - 1] == s) return;
+    // the first sample of its sub-bin: the run's end by galloping (samples are
+    // in mass order; most runs are one sample), its weight
+    uint32_t lo = i + 1, step = 1;  // ss[lo - 1] == s
+    while (lo < ns && ss[lo] == s) {
+        const uint32_t hi = min(ns, lo + step);
+        if (hi == lo + step && ss[hi - 1] == s) {
+            lo = hi;
+            step *= 2;
+            continue;
+        }
+        uint32_t a = lo, b = hi - 1;  // ss[a] == s, the end in (a, b]
+        while (a + 1 < b) {
+            const uint32_t m = (a + b) >> 1;
+            if (ss[m] == s) a = m; else b = m;
+        }
+        lo = ss[b] == s ? b + 1 : b;
+        break;
+    }
+    const uint64_t w = (lo < ns ? (uint64_t)pre[lo] : tot) - pre[i];
+    if (w * nbins > tot) {
+        start(s);
+        start(s + 1);
+        atomicAdd(&ctr->depth_h, 1u);
+    }
 }
 
-hipError_t launch_depth_table(const uint32_t* d_sub_scan, const Counters* d_ctr, uint32_t nsub, uint32_t nbins,
-                              uint16_t* d_tab, hipStream_t s) {
-    if (nbins == 0 || nbins > 65536u || (nsub & (nsub - 1))) return hipErrorInvalidValue;
-    int sb = 0;
-    while ((1u << sb) < nsub) ++sb;
-    DBI_LAUNCH(k_depth_table, dim3((nsub + 255) / 256), dim3(256), 0, s, d_sub_scan, d_ctr, nsub, nbins, sb, d_tab);
+// map[w].z = bin starts in the words before w: one thread per word, NT words
+// a block; a block's offset is the popcount of every word before it (each
+// thread sums a strided share, issued together: L2-resident, one launch in
+// place of a multi-launch scan).  *heavy = this map's heavy count.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_depth_base(uint4* __restrict__ map, uint32_t G, uint32_t* __restrict__ heavy,
+                                                   const Counters* __restrict__ ctr) {
+    __shared__ uint32_t s_tmp[NT / 64 + 1];
+    const uint32_t w = blockIdx.x * NT + threadIdx.x;
+    uint32_t before = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x * NT; i += NT) {
+        const uint4 e = map[i];
+        before += (uint32_t)__popc(e.x) + (uint32_t)__popc(e.y);
+    }
+    const uint4 e = w < G ? map[w] : make_uint4(0, 0, 0, 0);
+    const uint32_t c = (uint32_t)__popc(e.x) + (uint32_t)__popc(e.y);
+    uint32_t boff;
+    block_excl_scan<NT, uint32_t>(before, s_tmp, boff);  // (the block's sum of `before`: its offset)
+    uint32_t tot;
+    const uint32_t run = block_excl_scan<NT, uint32_t>(c, s_tmp, tot);
+    if (w < G) map[w].z = boff + run;
+    if (w == 0) *heavy = ctr->depth_h;
+}
+
+hipError_t launch_depth_map(const uint32_t* d_ss, const uint32_t* d_pre, uint32_t ns, uint32_t nbins, uint32_t nsub,
+                            uint4* d_map, uint32_t* d_heavy, Counters* d_ctr, hipStream_t s) {
+    if (nbins == 0 || nbins > 65536u || nsub < 64 || (nsub & (nsub - 1))) return hipErrorInvalidValue;
+    if (ns)  // (no sample: one bin; the regions overflow and the radix tail redoes the build)
+        DBI_LAUNCH(k_depth_mark, dim3((ns + 255) / 256), dim3(256), 0, s, d_ss, d_pre, ns, nbins, nsub, d_heavy, d_map,
+                   d_ctr);
+    const uint32_t G = nsub / 64;
+    DBI_LAUNCH(k_depth_base<1024>, dim3((G + 1023) / 1024), dim3(1024), 0, s, d_map, G, d_heavy, d_ctr);
     return hipGetLastError();
 }
 
@@ -3791,12 +3862,20 @@ struct ChunkSmem {
     uint32_t nbig, nwide, bad;
 };
 
-// local bins of a depth-bin chunk: a power of two >= CAP / 2 (about one
-// record per bin at the chunk target), two 16-bit counters per word
+// local bins of a depth-bin chunk: a power of two >= CAP * DBI_LOCAL_X / 2,
+// two 16-bit counters per word in the k0 / k1 arrays (free until the records
+// land).  Finer local bins split more of the composition clusters: SwissProt
+// records in local bins of <= 64 / 65-512 / > 512 records, 2^10 bins per
+// 1 984-record chunk 54 / 36 / 9.6 %, 2^13 64 / 31 / 4.7 %, the limit (2^18)
+// 73 / 23 / 3.6 % (tools/depth_sim.py).
+#ifndef DBI_LOCAL_X
+#define DBI_LOCAL_X 4
+#endif
 template <int CAP>
 constexpr uint32_t local_bins() {
     uint32_t nl = 1;
-    while (nl < (uint32_t)CAP / 2) nl <<= 1;
+    while (nl < (uint32_t)CAP * DBI_LOCAL_X / 2) nl <<= 1;
+    while (nl * 2u > (uint32_t)CAP * 16u) nl >>= 1;  // inside k0 and k1
     return nl;
 }
 
@@ -3915,8 +3994,9 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
     }
     if constexpr (LOCAL) {
         constexpr uint32_t NL = local_bins<CAP>(), NLW = NL / 2, WPT = (NLW + NT - 1) / NT;
-        static_assert(NLW * 4 <= CAP * 8, "the counters inside k0");
-        uint32_t* lc = reinterpret_cast<uint32_t*>(k0);  // k0 is free until the records land
+        static_assert(NLW * 4 <= CAP * 16, "the counters inside k0 and k1");
+        static_assert(__builtin_offsetof(ChunkSmem<NT, CAP>, k1) == CAP * 8, "k1 right after k0");
+        uint32_t* lc = reinterpret_cast<uint32_t*>(k0);  // k0 and k1 are free until the records land
         const uint4* __restrict__ in4 = reinterpret_cast<const uint4*>(in);
         const uint32_t w = threadIdx.x >> 6;
         uint4 rv[E];
@@ -3955,23 +4035,26 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
             }
         }
         __syncthreads();
-        // exclusive scan of the counters in bin order; each word becomes the
-        // starts of its two bins
-        uint32_t wd[WPT], part = 0;
+        // exclusive scan of the counters in bin order (each thread WPT
+        // consecutive words, read twice rather than held); each word becomes
+        // the starts of its two bins
+        uint32_t part = 0;
 #pragma unroll
         for (uint32_t j = 0; j < WPT; ++j) {
             const uint32_t i = threadIdx.x * WPT + j;
-            wd[j] = i < NLW ? lc[i] : 0u;
-            part += (wd[j] & 0xFFFFu) + (wd[j] >> 16);
+            const uint32_t wd = i < NLW ? lc[i] : 0u;
+            part += (wd & 0xFFFFu) + (wd >> 16);
         }
         uint32_t tot;
         uint32_t run = block_excl_scan<NT, uint32_t>(part, sm.u32, tot);
 #pragma unroll
         for (uint32_t j = 0; j < WPT; ++j) {
             const uint32_t i = threadIdx.x * WPT + j;
-            const uint32_t lo = wd[j] & 0xFFFFu;
-            if (i < NLW) lc[i] = run | ((run + lo) << 16);
-            run += lo + (wd[j] >> 16);
+            if (i < NLW) {
+                const uint32_t wd = lc[i], lo = wd & 0xFFFFu;
+                lc[i] = run | ((run + lo) << 16);
+                run += lo + (wd >> 16);
+            }
         }
         __syncthreads();
         uint32_t se[E];  // the bin's start | end << 16

@@ -87,6 +87,7 @@ struct ShardState {
     double ms_digest = 0, ms_partition = 0, ms_exchange = 0, ms_merge = 0;
     double ms_merge_gpu = 0;                // device time of the owner merge's kernels
     int split_sampled = 0, split_rounds = 0;  // dbi_build_sharded: the owner split's provenance
+    bool split_held = false;                // ... and the next build keeps it (balanced owners)
     dbi_shard_stats global{};               // filled by dbi_build_sharded (RCCL sums)
     uint64_t u_base = 0;                    // first global id of this owner's unique table
     bool u_base_known = false;
@@ -288,9 +289,10 @@ struct dbi_handle {
     int big_split = -1;                   // DBI_BIG_SPLIT: big tier in two size classes (1 always, 0 never, -1 long lists)
     bool h1_on = false;                   // this warm build's digest counts the first radix histogram (h1plan)
     // depth bins (warm lean builds: dbi_engine.hip warm_body_depth)
-    bool use_depth = true;                // DBI_DEPTH=0: the radix tail always
+    bool use_depth = true;                // option depth_bins=0: the radix tail always
     bool depth_off = false;               // this build's retry takes the radix tail (a region overflowed)
-    bool depth_keep_map = false;          // this build's retry keeps the depth map it computed (dtab)
+    bool depth_keep_map = false;          // this build's retry keeps the depth map it computed
+    const uint4* depth_map_of = nullptr;  // the map buffer a complete map was last enqueued into
     bool cur_local = false, tail_local = false;  // this / the last finished build's chunk sort took depth-bin chunks
     bool force_cold = false;              // dbi_set_cold: the next build takes the cold path (buffers kept)
     // dbi_set_option: sharded-build switches and test hooks
@@ -303,8 +305,9 @@ struct dbi_handle {
     uint64_t prev_unique = 0;             // uniques of the resident index (the depth map's sample)
     DevBuf<Rec> recR;                     // the digest's regions
     DevBuf<uint8_t> rdig;                 //   each record's low bin digit
-    DevBuf<uint32_t> rcur, dsub, desc, d1c, hist2, bstart;
-    DevBuf<uint16_t> dtab;                // sub-bin -> depth bin
+    DevBuf<uint32_t> rcur, dsub, dpre, desc, d1c, hist2, bstart;  // dsub / dpre: the map's samples
+    DevBuf<uint4> dmap;                   // the depth map (DepthMap)
+    DevBuf<uint32_t> dheavy;              // its heavy sub-bins (the next map's room for them)
     const dbi::PartOut* part_now = nullptr;  // run_digest: partition the warm digest's records (warm_body_depth)
     dbi::Hist1Plan h1plan{};
     bool capturing = false;               // stage events become event nodes

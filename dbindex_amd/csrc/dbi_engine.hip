@@ -542,7 +542,11 @@ void drop_graph(dbi_handle* h) {
     h->prev_mkey_valid = false;
 }
 
-int warm_body_depth(dbi_handle* h, const DepthPlan& pl, uint64_t* n_in, bool* sparse) {
+// DEPTH_FALLBACK: no map to use (the index it samples was reallocated on the
+// way here and no earlier map is in place): the caller runs the radix tail
+constexpr int DEPTH_FALLBACK = 1;
+
+int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_t* n_in, bool* sparse) {
     hipStream_t s = h->stream;
     int rc;
     const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
@@ -555,34 +559,45 @@ int warm_body_depth(dbi_handle* h, const DepthPlan& pl, uint64_t* n_in, bool* sp
     // a buffer that queued kernels use): the tail's (chunk sort, index), the
     // depth bins', the digest's (run_digest finds them in place)
     if ((rc = tail_buffers(h, cap, cap, true)) || (rc = h->recR.ensure(nreg_slots)) ||
-        (rc = h->rdig.ensure(nreg_slots + 16)) || (rc = h->rcur.ensure(DEPTH_XCDS * 256)) || (rc = h->dsub.ensure(nsub)) ||
-        (rc = h->dtab.ensure(nsub)) || (rc = h->desc.ensure(pl.max_chunks)) || (rc = h->d1c.ensure(512)) ||
+        (rc = h->rdig.ensure(nreg_slots + 16)) || (rc = h->rcur.ensure(DEPTH_XCDS * 256)) ||
+        (rc = h->dsub.ensure(DEPTH_SAMPLES)) || (rc = h->dpre.ensure(DEPTH_SAMPLES)) || (rc = h->dmap.ensure(nsub / 64)) ||
+        (rc = h->dheavy.ensure_zeroed(1, s)) || (rc = h->desc.ensure(pl.max_chunks)) || (rc = h->d1c.ensure(512)) ||
         (rc = h->hist2.ensure((size_t)pl.max_chunks << pl.b2)) || (rc = h->bstart.ensure(pl.nbins + 1)) ||
         (rc = h->blk.ensure(std::max<uint32_t>(ntiles, 1))) ||
         (rc = h->thr.ensure((size_t)ntiles * DIGEST_THREADS + 1)) || (rc = h->tile_pf.ensure(2 * ((size_t)ntiles + 2))) ||
-        (rc = h->scan_tmp.ensure(std::max({scan_u32_tmp_elems(nsub), scan_u32_tmp_elems((uint64_t)pl.max_chunks << pl.b2),
+        (rc = h->scan_tmp.ensure(std::max({scan_u32_tmp_elems(DEPTH_SAMPLES), scan_u32_tmp_elems((uint64_t)pl.max_chunks << pl.b2),
                                            scan_u32_tmp_elems(ntiles), h->scan_tmp.cap}))))
         return rc;
     // the map, from a sample of the resident index (the previous build's)
     const uint64_t U = std::min<uint64_t>({h->prev_unique, h->umass.cap, h->occ_off.cap ? h->occ_off.cap - 1 : 0});
     const BinMap sub = make_binmap(h->params.min_mh, h->params.max_mh, nsub);
     DBI_HIP(hipMemsetAsync(h->rcur.p, 0, sizeof(uint32_t) * DEPTH_XCDS * 256, s));
-    if (!h->depth_keep_map) {  // (a redo keeps the map: the failed attempt may have overwritten the index)
-        DBI_HIP(hipMemsetAsync(h->dsub.p, 0, sizeof(uint32_t) * nsub, s));
+    const uint32_t ns = (uint32_t)std::min<uint64_t>(DEPTH_SAMPLES, U);
+    // a redo keeps the map its first attempt computed (that attempt may have
+    // overwritten the index, or the redo's larger buffers moved it); any
+    // complete map is monotone in the mass, so it is exact, only its balance
+    // may be off
+    const bool keep = h->depth_keep_map && h->depth_map_of == h->dmap.p;
+    if (!keep && !index_kept) return DEPTH_FALLBACK;
+    if (!keep) {
+        DBI_HIP(hipMemsetAsync(h->dmap.p, 0, sizeof(uint4) * (nsub / 64), s));
         STAGE(h, "depth_map", by(0, 0, 0, 0, 0), ([&]() -> hipError_t {
-                  hipError_t e = launch_depth_sample(h->umass.p, h->occ_off.p, U, DEPTH_SAMPLES, sub, h->dsub.p, s);
+                  hipError_t e = launch_depth_sample(h->umass.p, h->occ_off.p, U, ns, sub, h->dsub.p, h->dpre.p, s);
                   if (e == hipSuccess)
-                      e = launch_scan_u32(h->dsub.p, h->dsub.p, nsub, h->scan_tmp.p, h->scan_tmp.cap,
+                      e = launch_scan_u32(h->dpre.p, h->dpre.p, ns, h->scan_tmp.p, h->scan_tmp.cap,
                                           &h->ctr.p->depth_w, s);
-                  return e == hipSuccess ? launch_depth_table(h->dsub.p, h->ctr.p, nsub, pl.nbins, h->dtab.p, s) : e;
+                  return e == hipSuccess ? launch_depth_map(h->dsub.p, h->dpre.p, ns, pl.nbins, nsub, h->dmap.p,
+                                                            h->dheavy.p, h->ctr.p, s)
+                                         : e;
               }()));
+        h->depth_map_of = h->dmap.p;
     }
     // the digest, partitioned into the regions
     PartOut po{};
     po.recs = h->recR.p;
     po.dig = h->rdig.p;
     po.cur = h->rcur.p;
-    po.dm = DepthMap{h->dtab.p, sub, pl.b2};
+    po.dm = DepthMap{h->dmap.p, sub, pl.b2, pl.nbins - 1};
     po.cap = pl.cap;
     po.b1 = pl.b1;
     h->part_now = &po;
@@ -623,7 +638,8 @@ int warm_body(dbi_handle* h, uint64_t* n_in, bool* sparse) {
         if ((rc0 = tail_buffers(h, std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull),
                                 std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull), true)))
             return rc0;
-        if (um == h->umass.p && oo == h->occ_off.p) return warm_body_depth(h, dpl, n_in, sparse);
+        const int rd = warm_body_depth(h, dpl, um == h->umass.p && oo == h->occ_off.p, n_in, sparse);
+        if (rd != DEPTH_FALLBACK) return rd;
     }
     // small tails: the bounded digest counts the first radix pass's histogram
     // as it writes the records (one kernel and its launch gap fewer, human

@@ -169,6 +169,7 @@ struct Counters {
     unsigned long long tail_in, tail_n;
     unsigned long long depth_w;    // depth bins: the sampled occurrence weight (the map's total)
     unsigned int part_chunks;      // depth bins: pass-2 chunks over the digest's regions (k_part_plan)
+    unsigned int depth_h;          // depth bins: heavy sub-bins of this map (k_depth_mark)
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads
     // (sharing the ticket's line cost the digest 30%)
@@ -245,22 +246,28 @@ struct Hist1Plan {
     uint32_t G;  // radix blocks over cap slots
 };
 // ---- depth bins (warm lean builds) ----------------------
-// 2^(b1 + b2) mass bins of about equal record counts: a monotone table over
+// 2^(b1 + b2) mass bins of about equal record counts: a monotone map of
 // 2^DEPTH_SUB_BITS linear sub-bins of [minMH, maxMH], built from a sample of the
 // previous build's index (occurrence-weighted; a heuristic: a stale or poor
 // map costs speed, never correctness).  The digest partitions its records by
 // the bin's high b1 bits into (digit, XCD) regions; one radix pass over the
 // low b2 bits orders them by bin; the chunk sort bins each chunk locally.
+// The map is a bit per sub-bin (1: a bin starts there) plus the starts before
+// each 64-sub-bin word, 16 B per word {mask lo, mask hi, base, 0}: bin = base
+// + popcount of the word's bits up to the sub-bin -- one 16-B load per record
+// (1 MiB at 2^22 sub-bins: L2-resident, where a u16 table of 2^22 entries was
+// 8 MiB).
 #ifndef DBI_DEPTH_SUB_BITS
-#define DBI_DEPTH_SUB_BITS 20
+#define DBI_DEPTH_SUB_BITS 22
 #endif
 constexpr int DEPTH_SUB_BITS = DBI_DEPTH_SUB_BITS;
 constexpr uint32_t DEPTH_XCDS = 8;        // regions per high digit: one per XCD (block b on XCD b % 8)
 constexpr uint32_t PART_CHUNK = 4096;     // records per pass-2 block (RADIX_THREADS * RADIX_ITEMS)
 struct DepthMap {
-    const uint16_t* tab;  // sub-bin -> bin (non-decreasing)
-    BinMap sub;           // the linear sub-bins
-    uint32_t b2;          // low bits of a bin (the pass-2 digit); the high bits: the digest's partition
+    const uint4* map;      // per 64 sub-bins: bit s of (y:x) -- sub-bin s starts a bin (s > 0); z: the bin before them
+    BinMap sub;            // the linear sub-bins
+    uint32_t b2;           // low bits of a bin (the pass-2 digit); the high bits: the digest's partition
+    uint32_t last;         // the last bin (2^(b1 + b2) - 1)
 };
 struct PartOut {          // the digest's partition (k_digest_bounded PART)
     Rec* recs;            // region r = d1 * DEPTH_XCDS + xcd at [r * cap, r * cap + cur[r])
@@ -270,12 +277,14 @@ struct PartOut {          // the digest's partition (k_digest_bounded PART)
     uint32_t cap;         // records per region (a multiple of 64)
     uint32_t b1;
 };
-// the map: occurrence-weighted histogram of ns sampled uniques over the
-// sub-bins (zeroed d_sub), its scan (total -> ctr->depth_w), the table
+// the map: ns evenly spaced uniques of the previous index (mass order) -> their
+// sub-bins and occurrence weights; the weights' scan (total -> ctr->depth_w);
+// the bin starts (zeroed d_map, nsub / 64 entries), then the word bases;
+// *d_heavy carries the map's heavy sub-bin count to the next map
 hipError_t launch_depth_sample(const double* d_umass, const uint32_t* d_occ_off, uint64_t n_unique, uint32_t ns,
-                               const BinMap& sub, uint32_t* d_sub, hipStream_t s);
-hipError_t launch_depth_table(const uint32_t* d_sub_scan, const Counters* d_ctr, uint32_t nsub, uint32_t nbins,
-                              uint16_t* d_tab, hipStream_t s);
+                               const BinMap& sub, uint32_t* d_ss, uint32_t* d_sw, hipStream_t s);
+hipError_t launch_depth_map(const uint32_t* d_ss, const uint32_t* d_pre, uint32_t ns, uint32_t nbins, uint32_t nsub,
+                            uint4* d_map, uint32_t* d_heavy, Counters* d_ctr, hipStream_t s);
 hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                  const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr, hipStream_t s,

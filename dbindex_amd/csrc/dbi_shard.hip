@@ -711,6 +711,7 @@ int dbi_shard_splitters_cost(const double* samples, int nshards, int32_t factor,
 
 namespace {
 constexpr int CB = DBI_COST_BANDS;
+constexpr double SPLIT_HOLD = 1.10;  // owners this balanced (slowest / mean merge time) keep their split
 // the fixed key bands of the cost profile: CB equal key ranges of [minMH, maxMH]
 void cost_bands(const dbi_handle* h, int32_t* bsplit) {
     const double f = (double)h->params.mass_group_factor;
@@ -1080,6 +1081,7 @@ int dbi_shard_stats_get(dbi_handle* h, dbi_shard_stats* out) {
     st.merge_gpu_ms = sh.ms_merge_gpu;
     st.split_sampled = sh.split_sampled;
     st.split_rounds = sh.split_rounds;
+    st.split_held = sh.split_held ? 1 : 0;
     st.rank = sh.rank;
     st.nshards = sh.nshards;
     st.p_begin = sh.p_begin;
@@ -1635,7 +1637,8 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     // its status, so that every rank returns an error (never a hang)
     const double t_digest = now_ms();
     auto& wm = h->shard_warm;
-    const auto& pf = h->shard_prof;
+    auto& pf = h->shard_prof;
+    h->shard.split_held = false;
     // a warm build of the same shard with a reusable split digests
     // device-sized: no host round trip before the count matrix
     const bool dev_digest = wm.valid && wm.n == n && !h->opt_shard_resample &&
@@ -1696,8 +1699,13 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
         }
         sample_keys(packed.data(), n, h->params.mass_group_factor, wm.keys);
         // the profile only where every rank holds the same one (a
-        // reopened handle or another build history must not split differently)
-        const bool prof = same_profile && pf.valid;
+        // reopened handle or another build history must not split differently);
+        // ranks whose profiles differ all drop theirs, so the next cost update
+        // (the same gathered merge times on every rank) makes them equal again
+        // at once (one rank's fresh profile beside the others'
+        // averaged ones disagreed on every later build's split hash)
+        if (!same_profile) pf = {};
+        const bool prof = pf.valid;
         split_from_keys(wm.keys, n, prof ? CB : 0, prof ? pf.split : nullptr, prof ? pf.cost : nullptr, split);
         sampled = true;
         have_split = true;
@@ -1901,6 +1909,20 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     }
     if (wm.valid && wm.n == n && (rc = dbi_shard_cost_update(h, n, wm.prev_split, mms.data(), recs.data())))
         return rc;
+    // hysteresis: the previous build ran this build's split and
+    // its owners' merge times were within SPLIT_HOLD of their mean -- keep the
+    // split instead of chasing the profile (every re-split moves the spiky
+    // low-mass key bands between owners and the slowest owner with them)
+    bool hold = wm.valid && wm.n == n && std::equal(sh.split, sh.split + (n - 1), wm.prev_split);
+    if (hold) {
+        double mx = 0.0, sum = 0.0;
+        for (int i = 0; i < n; ++i) {
+            hold = hold && mms[i] > 0.0;
+            mx = std::max(mx, mms[i]);
+            sum += mms[i];
+        }
+        hold = hold && mx <= SPLIT_HOLD * sum / n;
+    }
     std::copy(sh.split, sh.split + (n - 1), wm.prev_split);
     wm.prev_merge_ms = sh.ms_merge_gpu;
     wm.prev_recv = sh.n_recv;
@@ -1911,11 +1933,15 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     if (stale) {
         wm.valid = false;
     } else {
-        split_from_keys(wm.keys, n, pf.valid ? CB : 0, pf.valid ? pf.split : nullptr, pf.valid ? pf.cost : nullptr,
-                        wm.split);
+        if (hold)
+            std::copy(sh.split, sh.split + (n - 1), wm.split);
+        else
+            split_from_keys(wm.keys, n, pf.valid ? CB : 0, pf.valid ? pf.split : nullptr, pf.valid ? pf.cost : nullptr,
+                            wm.split);
         wm.valid = true;
         wm.n = n;
     }
+    sh.split_held = hold && !stale;
     sh.global.g_total = tot[0];
     sh.global.g_dropped = tot[1];
     sh.global.g_kept = tot[2];

@@ -30,6 +30,8 @@ from . import _native
 from ._native import DbiShardStats, MAX_SHARDS, SHARD_SAMPLES, check
 from .engine import Engine
 
+SPLIT_HOLD = 1.10  # owners this balanced (slowest / mean merge time) keep their split (dbi_shard.hip)
+
 
 def _p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
@@ -185,7 +187,10 @@ def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off
         row = np.zeros(SHARD_SAMPLES + 1, np.float64)
         check(L.dbi_shard_samples(eng.h, _p(row)))
         samples[r] = row
-    if balance:
+    held = getattr(engines[0], "_split_held", None) if balance else None
+    if held is not None and held.shape[0] == n - 1:
+        split = held  # the last build's owners were balanced: keep its split (dbi_build_sharded's hysteresis)
+    elif balance:
         s = np.ascontiguousarray(samples, np.float64).reshape(n * (SHARD_SAMPLES + 1))
         out = np.zeros(max(n - 1, 1), np.int32)
         check(L.dbi_shard_splitters_profiled(engines[0].h, _p(s), n, _p(out)))
@@ -206,6 +211,8 @@ def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off
         recs = np.array([st.n_received for st in sts], np.uint64)
         sp = np.ascontiguousarray(np.concatenate([split, np.zeros(1, np.int32)]), np.int32)
         check(L.dbi_shard_cost_update(engines[0].h, n, _p(sp), _p(mms), _p(recs)))
+        balanced = n > 1 and mms.min() > 0 and mms.max() <= SPLIT_HOLD * mms.mean()
+        engines[0]._split_held = split.copy() if balanced else None
     return split
 
 

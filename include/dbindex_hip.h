@@ -335,6 +335,9 @@ typedef struct dbi_shard_stats {
                                      owner split, 0 = it reused the previous build's split  */
     int32_t split_rounds;         /* count-matrix rounds (2: a rank lacked or disagreed on the
                                      split, every rank sampled and partitioned again)       */
+    int32_t split_held;           /* 1 = the next build keeps this build's split: the owners'
+                                     merge times were balanced (max <= 1.1 x mean)          */
+    int32_t reserved0;
 } dbi_shard_stats;
 
 /* Digest proteins [p_begin, p_end) of the global arrays (device pointers:

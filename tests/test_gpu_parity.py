@@ -186,7 +186,7 @@ def test_digest_counted_histogram(Engine, h1):
             assert_queries_equal(eng, oix, m, t, f"digest histogram={h1} [{k}]")
             hists.append(sum(1 for n, _, _ in eng.stage_times() if n == "radix_hist"))
     passes = hists[0]  # the cold build: one histogram kernel per radix pass
-    assert hists[1] == (passes - 1 if h1 == "1" else passes), hists
+    assert hists[1] == (passes - 1 if h1 == 1 else passes), hists
 
 
 @pytest.mark.parametrize("copies", [3000, 9000])

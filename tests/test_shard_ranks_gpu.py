@@ -41,9 +41,14 @@ def _rank_main(world: int, rank: int, name: str, plan: dict, q) -> None:
         comm = shard.ShardComm.host(name, world, rank, 0, 16 << 20)
         b, e = shard.protein_ranges(pp.offsets, world)[rank]
         out = {"builds": []}
-        with Engine(cp, 0) as eng:
+        eng = Engine(cp, 0)
+        try:
             eng.set_timing(False)
             for k in range(plan["builds"]):
+                if plan.get("reopen", {}).get(k) == rank:  # a fresh handle: no split, no cost profile
+                    eng.close()
+                    eng = Engine(cp, 0)
+                    eng.set_timing(False)
                 kind = plan.get("mutate", {}).get(k)
                 if kind:  # new contents in the same device buffers (same pointers and sizes)
                     res2, off2 = _mutated(pp, kind)
@@ -73,6 +78,8 @@ def _rank_main(world: int, rank: int, name: str, plan: dict, q) -> None:
                 shard.replicate(eng, comm)
                 out["replica"] = eng.export()
                 out["replica_query"] = eng.query(m, t)
+        finally:
+            eng.close()
         comm.close()
         q.put((rank, out))
     except Exception:  # the parent reports it
@@ -176,6 +183,22 @@ def test_ranks_disagreeing_split_resamples(oracle):
         assert all(b["ok"] for b in builds), [b.get("error") for b in builds]
         _assert_whole_index([b["export"] for b in builds], oracle, f"skew build {k}")
         want = 2 if k in (0, 2) else 1
+        assert {b["rounds"] for b in builds} == {want}, (k, [b["rounds"] for b in builds])
+
+
+def test_ranks_reopened_handle_converges(oracle):
+    """Rank 1 reopens its handle before build 4: a fresh handle has no split
+    and no cost profile, so build 4 samples (two rounds) and the profile
+    fingerprints differ; every rank drops its profile then, so build 5 already
+    reuses one common split (the ranks used to keep disagreeing,
+    build after build, while the reopened rank's fresh profile differed from
+    its peers' averaged ones)."""
+    res = _run(3, {"builds": 7, "reopen": {4: 1}})
+    for k in range(7):
+        builds = [r["builds"][k] for r in res]
+        assert all(b["ok"] for b in builds), [b.get("error") for b in builds]
+        _assert_whole_index([b["export"] for b in builds], oracle, f"reopen build {k}")
+        want = 2 if k in (0, 4) else 1
         assert {b["rounds"] for b in builds} == {want}, (k, [b["rounds"] for b in builds])
 
 
