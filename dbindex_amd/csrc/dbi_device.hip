@@ -3442,20 +3442,28 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return v;
 }
 
-__device__ __forceinline__ void ck_cx(uint64_t& a, uint64_t& b) {  // a: the lower index
-    const bool gt = a > b;
-    const uint64_t lo = gt ? b : a, hi = gt ? a : b;
+// the network over keys of type T (the 64-bit compact key; 32-bit keys
+// compile to v_min / v_max_u32)
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor_k(uint64_t v) { return lane_xor64<M>(v); }
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor_k(uint32_t v) { return lane_xor<M>(v); }
+
+template <typename T>
+__device__ __forceinline__ void ck_cx(T& a, T& b) {  // a: the lower index
+    const T lo = a < b ? a : b, hi = a < b ? b : a;
     a = lo;
     b = hi;
 }
 
-__device__ __forceinline__ uint64_t ck_pick(uint64_t a, uint64_t b, bool lower) {
+template <typename T>
+__device__ __forceinline__ T ck_pick(T a, T b, bool lower) {
     return ((a > b) == lower) ? b : a;  // lower: min, else max
 }
 
 // flip step of the K-merge: partner i ^ (K-1)
-template <int R, int K>
-__device__ __forceinline__ void ck_flip(uint64_t (&key)[R]) {
+template <int R, int K, typename T>
+__device__ __forceinline__ void ck_flip(T (&key)[R]) {
     if constexpr (K <= R) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -3465,7 +3473,7 @@ __device__ __forceinline__ void ck_flip(uint64_t (&key)[R]) {
 #pragma unroll
         for (int r = 0; r < R / 2; ++r) {  // registers r and R-1-r trade with the partner lane
             const int q = r ^ (R - 1);
-            const uint64_t br = lane_xor64<K / R - 1>(key[q]), bq = lane_xor64<K / R - 1>(key[r]);
+            const T br = lane_xor_k<K / R - 1>(key[q]), bq = lane_xor_k<K / R - 1>(key[r]);
             key[r] = ck_pick(key[r], br, lower);
             key[q] = ck_pick(key[q], bq, lower);
         }
@@ -3473,8 +3481,8 @@ __device__ __forceinline__ void ck_flip(uint64_t (&key)[R]) {
 }
 
 // half-cleaner step: partner i ^ J
-template <int R, int J>
-__device__ __forceinline__ void ck_half(uint64_t (&key)[R]) {
+template <int R, int J, typename T>
+__device__ __forceinline__ void ck_half(T (&key)[R]) {
     if constexpr (J < R) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -3482,12 +3490,12 @@ __device__ __forceinline__ void ck_half(uint64_t (&key)[R]) {
     } else {
         const bool lower = (lane_id() & (uint32_t)(J / R)) == 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) key[r] = ck_pick(key[r], lane_xor64<J / R>(key[r]), lower);
+        for (int r = 0; r < R; ++r) key[r] = ck_pick(key[r], lane_xor_k<J / R>(key[r]), lower);
     }
 }
 
-template <int R, int J>
-__device__ __forceinline__ void ck_clean(uint64_t (&key)[R]) {
+template <int R, int J, typename T>
+__device__ __forceinline__ void ck_clean(T (&key)[R]) {
     if constexpr (J >= 1) {
         ck_half<R, J>(key);
         ck_clean<R, J / 2>(key);
@@ -3495,8 +3503,8 @@ __device__ __forceinline__ void ck_clean(uint64_t (&key)[R]) {
 }
 
 // sorts the wave's 64R keys ascending (K = 64R at the top)
-template <int R, int K>
-__device__ __forceinline__ void ck_sort_wave(uint64_t (&key)[R]) {
+template <int R, int K, typename T>
+__device__ __forceinline__ void ck_sort_wave(T (&key)[R]) {
     if constexpr (K > 2) ck_sort_wave<R, K / 2>(key);
     ck_flip<R, K>(key);
     ck_clean<R, K / 4>(key);
@@ -3838,6 +3846,7 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
 // WAVE_SORT_MAX, else by the whole block; the full-key bitonic only where the
 // compact key does not hold.  LDS: 8+8+4 B per record.
 constexpr uint32_t RANK_MAX_RUN = 64;
+
 #ifndef DBI_TAG_SORT
 #define DBI_TAG_SORT 1  // single-mass bins above WAVE_SORT_MAX by the tag counting sort (tag_sort_block)
 #endif
@@ -3979,9 +3988,20 @@ __device__ bool tag_sort_block(unsigned long long* k0, unsigned long long* k1, u
 // counters' scan gives every record its place and its bin's bounds at once
 // (in place of the fine bins' run detection); the wide bins are written to
 // `out` unsorted for chunk_sort_mid.
+#ifdef DBI_PHASE_CLOCK  // experiment builds: summed phase cycles of the main chunk sort (dbi_debug_phase_clock)
+__device__ unsigned long long g_phase[32];  // [0, 16): main chunk sort, [16, 32): the big tier
+#define PHASE_MARK(k) \
+    do { if (threadIdx.x == 0) tph[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define PHASE_MARK(k) do { } while (0)
+#endif
 template <int NT, int CAP, bool BLOCK, bool LOCAL = false>
 __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, uint32_t m, const BinMap& bm,
                            const RecLoc& rl, ChunkSmem<NT, CAP>& sm, uint32_t* heads_out, bool ties) {
+#ifdef DBI_PHASE_CLOCK
+    unsigned long long tph[8] = {};  // (mark 4: after the block-level sorts, BLOCK only)
+#endif
+    PHASE_MARK(0);
     static_assert(CAP <= 65535, "16-bit positions");
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t E = (CAP + NT - 1) / NT;  // records per thread (contiguous) in the run pass
@@ -4141,6 +4161,7 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
     }
     }  // !LOCAL
     __syncthreads();
+    PHASE_MARK(1);
     // small bins: rank inside the bin (k-major: a wave's lanes share bins), kept in registers with the key
     // (ranking by a 64-bit compact key instead measured slower: the extra
     // barriers and the order check cost more than the cheaper compares save)
@@ -4176,6 +4197,7 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
             }
         }
     }
+    PHASE_MARK(2);
     // big bins, in place (disjoint from the small bins)
     const uint32_t nbig = sm.nbig;
     for (uint32_t r = threadIdx.x >> 6; r < nbig; r += NW) {
@@ -4191,6 +4213,7 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         if (!done) wave_bitonic(k0, k1, lo, L);
     }
     __syncthreads();
+    PHASE_MARK(3);
     if constexpr (BLOCK) {
         constexpr int R = NT * 4 >= CAP ? 4 : 8;
         static_assert(NT * R >= CAP, "compact-sort capacity");
@@ -4206,8 +4229,20 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         }
         __syncthreads();
     }
+    PHASE_MARK(4);
     *heads_out = finish_sorted<NT>(out, m, rl, k0, k1, sm.aux, sm.u32, &sm.bad, sm.wr, BLOCK ? 0u : sm.nwide,
                                    LOCAL && !BLOCK);
+#ifdef DBI_PHASE_CLOCK
+    PHASE_MARK(5);
+    if (threadIdx.x == 0) {
+        unsigned long long* g = g_phase + (BLOCK ? 16 : 0);
+        for (int k = 0; k < 5; ++k) atomicAdd(&g[k], tph[k + 1] - tph[k]);
+        atomicAdd(&g[8], 1ull);
+        atomicAdd(&g[9], (unsigned long long)m);
+        atomicAdd(&g[10], (unsigned long long)sm.nbig);
+        atomicAdd(&g[11], (unsigned long long)sm.nwide);
+    }
+#endif
 }
 
 // One chunk of m <= CAP records sorted in LDS by the record key with the flip
@@ -4443,6 +4478,18 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
                    d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr);
     return hipGetLastError();
 }
+
+#ifdef DBI_PHASE_CLOCK
+}  // namespace dbi
+extern "C" int dbi_debug_phase_clock(unsigned long long* out, int reset) {
+    if (reset) {
+        unsigned long long z[32] = {};
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(dbi::g_phase), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dbi::g_phase), 32 * 8, 0, hipMemcpyDeviceToHost);
+}
+namespace dbi {
+#endif
 
 #ifdef DBI_CLOCK_CHUNKS
 }  // namespace dbi
