@@ -900,11 +900,40 @@ def run_trembl(args, world: int, rank: int, dev: int, coord, options=None) -> No
                          "note": "algorithmic HBM bytes per step are R + 8P (no records written): "
                                  f"{alg / 1e9:.1f} GB; the count walk is VALU-bound (~7.5e11 peptide "
                                  "steps per step), so the HBM fraction is tiny by construction"},
+            "issue_roofline": trembl_issue_roofline(len(chunks), ms),
             "cpu_baseline": cpu,
         }), flush=True)
     eng.close()
     if comm is not None:
         comm.close()
+
+
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 256 CUs x 4 SIMDs, one per 2 cycles at 2.4 GHz
+
+
+def trembl_issue_roofline(chunks_per_step: int, ms: float):
+    """configs[4] is VALU-bound, so its roofline is the VALU issue rate
+    (VERDICT r04): the bucket-count kernel's SQ_INSTS_VALU per launch from the
+    newest profiles/*_trembl_sq.json (tools/sq_kernel_totals.py over a
+    rocprofv3 --pmc pass of this bench, tools/gpu_round.sh pmc_sq_trembl) x the
+    launches of one step (one per chunk), over the step time, against the
+    chip's VALU issue peak (MI355X_MICROARCH.md: a SIMD issues a wave64 VALU
+    instruction every 2 cycles)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trembl_sq.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    k = next((v for n, v in d["kernels"].items() if "k_digest_count_cuts<true, true>" in n), None)
+    if not k or not k.get("launches"):
+        return None
+    per_launch = k["SQ_INSTS_VALU"] / k["launches"]
+    achieved = per_launch * chunks_per_step / (ms * 1e-3)
+    return {"bound": "valu", "kernel": "digest_count (bucket pass)", "achieved": achieved, "peak": VALU_ISSUE_PEAK,
+            "unit": "wave64 VALU instructions/s", "frac": achieved / VALU_ISSUE_PEAK,
+            "valu_per_step": per_launch * chunks_per_step, "source": os.path.relpath(files[-1], ROOT),
+            "salu_per_step": k.get("SQ_INSTS_SALU", 0.0) / k["launches"] * chunks_per_step,
+            "lds_per_step": k.get("SQ_INSTS_LDS", 0.0) / k["launches"] * chunks_per_step}
 
 
 if __name__ == "__main__":

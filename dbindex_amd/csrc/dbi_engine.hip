@@ -552,7 +552,7 @@ int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_
     const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
     const uint32_t nsub = 1u << DEPTH_SUB_BITS;
     const uint64_t nreg_slots = (uint64_t)pl.nreg * pl.cap;
-    const uint32_t T = chunk_target(h, cap);
+    const uint32_t T = h->chunk_t ? h->chunk_t : cap >= CHUNK_T_MIN_RECS ? (uint32_t)CHUNK_T_DEPTH : chunk_target(h, cap);
     const uint32_t nchunks = (uint32_t)std::max<uint64_t>((cap + T - 1) / T, 1);
     const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
     // every allocation before the first launch (a reallocation must never free

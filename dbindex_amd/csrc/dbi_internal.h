@@ -198,6 +198,7 @@ constexpr int CHUNK_CAP = 1984;     // records per chunk sorted in LDS (20 B eac
 constexpr int CHUNK_T = 1536;       // target chunk size (whole mass bins; DBI_CHUNK_T A/B, round 3: 1024-1792 measured, 1536 best since the chunk pairs)
 constexpr int CHUNK_T_SMALL = 1280;  // below CHUNK_T_MIN_RECS records (human scale: 0.059 vs 0.069 ms, more blocks to fill 256 CUs)
 constexpr uint64_t CHUNK_T_MIN_RECS = 8ull << 20;
+constexpr int CHUNK_T_DEPTH = 1792;  // depth-bin chunks from CHUNK_T_MIN_RECS records (SwissProt: 3.75-3.83 -> 3.73-3.76 ms, r05s / r05t)
 constexpr int BIN_AVG = 8;          // target records per fine mass bin (rank-sorted by one wave)
 #ifndef DBI_WAVE_SORT_LIMIT
 #define DBI_WAVE_SORT_LIMIT 512

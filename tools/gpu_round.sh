@@ -2,7 +2,7 @@
 # tools/gpu_round.sh TAG [what...] — one GPU-box session: parity tests, bench,
 # rocprofv3 kernel trace + stats, HBM counter passes.  Every GPU step has its
 # own time limit; the script stops at the first failure.
-#   what: tests smoke bench bench_h prof prof_semi pmc pmc_sq (default: tests bench prof)
+#   what: tests smoke bench bench_h prof prof_semi pmc pmc_sq pmc_sq_trembl (default: tests bench prof)
 set -u -o pipefail
 TAG=${1:-r}
 shift || true
@@ -46,6 +46,10 @@ for w in $WHAT; do
                 -- python3 bench.py --config semi --steps 2 --warmup 3 --queries 0 --no-cpu-baseline --no-cold
            step prof_semi2 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/semi/prof" -o run \
                 -- python3 bench.py --config semi --steps 2 --warmup 3 --queries 0 --no-cpu-baseline --no-cold ;;
+    pmc_sq_trembl) export TMPDIR=/tmp
+           step pmc_sq_trembl 900 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+                --output-format csv -d "$OUT/trembl_sq" -o run \
+                -- python3 bench.py --config trembl --steps 1 --warmup 0 --no-cpu-baseline ;;
     pmc_sq) export TMPDIR=/tmp
            step pmc_sq 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
                 --output-format csv -d "$OUT/pmc_sq" -o run \
