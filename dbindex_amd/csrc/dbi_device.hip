@@ -2933,7 +2933,8 @@ __global__ void k_depth_starts(const uint32_t* __restrict__ offs, const uint32_t
 // starting in [c*T, (c+1)*T), its last bin split off as chunk 2c+1 when the
 // two together exceed CHUNK_CAP (a bin above it is a big chunk of its own)
 __global__ void k_depth_chunks(const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t T, uint32_t nchunks,
-                               uint32_t* __restrict__ chunk_lo, const Counters* __restrict__ ctr) {
+                               uint32_t* __restrict__ chunk_lo, Counters* __restrict__ ctr,
+                               uint32_t* __restrict__ split_list) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c > nchunks) return;
     const uint32_t n = (uint32_t)ctr->tail_n;
@@ -2954,15 +2955,16 @@ __global__ void k_depth_chunks(const uint32_t* __restrict__ bstart, uint32_t nb,
     uint32_t split = s1;
     if (s1 - s0 > (uint32_t)CHUNK_CAP && j1 > 0 && bstart[j1 - 1] > s0) split = bstart[j1 - 1];
     chunk_lo[2 * c + 1] = split;
+    if (split != s1) split_list[atomicAdd(&ctr->n_split, 1u)] = c;  // (k_chunk_sort runs these first)
 }
 
 hipError_t launch_depth_bounds(const uint32_t* d_offs, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
                                uint32_t* d_bstart, uint32_t T, uint32_t nchunks, uint32_t* d_chunk_lo,
-                               const Counters* d_ctr, hipStream_t s) {
+                               Counters* d_ctr, hipStream_t s, uint32_t* d_split_list) {
     const uint32_t nb = 1u << (b1 + b2);
     DBI_LAUNCH(k_depth_starts, dim3((nb + 1 + 255) / 256), dim3(256), 0, s, d_offs, d_d1c, b1, b2, d_bstart, d_ctr);
     DBI_LAUNCH(k_depth_chunks, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_bstart, nb, T, nchunks, d_chunk_lo,
-               d_ctr);
+               d_ctr, d_split_list);
     return hipGetLastError();
 }
 
@@ -4307,25 +4309,31 @@ __device__ unsigned long long g_chunk_clock[1u << 18][2];
 
 // One block per chunk pair (k_chunk_bounds / launch_depth_bounds).  Radix
 // tail: chunk 2c here, chunk 2c+1 (one big bin) to the list kernels.  LOCAL
-// (depth bins): both chunks of the pair here, one after the other (2c+1 is
-// empty unless the pair was split).  Measured against one block per chunk:
-// block b sorting chunk b put every non-empty chunk on every other XCD
+// (depth bins): 2c+1 is empty unless the pair was split; the split ones
+// (listed by k_depth_chunks) take the grid's first nfront blocks, so the
+// launch starts with its heaviest work instead of ending with it -- when the
+// list fits nfront (the previous build's count + a margin); otherwise each
+// pair's block sorts its 2c+1 after 2c.  Measured against one block per
+// chunk: block b sorting chunk b put every non-empty chunk on every other XCD
 // (blocks go to the XCDs round-robin; half the chip idle, 1.76 vs 0.82 ms);
 // the even chunks in the grid's first half and the odd ones in its second
 // left the split chunks as the launch's tail (1.29-1.31 vs 1.21 ms).
-#ifndef DBI_LOCAL_PAIRS
-#define DBI_LOCAL_PAIRS 1
-#endif
 template <int NT, int CAP, bool LOCAL = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
              const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
              uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, uint32_t ties,
-             Counters* __restrict__ ctr) {
+             Counters* __restrict__ ctr, const uint32_t* __restrict__ split_list, uint32_t nfront) {
     __shared__ ChunkSmem<NT, CAP> sm;
-    const uint32_t half = gridDim.x >> 1;
-    const uint32_t c = !LOCAL || DBI_LOCAL_PAIRS ? 2 * blockIdx.x
-                       : blockIdx.x < half ? 2 * blockIdx.x : 2 * (blockIdx.x - half) + 1;
+    const bool front_ok = LOCAL && ctr->n_split <= nfront;  // block-uniform
+    if (LOCAL && blockIdx.x < nfront) {  // a split pair's second chunk, or nothing
+        if (!front_ok || blockIdx.x >= ctr->n_split) return;
+        const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
+        chunk_sort_one<NT, CAP, LOCAL>(2 * split_list[blockIdx.x] + 1, in, out, bm, chunk_lo, rl, ucount, big_list,
+                                       mid_list, ties, ctr, sm);
+        return;
+    }
+    const uint32_t c = 2 * (blockIdx.x - (LOCAL ? nfront : 0u));
 #ifdef DBI_CLOCK_CHUNKS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -4342,9 +4350,12 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
     }
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
     chunk_sort_one<NT, CAP, LOCAL>(c, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr, sm);
-    if constexpr (LOCAL && DBI_LOCAL_PAIRS) {
-        __syncthreads();  // the LDS is the next chunk's
-        chunk_sort_one<NT, CAP, LOCAL>(c + 1, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr, sm);
+    if constexpr (LOCAL) {
+        if (!front_ok || chunk_lo[c + 2] == chunk_lo[c + 1]) {  // (empty: its unique count 0)
+            __syncthreads();  // the LDS is the next chunk's
+            chunk_sort_one<NT, CAP, LOCAL>(c + 1, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr,
+                                           sm);
+        }
     }
 #ifdef DBI_CLOCK_CHUNKS
     __syncthreads();
@@ -4467,15 +4478,17 @@ k_bin_sort_mid(const Rec* in, Rec* out, const uint32_t* __restrict__ chunk_lo,  
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                              uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s,
-                             bool local) {
+                             bool local, const uint32_t* d_split_list, uint32_t nfront) {
     if (nchunks == 0) return hipSuccess;
+    if (local && nfront && !d_split_list) return hipErrorInvalidValue;
     if (local)
-        DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP, true>), dim3(DBI_LOCAL_PAIRS ? nchunks : 2 * nchunks),
-                   dim3(CHUNK_THREADS), 0, s, d_in,
-                   d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr);
+        DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP, true>), dim3(nfront + nchunks), dim3(CHUNK_THREADS), 0, s,
+                   d_in, d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr,
+                   d_split_list, nfront);
     else
         DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
-                   d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr);
+                   d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr,
+                   (const uint32_t*)nullptr, 0u);
     return hipGetLastError();
 }
 

@@ -175,6 +175,7 @@ struct dbi_handle {
     bool inputs_ptm = false;            // ... and they carry inline '[formula]' PTMs (no dbi_rebuild)
     bool hc_final = false;              // hc holds the counters after the build's last kernel
     uint64_t last_kept = 0;             // the previous build's records (bins of a device-sized tail)
+    uint32_t grid_split = 0;              // depth bins: k_chunk_sort's front blocks for split pairs (previous build's count + a margin)
     uint32_t grid_mid = 0, grid_big = 0;  // list-kernel grids of a device-sized tail, from the previous build (0: one block per possible entry; GRID_NONE: that list was empty, the kernel is not launched)
     bool skip_mid = false, skip_big = false;  // the last tail did not launch that list kernel (GRID_NONE)
     // records of this build may repeat exactly (the addSequence flow: the same occurrence added
@@ -269,7 +270,7 @@ struct dbi_handle {
         uint64_t prev_unique = 0;         // depth bins: the sampled index
         uint32_t depth_cap = 0;           // depth bins: region capacity (0: the radix tail)
         bool tail_local = false;          // the previous build's tail (its list grids)
-        uint32_t grid_mid = 0, grid_big = 0;
+        uint32_t grid_mid = 0, grid_big = 0, grid_split = 0;
         bool giants = true;
         bool timing = false;
         char timing_only[32] = {};
@@ -278,7 +279,8 @@ struct dbi_handle {
             return d_res == o.d_res && d_poff == o.d_poff && n_res == o.n_res && n_prot == o.n_prot &&
                    cap == o.cap && last_kept == o.last_kept && alloc_gen == o.alloc_gen && dp_gen == o.dp_gen &&
                    prev_unique == o.prev_unique && depth_cap == o.depth_cap && tail_local == o.tail_local &&
-                   grid_mid == o.grid_mid && grid_big == o.grid_big && giants == o.giants && timing == o.timing &&
+                   grid_mid == o.grid_mid && grid_big == o.grid_big && grid_split == o.grid_split &&
+                   giants == o.giants && timing == o.timing &&
                    std::strncmp(timing_only, o.timing_only, sizeof(timing_only)) == 0;
         }
     };
@@ -306,6 +308,7 @@ struct dbi_handle {
     DevBuf<Rec> recR;                     // the digest's regions
     DevBuf<uint8_t> rdig;                 //   each record's low bin digit
     DevBuf<uint32_t> rcur, dsub, dpre, desc, d1c, hist2, bstart;  // dsub / dpre: the map's samples
+    DevBuf<uint32_t> split_list;          // depth bins: the split chunk pairs
     DevBuf<uint4> dmap;                   // the depth map (DepthMap)
     DevBuf<uint32_t> dheavy;              // its heavy sub-bins (the next map's room for them)
     const dbi::PartOut* part_now = nullptr;  // run_digest: partition the warm digest's records (warm_body_depth)

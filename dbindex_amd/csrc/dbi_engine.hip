@@ -241,9 +241,13 @@ int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nc
     hipStream_t s = h->stream;
     const uint32_t n32 = (uint32_t)n;
     const size_t seg_cap = giant_seg_cap(n);
+    // depth bins: the split pairs' second chunks in front blocks (the previous
+    // depth build's count + a margin; more, and the pairs' own blocks sort them)
+    const uint32_t nfront = local && (est || d_n) && h->tail_local ? std::min(h->grid_split, nchunks) : 0u;
     STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
           launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                            h->mid_list.p, h->exact_dups, h->ctr.p, s, local));
+                            h->mid_list.p, h->exact_dups, h->ctr.p, s, local, local ? h->split_list.p : nullptr,
+                            nfront));
     // one block per listed bin (mid: every bin above the wave sort's reach) or
     // chunk (big: above CHUNK_CAP); the lists are filled on the device.  A device-sized tail
     // launches the previous build's list lengths plus a margin instead (a grid
@@ -350,6 +354,7 @@ int finish_build(dbi_handle* h) {
     h->lists_short = chunk_lists_short(h);
     h->grid_mid = h->hc.n_mid ? h->hc.n_mid + h->hc.n_mid / 8 + 32 : GRID_NONE;
     h->grid_big = h->hc.n_big ? h->hc.n_big + h->hc.n_big / 8 + 16 : GRID_NONE;
+    h->grid_split = h->cur_local ? h->hc.n_split + h->hc.n_split / 8 + 32 : 0u;
     h->giants_seen = h->hc.n_giant > 0;
     h->tail_local = h->cur_local;
     h->force_cold = false;
@@ -518,6 +523,7 @@ dbi_handle::GraphKey graph_key(const dbi_handle* h) {
     k.last_kept = h->last_kept;
     k.grid_mid = h->grid_mid;
     k.grid_big = h->grid_big;
+    k.grid_split = h->grid_split;
     k.prev_unique = h->prev_unique;
     k.tail_local = h->tail_local;
     const DepthPlan dpl = depth_plan(h);
@@ -563,6 +569,7 @@ int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_
         (rc = h->dsub.ensure(DEPTH_SAMPLES)) || (rc = h->dpre.ensure(DEPTH_SAMPLES)) || (rc = h->dmap.ensure(nsub / 64)) ||
         (rc = h->dheavy.ensure_zeroed(1, s)) || (rc = h->desc.ensure(pl.max_chunks)) || (rc = h->d1c.ensure(512)) ||
         (rc = h->hist2.ensure((size_t)pl.max_chunks << pl.b2)) || (rc = h->bstart.ensure(pl.nbins + 1)) ||
+        (rc = h->split_list.ensure(nchunks)) ||
         (rc = h->blk.ensure(std::max<uint32_t>(ntiles, 1))) ||
         (rc = h->thr.ensure((size_t)ntiles * DIGEST_THREADS + 1)) || (rc = h->tile_pf.ensure(2 * ((size_t)ntiles + 2))) ||
         (rc = h->scan_tmp.ensure(std::max({scan_u32_tmp_elems(DEPTH_SAMPLES), scan_u32_tmp_elems((uint64_t)pl.max_chunks << pl.b2),
@@ -620,7 +627,8 @@ int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_
           launch_part_scatter(h->recR.p, h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2,
                               pl.max_chunks, h->hist2.p, h->recA.p, h->ctr.p, s));
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
-          launch_depth_bounds(h->hist2.p, h->d1c.p, pl.b1, pl.b2, h->bstart.p, T, nchunks, h->chunk_lo.p, h->ctr.p, s));
+          launch_depth_bounds(h->hist2.p, h->d1c.p, pl.b1, pl.b2, h->bstart.p, T, nchunks, h->chunk_lo.p, h->ctr.p, s,
+                              h->split_list.p));
     if ((rc = sort_chunks(h, h->recA.p, h->recB.p, sub, nchunks, cap, &h->ctr.p->tail_n, true, true))) return rc;
     h->stats.n_bins = pl.nbins;
     return 0;
@@ -773,7 +781,7 @@ int build_digest(dbi_handle* h) {
         // stage table restarts)
         drop_graph(h);
         h->prev_key_valid = false;
-        h->grid_mid = h->grid_big = 0;
+        h->grid_mid = h->grid_big = h->grid_split = 0;
         h->giants_seen = true;
         if (need > n_in && (rc = h->recA.ensure(need + need / 8))) return rc;
         DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), h->stream));
@@ -1196,6 +1204,9 @@ void dbi_close(dbi_handle* h) {
     h->h_row.release(); h->h_orow.release(); h->h_sums.release(); h->kr_scratch.release();
     h->r_mass.release(); h->r_pid.release(); h->r_off.release(); h->r_len.release(); h->r_occ_off.release();
     h->r_occ.release();
+    h->recR.release(); h->rdig.release(); h->rcur.release(); h->dsub.release(); h->dpre.release(); h->dmap.release();
+    h->dheavy.release(); h->desc.release(); h->d1c.release(); h->hist2.release(); h->bstart.release();
+    h->split_list.release();
     drop_graph(h);
     for (auto& ev : h->evpool)
         if (ev) (void)hipEventDestroy(ev);
@@ -1649,7 +1660,7 @@ int dbi_set_cold(dbi_handle* h) {
     drop_graph(h);
     h->force_cold = true;
     h->prev_key_valid = false;
-    h->grid_mid = h->grid_big = 0;
+    h->grid_mid = h->grid_big = h->grid_split = 0;
     h->giants_seen = true;
     return 0;
 }

@@ -170,6 +170,7 @@ struct Counters {
     unsigned long long depth_w;    // depth bins: the sampled occurrence weight (the map's total)
     unsigned int part_chunks;      // depth bins: pass-2 chunks over the digest's regions (k_part_plan)
     unsigned int depth_h;          // depth bins: heavy sub-bins of this map (k_depth_mark)
+    unsigned int n_split;          // depth bins: chunk pairs split in two (k_depth_chunks' split_list)
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads
     // (sharing the ticket's line cost the digest 30%)
@@ -307,9 +308,10 @@ hipError_t launch_part_scatter(const Rec* d_recs, const uint8_t* d_dig, const ui
 // chunk pairs over the bin-ordered records from the pass-2 offsets: bin
 // starts (bstart: nbins + 1), then chunk_lo[2c] = first bin start at or after
 // c*T, chunk_lo[2c+1] = the last bin's start when the chunk exceeds CHUNK_CAP
+// (those pairs c listed in d_split_list[0, ctr->n_split))
 hipError_t launch_depth_bounds(const uint32_t* d_offs, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
                                uint32_t* d_bstart, uint32_t T, uint32_t nchunks, uint32_t* d_chunk_lo,
-                               const Counters* d_ctr, hipStream_t s);
+                               Counters* d_ctr, hipStream_t s, uint32_t* d_split_list);
 // semi-specific enzymes (no mandatory residues, no windows): one walk per start
 // into slots bounded by the bit maps (REC_SENTINEL in the unused ones)
 hipError_t launch_digest_semi_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
@@ -437,7 +439,7 @@ hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, 
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                              uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s,
-                             bool local = false);
+                             bool local = false, const uint32_t* d_split_list = nullptr, uint32_t nfront = 0);
 hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_mid_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s);
