@@ -269,6 +269,7 @@ struct dbi_handle {
         uint64_t n_res = 0, n_prot = 0, cap = 0, last_kept = 0, alloc_gen = 0, dp_gen = 0;
         uint64_t prev_unique = 0;         // depth bins: the sampled index
         uint32_t depth_cap = 0;           // depth bins: region capacity (0: the radix tail)
+        bool depth_fresh = false;         // depth bins: the map is sampled in this build
         bool tail_local = false;          // the previous build's tail (its list grids)
         uint32_t grid_mid = 0, grid_big = 0, grid_split = 0;
         bool giants = true;
@@ -278,7 +279,8 @@ struct dbi_handle {
         bool operator==(const GraphKey& o) const {
             return d_res == o.d_res && d_poff == o.d_poff && n_res == o.n_res && n_prot == o.n_prot &&
                    cap == o.cap && last_kept == o.last_kept && alloc_gen == o.alloc_gen && dp_gen == o.dp_gen &&
-                   prev_unique == o.prev_unique && depth_cap == o.depth_cap && tail_local == o.tail_local &&
+                   prev_unique == o.prev_unique && depth_cap == o.depth_cap && depth_fresh == o.depth_fresh &&
+                   tail_local == o.tail_local &&
                    grid_mid == o.grid_mid && grid_big == o.grid_big && grid_split == o.grid_split &&
                    giants == o.giants && timing == o.timing &&
                    std::strncmp(timing_only, o.timing_only, sizeof(timing_only)) == 0;
@@ -295,6 +297,9 @@ struct dbi_handle {
     bool depth_off = false;               // this build's retry takes the radix tail (a region overflowed)
     bool depth_keep_map = false;          // this build's retry keeps the depth map it computed
     const uint4* depth_map_of = nullptr;  // the map buffer a complete map was last enqueued into
+    uint64_t depth_map_unique = 0;        // ... sampled from an index of this many unique peptides
+    uint32_t depth_map_nbins = 0;         // ... for this many bins
+    bool opt_depth_map_reuse = true;      // option depth_map_reuse: keep the map while the index's size holds
     bool cur_local = false, tail_local = false;  // this / the last finished build's chunk sort took depth-bin chunks
     bool force_cold = false;              // dbi_set_cold: the next build takes the cold path (buffers kept)
     // dbi_set_option: sharded-build switches and test hooks

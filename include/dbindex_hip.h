@@ -262,7 +262,9 @@ int dbi_device_view(dbi_handle* h, dbi_device_index* out);
  * environment.  Integer options: "build_graph", "digest_hist",
  * "semi_bounded", "depth_bins" (0 / 1: the warm build's hipGraph, the
  * digest-counted first radix histogram of small tails, the bounded
- * semi-specific digest, depth bins); "big_split" (-1: by the list length, 0,
+ * semi-specific digest, depth bins); "depth_map_reuse" (1: the depth-bin map
+ * is sampled again only when the resident index changes size, 0: every
+ * build); "big_split" (-1: by the list length, 0,
  * 1: the big chunk tier's two size classes); "bin_bits_max", "split_above",
  * "chunk_target" (0: by size); "shard_full_path", "shard_dev_digest",
  * "shard_resample" (0 / 1, dbi_build_sharded); "test_split_skew" (a rank, -1

@@ -34,23 +34,27 @@ def _stages(eng):
     return {name for name, _, _ in eng.stage_times()}
 
 
-@pytest.mark.parametrize("depth", [1, 0])
-def test_depth_warm_builds_match_oracle(Engine, depth):
+@pytest.mark.parametrize("depth,reuse", [(1, 1), (1, 0), (0, 1)])
+def test_depth_warm_builds_match_oracle(Engine, depth, reuse):
     """Human scale (configs[1], 1.9M records): cold, then warm builds -- every
     stage timed (no graph), then untimed (captured, replayed) -- each equal to
-    the oracle; with option depth_bins=0 the radix tail runs instead."""
+    the oracle; with option depth_bins=0 the radix tail runs instead.  The map
+    is sampled again only when the index changes size (option
+    depth_map_reuse=0: every build)."""
     pp = fasta.config("human")
     cp = DBIndexSearchParams.trypsin(2).to_c()
     oix = cref.Index(cp, pp.residues, pp.offsets)
-    with Engine(cp, options={"depth_bins": depth}) as eng:
+    with Engine(cp, options={"depth_bins": depth, "depth_map_reuse": reuse}) as eng:
         eng.build(pp)
         assert "bin_scatter" not in _stages(eng)  # cold: count + emit, the radix tail
         assert_index_equal(eng, oix, "cold")
-        for k in range(2):
+        for k in range(3):
             eng.build(pp)
             names = _stages(eng)
             assert ("bin_scatter" in names) == (depth == 1), names
             assert ("radix_scatter" in names) == (depth == 0), names
+            if depth and k == 2:  # (k = 0 is a redo, whose stage table starts after the map)
+                assert ("depth_map" in names) == (reuse == 0), names
             assert_index_equal(eng, oix, f"warm timed {k}")
         eng.set_timing(False)
         for k in range(4):
