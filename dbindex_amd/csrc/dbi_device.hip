@@ -74,10 +74,38 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
     return v;
 }
 
+// 32-bit sums by DPP (VALU lane moves, no ds_bpermute round trips): shifts of
+// 1, 2, 4, 8 inside each 16-lane row, then row 0's / rows 0-1's last lane
+// broadcast into the rows above (row_bcast:15 / :31)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_or_zero(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+template <>
+__device__ __forceinline__ uint32_t wave_incl_scan<uint32_t>(uint32_t v) {
+    v += dpp_or_zero<0x111, 0xF>(v);  // row_shr:1
+    v += dpp_or_zero<0x112, 0xF>(v);  // row_shr:2
+    v += dpp_or_zero<0x114, 0xF>(v);  // row_shr:4
+    v += dpp_or_zero<0x118, 0xF>(v);  // row_shr:8
+    v += dpp_or_zero<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+    v += dpp_or_zero<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+template <>
+__device__ __forceinline__ uint32_t wave_sum<uint32_t>(uint32_t v) {
+    v += lane_xor<1>(v);
+    v += lane_xor<2>(v);
+    v += lane_xor<4>(v);
+    v += lane_xor<8>(v);
+    v += lane_xor<16>(v);
+    v += lane_xor<32>(v);
     return v;
 }
 
@@ -3426,23 +3454,20 @@ __device__ __forceinline__ uint64_t ck_q0(uint64_t key, uint64_t mb0) {
 
 __device__ __forceinline__ uint32_t ck_idx(uint64_t key) { return (uint32_t)key & ((1u << CK_IDX_BITS) - 1u); }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t o = __shfl_xor(v, d, 64);
-        v = o < v ? o : v;
-    }
+// (DPP / row-swap exchanges, dbi_lane.h: no ds_bpermute round trips)
+template <bool MAX>
+__device__ __forceinline__ uint64_t wave_minmax_u64(uint64_t v) {
+    uint64_t o;
+    o = lane_xor64<1>(v); v = (o > v) == MAX ? o : v;
+    o = lane_xor64<2>(v); v = (o > v) == MAX ? o : v;
+    o = lane_xor64<4>(v); v = (o > v) == MAX ? o : v;
+    o = lane_xor64<8>(v); v = (o > v) == MAX ? o : v;
+    o = lane_xor64<16>(v); v = (o > v) == MAX ? o : v;
+    o = lane_xor64<32>(v); v = (o > v) == MAX ? o : v;
     return v;
 }
-
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t o = __shfl_xor(v, d, 64);
-        v = o > v ? o : v;
-    }
-    return v;
-}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) { return wave_minmax_u64<false>(v); }
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) { return wave_minmax_u64<true>(v); }
 
 // the network over keys of type T (the 64-bit compact key; 32-bit keys
 // compile to v_min / v_max_u32)
