@@ -2003,7 +2003,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
                 if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
             }
         }
-        flush = __shfl(last, 0, 64) != 0;
+        flush = __builtin_amdgcn_readlane((int)last, 0) != 0;
     }
     if (H1 && flush) {
         __threadfence_block();
@@ -3724,16 +3724,16 @@ __device__ bool ck_run_block(unsigned long long* k0, unsigned long long* k1, uin
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_max(uint32_t v, uint32_t* s_tmp) {
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d, 64);
-        if ((int)lane >= d) inc = max(inc, o);
-    }
+    uint32_t inc = v;  // inclusive max-scan by DPP (0 is the identity), as wave_incl_scan
+    inc = max(inc, dpp_or_zero<0x111, 0xF>(inc));
+    inc = max(inc, dpp_or_zero<0x112, 0xF>(inc));
+    inc = max(inc, dpp_or_zero<0x114, 0xF>(inc));
+    inc = max(inc, dpp_or_zero<0x118, 0xF>(inc));
+    inc = max(inc, dpp_or_zero<0x142, 0xA>(inc));
+    inc = max(inc, dpp_or_zero<0x143, 0xC>(inc));
     if (lane == 63) s_tmp[w] = inc;
     __syncthreads();
-    uint32_t r = __shfl_up(inc, 1, 64);
-    if (lane == 0) r = 0;
+    uint32_t r = dpp_or_zero<0x138, 0xF>(inc);  // wave_shr:1 (lane 0: 0)
     for (uint32_t q = 0; q < w; ++q) r = max(r, s_tmp[q]);
     __syncthreads();
     return r;
@@ -3800,7 +3800,7 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
         const uint64_t bal = __ballot(dup);
         uint32_t base = 0;
         if (bal && lane_id() == 0) base = atomicAdd(&s_u32[NT / 64], (uint32_t)__popcll(bal));
-        base = __shfl(base, 0, 64);
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, 0);
         if (dup) a16[2 * (base + (uint32_t)__popcll(bal & lanemask_lt())) + 1] = (uint16_t)p;
         if (p < m) {
             a16[2 * p] = (uint16_t)(dup ? 0u : p);
