@@ -106,3 +106,34 @@ def test_depth_equal_mass_spikes(Engine):
         for k in range(5):
             eng.build(c)
             assert_index_equal(eng, oc, f"spiked build {k}")
+
+
+def test_options_and_cold_builds(Engine):
+    """dbi_set_option refuses an unknown name or a value out of range
+    (DBI_E_INVALID, the handle stays usable); dbi_set_cold makes the next build
+    a cold one (count + emit digest, the radix tail), after which warm builds
+    take depth bins again -- every build equal to the oracle."""
+    from dbindex_amd._native import DBIndexStoreException
+    pp = fasta.config("human").slice(0, 8000)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    with Engine(cp) as eng:
+        with pytest.raises(DBIndexStoreException, match="INVALID"):
+            eng.set_option("no_such_option", 1)
+        with pytest.raises(DBIndexStoreException, match="INVALID"):
+            eng.set_option("chunk_target", 1 << 20)
+        with pytest.raises(DBIndexStoreException, match="INVALID"):
+            eng.set_option("test_fail", 3)  # a string option given a number
+        for k in range(3):
+            eng.build(pp)
+            assert_index_equal(eng, oix, f"before cold {k}")
+        assert "bin_scatter" in _stages(eng)
+        eng.set_cold()
+        eng.build(pp)
+        names = _stages(eng)
+        assert "digest_count" in names and "digest_emit" in names and "bin_scatter" not in names, names
+        assert_index_equal(eng, oix, "cold again")
+        for k in range(3):
+            eng.build(pp)
+            assert_index_equal(eng, oix, f"after cold {k}")
+        assert "bin_scatter" in _stages(eng)
