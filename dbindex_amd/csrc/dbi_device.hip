@@ -828,15 +828,22 @@ __device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi) {
 }
 
 // Bucket counts of one thread's starts (ascending) when NUM_BUCKETS <= 8: the
-// per-thread counts in registers, and for every bucket boundary the first
-// window position whose prefix passes it for the current start (p[q] > p[s-1]
-// + T_k).  That position only moves forward from one start to the next (the
-// threshold grows with the start's prefix), so it is tracked, not searched:
-// about one LDS read per boundary and start.
+// per-thread counts in registers, and for every bucket boundary a merge
+// pointer -- the first window position whose prefix passes it for the current
+// start (p[q] > p[s-1] + T_k), over the whole window, not only the start's
+// ends.  That position only moves forward from one start to the next (the
+// threshold grows with the start's prefix), about one residue per start, so
+// it is advanced (hist_advance) at every start, ends or not, with the prefixes
+// at it and before it kept in registers.  Boundaries that no
+// kept end can pass (above maxMH) or that every kept end passes (below minMH)
+// are settled for the whole kernel: [k0, k1) is wave-uniform.
 constexpr int HIST_FAST_MAX = 8;
 struct HistTrack {
-    uint32_t t[HIST_FAST_MAX];  // the boundary's position (0: not yet found)
+    uint32_t q[HIST_FAST_MAX];   // the boundary's pointer (0: not yet placed; T_k > any residue: never 0 once placed)
+    uint32_t v[HIST_FAST_MAX];   // p[q]
+    uint32_t pv[HIST_FAST_MAX];  // p[q - 1]
     uint32_t c[HIST_FAST_MAX + 1];  // c[k]: ends at or past boundary k (k < 8); c[8]: ends
+    uint32_t k0, k1;  // boundaries below k0: every kept end past them; from k1 on: none
 };
 
 // first q in [t, hi + 1] with p[q] > a (p non-decreasing): gallop, then bisect
@@ -853,6 +860,65 @@ __device__ __forceinline__ uint32_t prefix_seek(const CutSmem& cs, uint32_t t, u
         if ((int64_t)cs.p(mid) > a) up = mid; else lo = mid;
     }
     return up;
+}
+
+// Every start, in order: each tracked boundary's pointer -- the first window
+// position q with p[q] > p[s-1] + T_k -- moved to this start's threshold.
+// The threshold grows by one residue's mass per start, so the pointer moves a
+// step or two: the next three prefixes of every pointer are read in one LDS
+// round trip and the pointer advanced branch-free (more than three steps
+// need three residues lighter than the one the threshold grew by, or a start
+// skipped: a gallop then).  The prefixes at the pointer and before it stay
+// in registers.  The slack words past the window read as above every
+// threshold, so no pointer passes p[nbytes].
+__device__ __forceinline__ void hist_advance(const CutLimits& cl, const CutSmem& cs, uint32_t nbytes, uint32_t upb,
+                                             uint32_t ps, HistTrack& ht) {
+    uint32_t w1[HIST_FAST_MAX], w2[HIST_FAST_MAX], w3[HIST_FAST_MAX];
+#pragma unroll
+    for (int k = 0; k < HIST_FAST_MAX; ++k) {
+        if ((uint32_t)k >= ht.k0 && (uint32_t)k < ht.k1 && (ht.q[k] == 0u || ht.q[k] < ps)) {  // first start
+            const uint32_t q = prefix_seek(cs, ps, nbytes - 1u, (int64_t)(upb + (uint32_t)cl.t_b[k]));
+            ht.q[k] = q;
+            ht.v[k] = cs.p(q);
+            ht.pv[k] = q > 0u ? cs.p(q - 1u) : 0u;  // (q >= ps; p[q - 1] <= the threshold)
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < HIST_FAST_MAX; ++k) {
+        if ((uint32_t)k >= ht.k0 && (uint32_t)k < ht.k1) {
+            const uint32_t q = min(ht.q[k], nbytes);
+            w1[k] = cs.p(q + 1u);
+            w2[k] = cs.p(q + 2u);
+            w3[k] = cs.p(q + 3u);
+        }
+    }
+    bool more = false;
+#pragma unroll
+    for (int k = 0; k < HIST_FAST_MAX; ++k) {
+        if ((uint32_t)k >= ht.k0 && (uint32_t)k < ht.k1) {
+            const uint32_t athr = upb + (uint32_t)cl.t_b[k];
+            const uint32_t q = ht.q[k], v = ht.v[k], pv = ht.pv[k];
+            const bool a0 = v <= athr, a1 = a0 && w1[k] <= athr, a2 = a1 && w2[k] <= athr;
+            more |= a2 && w3[k] <= athr;
+            ht.q[k] = q + (uint32_t)a0 + (uint32_t)a1 + (uint32_t)a2;
+            ht.pv[k] = a2 ? w2[k] : a1 ? w1[k] : a0 ? v : pv;
+            ht.v[k] = a2 ? w3[k] : a1 ? w2[k] : a0 ? w1[k] : v;
+        }
+    }
+    if (more) {
+#pragma unroll
+        for (int k = 0; k < HIST_FAST_MAX; ++k) {
+            if ((uint32_t)k >= ht.k0 && (uint32_t)k < ht.k1) {
+                const uint32_t athr = upb + (uint32_t)cl.t_b[k];
+                if (ht.v[k] <= athr) {
+                    const uint32_t q = prefix_seek(cs, ht.q[k], nbytes - 1u, (int64_t)athr);
+                    ht.q[k] = q;
+                    ht.v[k] = cs.p(q);
+                    ht.pv[k] = cs.p(q - 1u);
+                }
+            }
+        }
+    }
 }
 
 // first e in [a, b] with D(e) > t (D non-decreasing; b + 1 when none)
@@ -880,6 +946,8 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
     CutCount r{0u, 0u, true};
     if (!(dp.m0 <= dp.max_mh)) return r;  // while condition before the first residue (:284)
     if (ps + 2 > nbytes) { r.exact = false; return r; }
+    const int64_t pb = ps > 0 ? (int64_t)cs.p(ps - 1) : 0;
+    if constexpr (HIST && FAST) hist_advance(cl, cs, nbytes, (uint32_t)pb, ps, ht);  // every start: pointers in step
     // horizon: relative positions 0..h (the window's last position, whose cut is unknown, excluded)
     const uint32_t h = min(63u, nbytes - 2 - ps);
     const uint64_t hmask = bit_range(0, h);
@@ -894,7 +962,6 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
         H = xk - 1;
         ends = true;
     }
-    const int64_t pb = ps > 0 ? (int64_t)cs.p(ps - 1) : 0;
     auto D = [&](uint32_t e) -> int64_t { return (int64_t)cs.p(ps + e) - pb; };
     // last position with m <= maxMH (the walk stops past it: :284, :326)
     int Y;
@@ -946,72 +1013,35 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
     if constexpr (HIST && FAST) {
       if (n) {
         // absolute window positions of the first / last end; end q is past
-        // boundary k when p[q] > pb + T_k (the first such q tracked per k).
-        // u32 arithmetic (fast: 3 <= T_k < 2^31; a window's prefix + T_k < 2^32).
-        // The tracked position moves ~one residue per start, so every
-        // boundary's next prefixes are loaded together (p[q-1 .. q+2]: one LDS
-        // round trip for all boundaries) and a search runs only when it moved
-        // further.  ht.c[k] (k < 8) sums G_k, the ends at or past boundary k;
-        // ht.c[8] sums n (the bucket counts are their differences, at the flush).
+        // boundary k when p[q] > pb + T_k, and the pointer (hist_advance) is
+        // the first such position: the ends from it on are past (u32
+        // arithmetic; fast: 3 <= T_k < 2^31, a window's prefix + T_k < 2^32).
+        // ht.c[k] (k < 8) sums G_k, the ends at or past boundary k; ht.c[8]
+        // sums n (the bucket counts are their differences, at the flush).  An
+        // end within CUT_EPS of a boundary: the start is recounted by the
+        // exact walk (its counts here are never added).  Past qhi + 1 the
+        // prefix before the pointer is still the nearest one below the
+        // boundary (>= p[qhi]); before qlo the first end is past p[q].
         const uint32_t qlo = ps + (uint32_t)lo, qhi = ps + (uint32_t)Y;
         const uint32_t upb = (uint32_t)pb;
-        const uint32_t dlo = (uint32_t)D((uint32_t)lo), dhi = (uint32_t)D((uint32_t)Y);
-        uint32_t pos[HIST_FAST_MAX];
-        uint32_t v[HIST_FAST_MAX][4];  // p[q-1], p[q], p[q+1], p[q+2] (slack words past the window)
-        uint32_t need = 0;  // bit k: boundary k falls among the ends (or too close to tell)
-#pragma unroll
-        for (int k = 0; k < HIST_FAST_MAX; ++k) {
-            const uint32_t t = (uint32_t)cl.t_b[k];
-            pos[k] = qhi + 1u;  // every end below the boundary (k >= nb: unused)
-            if (k < dp.nb && dhi + (uint32_t)CUT_EPS_FX > t) {
-                if (dlo >= t + (uint32_t)CUT_EPS_FX) {
-                    pos[k] = qlo;  // every end past it
-                } else {
-                    uint32_t q = ht.t[k];
-                    q = (q < qlo || q > qhi + 1u) ? qlo : q;  // first use, or left behind
-                    pos[k] = q;
-                    need |= 1u << k;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) v[k][i] = cs.p(q + (uint32_t)i - 1u);  // q >= qlo >= 1
-                }
-            }
-        }
+        uint32_t g[HIST_FAST_MAX];
         bool bad = false;
 #pragma unroll
         for (int k = 0; k < HIST_FAST_MAX; ++k) {
-            if (need & (1u << k)) {
-                const uint32_t t = (uint32_t)cl.t_b[k], athr = upb + t;
-                uint32_t q = pos[k];
-                // how many of p[q], p[q+1], p[q+2] are <= athr (ascending prefixes;
-                // past qhi they only move q' to qhi + 1)
-                // (the first one above athr: the slack words past the window are not prefixes)
-                const uint32_t a = v[k][1] > athr ? 0u : v[k][2] > athr ? 1u : v[k][3] > athr ? 2u : 3u;
-                uint32_t phi, plo;  // p[q'] (q' <= qhi) and p[q' - 1] (q' > qlo)
-                if (a == 3u && q + 3u <= qhi) {  // moved further: search (rare)
-                    q = prefix_seek(cs, q + 3u, qhi, (int64_t)athr);
-                    phi = cs.p(q);
-                    plo = cs.p(q - 1u);
-                } else {
-                    // q' = q + d, clamped to qhi + 1: plo = p[q' - 1] = v[d], phi = p[q'] = v[d + 1]
-                    // (read only when q' <= qhi, where d = a <= 2)
-                    const uint32_t d = min(a, qhi + 1u - q);
-                    phi = d == 0u ? v[k][1] : d == 1u ? v[k][2] : v[k][3];
-                    plo = d == 0u ? v[k][0] : d == 1u ? v[k][1] : d == 2u ? v[k][2] : v[k][3];
-                    q += d;
-                }
-                ht.t[k] = q;
-                if (q <= qhi && phi - upb < t + (uint32_t)CUT_EPS_FX) bad = true;
-                if (q > qlo && plo - upb + (uint32_t)CUT_EPS_FX > t) bad = true;
-                pos[k] = q;
+            g[k] = 0u;
+            if ((uint32_t)k < ht.k0) {  // (uniform branches)
+                g[k] = n;
+            } else if ((uint32_t)k < ht.k1) {
+                const uint32_t t = (uint32_t)cl.t_b[k], q = ht.q[k];
+                if (q <= qhi && ht.v[k] - upb < t + (uint32_t)CUT_EPS_FX) bad = true;
+                if (q > qlo && ht.pv[k] - upb + (uint32_t)CUT_EPS_FX > t) bad = true;
+                const uint32_t sh = q - ps;  // q >= ps (p[q] > pb + T_k >= p[ps - 1] + 3)
+                g[k] = sh >= 64u ? 0u : (uint32_t)__popcll(em >> sh);
             }
         }
         if (bad) { r.exact = false; return r; }
-        // G_k = ends at or past boundary k's position (em: ends, bits from ps)
 #pragma unroll
-        for (int k = 0; k < HIST_FAST_MAX; ++k) {
-            const uint32_t sh = pos[k] - ps;  // <= Y + 1 <= 64
-            if (k < dp.nb) ht.c[k] += sh >= 64u ? 0u : (uint32_t)__popcll(em >> sh);
-        }
+        for (int k = 0; k < HIST_FAST_MAX; ++k) ht.c[k] += g[k];
         ht.c[HIST_FAST_MAX] += n;
       }
     } else if (HIST && n) {
@@ -1101,8 +1131,20 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     HistTrack ht;
     const CutLimits cl = cut_limits(dp);
     constexpr bool fast = HIST && FAST;  // (count_fast_ok on the host)
+    ht.k0 = ht.k1 = 0;
 #pragma unroll
-    for (int k = 0; k < HIST_FAST_MAX; ++k) ht.t[k] = 0;
+    for (int k = 0; k < HIST_FAST_MAX; ++k) {
+        ht.q[k] = ht.v[k] = ht.pv[k] = 0;
+        // an exact start's kept ends lie at least CUT_EPS inside [minMH, maxMH]
+        // in prefix units (count_by_masks' limit checks), so a boundary at or
+        // below minMH is surely passed by all of them, one at or above maxMH
+        // by none (SQLiteMult: a 1000-Da edge equal to maxMH, 6000 Da)
+        if (k < dp.nb && cl.t_b[k] <= cl.t_min) ht.k0 = k + 1;
+        if (k < dp.nb && cl.t_b[k] < cl.t_max) ht.k1 = k + 1;
+    }
+#ifdef DBI_X_NOBUCKET
+    ht.k1 = ht.k0;  // experiment build: no boundary work (results not valid)
+#endif
 #pragma unroll
     for (int k = 0; k <= HIST_FAST_MAX; ++k) ht.c[k] = 0;
     TileCtx tc;
