@@ -1142,9 +1142,6 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
         if (k < dp.nb && cl.t_b[k] <= cl.t_min) ht.k0 = k + 1;
         if (k < dp.nb && cl.t_b[k] < cl.t_max) ht.k1 = k + 1;
     }
-#ifdef DBI_X_NOBUCKET
-    ht.k1 = ht.k0;  // experiment build: no boundary work (results not valid)
-#endif
 #pragma unroll
     for (int k = 0; k <= HIST_FAST_MAX; ++k) ht.c[k] = 0;
     TileCtx tc;
@@ -1383,6 +1380,10 @@ __device__ __forceinline__ uint32_t first_bit_128(uint64_t lo, uint64_t hi) {
 // bits [0, x) of a 64-bit word, x <= 64
 __device__ __forceinline__ uint64_t low_bits(uint32_t x) { return x >= 64 ? ~0ull : ((1ull << x) - 1ull); }
 
+template <uint32_t R>
+__device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32_t n, uint32_t* s_cnt,
+                          uint32_t* s_run, uint32_t* s_tmp, uint4* stage, uint16_t* sdig, Counters* __restrict__ ctr);
+
 // ---------------------------------------------------------------------------
 // Bounded semi-specific digest (no mandatory residues, no windows; warm
 // builds): one walk per start instead of the fused kernel's count walk +
@@ -1400,12 +1401,15 @@ __device__ __forceinline__ uint64_t low_bits(uint32_t x) { return x >= 64 ? ~0ul
 // records into its slots, and the unused slots get REC_SENTINEL, which the
 // first radix pass drops -- as in k_digest_bounded.
 // ---------------------------------------------------------------------------
-template <bool DROP>
+// PART: the tile's records partitioned afterwards into the regions of their
+// fine bins' low digit (part_tile, PartOut::lsd: the radix tail's first pass,
+// fused; the slots are scratch).
+template <bool DROP, bool PART = false>
 __global__ void __launch_bounds__(DIGEST_THREADS)
 k_digest_semi_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                       const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
                       uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, Rec* __restrict__ d_out, uint64_t cap,
-                      Counters* __restrict__ d_ctr) {
+                      Counters* __restrict__ d_ctr, PartOut po) {
     __shared__ DigestSmem sm;
     __shared__ unsigned long long s_base;
     TileCtx tc;
@@ -1461,21 +1465,42 @@ k_digest_semi_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const
         if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
         if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
     }
+    if constexpr (PART) {  // the walks' LDS is dead: the counters in the mass table, the stage over window + candidates
+        constexpr size_t b0 = offsetof(DigestSmem, win), b1 = offsetof(DigestSmem, tmp);
+        constexpr uint32_t R = (uint32_t)((b1 - b0) / 18 / 64 * 64);  // 16 B + 2 B per staged record
+        static_assert(b0 % 16 == 0 && R >= 512 && sizeof(sm.mass) >= 512 * sizeof(uint32_t), "partition stage");
+        uint8_t* st = reinterpret_cast<uint8_t*>(&sm) + b0;
+        uint32_t* p_cnt = reinterpret_cast<uint32_t*>(sm.mass);
+        part_tile<R>(po, d_out + base, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
+                     reinterpret_cast<uint16_t*>(st + 16 * R), d_ctr);
+    }
 }
 
 hipError_t launch_digest_semi_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                       const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                       const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr,
-                                      hipStream_t s) {
+                                      hipStream_t s, const PartOut* part) {
     const uint32_t nblk = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     if (nblk == 0) return hipSuccess;
     if (!dp.semi || dp.mand_mode || dp.filter) return hipErrorInvalidValue;
-    if (dp.drop_mass <= dp.max_mh)
-        DBI_LAUNCH((k_digest_semi_bounded<true>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags,
-                   d_res, d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr);
-    else
-        DBI_LAUNCH((k_digest_semi_bounded<false>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags,
-                   d_res, d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr);
+    PartOut po{};
+    if (part) {
+        if (!part->lsd || part->b1 < 1 || part->b1 > 8 || part->dm.b2 < 1 || part->dm.b2 > RADIX_BITS || part->cap % 64)
+            return hipErrorInvalidValue;
+        po = *part;
+    }
+#define DBI_DIGEST_S(DROP, PART)                                                                                     \
+    DBI_LAUNCH((k_digest_semi_bounded<DROP, PART>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags, \
+               d_res, d_poff, n_prot, n_res, d_tile_pf, d_out, cap, d_ctr, po)
+    const bool drop = dp.drop_mass <= dp.max_mh;
+    if (part) {
+        if (drop) DBI_DIGEST_S(true, true);
+        else DBI_DIGEST_S(false, true);
+    } else {
+        if (drop) DBI_DIGEST_S(true, false);
+        else DBI_DIGEST_S(false, false);
+    }
+#undef DBI_DIGEST_S
     return hipGetLastError();
 }
 
@@ -1727,13 +1752,22 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // A region that would overflow takes nothing and flags the build (ERR_PART:
 // redone by the radix tail).  The records never go through a full radix pass
 // of their own: this is the first pass, fused.
-// s_cnt / s_gof: 256 words each; stage: PART_R x 16 B, then PART_R x 2 B.
+// s_cnt / s_run: 256 words each; stage: PART_R x 16 B, then PART_R x 2 B.
+// A tile of more than R records (semi-specific: ~20 k) takes several rounds.
+// Measured without gain there: counting a tile's digits first and reserving
+// each digit's run once, so that the rounds need no global atomic (semi-tryptic
+// digest 24.1 -> 25.8 ms), and loading the next round's records while one is
+// written (24.8 ms): the partition moves its bytes (the slots read back, the
+// regions written) at about the copy rate.
 template <uint32_t R>
 __device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32_t n, uint32_t* s_cnt,
-                          uint32_t* s_gof, uint32_t* s_tmp, uint4* stage, uint16_t* sdig, Counters* __restrict__ ctr) {
+                          uint32_t* s_run, uint32_t* s_tmp, uint4* stage, uint16_t* sdig, Counters* __restrict__ ctr) {
     constexpr uint32_t KI = (R + DIGEST_THREADS - 1) / DIGEST_THREADS;
     const uint32_t tid = threadIdx.x, xcd = xcc_id(), D1 = 1u << po.b1;
     const uint32_t b2 = po.dm.b2, m2 = (1u << b2) - 1u;
+    // the region digit of a bin (depth: its high b1 bits; lsd: its low b1 bits) and its pass-2 digit
+    auto d1_of = [&](uint32_t b) { return po.lsd ? b & (D1 - 1u) : b >> b2; };
+    auto d2_of = [&](uint32_t b) { return po.lsd ? (b >> po.b1) & m2 : b & m2; };
     const uint4* __restrict__ src4 = reinterpret_cast<const uint4*>(src);
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(po.recs);
     // every record of the tile acknowledged by the L2 before the barrier: the
@@ -1755,8 +1789,8 @@ __device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32
             bin[k] = ~0u;
             rk[k] = 0;
             if (k * DIGEST_THREADS + tid < nr && (rv[k].x & rv[k].y) != 0xFFFFFFFFu) {  // not a sentinel
-                bin[k] = depth_bin(u4_mass(rv[k]), po.dm);
-                rk[k] = atomicAdd(&s_cnt[bin[k] >> b2], 1u);
+                bin[k] = po.lsd ? bin_of(u4_mass(rv[k]), po.lin) : depth_bin(u4_mass(rv[k]), po.dm);
+                rk[k] = atomicAdd(&s_cnt[d1_of(bin[k])], 1u);
             }
         }
         __syncthreads();
@@ -1775,25 +1809,25 @@ __device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32
                 if (o + c <= po.cap) g = (tid * DEPTH_XCDS + xcd) * po.cap + o - lstart;
                 else atomicOr(&ctr->err, ERR_PART);
             }
-            s_gof[tid] = g;
+            s_run[tid] = g;
             s_cnt[tid] = lstart;
         }
         __syncthreads();
 #pragma unroll
         for (uint32_t k = 0; k < KI; ++k) {
             if (bin[k] != ~0u) {
-                const uint32_t at = s_cnt[bin[k] >> b2] + rk[k];
+                const uint32_t at = s_cnt[d1_of(bin[k])] + rk[k];
                 stage[at] = rv[k];
-                sdig[at] = (uint16_t)bin[k];
+                sdig[at] = (uint16_t)(d1_of(bin[k]) << 8 | d2_of(bin[k]));
             }
         }
         __syncthreads();
         for (uint32_t t = tid; t < nvalid; t += DIGEST_THREADS) {
             const uint32_t bb = sdig[t];
-            const uint32_t g = s_gof[bb >> b2];
+            const uint32_t g = s_run[bb >> 8];
             if (g != ~0u) {
                 out4[g + t] = stage[t];
-                po.dig[g + t] = (uint8_t)(bb & m2);
+                po.dig[g + t] = (uint8_t)(bb & 0xFFu);
             }
         }
     }
@@ -2848,15 +2882,22 @@ __device__ __forceinline__ uint32_t part_hidx(const PartChunk& pc, uint32_t c, u
     return (pc.first << b2) + d2 * pc.nch + (c - pc.first);
 }
 
-// the low digits (bytes) of one chunk counted in per-wave LDS rows
+// the pass-2 digits (bytes) of one chunk counted in per-wave LDS rows.  LSD:
+// the histogram is digit-major over every chunk of the grid (the chunks past
+// ctr->part_chunks count nothing), so the scan orders records by (d2, d1)
+template <bool LSD>
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_part_hist(const uint8_t* __restrict__ dig, const uint32_t* __restrict__ cur, uint32_t cap,
             const uint32_t* __restrict__ desc, const uint32_t* __restrict__ d1c, uint32_t b1, uint32_t b2,
             uint32_t* __restrict__ hist, const Counters* __restrict__ ctr) {
     __shared__ uint32_t cnt[RADIX_NW][RADIX_D];
     const uint32_t c = xcd_contiguous_block();
-    if (c >= ctr->part_chunks) return;
     const uint32_t w = threadIdx.x >> 6, D2 = 1u << b2;
+    if (c >= ctr->part_chunks) {
+        if (LSD)
+            for (uint32_t d = threadIdx.x; d < D2; d += RADIX_THREADS) hist[(size_t)d * gridDim.x + c] = 0u;
+        return;
+    }
     for (uint32_t d = lane_id(); d < D2; d += 64) cnt[w][d] = 0;
     const PartChunk pc = part_chunk(c, cur, cap, desc, d1c, b1);
     static_assert(PART_CHUNK == RADIX_THREADS * 8, "one 8-B load per thread");
@@ -2872,28 +2913,36 @@ k_part_hist(const uint8_t* __restrict__ dig, const uint32_t* __restrict__ cur, u
         uint32_t t = 0;
 #pragma unroll
         for (uint32_t ww = 0; ww < (uint32_t)RADIX_NW; ++ww) t += cnt[ww][d];
-        hist[part_hidx(pc, c, d, b2)] = t;
+        hist[LSD ? (size_t)d * gridDim.x + c : part_hidx(pc, c, d, b2)] = t;
     }
 }
 
 hipError_t launch_part_hist(const uint8_t* d_dig, const uint32_t* d_cur, uint32_t cap, const uint32_t* d_desc,
                             const uint32_t* d_d1c, uint32_t b1, uint32_t b2, uint32_t max_chunks, uint32_t* d_hist,
-                            const Counters* d_ctr, hipStream_t s) {
+                            const Counters* d_ctr, hipStream_t s, bool lsd) {
     if (max_chunks == 0) return hipSuccess;
     if (b2 < 1 || b2 > (uint32_t)RADIX_BITS) return hipErrorInvalidValue;
-    DBI_LAUNCH(k_part_hist, dim3(max_chunks), dim3(RADIX_THREADS), 0, s, d_dig, d_cur, cap, d_desc, d_d1c, b1, b2,
-               d_hist, d_ctr);
+    if (lsd)
+        DBI_LAUNCH(k_part_hist<true>, dim3(max_chunks), dim3(RADIX_THREADS), 0, s, d_dig, d_cur, cap, d_desc, d_d1c,
+                   b1, b2, d_hist, d_ctr);
+    else
+        DBI_LAUNCH(k_part_hist<false>, dim3(max_chunks), dim3(RADIX_THREADS), 0, s, d_dig, d_cur, cap, d_desc, d_d1c,
+                   b1, b2, d_hist, d_ctr);
     return hipGetLastError();
 }
 
 // The pass over the low digit: a chunk's records ranked per digit in input
 // order (wave ballots, as k_radix_scatter), exchanged through LDS and written
-// as digit runs to their (high digit, low digit) = bin place.
+// as digit runs to their (high digit, low digit) = bin place.  LSD: the
+// second pass of linear bins (order (d2, d1)), each record's next-pass digit
+// written beside it (ndig), as k_radix_scatter does.
+template <bool LSD>
 __global__ void __launch_bounds__(RADIX_THREADS)
 k_part_scatter(const Rec* __restrict__ recs, const uint8_t* __restrict__ dig, const uint32_t* __restrict__ cur,
                uint32_t cap, const uint32_t* __restrict__ desc, const uint32_t* __restrict__ d1c, uint32_t b1,
                uint32_t b2, const uint32_t* __restrict__ offs, Rec* __restrict__ out,
-               const Counters* __restrict__ ctr) {
+               const Counters* __restrict__ ctr, uint8_t* __restrict__ ndig, BinMap bm, uint32_t nshift,
+               uint32_t nbits) {
     __shared__ uint16_t cnt[RADIX_NW][RADIX_D];
     __shared__ uint4 stage[RADIX_CHUNK];
     __shared__ uint8_t sdig[RADIX_CHUNK];
@@ -2923,7 +2972,8 @@ k_part_scatter(const Rec* __restrict__ recs, const uint8_t* __restrict__ dig, co
             dd[k] = i < pc.n ? (uint32_t)dig[pc.lo + i] : 0u;
         }
     }
-    const uint32_t goff = threadIdx.x < D2 ? offs[part_hidx(pc, c, threadIdx.x, b2)] : 0u;
+    const uint32_t goff =
+        threadIdx.x < D2 ? offs[LSD ? (size_t)threadIdx.x * gridDim.x + c : part_hidx(pc, c, threadIdx.x, b2)] : 0u;
     uint32_t pos[RADIX_ITEMS];
     uint32_t vmask = 0;
 #pragma unroll
@@ -2969,17 +3019,25 @@ k_part_scatter(const Rec* __restrict__ recs, const uint8_t* __restrict__ dig, co
     }
     __syncthreads();
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(out);
-    for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) out4[gofs[sdig[t]] + t] = stage[t];
+    for (uint32_t t = threadIdx.x; t < nvalid; t += RADIX_THREADS) {
+        const uint32_t at = gofs[sdig[t]] + t;
+        out4[at] = stage[t];
+        if (LSD && ndig) ndig[at] = (uint8_t)((bin_of(u4_mass(stage[t]), bm) >> nshift) & ((1u << nbits) - 1u));
+    }
 }
 
 hipError_t launch_part_scatter(const Rec* d_recs, const uint8_t* d_dig, const uint32_t* d_cur, uint32_t cap,
                                const uint32_t* d_desc, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
                                uint32_t max_chunks, const uint32_t* d_offs, Rec* d_out, const Counters* d_ctr,
-                               hipStream_t s) {
+                               hipStream_t s, bool lsd, uint8_t* d_ndig, BinMap bm, uint32_t nshift, uint32_t nbits) {
     if (max_chunks == 0) return hipSuccess;
-    if (b2 < 1 || b2 > (uint32_t)RADIX_BITS) return hipErrorInvalidValue;
-    DBI_LAUNCH(k_part_scatter, dim3(max_chunks), dim3(RADIX_THREADS), 0, s, d_recs, d_dig, d_cur, cap, d_desc, d_d1c,
-               b1, b2, d_offs, d_out, d_ctr);
+    if (b2 < 1 || b2 > (uint32_t)RADIX_BITS || (d_ndig && (!lsd || nbits < 1 || nbits > 8))) return hipErrorInvalidValue;
+    if (lsd)
+        DBI_LAUNCH(k_part_scatter<true>, dim3(max_chunks), dim3(RADIX_THREADS), 0, s, d_recs, d_dig, d_cur, cap,
+                   d_desc, d_d1c, b1, b2, d_offs, d_out, d_ctr, d_ndig, bm, nshift, nbits);
+    else
+        DBI_LAUNCH(k_part_scatter<false>, dim3(max_chunks), dim3(RADIX_THREADS), 0, s, d_recs, d_dig, d_cur, cap,
+                   d_desc, d_d1c, b1, b2, d_offs, d_out, d_ctr, d_ndig, bm, nshift, nbits);
     return hipGetLastError();
 }
 

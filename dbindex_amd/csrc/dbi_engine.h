@@ -269,6 +269,7 @@ struct dbi_handle {
         uint64_t n_res = 0, n_prot = 0, cap = 0, last_kept = 0, alloc_gen = 0, dp_gen = 0;
         uint64_t prev_unique = 0;         // depth bins: the sampled index
         uint32_t depth_cap = 0;           // depth bins: region capacity (0: the radix tail)
+        uint32_t lsd_cap = 0;             // semi builds' first-digit partition: region capacity (0: none)
         bool depth_fresh = false;         // depth bins: the map is sampled in this build
         bool tail_local = false;          // the previous build's tail (its list grids)
         uint32_t grid_mid = 0, grid_big = 0, grid_split = 0;
@@ -279,7 +280,8 @@ struct dbi_handle {
         bool operator==(const GraphKey& o) const {
             return d_res == o.d_res && d_poff == o.d_poff && n_res == o.n_res && n_prot == o.n_prot &&
                    cap == o.cap && last_kept == o.last_kept && alloc_gen == o.alloc_gen && dp_gen == o.dp_gen &&
-                   prev_unique == o.prev_unique && depth_cap == o.depth_cap && depth_fresh == o.depth_fresh &&
+                   prev_unique == o.prev_unique && depth_cap == o.depth_cap && lsd_cap == o.lsd_cap &&
+                   depth_fresh == o.depth_fresh &&
                    tail_local == o.tail_local &&
                    grid_mid == o.grid_mid && grid_big == o.grid_big && grid_split == o.grid_split &&
                    giants == o.giants && timing == o.timing &&
@@ -294,6 +296,7 @@ struct dbi_handle {
     bool h1_on = false;                   // this warm build's digest counts the first radix histogram (h1plan)
     // depth bins (warm lean builds: dbi_engine.hip warm_body_depth)
     bool use_depth = true;                // option depth_bins=0: the radix tail always
+    bool use_semi_part = true;            // option semi_part=0: warm semi builds' first radix pass as its own kernels
     bool depth_off = false;               // this build's retry takes the radix tail (a region overflowed)
     bool depth_keep_map = false;          // this build's retry keeps the depth map it computed
     const uint4* depth_map_of = nullptr;  // the map buffer a complete map was last enqueued into

@@ -413,10 +413,10 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
             }
             const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
             if (bounded && !lean)
-                STAGE(h, "digest", by(1, 16, 0, 4, 0),
+                STAGE(h, "digest", by(1, h->part_now ? 17 : 16, 0, 4, 0),
                       launch_digest_semi_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
                                                  (uint32_t)h->n_prot, (uint32_t)R, h->tile_pf.p, h->recA.p, cap,
-                                                 h->ctr.p, s));
+                                                 h->ctr.p, s, dev_sized ? h->part_now : nullptr));
             else if (bounded)
                 STAGE(h, "digest", by(1, h->part_now ? 17 : 16, 0, 4, 0),
                       launch_digest_bounded(h->dp, h->mass_tab.p, h->flags_tab.p, h->d_res, h->d_poff,
@@ -524,6 +524,122 @@ bool depth_map_reusable(const dbi_handle* h, uint32_t nbins) {
            h->prev_unique != 0 && h->depth_map_unique == h->prev_unique && h->depth_map_nbins == nbins;
 }
 
+// Warm semi-specific builds: the radix tail's first
+// LSD pass -- its histogram over the sparse slots and its scatter, two full
+// passes over 16-B records -- fused into the digest: each tile partitions its
+// records by the low digit (b1 bits) of their linear fine bin into (digit,
+// XCD) regions (part_tile, PartOut::lsd), one pass over the regions by the
+// second digit (k_part_hist / k_part_scatter, digit-major: a stable LSD pass)
+// writes them dense, with each record's third digit beside it, and the radix
+// tail goes on from its third pass.  Any order inside a digit is fine for an
+// LSD pass; the chunk sort orders every bin by the full record key.
+constexpr uint64_t LSD_MIN_RECS = 1u << 16;
+struct LsdPlan {
+    bool on = false;
+    uint32_t nbins = 0, b1 = 0, b2 = 0, cap = 0, nreg = 0, max_chunks = 0;
+    int passes = 0;
+    int width[8] = {};
+};
+
+LsdPlan lsd_plan(const dbi_handle* h) {
+    LsdPlan p;
+    const uint64_t n = h->last_kept, slots = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
+    if (!h->use_semi_part || h->depth_off || !h->dp.semi || lean_digest(h) || !bounded_digest(h) ||
+        n < LSD_MIN_RECS || slots < 1024)
+        return p;
+    p.nbins = choose_nbins(std::min(n, slots), h->bin_bits_max);  // build_tail's bins (n_est = the last count)
+    p.passes = radix_plan(p.nbins, true, p.width);
+    if (p.passes < 2 || p.width[0] < 1 || p.width[0] > 8 || p.width[1] < 1 || p.width[1] > RADIX_BITS) return LsdPlan{};
+    p.b1 = (uint32_t)p.width[0];
+    p.b2 = (uint32_t)p.width[1];
+    p.nreg = (1u << p.b1) * DEPTH_XCDS;
+    const double share = (double)n / (double)p.nreg * h->depth_slack;
+    p.cap = (uint32_t)std::min<double>((share + 256.0 + 63.0) / 64.0, (double)(1u << 26)) * 64u;
+    if ((uint64_t)p.nreg * p.cap >= (1ull << 32) - 1 || p.cap / PART_CHUNK >= 65536u) return LsdPlan{};
+    p.max_chunks = (uint32_t)std::min<uint64_t>((uint64_t)p.nreg * ((p.cap + PART_CHUNK - 1) / PART_CHUNK),
+                                                 slots / PART_CHUNK + p.nreg);
+    p.on = true;
+    return p;
+}
+
+int warm_body_lsd(dbi_handle* h, const LsdPlan& pl, uint64_t* n_in, bool* sparse) {
+    hipStream_t s = h->stream;
+    int rc;
+    const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
+    const uint32_t cap32 = (uint32_t)cap;
+    const uint64_t nreg_slots = (uint64_t)pl.nreg * pl.cap;
+    const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
+    const BinMap bm = make_binmap(h->params.min_mh, h->params.max_mh, pl.nbins);
+    const uint32_t T = chunk_target(h, cap);
+    const uint32_t nchunks = (uint32_t)std::max<uint64_t>((cap + T - 1) / T, 1);
+    // every allocation before the first launch
+    if ((rc = tail_buffers(h, cap, cap, true, pl.passes, pl.width[pl.passes - 1])) ||
+        (rc = h->recR.ensure(nreg_slots)) || (rc = h->rdig.ensure(nreg_slots + 16)) ||
+        (rc = h->rcur.ensure(DEPTH_XCDS * 256)) || (rc = h->desc.ensure(pl.max_chunks)) || (rc = h->d1c.ensure(512)) ||
+        (rc = h->hist2.ensure((size_t)pl.max_chunks << pl.b2)) || (rc = h->blk.ensure(std::max<uint32_t>(ntiles, 1))) ||
+        (rc = h->thr.ensure((size_t)ntiles * DIGEST_THREADS + 1)) || (rc = h->tile_pf.ensure(2 * ((size_t)ntiles + 2))) ||
+        (rc = h->scan_tmp.ensure(std::max({scan_u32_tmp_elems((uint64_t)pl.max_chunks << pl.b2),
+                                           scan_u32_tmp_elems(ntiles), h->scan_tmp.cap}))))
+        return rc;
+    DBI_HIP(hipMemsetAsync(h->rcur.p, 0, sizeof(uint32_t) * DEPTH_XCDS * 256, s));
+    PartOut po{};
+    po.recs = h->recR.p;
+    po.dig = h->rdig.p;
+    po.cur = h->rcur.p;
+    po.dm.b2 = pl.b2;
+    po.cap = pl.cap;
+    po.b1 = pl.b1;
+    po.lsd = 1;
+    po.lin = bm;
+    h->part_now = &po;
+    uint64_t n = 0;
+    bool dev = false;
+    rc = run_digest(h, &n, n_in, sparse, &dev);
+    h->part_now = nullptr;
+    if (rc) return rc;
+    if (!dev) return set_error(DBI_E_STATE, "internal: warm build without device sizing");
+    const unsigned long long* d_n = &h->ctr.p->tail_n;  // k_part_plan: the records, 0 when anything overflowed
+    // the second LSD pass, region by region, into recA (dense), with the third digit of each record
+    const int nshift = pl.width[0] + pl.width[1], nbits = pl.passes > 2 ? pl.width[2] : 0;
+    STAGE(h, "part_plan", by(0, 0, 0, 0, 0),
+          launch_part_plan(h->rcur.p, pl.cap, pl.b1, cap, h->desc.p, h->d1c.p, h->ctr.p, s));
+    STAGE(h, "part_hist", by(0, 1, 0, 0, 0),
+          launch_part_hist(h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2, pl.max_chunks, h->hist2.p,
+                           h->ctr.p, s, true));
+    STAGE(h, "part_scan", by(0, 0, 0, 0, 0),
+          launch_scan_u32(h->hist2.p, h->hist2.p, (uint64_t)pl.max_chunks << pl.b2, h->scan_tmp.p, h->scan_tmp.cap,
+                          nullptr, s));
+    STAGE(h, "bin_scatter", by(0, nbits ? 33 : 32, 0, 0, 0),
+          launch_part_scatter(h->recR.p, h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2,
+                              pl.max_chunks, h->hist2.p, h->recA.p, h->ctr.p, s, true,
+                              nbits ? h->digits.p : nullptr, bm, (uint32_t)nshift, (uint32_t)nbits));
+    // the radix tail's remaining passes (build_tail's, from the third)
+    Rec* src = h->recA.p;
+    Rec* dst = h->recB.p;
+    int shift = nshift;
+    for (int ps = 2; ps < pl.passes; ++ps) {
+        const int bits = pl.width[ps];
+        const double hbytes = 8.0 * (double)radix_blocks(cap32) * (double)(1u << bits);
+        STAGE(h, "radix_hist", by(0, 1, 0, 0, 0), launch_radix_hist_u8(h->digits.p, cap32, bits, h->hist.p, s, d_n));
+        STAGE(h, "radix_scan", by(0, 0, 0, 0, 0),
+              launch_scan_u32(h->hist.p, h->hist.p, (uint64_t)radix_blocks(cap32) << bits, h->scan_tmp.p,
+                              h->scan_tmp.cap, nullptr, s));
+        h->stages[h->nstage - 1].cB = hbytes / std::max<double>(pl.nbins, 1.0);
+        const bool more = ps + 1 < pl.passes;
+        const int nb = more ? pl.width[ps + 1] : 0;
+        STAGE(h, "radix_scatter", by(0, more ? 33 : 32, 0, 0, 0),
+              launch_radix_scatter(src, dst, cap32, bm, shift, bits, false, h->hist.p, s, more ? h->digits.p : nullptr,
+                                   shift + bits, nb, d_n));
+        std::swap(src, dst);
+        shift += bits;
+    }
+    STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
+          launch_chunk_bounds(src, cap32, bm, T, nchunks, h->chunk_lo.p, s, d_n));
+    if ((rc = sort_chunks(h, src, dst, bm, nchunks, cap, d_n, false, false))) return rc;
+    h->stats.n_bins = pl.nbins;
+    return 0;
+}
+
 dbi_handle::GraphKey graph_key(const dbi_handle* h) {
     dbi_handle::GraphKey k{};
     k.d_res = h->d_res;
@@ -540,6 +656,8 @@ dbi_handle::GraphKey graph_key(const dbi_handle* h) {
     const DepthPlan dpl = depth_plan(h);
     k.depth_cap = dpl.on ? dpl.cap : 0u;
     k.depth_fresh = dpl.on && !depth_map_reusable(h, dpl.nbins);
+    const LsdPlan lpl = lsd_plan(h);
+    k.lsd_cap = lpl.on ? lpl.cap : 0u;
     k.giants = h->giants_seen;
     k.alloc_gen = g_alloc_gen.load(std::memory_order_relaxed);
     k.dp_gen = h->dp_gen;
@@ -663,6 +781,8 @@ int warm_body(dbi_handle* h, uint64_t* n_in, bool* sparse) {
         const int rd = warm_body_depth(h, dpl, um == h->umass.p && oo == h->occ_off.p, n_in, sparse);
         if (rd != DEPTH_FALLBACK) return rd;
     }
+    const LsdPlan lpl = lsd_plan(h);
+    if (lpl.on) return warm_body_lsd(h, lpl, n_in, sparse);
     // small tails: the bounded digest counts the first radix pass's histogram
     // as it writes the records (one kernel and its launch gap fewer, human
     // scale 0.33 -> 0.31 ms).  Bins and buffers planned here from what
@@ -1645,6 +1765,7 @@ int dbi_set_option(dbi_handle* h, const char* name, int64_t value) {
     else if (n == "digest_hist") h->use_h1 = on;
     else if (n == "semi_bounded") h->use_semi_bounded = on;
     else if (n == "depth_bins") h->use_depth = on;
+    else if (n == "semi_part") h->use_semi_part = on;
     else if (n == "depth_map_reuse") h->opt_depth_map_reuse = on;
     else if (n == "big_split" && ranged(-1, 1)) h->big_split = (int)value;
     else if (n == "bin_bits_max" && ranged(1, 32)) h->bin_bits_max = (int)value;

@@ -271,13 +271,17 @@ struct DepthMap {
     uint32_t b2;           // low bits of a bin (the pass-2 digit); the high bits: the digest's partition
     uint32_t last;         // the last bin (2^(b1 + b2) - 1)
 };
-struct PartOut {          // the digest's partition (k_digest_bounded PART)
+struct PartOut {          // the digest's partition (k_digest_bounded / k_digest_semi_bounded PART)
     Rec* recs;            // region r = d1 * DEPTH_XCDS + xcd at [r * cap, r * cap + cur[r])
-    uint8_t* dig;         // the low b2 bits of each record's bin, same positions
+    uint8_t* dig;         // each record's pass-2 digit (b2 bits), same positions
     uint32_t* cur;        // per region: records placed (zeroed before the digest)
-    DepthMap dm;
+    DepthMap dm;          // depth bins: d1 = the bin's high b1 bits, the digit its low b2 bits
     uint32_t cap;         // records per region (a multiple of 64)
     uint32_t b1;
+    // lsd (linear fine bins, semi-specific builds): d1 = the bin's LOW b1 bits
+    // (the first LSD pass), the digit the next dm.b2 bits (the second)
+    uint32_t lsd;
+    BinMap lin;
 };
 // the map: ns evenly spaced uniques of the previous index (mass order) -> their
 // sub-bins and occurrence weights; the weights' scan (total -> ctr->depth_w);
@@ -298,13 +302,18 @@ hipError_t launch_digest_bounded(const DevParams& dp, const double* d_mass_tab, 
 hipError_t launch_part_plan(const uint32_t* d_cur, uint32_t cap, uint32_t b1, uint64_t slot_cap, uint32_t* d_desc,
                             uint32_t* d_d1c, Counters* d_ctr, hipStream_t s);
 // hist[(first(d1) << b2) + d2 * nch(d1) + (c - first(d1))] = records of chunk c with digit d2
+// (records ordered by (d1, d2): depth bins); lsd: hist[d2 * max_chunks + c]
+// (ordered by (d2, d1): the second LSD pass of linear bins; the chunks past
+// ctr->part_chunks write zeros)
 hipError_t launch_part_hist(const uint8_t* d_dig, const uint32_t* d_cur, uint32_t cap, const uint32_t* d_desc,
                             const uint32_t* d_d1c, uint32_t b1, uint32_t b2, uint32_t max_chunks, uint32_t* d_hist,
-                            const Counters* d_ctr, hipStream_t s);
+                            const Counters* d_ctr, hipStream_t s, bool lsd = false);
+// lsd: also each record's next-pass digit ((bin_of(m, bm) >> nshift) & (2^nbits - 1)) into d_ndig
 hipError_t launch_part_scatter(const Rec* d_recs, const uint8_t* d_dig, const uint32_t* d_cur, uint32_t cap,
                                const uint32_t* d_desc, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
                                uint32_t max_chunks, const uint32_t* d_offs, Rec* d_out, const Counters* d_ctr,
-                               hipStream_t s);
+                               hipStream_t s, bool lsd = false, uint8_t* d_ndig = nullptr, BinMap bm = BinMap{},
+                               uint32_t nshift = 0, uint32_t nbits = 0);
 // chunk pairs over the bin-ordered records from the pass-2 offsets: bin
 // starts (bstart: nbins + 1), then chunk_lo[2c] = first bin start at or after
 // c*T, chunk_lo[2c+1] = the last bin's start when the chunk exceeds CHUNK_CAP
@@ -317,7 +326,7 @@ hipError_t launch_depth_bounds(const uint32_t* d_offs, const uint32_t* d_d1c, ui
 hipError_t launch_digest_semi_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                       const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
                                       const uint32_t* d_tile_pf, Rec* d_out, uint64_t cap, Counters* d_ctr,
-                                      hipStream_t s);
+                                      hipStream_t s, const PartOut* part = nullptr);
 // tail_in / tail_n of a device-sized build: the digest's slot and record
 // counts, or 0 / 0 when the slots needed exceed cap
 hipError_t launch_tail_counts(Counters* d_ctr, uint64_t cap, bool sparse, hipStream_t s);

@@ -137,3 +137,37 @@ def test_options_and_cold_builds(Engine):
             eng.build(pp)
             assert_index_equal(eng, oix, f"after cold {k}")
         assert "bin_scatter" in _stages(eng)
+
+
+def test_semi_first_digit_partition(Engine):
+    """Warm semi-specific builds partition their records in the digest by the
+    low digit of their linear fine bin (the radix tail's first LSD pass, fused:
+    part_hist / bin_scatter, then the remaining radix pass).  Proteome A, then
+    B: A with a block of GAAAAAAK repeats, whose equal-mass records crowd one
+    region past the capacity A's counts gave it (ERR_PART: redone by the radix
+    tail, the next build with more room), then A again.  Every build, timed and
+    replayed, equals its oracle (DBIndexer.java:237-405)."""
+    a = fasta.config("human").slice(0, 3000)
+    spike = a.residues.copy()
+    e = int(a.offsets[1500])
+    spike[:e] = np.resize(np.frombuffer(b"GAAAAAAK", np.uint8), e)
+    b = fasta.PackedProteins(spike, a.offsets.copy(), a.defs)
+    cp = DBIndexSearchParams.semi_tryptic(2).to_c()
+    oa, ob = cref.Index(cp, a.residues, a.offsets), cref.Index(cp, b.residues, b.offsets)
+    with Engine(cp) as eng:
+        seen_redo = False
+        for k, (p, o) in enumerate([(a, oa), (a, oa), (a, oa), (b, ob), (b, ob), (b, ob), (a, oa), (a, oa)]):
+            eng.build(p)
+            names = _stages(eng)
+            assert_index_equal(eng, o, f"semi build {k}")
+            if k in (1, 2):
+                assert {"part_hist", "bin_scatter"} <= names, (k, names)
+            if k == 3:  # A's region capacities: the spike overflows one, the radix tail redoes it
+                seen_redo = "bin_scatter" not in names and "radix_scatter" in names
+        assert seen_redo, "the spike did not overflow a region"
+        eng.set_timing(False)
+        for k in range(3):
+            eng.build(a)
+            assert_index_equal(eng, oa, f"semi untimed {k}")
+        m, t = query_masses(oa, 3000, seed=5)
+        assert_queries_equal(eng, oa, m, t, "semi queries")

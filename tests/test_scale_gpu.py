@@ -118,23 +118,36 @@ def test_swissprot_sharded_8_shards(Engine, swissprot, swissprot_oix):
             e.close()
 
 
-@pytest.mark.parametrize("big_split", ["auto", "1"])
-def test_swissprot_semi_slice(Engine, swissprot, big_split):
+@pytest.mark.parametrize("big_split,semi_part", [("auto", 1), ("1", 1), ("auto", 0)])
+def test_swissprot_semi_slice(Engine, swissprot, big_split, semi_part):
     """configs[3] parity on a 30k-protein slice (~55M semi-tryptic peptides),
     large enough to reach the 1024-thread big-chunk tier (equal-mass spikes).
     option big_split=1: the big tier in its two size classes (512-thread blocks
     for chunks of up to 3968 records, the rest 1024-thread), which the engine
-    otherwise uses only for lists longer than 1024 chunks (full semi-tryptic)."""
+    otherwise uses only for lists longer than 1024 chunks (full semi-tryptic).
+    Warm builds partition their records by the first LSD digit in the digest
+    (semi_part=1: part_hist / bin_scatter, then the radix tail's third pass),
+    or run the radix tail's three passes (semi_part=0); a timed warm build
+    shows which stages ran."""
     pp = swissprot.slice(0, 30000)
     cp = DBIndexSearchParams.semi_tryptic(2).to_c()
+    opts = {"semi_part": semi_part}
+    if big_split != "auto":
+        opts["big_split"] = int(big_split)
     with cref.threads(THREADS):
         oix = cref.Index(cp, pp.residues, pp.offsets)
         m, t = query_masses(oix, 1_000_000)
-        with Engine(cp, options={} if big_split == "auto" else {"big_split": int(big_split)}) as eng:
-            for phase in ("cold", "warm", "replay"):
+        with Engine(cp, options=opts) as eng:
+            for phase in ("cold", "warm", "replay", "timed"):
+                eng.set_timing(phase == "timed")
                 st = eng.build(pp)
                 assert st.n_big_bins > 0, "slice too small to reach the big-chunk tier"
-                assert_index_equal(eng, oix, f"semi slice [{phase}, big split {big_split}]")
+                assert_index_equal(eng, oix, f"semi slice [{phase}, big split {big_split}, semi_part {semi_part}]")
+            names = {name for name, _, _ in eng.stage_times()}
+            if semi_part:
+                assert {"part_hist", "bin_scatter", "radix_scatter"} <= names, names
+            else:
+                assert "bin_scatter" not in names and "radix_scatter" in names, names
             assert_queries_equal(eng, oix, m, t, "semi slice 1M queries")
 
 
