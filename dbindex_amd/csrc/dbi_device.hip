@@ -957,7 +957,13 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
     uint32_t H = h;
     bool ends = false;  // the walk emits nothing past H
     if (S) { H = (uint32_t)__ffsll((long long)S) - 1; ends = true; }  // protein end (:284 end < length)
-    const uint32_t xk = select_bit(V, (uint32_t)dp.max_missed + 2u);  // mc > max_missed at cuts from here (:322)
+    // mc > max_missed at cuts from here (:322): the (maxMC+2)-th cleave residue;
+    // a horizon of cleave residues only (non-specific digests): its position
+    // directly, no bit select
+    const uint32_t kmc = (uint32_t)dp.max_missed + 2u;
+    uint32_t xk;
+    if (V == hmask) xk = kmc <= h + 1u ? kmc - 1u : 64u;
+    else xk = select_bit(V, kmc);
     if (xk <= H) {  // xk >= 1
         H = xk - 1;
         ends = true;
