@@ -219,7 +219,7 @@ def main() -> None:
 
     # warmup: every stage carries HIP events in its dispatch packet -> the
     # per-kernel breakdown and the dominant kernel
-    # (the first build is cold: count + emit; the second may grow the bounded
+    # (the first build is cold: slot count + bounded digest; the second may grow the bounded
     # digest's reservation and run it twice: neither is a steady-state build).
     # The last two warmup builds already time only the dominant kernel, as the
     # timed region does: the engine captures its warm build as a hipGraph on
@@ -560,7 +560,7 @@ def cpu_baseline_legs(prm, sample) -> dict:
 
 def cold_legs(eng, prm, pp, d_res, d_off, dev: int, config: str, options=None) -> dict:
     """The one-off build (DBIndexer.java:508-684) beside the warm steady state:
-    cold_ms -- this engine forced cold (dbi_set_cold: count + emit digest,
+    cold_ms -- this engine forced cold (dbi_set_cold: slot count + bounded digest,
     radix tail, full list grids; buffers kept), best of 3; first_build_ms -- a
     fresh engine's first build (its allocations included); end_to_end -- a
     FASTA file of the proteome written to a temporary directory (untimed),
@@ -585,7 +585,7 @@ def cold_legs(eng, prm, pp, d_res, d_off, dev: int, config: str, options=None) -
         ts.append(1e3 * (time.perf_counter() - t))
     out = dict(cold_ms=min(ts), cold_ms_runs=ts, peptides=st.n_total,
                cold_peptides_per_s=st.n_total / (min(ts) * 1e-3),
-               cold_kind="dbi_set_cold on the benched engine: count + emit digest, radix tail, full list grids "
+               cold_kind="dbi_set_cold on the benched engine: slot count + bounded digest, radix tail, full list grids "
                          "(device buffers kept)")
     if st.n_total > 200_000_000:  # (semi-tryptic: a second engine's ~100 GB would not fit beside this one)
         out["first_build_ms"] = out["end_to_end"] = None

@@ -2738,22 +2738,27 @@ hipError_t launch_depth_sample(const double* d_umass, const uint32_t* d_occ_off,
 // spike -- gets a bin of its own (starts at it and after it), so a bin never
 // holds a heavy sub-bin plus its quantile's share (SwissProt: 787 -> ~420
 // depth bins above the 1 984-record chunk capacity, tools/depth_sim.py).
-// nq leaves room for the previous map's heavy sub-bins (2 starts each): the
-// bins stay <= nbins; more heavies than that only merge the top bins.
+// nq leaves room for the map's heavy sub-bins (2 starts each), counted by a
+// first pass of the same kernel (COUNT; the handle's first map had no count
+// to go by when the room came from the previous map's, and its extra starts
+// piled the top quantiles into the last bin: a region overflow at SwissProt
+// scale); the bins stay <= nbins, more heavies than that only merge the top.
+template <bool COUNT>
 __global__ void k_depth_mark(const uint32_t* __restrict__ ss, const uint32_t* __restrict__ pre, uint32_t ns,
-                             uint32_t nbins, uint32_t nsub, const uint32_t* __restrict__ prev_h,
-                             uint4* __restrict__ map, Counters* __restrict__ ctr) {
+                             uint32_t nbins, uint32_t nsub, uint4* __restrict__ map, Counters* __restrict__ ctr) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ns) return;
     const unsigned long long tot = ctr->depth_w;
     if (tot == 0) return;
-    const uint32_t hp = *prev_h;
-    const uint64_t nq = 4ull * hp <= nbins ? nbins - 2ull * hp : nbins / 2u;
     const uint32_t s = ss[i];
     auto start = [&](uint32_t b) {
         if (b > 0 && b < nsub) atomicOr(reinterpret_cast<unsigned long long*>(&map[b >> 6]), 1ull << (b & 63u));
     };
-    if (i > 0 && (uint64_t)pre[i] * nq / tot != (uint64_t)pre[i - 1] * nq / tot) start(s);
+    if (!COUNT) {
+        const uint32_t hp = ctr->depth_hc;
+        const uint64_t nq = 4ull * hp <= nbins ? nbins - 2ull * hp : nbins / 2u;
+        if (i > 0 && (uint64_t)pre[i] * nq / tot != (uint64_t)pre[i - 1] * nq / tot) start(s);
+    }
     if (i > 0 && ss[i - 1] == s) return;
     // the first sample of its sub-bin: the run's end by galloping (samples are
     // in mass order; most runs are one sample), its weight
@@ -2775,9 +2780,13 @@ __global__ void k_depth_mark(const uint32_t* __restrict__ ss, const uint32_t* __
     }
     const uint64_t w = (lo < ns ? (uint64_t)pre[lo] : tot) - pre[i];
     if (w * nbins > tot) {
-        start(s);
-        start(s + 1);
-        atomicAdd(&ctr->depth_h, 1u);
+        if (COUNT) {
+            atomicAdd(&ctr->depth_hc, 1u);
+        } else {
+            start(s);
+            start(s + 1);
+            atomicAdd(&ctr->depth_h, 1u);
+        }
     }
 }
 
@@ -2809,7 +2818,10 @@ hipError_t launch_depth_map(const uint32_t* d_ss, const uint32_t* d_pre, uint32_
                             uint4* d_map, uint32_t* d_heavy, Counters* d_ctr, hipStream_t s) {
     if (nbins == 0 || nbins > 65536u || nsub < 64 || (nsub & (nsub - 1))) return hipErrorInvalidValue;
     if (ns)  // (no sample: one bin; the regions overflow and the radix tail redoes the build)
-        DBI_LAUNCH(k_depth_mark, dim3((ns + 255) / 256), dim3(256), 0, s, d_ss, d_pre, ns, nbins, nsub, d_heavy, d_map,
+        DBI_LAUNCH(k_depth_mark<true>, dim3((ns + 255) / 256), dim3(256), 0, s, d_ss, d_pre, ns, nbins, nsub, d_map,
+                   d_ctr);
+    if (ns)
+        DBI_LAUNCH(k_depth_mark<false>, dim3((ns + 255) / 256), dim3(256), 0, s, d_ss, d_pre, ns, nbins, nsub, d_map,
                    d_ctr);
     const uint32_t G = nsub / 64;
     DBI_LAUNCH(k_depth_base<1024>, dim3((G + 1023) / 1024), dim3(1024), 0, s, d_map, G, d_heavy, d_ctr);

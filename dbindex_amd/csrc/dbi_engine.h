@@ -311,7 +311,10 @@ struct dbi_handle {
     bool opt_shard_resample = false;      // every sharded build samples its split again
     int opt_test_split_skew = -1;         // this rank's reused split is skewed (a forced resample)
     std::string opt_test_fail;            // "<phase>@<rank>": an injected local failure
-    double depth_slack = 1.25;            // region capacity / its share of the previous build's records
+    // region capacity / its share of the previous build's records (doubled after an overflow):
+    // the depth bins' regions, the semi builds' low-digit regions
+    double depth_slack = 1.25;
+    double lsd_slack = 1.25;
     uint64_t prev_unique = 0;             // uniques of the resident index (the depth map's sample)
     DevBuf<Rec> recR;                     // the digest's regions
     DevBuf<uint8_t> rdig;                 //   each record's low bin digit

@@ -170,6 +170,7 @@ struct Counters {
     unsigned long long depth_w;    // depth bins: the sampled occurrence weight (the map's total)
     unsigned int part_chunks;      // depth bins: pass-2 chunks over the digest's regions (k_part_plan)
     unsigned int depth_h;          // depth bins: heavy sub-bins of this map (k_depth_mark)
+    unsigned int depth_hc;         // depth bins: the same, from the map's counting pass (room for them)
     unsigned int n_split;          // depth bins: chunk pairs split in two (k_depth_chunks' split_list)
     // hot lines apart: the digest's per-tile ticket (every block, waits for
     // the result), and the layout word every block of every kernel reads

@@ -46,7 +46,7 @@ def test_depth_warm_builds_match_oracle(Engine, depth, reuse):
     oix = cref.Index(cp, pp.residues, pp.offsets)
     with Engine(cp, options={"depth_bins": depth, "depth_map_reuse": reuse}) as eng:
         eng.build(pp)
-        assert "bin_scatter" not in _stages(eng)  # cold: count + emit, the radix tail
+        assert "bin_scatter" not in _stages(eng)  # cold: the bounded digest's slot count, then the radix tail
         assert_index_equal(eng, oix, "cold")
         for k in range(3):
             eng.build(pp)
@@ -111,7 +111,8 @@ def test_depth_equal_mass_spikes(Engine):
 def test_options_and_cold_builds(Engine):
     """dbi_set_option refuses an unknown name or a value out of range
     (DBI_E_INVALID, the handle stays usable); dbi_set_cold makes the next build
-    a cold one (count + emit digest, the radix tail), after which warm builds
+    a cold one (the bounded digest's slot count, then its pass into exactly
+    that, and the radix tail), after which warm builds
     take depth bins again -- every build equal to the oracle."""
     from dbindex_amd._native import DBIndexStoreException
     pp = fasta.config("human").slice(0, 8000)
@@ -131,7 +132,8 @@ def test_options_and_cold_builds(Engine):
         eng.set_cold()
         eng.build(pp)
         names = _stages(eng)
-        assert "digest_count" in names and "digest_emit" in names and "bin_scatter" not in names, names
+        assert "digest_slots" in names and "digest" in names and "radix_scatter" in names, names
+        assert "bin_scatter" not in names and "digest_emit" not in names, names
         assert_index_equal(eng, oix, "cold again")
         for k in range(3):
             eng.build(pp)

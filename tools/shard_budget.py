@@ -47,7 +47,9 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-balance", action="store_true", help="record-balanced splitters on every build")
     ap.add_argument("--no-fixed", action="store_true", help="skip the one-rank fixed-cost measurement")
+    ap.add_argument("--option", action="append", default=[], help="engine option NAME=VALUE (every shard)")
     a = ap.parse_args()
+    opts = {kv.split("=", 1)[0]: int(kv.split("=", 1)[1]) for kv in a.option}
     from dbindex_amd import fasta, shard
     from dbindex_amd._native import DeviceBuffer, synchronize
     from dbindex_amd.engine import Engine
@@ -58,7 +60,7 @@ def main() -> int:
     d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), 0)
     synchronize(0)
     k = a.shards
-    engines = [Engine(cp, 0) for _ in range(k)]
+    engines = [Engine(cp, 0, options=opts) for _ in range(k)]
     ranges = shard.protein_ranges(pp.offsets, k)
     best = None
     try:
@@ -86,6 +88,7 @@ def main() -> int:
                         merge += ms
                 rows.append(dict(shard=r, proteins=int(ranges[r][1] - ranges[r][0]), digest_ms=dig,
                                  partition_ms=part, local_exchange_ms=exch, merge_ms=merge,
+                                 merge_span_ms=float(st.merge_gpu_ms),  # (device span: launch gaps inside)
                                  n_total=int(st.n_total), n_dropped=int(st.n_dropped), n_sent=int(st.n_sent),
                                  n_received=int(st.n_received),
                                  wall_digest_ms=st.digest_ms, wall_merge_ms=st.merge_ms, stages=stages,
@@ -117,7 +120,7 @@ def main() -> int:
         import time
         comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
         fixed = []
-        with Engine(cp, 0, options={"shard_full_path": 1}) as e1:
+        with Engine(cp, 0, options={"shard_full_path": 1, **opts}) as e1:
             # kernel times from timed builds, wall times from untimed ones (a
             # build with every stage timed also waits for the exchange)
             for i in range(2 * a.reps + 4):
