@@ -920,7 +920,7 @@ def trembl_issue_roofline(chunks_per_step: int, ms: float):
     chip's VALU issue peak (MI355X_MICROARCH.md: a SIMD issues a wave64 VALU
     instruction every 2 cycles)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trembl_sq.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trembl_sq.json")), key=os.path.getmtime)
     if not files:
         return None
     d = json.load(open(files[-1]))
