@@ -204,6 +204,13 @@ struct dbi_handle {
         bool valid = false;
         int32_t split[DBI_COST_BANDS - 1] = {};  // fixed key bands over [minMH, maxMH]
         double cost[DBI_COST_BANDS] = {};        // smoothed merge time per record
+        // the owner split whose slowest merge was the fastest so far, and the
+        // profile updates since one beat it: after SPLIT_TRIES the next builds
+        // keep that split (the profile's re-splits stop chasing spikes)
+        bool has_best = false;
+        int best_n = 0, since_best = 0;
+        int32_t best_split[dbi::MAX_SHARDS - 1] = {};
+        double best_max = 0.0;
     } shard_prof;
     // what a warm dbi_build_sharded reuses: the sorted sample keys of the last
     // sampled build (every rank's: all-gathered) and the split the previous

@@ -712,6 +712,8 @@ int dbi_shard_splitters_cost(const double* samples, int nshards, int32_t factor,
 namespace {
 constexpr int CB = DBI_COST_BANDS;
 constexpr double SPLIT_HOLD = 1.10;  // owners this balanced (slowest / mean merge time) keep their split
+constexpr int SPLIT_TRIES = 3;       // re-splits without a faster slowest owner: back to the best split, kept
+constexpr double SPLIT_BETTER = 0.98;  // (a split beats the best by 2 %)
 // the fixed key bands of the cost profile: CB equal key ranges of [minMH, maxMH]
 void cost_bands(const dbi_handle* h, int32_t* bsplit) {
     const double f = (double)h->params.mass_group_factor;
@@ -743,12 +745,39 @@ int dbi_shard_cost_update(dbi_handle* h, int nshards, const int32_t* split, cons
     }
     std::copy(bs, bs + CB - 1, pf.split);
     pf.valid = true;
+    // the best split so far (by its slowest owner): the same numbers on every rank
+    double mx = 0.0;
+    for (int r = 0; r < nshards; ++r) mx = std::max(mx, merge_ms[r]);
+    const bool same = pf.has_best && pf.best_n == nshards && std::equal(split, split + nshards - 1, pf.best_split);
+    if (same) {
+        pf.best_max = 0.5 * pf.best_max + 0.5 * mx;  // the best split re-measured (kept when frozen)
+    } else if (!pf.has_best || pf.best_n != nshards || mx < SPLIT_BETTER * pf.best_max) {
+        pf.has_best = true;
+        pf.best_n = nshards;
+        pf.best_max = mx;
+        std::copy(split, split + nshards - 1, pf.best_split);
+        pf.since_best = 0;
+    } else {
+        ++pf.since_best;
+    }
     return 0;
 }
+
+namespace dbi {
+// the profile's split search has stopped: the best split is kept
+bool shard_split_frozen(const dbi_handle* h, int nshards) {
+    const auto& pf = h->shard_prof;
+    return pf.valid && pf.has_best && pf.best_n == nshards && pf.since_best >= SPLIT_TRIES;
+}
+}  // namespace dbi
 
 int dbi_shard_splitters_profiled(dbi_handle* h, const double* samples, int nshards, int32_t* split) {
     if (!h) return set_error(DBI_E_INVALID, "NULL handle");
     const auto& pf = h->shard_prof;
+    if (split && nshards > 1 && dbi::shard_split_frozen(h, nshards)) {
+        std::copy(pf.best_split, pf.best_split + nshards - 1, split);
+        return 0;
+    }
     return dbi_shard_splitters_cost(samples, nshards, h->params.mass_group_factor, pf.valid ? CB : 0,
                                     pf.valid ? pf.split : nullptr, pf.valid ? pf.cost : nullptr, split);
 }
@@ -1935,6 +1964,8 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
     } else {
         if (hold)
             std::copy(sh.split, sh.split + (n - 1), wm.split);
+        else if (shard_split_frozen(h, n))  // the search stopped: the best split, kept
+            std::copy(pf.best_split, pf.best_split + (n - 1), wm.split);
         else
             split_from_keys(wm.keys, n, pf.valid ? CB : 0, pf.valid ? pf.split : nullptr, pf.valid ? pf.cost : nullptr,
                             wm.split);
