@@ -253,16 +253,17 @@ int dbi_device_view(dbi_handle* h, dbi_device_index* out);
  * every launch carries HIP start/stop events in its own dispatch packet
  * (hipExtLaunchKernelGGL on the engine stream), so timing inserts no marker
  * packets and no idle gaps between kernels.  names[i] are static strings
- * ("digest_count", "digest_emit", "radix_scatter", "chunk_sort", ...);
+ * ("digest_slots", "digest", "radix_scatter", "chunk_sort", ...);
  * ms[i] = 0 for a stage that launched nothing or with timing off;
  * bytes[i] = algorithmic HBM bytes of that launch.
  * Arrays may be NULL to query *n. */
 /* Tuning switches and test hooks of one handle -- experiments and the test
  * suite; the defaults are the measured best, and nothing is read from the
  * environment.  Integer options: "build_graph", "digest_hist",
- * "semi_bounded", "depth_bins" (0 / 1: the warm build's hipGraph, the
- * digest-counted first radix histogram of small tails, the bounded
- * semi-specific digest, depth bins); "depth_map_reuse" (1: the depth-bin map
+ * "semi_bounded", "depth_bins", "semi_part" (0 / 1: the warm build's hipGraph,
+ * the digest-counted first radix histogram of small tails, the bounded
+ * semi-specific digest, depth bins, the semi-specific digest partitioning by
+ * the first radix digit); "depth_map_reuse" (1: the depth-bin map
  * is sampled again only when the resident index changes size, 0: every
  * build); "big_split" (-1: by the list length, 0,
  * 1: the big chunk tier's two size classes); "bin_bits_max", "split_above",
@@ -276,8 +277,9 @@ int dbi_set_option_str(dbi_handle* h, const char* name, const char* value);
 
 /* The next build starts cold, as the one-off build of DBIndexer.run
  * (DBIndexer.java:508-684) does: no capacity, chunk-list grids, depth-bin map
- * or build graph carried over from earlier builds (count + emit digest, the
- * radix tail), but the device buffers are kept -- the cold pipeline timed
+ * or build graph carried over from earlier builds (the bounded digest's slot
+ * count then its pass -- count + emit for the other digests -- and the radix
+ * tail), but the device buffers are kept -- the cold pipeline timed
  * without its allocations (bench.py cold_ms). */
 int dbi_set_cold(dbi_handle* h);
 
