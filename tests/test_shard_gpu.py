@@ -353,6 +353,56 @@ def test_sharded_cost_profile_splitters(native):
             e.close()
 
 
+def test_split_search_stops_at_the_best_split(native):
+    """The cost profile remembers the split whose slowest owner merge was the
+    fastest (dbi_shard_cost_update); after three re-splits that do not beat it
+    by 2 %, dbi_shard_splitters_profiled returns that split whatever the
+    profile says -- the same rule dbi_build_sharded applies to its warm split.
+    Then eight real sharded builds, balance on: every one equals the oracle."""
+    import ctypes
+    from dbindex_amd._native import SHARD_SAMPLES, check, lib
+    from dbindex_amd.engine import Engine
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    n = 4
+    f = cp.mass_group_factor
+    masses = np.linspace(600.0, 5000.0, SHARD_SAMPLES)
+    samples = np.concatenate([np.concatenate([masses, [1.0]]) for _ in range(n)]).astype(np.float64)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    recs = np.full(n, 1000, np.uint64)
+    with Engine(cp, 0) as eng:
+        L = lib()
+
+        def profiled():
+            out = np.zeros(n, np.int32)
+            check(L.dbi_shard_splitters_profiled(eng.h, p(samples), n, p(out)))
+            return out[: n - 1].copy()
+
+        best = np.array([int(1500 * f), int(2500 * f), int(3500 * f)], np.int32)
+        splits = [best, best + 10, best + 20, best + 30]
+        times = [[1.0, 1.0, 1.0, 1.0], [2.0, 1.0, 1.0, 1.0], [1.0, 1.9, 1.0, 1.0], [1.0, 1.0, 3.0, 1.0]]
+        for sp, ms in zip(splits, times):
+            sp_full = np.concatenate([sp, [0]]).astype(np.int32)
+            check(L.dbi_shard_cost_update(eng.h, n, p(sp_full), p(np.array(ms, np.float64)), p(recs)))
+        assert np.array_equal(profiled(), best)  # three re-splits no faster: the best split, kept
+        # the best split measured again (slower this time) does not restart the search
+        check(L.dbi_shard_cost_update(eng.h, n, p(np.concatenate([best, [0]]).astype(np.int32)),
+                                      p(np.array([1.5, 1.0, 1.0, 1.0], np.float64)), p(recs)))
+        assert np.array_equal(profiled(), best)
+    pp = fasta.config("human").slice(0, 6000)
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    d_res, d_off = _inputs(native, pp)
+    ranges = shard.protein_ranges(pp.offsets, 4)
+    engines = [Engine(cp, 0) for _ in range(4)]
+    try:
+        for rep in range(8):
+            shard.build_sharded_local(engines, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, ranges,
+                                      balance=True)
+            _assert_sharded_equal(engines, oix, f"split search [{rep}]")
+    finally:
+        for e in engines:
+            e.close()
+
+
 def test_sharded_local_merge_graph_replays(native):
     """Untimed repeated builds: each owner's merge is enqueued (build 0),
     captured as a hipGraph (build 1, the same merge again) and replayed (builds
