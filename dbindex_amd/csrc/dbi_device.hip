@@ -1471,8 +1471,8 @@ k_digest_semi_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const
         if (tk) atomicAdd(&d_ctr->n_kept, (unsigned long long)tk);
         if (td) atomicAdd(&d_ctr->n_dropped, (unsigned long long)td);
     }
-    if constexpr (PART) {  // the walks' LDS is dead: the counters in the mass table, the stage over window + candidates
-        constexpr size_t b0 = offsetof(DigestSmem, win), b1 = offsetof(DigestSmem, tmp);
+    if constexpr (PART) {  // the walks' LDS is dead: the counters in the mass table, the stage over the rest
+        constexpr size_t b0 = offsetof(DigestSmem, nokm), b1 = offsetof(DigestSmem, tmp);
         constexpr uint32_t R = (uint32_t)((b1 - b0) / 18 / 64 * 64);  // 16 B + 2 B per staged record
         static_assert(b0 % 16 == 0 && R >= 512 && sizeof(sm.mass) >= 512 * sizeof(uint32_t), "partition stage");
         uint8_t* st = reinterpret_cast<uint8_t*>(&sm) + b0;
