@@ -381,14 +381,43 @@ __device__ __forceinline__ WalkOut walk_lds(const DevParams& dp, const DigestSme
     return r;
 }
 
+// Where walk_global's records go: sink(k, m, tag, len) for its k-th kept one.
+struct RecSink {  // 16-B records at out[k] (below out_end)
+    Rec* __restrict__ out;
+    const Rec* out_end;
+    uint64_t loc;
+    __device__ __forceinline__ void operator()(uint32_t k, double m, uint32_t tag, uint32_t len) const {
+        Rec rec;
+        rec.q0 = rec_q0(m, tag);
+        rec.q1 = rec_q1(tag, loc, len);
+        if (out + k < out_end) out[k] = rec;
+    }
+};
+
 // The same loop reading residues from HBM (walks that run past the staged
 // window, e.g. through zero-mass residues): flags from the residue tables,
 // the cut from the next residue and the protein end pe.
+template <bool EMIT, bool SEMI, bool MAND, bool HIST = false, typename Sink = RecSink>
+__device__ WalkOut walk_global_to(const DevParams& dp, const double* __restrict__ s_mass,
+                                  const uint8_t* __restrict__ s_flags, const uint8_t* __restrict__ g_res,
+                                  uint32_t s, uint32_t pe, bool n_ok, const Sink& sink, uint32_t* hist = nullptr,
+                                  uint32_t hist_from = 0);
+
 template <bool EMIT, bool SEMI, bool MAND, bool HIST = false>
-__device__ WalkOut walk_global(const DevParams& dp, const double* __restrict__ s_mass,
-                               const uint8_t* __restrict__ s_flags, const uint8_t* __restrict__ g_res,
-                               uint32_t s, uint32_t pe, bool n_ok, uint64_t loc, Rec* __restrict__ out,
-                               const Rec* out_end, uint32_t* hist = nullptr, uint32_t hist_from = 0) {
+__device__ __forceinline__ WalkOut walk_global(const DevParams& dp, const double* __restrict__ s_mass,
+                                               const uint8_t* __restrict__ s_flags, const uint8_t* __restrict__ g_res,
+                                               uint32_t s, uint32_t pe, bool n_ok, uint64_t loc,
+                                               Rec* __restrict__ out, const Rec* out_end, uint32_t* hist = nullptr,
+                                               uint32_t hist_from = 0) {
+    return walk_global_to<EMIT, SEMI, MAND, HIST>(dp, s_mass, s_flags, g_res, s, pe, n_ok, RecSink{out, out_end, loc},
+                                                  hist, hist_from);
+}
+
+template <bool EMIT, bool SEMI, bool MAND, bool HIST, typename Sink>
+__device__ WalkOut walk_global_to(const DevParams& dp, const double* __restrict__ s_mass,
+                                  const uint8_t* __restrict__ s_flags, const uint8_t* __restrict__ g_res,
+                                  uint32_t s, uint32_t pe, bool n_ok, const Sink& sink, uint32_t* hist,
+                                  uint32_t hist_from) {
     WalkOut r{0u, 0u, false};
     double m = dp.m0;
     if (!(m <= dp.max_mh)) return r;
@@ -418,13 +447,7 @@ __device__ WalkOut walk_global(const DevParams& dp, const double* __restrict__ s
         }
         const bool drop = emit && m >= dp.drop_mass;
         const bool keep = emit && !drop && (!dp.filter || in_windows(dp, m));
-        if (EMIT && keep) {
-            const uint32_t tag = peptide_tag(head, tail, e - s + 1);
-            Rec rec;
-            rec.q0 = rec_q0(m, tag);
-            rec.q1 = rec_q1(tag, loc, e - s + 1);
-            if (out + kept < out_end) out[kept] = rec;
-        }
+        if (EMIT && keep) sink(kept, m, peptide_tag(head, tail, e - s + 1), e - s + 1);
         if (HIST && (keep || drop) && e >= hist_from) hist_add(dp, hist, m);
         kept += keep;
         dropped += drop;
@@ -1542,23 +1565,43 @@ constexpr int LD_WIN = 32 + LD_PRE + DIGEST_TILE + LD_HALO;  // + lb (16 + align
 constexpr int LD_WORDS = LD_WIN / 64 + 2;
 constexpr int LD_ENDS = 4;                          // candidate ends of one start, at most (maxMC + 2)
 
-struct LeanSmem {
+template <uint32_t POOL>
+struct LeanSmemT {
     double mass[256];
-    uint64_t clvm[LD_WORDS];  // bit q: cleave residue at LDS position q
+    uint32_t tmp[DIGEST_THREADS / 64 + 1];
+    alignas(16) uint64_t clvm[LD_WORDS];  // bit q: cleave residue at LDS position q
     uint64_t cutm[LD_WORDS];  // bit q: checkCleavage's C side holds at q (protein ends included)
     uint64_t stm[LD_WORDS];   // bit q: a protein starts at q (one past the window included)
     uint32_t pst[PST_CAP];    // poff[pf .. pl+1] (protein of a start: binary search)
     uint16_t wpre[LD_WORDS];  // protein starts marked in stm words before word w
     alignas(16) uint8_t win[LD_WIN + 16];
     uint8_t flags[256];
-    alignas(8) uint16_t cand[DIGEST_TILE];  // candidate starts (tile-local), compacted, then balanced
-    // the masses at a walk's candidate ends, [end][thread]; before the walks:
-    // the no-cut and N_ok maps and the balance counts
-    double endm[LD_ENDS][DIGEST_THREADS];
-    uint32_t tmp[DIGEST_THREADS / 64 + 1];
+    // the candidate starts (u16, tile-local, compacted, then balanced), then
+    // the walks' scratch: the masses at a walk's candidate ends ([end][thread],
+    // endm()), or -- a staged PART tile -- the tile's records; before the
+    // walks the no-cut and N_ok maps and the balance counts (behind the list)
+    alignas(16) uint8_t pool[POOL];
+    __device__ __forceinline__ uint16_t* cand() { return reinterpret_cast<uint16_t*>(pool); }
+    __device__ __forceinline__ const uint16_t* cand() const { return reinterpret_cast<const uint16_t*>(pool); }
+    __device__ __forceinline__ double* endm() { return reinterpret_cast<double*>(pool + 2 * DIGEST_TILE); }
+    __device__ __forceinline__ const double* endm() const {
+        return reinterpret_cast<const double*>(pool + 2 * DIGEST_TILE);
+    }
 };
+constexpr uint32_t LD_POOL = 2 * DIGEST_TILE + LD_ENDS * DIGEST_THREADS * 8;
+using LeanSmem = LeanSmemT<LD_POOL>;
 static_assert((2 * LD_WORDS * 8 + 4 * BAL_BUCKETS) <= LD_ENDS * DIGEST_THREADS * 8, "scratch inside endm");
 static_assert(LD_ENDS * DIGEST_THREADS * 8 % 16 == 0, "endm layout");
+// The partitioning digest (PART) keeps a tile's records in LDS while they are
+// written (stage mode, below): its pool takes every byte up to 26 KiB a block
+// (6 blocks per CU, the occupancy of the plain digest), so a tile of ~1 100
+// records (SwissProt: 1 106 on average, 1 302 at most) fits beside the list of
+// its ~460 candidate starts at 12 B a record.
+constexpr uint32_t LD_LDS_PART = 26624;
+constexpr uint32_t LD_HEAD = (uint32_t)sizeof(LeanSmemT<16>) - 16u;
+constexpr uint32_t LD_POOL_PART = (LD_LDS_PART - LD_HEAD - 64u) & ~15u;
+using LeanSmemP = LeanSmemT<LD_POOL_PART>;
+static_assert(LD_POOL_PART >= LD_POOL, "the PART pool holds the plain one");
 
 // Protein of start s: largest p in [pf, pl] with poff[p] <= s (LDS copy of
 // the tile's offsets, HBM when they did not fit), and its first residue.
@@ -1586,7 +1629,8 @@ struct LeanEnds {
 
 // known: last LDS position whose cut bit is known (the window's last one only
 // at the end of the residues)
-__device__ __forceinline__ LeanEnds lean_ends(const LeanSmem& sm, uint32_t p, uint32_t known, uint32_t kcl,
+template <typename SM>
+__device__ __forceinline__ LeanEnds lean_ends(const SM& sm, uint32_t p, uint32_t known, uint32_t kcl,
                                               uint32_t min_len) {
     const uint64_t cl0 = bits_from(sm.clvm, p), cl1 = bits_from(sm.clvm, p + 64);
     const uint64_t st0 = bits_from(sm.stm, p) & ~1ull, st1 = bits_from(sm.stm, p + 64);
@@ -1615,7 +1659,10 @@ struct LeanWalk {
     bool overflow;   // the walk goes on past the horizon: redo it with walk_global
 };
 
-__device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, LeanSmem& sm, uint32_t p, const LeanEnds& en) {
+// em[k * es]: where the mass at the walk's k-th listed end is parked
+template <typename SM>
+__device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, const SM& sm, uint32_t p, const LeanEnds& en,
+                                                double* __restrict__ em, uint32_t es) {
     LeanWalk w{~0u, 0u, 0u, false};
     double m = dp.m0;
     if (!(m <= dp.max_mh)) return w;  // while condition before the first residue (:284)
@@ -1652,7 +1699,6 @@ __device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, LeanSmem& s
     // [q, q+4): the list is ascending and 0xFF-padded, q + 4 <= 132).
     // Positions past `last` (at most 3) only add to a mass that is no longer used.
     const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(sm.win);
-    double* __restrict__ em = &sm.endm[0][threadIdx.x];
     uint32_t ne = pk & 0xFFu, rest = pk, j = 0;
     for (uint32_t q = 0; q <= last; q += 4) {
         const uint32_t a = p + q;
@@ -1662,7 +1708,7 @@ __device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, LeanSmem& s
         const double m0 = m + x0, m1 = m0 + x1, m2 = m1 + x2, m3 = m2 + x3;
         while (ne < q + 4u) {
             const uint32_t d = ne - q;
-            em[j * DIGEST_THREADS] = d == 0u ? m0 : d == 1u ? m1 : d == 2u ? m2 : m3;
+            em[j * es] = d == 0u ? m0 : d == 1u ? m1 : d == 2u ? m2 : m3;
             ++j;
             rest = (rest >> 8) | 0xFF000000u;  // 0xFF past the list
             ne = rest & 0xFFu;
@@ -1672,7 +1718,7 @@ __device__ __forceinline__ LeanWalk lean_masses(const DevParams& dp, LeanSmem& s
     }
     w.j = j;
     // still <= maxMH at the horizon: the walk goes on past it
-    w.overflow = en.open && j == nlist && em[(nlist - 1) * DIGEST_THREADS] <= dp.max_mh;
+    w.overflow = en.open && j == nlist && em[(nlist - 1) * es] <= dp.max_mh;
     return w;
 }
 
@@ -1699,18 +1745,17 @@ __device__ __forceinline__ void hist1_count(const Hist1& h1, uint32_t* s_h1, uin
 
 // The records of a lean walk (not overflowed) into out[0, kept); slot: the
 // global slot of out[0] (first-pass histogram, when h1.g is set).
-template <bool DROP, bool H1>
-__device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const LeanSmem& sm, uint32_t p, const LeanWalk& w,
-                                             uint64_t loc, Rec* __restrict__ out, const Hist1& h1, uint32_t* s_h1,
-                                             uint32_t c0, uint32_t slot) {
+template <bool DROP, bool H1, typename SM>
+__device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const SM& sm, uint32_t p, const LeanWalk& w,
+                                             const double* __restrict__ em, uint64_t loc, Rec* __restrict__ out,
+                                             const Hist1& h1, uint32_t* s_h1, uint32_t c0, uint32_t slot) {
     WalkOut r{0u, 0u, false};
     const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(sm.win);
-    const double* __restrict__ em = &sm.endm[0][threadIdx.x];
     const uint32_t head = __builtin_amdgcn_alignbyte(w32[(p >> 2) + 1], w32[p >> 2], p & 3u);
     uint32_t kept = 0, dropped = 0;
     const uint32_t nk = min(w.j, w.nreal);
     for (uint32_t k = 0; k < nk; ++k) {
-        const double mk = em[k * DIGEST_THREADS];
+        const double mk = em[k * DIGEST_THREADS];  // (lean_masses' es)
         if (!(mk <= dp.max_mh)) break;
         if (!(mk >= dp.min_mh)) continue;  // :331
         if (DROP && mk >= dp.drop_mass) {  // bucket > NUM_BUCKETS-1
@@ -1731,6 +1776,49 @@ __device__ __forceinline__ WalkOut lean_emit(const DevParams& dp, const LeanSmem
     r.dropped = dropped;
     return r;
 }
+
+// A staged PART tile (k_digest_bounded, stage mode): a record waits in LDS
+// as 12 B -- its mass and (candidate index << STAGE_LEN_BITS | length) --
+// until the tile is partitioned; the tag, protein and offset are rebuilt
+// from the window there.  The walk's end masses are parked in the record
+// slots themselves (em, stride 1), and lean_stage compacts the kept ones to
+// the front of them.
+constexpr uint32_t STAGE_LEN_BITS = 20;  // lengths < 2^20 (max_plen checked per tile)
+constexpr uint32_t STAGE_NONE = ~0u;     // an unused slot of the tile's bound
+
+template <bool DROP>
+__device__ __forceinline__ WalkOut lean_stage(const DevParams& dp, const LeanWalk& w, double* __restrict__ em,
+                                              uint32_t* __restrict__ ei, uint32_t j) {
+    WalkOut r{0u, 0u, false};
+    uint32_t kept = 0, dropped = 0;
+    const uint32_t nk = min(w.j, w.nreal);
+    for (uint32_t k = 0; k < nk; ++k) {
+        const double mk = em[k];
+        if (!(mk <= dp.max_mh)) break;
+        if (!(mk >= dp.min_mh)) continue;  // :331
+        if (DROP && mk >= dp.drop_mass) {  // bucket > NUM_BUCKETS-1
+            ++dropped;
+            continue;
+        }
+        em[kept] = mk;
+        ei[kept++] = j << STAGE_LEN_BITS | (((w.pk >> (8 * k)) & 0xFFu) + 1u);
+    }
+    r.kept = kept;
+    r.dropped = dropped;
+    return r;
+}
+
+struct StageSink {  // walk_global's records of a staged tile
+    double* __restrict__ em;
+    uint32_t* __restrict__ ei;
+    uint32_t j, room;
+    __device__ __forceinline__ void operator()(uint32_t k, double m, uint32_t, uint32_t len) const {
+        if (k < room) {
+            em[k] = m;
+            ei[k] = j << STAGE_LEN_BITS | len;
+        }
+    }
+};
 
 // ---- depth bins: the digest's partition ------------------------------------
 __device__ __forceinline__ uint32_t depth_bin(double m, const DepthMap& dm) {
@@ -1765,17 +1853,74 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // digest 24.1 -> 25.8 ms), and loading the next round's records while one is
 // written (24.8 ms): the partition moves its bytes (the slots read back, the
 // regions written) at about the copy rate.
-template <uint32_t R>
-__device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32_t n, uint32_t* s_cnt,
-                          uint32_t* s_run, uint32_t* s_tmp, uint4* stage, uint16_t* sdig, Counters* __restrict__ ctr) {
-    constexpr uint32_t KI = (R + DIGEST_THREADS - 1) / DIGEST_THREADS;
+// One round: rv[k] = record k * DIGEST_THREADS + tid of the round (nr of
+// them; REC_SENTINEL q0: none), s_cnt zeroed behind a barrier the caller put
+// after its last read of the stage.
+template <uint32_t KI>
+__device__ __forceinline__ void part_place(const PartOut& po, const uint4 (&rv)[KI], uint32_t nr, uint32_t* s_cnt,
+                                           uint32_t* s_run, uint32_t* s_tmp, uint4* stage, uint16_t* sdig,
+                                           Counters* __restrict__ ctr) {
     const uint32_t tid = threadIdx.x, xcd = xcc_id(), D1 = 1u << po.b1;
     const uint32_t b2 = po.dm.b2, m2 = (1u << b2) - 1u;
     // the region digit of a bin (depth: its high b1 bits; lsd: its low b1 bits) and its pass-2 digit
     auto d1_of = [&](uint32_t b) { return po.lsd ? b & (D1 - 1u) : b >> b2; };
     auto d2_of = [&](uint32_t b) { return po.lsd ? (b >> po.b1) & m2 : b & m2; };
-    const uint4* __restrict__ src4 = reinterpret_cast<const uint4*>(src);
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(po.recs);
+    uint32_t bin[KI], rk[KI];
+#pragma unroll
+    for (uint32_t k = 0; k < KI; ++k) {
+        bin[k] = ~0u;
+        rk[k] = 0;
+        if (k * DIGEST_THREADS + tid < nr && (rv[k].x & rv[k].y) != 0xFFFFFFFFu) {  // not a sentinel
+            bin[k] = po.lsd ? bin_of(u4_mass(rv[k]), po.lin) : depth_bin(u4_mass(rv[k]), po.dm);
+            rk[k] = atomicAdd(&s_cnt[d1_of(bin[k])], 1u);
+        }
+    }
+    __syncthreads();
+    // digit d's run: stage[lstart, lstart + c), region cursor o -> out[region(d) + o + (t - lstart)]
+    const uint32_t c = tid < D1 ? s_cnt[tid] : 0u;
+    uint32_t nvalid;
+    const uint32_t lstart = block_excl_scan<DIGEST_THREADS, uint32_t>(c, s_tmp, nvalid);
+    if (tid < D1) {
+        uint32_t g = ~0u;
+        if (c) {
+            // the cursor is this XCD's alone (its own 1-KiB row, cur[xcd][digit]): the add runs in
+            // this XCD's L2 (workgroup scope: no trip to the memory-side atomics); the kernel's end
+            // writes it back.  A wrong XCD id would lose adds: k_part_plan checks the cursors' sum.
+            const uint32_t o = __hip_atomic_fetch_add(&po.cur[xcd * 256u + tid], c, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (o + c <= po.cap) g = (tid * DEPTH_XCDS + xcd) * po.cap + o - lstart;
+            else atomicOr(&ctr->err, ERR_PART);
+        }
+        s_run[tid] = g;
+        s_cnt[tid] = lstart;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < KI; ++k) {
+        if (bin[k] != ~0u) {
+            const uint32_t at = s_cnt[d1_of(bin[k])] + rk[k];
+            stage[at] = rv[k];
+            sdig[at] = (uint16_t)(d1_of(bin[k]) << 8 | d2_of(bin[k]));
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < nvalid; t += DIGEST_THREADS) {
+        const uint32_t bb = sdig[t];
+        const uint32_t g = s_run[bb >> 8];
+        if (g != ~0u) {
+            out4[g + t] = stage[t];
+            po.dig[g + t] = (uint8_t)(bb & 0xFFu);
+        }
+    }
+}
+
+template <uint32_t R>
+__device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32_t n, uint32_t* s_cnt,
+                          uint32_t* s_run, uint32_t* s_tmp, uint4* stage, uint16_t* sdig, Counters* __restrict__ ctr) {
+    constexpr uint32_t KI = (R + DIGEST_THREADS - 1) / DIGEST_THREADS;
+    const uint32_t tid = threadIdx.x;
+    const uint4* __restrict__ src4 = reinterpret_cast<const uint4*>(src);
     // every record of the tile acknowledged by the L2 before the barrier: the
     // other waves read the slots back (from the L2: the lines were never in
     // this CU's L1).  (__threadfence() would write the L2 back to HBM per tile.)
@@ -1789,53 +1934,7 @@ __device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32
         for (uint32_t k = 0; k < KI; ++k)  // clamped: every load in flight together
             rv[k] = src4[r0 + min(k * DIGEST_THREADS + tid, nr - 1u)];
         __syncthreads();
-        uint32_t bin[KI], rk[KI];
-#pragma unroll
-        for (uint32_t k = 0; k < KI; ++k) {
-            bin[k] = ~0u;
-            rk[k] = 0;
-            if (k * DIGEST_THREADS + tid < nr && (rv[k].x & rv[k].y) != 0xFFFFFFFFu) {  // not a sentinel
-                bin[k] = po.lsd ? bin_of(u4_mass(rv[k]), po.lin) : depth_bin(u4_mass(rv[k]), po.dm);
-                rk[k] = atomicAdd(&s_cnt[d1_of(bin[k])], 1u);
-            }
-        }
-        __syncthreads();
-        // digit d's run: stage[lstart, lstart + c), region cursor o -> out[region(d) + o + (t - lstart)]
-        const uint32_t c = tid < D1 ? s_cnt[tid] : 0u;
-        uint32_t nvalid;
-        const uint32_t lstart = block_excl_scan<DIGEST_THREADS, uint32_t>(c, s_tmp, nvalid);
-        if (tid < D1) {
-            uint32_t g = ~0u;
-            if (c) {
-                // the cursor is this XCD's alone (its own 1-KiB row, cur[xcd][digit]): the add runs in
-                // this XCD's L2 (workgroup scope: no trip to the memory-side atomics); the kernel's end
-                // writes it back.  A wrong XCD id would lose adds: k_part_plan checks the cursors' sum.
-                const uint32_t o = __hip_atomic_fetch_add(&po.cur[xcd * 256u + tid], c, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (o + c <= po.cap) g = (tid * DEPTH_XCDS + xcd) * po.cap + o - lstart;
-                else atomicOr(&ctr->err, ERR_PART);
-            }
-            s_run[tid] = g;
-            s_cnt[tid] = lstart;
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t k = 0; k < KI; ++k) {
-            if (bin[k] != ~0u) {
-                const uint32_t at = s_cnt[d1_of(bin[k])] + rk[k];
-                stage[at] = rv[k];
-                sdig[at] = (uint16_t)(d1_of(bin[k]) << 8 | d2_of(bin[k]));
-            }
-        }
-        __syncthreads();
-        for (uint32_t t = tid; t < nvalid; t += DIGEST_THREADS) {
-            const uint32_t bb = sdig[t];
-            const uint32_t g = s_run[bb >> 8];
-            if (g != ~0u) {
-                out4[g + t] = stage[t];
-                po.dig[g + t] = (uint8_t)(bb & 0xFFu);
-            }
-        }
+        part_place<KI>(po, rv, nr, s_cnt, s_run, s_tmp, stage, sdig, ctr);
     }
 }
 
@@ -1848,7 +1947,8 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
                  const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
                  uint32_t n_res, const uint32_t* __restrict__ d_tile_pf, Rec* __restrict__ d_out, uint64_t cap,
                  Counters* __restrict__ d_ctr, Hist1 h1, PartOut po) {
-    __shared__ LeanSmem sm;
+    using SM = std::conditional_t<PART, LeanSmemP, LeanSmem>;
+    __shared__ SM sm;
     __shared__ uint32_t s_kept, s_waves, s_dup;
     __shared__ unsigned long long s_base;
     __shared__ uint32_t s_h1[H1 ? H1_LDS : 1];
@@ -1908,9 +2008,10 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     }
     const uint32_t np_all = pl - pf + 2;
     const uint32_t npst = np_all <= PST_CAP ? np_all : 0u;
-    uint64_t* nocm = reinterpret_cast<uint64_t*>(&sm.endm[0][0]);  // scratch until the walks
+    uint64_t* nocm = reinterpret_cast<uint64_t*>(sm.endm());  // scratch until the walks
     uint64_t* nokm = nocm + LD_WORDS;
     uint32_t* s_cnt = reinterpret_cast<uint32_t*>(nokm + LD_WORDS);
+    uint16_t* cand = sm.cand();
     __syncthreads();
     // window -> LDS, cleave / no-cut flags -> 16-bit slices of the bit maps
     // (every slice written: zeros past the window); protein starts
@@ -1997,15 +2098,16 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     uint32_t pos = block_excl_scan<DIGEST_THREADS, uint32_t>((uint32_t)__popc(mybits), sm.tmp, ncand);
 #pragma unroll
     for (int k = 0; k < STARTS_PER_THREAD; ++k)
-        if (mybits & (1u << k)) sm.cand[pos++] = (uint16_t)(tid * STARTS_PER_THREAD + k);
+        if (mybits & (1u << k)) cand[pos++] = (uint16_t)(tid * STARTS_PER_THREAD + k);
     __syncthreads();
 
     const uint32_t B = (uint32_t)dp.max_missed + 2u;  // records per start, at most
     const uint32_t min_len = (uint32_t)dp.min_len;
     const uint32_t known = w_end == n_res ? lend - 1u : lend - 2u;
-    const uint32_t w = rec_width(d_ctr->max_plen);
+    const uint32_t max_plen = d_ctr->max_plen;
+    const uint32_t w = rec_width(max_plen);
     if (tile == 0 && tid == 0 && !rec_layout_ok(w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
-    balance_candidates(sm.cand, s_cnt, ncand, B, t_end - t0);
+    balance_candidates(cand, s_cnt, ncand, B, t_end - t0);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
     // slot bounds: the candidate ends (B for a walk that may leave the horizon);
@@ -2014,7 +2116,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     uint32_t lim = 0;
     LeanEnds en0{0ull, 0ull, 0u, false}, en1{0ull, 0ull, 0u, false};
     for (uint32_t j = jb; j < je; ++j) {
-        const LeanEnds en = lean_ends(sm, off + sm.cand[j], known, B, min_len);
+        const LeanEnds en = lean_ends(sm, off + cand[j], known, B, min_len);
         if (j == jb) en0 = en;
         else if (j == jb + 1) en1 = en;
         lim += en.open ? B : (uint32_t)(__popcll(en.lo) + __popcll(en.hi));
@@ -2031,36 +2133,75 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
     Rec* __restrict__ o = d_out + base + excl_t;
     const uint32_t c0 = (uint32_t)(base / RADIX_CHUNK_D);
-    uint32_t kept = 0, dropped = 0;
-    for (uint32_t j = jb; j < je; ++j) {
-        const uint32_t p = off + sm.cand[j];
-        const uint32_t s = w0 + (p - lb);
-        const LeanWalk lw =
-            lean_masses(dp, sm, p, j == jb ? en0 : j == jb + 1 ? en1 : lean_ends(sm, p, known, B, min_len));
-        uint32_t pstart, pid;
+    // the protein of the start at LDS position p (global index s) and its first residue
+    auto protein_at = [&](uint32_t p, uint32_t s, uint32_t& pstart) {
+        uint32_t pid;
         if (pid_map) {
             pid = pid_base + sm.wpre[p >> 6] + (uint32_t)__popcll(sm.stm[p >> 6] & low_bits((p & 63u) + 1u));
             pstart = sm.pst[pid - pf];
         } else {
             pid = protein_of(sm.pst, npst, pf, pl, d_poff, s, pstart);
         }
-        const uint64_t loc = rec_loc(pid, s - pstart, w);
+        return pid;
+    };
+    // PART stage mode (block-uniform): the tile's records stay in LDS, 12 B
+    // each behind the candidate list (smass / sinfo, slot excl_t + k of each
+    // thread as in d_out), until part_place writes them into the regions --
+    // no slot of d_out is written or read back.  A tile whose slot bound does
+    // not fit (or a proteome with proteins of 2^20 residues) takes the slots.
+    constexpr uint32_t PR = PART ? (uint32_t)((sizeof(SM) - offsetof(SM, clvm)) / 18 / 64 * 64) : 64u;
+    bool stage = false;
+    double* smass = nullptr;
+    uint32_t* sinfo = nullptr;
+    if constexpr (PART) {
+        const uint32_t c16 = (2u * ncand + 15u) & ~15u;
+        const uint32_t room = (LD_POOL_PART - c16) / 12u;
+        stage = po.stage && tile_slots <= min(room, PR) && (max_plen >> STAGE_LEN_BITS) == 0;
+        smass = reinterpret_cast<double*>(sm.pool + c16);
+        sinfo = reinterpret_cast<uint32_t*>(sm.pool + c16 + 8u * room);
+    }
+    uint32_t kept = 0, dropped = 0;
+    for (uint32_t j = jb; j < je; ++j) {
+        const uint32_t p = off + cand[j];
+        const uint32_t s = w0 + (p - lb);
+        double* em = PART && stage ? smass + excl_t + kept : sm.endm() + tid;
+        const LeanWalk lw = lean_masses(dp, sm, p, j == jb ? en0 : j == jb + 1 ? en1 : lean_ends(sm, p, known, B, min_len),
+                                        em, PART && stage ? 1u : (uint32_t)DIGEST_THREADS);
         WalkOut wo;
-        if (lw.overflow) {
-            const uint32_t pe = d_poff[pid + 1];
-            wo = walk_global<true, false, false>(dp, sm.mass, sm.flags, d_res, s, pe, true, loc, o + kept, o + lim);
-            if constexpr (H1)  // rare: the records it wrote, read back
-                for (uint32_t k = kept; k < kept + wo.kept; ++k)
-                    hist1_count(h1, s_h1, c0, q0_mass(o[k].q0), (uint32_t)base + excl_t + k);
+        if (PART && stage) {
+            if (lw.overflow) {
+                uint32_t pstart;
+                const uint32_t pe = d_poff[protein_at(p, s, pstart) + 1];
+                wo = walk_global_to<true, false, false>(dp, sm.mass, sm.flags, d_res, s, pe, true,
+                                                        StageSink{em, sinfo + excl_t + kept, j, lim - kept});
+            } else {
+                wo = lean_stage<DROP>(dp, lw, em, sinfo + excl_t + kept, j);
+            }
         } else {
-            wo = lean_emit<DROP, H1>(dp, sm, p, lw, loc, o + kept, h1, s_h1, c0, (uint32_t)base + excl_t + kept);
+            uint32_t pstart;
+            const uint32_t pid = protein_at(p, s, pstart);
+            const uint64_t loc = rec_loc(pid, s - pstart, w);
+            if (lw.overflow) {
+                const uint32_t pe = d_poff[pid + 1];
+                wo = walk_global<true, false, false>(dp, sm.mass, sm.flags, d_res, s, pe, true, loc, o + kept, o + lim);
+                if constexpr (H1)  // rare: the records it wrote, read back
+                    for (uint32_t k = kept; k < kept + wo.kept; ++k)
+                        hist1_count(h1, s_h1, c0, q0_mass(o[k].q0), (uint32_t)base + excl_t + k);
+            } else {
+                wo = lean_emit<DROP, H1>(dp, sm, p, lw, em, loc, o + kept, h1, s_h1, c0,
+                                         (uint32_t)base + excl_t + kept);
+            }
         }
         kept += wo.kept;
         dropped += wo.dropped;
     }
     if (kept > lim) atomicOr(&d_ctr->err, ERR_SLOTS);  // the bound is an upper bound: never
-    const Rec sent{REC_SENTINEL, REC_SENTINEL};
-    for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
+    if (PART && stage) {
+        for (uint32_t k = kept; k < lim; ++k) sinfo[excl_t + k] = STAGE_NONE;
+    } else {
+        const Rec sent{REC_SENTINEL, REC_SENTINEL};
+        for (uint32_t k = kept; k < lim; ++k) o[k] = sent;
+    }
     bool flush;
     if (DROP) {
         const uint32_t tk = block_sum<DIGEST_THREADS, uint32_t>(kept, sm.tmp);
@@ -2095,13 +2236,51 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
         }
     }
     if constexpr (PART) {  // the walks' LDS is dead: the partition's counters and stage
-        constexpr size_t b0 = offsetof(LeanSmem, clvm), b1 = offsetof(LeanSmem, tmp);
-        constexpr uint32_t R = (uint32_t)((b1 - b0) / 18 / 64 * 64);  // 16 B + 2 B per staged record
-        static_assert(b0 % 16 == 0 && R >= 1024, "partition stage");
+        constexpr size_t b0 = offsetof(SM, clvm);
+        static_assert(b0 % 16 == 0 && PR >= 1024, "partition stage");
         uint8_t* st = reinterpret_cast<uint8_t*>(&sm) + b0;
         uint32_t* p_cnt = reinterpret_cast<uint32_t*>(sm.mass);
-        part_tile<R>(po, d_out + base, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
-                     reinterpret_cast<uint16_t*>(st + 16 * R), d_ctr);
+        if (stage) {
+            // every record rebuilt from its 12 B and the window: the tag from the
+            // peptide's end bytes (HBM past the window: walk_global's long ones),
+            // the protein and offset from the start's candidate index
+            constexpr uint32_t KS = (PR + DIGEST_THREADS - 1) / DIGEST_THREADS;
+            __syncthreads();  // every walk's records staged, the walks' mass-table reads done
+            p_cnt[tid] = 0;
+            const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(sm.win);
+            uint4 rr[KS];
+#pragma unroll
+            for (uint32_t k = 0; k < KS; ++k) {
+                const uint32_t i = k * DIGEST_THREADS + tid;
+                rr[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                const uint32_t info = i < tile_slots ? sinfo[i] : STAGE_NONE;
+                if (info != STAGE_NONE) {
+                    const double m = smass[i];
+                    const uint32_t len = info & ((1u << STAGE_LEN_BITS) - 1u);
+                    const uint32_t p = off + cand[info >> STAGE_LEN_BITS];
+                    const uint32_t s = w0 + (p - lb);
+                    uint32_t pstart;
+                    const uint32_t pid = protein_at(p, s, pstart);
+                    const uint32_t head = __builtin_amdgcn_alignbyte(w32[(p >> 2) + 1], w32[p >> 2], p & 3u);
+                    uint32_t tail = 0;
+                    if (p + len - 1u <= known) {
+                        const uint32_t q = p + len - 4u;  // p >= 16
+                        tail = __builtin_bswap32(__builtin_amdgcn_alignbyte(w32[(q >> 2) + 1], w32[q >> 2], q & 3u));
+                    } else {
+                        for (uint32_t b = 0; b < 4 && b < len; ++b) tail |= (uint32_t)d_res[s + len - 1u - b] << (8 * b);
+                    }
+                    const uint32_t tag = peptide_tag(head, tail, len);
+                    const uint64_t q0 = rec_q0(m, tag), q1 = rec_q1(tag, rec_loc(pid, s - pstart, w), len);
+                    rr[k] = make_uint4((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32));
+                }
+            }
+            __syncthreads();  // the stage, list and window read: part_place's stage overwrites them
+            part_place<KS>(po, rr, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
+                           reinterpret_cast<uint16_t*>(st + 16 * PR), d_ctr);
+        } else {
+            part_tile<PR>(po, d_out + base, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
+                          reinterpret_cast<uint16_t*>(st + 16 * PR), d_ctr);
+        }
     }
 }
 

@@ -304,6 +304,7 @@ struct dbi_handle {
     // depth bins (warm lean builds: dbi_engine.hip warm_body_depth)
     bool use_depth = true;                // option depth_bins=0: the radix tail always
     bool use_semi_part = true;            // option semi_part=0: warm semi builds' first radix pass as its own kernels
+    bool use_part_stage = true;           // option part_stage=0: the partitioning digest's records go through HBM slots
     bool depth_off = false;               // this build's retry takes the radix tail (a region overflowed)
     bool depth_keep_map = false;          // this build's retry keeps the depth map it computed
     const uint4* depth_map_of = nullptr;  // the map buffer a complete map was last enqueued into

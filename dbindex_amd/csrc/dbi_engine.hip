@@ -745,6 +745,7 @@ int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_
     po.dm = DepthMap{h->dmap.p, sub, pl.b2, pl.nbins - 1};
     po.cap = pl.cap;
     po.b1 = pl.b1;
+    po.stage = h->use_part_stage ? 1u : 0u;
     h->part_now = &po;
     uint64_t n = 0;
     bool dev = false;
@@ -1778,6 +1779,7 @@ int dbi_set_option(dbi_handle* h, const char* name, int64_t value) {
     else if (n == "semi_bounded") h->use_semi_bounded = on;
     else if (n == "depth_bins") h->use_depth = on;
     else if (n == "semi_part") h->use_semi_part = on;
+    else if (n == "part_stage") h->use_part_stage = on;
     else if (n == "depth_map_reuse") h->opt_depth_map_reuse = on;
     else if (n == "big_split" && ranged(-1, 1)) h->big_split = (int)value;
     else if (n == "bin_bits_max" && ranged(1, 32)) h->bin_bits_max = (int)value;

@@ -283,6 +283,7 @@ struct PartOut {          // the digest's partition (k_digest_bounded / k_digest
     // (the first LSD pass), the digit the next dm.b2 bits (the second)
     uint32_t lsd;
     BinMap lin;
+    uint32_t stage;       // lean digest: tiles that fit keep their records in LDS until partitioned
 };
 // the map: ns evenly spaced uniques of the previous index (mass order) -> their
 // sub-bins and occurrence weights; the weights' scan (total -> ctr->depth_w);

@@ -234,27 +234,43 @@ def _native_lib():
     return _native.lib()
 
 
+class _NativeFasta:
+    """Owns a dbi_fasta result: freed when the last array viewing its residues goes."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        from . import _native
+        _native.lib().dbi_fasta_free(self.ptr)
+
+
 def _from_native(call, with_defs: bool) -> PackedProteins:
+    """The parser's packed proteome without copying its residues: the array
+    views the library's buffer (2-MiB pages, dbi_fasta_read), which is freed
+    with the array; offsets and definitions are copied (small)."""
     import ctypes
     from . import _native
     out = ctypes.POINTER(_native.DbiFasta)()
     _native.check(call(ctypes.byref(out)))
-    try:
-        f = out.contents
-        P, R = f.n_proteins, f.n_residues
-        res = np.ctypeslib.as_array((ctypes.c_uint8 * max(R, 1)).from_address(f.residues))[:R].copy() if R else \
-            np.zeros(0, np.uint8)
-        offs = np.ctypeslib.as_array(f.offsets, shape=(P + 1,)).astype(np.uint64)
-        defs: List[str] = []
-        if with_defs and P:
-            doff = np.ctypeslib.as_array(f.def_off, shape=(P + 1,))
-            raw = ctypes.string_at(f.defs, int(doff[-1])).decode("latin-1")
-            defs = [raw[int(doff[i]):int(doff[i + 1])] for i in range(P)]
-        pp = PackedProteins(res, offs, defs)
-        pp.n_uniprot = int(f.n_uniprot)
-        return pp
-    finally:
-        _native.lib().dbi_fasta_free(out)
+    owner = _NativeFasta(out)
+    f = out.contents
+    P, R = f.n_proteins, f.n_residues
+    if R:
+        buf = (ctypes.c_uint8 * R).from_address(f.residues)
+        buf._owner = owner  # the memoryview under the array keeps buf, buf keeps the result
+        res = np.ctypeslib.as_array(buf)
+    else:
+        res = np.zeros(0, np.uint8)
+    offs = np.ctypeslib.as_array(f.offsets, shape=(P + 1,)).astype(np.uint64)
+    defs: List[str] = []
+    if with_defs and P:
+        doff = np.ctypeslib.as_array(f.def_off, shape=(P + 1,))
+        raw = ctypes.string_at(f.defs, int(doff[-1])).decode("latin-1")
+        defs = [raw[int(doff[i]):int(doff[i + 1])] for i in range(P)]
+    pp = PackedProteins(res, offs, defs)
+    pp.n_uniprot = int(f.n_uniprot)
+    return pp
 
 
 def uniprot_accession(definition: str) -> Optional[str]:

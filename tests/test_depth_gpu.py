@@ -173,3 +173,74 @@ def test_semi_first_digit_partition(Engine):
             assert_index_equal(eng, oa, f"semi untimed {k}")
         m, t = query_masses(oa, 3000, seed=5)
         assert_queries_equal(eng, oa, m, t, "semi queries")
+
+
+def _dense_block(rng, n_res):
+    """Residues with a K/R every 7-9 positions (random other residues between):
+    every cleavage-site start has maxMC + 1 candidate ends past MIN_PEP_LENGTH,
+    ~1 500 record slots per 4096-start digest tile -- above the LDS stage."""
+    other = np.frombuffer(b"ACDEFGHILMNQSTVWY", np.uint8)
+    out, n = [], 0
+    while n < n_res:
+        k = int(rng.integers(6, 9))
+        seg = other[rng.integers(0, len(other), k)]
+        out.append(np.append(seg, np.frombuffer(b"KR", np.uint8)[rng.integers(0, 2)]))
+        n += k + 1
+    return np.concatenate(out)[:n_res]
+
+
+@pytest.mark.parametrize("part_stage", [1, 0])
+def test_part_stage_paths(Engine, part_stage):
+    """The partitioning digest keeps a tile's records in LDS (12 B each: mass,
+    candidate index and length; tag, protein and offset rebuilt from the
+    window) when its slot bound fits, else writes them through HBM slots
+    (option part_stage=0: every tile).  One proteome holds both kinds of
+    tile -- a block of cleavage-dense proteins (~1 500 slots a tile) and
+    ordinary ones -- plus walks past the 128-position horizon (glycine runs
+    under a 20000-Da maxMH: walk_global into the stage) and empty / short
+    proteins; cold, warm timed and replayed builds equal the oracle
+    (DBIndexer.java:237-405)."""
+    rng = np.random.default_rng(21)
+    base = fasta.config("human").slice(0, 9000)
+    seqs = base.sequences()
+    dense = _dense_block(rng, 300_000).tobytes().decode()
+    cut = [0] + sorted(int(x) for x in rng.integers(1, len(dense), 700)) + [len(dense)]
+    seqs[2000:2000] = [dense[a:b] for a, b in zip(cut[:-1], cut[1:])]
+    longw = ["G" * 150 + "K" + "AAAAAAR", "M" + "G" * 140 + "R" + "GGGGGGGK", "GGGGGGK" + "G" * 200,
+             "A" * 129 + "KR" + "G" * 131, "PEPTIDEK" + "G" * 300 + "K", "", "K", "GGGGK"]
+    for i, s in enumerate(longw * 20):
+        seqs.insert(5000 + 37 * i, s)
+    pp = fasta.PackedProteins.from_sequences(seqs, [fasta.uniprot_header(i) for i in range(len(seqs))])
+    cp = DBIndexSearchParams.trypsin(2, max_precursor_mass=20000.0).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    with Engine(cp, options={"part_stage": part_stage}) as eng:
+        for k in range(4):
+            eng.build(pp)
+            if k >= 2:
+                assert "bin_scatter" in _stages(eng), (k, _stages(eng))
+            assert_index_equal(eng, oix, f"part_stage={part_stage} build {k}")
+        eng.set_timing(False)
+        for k in range(3):
+            eng.build(pp)
+            assert_index_equal(eng, oix, f"part_stage={part_stage} replay {k}")
+        m, t = query_masses(oix, 4000, seed=17)
+        assert_queries_equal(eng, oix, m, t, "queries")
+
+
+def test_part_stage_long_protein(Engine):
+    """A protein of 2^20 + 300 residues: record lengths may not fit the LDS
+    stage's 20 bits, so every tile takes the HBM slots; the index equals the
+    oracle (the record layout: 2 x 21 bits + the protein id)."""
+    rng = np.random.default_rng(5)
+    base = fasta.config("human").slice(0, 4000)
+    seqs = base.sequences()
+    other = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    seqs.insert(1000, other[rng.integers(0, 20, (1 << 20) + 300)].tobytes().decode())
+    pp = fasta.PackedProteins.from_sequences(seqs, [fasta.uniprot_header(i) for i in range(len(seqs))])
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    with Engine(cp) as eng:
+        for k in range(3):
+            eng.build(pp)
+            assert_index_equal(eng, oix, f"long protein build {k}")
+        assert "bin_scatter" in _stages(eng)

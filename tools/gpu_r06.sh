@@ -1,0 +1,64 @@
+#!/bin/bash
+# tools/gpu_r06.sh TAG STEP... — one GPU-box session of round 6.  Every GPU step
+# has its own time limit; the script stops at the first failure.
+#   t_depth   tests/test_depth_gpu.py
+#   t_scale   the SwissProt-scale parity tests (full tryptic + 8 shards)
+#   t_all     the whole GPU suite
+#   ab_stage  bench SwissProt with part_stage=1, 0, 1 (A/B on one box)
+#   bench     the driver's bench line (default flags)
+#   prof      rocprofv3 kernel trace + stats of the bench (SwissProt)
+#   pmc       FETCH_SIZE / WRITE_SIZE passes (SwissProt)
+#   sq        SQ counter pass (SwissProt)
+#   semi      semi bench, semi trace + PMC
+#   h2d       tools/probe/h2d_probe (host-to-device copy paths)
+set -u -o pipefail
+TAG=${1:-r06}
+shift || true
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+    local name=$1 to=$2
+    shift 2
+    echo "== $name $(date +%T)"
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name exit $rc"
+    tail -4 "$OUT/$name.log"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+}
+PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread"
+B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-cold --queries 0"
+for w in "$@"; do
+    case $w in
+    t_depth) step t_depth 600 $PT tests/test_depth_gpu.py ;;
+    t_scale) step t_scale 900 $PT tests/test_scale_gpu.py -k "full_tryptic or sharded_8 or semi_slice" ;;
+    t_all)   step t_all 1100 $PT tests -m gpu ;;
+    ab_stage) step ab1 300 $B --option part_stage=1
+              step ab0 300 $B --option part_stage=0
+              step ab1b 300 $B --option part_stage=1 ;;
+    bench)   step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench_h) step bench_h 300 python bench.py --config human --steps 20 --warmup 5 --no-cpu-baseline ;;
+    prof)    step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
+                -- python3 bench.py --steps 10 --warmup 5 --queries 0 --no-cpu-baseline --no-cold ;;
+    pmc)     step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
+                -- python3 bench.py --steps 5 --warmup 5 --queries 0 --no-cpu-baseline --no-cold
+             step pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
+                -- python3 bench.py --steps 5 --warmup 5 --queries 0 --no-cpu-baseline --no-cold ;;
+    sq)      step pmc_sq 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
+                --output-format csv -d "$OUT/pmc_sq" -o run \
+                -- python3 bench.py --steps 5 --warmup 5 --queries 0 --no-cpu-baseline --no-cold ;;
+    semi)    step semi_bench 600 python bench.py --config semi --steps 5 --warmup 5 --no-cpu-baseline --no-cold --queries 0
+             step semi_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/semi/prof" -o run \
+                -- python3 bench.py --config semi --steps 2 --warmup 4 --queries 0 --no-cpu-baseline --no-cold ;;
+    semi_pmc) step semi_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/semi/pmc_fetch" -o run \
+                -- python3 bench.py --config semi --steps 2 --warmup 4 --queries 0 --no-cpu-baseline --no-cold
+             step semi_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/semi/pmc_write" -o run \
+                -- python3 bench.py --config semi --steps 2 --warmup 4 --queries 0 --no-cpu-baseline --no-cold ;;
+    h2d)     step h2d 180 ./tools/probe/h2d_probe ;;
+    *) echo "unknown step $w"; exit 2 ;;
+    esac
+done
+echo ALLDONE
