@@ -14,6 +14,9 @@ from .params import DbiParams
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DBI_LIB_PATH") or os.path.join(HERE, "libdbindex_hip.so")  # override: experiments
+# the test-hook variant (options test_fail / test_split_skew; dbindex_amd/build.py):
+# only the failure-injection tests load it, in processes of their own (DBI_LIB_PATH)
+HOOKS_PATH = os.path.join(HERE, "libdbindex_hip_hooks.so")
 
 DBI_OK, DBI_E_INVALID, DBI_E_OOM, DBI_E_HIP, DBI_E_RCCL, DBI_E_STATE = 0, -1, -2, -3, -4, -5
 FILTER_INCLUDE, FILTER_SKIP, FILTER_SKIP_PROTEIN_START = 0, 1, 2

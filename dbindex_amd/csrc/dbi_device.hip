@@ -1938,6 +1938,14 @@ __device__ void part_tile(const PartOut& po, const Rec* __restrict__ src, uint32
     }
 }
 
+#ifdef DBI_DIGEST_CLOCK  // experiment builds: summed phase cycles of the partitioning digest (dbi_debug_digest_clock)
+__device__ unsigned long long g_dphase[16];
+#define DPHASE(k) \
+    do { if (PART && threadIdx.x == 0) dph[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define DPHASE(k) do { } while (0)
+#endif
+
 // H1: with the first radix histogram (Hist1; 80 VGPRs kept for 6 waves per
 // SIMD, where the LDS puts the blocks).  PART: the records are partitioned by
 // the depth bins' high digit afterwards (part_tile; the slots are scratch).
@@ -1952,6 +1960,10 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     __shared__ uint32_t s_kept, s_waves, s_dup;
     __shared__ unsigned long long s_base;
     __shared__ uint32_t s_h1[H1 ? H1_LDS : 1];
+#ifdef DBI_DIGEST_CLOCK
+    unsigned long long dph[8] = {};
+#endif
+    DPHASE(0);
     const uint32_t tid = threadIdx.x;
     if constexpr (H1)
         for (uint32_t i = tid; i < H1_LDS; i += DIGEST_THREADS) s_h1[i] = 0;
@@ -2088,6 +2100,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
         nokm[w] = (st | (((cl << 1) | (cl_p >> 63)) & ~nc)) & valid;
     }
     __syncthreads();
+    DPHASE(1);
     // cleavage-site compaction: thread t owns starts [16t, 16t+16) of the tile, in order
     const uint32_t off = lb + (t0 - w0);  // LDS position of the tile's first start
     const uint32_t n_here = t0 + tid * STARTS_PER_THREAD < t_end
@@ -2108,6 +2121,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     const uint32_t w = rec_width(max_plen);
     if (tile == 0 && tid == 0 && !rec_layout_ok(w, n_prot)) atomicOr(&d_ctr->err, ERR_LAYOUT);
     balance_candidates(cand, s_cnt, ncand, B, t_end - t0);
+    DPHASE(2);
     uint32_t jb, je;
     thread_share(ncand, jb, je);
     // slot bounds: the candidate ends (B for a walk that may leave the horizon);
@@ -2131,6 +2145,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     __syncthreads();
     const unsigned long long base = s_base;
     if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
+    DPHASE(3);
     Rec* __restrict__ o = d_out + base + excl_t;
     const uint32_t c0 = (uint32_t)(base / RADIX_CHUNK_D);
     // the protein of the start at LDS position p (global index s) and its first residue
@@ -2246,6 +2261,7 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
             // the protein and offset from the start's candidate index
             constexpr uint32_t KS = (PR + DIGEST_THREADS - 1) / DIGEST_THREADS;
             __syncthreads();  // every walk's records staged, the walks' mass-table reads done
+            DPHASE(4);
             p_cnt[tid] = 0;
             const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(sm.win);
             uint4 rr[KS];
@@ -2275,8 +2291,19 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
                 }
             }
             __syncthreads();  // the stage, list and window read: part_place's stage overwrites them
+            DPHASE(5);
             part_place<KS>(po, rr, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
                            reinterpret_cast<uint16_t*>(st + 16 * PR), d_ctr);
+#ifdef DBI_DIGEST_CLOCK
+            __syncthreads();
+            DPHASE(6);
+            if (threadIdx.x == 0) {
+                for (int k = 0; k < 6; ++k) atomicAdd(&g_dphase[k], dph[k + 1] - dph[k]);
+                atomicAdd(&g_dphase[8], 1ull);
+                atomicAdd(&g_dphase[9], (unsigned long long)tile_slots);
+                atomicAdd(&g_dphase[10], (unsigned long long)ncand);
+            }
+#endif
         } else {
             part_tile<PR>(po, d_out + base, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
                           reinterpret_cast<uint16_t*>(st + 16 * PR), d_ctr);
@@ -4108,10 +4135,12 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
     // string-verify every pair in one parallel round (each check is a chain
     // of HBM loads: never serialise them per thread)
     const uint32_t npairs = s_u32[NT / 64];
+#ifndef DBI_X_NOVERIFY  // (experiment builds: the verification's HBM reads left out -- results not valid)
     for (uint32_t q = threadIdx.x; q < npairs; q += NT) {
         const uint32_t p = a16[2 * q + 1];
         if (!rl.same(Rec{k0[p], k1[p]}, Rec{k0[p - 1], k1[p - 1]})) *s_bad = 1;
     }
+#endif
     __syncthreads();
     if (*s_bad == 0) {
         for (uint32_t p = threadIdx.x; p < m; p += NT)
@@ -4822,6 +4851,18 @@ extern "C" int dbi_debug_phase_clock(unsigned long long* out, int reset) {
         return (int)hipMemcpyToSymbol(HIP_SYMBOL(dbi::g_phase), z, sizeof(z), 0, hipMemcpyHostToDevice);
     }
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dbi::g_phase), 32 * 8, 0, hipMemcpyDeviceToHost);
+}
+namespace dbi {
+#endif
+
+#ifdef DBI_DIGEST_CLOCK
+}  // namespace dbi
+extern "C" int dbi_debug_digest_clock(unsigned long long* out, int reset) {
+    if (reset) {
+        unsigned long long z[16] = {};
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(dbi::g_dphase), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dbi::g_dphase), 16 * 8, 0, hipMemcpyDeviceToHost);
 }
 namespace dbi {
 #endif

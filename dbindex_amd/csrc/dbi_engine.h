@@ -123,6 +123,10 @@ struct dbi_handle {
 
     // inputs (owned copies for host builds)
     DevBuf<uint8_t> res;
+    // host residues -> HBM through a pinned staging ring (upload_inputs):
+    // UP_THREADS copy threads, two slots of UP_SLOT bytes each, a copy event per slot
+    uint8_t* up_host = nullptr;
+    std::vector<hipEvent_t> up_ev;
     DevBuf<uint64_t> poff64;
     DevBuf<uint32_t> poff;
     DevBuf<uint32_t> poff_g;            // sharded build: global u32 offsets (owner merge)
@@ -211,6 +215,7 @@ struct dbi_handle {
         int best_n = 0, since_best = 0;
         int32_t best_split[dbi::MAX_SHARDS - 1] = {};
         double best_max = 0.0;
+        uint64_t best_records = 0;  // records of the build that set the best split (another proteome: forgotten)
     } shard_prof;
     // what a warm dbi_build_sharded reuses: the sorted sample keys of the last
     // sampled build (every rank's: all-gathered) and the split the previous
@@ -323,6 +328,7 @@ struct dbi_handle {
     // the depth bins' regions, the semi builds' low-digit regions
     double depth_slack = 1.25;
     double lsd_slack = 1.25;
+    int slack_ok = 0;                     // warm region builds since the last overflow (or the last decay)
     uint64_t prev_unique = 0;             // uniques of the resident index (the depth map's sample)
     DevBuf<Rec> recR;                     // the digest's regions
     DevBuf<uint8_t> rdig;                 //   each record's low bin digit
@@ -391,7 +397,11 @@ inline int stage_begin(dbi_handle* h, const char* name, Bytes b) {
     st.bytes = 0;
     st.launched = false;
     t_launch_ev = LaunchEvents{};
-    if (h->timing && (h->timing_only.empty() || h->timing_only == name)) {
+    // the stage's two events are created on first use (an untimed engine --
+    // a one-off build -- creates none: 96 hipEventCreate took ms at dbi_open)
+    if (h->timing && (h->timing_only.empty() || h->timing_only == name) &&
+        ((h->evpool[st.eb] || hipEventCreate(&h->evpool[st.eb]) == hipSuccess) &&
+         (h->evpool[st.ee] || hipEventCreate(&h->evpool[st.ee]) == hipSuccess))) {
         if (h->capturing) {  // a graph: event-record nodes around the stage's kernels
             st.launched = hipEventRecord(h->evpool[st.eb], h->stream) == hipSuccess;
         } else {             // events in the kernels' own dispatch packets

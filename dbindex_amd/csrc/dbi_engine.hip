@@ -14,6 +14,7 @@
 #include <limits>
 #include <cstdlib>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dbi_engine.h"
@@ -345,6 +346,10 @@ int finish_build(dbi_handle* h) {
     bytes += h->recA.bytes() + h->recB.bytes() + h->hist.bytes() + h->ucount.bytes();
     bytes += h->big_list.bytes() + h->mid_list.bytes() + h->giant_list.bytes() + h->segs.bytes() + h->ws_key.bytes() + h->ws_k2.bytes() + h->umass.bytes() + h->upid.bytes();
     bytes += h->uoff.bytes() + h->ulen.bytes() + h->occ_off.bytes() + h->occ_pid.bytes();
+    // the digest's regions and the depth-bin plan (they were left out)
+    bytes += h->recR.bytes() + h->rdig.bytes() + h->rcur.bytes() + h->dsub.bytes() + h->dpre.bytes() + h->desc.bytes();
+    bytes += h->d1c.bytes() + h->hist2.bytes() + h->bstart.bytes() + h->split_list.bytes() + h->dmap.bytes();
+    bytes += h->dheavy.bytes() + h->digits.bytes();
     st.device_bytes = bytes;
     h->built = true;
     h->last_kept = st.n_kept;
@@ -687,6 +692,8 @@ void drop_graph(dbi_handle* h) {
 // DEPTH_FALLBACK: no map to use (the index it samples was reallocated on the
 // way here and no earlier map is in place): the caller runs the radix tail
 constexpr int DEPTH_FALLBACK = 1;
+constexpr double SLACK_MIN = 1.25;  // region room / the region's share of the previous build's records
+constexpr int SLACK_DECAY = 8;      // builds without an overflow before the room is halved back toward SLACK_MIN
 
 int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_t* n_in, bool* sparse) {
     hipStream_t s = h->stream;
@@ -909,6 +916,13 @@ int build_digest(dbi_handle* h) {
             h->hc_final = true;
             h->depth_off = false;
             h->depth_keep_map = false;
+            // the regions' room comes back down after SLACK_DECAY builds without an
+            // overflow (one transient spike does not size them at 8x for good)
+            if ((depth_plan(h).on || lsd_plan(h).on) && ++h->slack_ok >= SLACK_DECAY) {
+                h->slack_ok = 0;
+                h->depth_slack = std::max(SLACK_MIN, 0.5 * h->depth_slack);
+                h->lsd_slack = std::max(SLACK_MIN, 0.5 * h->lsd_slack);
+            }
             return 0;
         }
         if (part_over) {  // a depth-bin region overflowed: this build by the radix tail, the next with more room
@@ -916,6 +930,7 @@ int build_digest(dbi_handle* h) {
             h->depth_map_unique = 0;  // (and a freshly sampled map)
             h->depth_slack = std::min(8.0, 2.0 * h->depth_slack);
             h->lsd_slack = std::min(8.0, 2.0 * h->lsd_slack);
+            h->slack_ok = 0;
         }
         // a redo of a depth-bin build keeps its map (this attempt's finalize may have overwritten the index)
         h->depth_keep_map = !part_over && !h->depth_off;
@@ -1063,7 +1078,8 @@ int plan_ptms(const uint8_t* res, const uint64_t* off, uint64_t n_prot, PtmPlan&
     return 0;
 }
 
-int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off, uint64_t n_prot);
+int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off, uint64_t n_prot,
+                  bool* ptm = nullptr);
 
 int build_with_ptms(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off,
                     uint64_t n_prot) {
@@ -1158,13 +1174,71 @@ int build_with_ptms(dbi_handle* h, const uint8_t* residues, uint64_t n_res, cons
     return build_tail(h, h->hc.n_kept, h->params.min_mh, h->params.max_mh, n_in + extra, sparse);
 }
 
-int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off, uint64_t n_prot) {
+// Host residues -> HBM.  A pageable hipMemcpy of a buffer the runtime has not
+// seen pins it first (201 MB: 32 ms the first time, 3.6 ms once pinned;
+// hipHostRegister 7 ms + 3.5 ms; tools/probe/h2d_probe.hip on MI355X), and a
+// caller's freshly parsed proteome is always such a buffer.  So the copy goes
+// through a pinned ring owned by the handle: UP_THREADS threads each copy
+// every UP_THREADS-th slice into one of their two UP_SLOT slots (waiting for
+// that slot's previous DMA), look for '[' in it on the way (inline PTMs: the
+// caller then takes the PTM path), and queue its DMA on the engine stream.
+// Small inputs take one plain copy.
+constexpr uint64_t UP_SLOT = 2ull << 20;
+constexpr int UP_THREADS = 8;
+constexpr uint64_t UP_MIN = 16ull << 20;  // below: one pageable copy
+
+int upload_residues(dbi_handle* h, const uint8_t* residues, uint64_t n_res, bool* ptm) {
+    if (n_res < UP_MIN) {
+        if (ptm) *ptm = n_res && std::memchr(residues, '[', n_res) != nullptr;
+        if (n_res) DBI_HIP(hipMemcpyAsync(h->res.p, residues, n_res, hipMemcpyHostToDevice, h->stream));
+        return 0;
+    }
+    if (!h->up_host) {
+        DBI_HIP(hipHostMalloc((void**)&h->up_host, UP_SLOT * 2 * UP_THREADS, hipHostMallocDefault));
+        h->up_ev.assign(2 * UP_THREADS, nullptr);
+        for (auto& ev : h->up_ev) DBI_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    const uint64_t nslices = (n_res + UP_SLOT - 1) / UP_SLOT;
+    const int T = (int)std::min<uint64_t>(UP_THREADS, nslices);
+    std::atomic<bool> found{false};
+    std::atomic<int> err{0};
+    auto work = [&](int t) {
+        uint32_t k = 0;
+        for (uint64_t c = (uint64_t)t; c < nslices; c += (uint64_t)T, ++k) {
+            const int slot = 2 * t + (int)(k & 1u);
+            uint8_t* st = h->up_host + UP_SLOT * (uint64_t)slot;
+            const uint64_t a = c * UP_SLOT, len = std::min(UP_SLOT, n_res - a);
+            if (k >= 2 && hipEventSynchronize(h->up_ev[slot]) != hipSuccess) {  // the slot's last DMA done
+                err = 1;
+                return;
+            }
+            std::memcpy(st, residues + a, len);
+            if (ptm && !found.load(std::memory_order_relaxed) && std::memchr(st, '[', len)) found = true;
+            if (hipMemcpyAsync(h->res.p + a, st, len, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+                hipEventRecord(h->up_ev[slot], h->stream) != hipSuccess) {
+                err = 1;
+                return;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    if (err) return set_error(DBI_E_HIP, "staged host-to-device copy of the residues failed");
+    if (ptm) *ptm = found;
+    return 0;
+}
+
+int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint64_t* prot_off, uint64_t n_prot,
+                  bool* ptm) {
     int rc;
+    DBI_HIP(hipSetDevice(h->device));
     if ((rc = h->res.ensure(n_res + 16))) return rc;
     if ((rc = h->poff.ensure(n_prot + 1))) return rc;
     std::vector<uint32_t> off32(n_prot + 1);
     for (uint64_t i = 0; i <= n_prot; ++i) off32[i] = (uint32_t)prot_off[i];
-    if (n_res) DBI_HIP(hipMemcpyAsync(h->res.p, residues, n_res, hipMemcpyHostToDevice, h->stream));
+    if ((rc = upload_residues(h, residues, n_res, ptm))) return rc;
     DBI_HIP(hipMemcpyAsync(h->poff.p, off32.data(), sizeof(uint32_t) * (n_prot + 1), hipMemcpyHostToDevice, h->stream));
     DBI_HIP(hipStreamSynchronize(h->stream));  // off32 is a stack vector
     h->d_res = h->res.p;
@@ -1310,8 +1384,6 @@ int dbi_open(const dbi_params* params, int device, dbi_handle** out) {
     };
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(set_error(DBI_E_HIP, "hipStreamCreate failed"));
-    for (auto& ev : h->evpool)
-        if (hipEventCreate(&ev) != hipSuccess) return fail(set_error(DBI_E_HIP, "hipEventCreate failed"));
     if ((rc = h->mass_tab.ensure(256)) || (rc = h->flags_tab.ensure(256)) || (rc = h->ctr.ensure(1)))
         return fail(rc);
     uint8_t fl[256];
@@ -1360,6 +1432,9 @@ void dbi_close(dbi_handle* h) {
         if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : h->ev_merge)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : h->up_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (h->up_host) (void)hipHostFree(h->up_host);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1368,12 +1443,14 @@ int dbi_build(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint
     if (!h || (!residues && n_res) || !prot_off) return set_error(DBI_E_INVALID, "NULL argument");
     int rc;
     if ((rc = check_offsets_host(prot_off, n_res, n_prot))) return rc;
-    if (n_res && std::memchr(residues, '[', n_res)) {  // inline '[formula]' PTMs
+    if (n_res >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_res must be < 2^32-1 per device: shard the FASTA");
+    bool ptm = false;  // the upload looks for '[' as it copies
+    if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot, &ptm))) return rc;
+    if (ptm) {  // inline '[formula]' PTMs
         if ((rc = build_with_ptms(h, residues, n_res, prot_off, n_prot))) return rc;
         return finish_build(h);
     }
     if ((rc = begin_build(h, n_res, n_prot))) return rc;
-    if ((rc = upload_inputs(h, residues, n_res, prot_off, n_prot))) return rc;
     if ((rc = build_digest(h))) return rc;
     return finish_build(h);
 }
@@ -1788,7 +1865,9 @@ int dbi_set_option(dbi_handle* h, const char* name, int64_t value) {
     else if (n == "shard_full_path") h->opt_shard_full_path = on;
     else if (n == "shard_dev_digest") h->opt_shard_dev_digest = on;
     else if (n == "shard_resample") h->opt_shard_resample = on;
+#ifdef DBI_TEST_HOOKS  // (test builds: libdbindex_hip_hooks.so)
     else if (n == "test_split_skew" && ranged(-1, 1 << 20)) h->opt_test_split_skew = (int)value;
+#endif
     else return set_error(DBI_E_INVALID, "unknown option or value out of range: " + n);
     drop_graph(h);  // a captured build bakes the old setting in
     h->prev_key_valid = false;
@@ -1798,10 +1877,12 @@ int dbi_set_option(dbi_handle* h, const char* name, int64_t value) {
 int dbi_set_option_str(dbi_handle* h, const char* name, const char* value) {
     if (!h || !name || !value) return set_error(DBI_E_INVALID, "NULL argument");
     std::lock_guard<std::recursive_mutex> lk(h->qmu);
+#ifdef DBI_TEST_HOOKS  // (test builds: libdbindex_hip_hooks.so)
     if (std::string(name) == "test_fail") {
         h->opt_test_fail = value;
         return 0;
     }
+#endif
     return set_error(DBI_E_INVALID, std::string("unknown string option: ") + name);
 }
 

@@ -329,12 +329,19 @@ int peer_failed(const char* phase) {
     return set_error(DBI_E_STATE, std::string("another rank failed (") + phase + "); see that rank's error");
 }
 
-// Test hook: DBI_TEST_FAIL="<phase>@<rank>" makes that rank fail locally at
-// that phase (digest, partition, buffers, merge, qroute, qbuffers), so the
-// agreement paths run without a real failure.
+// Test hook (test builds only, -DDBI_TEST_HOOKS: libdbindex_hip_hooks.so):
+// option test_fail = "<phase>@<rank>" makes that rank fail locally at that
+// phase (digest, partition, buffers, merge, qroute, qbuffers), so the
+// agreement paths run without a real failure.  The product library has no
+// such option.
 int injected_failure(const dbi_handle* h, const char* phase, int rank) {
+#ifdef DBI_TEST_HOOKS
     if (h->opt_test_fail.empty() || h->opt_test_fail != std::string(phase) + "@" + std::to_string(rank)) return 0;
     return set_error(DBI_E_STATE, std::string("injected failure (option test_fail) in ") + phase);
+#else
+    (void)h, (void)phase, (void)rank;
+    return 0;
+#endif
 }
 
 // max over ranks of (rc != 0): 0 when every rank succeeded
@@ -709,11 +716,15 @@ int dbi_shard_splitters_cost(const double* samples, int nshards, int32_t factor,
     return 0;
 }
 
+namespace dbi {
+void forget_best_split(dbi_handle* h);
+}
 namespace {
 constexpr int CB = DBI_COST_BANDS;
 constexpr double SPLIT_HOLD = 1.10;  // owners this balanced (slowest / mean merge time) keep their split
 constexpr int SPLIT_TRIES = 3;       // re-splits without a faster slowest owner: back to the best split, kept
 constexpr double SPLIT_BETTER = 0.98;  // (a split beats the best by 2 %)
+constexpr double SPLIT_WORSE = 2.0;    // the best split re-measured this much slower: the search resumes
 // the fixed key bands of the cost profile: CB equal key ranges of [minMH, maxMH]
 void cost_bands(const dbi_handle* h, int32_t* bsplit) {
     const double f = (double)h->params.mass_group_factor;
@@ -747,14 +758,29 @@ int dbi_shard_cost_update(dbi_handle* h, int nshards, const int32_t* split, cons
     pf.valid = true;
     // the best split so far (by its slowest owner): the same numbers on every rank
     double mx = 0.0;
-    for (int r = 0; r < nshards; ++r) mx = std::max(mx, merge_ms[r]);
+    uint64_t total = 0;
+    for (int r = 0; r < nshards; ++r) {
+        mx = std::max(mx, merge_ms[r]);
+        total += records[r];
+    }
+    // the best split belongs to the proteome it was measured on: a build of
+    // another size (> 5 % more or fewer records) forgets it, and so does a
+    // re-measurement of it SPLIT_WORSE slower (the data under the split
+    // changed) -- the search runs again instead of staying frozen
+    const uint64_t br = pf.best_records;
+    if (pf.has_best && (total > br + br / 20 || total + br / 20 < br)) forget_best_split(h);
     const bool same = pf.has_best && pf.best_n == nshards && std::equal(split, split + nshards - 1, pf.best_split);
-    if (same) {
+    if (same && mx > SPLIT_WORSE * pf.best_max) {
+        forget_best_split(h);
+    } else if (same) {
         pf.best_max = 0.5 * pf.best_max + 0.5 * mx;  // the best split re-measured (kept when frozen)
-    } else if (!pf.has_best || pf.best_n != nshards || mx < SPLIT_BETTER * pf.best_max) {
+        return 0;
+    }
+    if (!pf.has_best || pf.best_n != nshards || mx < SPLIT_BETTER * pf.best_max) {
         pf.has_best = true;
         pf.best_n = nshards;
         pf.best_max = mx;
+        pf.best_records = total;
         std::copy(split, split + nshards - 1, pf.best_split);
         pf.since_best = 0;
     } else {
@@ -764,6 +790,13 @@ int dbi_shard_cost_update(dbi_handle* h, int nshards, const int32_t* split, cons
 }
 
 namespace dbi {
+void forget_best_split(dbi_handle* h) {
+    auto& pf = h->shard_prof;
+    pf.has_best = false;
+    pf.since_best = 0;
+    pf.best_records = 0;
+}
+
 // the profile's split search has stopped: the best split is kept
 bool shard_split_frozen(const dbi_handle* h, int nshards) {
     const auto& pf = h->shard_prof;
@@ -1759,7 +1792,9 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
             // test hook (option test_split_skew = this rank): its reused split
             // differs from its peers' (another build history): the count
             // matrix's hashes disagree and every rank samples again
+#ifdef DBI_TEST_HOOKS
             if (h->opt_test_split_skew == me && n > 1) split[0] += 1;
+#endif
         }
         if (!rc_part && have_split) rc_part = partition_launch(h, split);
         if (!rc_part) rc_part = injected_failure(h, "partition", me);
@@ -1961,6 +1996,7 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
                        tot[2] + wm.sampled_kept / 20 < wm.sampled_kept;
     if (stale) {
         wm.valid = false;
+        forget_best_split(h);  // (measured on another proteome)
     } else {
         if (hold)
             std::copy(sh.split, sh.split + (n - 1), wm.split);

@@ -187,9 +187,12 @@ def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off
         row = np.zeros(SHARD_SAMPLES + 1, np.float64)
         check(L.dbi_shard_samples(eng.h, _p(row)))
         samples[r] = row
+    # the split is held for a build of the same shape only: the
+    # same residues, proteins and shard ranges as the build that held it
+    shape = (int(n_res), int(n_prot), tuple((int(b), int(e)) for b, e in ranges))
     held = getattr(engines[0], "_split_held", None) if balance else None
-    if held is not None and held.shape[0] == n - 1:
-        split = held  # the last build's owners were balanced: keep its split (dbi_build_sharded's hysteresis)
+    if held is not None and held[0] == shape and held[1].shape[0] == n - 1:
+        split = held[1]  # the last two builds ran this split, balanced: keep it (dbi_build_sharded's hysteresis)
     elif balance:
         s = np.ascontiguousarray(samples, np.float64).reshape(n * (SHARD_SAMPLES + 1))
         out = np.zeros(max(n - 1, 1), np.int32)
@@ -212,7 +215,12 @@ def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off
         sp = np.ascontiguousarray(np.concatenate([split, np.zeros(1, np.int32)]), np.int32)
         check(L.dbi_shard_cost_update(engines[0].h, n, _p(sp), _p(mms), _p(recs)))
         balanced = n > 1 and mms.min() > 0 and mms.max() <= SPLIT_HOLD * mms.mean()
-        engines[0]._split_held = split.copy() if balanced else None
+        # as dbi_build_sharded: held when this build ran the previous build's
+        # split (same shape) and its owners were balanced
+        prev = getattr(engines[0], "_split_prev", None)
+        same = prev is not None and prev[0] == shape and np.array_equal(prev[1], split)
+        engines[0]._split_held = (shape, split.copy()) if balanced and same else None
+        engines[0]._split_prev = (shape, split.copy())
     return split
 
 

@@ -268,10 +268,14 @@ int dbi_device_view(dbi_handle* h, dbi_device_index* out);
  * build); "big_split" (-1: by the list length, 0,
  * 1: the big chunk tier's two size classes); "bin_bits_max", "split_above",
  * "chunk_target" (0: by size); "shard_full_path", "shard_dev_digest",
- * "shard_resample" (0 / 1, dbi_build_sharded); "test_split_skew" (a rank, -1
- * off: that rank's reused owner split is skewed).  String option
- * "test_fail" = "<phase>@<rank>" (or ""): an injected local failure of a
- * sharded build or query.  DBI_E_INVALID for an unknown name or value. */
+ * "shard_resample" (0 / 1, dbi_build_sharded); "part_stage" (0 / 1: the
+ * partitioning digest keeps a tile's records in LDS, 1, or writes them
+ * through HBM slots, 0).  Test-build library only
+ * (libdbindex_hip_hooks.so, -DDBI_TEST_HOOKS; the product library answers
+ * DBI_E_INVALID): "test_split_skew" (a rank, -1 off: that rank's reused owner
+ * split is skewed) and string option "test_fail" = "<phase>@<rank>" (or ""):
+ * an injected local failure of a sharded build or query.  DBI_E_INVALID for
+ * an unknown name or value. */
 int dbi_set_option(dbi_handle* h, const char* name, int64_t value);
 int dbi_set_option_str(dbi_handle* h, const char* name, const char* value);
 

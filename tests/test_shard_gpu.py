@@ -183,42 +183,82 @@ def test_shard_phase_order(native):
             _native.check(_native.lib().dbi_shard_merge(eng.h))
 
 
+def _failure_case(phase: str, q) -> None:
+    """test_sharded_rccl_local_failure_is_reported's body, in a process that
+    loaded the test-hook library (option test_fail exists only there)."""
+    import traceback
+    try:
+        from dbindex_amd import _native as native
+        from dbindex_amd.engine import Engine
+        pp = fasta.config("1k").slice(0, 200)
+        cp = DBIndexSearchParams.trypsin(2).to_c()
+        oix = cref.Index(cp, pp.residues, pp.offsets)
+        d_res, d_off = _inputs(native, pp)
+        m, t = query_masses(oix, 500)
+        dm, dt = native.DeviceBuffer.from_numpy(m, 0), native.DeviceBuffer.from_numpy(t, 0)
+        df, dc = native.DeviceBuffer(8 * m.shape[0], 0), native.DeviceBuffer(8 * m.shape[0], 0)
+        comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
+        try:
+            with Engine(cp, 0, options={"shard_full_path": 1}) as eng:  # one rank: the general path
+                build = lambda: shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr,  # noqa: E731
+                                                    pp.n_proteins, 0, pp.n_proteins)
+                query = lambda: shard.query_sharded(eng, comm, dm.ptr, dt.ptr, m.shape[0], df.ptr, dc.ptr)  # noqa: E731
+                if phase.startswith("q"):
+                    build()
+                eng.set_option("test_fail", f"{phase}@0")
+                try:
+                    query() if phase.startswith("q") else build()
+                    raise AssertionError("the injected failure was not reported")
+                except native.DBIndexStoreException as ex:
+                    assert "injected failure" in str(ex), str(ex)
+                eng.set_option("test_fail", "")
+                st = build()
+                assert st.g_total == oix.n_total and st.g_unique == oix.n_unique
+                query()
+                of, oc = oix.query_batch(m, t)
+                f, c = df.download(np.uint64, m.shape[0]), dc.download(np.uint64, m.shape[0])
+                assert np.array_equal(c, oc) and np.array_equal(f[oc > 0], of[oc > 0])
+        finally:
+            comm.close()
+        q.put("ok")
+    except Exception:
+        q.put(traceback.format_exc())
+
+
 @pytest.mark.parametrize("phase", ["digest", "partition", "buffers", "merge", "qroute", "qbuffers"])
 def test_sharded_rccl_local_failure_is_reported(native, phase):
     """A rank that fails locally still joins the next collective with its
     status, so every rank returns an error instead of waiting in RCCL
-    (option test_fail injects the failure; one rank here, the agreement
-    collectives are the same at N ranks).  The engine and the communicator
-    stay usable: the next build and query batch succeed."""
-    from dbindex_amd import _native
+    (option test_fail injects the failure -- test-build library only,
+    libdbindex_hip_hooks.so, in a process of its own; one rank here, the
+    agreement collectives are the same at N ranks).  The engine and the
+    communicator stay usable: the next build and query batch succeed.  The
+    product library does not know the option."""
+    import multiprocessing as mp
+    import os
     from dbindex_amd.engine import Engine
-    pp = fasta.config("1k").slice(0, 200)
-    cp = DBIndexSearchParams.trypsin(2).to_c()
-    oix = cref.Index(cp, pp.residues, pp.offsets)
-    d_res, d_off = _inputs(native, pp)
-    m, t = query_masses(oix, 500)
-    dm, dt = native.DeviceBuffer.from_numpy(m, 0), native.DeviceBuffer.from_numpy(t, 0)
-    df, dc = native.DeviceBuffer(8 * m.shape[0], 0), native.DeviceBuffer(8 * m.shape[0], 0)
-    comm = shard.ShardComm(shard.ShardComm.unique_id(), 1, 0, 0)
-    try:
-        with Engine(cp, 0, options={"shard_full_path": 1}) as eng:  # one rank: the general path, not the single-owner build
-            build = lambda: shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins,
-                                                0, pp.n_proteins)
-            query = lambda: shard.query_sharded(eng, comm, dm.ptr, dt.ptr, m.shape[0], df.ptr, dc.ptr)
-            if phase.startswith("q"):
-                build()
+    with Engine(DBIndexSearchParams.trypsin(2).to_c(), 0) as eng:
+        with pytest.raises(native.DBIndexStoreException, match="INVALID"):
             eng.set_option("test_fail", f"{phase}@0")
-            with pytest.raises(_native.DBIndexStoreException, match="injected failure"):
-                query() if phase.startswith("q") else build()
-            eng.set_option("test_fail", "")
-            st = build()
-            assert st.g_total == oix.n_total and st.g_unique == oix.n_unique
-            query()
-            of, oc = oix.query_batch(m, t)
-            f, c = df.download(np.uint64, m.shape[0]), dc.download(np.uint64, m.shape[0])
-            assert np.array_equal(c, oc) and np.array_equal(f[oc > 0], of[oc > 0])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_failure_case, args=(phase, q))
+    saved = os.environ.get("DBI_LIB_PATH")
+    os.environ["DBI_LIB_PATH"] = native.HOOKS_PATH
+    try:
+        p.start()
     finally:
-        comm.close()
+        if saved is None:
+            os.environ.pop("DBI_LIB_PATH", None)
+        else:
+            os.environ["DBI_LIB_PATH"] = saved
+    try:
+        res = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert res == "ok", res
 
 
 @pytest.mark.parametrize("k,nprot", [(1, 300), (3, 1000), (5, 1000)])
@@ -388,6 +428,25 @@ def test_split_search_stops_at_the_best_split(native):
         check(L.dbi_shard_cost_update(eng.h, n, p(np.concatenate([best, [0]]).astype(np.int32)),
                                       p(np.array([1.5, 1.0, 1.0, 1.0], np.float64)), p(recs)))
         assert np.array_equal(profiled(), best)
+
+        def search(recs_now, splits_ms):
+            for sp, ms in splits_ms:
+                check(L.dbi_shard_cost_update(eng.h, n, p(np.concatenate([sp, [0]]).astype(np.int32)),
+                                              p(np.array(ms, np.float64)), p(recs_now)))
+
+        # the freeze has ways out.  A frozen search only ever runs
+        # the best split again; measured far slower (> 2x) the search
+        # resumes (the profile's split, not the old best) ...
+        search(recs, [(best, [3.0, 1.0, 1.0, 1.0])])
+        assert not np.array_equal(profiled(), best)
+        # ... and settles again: a faster split, three re-splits no faster
+        other = best + 40
+        slow = [9.0, 1.0, 1.0, 1.0]
+        search(recs, [(other, [1.0, 1.0, 1.0, 1.2]), (best + 50, slow), (best + 60, slow), (best + 70, slow)])
+        assert np.array_equal(profiled(), other)
+        # a proteome of another size (3x the records) forgets the old best split
+        search(recs * np.uint64(3), [(other, [1.0, 1.0, 1.0, 1.2])])
+        assert not np.array_equal(profiled(), other)
     pp = fasta.config("human").slice(0, 6000)
     oix = cref.Index(cp, pp.residues, pp.offsets)
     d_res, d_off = _inputs(native, pp)

@@ -104,13 +104,30 @@ def _mutated(pp, kind: str):
     return res, off.astype(np.uint64)
 
 
+HOOK_OPTIONS = ("test_fail", "test_split_skew")
+
+
 def _run(world: int, plan: dict):
+    from dbindex_amd._native import HOOKS_PATH
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     name = "/dbi_test_" + uuid.uuid4().hex[:12]
     procs = [ctx.Process(target=_rank_main, args=(world, r, name, plan, q)) for r in range(world)]
-    for p in procs:
-        p.start()
+    # the test hooks live in the test-build library only: the ranks of a plan
+    # that sets them load it (a spawned child reads DBI_LIB_PATH at import)
+    hooks = any(k in HOOK_OPTIONS for opts in plan.get("options", {}).values() for k in opts)
+    saved = os.environ.get("DBI_LIB_PATH")
+    if hooks:
+        os.environ["DBI_LIB_PATH"] = HOOKS_PATH
+    try:
+        for p in procs:
+            p.start()
+    finally:
+        if hooks:
+            if saved is None:
+                os.environ.pop("DBI_LIB_PATH", None)
+            else:
+                os.environ["DBI_LIB_PATH"] = saved
     res = {}
     try:
         for _ in range(world):

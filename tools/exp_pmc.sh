@@ -1,6 +1,6 @@
 #!/bin/bash
 # tools/exp_pmc.sh TAG variant... — FETCH_SIZE / WRITE_SIZE passes of the SwissProt
-# bench for experiment builds (dbindex_amd/exp/<variant>.so; "base" = in-tree),
+# bench for experiment builds (tools/exp/<variant>.so; "base" = in-tree),
 # with each kernel's traffic per launch (2 x FETCH + WRITE, MI355X_MICROARCH.md).
 set -u -o pipefail
 TAG=$1; shift
@@ -8,7 +8,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"; cd "$ROOT"; export TMPDIR=/tmp
 for v in "$@"; do
-    if [ "$v" = base ]; then unset DBI_LIB_PATH; else export DBI_LIB_PATH=dbindex_amd/exp/$v.so; fi
+    if [ "$v" = base ]; then unset DBI_LIB_PATH; else export DBI_LIB_PATH=tools/exp/$v.so; fi
     timeout -k 10 200 python bench.py --steps 10 --warmup 5 --no-cpu-baseline --queries 0 --no-cold > "$OUT/$v.json" 2> "$OUT/$v.err" || { tail -5 "$OUT/$v.err"; exit 1; }
     for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d "$OUT/${v}_$c" -o run \

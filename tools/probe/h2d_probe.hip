@@ -62,6 +62,46 @@ int main(int argc, char** argv) {
                     n / ms / 1e6, now_ms() - t);
         std::free(m);
     }
+    // device allocation cost by size (the one-off build's buffers), hipMalloc vs the stream-ordered pool
+    {
+        const size_t sizes[] = {1u << 20, 64u << 20, 512u << 20, 1024ull << 20, 4096ull << 20};
+        for (size_t sz : sizes) {
+            void* p[3];
+            double ta = 0, tf = 0;
+            for (int k = 0; k < 3; ++k) {
+                t = now_ms();
+                CK(hipMalloc(&p[k], sz));
+                ta += now_ms() - t;
+            }
+            for (int k = 0; k < 3; ++k) {
+                t = now_ms();
+                CK(hipFree(p[k]));
+                tf += now_ms() - t;
+            }
+            std::printf("hipMalloc %zu MiB: %.3f ms, hipFree %.3f ms (avg of 3)\n", sz >> 20, ta / 3, tf / 3);
+        }
+        hipStream_t s2;
+        CK(hipStreamCreate(&s2));
+        for (int r = 0; r < 2; ++r) {
+            void* q[4];
+            t = now_ms();
+            for (int k = 0; k < 4; ++k) CK(hipMallocAsync(&q[k], 1024ull << 20, s2));
+            CK(hipStreamSynchronize(s2));
+            const double ta = now_ms() - t;
+            t = now_ms();
+            for (int k = 0; k < 4; ++k) CK(hipFreeAsync(q[k], s2));
+            CK(hipStreamSynchronize(s2));
+            std::printf("hipMallocAsync 4 x 1 GiB (round %d): %.3f ms, hipFreeAsync %.3f ms\n", r, ta, now_ms() - t);
+        }
+        t = now_ms();
+        hipStream_t s3;
+        CK(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+        std::printf("hipStreamCreate: %.3f ms\n", now_ms() - t);
+        t = now_ms();
+        hipEvent_t evs[96];
+        for (auto& e : evs) CK(hipEventCreate(&e));
+        std::printf("96 x hipEventCreate: %.3f ms\n", now_ms() - t);
+    }
     // pinned staging ring: 4 MiB chunks, 16 threads memcpy into two pinned halves
     {
         const size_t C = 8u << 20;

@@ -141,9 +141,14 @@ def main() -> int:
         best["fixed_note"] = (f"median one-rank general-path wall - kernel time ({f:.3f} ms: host syncs, launch gaps, "
                               f"host logic) + 2 x {ALLGATHER_US} us of multi-rank all-gather latency")
         best["model_ms"] = best["model_ms_without_fixed"] + best["fixed_ms"]
-    print(json.dumps(best))
+    os.write(JSON_FD, (json.dumps(best) + "\n").encode())
     return 0
 
 
 if __name__ == "__main__":
+    import os
+    # the JSON line alone on stdout: RCCL prints its version banner on fd 1
+    # when a communicator comes up, so fd 1 becomes stderr for the run
+    JSON_FD = os.dup(1)
+    os.dup2(2, 1)
     sys.exit(main())
