@@ -1821,12 +1821,15 @@ struct StageSink {  // walk_global's records of a staged tile
 };
 
 // ---- depth bins: the digest's partition ------------------------------------
-__device__ __forceinline__ uint32_t depth_bin(double m, const DepthMap& dm) {
-    const uint32_t sb = bin_of(m, dm.sub);
-    const uint4 e = dm.map[sb >> 6];
+// the bin of sub-bin sb from its map word e = dm.map[sb >> 6]
+__device__ __forceinline__ uint32_t depth_bin_of(const uint4& e, uint32_t sb, const DepthMap& dm) {
     const uint64_t mask = (uint64_t)e.y << 32 | e.x;
     const uint32_t b = e.z + (uint32_t)__popcll(mask & (~0ull >> (63u - (sb & 63u))));
     return min(b, dm.last);  // (a map whose starts outnumber the bins: the top ones share the last)
+}
+__device__ __forceinline__ uint32_t depth_bin(double m, const DepthMap& dm) {
+    const uint32_t sb = bin_of(m, dm.sub);
+    return depth_bin_of(dm.map[sb >> 6], sb, dm);
 }
 
 // the XCD this wave runs on (HW_REG_XCC_ID, bits 3:0; MI355X_MICROARCH.md: blockIdx % 8 only says
@@ -1859,7 +1862,12 @@ __device__ __forceinline__ uint32_t xcc_id() {
 template <uint32_t KI>
 __device__ __forceinline__ void part_place(const PartOut& po, const uint4 (&rv)[KI], uint32_t nr, uint32_t* s_cnt,
                                            uint32_t* s_run, uint32_t* s_tmp, uint4* stage, uint16_t* sdig,
-                                           Counters* __restrict__ ctr) {
+                                           Counters* __restrict__ ctr, unsigned long long* clk = nullptr) {
+#ifdef DBI_DIGEST_CLOCK
+#define PCLK(k) do { if (clk && threadIdx.x == 0) clk[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define PCLK(k) do { } while (0)
+#endif
     const uint32_t tid = threadIdx.x, xcd = xcc_id(), D1 = 1u << po.b1;
     const uint32_t b2 = po.dm.b2, m2 = (1u << b2) - 1u;
     // the region digit of a bin (depth: its high b1 bits; lsd: its low b1 bits) and its pass-2 digit
@@ -1867,6 +1875,20 @@ __device__ __forceinline__ void part_place(const PartOut& po, const uint4 (&rv)[
     auto d2_of = [&](uint32_t b) { return po.lsd ? (b >> po.b1) & m2 : b & m2; };
     uint4* __restrict__ out4 = reinterpret_cast<uint4*>(po.recs);
     uint32_t bin[KI], rk[KI];
+#ifdef DBI_DIGEST_CLOCK  // (clock builds: the bins apart from the ranks)
+#pragma unroll
+    for (uint32_t k = 0; k < KI; ++k) {
+        bin[k] = ~0u;
+        rk[k] = 0;
+        if (k * DIGEST_THREADS + tid < nr && (rv[k].x & rv[k].y) != 0xFFFFFFFFu)
+            bin[k] = po.lsd ? bin_of(u4_mass(rv[k]), po.lin) : depth_bin(u4_mass(rv[k]), po.dm);
+    }
+    __syncthreads();
+    if (clk && threadIdx.x == 0) clk[3] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (uint32_t k = 0; k < KI; ++k)
+        if (bin[k] != ~0u) rk[k] = atomicAdd(&s_cnt[d1_of(bin[k])], 1u);
+#else
 #pragma unroll
     for (uint32_t k = 0; k < KI; ++k) {
         bin[k] = ~0u;
@@ -1876,7 +1898,9 @@ __device__ __forceinline__ void part_place(const PartOut& po, const uint4 (&rv)[
             rk[k] = atomicAdd(&s_cnt[d1_of(bin[k])], 1u);
         }
     }
+#endif
     __syncthreads();
+    PCLK(0);
     // digit d's run: stage[lstart, lstart + c), region cursor o -> out[region(d) + o + (t - lstart)]
     const uint32_t c = tid < D1 ? s_cnt[tid] : 0u;
     uint32_t nvalid;
@@ -1896,6 +1920,7 @@ __device__ __forceinline__ void part_place(const PartOut& po, const uint4 (&rv)[
         s_cnt[tid] = lstart;
     }
     __syncthreads();
+    PCLK(1);
 #pragma unroll
     for (uint32_t k = 0; k < KI; ++k) {
         if (bin[k] != ~0u) {
@@ -1905,6 +1930,7 @@ __device__ __forceinline__ void part_place(const PartOut& po, const uint4 (&rv)[
         }
     }
     __syncthreads();
+    PCLK(2);
     for (uint32_t t = tid; t < nvalid; t += DIGEST_THREADS) {
         const uint32_t bb = sdig[t];
         const uint32_t g = s_run[bb >> 8];
@@ -1913,6 +1939,7 @@ __device__ __forceinline__ void part_place(const PartOut& po, const uint4 (&rv)[
             po.dig[g + t] = (uint8_t)(bb & 0xFFu);
         }
     }
+#undef PCLK
 }
 
 template <uint32_t R>
@@ -2137,28 +2164,6 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
     }
     uint32_t tile_slots;
     const uint32_t excl_t = block_excl_scan<DIGEST_THREADS, uint32_t>(lim, sm.tmp, tile_slots);
-    // the tile's output region: one atomic add, in whatever order the tiles
-    // get here (no tile waits for another; the chunk sort does not need
-    // records in first-appearance order, ck_fix_runs); ctr->n_slots ends as
-    // the total
-    if (tid == 0) s_base = atomicAdd(&d_ctr->n_slots, (unsigned long long)tile_slots);
-    __syncthreads();
-    const unsigned long long base = s_base;
-    if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
-    DPHASE(3);
-    Rec* __restrict__ o = d_out + base + excl_t;
-    const uint32_t c0 = (uint32_t)(base / RADIX_CHUNK_D);
-    // the protein of the start at LDS position p (global index s) and its first residue
-    auto protein_at = [&](uint32_t p, uint32_t s, uint32_t& pstart) {
-        uint32_t pid;
-        if (pid_map) {
-            pid = pid_base + sm.wpre[p >> 6] + (uint32_t)__popcll(sm.stm[p >> 6] & low_bits((p & 63u) + 1u));
-            pstart = sm.pst[pid - pf];
-        } else {
-            pid = protein_of(sm.pst, npst, pf, pl, d_poff, s, pstart);
-        }
-        return pid;
-    };
     // PART stage mode (block-uniform): the tile's records stay in LDS, 12 B
     // each behind the candidate list (smass / sinfo, slot excl_t + k of each
     // thread as in d_out), until part_place writes them into the regions --
@@ -2175,6 +2180,34 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
         smass = reinterpret_cast<double*>(sm.pool + c16);
         sinfo = reinterpret_cast<uint32_t*>(sm.pool + c16 + 8u * room);
     }
+    // the tile's output region: one atomic add, in whatever order the tiles
+    // get here (no tile waits for another; the chunk sort does not need
+    // records in first-appearance order, ck_fix_runs); ctr->n_slots ends as
+    // the total.  A staged tile takes none: its records never touch d_out
+    // (n_slots counts the slots of the tiles that did; one contended device
+    // atomic and a barrier's wait for it fewer per tile)
+    unsigned long long base = 0;
+    if (!stage) {
+        if (tid == 0) s_base = atomicAdd(&d_ctr->n_slots, (unsigned long long)tile_slots);
+        __syncthreads();
+        base = s_base;
+        if (base + tile_slots > cap) return;  // too small: the caller grows it and runs again
+    }
+    DPHASE(3);
+
+    Rec* __restrict__ o = d_out + base + excl_t;
+    const uint32_t c0 = (uint32_t)(base / RADIX_CHUNK_D);
+    // the protein of the start at LDS position p (global index s) and its first residue
+    auto protein_at = [&](uint32_t p, uint32_t s, uint32_t& pstart) {
+        uint32_t pid;
+        if (pid_map) {
+            pid = pid_base + sm.wpre[p >> 6] + (uint32_t)__popcll(sm.stm[p >> 6] & low_bits((p & 63u) + 1u));
+            pstart = sm.pst[pid - pf];
+        } else {
+            pid = protein_of(sm.pst, npst, pf, pl, d_poff, s, pstart);
+        }
+        return pid;
+    };
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
         const uint32_t p = off + cand[j];
@@ -2292,12 +2325,23 @@ k_digest_bounded(DevParams dp, const double* __restrict__ d_mass_tab, const uint
             }
             __syncthreads();  // the stage, list and window read: part_place's stage overwrites them
             DPHASE(5);
+#ifdef DBI_DIGEST_CLOCK
+            unsigned long long pcl[4] = {};
+            part_place<KS>(po, rr, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
+                           reinterpret_cast<uint16_t*>(st + 16 * PR), d_ctr, pcl);
+#else
             part_place<KS>(po, rr, tile_slots, p_cnt, p_cnt + 256, sm.tmp, reinterpret_cast<uint4*>(st),
                            reinterpret_cast<uint16_t*>(st + 16 * PR), d_ctr);
+#endif
 #ifdef DBI_DIGEST_CLOCK
             __syncthreads();
             DPHASE(6);
             if (threadIdx.x == 0) {
+                atomicAdd(&g_dphase[11], pcl[0] - dph[5]);   // bins + ranks
+                atomicAdd(&g_dphase[15], pcl[3] - dph[5]);   // bins alone
+                atomicAdd(&g_dphase[12], pcl[1] - pcl[0]);   // scan + region reservation
+                atomicAdd(&g_dphase[13], pcl[2] - pcl[1]);   // restage in digit order
+                atomicAdd(&g_dphase[14], dph[6] - pcl[2]);   // runs written
                 for (int k = 0; k < 6; ++k) atomicAdd(&g_dphase[k], dph[k + 1] - dph[k]);
                 atomicAdd(&g_dphase[8], 1ull);
                 atomicAdd(&g_dphase[9], (unsigned long long)tile_slots);

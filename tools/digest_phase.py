@@ -43,7 +43,11 @@ def main():
     tot = sum(v[:6])
     out = dict(staged_tiles_per_build=tiles / reps, slots_per_tile=v[9] / tiles, candidates_per_tile=v[10] / tiles,
                phases={n: dict(cycles_per_tile=v[k] / tiles, share=v[k] / tot if tot else 0.0)
-                       for k, n in enumerate(NAMES)})
+                       for k, n in enumerate(NAMES)},
+               partition={n: dict(cycles_per_tile=v[11 + k] / tiles, share=v[11 + k] / tot if tot else 0.0)
+                          for k, n in enumerate(["bins + ranks", "scan + region reservation",
+                                                 "restage in digit order", "runs written"])},
+               bins_alone=dict(cycles_per_tile=v[15] / tiles, share=v[15] / tot if tot else 0.0))
     print(json.dumps(out, indent=1))
 
 

@@ -11,6 +11,12 @@
 #   sq        SQ counter pass (SwissProt)
 #   semi      semi bench, semi trace + PMC
 #   h2d       tools/probe/h2d_probe (host-to-device copy paths)
+#   dclock    digest phase clocks (tools/exp/dclock.so)
+#   noverify  chunk-sort traffic with / without string verification (tools/exp/noverify.so)
+#   ab_prev   bench of tools/exp/prev.so (the last commit) against the tree, twice each
+#   allconf   tools/bench_all.sh: every config's bench line (+ --merge)
+#   budget    tools/shard_budget.py (N = 8 model, 12 builds)
+#   e2e       bench with the cold / end-to-end legs, no CPU baseline
 set -u -o pipefail
 TAG=${1:-r06}
 shift || true
@@ -58,6 +64,24 @@ for w in "$@"; do
              step semi_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/semi/pmc_write" -o run \
                 -- python3 bench.py --config semi --steps 2 --warmup 4 --queries 0 --no-cpu-baseline --no-cold ;;
     h2d)     step h2d 180 ./tools/probe/h2d_probe ;;
+    dclock)  export DBI_LIB_PATH=tools/exp/dclock.so
+             step dclock 300 python tools/digest_phase.py
+             unset DBI_LIB_PATH ;;
+    noverify) step noverify 900 bash tools/exp_pmc.sh $TAG/exp base noverify ;;
+    ab_prev) for r in 1 2; do
+                 DBI_LIB_PATH=tools/exp/prev.so step prev$r 300 $B
+                 step cur$r 300 $B
+             done
+             python3 tools/ab_table.py "$OUT" prev1 cur1 prev2 cur2 ;;
+    ab3)     for r in 1 2; do   # ab3 A B: tools/exp/A.so, tools/exp/B.so and the tree
+                 DBI_LIB_PATH=tools/exp/$V1.so step ${V1}$r 300 $B
+                 DBI_LIB_PATH=tools/exp/$V2.so step ${V2}$r 300 $B
+                 step cur$r 300 $B
+             done
+             python3 tools/ab_table.py "$OUT" ${V1}1 ${V2}1 cur1 ${V1}2 ${V2}2 cur2 ;;
+    allconf) step allconf 1100 bash tools/bench_all.sh $TAG/bench ;;
+    budget)  step budget 900 bash -c "python tools/shard_budget.py --reps 12 > $OUT/shard_budget8.json" ;;
+    e2e)     step e2e 300 python bench.py --steps 10 --warmup 5 --no-cpu-baseline --queries 0 ;;
     *) echo "unknown step $w"; exit 2 ;;
     esac
 done
