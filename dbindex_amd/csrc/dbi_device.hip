@@ -3095,8 +3095,12 @@ k_part_plan(const uint32_t* __restrict__ cur, uint32_t cap, uint32_t b1, uint64_
     }
     uint32_t all_placed;
     block_excl_scan<256, uint32_t>(placed, s_tmp, all_placed);
-    const bool ok = ctr->n_slots <= slot_cap && !(ctr->err & ERR_PART) && all_placed == ctr->n_kept;
-    if (d == 0 && !(ctr->err & ERR_PART) && ctr->n_slots <= slot_cap && all_placed != ctr->n_kept)
+    // the records must fit the tail's buffers too: a tile staged in LDS
+    // reserves no slots, so n_slots alone no longer bounds n_kept (a grown
+    // proteome: nothing downstream runs, the host grows them and redoes it)
+    const bool fits = ctr->n_slots <= slot_cap && ctr->n_kept <= slot_cap;
+    const bool ok = fits && !(ctr->err & ERR_PART) && all_placed == ctr->n_kept;
+    if (d == 0 && !(ctr->err & ERR_PART) && fits && all_placed != ctr->n_kept)
         atomicOr(&ctr->err, ERR_PART);  // (lost cursor adds: redone by the radix tail)
     uint32_t nch = 0;
     if (ok && d < D1) {
