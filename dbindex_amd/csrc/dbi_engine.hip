@@ -448,7 +448,7 @@ int run_digest(dbi_handle* h, uint64_t* n_out, uint64_t* n_in_out, bool* sparse_
             }
             if ((rc = read_counters(h))) return rc;
             n = h->hc.n_kept;
-            const uint64_t need = bounded ? std::max(h->hc.n_slots, n) : n;
+            const uint64_t need = bounded ? std::max<uint64_t>(h->hc.n_slots, n) : n;
             if (need >= (1ull << 32) - 1)
                 return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences (or bounded-digest slots) on "
                                                 "one device: shard the FASTA");
@@ -907,7 +907,7 @@ int build_digest(dbi_handle* h) {
         // and the chunk lists their grids?
         if ((rc = read_counters(h))) return rc;
         // (a digest tile staged in LDS reserves no slots: n_kept can exceed n_slots)
-        const uint64_t need = sparse ? std::max(h->hc.n_slots, h->hc.n_kept) : h->hc.n_kept;
+        const uint64_t need = sparse ? std::max<uint64_t>(h->hc.n_slots, h->hc.n_kept) : h->hc.n_kept;
         if (need >= (1ull << 32) - 1)
             return set_error(DBI_E_INVALID, "more than 2^32-2 peptide occurrences (or bounded-digest slots) on "
                                             "one device: shard the FASTA");

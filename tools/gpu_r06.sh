@@ -40,6 +40,7 @@ B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-cold --queries 0
 for w in "$@"; do
     case $w in
     t_depth) step t_depth 600 $PT tests/test_depth_gpu.py ;;
+    t_graph) step t_graph 600 $PT tests/test_graph_gpu.py tests/test_depth_gpu.py ;;
     t_scale) step t_scale 900 $PT tests/test_scale_gpu.py -k "full_tryptic or sharded_8 or semi_slice" ;;
     t_all)   step t_all 1100 $PT tests -m gpu ;;
     ab_stage) step ab1 300 $B --option part_stage=1
