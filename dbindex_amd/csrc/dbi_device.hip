@@ -4186,48 +4186,69 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
 #ifndef DBI_X_NOVERIFY  // (experiment builds: the verification's HBM reads left out -- results not valid)
     for (uint32_t q = threadIdx.x; q < npairs; q += NT) {
         const uint32_t p = a16[2 * q + 1];
-        if (!rl.same(Rec{k0[p], k1[p]}, Rec{k0[p - 1], k1[p - 1]})) *s_bad = 1;
+        if (!rl.same(Rec{k0[p], k1[p]}, Rec{k0[p - 1], k1[p - 1]})) {
+            *s_bad = 1;
+            a16[2 * p] = 0x8000u;  // (a dup's head entry is 0) a string boundary inside p's group
+        }
     }
 #endif
     __syncthreads();
+#ifdef DBI_X_NOREGROUP  // (experiment builds: tag collisions left merged -- results not valid)
+    if (true) {
+#else
     if (*s_bad == 0) {
+#endif
         for (uint32_t p = threadIdx.x; p < m; p += NT)
             if (!nw || !in_ranges(wr, nw, p))
                 out[p] = Rec{(k0[p] & ~0xFFull) | (a16[2 * p] == p ? 1ull : 0ull), k1[p]};  // p == 0 always a head
         return heads;
     }
-    // 16-bit tag collision (rare, block-uniform): group start gs(p) = max head
-    // position <= p (block max-scan over contiguous per-thread ranges)
+    // 16-bit tag collision (block-uniform; SwissProt: ~10 000 per build, the
+    // equal (mass, tag) runs of isobaric permutations): group start gs(p) = max
+    // head position <= p (block max-scan over contiguous per-thread ranges).
+    // Only a group holding a failed pair (bit 15 of its entry, set above) has
+    // several strings; every other group is one string (its neighbours
+    // verified equal), so its leader is its start, with no string read.
+    // aux[p]: bit 31 = a failed pair ends at p; bit 30 (on a group start) =
+    // the group holds several strings -- kept through the leader pass below.
+    constexpr uint32_t FAILED = 1u << 31, MIXED = 1u << 30;
     {
         const uint32_t E = (m + NT - 1) / NT;
         const uint32_t lo = min(threadIdx.x * E, m), hi = min(lo + E, m);
         uint32_t run = 0;
-        for (uint32_t p = lo; p < hi; ++p) run = max(run, (uint32_t)a16[2 * p]);
+        for (uint32_t p = lo; p < hi; ++p) run = max(run, (uint32_t)a16[2 * p] & 0x7FFFu);
         uint32_t cur = block_excl_max<NT>(run, s_u32);
         for (uint32_t p = lo; p < hi; ++p) {
-            cur = max(cur, (uint32_t)a16[2 * p]);
-            aux[p] = cur;  // group start of p (the pair list is dead)
+            const uint32_t v = a16[2 * p];
+            cur = max(cur, v & 0x7FFFu);
+            aux[p] = cur | (v & 0x8000u ? FAILED : 0u);  // group start of p (the pair list is dead)
         }
     }
     __syncthreads();
+    for (uint32_t p = threadIdx.x; p < m; p += NT)
+        if (aux[p] & FAILED) atomicOr(&aux[aux[p] & 0xFFFFu], MIXED);
+    __syncthreads();
     // leader = position of the first occurrence of p's string in its group
     // (sorted order inside a group = first appearance); group start kept in
-    // the high half
+    // bits 16-29
     for (uint32_t p = threadIdx.x; p < m; p += NT) {
-        const uint32_t gs = aux[p];
-        const Rec me{k0[p], k1[p]};
-        uint32_t lead = p;
-        for (uint32_t q = gs; q < p; ++q)
-            if (rl.same(Rec{k0[q], k1[q]}, me)) { lead = q; break; }
-        aux[p] = (gs << 16) | lead;
+        const uint32_t a = aux[p], gs = a & 0xFFFFu;
+        uint32_t lead = gs;
+        if (aux[gs] & MIXED) {  // (bit 30 of the start's entry survives its rewrite)
+            const Rec me{k0[p], k1[p]};
+            lead = p;
+            for (uint32_t q = gs; q < p; ++q)
+                if (rl.same(Rec{k0[q], k1[q]}, me)) { lead = q; break; }
+        }
+        aux[p] = (a & MIXED) | (gs << 16) | lead;
     }
     __syncthreads();
     heads = 0;
     for (uint32_t p = threadIdx.x; p < m; p += NT) {
         if (nw && in_ranges(wr, nw, p)) continue;  // a head of its own (one-record group), not written
-        const uint32_t gs = aux[p] >> 16, lead = aux[p] & 0xFFFFu;
+        const uint32_t gs = (aux[p] >> 16) & 0x3FFFu, lead = aux[p] & 0xFFFFu;
         uint32_t np = gs;
-        for (uint32_t q = gs; q < m && (aux[q] >> 16) == gs; ++q) {
+        for (uint32_t q = gs; q < m && ((aux[q] >> 16) & 0x3FFFu) == gs; ++q) {
             const uint32_t lq = aux[q] & 0xFFFFu;
             np += (lq < lead) | ((lq == lead) & (q < p));
         }
@@ -4403,7 +4424,7 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
     unsigned long long tph[8] = {};  // (mark 4: after the block-level sorts, BLOCK only)
 #endif
     PHASE_MARK(0);
-    static_assert(CAP <= 65535, "16-bit positions");
+    static_assert(CAP < 16384, "positions in 14 bits (finish_sorted's collision regroup)");
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t E = (CAP + NT - 1) / NT;  // records per thread (contiguous) in the run pass
     static_assert(E <= 32, "run-head bit mask");
@@ -4653,6 +4674,7 @@ template <int NT, int CAP>
 __device__ uint32_t bitonic_chunk(const Rec* in, Rec* out, uint32_t m, const RecLoc& rl,
                                   unsigned long long* k0, unsigned long long* k1, uint32_t* aux, uint32_t* s_u32,
                                   uint32_t* s_bad, uint64_t* s_min, uint16_t* s_tcnt) {
+    static_assert(CAP < 16384, "positions in 14 bits (finish_sorted's collision regroup)");
     for (uint32_t i = threadIdx.x; i < m; i += NT) {
         const Rec r = in[i];
         k0[i] = r.q0;
