@@ -4247,10 +4247,13 @@ __device__ uint32_t finish_sorted(Rec* __restrict__ out, uint32_t m, const RecLo
     for (uint32_t p = threadIdx.x; p < m; p += NT) {
         if (nw && in_ranges(wr, nw, p)) continue;  // a head of its own (one-record group), not written
         const uint32_t gs = (aux[p] >> 16) & 0x3FFFu, lead = aux[p] & 0xFFFFu;
-        uint32_t np = gs;
-        for (uint32_t q = gs; q < m && ((aux[q] >> 16) & 0x3FFFu) == gs; ++q) {
-            const uint32_t lq = aux[q] & 0xFFFFu;
-            np += (lq < lead) | ((lq == lead) & (q < p));
+        uint32_t np = p;  // a one-string group keeps its order
+        if (aux[gs] & MIXED) {
+            np = gs;
+            for (uint32_t q = gs; q < m && ((aux[q] >> 16) & 0x3FFFu) == gs; ++q) {
+                const uint32_t lq = aux[q] & 0xFFFFu;
+                np += (lq < lead) | ((lq == lead) & (q < p));
+            }
         }
         out[np] = Rec{(k0[p] & ~0xFFull) | (lead == p ? 1ull : 0ull), k1[p]};
         heads += lead == p;
