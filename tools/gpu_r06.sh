@@ -17,6 +17,7 @@
 #   allconf   tools/bench_all.sh: every config's bench line (+ --merge)
 #   budget    tools/shard_budget.py (N = 8 model, 12 builds)
 #   e2e       bench with the cold / end-to-end legs, no CPU baseline
+#   e2e_trace HIP API + kernel + copy trace of fresh engines' builds (tools/e2e_trace.py)
 set -u -o pipefail
 TAG=${1:-r06}
 shift || true
@@ -83,6 +84,9 @@ for w in "$@"; do
     allconf) step allconf 1100 bash tools/bench_all.sh $TAG/bench ;;
     budget)  step budget 900 bash -c "python tools/shard_budget.py --reps 12 > $OUT/shard_budget8.json" ;;
     e2e)     step e2e 300 python bench.py --steps 10 --warmup 5 --no-cpu-baseline --queries 0 ;;
+    e2e_trace) step e2e_trace 300 rocprofv3 --hip-runtime-trace --kernel-trace --memory-copy-trace --output-format csv \
+                -d "$OUT/trace" -o run -- python3 tools/e2e_trace.py
+             python3 tools/api_timeline.py "$OUT/trace" > "$OUT/e2e_timeline.txt" ;;
     *) echo "unknown step $w"; exit 2 ;;
     esac
 done
