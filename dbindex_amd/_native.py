@@ -178,6 +178,7 @@ SIGNATURES = [
     ("dbi_fasta_parse", c_int, [P, c_uint64, c_int, POINTER(POINTER(DbiFasta))]),
     ("dbi_fasta_read", c_int, [c_char_p, c_int, POINTER(POINTER(DbiFasta))]),
     ("dbi_fasta_free", None, [POINTER(DbiFasta)]),
+    ("dbi_build_fasta", c_int, [P, c_char_p, c_int, POINTER(POINTER(DbiFasta))]),
     ("dbi_dev_alloc", c_int, [c_int, c_uint64, POINTER(c_void_p)]),
     ("dbi_dev_free", c_int, [c_int, P]),
     ("dbi_dev_copy_h2d", c_int, [c_int, P, P, c_uint64]),

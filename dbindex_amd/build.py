@@ -73,7 +73,7 @@ def build(force: bool = False, verbose: bool = False, lib_out: str = LIB, define
     (LIB_HOOKS: dbi_engine / dbi_shard again with -DDBI_TEST_HOOKS, every
     other object shared), which only the failure-injection tests load."""
     deps = [os.path.join(CSRC, s) for s in SOURCES]
-    deps += [os.path.join(CSRC, "dbi_internal.h"), os.path.join(CSRC, "dbi_lane.h"), os.path.join(CSRC, "dbi_engine.h"), os.path.join(ROOT, "include", "dbindex_hip.h")]
+    deps += [os.path.join(CSRC, "dbi_internal.h"), os.path.join(CSRC, "dbi_lane.h"), os.path.join(CSRC, "dbi_engine.h"), os.path.join(CSRC, "dbi_fasta.h"), os.path.join(ROOT, "include", "dbindex_hip.h")]
     main = lib_out == LIB
     if not force and _newer(lib_out, deps) and (not main or _newer(LIB_HOOKS, deps)):
         return lib_out

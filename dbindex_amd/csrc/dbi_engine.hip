@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "dbi_engine.h"
+#include "dbi_fasta.h"
 
 namespace dbi {
 
@@ -1177,41 +1178,103 @@ int build_with_ptms(dbi_handle* h, const uint8_t* residues, uint64_t n_res, cons
     return build_tail(h, h->hc.n_kept, h->params.min_mh, h->params.max_mh, n_in + extra, sparse);
 }
 
-// Host residues -> HBM.  A pageable hipMemcpy of a buffer the runtime has not
-// seen pins it first (201 MB: 32 ms the first time, 3.6 ms once pinned;
-// hipHostRegister 7 ms + 3.5 ms; tools/probe/h2d_probe.hip on MI355X), and a
-// caller's freshly parsed proteome is always such a buffer.  So the copy goes
-// through a pinned ring owned by the handle: UP_THREADS threads each copy
+// Host residues -> HBM.  The first large pageable hipMemcpy of a process pays
+// the runtime's one-time setup (~200 ms on MI355X boxes, even for 64 MiB;
+// later ones of a fresh 201-MB buffer ~4.5 ms), and registering the caller's
+// buffer costs ~0.04 ms a MiB (tools/probe/h2d_probe.hip, h2d_ring.hip).  So
+// the copy goes through a pinned ring owned by the handle: UP_THREADS threads each copy
 // every UP_THREADS-th slice into one of their two UP_SLOT slots (waiting for
 // that slot's previous DMA), look for '[' in it on the way (inline PTMs: the
 // caller then takes the PTM path), and queue its DMA on the engine stream.
 // Small inputs take one plain copy.
-constexpr uint64_t UP_SLOT = 1ull << 20;
+constexpr uint64_t UP_SLOT = 2ull << 20;  // (1 MiB: ~6.7 ms for 201 MB, 2 MiB: ~5.1, tools/probe/h2d_ring.hip)
 constexpr int UP_THREADS = 8;
 constexpr uint64_t UP_MIN = 16ull << 20;  // below: one pageable copy
 
+// A parser-owned residue buffer goes to HBM without a staging copy: pinned
+// in UP_REG pieces (2-MiB pages: ~0.1 ms a piece), each piece's DMA queued as
+// soon as it is pinned, all unpinned once the stream has drained (201 MB:
+// ~4.3 ms vs ~6.6 ms through the ring; tools/probe/h2d_ring.hip).  Returns
+// false (nothing left pinned) when the runtime refuses a registration, e.g.
+// of memory the caller registered itself: the ring then copies it.
+constexpr uint64_t UP_REG = 32ull << 20;
+
+// The handle's pinned staging ring (UP_RING bytes) and at least nev events
+// for its slots.  Host pages pinned by registration: hipHostMalloc of the
+// same 16 MiB took ~0.15-0.2 ms a MiB on MI355X boxes, hipHostRegister ~0.04
+// (tools/probe/h2d_probe.hip).
+constexpr uint64_t UP_RING = UP_SLOT * 2 * UP_THREADS;
+
+int ensure_ring(dbi_handle* h, size_t nev) {
+    if (!h->up_host) {
+        void* p = nullptr;
+        if (posix_memalign(&p, 2ull << 20, UP_RING) != 0) return set_error(DBI_E_OOM, "staging ring");
+        (void)madvise(p, UP_RING, MADV_HUGEPAGE);
+        if (hipHostRegister(p, UP_RING, hipHostRegisterDefault) != hipSuccess) {
+            std::free(p);
+            return set_error(DBI_E_HIP, "hipHostRegister of the staging ring failed");
+        }
+        h->up_host = (uint8_t*)p;
+    }
+    while (h->up_ev.size() < nev) {
+        hipEvent_t ev = nullptr;
+        DBI_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        h->up_ev.push_back(ev);
+    }
+    return 0;
+}
+
+bool upload_registered(dbi_handle* h, const uint8_t* residues, uint64_t n_res) {
+    const uintptr_t base = (uintptr_t)residues & ~(uintptr_t)((2ull << 20) - 1);  // (the buffer is 2-MiB aligned)
+    const uint64_t span = (uint64_t)((uintptr_t)residues + n_res - base);
+    std::vector<void*> pinned;
+    bool ok = true;
+    for (uint64_t o = 0; o < span && ok; o += UP_REG) {
+        uint8_t* a = (uint8_t*)(base + o);
+        const uint64_t len = std::min(UP_REG, span - o);
+        if (hipHostRegister(a, len, hipHostRegisterDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            ok = false;
+            break;
+        }
+        pinned.push_back(a);
+        const uint8_t* lo = std::max<const uint8_t*>(a, residues);
+        const uint8_t* hi = std::min<const uint8_t*>(a + len, residues + n_res);
+        if (hi > lo && hipMemcpyAsync(h->res.p + (lo - residues), lo, (size_t)(hi - lo), hipMemcpyHostToDevice,
+                                      h->stream) != hipSuccess)
+            ok = false;
+    }
+    ok = hipStreamSynchronize(h->stream) == hipSuccess && ok;
+    for (void* a : pinned) (void)hipHostUnregister(a);
+    return ok;
+}
+
 int upload_residues(dbi_handle* h, const uint8_t* residues, uint64_t n_res, bool* ptm) {
+    bool ptm_known = false, brackets = false;
+    if (n_res >= UP_MIN && fasta_residue_buffer(residues, n_res, &ptm_known, &brackets)) {
+        if (ptm && !ptm_known) {  // (a parser without AVX-512 did not look): 8 threads scan
+            std::atomic<bool> any{false};
+            std::vector<std::thread> th;
+            for (int t = 0; t < UP_THREADS; ++t)
+                th.emplace_back([&, t] {
+                    const uint64_t a = n_res * (uint64_t)t / UP_THREADS, e = n_res * (uint64_t)(t + 1) / UP_THREADS;
+                    if (e > a && std::memchr(residues + a, '[', e - a)) any = true;
+                });
+            for (auto& x : th) x.join();
+            brackets = any;
+        }
+        if (upload_registered(h, residues, n_res)) {
+            if (ptm) *ptm = brackets;
+            return 0;
+        }
+    }
     if (n_res < UP_MIN) {
         if (ptm) *ptm = n_res && std::memchr(residues, '[', n_res) != nullptr;
         if (n_res) DBI_HIP(hipMemcpyAsync(h->res.p, residues, n_res, hipMemcpyHostToDevice, h->stream));
         return 0;
     }
-    if (!h->up_host) {
-        // host pages pinned by registration: hipHostMalloc of the same 16 MiB
-        // took ~0.15-0.2 ms a MiB on MI355X boxes, hipHostRegister ~0.04
-        // (tools/probe/h2d_probe.hip)
-        void* p = nullptr;
-        const uint64_t bytes = UP_SLOT * 2 * UP_THREADS;
-        if (posix_memalign(&p, 2ull << 20, bytes) != 0) return set_error(DBI_E_OOM, "staging ring");
-        (void)madvise(p, bytes, MADV_HUGEPAGE);
-        if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
-            std::free(p);
-            return set_error(DBI_E_HIP, "hipHostRegister of the staging ring failed");
-        }
-        h->up_host = (uint8_t*)p;
-        h->up_ev.assign(2 * UP_THREADS, nullptr);
-        for (auto& ev : h->up_ev) DBI_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    }
+    int rc;
+    if ((rc = ensure_ring(h, 2 * UP_THREADS))) return rc;
     const uint64_t nslices = (n_res + UP_SLOT - 1) / UP_SLOT;
     const int T = (int)std::min<uint64_t>(UP_THREADS, nslices);
     std::atomic<bool> found{false};
@@ -1261,6 +1324,55 @@ int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const 
     h->inputs_ptm = false;
     return 0;
 }
+
+// The fused one-off build's residue sink (dbi_build_fasta): each parse thread
+// packs into two slots of the handle's pinned ring (UP_RING / (2 x threads)
+// bytes each: 1 MiB at 16 threads), and a filled slot's DMA is queued on the
+// engine stream at once, so the upload runs under the rest of the parse.  The
+// ring's registration runs beside the count pass.
+struct DeviceSink : FastaSink {
+    dbi_handle* h;
+    std::thread reg;
+    int reg_rc = 0;
+    uint64_t slot_bytes = 0;
+    std::vector<uint32_t> k;  // per thread: slots handed out
+    explicit DeviceSink(dbi_handle* hh) : h(hh) {
+        reg = std::thread([this] {
+            (void)hipSetDevice(h->device);
+            reg_rc = ensure_ring(h, 2 * UP_THREADS);
+        });
+    }
+    ~DeviceSink() override {
+        if (reg.joinable()) reg.join();
+    }
+    int sized(uint64_t n_res, uint64_t n_prot, int threads, bool ptm_known, bool ptm, bool* stream) override {
+        *stream = false;
+        if (reg.joinable()) reg.join();
+        if (reg_rc) return reg_rc;
+        if (!ptm_known || ptm) return 0;  // inline PTMs (or a parser that did not look): dbi_build's path
+        if (n_res >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_res must be < 2^32-1 per device: shard the FASTA");
+        if (n_prot >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_prot must be < 2^32-1");
+        int rc;
+        if ((rc = h->res.ensure(n_res + 16)) || (rc = h->poff.ensure(n_prot + 1))) return rc;
+        if ((rc = ensure_ring(h, 2 * (size_t)threads))) return rc;
+        slot_bytes = (UP_RING / (2 * (uint64_t)threads)) & ~((64ull << 10) - 1);
+        if (slot_bytes == 0) return 0;  // (more than 256 threads: not streamed)
+        k.assign(threads, 0);
+        *stream = true;
+        return 0;
+    }
+    uint8_t* slot(int t, uint64_t* cap) override {
+        const uint32_t i = 2 * (uint32_t)t + (k[t] & 1u);
+        if (k[t]++ >= 2) (void)hipEventSynchronize(h->up_ev[i]);  // the slot's last DMA done
+        *cap = slot_bytes;
+        return h->up_host + slot_bytes * i;
+    }
+    bool flush(int, uint64_t at, const uint8_t* p, uint64_t n) override {
+        const uint64_t i = (uint64_t)(p - h->up_host) / slot_bytes;
+        return hipMemcpyAsync(h->res.p + at, p, n, hipMemcpyHostToDevice, h->stream) == hipSuccess &&
+               hipEventRecord(h->up_ev[i], h->stream) == hipSuccess;
+    }
+};
 
 }  // namespace
 
@@ -1470,6 +1582,39 @@ int dbi_build(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint
     if ((rc = begin_build(h, n_res, n_prot))) return rc;
     if ((rc = build_digest(h))) return rc;
     return finish_build(h);
+}
+
+int dbi_build_fasta(dbi_handle* h, const char* path, int threads, dbi_fasta** out) {
+    if (out) *out = nullptr;
+    if (!h || !path) return set_error(DBI_E_INVALID, "NULL argument");
+    DBI_HIP(hipSetDevice(h->device));
+    dbi_fasta* f = nullptr;
+    int rc;
+    {
+        DeviceSink sink(h);
+        rc = fasta_read_core(path, threads, &sink, &f);
+    }
+    if (!rc && f->residues) {  // not streamed (inline PTMs): the two-step path over the host copy
+        rc = dbi_build(h, f->residues, f->n_residues, f->offsets, f->n_proteins);
+    } else if (!rc) {
+        const uint64_t P = f->n_proteins;
+        std::vector<uint32_t> off32(P + 1);
+        for (uint64_t i = 0; i <= P; ++i) off32[i] = (uint32_t)f->offsets[i];
+        if (hipMemcpyAsync(h->poff.p, off32.data(), sizeof(uint32_t) * (P + 1), hipMemcpyHostToDevice, h->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)  // (off32 is a stack vector; the residue DMAs are done too)
+            rc = set_error(DBI_E_HIP, "offset upload failed");
+        if (!rc) {
+            h->d_res = h->res.p;
+            h->d_poff = h->poff.p;
+            h->inputs_resident = true;
+            h->inputs_ptm = false;
+            if (!(rc = begin_build(h, f->n_residues, P)) && !(rc = build_digest(h))) rc = finish_build(h);
+        }
+    }
+    if (out && !rc) *out = f;
+    else dbi_fasta_free(f);
+    return rc;
 }
 
 int dbi_build_device(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, const uint64_t* d_prot_off,

@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -28,8 +29,12 @@
 #if defined(__SSE2__) && !defined(__HIP_DEVICE_COMPILE__)
 #include <emmintrin.h>
 #endif
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+#define DBI_FASTA_AVX512 1
+#endif
 
-#include "../../include/dbindex_hip.h"
+#include "dbi_fasta.h"
 
 namespace dbi {
 int set_error(int code, const std::string& msg);
@@ -50,8 +55,101 @@ inline __m128i ws_bytes16(const char* p) {
 }
 #endif
 
+#ifdef DBI_FASTA_AVX512
+// AVX-512 (VBMI2: byte compress) variants, picked at run time: 64 bytes a
+// step, whitespace as a 64-bit mask, the kept bytes compressed in a register
+// and written by a byte-masked store (never past the bytes it packs); the
+// last partial block by a masked load.  The SSE2 pack's line-end cases
+// (a temporary and a store-forwarded reload per 16 bytes) made packing ~3x
+// slower than counting.
+__attribute__((target("avx512f,avx512bw"))) inline uint64_t ws_mask64(__m512i v) {
+    const __mmask64 sp = _mm512_cmpeq_epi8_mask(v, _mm512_set1_epi8(' '));
+    const __mmask64 ctl = _mm512_cmple_epu8_mask(_mm512_sub_epi8(v, _mm512_set1_epi8(9)), _mm512_set1_epi8(4));
+    return (uint64_t)(sp | ctl);
+}
+
+__attribute__((target("avx512f,avx512bw,popcnt"))) uint64_t count_residues_512(const char* b, uint64_t len) {
+    uint64_t n = 0, i = 0;
+    for (; i + 64 <= len; i += 64) n += 64 - (uint64_t)__builtin_popcountll(ws_mask64(_mm512_loadu_si512(b + i)));
+    if (i < len) {
+        const __mmask64 valid = (__mmask64)(~0ull >> (64 - (len - i)));
+        n += (uint64_t)__builtin_popcountll(~ws_mask64(_mm512_maskz_loadu_epi8(valid, b + i)) & valid);
+    }
+    return n;
+}
+
+__attribute__((target("avx512f,avx512bw,avx512vbmi2,popcnt")))
+uint64_t pack_residues_512(uint8_t* out, const char* b, uint64_t len) {
+    uint64_t n = 0, i = 0;
+    for (; i < len; i += 64) {
+        const __mmask64 valid = len - i >= 64 ? (__mmask64)~0ull : (__mmask64)(~0ull >> (64 - (len - i)));
+        const __m512i v = _mm512_maskz_loadu_epi8(valid, b + i);
+        const __mmask64 keep = (__mmask64)(~ws_mask64(v)) & valid;
+        const uint32_t k = (uint32_t)__builtin_popcountll((uint64_t)keep);
+        if (keep == valid && k == 64) {
+            _mm512_storeu_si512(out + n, v);
+        } else {
+            const __m512i c = _mm512_maskz_compress_epi8(keep, v);
+            _mm512_mask_storeu_epi8(out + n, (__mmask64)(k == 64 ? ~0ull : (1ull << k) - 1ull), c);
+        }
+        n += k;
+    }
+    return n;
+}
+
+// One record's sequence in one pass: from b[s] up to the next record start
+// (a '>' right after a newline) or n, counting (WRITE: packing into out) the
+// non-whitespace bytes; *end = that record start.  (The SSE2 path finds the
+// record start by memchr first, then counts or packs: two passes.)
+template <bool WRITE>
+__attribute__((target("avx512f,avx512bw,avx512vbmi2,popcnt,bmi")))
+uint64_t seq_scan_512(uint8_t* out, const char* b, uint64_t n, uint64_t s, uint64_t* end, uint64_t* brackets) {
+    uint64_t cnt = 0, br = 0;
+    uint64_t prev_nl = s > 0 && b[s - 1] == '\n';
+    for (uint64_t i = s; i < n; i += 64) {
+        const __mmask64 valid = n - i >= 64 ? (__mmask64)~0ull : (__mmask64)(~0ull >> (64 - (n - i)));
+        const __m512i v = _mm512_maskz_loadu_epi8(valid, b + i);
+        const uint64_t nl = (uint64_t)_mm512_cmpeq_epi8_mask(v, _mm512_set1_epi8('\n'));
+        const uint64_t gt = (uint64_t)_mm512_cmpeq_epi8_mask(v, _mm512_set1_epi8('>'));
+        const uint64_t start = gt & ((nl << 1) | prev_nl) & (uint64_t)valid;
+        uint64_t lim = (uint64_t)valid;
+        uint32_t j = 64;
+        if (start) {
+            j = (uint32_t)__builtin_ctzll(start);
+            lim &= j ? ~0ull >> (64 - j) : 0ull;
+        }
+        const uint64_t keep = ~ws_mask64(v) & lim;
+        const uint32_t k = (uint32_t)__builtin_popcountll(keep);
+        if (!WRITE) br |= (uint64_t)_mm512_cmpeq_epi8_mask(v, _mm512_set1_epi8('[')) & keep;  // inline PTMs
+        if (WRITE) {
+            if (k == 64) {
+                _mm512_storeu_si512(out + cnt, v);
+            } else if (k) {
+                const __m512i c = _mm512_maskz_compress_epi8((__mmask64)keep, v);
+                _mm512_mask_storeu_epi8(out + cnt, (__mmask64)((1ull << k) - 1ull), c);
+            }
+        }
+        cnt += k;
+        if (start) {
+            *end = i + j;
+            if (!WRITE) *brackets |= br;
+            return cnt;
+        }
+        prev_nl = nl >> 63;
+    }
+    *end = n;
+    if (!WRITE) *brackets |= br;
+    return cnt;
+}
+
+const bool g_avx512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vbmi2");
+#endif
+
 // non-whitespace bytes of b[0, len)
 uint64_t count_residues(const char* b, uint64_t len) {
+#ifdef DBI_FASTA_AVX512
+    if (g_avx512) return count_residues_512(b, len);
+#endif
     uint64_t n = 0, i = 0;
 #if defined(__SSE2__) && !defined(__HIP_DEVICE_COMPILE__)
     // whitespace bytes counted per byte lane (a mask byte is -1), folded by
@@ -71,6 +169,9 @@ uint64_t count_residues(const char* b, uint64_t len) {
 // the non-whitespace bytes of b[0, len) packed into out; returns their count.
 // Never writes past the bytes it packs (the threads' output ranges abut).
 uint64_t pack_residues(uint8_t* out, const char* b, uint64_t len) {
+#ifdef DBI_FASTA_AVX512
+    if (g_avx512) return pack_residues_512(out, b, len);
+#endif
     uint64_t n = 0, i = 0;
 #if defined(__SSE2__) && !defined(__HIP_DEVICE_COMPILE__)
     for (; i + 16 <= len; i += 16) {
@@ -120,6 +221,7 @@ uint64_t next_record(const char* b, uint64_t n, uint64_t p) {
 struct Part {
     uint64_t lo = 0, hi = 0;          // byte range: records starting in [lo, hi)
     uint64_t n_rec = 0, n_res = 0, n_def = 0, n_uni = 0;
+    bool ptm_known = false, ptm = false;  // (the AVX-512 count pass sees '[' on the way)
 };
 
 // definition of the record at p ('>' at b[p]): [p+1, e) with trailing CR/LF removed; returns the line end
@@ -142,12 +244,39 @@ bool uniprot(const char* d, uint64_t len) {
     return k < sp && k > 3;
 }
 
-// pass over the records starting in [lo, hi); write = false: count only
-template <bool WRITE>
+// Thread t's residue stream into a FastaSink (the fused FASTA build): the
+// records' residues packed into the sink's staging slot, handed over when the
+// next record does not fit; a record longer than a slot goes through a
+// temporary buffer in slot-sized pieces.
+struct SinkCursor {
+    dbi::FastaSink* sink = nullptr;
+    int t = 0;
+    uint8_t* slot = nullptr;
+    uint64_t cap = 0, used = 0, at = 0;  // at: the global residue index of slot[0]
+    bool ok = true;
+    void flush() {
+        if (used) ok = sink->flush(t, at, slot, used) && ok;
+        at += used;
+        used = 0;
+        slot = sink->slot(t, &cap);
+    }
+    uint8_t* room(uint64_t c) {  // c more residues fit (a flush first if not)
+        if (!slot || used + c > cap) flush();
+        return c <= cap ? slot + used : nullptr;
+    }
+};
+
+// pass over the records starting in [lo, hi): MODE 0 counts (and, given
+// cnts, keeps every record's residue count), 1 writes the residues into res,
+// 2 streams them through cur (record sizes from cnts)
+template <int MODE>
 void scan_part(const char* b, uint64_t n, Part& pt, uint8_t* res, uint64_t* off, char* defs, uint64_t* doff,
-               uint64_t res0, uint64_t rec0, uint64_t def0) {
+               uint64_t res0, uint64_t rec0, uint64_t def0, std::vector<uint32_t>* cnts = nullptr,
+               SinkCursor* cur = nullptr) {
+    constexpr bool WRITE = MODE != 0;
     uint64_t p = pt.lo;
-    uint64_t nr = 0, nres = 0, ndef = 0, nuni = 0;
+    uint64_t nr = 0, nres = 0, ndef = 0, nuni = 0, brackets = 0;
+    std::vector<uint8_t> big;  // MODE 2: a record longer than a slot
     while (p < pt.hi) {
         uint64_t de;
         const uint64_t le = def_range(b, n, p, &de);
@@ -162,8 +291,40 @@ void scan_part(const char* b, uint64_t n, Part& pt, uint8_t* res, uint64_t* off,
         ndef += dl;
         // sequence: every non-whitespace byte up to the next record start
         const uint64_t s0 = le < n ? le + 1 : n;
-        const uint64_t s1 = next_record(b, n, le < n ? le : n);
-        nres += WRITE ? pack_residues(res + res0 + nres, b + s0, s1 - s0) : count_residues(b + s0, s1 - s0);
+        uint64_t s1, c;
+        uint8_t* dst = nullptr;
+        if (MODE == 1) dst = res + res0 + nres;
+        if (MODE == 2) {
+            dst = cur->room((*cnts)[nr]);
+            if (!dst) {
+                big.resize((*cnts)[nr]);
+                dst = big.data();
+            }
+        }
+#ifdef DBI_FASTA_AVX512
+        if (g_avx512) {
+            c = seq_scan_512<WRITE>(dst, b, n, s0, &s1, &brackets);
+        } else
+#endif
+        {
+            s1 = next_record(b, n, le < n ? le : n);
+            c = WRITE ? pack_residues(dst, b + s0, s1 - s0) : count_residues(b + s0, s1 - s0);
+        }
+        if (MODE == 0 && cnts) cnts->push_back((uint32_t)c);
+        if (MODE == 2) {
+            if (dst == big.data()) {
+                for (uint64_t k = 0; k < c;) {
+                    const uint64_t piece = std::min<uint64_t>(c - k, std::max<uint64_t>(cur->cap, 1));
+                    uint8_t* q = cur->room(piece);
+                    std::memcpy(q, big.data() + k, piece);
+                    cur->used += piece;
+                    k += piece;
+                }
+            } else {
+                cur->used += c;
+            }
+        }
+        nres += c;
         ++nr;
         p = s1;
     }
@@ -172,6 +333,10 @@ void scan_part(const char* b, uint64_t n, Part& pt, uint8_t* res, uint64_t* off,
         pt.n_res = nres;
         pt.n_def = ndef;
         pt.n_uni = nuni;
+#ifdef DBI_FASTA_AVX512
+        pt.ptm_known = g_avx512;
+#endif
+        pt.ptm = brackets != 0;
     }
 }
 
@@ -193,12 +358,34 @@ int parse_threads(int threads) {
     return threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 }
 
+// The live dbi_fasta residue buffers on 2-MiB pages: dbi_build registers
+// such a buffer for DMA directly (~0.6 ms for 201 MB on 2-MiB pages; ~10 ms
+// on 4-KiB pages, which go through the engine's pinned ring instead).
+struct ResidueBuf {
+    uintptr_t p;
+    uint64_t n;
+    bool ptm_known, ptm;
+};
+std::mutex g_bufs_mu;
+std::vector<ResidueBuf> g_bufs;
+
 }  // namespace
 
-extern "C" {
+namespace dbi {
+bool fasta_residue_buffer(const void* p, uint64_t n, bool* ptm_known, bool* ptm) {
+    std::lock_guard<std::mutex> lk(g_bufs_mu);
+    const uintptr_t a = (uintptr_t)p;
+    for (const ResidueBuf& r : g_bufs)
+        if (a >= r.p && a + n <= r.p + r.n) {
+            *ptm_known = r.ptm_known;
+            *ptm = r.ptm;
+            return true;
+        }
+    return false;
+}
 
-int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out) {
-    if (!out || (!buf && len)) return dbi::set_error(DBI_E_INVALID, "NULL argument");
+int fasta_parse_core(const char* buf, uint64_t len, int threads, FastaSink* sink, dbi_fasta** out) {
+    if (!out || (!buf && len)) return set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
     int T = parse_threads(threads);
     T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)T, len / (1u << 20) + 1));  // >= 1 MiB per thread
@@ -216,8 +403,12 @@ int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out)
         fn(0);
         for (auto& x : th) x.join();
     };
-    run([&](int t) { scan_part<false>(buf, len, parts[t], nullptr, nullptr, nullptr, nullptr, 0, 0, 0); });
+    std::vector<std::vector<uint32_t>> cnts(sink ? T : 0);
+    run([&](int t) {
+        scan_part<0>(buf, len, parts[t], nullptr, nullptr, nullptr, nullptr, 0, 0, 0, sink ? &cnts[t] : nullptr);
+    });
     uint64_t R = 0, P = 0, D = 0, U = 0;
+    bool ptm_known = true, ptm = false;
     std::vector<uint64_t> r0(T), p0(T), d0(T);
     for (int t = 0; t < T; ++t) {
         r0[t] = R;
@@ -227,33 +418,77 @@ int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out)
         P += parts[t].n_rec;
         D += parts[t].n_def;
         U += parts[t].n_uni;
+        ptm_known &= parts[t].ptm_known;
+        ptm |= parts[t].ptm;
+    }
+    bool stream = false;
+    if (sink) {
+        const int rc = sink->sized(R, P, T, ptm_known, ptm, &stream);
+        if (rc) return rc;
     }
     dbi_fasta* f = (dbi_fasta*)std::calloc(1, sizeof(dbi_fasta));
-    if (!f) return dbi::set_error(DBI_E_OOM, "calloc");
+    if (!f) return set_error(DBI_E_OOM, "calloc");
     f->n_proteins = P;
     f->n_residues = R;
     f->n_uniprot = U;
-    f->residues = (uint8_t*)alloc_big(std::max<uint64_t>(R, 1) + 16);
+    f->residues = stream ? nullptr : (uint8_t*)alloc_big(std::max<uint64_t>(R, 1) + 16);
     f->offsets = (uint64_t*)std::malloc(8 * (P + 1));
     f->defs = (char*)std::malloc(std::max<uint64_t>(D, 1));
     f->def_off = (uint64_t*)std::malloc(8 * (P + 1));
-    if (!f->residues || !f->offsets || !f->defs || !f->def_off) {
+    if ((!stream && !f->residues) || !f->offsets || !f->defs || !f->def_off) {
         dbi_fasta_free(f);
-        return dbi::set_error(DBI_E_OOM, "malloc");
+        return set_error(DBI_E_OOM, "malloc");
     }
-    run([&](int t) {
-        scan_part<true>(buf, len, parts[t], f->residues, f->offsets, f->defs, f->def_off, r0[t], p0[t], d0[t]);
-    });
+    if (stream) {
+        std::vector<SinkCursor> cur(T);
+        run([&](int t) {
+            cur[t].sink = sink;
+            cur[t].t = t;
+            cur[t].at = r0[t];
+            scan_part<2>(buf, len, parts[t], nullptr, f->offsets, f->defs, f->def_off, r0[t], p0[t], d0[t], &cnts[t],
+                         &cur[t]);
+            if (cur[t].used) cur[t].ok = sink->flush(t, cur[t].at, cur[t].slot, cur[t].used) && cur[t].ok;
+        });
+        for (const SinkCursor& c : cur)
+            if (!c.ok) {
+                dbi_fasta_free(f);
+                return set_error(DBI_E_HIP, "streaming the FASTA residues to the device failed");
+            }
+    } else {
+        run([&](int t) {
+            scan_part<1>(buf, len, parts[t], f->residues, f->offsets, f->defs, f->def_off, r0[t], p0[t], d0[t]);
+        });
+        std::memset(f->residues + R, 0, 16);
+        if (R + 16 >= (2u << 20)) {  // (alloc_big's 2-MiB pages)
+            std::lock_guard<std::mutex> lk(g_bufs_mu);
+            g_bufs.push_back({(uintptr_t)f->residues, R + 16, ptm_known, ptm});
+        }
+    }
     f->offsets[P] = R;
     f->def_off[P] = D;
-    std::memset(f->residues + R, 0, 16);
     *out = f;
     return 0;
 }
+}  // namespace dbi
 
-// The file is read by T threads with pread into one huge-page buffer (an
-// mmap of it would fault 4-KiB page-cache pages in one by one), then parsed.
-int dbi_fasta_read(const char* path, int threads, dbi_fasta** out) {
+extern "C" {
+
+int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out) {
+    return dbi::fasta_parse_core(buf, len, threads, nullptr, out);
+}
+
+// The file is mapped read-only and parsed in place: the parse threads' first
+// touches map the page-cache pages (fault-around, in parallel), with no copy
+// and no fresh pages to zero.  (A parallel pread into a huge-page buffer,
+// the previous way, paid a 257-MB copy and the buffer's page faults: 52-66
+// vs 35-43 ms for the SwissProt-scale file on 8 threads.)  Files that cannot
+// be mapped are read with pread.
+int dbi_fasta_read(const char* path, int threads, dbi_fasta** out) { return dbi::fasta_read_core(path, threads, nullptr, out); }
+
+}  // extern "C"
+
+namespace dbi {
+int fasta_read_core(const char* path, int threads, FastaSink* sink, dbi_fasta** out) {
     if (!path || !out) return dbi::set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
     const int fd = ::open(path, O_RDONLY);
@@ -264,6 +499,16 @@ int dbi_fasta_read(const char* path, int threads, dbi_fasta** out) {
         return dbi::set_error(DBI_E_INVALID, std::string("cannot stat FASTA file ") + path);
     }
     const uint64_t len = (uint64_t)st.st_size;
+    if (len > 0) {
+        void* m = ::mmap(nullptr, (size_t)len, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m != MAP_FAILED) {
+            ::close(fd);
+            (void)::madvise(m, (size_t)len, MADV_SEQUENTIAL);
+            const int rc = fasta_parse_core((const char*)m, len, threads, sink, out);
+            ::munmap(m, (size_t)len);
+            return rc;
+        }
+    }
     char* buf = (char*)alloc_big(std::max<uint64_t>(len, 1));
     if (!buf) {
         ::close(fd);
@@ -290,13 +535,24 @@ int dbi_fasta_read(const char* path, int threads, dbi_fasta** out) {
     ::close(fd);
     int rc;
     if (std::count(bad.begin(), bad.end(), 1)) rc = dbi::set_error(DBI_E_INVALID, std::string("cannot read FASTA file ") + path);
-    else rc = dbi_fasta_parse(buf, len, threads, out);
+    else rc = fasta_parse_core(buf, len, threads, sink, out);
     std::free(buf);
     return rc;
 }
+}  // namespace dbi
+
+extern "C" {
 
 void dbi_fasta_free(dbi_fasta* f) {
     if (!f) return;
+    {
+        std::lock_guard<std::mutex> lk(g_bufs_mu);
+        for (size_t i = 0; i < g_bufs.size(); ++i)
+            if (g_bufs[i].p == (uintptr_t)f->residues) {
+                g_bufs.erase(g_bufs.begin() + (long)i);
+                break;
+            }
+    }
     std::free(f->residues);
     std::free(f->offsets);
     std::free(f->defs);

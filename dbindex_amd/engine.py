@@ -86,6 +86,26 @@ class Engine:
         check(_native.lib().dbi_build(self.h, _p(res), res.shape[0], _p(off), off.shape[0] - 1))
         return self.stats()
 
+    def build_fasta(self, path: str, threads: int = 0, with_defs: bool = False):
+        """The one-off build from a FASTA file (dbi_build_fasta: parse and
+        upload fused, DBIndexer.run).  Returns (BuildStats, offsets, defs):
+        the file's protein offsets (u64, P+1) and, with_defs, its definitions;
+        the residues stay in HBM."""
+        out = ctypes.POINTER(_native.DbiFasta)()
+        check(_native.lib().dbi_build_fasta(self.h, path.encode(), threads, ctypes.byref(out)))
+        try:
+            f = out.contents
+            P = int(f.n_proteins)
+            offs = np.ctypeslib.as_array(f.offsets, shape=(P + 1,)).astype(np.uint64)
+            defs = []
+            if with_defs and P:
+                doff = np.ctypeslib.as_array(f.def_off, shape=(P + 1,))
+                raw = ctypes.string_at(f.defs, int(doff[-1])).decode("latin-1")
+                defs = [raw[int(doff[i]):int(doff[i + 1])] for i in range(P)]
+        finally:
+            _native.lib().dbi_fasta_free(out)
+        return self.stats(), offs, defs
+
     def build_device(self, d_residues: int, n_res: int, d_offsets: int, n_prot: int,
                      stream: int = 0) -> BuildStats:
         check(_native.lib().dbi_build_device(self.h, ctypes.c_void_p(d_residues), n_res,

@@ -76,6 +76,63 @@ def test_fasta_file_build_matches_oracle(engine_cls, tmp_path, n):
         assert_queries_equal(eng, oix, m, t, f"fasta file {n} queries")
 
 
+@pytest.mark.parametrize("ptm", [False, True])
+def test_fasta_file_registered_upload(engine_cls, tmp_path, ptm):
+    """A parsed proteome above the upload's 16-MiB ring threshold: dbi_build
+    pins the parser's own 2-MiB-page buffer and DMAs it directly (no staging
+    copy), taking the parser's '[' finding for the inline-PTM decision; the
+    same residues from a plain numpy copy go through the pinned ring.  Both
+    indexes equal the oracle's."""
+    pp = fasta.config("swissprot").slice(0, 60000)
+    seqs = pp.sequences()
+    if ptm:  # a few inline formulas far into the file (DBIndexer.java:288-303)
+        for i in (41000, 52345, 59999):
+            s = seqs[i]
+            seqs[i] = s[:5] + "[HPO3]" + s[5:]
+        pp = fasta.PackedProteins.from_sequences(seqs)
+    path = str(tmp_path / "big.fasta")
+    with open(path, "w") as fh:
+        fasta.write_fasta(pp, fh)
+    got = fasta.read_fasta(path, threads=8, with_defs=False)
+    assert got.n_residues > (16 << 20) and np.array_equal(got.residues, pp.residues)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, pp.residues, pp.offsets)
+    copy = fasta.PackedProteins(np.array(got.residues), np.array(got.offsets))
+    with engine_cls(cp) as eng:
+        for src, what in ((got, "parser buffer"), (copy, "numpy copy"), (got, "parser buffer again")):
+            eng.build(src)
+            assert_index_equal(eng, oix, f"{what} ptm={ptm}")
+
+
+@pytest.mark.parametrize("n,threads,ptm", [(1000, 0, False), (60000, 3, False), (60000, 16, False),
+                                           (60000, 0, True)])
+def test_build_fasta_fused(engine_cls, tmp_path, n, threads, ptm):
+    """dbi_build_fasta (parse + upload fused: the parse threads stream their
+    packed residues through the pinned ring as they go) builds the index of
+    the file that dbi_fasta_read + dbi_build builds: the oracle's, cold and
+    warm, with the file's offsets and definitions handed back; a file with
+    inline '[formula]' PTMs takes dbi_build's PTM path."""
+    pp = fasta.config("1k") if n <= 1000 else fasta.config("swissprot").slice(0, n)
+    if ptm:
+        seqs = pp.sequences()
+        for i in (7, n // 2, n - 1):
+            seqs[i] = seqs[i][:5] + "[HPO3]" + seqs[i][5:]
+        pp = fasta.PackedProteins.from_sequences(seqs)
+    path = str(tmp_path / "fused.fasta")
+    _write_swissprot_style(path, pp)
+    items, res, off = _iter_parse(path)
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    oix = cref.Index(cp, res, off)
+    with engine_cls(cp) as eng:
+        for phase in ("cold", "warm"):
+            st, offs, defs = eng.build_fasta(path, threads=threads, with_defs=True)
+            assert np.array_equal(offs, off) and defs == [d.rstrip("\r") for d, _ in items]
+            assert st.n_total == oix.n_total
+            assert_index_equal(eng, oix, f"build_fasta {n} t{threads} ptm={ptm} [{phase}]")
+        m, t = query_masses(oix, 2000, seed=5)
+        assert_queries_equal(eng, oix, m, t, f"build_fasta {n} queries")
+
+
 def test_indexer_run_on_a_fasta_file(tmp_path):
     """DBIndexer.run(path): proteins in file order, ids = FASTA positions, the
     store answers like the oracle built from the reference-semantics parse."""

@@ -212,6 +212,41 @@ def test_native_fasta_parser_matches_iter_fasta(threads):
         assert got.n_uniprot == sum(fasta.uniprot_accession(d) is not None for d, _ in want)
 
 
+def test_native_fasta_parser_random_layouts(tmp_path):
+    """Seeded random FASTA texts against iter_fasta: records whose lines and
+    whitespace (spaces, tabs, CR, VT, FF, blank lines) fall at every offset of
+    the parser's 64-byte blocks, '>' inside sequence lines and definitions,
+    empty records, with and without a final newline; parsed from memory and
+    read from a file (mapped), on 1 and 5 threads."""
+    rng = np.random.default_rng(17)
+    ws = [" ", "\t", "\r", "\x0b", "\x0c", "\n", "\n\n", "\r\n"]
+    for case in range(12):
+        parts = [] if case % 3 else ["preamble line\n"]
+        for r in range(int(rng.integers(1, 60))):
+            d = "".join(rng.choice(list("ABC|x >"), int(rng.integers(0, 30))))
+            parts.append(">" + d + ("\r\n" if rng.random() < 0.2 else "\n"))
+            n = int(rng.integers(0, 400))
+            seq = []
+            for _ in range(n):
+                seq.append(str(rng.choice(list("ACDEFGHIKLMNPQRSTVWY>"), p=[0.0495] * 20 + [0.01])))
+                if rng.random() < 0.04:
+                    seq.append(str(rng.choice(ws)))
+                if rng.random() < 1 / 61:
+                    seq.append("\n")
+            parts.append("".join(seq) + ("\n" if rng.random() < 0.8 else ""))
+        t = "".join(parts)
+        if rng.random() < 0.5:
+            t = t.rstrip("\n")
+        want = list(fasta.iter_fasta(io.StringIO(t)))
+        path = tmp_path / f"r{case}.fasta"
+        path.write_bytes(t.encode())
+        for threads in (1, 5):
+            for got in (fasta.parse_fasta(t, threads=threads), fasta.read_fasta(str(path), threads=threads)):
+                assert got.n_proteins == len(want), (case, threads)
+                assert got.defs == [d for d, _ in want]
+                assert got.sequences() == [s for _, s in want], (case, threads)
+
+
 def test_native_fasta_read_file(tmp_path):
     pp = fasta.config("1k")
     path = tmp_path / "p.fasta"

@@ -11,6 +11,7 @@
 #   sq        SQ counter pass (SwissProt)
 #   semi      semi bench, semi trace + PMC
 #   h2d       tools/probe/h2d_probe (host-to-device copy paths)
+#   ring      tools/probe/h2d_ring (the residue upload's staged-ring variants)
 #   dclock    digest phase clocks (tools/exp/dclock.so)
 #   noverify  chunk-sort traffic with / without string verification (tools/exp/noverify.so)
 #   ab_prev   bench of tools/exp/prev.so (the last commit) against the tree, twice each
@@ -66,6 +67,7 @@ for w in "$@"; do
              step semi_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/semi/pmc_write" -o run \
                 -- python3 bench.py --config semi --steps 2 --warmup 4 --queries 0 --no-cpu-baseline --no-cold ;;
     h2d)     step h2d 180 ./tools/probe/h2d_probe ;;
+    ring)    step ring 240 ./tools/probe/h2d_ring ;;
     dclock)  export DBI_LIB_PATH=tools/exp/dclock.so
              step dclock 300 python tools/digest_phase.py
              unset DBI_LIB_PATH ;;
