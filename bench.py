@@ -615,37 +615,16 @@ def cold_legs(eng, prm, pp, d_res, d_off, dev: int, config: str, options=None) -
             synchronize(dev)
             t_built = time.perf_counter()
         t2 = time.perf_counter()
-        same = rp.n_proteins == pp.n_proteins and rp.n_residues == pp.n_residues and st3.n_total == st.n_total
-        del rp
-        # the fused one-off path (dbi_build_fasta: the parse threads stream
-        # their residues to HBM as they go): a fresh engine, then the file
-        t3 = time.perf_counter()
-        with Engine(prm, device=dev, options=options) as e4:
-            e4.set_timing(False)
-            t_open4 = time.perf_counter()
-            st4, offs4, _ = e4.build_fasta(path, threads=threads)
-            synchronize(dev)
-            t_built4 = time.perf_counter()
-        same4 = len(offs4) == pp.n_proteins + 1 and int(offs4[-1]) == pp.n_residues and st4.n_total == st.n_total
+    same = rp.n_proteins == pp.n_proteins and rp.n_residues == pp.n_residues and st3.n_total == st.n_total
     # end to end = FASTA file -> index resident in HBM, ready for queries
     # (DBIndexer.run then keeps it); the engine's teardown is reported apart
-    two_step = dict(ms=1e3 * (t_built - t0), fasta_read_ms=1e3 * (t1 - t0), build_ms=1e3 * (t_built - t1),
-                    open_ms=1e3 * (t_open - t1), dbi_build_ms=1e3 * (t_built - t_open),
-                    close_ms_not_included=1e3 * (t2 - t_built), same_proteome=bool(same),
-                    kind="dbi_fasta_read of the written FASTA, then a fresh engine's dbi_build (host residues: "
-                         "H2D + cold build, allocations included)")
-    call_ms = 1e3 * (t_built4 - t_open4)
-    dev_build_ms = float(st4.build_ms)  # (begin_build -> index ready, host clock)
-    out["end_to_end"] = dict(ms=1e3 * (t_built4 - t3), fasta_read_ms=call_ms - dev_build_ms,
-                             build_ms=1e3 * (t_open4 - t3) + dev_build_ms, open_ms=1e3 * (t_open4 - t3),
-                             build_fasta_ms=call_ms, fasta_bytes=size, fasta_write_s_untimed=write_s,
-                             parser_threads=threads, peptides_per_s=st4.n_total / (t_built4 - t3),
-                             same_proteome=bool(same4),
-                             kind="a fresh engine (dbi_open), then dbi_build_fasta of the written FASTA: parse with "
-                                  "the residues streamed to HBM as they are packed, then the cold build; "
-                                  "fasta_read_ms = parse + overlapped upload, build_ms = open + the build after "
-                                  "the parse",
-                             two_step=two_step)
+    out["end_to_end"] = dict(ms=1e3 * (t_built - t0), fasta_read_ms=1e3 * (t1 - t0), build_ms=1e3 * (t_built - t1),
+                             open_ms=1e3 * (t_open - t1), dbi_build_ms=1e3 * (t_built - t_open),
+                             close_ms_not_included=1e3 * (t2 - t_built),
+                             fasta_bytes=size, fasta_write_s_untimed=write_s, parser_threads=threads,
+                             peptides_per_s=st3.n_total / (t_built - t0), same_proteome=bool(same),
+                             kind="dbi_fasta_read of the written FASTA, then a fresh engine's dbi_build "
+                                  "(host residues: H2D + cold build, allocations included)")
     return out
 
 

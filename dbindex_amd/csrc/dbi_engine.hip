@@ -1199,13 +1199,12 @@ constexpr uint64_t UP_MIN = 16ull << 20;  // below: one pageable copy
 // of memory the caller registered itself: the ring then copies it.
 constexpr uint64_t UP_REG = 32ull << 20;
 
-// The handle's pinned staging ring (UP_RING bytes) and at least nev events
-// for its slots.  Host pages pinned by registration: hipHostMalloc of the
-// same 16 MiB took ~0.15-0.2 ms a MiB on MI355X boxes, hipHostRegister ~0.04
-// (tools/probe/h2d_probe.hip).
+// The handle's pinned staging ring and its slots' events.  Host pages pinned
+// by registration: hipHostMalloc of the same 16 MiB took ~0.15-0.2 ms a MiB
+// on MI355X boxes, hipHostRegister ~0.04 (tools/probe/h2d_probe.hip).
 constexpr uint64_t UP_RING = UP_SLOT * 2 * UP_THREADS;
 
-int ensure_ring(dbi_handle* h, size_t nev) {
+int ensure_ring(dbi_handle* h) {
     if (!h->up_host) {
         void* p = nullptr;
         if (posix_memalign(&p, 2ull << 20, UP_RING) != 0) return set_error(DBI_E_OOM, "staging ring");
@@ -1216,7 +1215,7 @@ int ensure_ring(dbi_handle* h, size_t nev) {
         }
         h->up_host = (uint8_t*)p;
     }
-    while (h->up_ev.size() < nev) {
+    while (h->up_ev.size() < 2 * UP_THREADS) {
         hipEvent_t ev = nullptr;
         DBI_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         h->up_ev.push_back(ev);
@@ -1274,7 +1273,7 @@ int upload_residues(dbi_handle* h, const uint8_t* residues, uint64_t n_res, bool
         return 0;
     }
     int rc;
-    if ((rc = ensure_ring(h, 2 * UP_THREADS))) return rc;
+    if ((rc = ensure_ring(h))) return rc;
     const uint64_t nslices = (n_res + UP_SLOT - 1) / UP_SLOT;
     const int T = (int)std::min<uint64_t>(UP_THREADS, nslices);
     std::atomic<bool> found{false};
@@ -1324,55 +1323,6 @@ int upload_inputs(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const 
     h->inputs_ptm = false;
     return 0;
 }
-
-// The fused one-off build's residue sink (dbi_build_fasta): each parse thread
-// packs into two slots of the handle's pinned ring (UP_RING / (2 x threads)
-// bytes each: 1 MiB at 16 threads), and a filled slot's DMA is queued on the
-// engine stream at once, so the upload runs under the rest of the parse.  The
-// ring's registration runs beside the count pass.
-struct DeviceSink : FastaSink {
-    dbi_handle* h;
-    std::thread reg;
-    int reg_rc = 0;
-    uint64_t slot_bytes = 0;
-    std::vector<uint32_t> k;  // per thread: slots handed out
-    explicit DeviceSink(dbi_handle* hh) : h(hh) {
-        reg = std::thread([this] {
-            (void)hipSetDevice(h->device);
-            reg_rc = ensure_ring(h, 2 * UP_THREADS);
-        });
-    }
-    ~DeviceSink() override {
-        if (reg.joinable()) reg.join();
-    }
-    int sized(uint64_t n_res, uint64_t n_prot, int threads, bool ptm_known, bool ptm, bool* stream) override {
-        *stream = false;
-        if (reg.joinable()) reg.join();
-        if (reg_rc) return reg_rc;
-        if (!ptm_known || ptm) return 0;  // inline PTMs (or a parser that did not look): dbi_build's path
-        if (n_res >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_res must be < 2^32-1 per device: shard the FASTA");
-        if (n_prot >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_prot must be < 2^32-1");
-        int rc;
-        if ((rc = h->res.ensure(n_res + 16)) || (rc = h->poff.ensure(n_prot + 1))) return rc;
-        if ((rc = ensure_ring(h, 2 * (size_t)threads))) return rc;
-        slot_bytes = (UP_RING / (2 * (uint64_t)threads)) & ~((64ull << 10) - 1);
-        if (slot_bytes == 0) return 0;  // (more than 256 threads: not streamed)
-        k.assign(threads, 0);
-        *stream = true;
-        return 0;
-    }
-    uint8_t* slot(int t, uint64_t* cap) override {
-        const uint32_t i = 2 * (uint32_t)t + (k[t] & 1u);
-        if (k[t]++ >= 2) (void)hipEventSynchronize(h->up_ev[i]);  // the slot's last DMA done
-        *cap = slot_bytes;
-        return h->up_host + slot_bytes * i;
-    }
-    bool flush(int, uint64_t at, const uint8_t* p, uint64_t n) override {
-        const uint64_t i = (uint64_t)(p - h->up_host) / slot_bytes;
-        return hipMemcpyAsync(h->res.p + at, p, n, hipMemcpyHostToDevice, h->stream) == hipSuccess &&
-               hipEventRecord(h->up_ev[i], h->stream) == hipSuccess;
-    }
-};
 
 }  // namespace
 
@@ -1587,31 +1537,9 @@ int dbi_build(dbi_handle* h, const uint8_t* residues, uint64_t n_res, const uint
 int dbi_build_fasta(dbi_handle* h, const char* path, int threads, dbi_fasta** out) {
     if (out) *out = nullptr;
     if (!h || !path) return set_error(DBI_E_INVALID, "NULL argument");
-    DBI_HIP(hipSetDevice(h->device));
     dbi_fasta* f = nullptr;
-    int rc;
-    {
-        DeviceSink sink(h);
-        rc = fasta_read_core(path, threads, &sink, &f);
-    }
-    if (!rc && f->residues) {  // not streamed (inline PTMs): the two-step path over the host copy
-        rc = dbi_build(h, f->residues, f->n_residues, f->offsets, f->n_proteins);
-    } else if (!rc) {
-        const uint64_t P = f->n_proteins;
-        std::vector<uint32_t> off32(P + 1);
-        for (uint64_t i = 0; i <= P; ++i) off32[i] = (uint32_t)f->offsets[i];
-        if (hipMemcpyAsync(h->poff.p, off32.data(), sizeof(uint32_t) * (P + 1), hipMemcpyHostToDevice, h->stream) !=
-                hipSuccess ||
-            hipStreamSynchronize(h->stream) != hipSuccess)  // (off32 is a stack vector; the residue DMAs are done too)
-            rc = set_error(DBI_E_HIP, "offset upload failed");
-        if (!rc) {
-            h->d_res = h->res.p;
-            h->d_poff = h->poff.p;
-            h->inputs_resident = true;
-            h->inputs_ptm = false;
-            if (!(rc = begin_build(h, f->n_residues, P)) && !(rc = build_digest(h))) rc = finish_build(h);
-        }
-    }
+    int rc = dbi_fasta_read(path, threads, &f);
+    if (!rc) rc = dbi_build(h, f->residues, f->n_residues, f->offsets, f->n_proteins);
     if (out && !rc) *out = f;
     else dbi_fasta_free(f);
     return rc;

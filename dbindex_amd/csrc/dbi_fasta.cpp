@@ -34,6 +34,7 @@
 #define DBI_FASTA_AVX512 1
 #endif
 
+#include "../../include/dbindex_hip.h"
 #include "dbi_fasta.h"
 
 namespace dbi {
@@ -244,39 +245,12 @@ bool uniprot(const char* d, uint64_t len) {
     return k < sp && k > 3;
 }
 
-// Thread t's residue stream into a FastaSink (the fused FASTA build): the
-// records' residues packed into the sink's staging slot, handed over when the
-// next record does not fit; a record longer than a slot goes through a
-// temporary buffer in slot-sized pieces.
-struct SinkCursor {
-    dbi::FastaSink* sink = nullptr;
-    int t = 0;
-    uint8_t* slot = nullptr;
-    uint64_t cap = 0, used = 0, at = 0;  // at: the global residue index of slot[0]
-    bool ok = true;
-    void flush() {
-        if (used) ok = sink->flush(t, at, slot, used) && ok;
-        at += used;
-        used = 0;
-        slot = sink->slot(t, &cap);
-    }
-    uint8_t* room(uint64_t c) {  // c more residues fit (a flush first if not)
-        if (!slot || used + c > cap) flush();
-        return c <= cap ? slot + used : nullptr;
-    }
-};
-
-// pass over the records starting in [lo, hi): MODE 0 counts (and, given
-// cnts, keeps every record's residue count), 1 writes the residues into res,
-// 2 streams them through cur (record sizes from cnts)
-template <int MODE>
+// pass over the records starting in [lo, hi); write = false: count only
+template <bool WRITE>
 void scan_part(const char* b, uint64_t n, Part& pt, uint8_t* res, uint64_t* off, char* defs, uint64_t* doff,
-               uint64_t res0, uint64_t rec0, uint64_t def0, std::vector<uint32_t>* cnts = nullptr,
-               SinkCursor* cur = nullptr) {
-    constexpr bool WRITE = MODE != 0;
+               uint64_t res0, uint64_t rec0, uint64_t def0) {
     uint64_t p = pt.lo;
     uint64_t nr = 0, nres = 0, ndef = 0, nuni = 0, brackets = 0;
-    std::vector<uint8_t> big;  // MODE 2: a record longer than a slot
     while (p < pt.hi) {
         uint64_t de;
         const uint64_t le = def_range(b, n, p, &de);
@@ -291,40 +265,16 @@ void scan_part(const char* b, uint64_t n, Part& pt, uint8_t* res, uint64_t* off,
         ndef += dl;
         // sequence: every non-whitespace byte up to the next record start
         const uint64_t s0 = le < n ? le + 1 : n;
-        uint64_t s1, c;
-        uint8_t* dst = nullptr;
-        if (MODE == 1) dst = res + res0 + nres;
-        if (MODE == 2) {
-            dst = cur->room((*cnts)[nr]);
-            if (!dst) {
-                big.resize((*cnts)[nr]);
-                dst = big.data();
-            }
-        }
+        uint64_t s1;
 #ifdef DBI_FASTA_AVX512
         if (g_avx512) {
-            c = seq_scan_512<WRITE>(dst, b, n, s0, &s1, &brackets);
+            nres += seq_scan_512<WRITE>(WRITE ? res + res0 + nres : nullptr, b, n, s0, &s1, &brackets);
         } else
 #endif
         {
             s1 = next_record(b, n, le < n ? le : n);
-            c = WRITE ? pack_residues(dst, b + s0, s1 - s0) : count_residues(b + s0, s1 - s0);
+            nres += WRITE ? pack_residues(res + res0 + nres, b + s0, s1 - s0) : count_residues(b + s0, s1 - s0);
         }
-        if (MODE == 0 && cnts) cnts->push_back((uint32_t)c);
-        if (MODE == 2) {
-            if (dst == big.data()) {
-                for (uint64_t k = 0; k < c;) {
-                    const uint64_t piece = std::min<uint64_t>(c - k, std::max<uint64_t>(cur->cap, 1));
-                    uint8_t* q = cur->room(piece);
-                    std::memcpy(q, big.data() + k, piece);
-                    cur->used += piece;
-                    k += piece;
-                }
-            } else {
-                cur->used += c;
-            }
-        }
-        nres += c;
         ++nr;
         p = s1;
     }
@@ -383,9 +333,12 @@ bool fasta_residue_buffer(const void* p, uint64_t n, bool* ptm_known, bool* ptm)
         }
     return false;
 }
+}  // namespace dbi
 
-int fasta_parse_core(const char* buf, uint64_t len, int threads, FastaSink* sink, dbi_fasta** out) {
-    if (!out || (!buf && len)) return set_error(DBI_E_INVALID, "NULL argument");
+extern "C" {
+
+int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out) {
+    if (!out || (!buf && len)) return dbi::set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
     int T = parse_threads(threads);
     T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)T, len / (1u << 20) + 1));  // >= 1 MiB per thread
@@ -403,10 +356,7 @@ int fasta_parse_core(const char* buf, uint64_t len, int threads, FastaSink* sink
         fn(0);
         for (auto& x : th) x.join();
     };
-    std::vector<std::vector<uint32_t>> cnts(sink ? T : 0);
-    run([&](int t) {
-        scan_part<0>(buf, len, parts[t], nullptr, nullptr, nullptr, nullptr, 0, 0, 0, sink ? &cnts[t] : nullptr);
-    });
+    run([&](int t) { scan_part<false>(buf, len, parts[t], nullptr, nullptr, nullptr, nullptr, 0, 0, 0); });
     uint64_t R = 0, P = 0, D = 0, U = 0;
     bool ptm_known = true, ptm = false;
     std::vector<uint64_t> r0(T), p0(T), d0(T);
@@ -421,60 +371,31 @@ int fasta_parse_core(const char* buf, uint64_t len, int threads, FastaSink* sink
         ptm_known &= parts[t].ptm_known;
         ptm |= parts[t].ptm;
     }
-    bool stream = false;
-    if (sink) {
-        const int rc = sink->sized(R, P, T, ptm_known, ptm, &stream);
-        if (rc) return rc;
-    }
     dbi_fasta* f = (dbi_fasta*)std::calloc(1, sizeof(dbi_fasta));
-    if (!f) return set_error(DBI_E_OOM, "calloc");
+    if (!f) return dbi::set_error(DBI_E_OOM, "calloc");
     f->n_proteins = P;
     f->n_residues = R;
     f->n_uniprot = U;
-    f->residues = stream ? nullptr : (uint8_t*)alloc_big(std::max<uint64_t>(R, 1) + 16);
+    f->residues = (uint8_t*)alloc_big(std::max<uint64_t>(R, 1) + 16);
     f->offsets = (uint64_t*)std::malloc(8 * (P + 1));
     f->defs = (char*)std::malloc(std::max<uint64_t>(D, 1));
     f->def_off = (uint64_t*)std::malloc(8 * (P + 1));
-    if ((!stream && !f->residues) || !f->offsets || !f->defs || !f->def_off) {
+    if (!f->residues || !f->offsets || !f->defs || !f->def_off) {
         dbi_fasta_free(f);
-        return set_error(DBI_E_OOM, "malloc");
+        return dbi::set_error(DBI_E_OOM, "malloc");
     }
-    if (stream) {
-        std::vector<SinkCursor> cur(T);
-        run([&](int t) {
-            cur[t].sink = sink;
-            cur[t].t = t;
-            cur[t].at = r0[t];
-            scan_part<2>(buf, len, parts[t], nullptr, f->offsets, f->defs, f->def_off, r0[t], p0[t], d0[t], &cnts[t],
-                         &cur[t]);
-            if (cur[t].used) cur[t].ok = sink->flush(t, cur[t].at, cur[t].slot, cur[t].used) && cur[t].ok;
-        });
-        for (const SinkCursor& c : cur)
-            if (!c.ok) {
-                dbi_fasta_free(f);
-                return set_error(DBI_E_HIP, "streaming the FASTA residues to the device failed");
-            }
-    } else {
-        run([&](int t) {
-            scan_part<1>(buf, len, parts[t], f->residues, f->offsets, f->defs, f->def_off, r0[t], p0[t], d0[t]);
-        });
-        std::memset(f->residues + R, 0, 16);
-        if (R + 16 >= (2u << 20)) {  // (alloc_big's 2-MiB pages)
-            std::lock_guard<std::mutex> lk(g_bufs_mu);
-            g_bufs.push_back({(uintptr_t)f->residues, R + 16, ptm_known, ptm});
-        }
+    run([&](int t) {
+        scan_part<true>(buf, len, parts[t], f->residues, f->offsets, f->defs, f->def_off, r0[t], p0[t], d0[t]);
+    });
+    std::memset(f->residues + R, 0, 16);
+    if (R + 16 >= (2u << 20)) {  // (alloc_big's 2-MiB pages)
+        std::lock_guard<std::mutex> lk(g_bufs_mu);
+        g_bufs.push_back({(uintptr_t)f->residues, R + 16, ptm_known, ptm});
     }
     f->offsets[P] = R;
     f->def_off[P] = D;
     *out = f;
     return 0;
-}
-}  // namespace dbi
-
-extern "C" {
-
-int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out) {
-    return dbi::fasta_parse_core(buf, len, threads, nullptr, out);
 }
 
 // The file is mapped read-only and parsed in place: the parse threads' first
@@ -483,12 +404,7 @@ int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out)
 // the previous way, paid a 257-MB copy and the buffer's page faults: 52-66
 // vs 35-43 ms for the SwissProt-scale file on 8 threads.)  Files that cannot
 // be mapped are read with pread.
-int dbi_fasta_read(const char* path, int threads, dbi_fasta** out) { return dbi::fasta_read_core(path, threads, nullptr, out); }
-
-}  // extern "C"
-
-namespace dbi {
-int fasta_read_core(const char* path, int threads, FastaSink* sink, dbi_fasta** out) {
+int dbi_fasta_read(const char* path, int threads, dbi_fasta** out) {
     if (!path || !out) return dbi::set_error(DBI_E_INVALID, "NULL argument");
     *out = nullptr;
     const int fd = ::open(path, O_RDONLY);
@@ -504,7 +420,7 @@ int fasta_read_core(const char* path, int threads, FastaSink* sink, dbi_fasta** 
         if (m != MAP_FAILED) {
             ::close(fd);
             (void)::madvise(m, (size_t)len, MADV_SEQUENTIAL);
-            const int rc = fasta_parse_core((const char*)m, len, threads, sink, out);
+            const int rc = dbi_fasta_parse((const char*)m, len, threads, out);
             ::munmap(m, (size_t)len);
             return rc;
         }
@@ -535,13 +451,10 @@ int fasta_read_core(const char* path, int threads, FastaSink* sink, dbi_fasta** 
     ::close(fd);
     int rc;
     if (std::count(bad.begin(), bad.end(), 1)) rc = dbi::set_error(DBI_E_INVALID, std::string("cannot read FASTA file ") + path);
-    else rc = fasta_parse_core(buf, len, threads, sink, out);
+    else rc = dbi_fasta_parse(buf, len, threads, out);
     std::free(buf);
     return rc;
 }
-}  // namespace dbi
-
-extern "C" {
 
 void dbi_fasta_free(dbi_fasta* f) {
     if (!f) return;

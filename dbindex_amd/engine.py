@@ -87,10 +87,9 @@ class Engine:
         return self.stats()
 
     def build_fasta(self, path: str, threads: int = 0, with_defs: bool = False):
-        """The one-off build from a FASTA file (dbi_build_fasta: parse and
-        upload fused, DBIndexer.run).  Returns (BuildStats, offsets, defs):
-        the file's protein offsets (u64, P+1) and, with_defs, its definitions;
-        the residues stay in HBM."""
+        """The one-off build from a FASTA file in one call (dbi_build_fasta,
+        DBIndexer.run).  Returns (BuildStats, offsets, defs): the file's
+        protein offsets (u64, P+1) and, with_defs, its definitions."""
         out = ctypes.POINTER(_native.DbiFasta)()
         check(_native.lib().dbi_build_fasta(self.h, path.encode(), threads, ctypes.byref(out)))
         try:

@@ -596,13 +596,12 @@ int dbi_fasta_parse(const char* buf, uint64_t len, int threads, dbi_fasta** out)
 int dbi_fasta_read(const char* path, int threads, dbi_fasta** out);
 void dbi_fasta_free(dbi_fasta* f);
 
-/* The one-off build from a FASTA file (DBIndexer.run, DBIndexer.java:546-616):
- * dbi_fasta_read + dbi_build fused -- the parse threads hand their packed
- * residues to the device as they go, so the upload runs under the parse.
- * Same index as dbi_fasta_read + dbi_build of the file.  *out (optional; free
- * with dbi_fasta_free) gets the file's offsets and definitions; its residues
- * are NULL (they are in HBM: dbi_device_view), except for a file with inline
- * '[formula]' PTMs, which takes dbi_build's PTM path over a host copy. */
+/* The one-off build from a FASTA file (DBIndexer.run, DBIndexer.java:546-616)
+ * in one call: dbi_fasta_read, then dbi_build of its output (whose 2-MiB-page
+ * residue buffer is pinned and DMA'd to HBM without a staging copy).  *out
+ * (optional; free with dbi_fasta_free) gets the parsed file -- definitions
+ * and offsets for the ProteinCache.  (Streaming each parse thread's residues
+ * to HBM during the parse measured slower: DESIGN.md §7.) */
 int dbi_build_fasta(dbi_handle* h, const char* path, int threads, dbi_fasta** out);
 
 /* ------------------------------------------------------------------------ */

@@ -106,12 +106,11 @@ def test_fasta_file_registered_upload(engine_cls, tmp_path, ptm):
 
 @pytest.mark.parametrize("n,threads,ptm", [(1000, 0, False), (60000, 3, False), (60000, 16, False),
                                            (60000, 0, True)])
-def test_build_fasta_fused(engine_cls, tmp_path, n, threads, ptm):
-    """dbi_build_fasta (parse + upload fused: the parse threads stream their
-    packed residues through the pinned ring as they go) builds the index of
-    the file that dbi_fasta_read + dbi_build builds: the oracle's, cold and
-    warm, with the file's offsets and definitions handed back; a file with
-    inline '[formula]' PTMs takes dbi_build's PTM path."""
+def test_build_fasta_one_call(engine_cls, tmp_path, n, threads, ptm):
+    """dbi_build_fasta (the one-off build in one call: the parser's pinned
+    residue buffer DMA'd straight to HBM) builds the oracle's index of the
+    file, cold and warm, with the file's offsets and definitions handed back;
+    a file with inline '[formula]' PTMs takes dbi_build's PTM path."""
     pp = fasta.config("1k") if n <= 1000 else fasta.config("swissprot").slice(0, n)
     if ptm:
         seqs = pp.sequences()

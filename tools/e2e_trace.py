@@ -2,10 +2,11 @@
 trace: where dbi_open + dbi_build spend their time beyond the cold kernels.
 
   rocprofv3 --hip-runtime-trace --kernel-trace --memory-copy-trace --output-format csv \
-      -d gpurun_out/TAG/trace -- python3 tools/e2e_trace.py
+      -d gpurun_out/TAG/trace -- python3 tools/e2e_trace.py [config] [fasta]
   python3 tools/api_timeline.py gpurun_out/TAG/trace
 
-Each phase is preceded by a dbi_runtime_info_get call (hipRuntimeGetVersion), which
+With "fasta" the builds are dbi_build_fasta of the proteome written as a
+FASTA file.  Each phase is preceded by a dbi_runtime_info_get call (hipRuntimeGetVersion), which
 tools/api_timeline.py uses as the phase marker.  The process first builds once
 on another engine (code objects loaded, as in bench.py's end-to-end leg)."""
 import json
@@ -30,6 +31,13 @@ def main() -> None:
         e.build(pp)
         synchronize(0)
     out = []
+    fused = len(sys.argv) > 2 and sys.argv[2] == "fasta"
+    if fused:  # dbi_build_fasta of the proteome written as a FASTA file
+        import tempfile
+        td = tempfile.mkdtemp()
+        path = os.path.join(td, "p.fasta")
+        with open(path, "w") as fh:
+            fasta.write_fasta(pp, fh)
     for rep in range(3):
         runtime_info()  # marker: open
         t0 = time.perf_counter()
@@ -37,7 +45,10 @@ def main() -> None:
         e3.set_timing(False)
         runtime_info()  # marker: build
         t1 = time.perf_counter()
-        e3.build(pp)
+        if fused:
+            e3.build_fasta(path)
+        else:
+            e3.build(pp)
         synchronize(0)
         t2 = time.perf_counter()
         runtime_info()  # marker: close

@@ -89,6 +89,9 @@ for w in "$@"; do
     e2e_trace) step e2e_trace 300 rocprofv3 --hip-runtime-trace --kernel-trace --memory-copy-trace --output-format csv \
                 -d "$OUT/trace" -o run -- python3 tools/e2e_trace.py
              python3 tools/api_timeline.py "$OUT/trace" > "$OUT/e2e_timeline.txt" ;;
+    e2e_trace_fasta) step e2e_trace_fasta 300 rocprofv3 --hip-runtime-trace --kernel-trace --memory-copy-trace --output-format csv \
+                -d "$OUT/trace_fasta" -o run -- python3 tools/e2e_trace.py swissprot fasta
+             python3 tools/api_timeline.py "$OUT/trace_fasta" > "$OUT/e2e_fasta_timeline.txt" ;;
     *) echo "unknown step $w"; exit 2 ;;
     esac
 done
