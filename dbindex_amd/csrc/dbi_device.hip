@@ -4414,7 +4414,7 @@ __device__ bool tag_sort_block(unsigned long long* k0, unsigned long long* k1, u
 // (in place of the fine bins' run detection); the wide bins are written to
 // `out` unsorted for chunk_sort_mid.
 #ifdef DBI_PHASE_CLOCK  // experiment builds: summed phase cycles of the main chunk sort (dbi_debug_phase_clock)
-__device__ unsigned long long g_phase[32];  // [0, 16): main chunk sort, [16, 32): the big tier
+__device__ unsigned long long g_phase[48];  // [0, 16): main chunk sort, [16, 32): the big tier, [32, 40): its block sorts
 #define PHASE_MARK(k) \
     do { if (threadIdx.x == 0) tph[k] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
@@ -4648,6 +4648,34 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
             const uint32_t lo = b & 0xFFFFu, L = (b >> 16) - lo;
             if (L <= WAVE_SORT_MAX) continue;
             // (the big tier only: in the mid kernel its registers cost a block per CU)
+#ifdef DBI_PHASE_CLOCK  // which block-level sort each wide bin took, and its cycles: g_phase[33..39]
+            const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
+            int path = 0;
+            if constexpr (DBI_TAG_SORT && CAP > 2048)
+                if (tag_sort_block<NT, CAP>(k0, k1, lo, L, a16, a16 + CAP, sm.tcnt, sm.u32)) path = 1;
+            if (!path) path = ck_run_block<NT, R>(k0, k1, lo, L, sm.mins) ? 2 : 3;
+            if (path == 3) block_bitonic<NT>(k0, k1, lo, L);
+            if (threadIdx.x == 0) {
+                atomicAdd(&g_phase[32 + path], 1ull);
+                atomicAdd(&g_phase[36 + path], __builtin_amdgcn_s_memtime() - tb0);
+                sm.bad = 0;
+            }
+            __syncthreads();
+            // distinct masses of the (now sorted) bin: g_phase[40] sum, [41] bins with <= 16, [42] <= 256, [43] max
+            uint32_t dk = 0;
+            for (uint32_t i = threadIdx.x; i < L; i += NT) dk += i == 0 || (k0[lo + i] >> 8) != (k0[lo + i - 1] >> 8);
+            atomicAdd(&sm.bad, dk);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const unsigned long long K = sm.bad;
+                atomicAdd(&g_phase[40], K);
+                if (K <= 16) atomicAdd(&g_phase[41], 1ull);
+                if (K <= 256) atomicAdd(&g_phase[42], 1ull);
+                atomicMax(&g_phase[43], K);
+            }
+            __syncthreads();
+            continue;
+#endif
             if constexpr (DBI_TAG_SORT && CAP > 2048)
                 if (tag_sort_block<NT, CAP>(k0, k1, lo, L, a16, a16 + CAP, sm.tcnt, sm.u32)) continue;
             if (!ck_run_block<NT, R>(k0, k1, lo, L, sm.mins)) block_bitonic<NT>(k0, k1, lo, L);
@@ -4920,10 +4948,10 @@ hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, cons
 }  // namespace dbi
 extern "C" int dbi_debug_phase_clock(unsigned long long* out, int reset) {
     if (reset) {
-        unsigned long long z[32] = {};
+        unsigned long long z[48] = {};
         return (int)hipMemcpyToSymbol(HIP_SYMBOL(dbi::g_phase), z, sizeof(z), 0, hipMemcpyHostToDevice);
     }
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dbi::g_phase), 32 * 8, 0, hipMemcpyDeviceToHost);
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dbi::g_phase), 48 * 8, 0, hipMemcpyDeviceToHost);
 }
 namespace dbi {
 #endif

@@ -292,6 +292,30 @@ def test_giant_chunks(Engine, kind):
     assert oix.n_kept > 8000
 
 
+@pytest.mark.parametrize("n,dups,copies", [(2600, 0, 300), (3000, 500, 900)])
+def test_multi_mass_wide_bins(Engine, n, dups, copies):
+    """One mass bin of ~3 000 / ~4 400 records (the big tier's 512- and
+    1024-thread classes) holding ~55 distinct fp64 masses within 0.07 mDa (a
+    3.7-uDa residue letter repeated 0..19 times, shuffled into one
+    composition: ulp-level sums) beside a spike of `copies` repeats of one
+    peptide: the semi-tryptic big bins' shape (profiles/r06p2: ~30 masses,
+    one dominant) through the block-level compact-key sort; duplicates across
+    proteins keep first appearance.  Cold (radix tail) and warm (depth bins)."""
+    prm = DBIndexSearchParams.trypsin(0)
+    prm.residue_mass.update({"U": 0.0000037})
+    rng = np.random.default_rng(9)
+    seqs = []
+    for _ in range(n):
+        core = list("GGAWDEFH") + ["U"] * int(rng.integers(0, 20))
+        rng.shuffle(core)
+        seqs.append("MR" + "".join(core) + "K")
+    seqs += [seqs[int(i)] for i in rng.integers(0, n, dups)]
+    seqs[n // 3:n // 3] = ["MRGGUAWDUEFHK"] * copies
+    pp = fasta.PackedProteins.from_sequences(seqs)
+    oix = _check(Engine, prm, pp, f"multi-mass wide bin {n}+{dups}+{copies}", nq=500)
+    assert oix.n_kept == n + dups + copies
+
+
 def test_isobaric_runs(Engine):
     """I/L swaps give bit-identical masses: equal-mass runs holding several
     peptide strings must group by string, first appearance first."""

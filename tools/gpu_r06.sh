@@ -13,6 +13,7 @@
 #   h2d       tools/probe/h2d_probe (host-to-device copy paths)
 #   ring      tools/probe/h2d_ring (the residue upload's staged-ring variants)
 #   dclock    digest phase clocks (tools/exp/dclock.so)
+#   pclock    chunk-sort phase clocks, semi and SwissProt (tools/exp/pclock.so)
 #   noverify  chunk-sort traffic with / without string verification (tools/exp/noverify.so)
 #   ab_prev   bench of tools/exp/prev.so (the last commit) against the tree, twice each
 #   allconf   tools/bench_all.sh: every config's bench line (+ --merge)
@@ -92,6 +93,10 @@ for w in "$@"; do
     e2e_trace_fasta) step e2e_trace_fasta 300 rocprofv3 --hip-runtime-trace --kernel-trace --memory-copy-trace --output-format csv \
                 -d "$OUT/trace_fasta" -o run -- python3 tools/e2e_trace.py swissprot fasta
              python3 tools/api_timeline.py "$OUT/trace_fasta" > "$OUT/e2e_fasta_timeline.txt" ;;
+    pclock)  export DBI_LIB_PATH=tools/exp/pclock.so
+             step pclock_semi 400 python tools/chunk_phase.py semi
+             step pclock_sp 300 python tools/chunk_phase.py swissprot
+             unset DBI_LIB_PATH ;;
     *) echo "unknown step $w"; exit 2 ;;
     esac
 done
