@@ -861,11 +861,15 @@ __device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi) {
 // kept end can pass (above maxMH) or that every kept end passes (below minMH)
 // are settled for the whole kernel: [k0, k1) is wave-uniform.
 constexpr int HIST_FAST_MAX = 8;
+// Tracked boundary i (i < KT, the kernel's compile-time count) is boundary
+// k0 + i: a kernel per KT, so the per-start loops hold no disabled
+// iterations and index registers statically (KT = k1 - k0, launch_digest).
 struct HistTrack {
     uint32_t q[HIST_FAST_MAX];   // the boundary's pointer (0: not yet placed; T_k > any residue: never 0 once placed)
     uint32_t v[HIST_FAST_MAX];   // p[q]
     uint32_t pv[HIST_FAST_MAX];  // p[q - 1]
-    uint32_t c[HIST_FAST_MAX + 1];  // c[k]: ends at or past boundary k (k < 8); c[8]: ends
+    uint32_t t[HIST_FAST_MAX];   // T of tracked boundary i (= CutLimits::t_b[k0 + i])
+    uint32_t c[HIST_FAST_MAX + 1];  // c[i]: ends at or past tracked boundary i; c[8]: ends
     uint32_t k0, k1;  // boundaries below k0: every kept end past them; from k1 on: none
 };
 
@@ -894,51 +898,46 @@ __device__ __forceinline__ uint32_t prefix_seek(const CutSmem& cs, uint32_t t, u
 // skipped: a gallop then).  The prefixes at the pointer and before it stay
 // in registers.  The slack words past the window read as above every
 // threshold, so no pointer passes p[nbytes].
-__device__ __forceinline__ void hist_advance(const CutLimits& cl, const CutSmem& cs, uint32_t nbytes, uint32_t upb,
-                                             uint32_t ps, HistTrack& ht) {
+template <int KT>
+__device__ __forceinline__ void hist_advance(const CutSmem& cs, uint32_t nbytes, uint32_t upb, uint32_t ps,
+                                             HistTrack& ht) {
     uint32_t w1[HIST_FAST_MAX], w2[HIST_FAST_MAX], w3[HIST_FAST_MAX];
 #pragma unroll
-    for (int k = 0; k < HIST_FAST_MAX; ++k) {
-        if ((uint32_t)k >= ht.k0 && (uint32_t)k < ht.k1 && (ht.q[k] == 0u || ht.q[k] < ps)) {  // first start
-            const uint32_t q = prefix_seek(cs, ps, nbytes - 1u, (int64_t)(upb + (uint32_t)cl.t_b[k]));
-            ht.q[k] = q;
-            ht.v[k] = cs.p(q);
-            ht.pv[k] = q > 0u ? cs.p(q - 1u) : 0u;  // (q >= ps; p[q - 1] <= the threshold)
+    for (int i = 0; i < KT; ++i) {
+        if (ht.q[i] == 0u || ht.q[i] < ps) {  // first start
+            const uint32_t q = prefix_seek(cs, ps, nbytes - 1u, (int64_t)(upb + ht.t[i]));
+            ht.q[i] = q;
+            ht.v[i] = cs.p(q);
+            ht.pv[i] = q > 0u ? cs.p(q - 1u) : 0u;  // (q >= ps; p[q - 1] <= the threshold)
         }
     }
 #pragma unroll
-    for (int k = 0; k < HIST_FAST_MAX; ++k) {
-        if ((uint32_t)k >= ht.k0 && (uint32_t)k < ht.k1) {
-            const uint32_t q = min(ht.q[k], nbytes);
-            w1[k] = cs.p(q + 1u);
-            w2[k] = cs.p(q + 2u);
-            w3[k] = cs.p(q + 3u);
-        }
+    for (int i = 0; i < KT; ++i) {
+        const uint32_t q = min(ht.q[i], nbytes);
+        w1[i] = cs.p(q + 1u);
+        w2[i] = cs.p(q + 2u);
+        w3[i] = cs.p(q + 3u);
     }
     bool more = false;
 #pragma unroll
-    for (int k = 0; k < HIST_FAST_MAX; ++k) {
-        if ((uint32_t)k >= ht.k0 && (uint32_t)k < ht.k1) {
-            const uint32_t athr = upb + (uint32_t)cl.t_b[k];
-            const uint32_t q = ht.q[k], v = ht.v[k], pv = ht.pv[k];
-            const bool a0 = v <= athr, a1 = a0 && w1[k] <= athr, a2 = a1 && w2[k] <= athr;
-            more |= a2 && w3[k] <= athr;
-            ht.q[k] = q + (uint32_t)a0 + (uint32_t)a1 + (uint32_t)a2;
-            ht.pv[k] = a2 ? w2[k] : a1 ? w1[k] : a0 ? v : pv;
-            ht.v[k] = a2 ? w3[k] : a1 ? w2[k] : a0 ? w1[k] : v;
-        }
+    for (int i = 0; i < KT; ++i) {
+        const uint32_t athr = upb + ht.t[i];
+        const uint32_t q = ht.q[i], v = ht.v[i], pv = ht.pv[i];
+        const bool a0 = v <= athr, a1 = a0 && w1[i] <= athr, a2 = a1 && w2[i] <= athr;
+        more |= a2 && w3[i] <= athr;
+        ht.q[i] = q + (uint32_t)a0 + (uint32_t)a1 + (uint32_t)a2;
+        ht.pv[i] = a2 ? w2[i] : a1 ? w1[i] : a0 ? v : pv;
+        ht.v[i] = a2 ? w3[i] : a1 ? w2[i] : a0 ? w1[i] : v;
     }
     if (more) {
 #pragma unroll
-        for (int k = 0; k < HIST_FAST_MAX; ++k) {
-            if ((uint32_t)k >= ht.k0 && (uint32_t)k < ht.k1) {
-                const uint32_t athr = upb + (uint32_t)cl.t_b[k];
-                if (ht.v[k] <= athr) {
-                    const uint32_t q = prefix_seek(cs, ht.q[k], nbytes - 1u, (int64_t)athr);
-                    ht.q[k] = q;
-                    ht.v[k] = cs.p(q);
-                    ht.pv[k] = cs.p(q - 1u);
-                }
+        for (int i = 0; i < KT; ++i) {
+            const uint32_t athr = upb + ht.t[i];
+            if (ht.v[i] <= athr) {
+                const uint32_t q = prefix_seek(cs, ht.q[i], nbytes - 1u, (int64_t)athr);
+                ht.q[i] = q;
+                ht.v[i] = cs.p(q);
+                ht.pv[i] = cs.p(q - 1u);
             }
         }
     }
@@ -962,7 +961,7 @@ __device__ __forceinline__ uint32_t first_above(DF D, uint32_t a, uint32_t b, in
 // boundaries in one walk, binary-search path) and the start is recounted by
 // the exact walk.
 // FAST (a kernel of its own: the binary-search path's code is not in it)
-template <bool HIST = false, bool FAST = false>
+template <bool HIST = false, bool FAST = false, int KT = 0>
 __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const CutLimits& cl, const DigestSmem& sm,
                                                    const CutSmem& cs, uint32_t nbytes, uint32_t ps, uint32_t* hist,
                                                    HistTrack& ht) {
@@ -970,7 +969,7 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
     if (!(dp.m0 <= dp.max_mh)) return r;  // while condition before the first residue (:284)
     if (ps + 2 > nbytes) { r.exact = false; return r; }
     const int64_t pb = ps > 0 ? (int64_t)cs.p(ps - 1) : 0;
-    if constexpr (HIST && FAST) hist_advance(cl, cs, nbytes, (uint32_t)pb, ps, ht);  // every start: pointers in step
+    if constexpr (HIST && FAST) hist_advance<KT>(cs, nbytes, (uint32_t)pb, ps, ht);  // every start: pointers in step
     // horizon: relative positions 0..h (the window's last position, whose cut is unknown, excluded)
     const uint32_t h = min(63u, nbytes - 2 - ps);
     const uint64_t hmask = bit_range(0, h);
@@ -1056,21 +1055,16 @@ __device__ __forceinline__ CutCount count_by_masks(const DevParams& dp, const Cu
         uint32_t g[HIST_FAST_MAX];
         bool bad = false;
 #pragma unroll
-        for (int k = 0; k < HIST_FAST_MAX; ++k) {
-            g[k] = 0u;
-            if ((uint32_t)k < ht.k0) {  // (uniform branches)
-                g[k] = n;
-            } else if ((uint32_t)k < ht.k1) {
-                const uint32_t t = (uint32_t)cl.t_b[k], q = ht.q[k];
-                if (q <= qhi && ht.v[k] - upb < t + (uint32_t)CUT_EPS_FX) bad = true;
-                if (q > qlo && ht.pv[k] - upb + (uint32_t)CUT_EPS_FX > t) bad = true;
-                const uint32_t sh = q - ps;  // q >= ps (p[q] > pb + T_k >= p[ps - 1] + 3)
-                g[k] = sh >= 64u ? 0u : (uint32_t)__popcll(em >> sh);
-            }
+        for (int i = 0; i < KT; ++i) {  // (boundaries below k0: every end past them -- c[8] at the flush)
+            const uint32_t t = ht.t[i], q = ht.q[i];
+            if (q <= qhi && ht.v[i] - upb < t + (uint32_t)CUT_EPS_FX) bad = true;
+            if (q > qlo && ht.pv[i] - upb + (uint32_t)CUT_EPS_FX > t) bad = true;
+            const uint32_t sh = q - ps;  // q >= ps (p[q] > pb + T_k >= p[ps - 1] + 3)
+            g[i] = sh >= 64u ? 0u : (uint32_t)__popcll(em >> sh);
         }
         if (bad) { r.exact = false; return r; }
 #pragma unroll
-        for (int k = 0; k < HIST_FAST_MAX; ++k) ht.c[k] += g[k];
+        for (int i = 0; i < KT; ++i) ht.c[i] += g[i];
         ht.c[HIST_FAST_MAX] += n;
       }
     } else if (HIST && n) {
@@ -1144,7 +1138,7 @@ __device__ void build_cut_tables(const DigestSmem& sm, CutSmem& cs, uint32_t nby
     __syncthreads();
 }
 
-template <bool HIST, bool FAST = false>
+template <bool HIST, bool FAST = false, int KT = 0>
 __global__ void __launch_bounds__(DIGEST_THREADS) __attribute__((amdgpu_waves_per_eu(HIST ? 4 : 1, 8)))
 k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const uint8_t* __restrict__ d_flags,
                     const uint8_t* __restrict__ d_res, const uint32_t* __restrict__ d_poff, uint32_t n_prot,
@@ -1173,6 +1167,14 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     }
 #pragma unroll
     for (int k = 0; k <= HIST_FAST_MAX; ++k) ht.c[k] = 0;
+    const bool kt_ok = (ht.k1 > ht.k0 ? ht.k1 - ht.k0 : 0u) == (uint32_t)KT;
+#pragma unroll
+    for (int i = 0; i < HIST_FAST_MAX; ++i) {  // tracked boundary i = k0 + i (KT = k1 - k0, launch_digest)
+        ht.t[i] = 0;
+#pragma unroll
+        for (int k = 0; k < HIST_FAST_MAX; ++k)
+            if ((uint32_t)k == ht.k0 + (uint32_t)i) ht.t[i] = (uint32_t)cl.t_b[k];
+    }
     TileCtx tc;
     const uint32_t ncand = digest_prepare<false>(sm, tc, blockIdx.x, gridDim.x, d_mass_tab, d_flags, d_res, d_poff, n_prot, n_res,
                                                  d_tile_pf, d_ctr);
@@ -1181,7 +1183,10 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
     thread_share(ncand, jb, je);
     uint32_t kept = 0, dropped = 0;
     for (uint32_t j = jb; j < je; ++j) {
-        CutCount r = count_by_masks<HIST, FAST>(dp, cl, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0, s_hist, ht);
+        // (a launch whose KT is not this kernel's k1 - k0 -- never, launch_digest derives both alike --
+        // walks every start)
+        CutCount r{0u, 0u, false};
+        if (!fast || kt_ok) r = count_by_masks<HIST, FAST, KT>(dp, cl, sm, cs, tc.nbytes, tc.t0 + sm.cand[j] - tc.w0, s_hist, ht);
         if (!r.exact) {
             const WalkOut w = walk_candidate<false, false, false, HIST>(dp, sm, tc, d_res, d_poff, j, nullptr, nullptr,
                                                                         s_hist);
@@ -1196,7 +1201,11 @@ k_digest_count_cuts(DevParams dp, const double* __restrict__ d_mass_tab, const u
         uint32_t above = ht.c[HIST_FAST_MAX];  // every end is past "boundary -1"
 #pragma unroll
         for (int k = 0; k <= HIST_FAST_MAX; ++k) {
-            const uint32_t past = k < dp.nb ? ht.c[k] : 0u;
+            uint32_t past = (uint32_t)k < ht.k0 ? ht.c[HIST_FAST_MAX] : 0u;  // below k0: every end; from k1: none
+#pragma unroll
+            for (int i = 0; i < KT; ++i)
+                if ((uint32_t)k == ht.k0 + (uint32_t)i) past = ht.c[i];
+            if (k >= dp.nb) past = 0u;
             const uint32_t v = k <= dp.nb ? wave_sum(above - past) : 0u;
             if (k <= dp.nb && lane_id() == 0 && v) atomicAdd(&s_hist[k], v);
             if (k < dp.nb) above = past;
@@ -2399,6 +2408,19 @@ static bool count_fast_ok(const DevParams& dp) {
            cut_threshold((double)(dp.nb * dp.br), dp.m0) < (1ll << 31);
 }
 
+// the tracked boundaries' count k1 - k0, as k_digest_count_cuts derives k0 / k1
+// from the same thresholds (cut_threshold: host and device)
+static int count_tracked(const DevParams& dp) {
+    const int64_t t_min = cut_threshold(dp.min_mh, dp.m0), t_max = cut_threshold(dp.max_mh, dp.m0);
+    int k0 = 0, k1 = 0;
+    for (int k = 0; k < HIST_FAST_MAX; ++k) {
+        const int64_t tb = cut_threshold((double)((k + 1) * dp.br), dp.m0);
+        if (k < dp.nb && tb <= t_min) k0 = k + 1;
+        if (k < dp.nb && tb < t_max) k1 = k + 1;
+    }
+    return std::max(0, k1 - k0);
+}
+
 template <bool EMIT, bool HIST = false>
 static hipError_t launch_digest(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                 const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res,
@@ -2411,10 +2433,23 @@ static hipError_t launch_digest(const DevParams& dp, const double* d_mass_tab, c
     DBI_LAUNCH((k_digest<EMIT, SEMI, MAND, HIST>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
                        d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_out, d_ctr, d_hist)
     if (!EMIT && !dp.semi && !dp.mand_mode && dp.cut_count) {
-        if (HIST && count_fast_ok(dp))
-            DBI_LAUNCH((k_digest_count_cuts<HIST, true>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab,
-                       d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr, d_hist);
-        else
+        if (HIST && count_fast_ok(dp)) {
+#define DBI_COUNT_KT(KT)                                                                                   \
+    DBI_LAUNCH((k_digest_count_cuts<HIST, true, KT>), dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, \
+               d_flags, d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr, d_hist)
+            switch (count_tracked(dp)) {
+            case 0: DBI_COUNT_KT(0); break;
+            case 1: DBI_COUNT_KT(1); break;
+            case 2: DBI_COUNT_KT(2); break;
+            case 3: DBI_COUNT_KT(3); break;
+            case 4: DBI_COUNT_KT(4); break;
+            case 5: DBI_COUNT_KT(5); break;
+            case 6: DBI_COUNT_KT(6); break;
+            case 7: DBI_COUNT_KT(7); break;
+            default: DBI_COUNT_KT(8); break;
+            }
+#undef DBI_COUNT_KT
+        } else
             DBI_LAUNCH(k_digest_count_cuts<HIST>, dim3(nblk), dim3(DIGEST_THREADS), 0, s, dp, d_mass_tab, d_flags,
                        d_res, d_poff, n_prot, n_res, d_tile_pf, d_blk, d_thr, d_ctr, d_hist);
         return hipGetLastError();
