@@ -927,7 +927,9 @@ def trembl_issue_roofline(chunks_per_step: int, ms: float):
     if not files:
         return None
     d = json.load(open(files[-1]))
-    k = next((v for n, v in d["kernels"].items() if "k_digest_count_cuts<true, true>" in n), None)
+    # (the bucket kernel: k_digest_count_cuts<true, true> up to round 5, <true, true, KT> since -- one per
+    # tracked-boundary count)
+    k = next((v for n, v in d["kernels"].items() if "k_digest_count_cuts<true, true" in n), None)
     if not k or not k.get("launches"):
         return None
     per_launch = k["SQ_INSTS_VALU"] / k["launches"]

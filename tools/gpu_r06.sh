@@ -13,6 +13,7 @@
 #   h2d       tools/probe/h2d_probe (host-to-device copy paths)
 #   ring      tools/probe/h2d_ring (the residue upload's staged-ring variants)
 #   dclock    digest phase clocks (tools/exp/dclock.so)
+#   sq_trembl SQ counter pass of the TrEMBL bench (the bucket kernel's VALU count)
 #   pclock    chunk-sort phase clocks, semi and SwissProt (tools/exp/pclock.so)
 #   noverify  chunk-sort traffic with / without string verification (tools/exp/noverify.so)
 #   ab_prev   bench of tools/exp/prev.so (the last commit) against the tree, twice each
@@ -97,6 +98,10 @@ for w in "$@"; do
              step pclock_semi 400 python tools/chunk_phase.py semi
              step pclock_sp 300 python tools/chunk_phase.py swissprot
              unset DBI_LIB_PATH ;;
+    sq_trembl) step pmc_sq_trembl 900 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+                --output-format csv -d "$OUT/trembl_sq" -o run \
+                -- python3 bench.py --config trembl --steps 1 --warmup 0 --no-cpu-baseline
+             python3 tools/sq_kernel_totals.py "$OUT/trembl_sq" > "$OUT/trembl_sq.json" ;;
     *) echo "unknown step $w"; exit 2 ;;
     esac
 done
