@@ -4664,6 +4664,18 @@ __device__ void sort_chunk(const Rec* __restrict__ in, Rec* __restrict__ out, ui
         const uint32_t b = sm.big[r];
         const uint32_t lo = b & 0xFFFFu, L = (b >> 16) - lo;
         if (L > WAVE_SORT_MAX) continue;
+#ifdef DBI_PHASE_CLOCK  // wave-sorted bins: g_phase[44 + BLOCK] count, [46 + BLOCK] single-mass ones
+        {
+            bool one = true;
+            const uint64_t mb = k0[lo] >> 8;
+            for (uint32_t i = lane_id(); i < L; i += 64) one &= (k0[lo + i] >> 8) == mb;
+            one = __ballot(!one) == 0;
+            if (lane_id() == 0) {
+                atomicAdd(&g_phase[44 + (BLOCK ? 1 : 0)], 1ull);
+                if (one) atomicAdd(&g_phase[46 + (BLOCK ? 1 : 0)], 1ull);
+            }
+        }
+#endif
         bool done;
         if constexpr (WAVE_SORT_MAX > 256)
             done = L <= 128 ? ck_run_wave<2>(k0, k1, lo, L)

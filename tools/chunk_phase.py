@@ -60,6 +60,8 @@ def main():
     nb = max(sum(v[33:36]), 1)
     out["big_tier_distinct_masses"] = dict(mean_per_bin=v[40] / nb, share_le16=v[41] / nb, share_le256=v[42] / nb,
                                            max=v[43])
+    out["wave_sorted_bins"] = {n: dict(per_build=v[44 + k] / reps, single_mass_share=v[46 + k] / max(v[44 + k], 1))
+                               for k, n in ((0, "chunk_sort"), (1, "big_tier"))}
     print(json.dumps(out, indent=1))
 
 
