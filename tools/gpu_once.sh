@@ -1,6 +1,9 @@
-# one-off GPU session script (changes per call): the round-end steps
+# one-off GPU session script (changes per call): A/B of an experiment library
 set -o pipefail
-O=gpurun_out/r06f2; mkdir -p $O
-timeout -k 10 1000 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread tests -m gpu > $O/t_all.log 2>&1; rc=$?; tail -3 $O/t_all.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1; rc=$?; tail -2 $O/smoke.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; rc=$?; tail -c 600 $O/bench.json; exit $rc
+O=gpurun_out/r06o2; mkdir -p $O
+B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-cold --queries 0"
+for r in 1 2 3; do
+  DBI_LIB_PATH=tools/exp/optim.so timeout -k 10 300 $B > $O/optim$r.log 2>&1 || exit 1
+  timeout -k 10 300 $B > $O/cur$r.log 2>&1 || exit 1
+done
+python3 tools/ab_table.py $O optim1 cur1 optim2 cur2 optim3 cur3
