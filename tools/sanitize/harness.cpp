@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unistd.h>
 #include <random>
 #include <string>
 #include <vector>
@@ -100,6 +101,21 @@ static void fasta_cases() {
     CHECK(dbi_fasta_parse(big.data(), big.size(), 16, &b) == 0);
     CHECK(a->n_proteins == 3000 && b->n_proteins == 3000 && a->n_residues == b->n_residues);
     CHECK(std::memcmp(a->offsets, b->offsets, 8 * (a->n_proteins + 1)) == 0);
+    // the same text read from a file (mapped: the scans' last blocks end at the mapping's end)
+    char path[] = "/tmp/dbi_sanitize_XXXXXX";
+    const int fd = mkstemp(path);
+    CHECK(fd >= 0);
+    CHECK(write(fd, big.data(), big.size()) == (ssize_t)big.size());
+    close(fd);
+    for (int th : {1, 5, 16}) {
+        dbi_fasta* r = nullptr;
+        CHECK(dbi_fasta_read(path, th, &r) == 0);
+        CHECK(r->n_proteins == a->n_proteins && r->n_residues == a->n_residues);
+        CHECK(std::memcmp(r->offsets, a->offsets, 8 * (a->n_proteins + 1)) == 0);
+        CHECK(std::memcmp(r->residues, a->residues, a->n_residues) == 0);
+        dbi_fasta_free(r);
+    }
+    unlink(path);
     dbi_fasta_free(a);
     dbi_fasta_free(b);
     CHECK(dbi_fasta_read("/nonexistent/file.fasta", 2, &a) != 0);
