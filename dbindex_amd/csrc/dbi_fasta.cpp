@@ -143,7 +143,11 @@ uint64_t seq_scan_512(uint8_t* out, const char* b, uint64_t n, uint64_t s, uint6
     return cnt;
 }
 
-const bool g_avx512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vbmi2");
+bool detect_avx512() {
+    __builtin_cpu_init();  // (a static initializer may run before the runtime's own CPU detection)
+    return __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vbmi2");
+}
+const bool g_avx512 = detect_avx512();
 #endif
 
 // non-whitespace bytes of b[0, len)
