@@ -232,9 +232,12 @@ __device__ __forceinline__ uint32_t find_le(const uint32_t* poff, uint32_t lo, u
 // per-tile binary search over the offsets (20 dependent loads at SwissProt
 // scale).  Threads also fold their protein's length into ctr->max_plen.
 __global__ void k_tile_proteins(const uint32_t* __restrict__ poff, uint32_t n_prot, uint32_t n_res, uint32_t ntiles,
-                                uint32_t* __restrict__ tile_pf, Counters* __restrict__ ctr) {
+                                uint32_t* __restrict__ tile_pf, Counters* __restrict__ ctr, uint32_t* __restrict__ zero,
+                                uint32_t n_zero) {
     constexpr int64_t TL = DIGEST_TILE;
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0)  // the partitioning digest's region cursors back to zero (a memset node fewer)
+        for (uint32_t i = threadIdx.x; i < n_zero; i += blockDim.x) zero[i] = 0;
     uint32_t len = 0;
     if (p < n_prot) {
         const int64_t a = poff[p], e = poff[p + 1];
@@ -271,11 +274,12 @@ __global__ void k_tile_proteins(const uint32_t* __restrict__ poff, uint32_t n_pr
 }
 
 hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res, uint32_t* d_tile_pf,
-                                Counters* d_ctr, hipStream_t s) {
-    if (n_res == 0 || n_prot == 0) return hipSuccess;
+                                Counters* d_ctr, hipStream_t s, uint32_t* d_zero, uint32_t n_zero) {
+    if (n_res == 0 || n_prot == 0)
+        return d_zero && n_zero ? hipMemsetAsync(d_zero, 0, sizeof(uint32_t) * n_zero, s) : hipSuccess;
     const uint32_t ntiles = (n_res + DIGEST_TILE - 1) / DIGEST_TILE;
     DBI_LAUNCH(k_tile_proteins, dim3((n_prot + 255) / 256), dim3(256), 0, s, d_poff, n_prot, n_res, ntiles,
-               d_tile_pf, d_ctr);
+               d_tile_pf, d_ctr, d_zero, d_zero ? n_zero : 0u);
     return hipGetLastError();
 }
 
@@ -5755,14 +5759,17 @@ hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const
     return hipGetLastError();
 }
 
-__global__ void k_off64_to_32(const uint64_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t n) {
+__global__ void k_off64_to_32(const uint64_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t n,
+                              Counters* __restrict__ ctr) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = (uint32_t)in[i];
+    if (ctr && blockIdx.x == 0)  // a build's counters back to zero (dbi_build_device: a memset fewer)
+        for (uint32_t k = threadIdx.x; k < sizeof(Counters) / 4; k += blockDim.x) reinterpret_cast<uint32_t*>(ctr)[k] = 0;
 }
 
-hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    DBI_LAUNCH(k_off64_to_32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, d_out, n);
+hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s, Counters* d_ctr) {
+    if (n == 0) return d_ctr ? hipMemsetAsync(d_ctr, 0, sizeof(Counters), s) : hipSuccess;
+    DBI_LAUNCH(k_off64_to_32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_in, d_out, n, d_ctr);
     return hipGetLastError();
 }
 

@@ -438,7 +438,7 @@ inline Bytes by(double cR, double cN, double cU, double cP, double cB) {
 
 int read_counters(dbi_handle* h);
 const char* ptm_device_msg();  // ERR_PTM's message
-int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot);
+int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot, bool zero_ctr = true);  // zero_ctr false: the caller zeroes the counters on the stream itself
 int prepare_tiles(dbi_handle* h);
 // digest of h->d_res / h->d_poff into recA: *n records (*n_in slots, REC_SENTINEL
 // in the unused ones when *sparse)

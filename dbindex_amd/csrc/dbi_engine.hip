@@ -375,9 +375,10 @@ int prepare_tiles(dbi_handle* h) {
     const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
     int rc;
     if ((rc = h->tile_pf.ensure(2 * ((size_t)ntiles + 2)))) return rc;  // first + last protein of every tile
+    // (a partitioning digest's region cursors are zeroed by the same kernel)
     STAGE(h, "tile_proteins", by(0, 0, 0, 4, 0),
           launch_tile_proteins(h->d_poff, (uint32_t)h->n_prot, (uint32_t)h->n_res, h->tile_pf.p, h->ctr.p,
-                               h->stream));
+                               h->stream, h->part_now ? h->part_now->cur : nullptr, DEPTH_XCDS * 256));
     return 0;
 }
 
@@ -595,7 +596,6 @@ int warm_body_lsd(dbi_handle* h, const LsdPlan& pl, uint64_t* n_in, bool* sparse
         (rc = h->scan_tmp.ensure(std::max({scan_u32_tmp_elems((uint64_t)pl.max_chunks << pl.b2),
                                            scan_u32_tmp_elems(ntiles), h->scan_tmp.cap}))))
         return rc;
-    DBI_HIP(hipMemsetAsync(h->rcur.p, 0, sizeof(uint32_t) * DEPTH_XCDS * 256, s));
     PartOut po{};
     po.recs = h->recR.p;
     po.dig = h->rdig.p;
@@ -724,7 +724,6 @@ int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_
     // the map, from a sample of the resident index (the previous build's)
     const uint64_t U = std::min<uint64_t>({h->prev_unique, h->umass.cap, h->occ_off.cap ? h->occ_off.cap - 1 : 0});
     const BinMap sub = make_binmap(h->params.min_mh, h->params.max_mh, nsub);
-    DBI_HIP(hipMemsetAsync(h->rcur.p, 0, sizeof(uint32_t) * DEPTH_XCDS * 256, s));
     const uint32_t ns = (uint32_t)std::min<uint64_t>(DEPTH_SAMPLES, U);
     // a redo keeps the map its first attempt computed (that attempt may have
     // overwritten the index, or the redo's larger buffers moved it); any
@@ -956,7 +955,7 @@ int build_digest(dbi_handle* h) {
     }
 }
 
-int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
+int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot, bool zero_ctr) {
     if (n_res >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_res must be < 2^32-1 per device: shard the FASTA");
     if (n_prot >= (1ull << 32) - 1) return set_error(DBI_E_INVALID, "n_prot must be < 2^32-1");
     DBI_HIP(hipSetDevice(h->device));
@@ -972,7 +971,7 @@ int begin_build(dbi_handle* h, uint64_t n_res, uint64_t n_prot) {
     h->nstage = 0;
     h->hc_final = false;
     h->t0 = std::chrono::steady_clock::now();
-    DBI_HIP(hipMemsetAsync(h->ctr.p, 0, sizeof(Counters), h->stream));
+    if (zero_ctr) DBI_HIP(hipMemsetAsync(h->ctr.p, 0, sizeof(Counters), h->stream));
     return 0;
 }
 
@@ -1549,7 +1548,7 @@ int dbi_build_device(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, c
                      uint64_t n_prot, void* stream) {
     if (!h || (!d_residues && n_res) || !d_prot_off) return set_error(DBI_E_INVALID, "NULL argument");
     int rc;
-    if ((rc = begin_build(h, n_res, n_prot))) return rc;
+    if ((rc = begin_build(h, n_res, n_prot, false))) return rc;  // (the counters: zeroed by the offsets' conversion)
     hipStream_t user = (hipStream_t)stream;
     if (user) {
         // order the engine stream after the caller's producer work
@@ -1560,7 +1559,7 @@ int dbi_build_device(dbi_handle* h, const uint8_t* d_residues, uint64_t n_res, c
         DBI_HIP(hipEventDestroy(ev));
     }
     if ((rc = h->poff.ensure(n_prot + 1))) return rc;
-    DBI_HIP(launch_off64_to_32(d_prot_off, h->poff.p, n_prot + 1, h->stream));
+    DBI_HIP(launch_off64_to_32(d_prot_off, h->poff.p, n_prot + 1, h->stream, h->ctr.p));
     h->d_res = d_residues;
     h->d_poff = h->poff.p;
     if ((rc = build_digest(h))) return rc;

@@ -217,7 +217,7 @@ constexpr int BIG_CAP = 7936;       // records per oversize chunk sorted in LDS 
 // tile_pf[t] = protein holding residue min(t*DIGEST_TILE, R-1); ctr->max_plen
 // = longest protein (the record field width, see Rec)
 hipError_t launch_tile_proteins(const uint32_t* d_poff, uint32_t n_prot, uint32_t n_res, uint32_t* d_tile_pf,
-                                Counters* d_ctr, hipStream_t s);
+                                Counters* d_ctr, hipStream_t s, uint32_t* d_zero = nullptr, uint32_t n_zero = 0);
 hipError_t launch_digest_count(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
                                const uint8_t* d_res, const uint32_t* d_poff, uint32_t n_prot,
                                uint32_t n_res, const uint32_t* d_tile_pf, uint32_t* d_blk, uint32_t* d_thr,
@@ -494,7 +494,8 @@ hipError_t launch_key_range(const double* d_umass, uint32_t n_unique, int32_t fa
 hipError_t launch_occ_to_recs(const double* d_mass, const uint32_t* d_pid, const uint32_t* d_off,
                               const uint32_t* d_len, const uint32_t* d_poff, const uint8_t* d_res, uint64_t n,
                               uint64_t n_prot, Rec* d_out, Counters* d_ctr, hipStream_t s);
-hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s);
+hipError_t launch_off64_to_32(const uint64_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s,
+                              Counters* d_ctr = nullptr);  // d_ctr: zeroed too
 // query hits: per-query hit / protein-id counts -> u64 offsets (row, occ_row:
 // nq + 1 entries each, totals also at tot[0..1]); sums: scan2_tmp_elems(nq)
 size_t scan2_tmp_elems(uint64_t n);
