@@ -3516,6 +3516,64 @@ hipError_t launch_expand_locs_hist(const uint64_t* d_locs, uint32_t n, const uin
     return hipGetLastError();
 }
 
+// The owner merge on depth bins (round 6): the expansion
+// partitions its records by the depth bin's high digit into (digit, XCD)
+// regions exactly as the lean digest's tiles do (part_place: LDS ranks, one
+// region reservation per digit, digit runs written by consecutive lanes), so
+// the owner's records take the single-device tail from there -- one pass over
+// the low digit (bin_scatter), the chunk sort binning each chunk in LDS,
+// finalize -- instead of the radix tail's passes.  One block per
+// EXPAND_PART_R received words.
+constexpr uint32_t EXPAND_PART_R = 1024;  // (2048: 38 KiB of LDS, 16 waves per CU -- the gathers' latency showed)
+__global__ void __launch_bounds__(DIGEST_THREADS)
+k_expand_locs_part(const unsigned long long* __restrict__ locs, uint32_t n, const uint8_t* __restrict__ res,
+                   const uint32_t* __restrict__ poff, const double* __restrict__ mass_tab, double m0, uint32_t w,
+                   PartOut po, Counters* __restrict__ ctr) {
+    constexpr uint32_t KI = EXPAND_PART_R / DIGEST_THREADS;
+    static_assert(DIGEST_THREADS == 256, "one mass-table entry and one digit counter per thread");
+    __shared__ double smass[256];
+    __shared__ uint32_t s_cnt[256], s_run[256], s_tmp[DIGEST_THREADS / 64 + 1];
+    __shared__ uint4 stage[EXPAND_PART_R];
+    __shared__ uint16_t sdig[EXPAND_PART_R];
+    const uint32_t tid = threadIdx.x;
+    smass[tid] = mass_tab[tid];
+    s_cnt[tid] = 0;
+    __syncthreads();
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(res) & 3u);
+    const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(res - mis);
+    const uint32_t base = blockIdx.x * EXPAND_PART_R;
+    const uint32_t nr = min(EXPAND_PART_R, n - base);
+    // the expansion one record at a time (a residue gather loop per record:
+    // not unrolled, few registers, many waves in flight), each into the stage
+    // at its own index; then the records back into registers for part_place
+    // (which restages them in digit order)
+#pragma unroll 1
+    for (uint32_t i = tid; i < nr; i += DIGEST_THREADS) {
+        const Rec r = expand_loc(locs[base + i], w32, mis, poff, smass, m0, w);
+        stage[i] = make_uint4((uint32_t)r.q0, (uint32_t)(r.q0 >> 32), (uint32_t)r.q1, (uint32_t)(r.q1 >> 32));
+    }
+    __syncthreads();
+    uint4 rv[KI];
+#pragma unroll
+    for (uint32_t k = 0; k < KI; ++k) {
+        const uint32_t i = k * DIGEST_THREADS + tid;
+        rv[k] = i < nr ? stage[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // (past nr: part_place skips it)
+    }
+    __syncthreads();  // (part_place's restage overwrites the stage)
+    part_place<KI>(po, rv, nr, s_cnt, s_run, s_tmp, stage, sdig, ctr);
+}
+
+hipError_t launch_expand_locs_part(const uint64_t* d_locs, uint32_t n, const uint8_t* d_res, const uint32_t* d_poff,
+                                   const double* d_mass_tab, double m0, uint32_t w, const PartOut& po,
+                                   Counters* d_ctr, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (po.lsd || po.b1 < 1 || po.b1 > 8 || po.dm.b2 < 1 || po.dm.b2 > 8) return hipErrorInvalidValue;
+    const uint32_t g = (n + EXPAND_PART_R - 1) / EXPAND_PART_R;
+    DBI_LAUNCH(k_expand_locs_part, dim3(g), dim3(DIGEST_THREADS), 0, s, (const unsigned long long*)d_locs, n, d_res,
+               d_poff, d_mass_tab, m0, w, po, d_ctr);
+    return hipGetLastError();
+}
+
 hipError_t launch_pair_hist(const Rec* d_in, uint32_t n, uint32_t nshards, uint32_t* d_hist, hipStream_t s) {
     return radix_hist(d_in, n, PairDigit{}, owner_bits(nshards), false, d_hist, s);
 }

@@ -315,6 +315,15 @@ struct dbi_handle {
     const uint4* depth_map_of = nullptr;  // the map buffer a complete map was last enqueued into
     uint64_t depth_map_unique = 0;        // ... sampled from an index of this many unique peptides
     uint32_t depth_map_nbins = 0;         // ... for this many bins
+    double depth_map_lo = 0, depth_map_scale = 0;  // ... over these sub-bins (BinMap lo, scale)
+    // owner merges on depth bins (dbi_shard.hip merge_body): the index the map samples is this
+    // owner's own slice, left by its last merge (not a replica, not a single-device build)
+    bool opt_owner_depth = true;          // option owner_depth=0: owner merges by the radix tail
+    uint64_t owner_serial = ~0ull;        // build_serial after this handle's last owner merge
+    const void* owner_umass = nullptr;    // ... and its index buffers
+    const void* owner_occ = nullptr;
+    double owner_lo = 0, owner_hi = 0;    // ... and its mass range
+    double owner_us_radix = 0, owner_us_depth = 0;  // merge device time per 1000 records received, by tail (averaged)
     bool opt_depth_map_reuse = true;      // option depth_map_reuse: keep the map while the index's size holds
     bool cur_local = false, tail_local = false;  // this / the last finished build's chunk sort took depth-bin chunks
     bool force_cold = false;              // dbi_set_cold: the next build takes the cold path (buffers kept)
@@ -360,9 +369,12 @@ struct dbi_handle {
         const void* xrecv = nullptr;
         uint32_t width = 0;
         int nstage0 = 0;          // stage slots (event pool) the merge's stages start at
+        uint32_t depth_cap = 0;   // depth bins: region capacity (0: the radix tail)
+        bool depth_fresh = false; // depth bins: the map is sampled in this merge
         bool operator==(const MergeKey& o) const {
             return g == o.g && n_recv == o.n_recv && lo == o.lo && hi == o.hi && xrecv == o.xrecv &&
-                   width == o.width && nstage0 == o.nstage0;
+                   width == o.width && nstage0 == o.nstage0 && depth_cap == o.depth_cap &&
+                   depth_fresh == o.depth_fresh;
         }
     };
     struct {
@@ -453,5 +465,19 @@ uint32_t choose_nbins(uint64_t n, int max_bits);  // fine mass bins of a tail ov
 int radix_plan(uint32_t nbins, bool sparse, int* width);  // LSD digit widths; returns the passes
 int finish_build(dbi_handle* h);
 bool bounded_digest(const dbi_handle* h);  // a warm build digests into bounded slots (device-sized)
+// depth-bin tails (dbi_engine.hip): the bins and regions for about n records,
+// the map's reuse test, the allocations, the map, and the tail from the
+// filled regions (the lean warm build's, and the owner merge's: dbi_shard.hip)
+struct DepthPlan {
+    bool on = false;
+    uint32_t b1 = 0, b2 = 0, nbins = 0, cap = 0, nreg = 0, max_chunks = 0;
+};
+DepthPlan depth_plan_n(const dbi_handle* h, uint64_t n, uint64_t slots);
+bool depth_map_reusable(const dbi_handle* h, uint32_t nbins, const BinMap& sub);
+int depth_buffers(dbi_handle* h, const DepthPlan& pl, uint32_t nchunks);
+int depth_map_enqueue(dbi_handle* h, const DepthPlan& pl, const BinMap& sub, uint64_t U);
+int depth_tail(dbi_handle* h, const DepthPlan& pl, const BinMap& sub, uint64_t cap, uint32_t T, uint32_t nchunks,
+               bool est);
+uint32_t chunk_target(const dbi_handle* h, uint64_t n);
 
 }  // namespace dbi

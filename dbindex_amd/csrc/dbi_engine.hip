@@ -502,17 +502,11 @@ constexpr uint64_t DEPTH_MIN_RECS = 1u << 14;
 #define DBI_DEPTH_SAMPLES (1u << 19)
 #endif
 constexpr uint32_t DEPTH_SAMPLES = DBI_DEPTH_SAMPLES;  // uniques of the previous index sampled for the map
-struct DepthPlan {
-    bool on = false;
-    uint32_t b1 = 0, b2 = 0, nbins = 0, cap = 0, nreg = 0, max_chunks = 0;
-};
-
-DepthPlan depth_plan(const dbi_handle* h) {
+// the bins and regions of a depth-bin tail over about n records (slots: the
+// record buffers' capacity)
+DepthPlan depth_plan_n(const dbi_handle* h, uint64_t n, uint64_t slots) {
     DepthPlan p;
-    const uint64_t n = h->last_kept, slots = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
-    if (!h->use_depth || h->depth_off || !lean_digest(h) || h->prev_unique == 0 || n < DEPTH_MIN_RECS ||
-        slots < 1024)
-        return p;
+    if (n < DEPTH_MIN_RECS || slots < 1024) return p;
     int B = 9;
     while (B < 16 && (DEPTH_BIN_AVG << (B + 1)) <= n) ++B;
     p.b1 = (uint32_t)std::max(1, std::min(8, B - 8));  // the pass over the low digit: 8 bits when B >= 9
@@ -528,15 +522,89 @@ DepthPlan depth_plan(const dbi_handle* h) {
     return p;
 }
 
+DepthPlan depth_plan(const dbi_handle* h) {
+    if (!h->use_depth || h->depth_off || !lean_digest(h) || h->prev_unique == 0) return DepthPlan{};
+    return depth_plan_n(h, h->last_kept, std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull));
+}
+
 // the map of the last depth build still fits: sampled from an index of the
 // same size (the previous build's, the one this build would sample), for the
-// same bin count.  The map is a plan, never a result (any monotone map gives
-// the exact index): it is sampled again when the index changes size, after a
-// region overflow, and on cold builds; option depth_map_reuse=0 samples every
-// build (0.08 ms at SwissProt scale).
-bool depth_map_reusable(const dbi_handle* h, uint32_t nbins) {
+// same bin count and sub-bin range.  The map is a plan, never a result (any
+// monotone map gives the exact index): it is sampled again when the index
+// changes size, after a region overflow, and on cold builds; option
+// depth_map_reuse=0 samples every build (0.08 ms at SwissProt scale).
+bool depth_map_reusable(const dbi_handle* h, uint32_t nbins, const BinMap& sub) {
     return h->opt_depth_map_reuse && h->depth_map_of != nullptr && h->depth_map_of == h->dmap.p &&
-           h->prev_unique != 0 && h->depth_map_unique == h->prev_unique && h->depth_map_nbins == nbins;
+           h->prev_unique != 0 && h->depth_map_unique == h->prev_unique && h->depth_map_nbins == nbins &&
+           h->depth_map_lo == sub.lo && h->depth_map_scale == sub.scale;
+}
+bool depth_map_reusable(const dbi_handle* h, uint32_t nbins) {
+    return depth_map_reusable(h, nbins, make_binmap(h->params.min_mh, h->params.max_mh, 1u << DEPTH_SUB_BITS));
+}
+
+// every buffer of a depth-bin tail past the record buffers (tail_buffers)
+int depth_buffers(dbi_handle* h, const DepthPlan& pl, uint32_t nchunks) {
+    const uint64_t nreg_slots = (uint64_t)pl.nreg * pl.cap;
+    int rc;
+    if ((rc = h->recR.ensure(nreg_slots)) || (rc = h->rdig.ensure(nreg_slots + 16)) ||
+        (rc = h->rcur.ensure(DEPTH_XCDS * 256)) || (rc = h->dsub.ensure(DEPTH_SAMPLES)) ||
+        (rc = h->dpre.ensure(DEPTH_SAMPLES)) || (rc = h->dmap.ensure((1u << DEPTH_SUB_BITS) / 64)) ||
+        (rc = h->dheavy.ensure_zeroed(1, h->stream)) || (rc = h->desc.ensure(pl.max_chunks)) ||
+        (rc = h->d1c.ensure(512)) || (rc = h->hist2.ensure((size_t)pl.max_chunks << pl.b2)) ||
+        (rc = h->bstart.ensure(pl.nbins + 1)) || (rc = h->split_list.ensure(nchunks)) ||
+        (rc = h->scan_tmp.ensure(std::max({scan_u32_tmp_elems(DEPTH_SAMPLES),
+                                           scan_u32_tmp_elems((uint64_t)pl.max_chunks << pl.b2), h->scan_tmp.cap}))))
+        return rc;
+    return 0;
+}
+
+// the map over sub's sub-bins, sampled from the resident index's U uniques
+int depth_map_enqueue(dbi_handle* h, const DepthPlan& pl, const BinMap& sub, uint64_t U) {
+    hipStream_t s = h->stream;
+    const uint32_t nsub = 1u << DEPTH_SUB_BITS;
+    const uint32_t ns = (uint32_t)std::min<uint64_t>(DEPTH_SAMPLES, U);
+    DBI_HIP(hipMemsetAsync(h->dmap.p, 0, sizeof(uint4) * (nsub / 64), s));
+    STAGE(h, "depth_map", by(0, 0, 0, 0, 0), ([&]() -> hipError_t {
+              hipError_t e = launch_depth_sample(h->umass.p, h->occ_off.p, U, ns, sub, h->dsub.p, h->dpre.p, s);
+              if (e == hipSuccess)
+                  e = launch_scan_u32(h->dpre.p, h->dpre.p, ns, h->scan_tmp.p, h->scan_tmp.cap, &h->ctr.p->depth_w, s);
+              return e == hipSuccess
+                         ? launch_depth_map(h->dsub.p, h->dpre.p, ns, pl.nbins, nsub, h->dmap.p, h->dheavy.p, h->ctr.p, s)
+                         : e;
+          }()));
+    h->depth_map_of = h->dmap.p;
+    h->depth_map_unique = h->prev_unique;
+    h->depth_map_nbins = pl.nbins;
+    h->depth_map_lo = sub.lo;
+    h->depth_map_scale = sub.scale;
+    return 0;
+}
+
+// the regions (filled: the digest's or the owner expansion's partition) ->
+// one radix pass over the low digit into bin order (recA), the chunks of whole
+// bins, the chunk sort and finalize over cap record slots (the records: the
+// device count ctr->tail_n, 0 when a region overflowed)
+int depth_tail(dbi_handle* h, const DepthPlan& pl, const BinMap& sub, uint64_t cap, uint32_t T, uint32_t nchunks,
+               bool est) {
+    hipStream_t s = h->stream;
+    STAGE(h, "part_plan", by(0, 0, 0, 0, 0),
+          launch_part_plan(h->rcur.p, pl.cap, pl.b1, cap, h->desc.p, h->d1c.p, h->ctr.p, s));
+    STAGE(h, "part_hist", by(0, 1, 0, 0, 0),
+          launch_part_hist(h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2, pl.max_chunks, h->hist2.p,
+                           h->ctr.p, s));
+    STAGE(h, "part_scan", by(0, 0, 0, 0, 0),
+          launch_scan_u32(h->hist2.p, h->hist2.p, (uint64_t)pl.max_chunks << pl.b2, h->scan_tmp.p, h->scan_tmp.cap,
+                          nullptr, s));
+    STAGE(h, "bin_scatter", by(0, 33, 0, 0, 0),
+          launch_part_scatter(h->recR.p, h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2,
+                              pl.max_chunks, h->hist2.p, h->recA.p, h->ctr.p, s));
+    STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
+          launch_depth_bounds(h->hist2.p, h->d1c.p, pl.b1, pl.b2, h->bstart.p, T, nchunks, h->chunk_lo.p, h->ctr.p, s,
+                              h->split_list.p));
+    int rc;
+    if ((rc = sort_chunks(h, h->recA.p, h->recB.p, sub, nchunks, cap, &h->ctr.p->tail_n, est, true))) return rc;
+    h->stats.n_bins = pl.nbins;
+    return 0;
 }
 
 // Warm semi-specific builds: the radix tail's first
@@ -699,53 +767,29 @@ constexpr double SLACK_MIN = 1.25;  // region room / the region's share of the p
 constexpr int SLACK_DECAY = 8;      // builds without an overflow before the room is halved back toward SLACK_MIN
 
 int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_t* n_in, bool* sparse) {
-    hipStream_t s = h->stream;
     int rc;
     const uint64_t cap = std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull);
-    const uint32_t nsub = 1u << DEPTH_SUB_BITS;
-    const uint64_t nreg_slots = (uint64_t)pl.nreg * pl.cap;
     const uint32_t T = h->chunk_t ? h->chunk_t : cap >= CHUNK_T_MIN_RECS ? (uint32_t)CHUNK_T_DEPTH : chunk_target(h, cap);
     const uint32_t nchunks = (uint32_t)std::max<uint64_t>((cap + T - 1) / T, 1);
     const uint32_t ntiles = (uint32_t)((h->n_res + DIGEST_TILE - 1) / DIGEST_TILE);
     // every allocation before the first launch (a reallocation must never free
     // a buffer that queued kernels use): the tail's (chunk sort, index), the
     // depth bins', the digest's (run_digest finds them in place)
-    if ((rc = tail_buffers(h, cap, cap, true)) || (rc = h->recR.ensure(nreg_slots)) ||
-        (rc = h->rdig.ensure(nreg_slots + 16)) || (rc = h->rcur.ensure(DEPTH_XCDS * 256)) ||
-        (rc = h->dsub.ensure(DEPTH_SAMPLES)) || (rc = h->dpre.ensure(DEPTH_SAMPLES)) || (rc = h->dmap.ensure(nsub / 64)) ||
-        (rc = h->dheavy.ensure_zeroed(1, s)) || (rc = h->desc.ensure(pl.max_chunks)) || (rc = h->d1c.ensure(512)) ||
-        (rc = h->hist2.ensure((size_t)pl.max_chunks << pl.b2)) || (rc = h->bstart.ensure(pl.nbins + 1)) ||
-        (rc = h->split_list.ensure(nchunks)) ||
+    if ((rc = tail_buffers(h, cap, cap, true)) || (rc = depth_buffers(h, pl, nchunks)) ||
         (rc = h->blk.ensure(std::max<uint32_t>(ntiles, 1))) ||
         (rc = h->thr.ensure((size_t)ntiles * DIGEST_THREADS + 1)) || (rc = h->tile_pf.ensure(2 * ((size_t)ntiles + 2))) ||
-        (rc = h->scan_tmp.ensure(std::max({scan_u32_tmp_elems(DEPTH_SAMPLES), scan_u32_tmp_elems((uint64_t)pl.max_chunks << pl.b2),
-                                           scan_u32_tmp_elems(ntiles), h->scan_tmp.cap}))))
+        (rc = h->scan_tmp.ensure(std::max<size_t>(scan_u32_tmp_elems(ntiles), h->scan_tmp.cap))))
         return rc;
     // the map, from a sample of the resident index (the previous build's)
     const uint64_t U = std::min<uint64_t>({h->prev_unique, h->umass.cap, h->occ_off.cap ? h->occ_off.cap - 1 : 0});
-    const BinMap sub = make_binmap(h->params.min_mh, h->params.max_mh, nsub);
-    const uint32_t ns = (uint32_t)std::min<uint64_t>(DEPTH_SAMPLES, U);
+    const BinMap sub = make_binmap(h->params.min_mh, h->params.max_mh, 1u << DEPTH_SUB_BITS);
     // a redo keeps the map its first attempt computed (that attempt may have
     // overwritten the index, or the redo's larger buffers moved it); any
     // complete map is monotone in the mass, so it is exact, only its balance
     // may be off
     const bool keep = (h->depth_keep_map && h->depth_map_of == h->dmap.p) || depth_map_reusable(h, pl.nbins);
     if (!keep && !index_kept) return DEPTH_FALLBACK;
-    if (!keep) {
-        DBI_HIP(hipMemsetAsync(h->dmap.p, 0, sizeof(uint4) * (nsub / 64), s));
-        STAGE(h, "depth_map", by(0, 0, 0, 0, 0), ([&]() -> hipError_t {
-                  hipError_t e = launch_depth_sample(h->umass.p, h->occ_off.p, U, ns, sub, h->dsub.p, h->dpre.p, s);
-                  if (e == hipSuccess)
-                      e = launch_scan_u32(h->dpre.p, h->dpre.p, ns, h->scan_tmp.p, h->scan_tmp.cap,
-                                          &h->ctr.p->depth_w, s);
-                  return e == hipSuccess ? launch_depth_map(h->dsub.p, h->dpre.p, ns, pl.nbins, nsub, h->dmap.p,
-                                                            h->dheavy.p, h->ctr.p, s)
-                                         : e;
-              }()));
-        h->depth_map_of = h->dmap.p;
-        h->depth_map_unique = h->prev_unique;
-        h->depth_map_nbins = pl.nbins;
-    }
+    if (!keep && (rc = depth_map_enqueue(h, pl, sub, U))) return rc;
     // the digest, partitioned into the regions
     PartOut po{};
     po.recs = h->recR.p;
@@ -762,24 +806,7 @@ int warm_body_depth(dbi_handle* h, const DepthPlan& pl, bool index_kept, uint64_
     h->part_now = nullptr;
     if (rc) return rc;
     if (!dev) return set_error(DBI_E_STATE, "internal: warm build without device sizing");
-    // one radix pass over the low digit, region by region, into bin order (recA)
-    STAGE(h, "part_plan", by(0, 0, 0, 0, 0),
-          launch_part_plan(h->rcur.p, pl.cap, pl.b1, cap, h->desc.p, h->d1c.p, h->ctr.p, s));
-    STAGE(h, "part_hist", by(0, 1, 0, 0, 0),
-          launch_part_hist(h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2, pl.max_chunks, h->hist2.p,
-                           h->ctr.p, s));
-    STAGE(h, "part_scan", by(0, 0, 0, 0, 0),
-          launch_scan_u32(h->hist2.p, h->hist2.p, (uint64_t)pl.max_chunks << pl.b2, h->scan_tmp.p, h->scan_tmp.cap,
-                          nullptr, s));
-    STAGE(h, "bin_scatter", by(0, 33, 0, 0, 0),
-          launch_part_scatter(h->recR.p, h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2,
-                              pl.max_chunks, h->hist2.p, h->recA.p, h->ctr.p, s));
-    STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
-          launch_depth_bounds(h->hist2.p, h->d1c.p, pl.b1, pl.b2, h->bstart.p, T, nchunks, h->chunk_lo.p, h->ctr.p, s,
-                              h->split_list.p));
-    if ((rc = sort_chunks(h, h->recA.p, h->recB.p, sub, nchunks, cap, &h->ctr.p->tail_n, true, true))) return rc;
-    h->stats.n_bins = pl.nbins;
-    return 0;
+    return depth_tail(h, pl, sub, cap, T, nchunks, true);
 }
 
 // digest + tail of a warm device-sized build, enqueued (or captured)
@@ -1944,6 +1971,7 @@ int dbi_set_option(dbi_handle* h, const char* name, int64_t value) {
     else if (n == "digest_hist") h->use_h1 = on;
     else if (n == "semi_bounded") h->use_semi_bounded = on;
     else if (n == "depth_bins") h->use_depth = on;
+    else if (n == "owner_depth") h->opt_owner_depth = on;
     else if (n == "semi_part") h->use_semi_part = on;
     else if (n == "part_stage") h->use_part_stage = on;
     else if (n == "depth_map_reuse") h->opt_depth_map_reuse = on;

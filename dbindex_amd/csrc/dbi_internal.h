@@ -407,6 +407,12 @@ hipError_t launch_expand_locs(const uint64_t* d_locs, uint64_t n, const uint8_t*
 hipError_t launch_expand_locs_hist(const uint64_t* d_locs, uint32_t n, const uint8_t* d_res, const uint32_t* d_poff,
                                    const double* d_mass_tab, double m0, uint32_t w, Rec* d_out, const BinMap& bm,
                                    int bits, uint32_t* d_hist, hipStream_t s);
+// the same, partitioned by the depth bin's high digit into po's (digit, XCD)
+// regions with each record's low digit (the owner merge on depth bins;
+// po.cur zeroed, ctr->n_kept = n for k_part_plan's check)
+hipError_t launch_expand_locs_part(const uint64_t* d_locs, uint32_t n, const uint8_t* d_res, const uint32_t* d_poff,
+                                   const double* d_mass_tab, double m0, uint32_t w, const PartOut& po,
+                                   Counters* d_ctr, hipStream_t s);
 // stable partition of query routing pairs (q0 = owner, q1 = query index) by owner
 hipError_t launch_pair_hist(const Rec* d_in, uint32_t n, uint32_t nshards, uint32_t* d_hist, hipStream_t s);
 hipError_t launch_pair_scatter(const Rec* d_in, Rec* d_out, uint32_t n, uint32_t nshards, const uint32_t* d_hist,

@@ -952,7 +952,47 @@ namespace {
 struct MergeRange {
     double lo = 0, hi = 0;
     bool first = false;  // the handle's first build (code objects load): not timed
+    // depth bins (attempt 0 of a warm owner): the plan, the map sampled in this merge, the chunks
+    DepthPlan dpl{};
+    bool fresh = false;
+    bool part_over = false;  // attempt 0's regions overflowed: the redo takes the radix tail
+    BinMap sub{};
+    uint32_t T = 0, nchunks = 0;
 };
+
+// The owner merge on depth bins: the single-device warm
+// tail -- the records partitioned by the depth bins' high digit on their way
+// in (k_expand_locs_part), one pass over the low digit, chunks of whole bins
+// binned in LDS by the chunk sort -- instead of the radix tail's passes.  The
+// map comes from this owner's previous slice of the index (its mass range
+// [lo, hi] in 2^DEPTH_SUB_BITS sub-bins), or the map that slice gave last
+// time; a merge with neither (the first, after a replica or a single-device
+// build on the handle), or whose key range moved since that slice (the
+// records outside the sampled range would crowd the end bins' regions), takes
+// the radix tail.  Any monotone map gives the exact index: a stale one costs
+// balance, never correctness.
+void owner_depth_plan(dbi_handle* h, MergeRange& mr, uint64_t n_recv) {
+    mr.dpl = DepthPlan{};
+    mr.fresh = false;
+    if (!h->opt_owner_depth || !h->use_depth || n_recv == 0) return;
+    // measured per owner: a slice whose depth-bin merges ran slower per record
+    // than its radix-tail ones keeps the radix tail (the lowest masses: few
+    // distinct masses per depth bin, chunks for the big tier)
+    if (h->owner_us_depth > 0.0 && h->owner_us_radix > 0.0 && h->owner_us_depth > h->owner_us_radix) return;
+    const DepthPlan pl = depth_plan_n(h, n_recv, std::min<uint64_t>(h->recA.cap, 0xFFFFFFFEull));
+    if (!pl.on) return;
+    const BinMap sub = make_binmap(mr.lo, mr.hi, 1u << DEPTH_SUB_BITS);
+    const bool reuse = depth_map_reusable(h, pl.nbins, sub);
+    const bool own_index = h->owner_serial == h->build_serial && h->owner_umass == h->umass.p &&
+                           h->owner_occ == h->occ_off.p && h->prev_unique > 0 && h->owner_lo == mr.lo &&
+                           h->owner_hi == mr.hi;
+    if (!reuse && !own_index) return;
+    mr.dpl = pl;
+    mr.fresh = !reuse;
+    mr.sub = sub;
+    mr.T = h->chunk_t ? h->chunk_t : (uint32_t)CHUNK_T_DEPTH;
+    mr.nchunks = (uint32_t)std::max<uint64_t>((n_recv + mr.T - 1) / mr.T, 1);
+}
 
 int merge_begin(dbi_handle* h, MergeRange& mr) {
     ShardState& sh = h->shard;
@@ -972,7 +1012,17 @@ int merge_begin(dbi_handle* h, MergeRange& mr) {
     mr.hi = std::max(hi, mr.lo);
     for (int e = 0; e < 2; ++e)
         if (!h->ev_merge[e]) DBI_HIP(hipEventCreate(&h->ev_merge[e]));
-    if ((rc = tail_buffers(h, sh.n_recv, sh.n_recv, false))) return rc;
+    // an owner's tail buffers -- its index among them -- grow with 1/8 to spare:
+    // its share moves a little from build to build (the splitters), and an
+    // index left in place is what the next merge's depth map samples
+    const uint64_t room = h->umass.cap < sh.n_recv ? sh.n_recv + sh.n_recv / 8 : sh.n_recv;
+    // (and for the radix tail's plan over exactly n_recv: no allocation once its kernels are queued)
+    if ((rc = tail_buffers(h, room, room, false)) || (rc = tail_buffers(h, sh.n_recv, sh.n_recv, false))) return rc;
+    owner_depth_plan(h, mr, sh.n_recv);
+    if (mr.dpl.on) {
+        if ((rc = depth_buffers(h, mr.dpl, mr.nchunks))) return rc;
+        owner_depth_plan(h, mr, sh.n_recv);  // (the map's buffer may have moved: sampled again)
+    }
     mr.first = h->build_serial == 0;
     return 0;
 }
@@ -989,6 +1039,29 @@ int merge_body(dbi_handle* h, const MergeRange& mr, int attempt) {
     DBI_HIP(hipMemsetAsync(h->ctr.p, 0, offsetof(Counters, max_plen), s));
     hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(64), 0, s, &h->ctr.p->n_kept, (unsigned long long)sh.n_recv);
     DBI_HIP(hipGetLastError());
+    // depth bins; a redo (chunk lists longer than their grids) keeps attempt
+    // 0's map (its finalize may have overwritten the index the map sampled),
+    // after a region overflow the radix tail
+    if (mr.dpl.on && !mr.part_over) {
+        int rc;
+        DBI_HIP(hipMemsetAsync(h->rcur.p, 0, sizeof(uint32_t) * DEPTH_XCDS * 256, s));
+        const uint64_t U = std::min<uint64_t>({h->prev_unique, h->umass.cap, h->occ_off.cap ? h->occ_off.cap - 1 : 0});
+        if (attempt == 0 && mr.fresh && (rc = depth_map_enqueue(h, mr.dpl, mr.sub, U))) return rc;
+        PartOut po{};
+        po.recs = h->recR.p;
+        po.dig = h->rdig.p;
+        po.cur = h->rcur.p;
+        po.dm = DepthMap{h->dmap.p, mr.sub, mr.dpl.b2, mr.dpl.nbins - 1};
+        po.cap = mr.dpl.cap;
+        po.b1 = mr.dpl.b1;
+        STAGE(h, "owner_expand", by(0, 0, 0, 0, 0),
+              launch_expand_locs_part(h->xrecv.p, (uint32_t)sh.n_recv, h->d_res, h->d_poff, h->mass_tab.p, h->dp.m0,
+                                      sh.width, po, h->ctr.p, s));
+        h->stages[h->nstage - 1].c0 = 25.0 * (double)sh.n_recv;  // 8 B in, 16 B + the digit out (+ the residues)
+        if ((rc = depth_tail(h, mr.dpl, mr.sub, sh.n_recv, mr.T, mr.nchunks, attempt == 0))) return rc;
+        DBI_HIP(hipEventRecord(h->ev_merge[1], s));
+        return 0;
+    }
     // the received location words -> records (mass + tag from the residues);
     // recA is free (the partition read it before the exchange was enqueued).
     // The expansion also counts the tail's first radix histogram (the same
@@ -1030,6 +1103,8 @@ int merge_enqueue(dbi_handle* h, const MergeRange& mr, int attempt) {
     k.xrecv = h->xrecv.p;
     k.width = h->shard.width;
     k.nstage0 = h->nstage;
+    k.depth_cap = mr.dpl.on ? mr.dpl.cap : 0u;
+    k.depth_fresh = mr.dpl.on && mr.fresh;
     auto& mg = h->mgraph;
     if (mg.exec && mg.key == k) {
         DBI_HIP(hipGraphLaunch(mg.exec, h->stream));
@@ -1090,9 +1165,27 @@ int merge_enqueue(dbi_handle* h, const MergeRange& mr, int attempt) {
 int merge_done(dbi_handle* h, const MergeRange& mr) {
     int rc;
     if ((rc = finish_build(h))) return rc;
+    // the index is this owner's slice: the next merge's depth map samples it
+    h->owner_serial = h->build_serial;
+    h->owner_umass = h->umass.p;
+    h->owner_occ = h->occ_off.p;
+    h->owner_lo = mr.lo;
+    h->owner_hi = mr.hi;
+    if (h->hc.err & ERR_PART) {  // a region overflowed (redone by the radix tail): more room, a fresh map
+        h->depth_slack = std::min(8.0, 2.0 * h->depth_slack);
+        h->depth_map_unique = 0;
+    }
     float mg = 0.f;
     h->shard.ms_merge_gpu =
         !mr.first && hipEventElapsedTime(&mg, h->ev_merge[0], h->ev_merge[1]) == hipSuccess ? (double)mg : 0.0;
+    // (a depth merge that sampled its map is not counted: the map, and its
+    // first chunk lists against the radix tail's grids, are one-off costs)
+    const bool depth = mr.dpl.on && !mr.part_over;
+    if (h->shard.ms_merge_gpu > 0.0 && h->shard.n_recv > 0 && !(h->hc.err & ERR_PART) && !(depth && mr.fresh)) {
+        double& us = depth ? h->owner_us_depth : h->owner_us_radix;
+        const double v = 1e6 * h->shard.ms_merge_gpu / (double)h->shard.n_recv;
+        us = us > 0.0 ? 0.5 * us + 0.5 * v : v;
+    }
     return 0;
 }
 
@@ -1106,8 +1199,9 @@ __global__ void k_totals_row(const Counters* __restrict__ ctr, unsigned long lon
     for (int i = 0; i < 8; ++i) keys += ctr->n_keys_shard[i];
     row[3] = ctr->n_unique;
     row[4] = keys;
-    const bool redo = (ctr->err & ERR_GRID) || (skip_mid && ctr->n_mid) || (skip_big && ctr->n_big);
-    row[7] = (redo ? 1ull : 0ull) | ((unsigned long long)(ctr->err & ~ERR_GRID) << 8);
+    // (a depth-bin region that overflowed: the merge again, by the radix tail)
+    const bool redo = (ctr->err & (ERR_GRID | ERR_PART)) || (skip_mid && ctr->n_mid) || (skip_big && ctr->n_big);
+    row[7] = (redo ? 1ull : 0ull) | ((unsigned long long)(ctr->err & ~(ERR_GRID | ERR_PART)) << 8);
 }
 }  // namespace
 }  // namespace dbi
@@ -1126,7 +1220,8 @@ int dbi_shard_merge(dbi_handle* h) {
         const int nstage0 = h->nstage;
         if ((rc = merge_enqueue(h, mr, attempt))) return rc;
         if ((rc = merge_done(h, mr))) return rc;  // (synchronises)
-        if (!h->lists_short) break;
+        if (h->hc.err & ERR_PART) mr.part_over = true;
+        if (!h->lists_short && !(h->hc.err & ERR_PART)) break;
         if (attempt > 0) return set_error(DBI_E_STATE, "internal: chunk lists outgrew full grids");
         h->nstage = nstage0;
     }
@@ -1936,6 +2031,11 @@ int dbi_build_sharded(dbi_handle* h, dbi_comm* c, const uint8_t* d_res, uint64_t
         DBI_HIP(hipMemcpyAsync(&h->hc, h->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, s));
         DBI_HIP(hipStreamSynchronize(s));
         if (rc_merge) return rc_merge;
+        if (h->hc.err & ERR_PART) {  // this owner's depth-bin region overflowed: more room, a fresh map next time
+            h->depth_slack = std::min(8.0, 2.0 * h->depth_slack);
+            h->depth_map_unique = 0;
+            mr.part_over = true;
+        }
         bool any_redo = false;
         for (int i = 0; i < n; ++i) {
             const unsigned long long* r = rows.data() + (size_t)i * TOTALS_W;

@@ -22,7 +22,7 @@ whole proteome, identical row for row to a single-device build.
 from __future__ import annotations
 
 import ctypes
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -172,12 +172,14 @@ def build_sharded(eng: Engine, comm: ShardComm, d_res: int, n_res: int, d_off: i
 
 
 def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off: int, n_prot: int,
-                        ranges: Sequence[Tuple[int, int]], profile=None, balance: bool = False) -> np.ndarray:
+                        ranges: Sequence[Tuple[int, int]], profile=None, balance: bool = False,
+                        split: Optional[np.ndarray] = None) -> np.ndarray:
     """Every shard's handle in this process (exchange by device copies): the
     phases of dbi_build_sharded one by one.  ``profile`` = (band_split,
     band_cost): cost-balanced splitters; ``balance``: the splitters follow the
     merge-cost profile engines[0] keeps and this build updates, as
-    dbi_build_sharded does.  Returns the owner splitters."""
+    dbi_build_sharded does; ``split``: these owner splitters (a warm
+    dbi_build_sharded reusing its split).  Returns the owner splitters."""
     n = len(engines)
     assert 1 <= n <= MAX_SHARDS and len(ranges) == n
     L = _native.lib()
@@ -191,7 +193,9 @@ def build_sharded_local(engines: Sequence[Engine], d_res: int, n_res: int, d_off
     # same residues, proteins and shard ranges as the build that held it
     shape = (int(n_res), int(n_prot), tuple((int(b), int(e)) for b, e in ranges))
     held = getattr(engines[0], "_split_held", None) if balance else None
-    if held is not None and held[0] == shape and held[1].shape[0] == n - 1:
+    if split is not None:
+        split = np.ascontiguousarray(split, np.int32)[: n - 1]
+    elif held is not None and held[0] == shape and held[1].shape[0] == n - 1:
         split = held[1]  # the last two builds ran this split, balanced: keep it (dbi_build_sharded's hysteresis)
     elif balance:
         s = np.ascontiguousarray(samples, np.float64).reshape(n * (SHARD_SAMPLES + 1))

@@ -487,3 +487,54 @@ def test_sharded_local_merge_graph_replays(native):
     finally:
         for e in engines:
             e.close()
+
+
+def _stage_names(e):
+    return {n for n, _, _ in e.stage_times()}
+
+
+def test_sharded_owner_depth_bins(native):
+    """Warm owner merges on depth bins: an owner's first
+    merge takes the radix tail (no slice of its own to sample yet), and so does
+    one whose key range moved since its slice (a new split); the next ones
+    (the cold build's split reused) partition the received records by depth bin on their way in (the map
+    sampled from the owner's previous slice, then reused), enqueued, captured
+    as a graph and replayed -- each equal to the oracle; option owner_depth=0
+    takes the radix tail again.  Then a proteome of another mass distribution
+    under the map of the first: any monotone map gives the exact index (a
+    region that overflows is redone by the radix tail), and the first again."""
+    from dbindex_amd.engine import Engine
+    cp = DBIndexSearchParams.trypsin(2).to_c()
+    a = fasta.config("human")
+    heavy = str.maketrans({"G": "W", "A": "Y", "S": "F", "V": "H"})
+    b = fasta.PackedProteins.from_sequences([s.translate(heavy) for s in a.sequences()])
+    oa, ob = (cref.Index(cp, p.residues, p.offsets) for p in (a, b))
+    bufs = {id(p): _inputs(native, p) for p in (a, b)}
+    engines = [Engine(cp, 0) for _ in range(4)]
+    depth_stages = {"part_plan", "bin_scatter"}
+    try:
+        plan = [(a, oa, "cold")] + [(a, oa, "warm")] * 5 + [(a, oa, "radix")] + [(b, ob, "other")] * 2 + \
+               [(a, oa, "back")] * 2
+        split = None
+        for k, (p, o, what) in enumerate(plan):
+            for e in engines:
+                e.set_option("owner_depth", 0 if what == "radix" else 1)
+                e.set_timing(k < 3 or what != "warm")  # builds 3-5: the merge captured, then replayed
+            d_res, d_off = bufs[id(p)]
+            # the warm builds of the first proteome reuse the cold build's split
+            # (as dbi_build_sharded's warm builds do); the other proteome and the
+            # return to the first sample theirs
+            sp = shard.build_sharded_local(engines, d_res.ptr, p.n_residues, d_off.ptr, p.n_proteins,
+                                           shard.protein_ranges(p.offsets, 4),
+                                           split=split if what in ("warm", "radix") else None)
+            if k == 0:
+                split = sp
+            _assert_sharded_equal(engines, o, f"owner depth build {k} ({what})", nq=400)
+            names = [_stage_names(e) for e in engines]
+            if what in ("cold", "radix"):
+                assert all(not (depth_stages & s) for s in names), (k, what)
+            elif what == "warm":
+                assert all(depth_stages <= s for s in names), (k, what, names)
+    finally:
+        for e in engines:
+            e.close()

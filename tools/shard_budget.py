@@ -102,7 +102,10 @@ def main() -> int:
             xch = link_bytes / (LINK_GBS * 1e6)
             tot = front + xch + back
             history.append(dict(merge_max_ms=back, model_ms_without_fixed=tot,
-                                merge_ms=[round(x["merge_ms"], 3) for x in rows], split=[int(v) for v in split]))
+                                merge_ms=[round(x["merge_ms"], 3) for x in rows], split=[int(v) for v in split],
+                                depth=[int("bin_scatter" in x["stages"]) for x in rows],
+                                merge_stages=[{n: v for n, v in x["stages"].items()
+                                               if n not in DIGEST + PARTITION + ("exchange",)} for x in rows]))
             if best is None or tot < best["model_ms_without_fixed"]:
                 best = dict(config=a.config, shards=k, rows=rows, front_ms=front, exchange_model_ms=xch,
                             merge_max_ms=back, model_ms_without_fixed=tot, link_gbs=LINK_GBS)
