@@ -33,7 +33,7 @@ def _rank_main(world: int, rank: int, name: str, plan: dict, q) -> None:
         from dbindex_amd._native import DBIndexStoreException, DeviceBuffer, synchronize
         from dbindex_amd.engine import Engine
         from dbindex_amd.params import DBIndexSearchParams
-        pp = fasta.config("1k").slice(0, NPROT)
+        pp = fasta.config(plan.get("config", "1k")).slice(0, plan.get("nprot", NPROT))
         cp = DBIndexSearchParams.trypsin(2).to_c()
         d_res = DeviceBuffer.from_numpy(np.concatenate([pp.residues, np.zeros(16, np.uint8)]), 0)
         d_off = DeviceBuffer.from_numpy(pp.offsets.astype(np.uint64), 0)
@@ -62,7 +62,8 @@ def _rank_main(world: int, rank: int, name: str, plan: dict, q) -> None:
                     st = shard.build_sharded(eng, comm, d_res.ptr, pp.n_residues, d_off.ptr, pp.n_proteins, b, e)
                     out["builds"].append(dict(ok=True, export=eng.export(), sampled=st.split_sampled,
                                               rounds=st.split_rounds, g_total=st.g_total, g_unique=st.g_unique,
-                                              g_keys=st.g_keys, key_lo=st.key_lo, key_hi=st.key_hi))
+                                              g_keys=st.g_keys, key_lo=st.key_lo, key_hi=st.key_hi,
+                                              stages=sorted({n for n, _, _ in eng.stage_times()})))
                 except DBIndexStoreException as ex:
                     out["builds"].append(dict(ok=False, error=str(ex)))
                 for key, (_, after) in opts.items():
@@ -253,3 +254,27 @@ def test_ranks_device_sized_digest_redone(oracle, kind):
         _assert_whole_index([b["export"] for b in builds], oracle if k < 2 else oix2, f"{kind} build {k}")
     assert {b["rounds"] for b in [r["builds"][1] for r in res]} == {1}
     assert {b["rounds"] for b in [r["builds"][2] for r in res]} == {2}, [r["builds"][2]["rounds"] for r in res]
+
+
+def test_ranks_owner_depth_bins():
+    """The RCCL driver's warm owners on depth bins, two
+    ranks over 6 000 human-scale proteins: build 0 samples its split (each
+    owner's first merge: the radix tail), build 1 reuses it -- the same key
+    ranges -- so every owner samples the map from its own previous slice and
+    partitions the received records by depth bin; later builds follow the
+    cost profile's splits.  Every build equals the oracle."""
+    from dbindex_amd import _native, fasta
+    from dbindex_amd.params import DBIndexSearchParams
+    from oracle import cref
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the gpu tests need an MI355X")
+    pp = fasta.config("human").slice(0, 6000)
+    oix = cref.Index(DBIndexSearchParams.trypsin(2).to_c(), pp.residues, pp.offsets)
+    res = _run(2, {"builds": 4, "config": "human", "nprot": 6000})
+    for k in range(4):
+        builds = [r["builds"][k] for r in res]
+        assert all(b["ok"] for b in builds), [b.get("error") for b in builds]
+        _assert_whole_index([b["export"] for b in builds], oix, f"owner depth build {k}")
+        assert all(b["g_total"] == oix.n_total and b["g_unique"] == oix.n_unique for b in builds)
+    depth = [["bin_scatter" in b["stages"] for b in r["builds"]] for r in res]
+    assert not any(d[0] for d in depth) and all(d[1] for d in depth), depth
