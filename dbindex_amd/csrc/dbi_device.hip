@@ -3371,9 +3371,11 @@ __global__ void k_depth_starts(const uint32_t* __restrict__ offs, const uint32_t
 // chunk pairs over the bins (k_chunk_bounds' layout): chunk 2c = the bins
 // starting in [c*T, (c+1)*T), its last bin split off as chunk 2c+1 when the
 // two together exceed CHUNK_CAP (a bin above it is a big chunk of its own)
+// big_list (optional): the chunks above CHUNK_CAP listed here, so that the
+// big tier can run beside the chunk sort (which then skips them)
 __global__ void k_depth_chunks(const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t T, uint32_t nchunks,
                                uint32_t* __restrict__ chunk_lo, Counters* __restrict__ ctr,
-                               uint32_t* __restrict__ split_list) {
+                               uint32_t* __restrict__ split_list, uint32_t* __restrict__ big_list) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c > nchunks) return;
     const uint32_t n = (uint32_t)ctr->tail_n;
@@ -3395,15 +3397,19 @@ __global__ void k_depth_chunks(const uint32_t* __restrict__ bstart, uint32_t nb,
     if (s1 - s0 > (uint32_t)CHUNK_CAP && j1 > 0 && bstart[j1 - 1] > s0) split = bstart[j1 - 1];
     chunk_lo[2 * c + 1] = split;
     if (split != s1) split_list[atomicAdd(&ctr->n_split, 1u)] = c;  // (k_chunk_sort runs these first)
+    if (big_list) {
+        if (split - s0 > (uint32_t)CHUNK_CAP) big_list[atomicAdd(&ctr->n_big, 1u)] = 2 * c;
+        if (s1 - split > (uint32_t)CHUNK_CAP) big_list[atomicAdd(&ctr->n_big, 1u)] = 2 * c + 1;
+    }
 }
 
 hipError_t launch_depth_bounds(const uint32_t* d_offs, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
                                uint32_t* d_bstart, uint32_t T, uint32_t nchunks, uint32_t* d_chunk_lo,
-                               Counters* d_ctr, hipStream_t s, uint32_t* d_split_list) {
+                               Counters* d_ctr, hipStream_t s, uint32_t* d_split_list, uint32_t* d_big_list) {
     const uint32_t nb = 1u << (b1 + b2);
     DBI_LAUNCH(k_depth_starts, dim3((nb + 1 + 255) / 256), dim3(256), 0, s, d_offs, d_d1c, b1, b2, d_bstart, d_ctr);
     DBI_LAUNCH(k_depth_chunks, dim3((nchunks + 1 + 255) / 256), dim3(256), 0, s, d_bstart, nb, T, nchunks, d_chunk_lo,
-               d_ctr, d_split_list);
+               d_ctr, d_split_list, d_big_list);
     return hipGetLastError();
 }
 
@@ -4842,15 +4848,15 @@ template <int NT, int CAP, bool LOCAL>
 __device__ void chunk_sort_one(uint32_t c, const Rec* __restrict__ in, Rec* __restrict__ out, const BinMap& bm,
                                const uint32_t* __restrict__ chunk_lo, const RecLoc& rl, uint32_t* __restrict__ ucount,
                                uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, uint32_t ties,
-                               Counters* __restrict__ ctr, ChunkSmem<NT, CAP>& sm) {
+                               Counters* __restrict__ ctr, ChunkSmem<NT, CAP>& sm, bool listed = false) {
     const uint32_t a = chunk_lo[c];
     const uint32_t m = chunk_lo[c + 1] - a;
     if (m == 0) {
         if (threadIdx.x == 0) ucount[c] = 0;
         return;
     }
-    if (m > (uint32_t)CAP) {
-        if (threadIdx.x == 0) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
+    if (m > (uint32_t)CAP) {  // (listed: k_depth_chunks put it on big_list already)
+        if (threadIdx.x == 0 && !listed) big_list[atomicAdd(&ctr->n_big, 1u)] = c;
         return;
     }
     uint32_t h = 0;
@@ -4884,14 +4890,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const uint32_t* __restrict__ chunk_lo,
              const uint8_t* __restrict__ res, const uint32_t* __restrict__ poff, uint32_t* __restrict__ ucount,
              uint32_t* __restrict__ big_list, uint32_t* __restrict__ mid_list, uint32_t ties,
-             Counters* __restrict__ ctr, const uint32_t* __restrict__ split_list, uint32_t nfront) {
+             Counters* __restrict__ ctr, const uint32_t* __restrict__ split_list, uint32_t nfront, uint32_t listed) {
     __shared__ ChunkSmem<NT, CAP> sm;
     const bool front_ok = LOCAL && ctr->n_split <= nfront;  // block-uniform
     if (LOCAL && blockIdx.x < nfront) {  // a split pair's second chunk, or nothing
         if (!front_ok || blockIdx.x >= ctr->n_split) return;
         const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
         chunk_sort_one<NT, CAP, LOCAL>(2 * split_list[blockIdx.x] + 1, in, out, bm, chunk_lo, rl, ucount, big_list,
-                                       mid_list, ties, ctr, sm);
+                                       mid_list, ties, ctr, sm, listed != 0);
         return;
     }
     const uint32_t c = 2 * (blockIdx.x - (LOCAL ? nfront : 0u));
@@ -4910,12 +4916,13 @@ k_chunk_sort(const Rec* __restrict__ in, Rec* __restrict__ out, BinMap bm, const
         }
     }
     const RecLoc rl{res, poff, rec_width(ctr->max_plen)};
-    chunk_sort_one<NT, CAP, LOCAL>(c, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr, sm);
+    chunk_sort_one<NT, CAP, LOCAL>(c, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr, sm,
+                                   listed != 0);
     if constexpr (LOCAL) {
         if (!front_ok || chunk_lo[c + 2] == chunk_lo[c + 1]) {  // (empty: its unique count 0)
             __syncthreads();  // the LDS is the next chunk's
             chunk_sort_one<NT, CAP, LOCAL>(c + 1, in, out, bm, chunk_lo, rl, ucount, big_list, mid_list, ties, ctr,
-                                           sm);
+                                           sm, listed != 0);
         }
     }
 #ifdef DBI_CLOCK_CHUNKS
@@ -5039,17 +5046,18 @@ k_bin_sort_mid(const Rec* in, Rec* out, const uint32_t* __restrict__ chunk_lo,  
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                              uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s,
-                             bool local, const uint32_t* d_split_list, uint32_t nfront) {
+                             bool local, const uint32_t* d_split_list, uint32_t nfront, bool big_listed) {
     if (nchunks == 0) return hipSuccess;
     if (local && nfront && !d_split_list) return hipErrorInvalidValue;
+    if (big_listed && !local) return hipErrorInvalidValue;  // (only k_depth_chunks lists the big chunks)
     if (local)
         DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP, true>), dim3(nfront + nchunks), dim3(CHUNK_THREADS), 0, s,
                    d_in, d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr,
-                   d_split_list, nfront);
+                   d_split_list, nfront, big_listed ? 1u : 0u);
     else
         DBI_LAUNCH((k_chunk_sort<CHUNK_THREADS, CHUNK_CAP>), dim3(nchunks), dim3(CHUNK_THREADS), 0, s, d_in,
                    d_out, bm, d_chunk_lo, d_res, d_poff, d_ucount, d_big_list, d_mid_list, ties ? 1u : 0u, d_ctr,
-                   (const uint32_t*)nullptr, 0u);
+                   (const uint32_t*)nullptr, 0u, 0u);
     return hipGetLastError();
 }
 

@@ -319,6 +319,10 @@ struct dbi_handle {
     // owner merges on depth bins (dbi_shard.hip merge_body): the index the map samples is this
     // owner's own slice, left by its last merge (not a replica, not a single-device build)
     bool opt_owner_depth = true;          // option owner_depth=0: owner merges by the radix tail
+    bool opt_big_side = true;             // option big_side=0: depth tails' big tier after the mid tier, not beside the chunk sort
+    hipStream_t side = nullptr;           // the big tier's stream (sort_chunks), created on first use
+    hipEvent_t ev_side[2] = {nullptr, nullptr};  // its fork / join
+    hipStream_t stage_stream = nullptr;   // set while stages are enqueued on the side stream (graph timing events)
     uint64_t owner_serial = ~0ull;        // build_serial after this handle's last owner merge
     const void* owner_umass = nullptr;    // ... and its index buffers
     const void* owner_occ = nullptr;
@@ -414,8 +418,8 @@ inline int stage_begin(dbi_handle* h, const char* name, Bytes b) {
     if (h->timing && (h->timing_only.empty() || h->timing_only == name) &&
         ((h->evpool[st.eb] || hipEventCreate(&h->evpool[st.eb]) == hipSuccess) &&
          (h->evpool[st.ee] || hipEventCreate(&h->evpool[st.ee]) == hipSuccess))) {
-        if (h->capturing) {  // a graph: event-record nodes around the stage's kernels
-            st.launched = hipEventRecord(h->evpool[st.eb], h->stream) == hipSuccess;
+        if (h->capturing) {  // a graph: event-record nodes around the stage's kernels (on their stream)
+            st.launched = hipEventRecord(h->evpool[st.eb], h->stage_stream ? h->stage_stream : h->stream) == hipSuccess;
         } else {             // events in the kernels' own dispatch packets
             t_launch_ev = LaunchEvents{h->evpool[st.eb], h->evpool[st.ee]};
         }
@@ -426,7 +430,8 @@ inline int stage_begin(dbi_handle* h, const char* name, Bytes b) {
 inline void stage_end(dbi_handle* h, int i) {
     if (i >= 0 && h->capturing) {
         auto& st = h->stages[i];
-        if (st.launched) st.launched = hipEventRecord(h->evpool[st.ee], h->stream) == hipSuccess;
+        if (st.launched)
+            st.launched = hipEventRecord(h->evpool[st.ee], h->stage_stream ? h->stage_stream : h->stream) == hipSuccess;
     } else if (i >= 0) {
         // the first launch of the stage consumed `start`: otherwise nothing ran
         h->stages[i].launched = t_launch_ev.stop != nullptr && t_launch_ev.start == nullptr;

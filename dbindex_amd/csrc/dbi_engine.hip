@@ -178,7 +178,7 @@ int tail_buffers(dbi_handle* h, uint64_t n, uint64_t n_in, bool sparse) {
 }
 
 int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nchunks, uint64_t n,
-                const unsigned long long* d_n, bool est, bool local);
+                const unsigned long long* d_n, bool est, bool local, bool big_listed = false);
 
 int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, bool sparse,
                const unsigned long long* d_n_in, const unsigned long long* d_n, uint64_t n_est, bool est) {
@@ -240,18 +240,35 @@ int build_tail(dbi_handle* h, uint64_t n, double lo, double hi, uint64_t n_in, b
 // The chunk sort tiers, the unique counts' scan and finalize over the chunk
 // pairs in h->chunk_lo (src: records in bin order; the index from dst).
 // local: depth-bin chunks (sort_chunk LOCAL; chunk_sort_mid sorts dst in place).
+// the side stream and its fork / join events (created on first use)
+int ensure_side(dbi_handle* h) {
+    if (!h->side && hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) {
+        h->side = nullptr;
+        return set_error(DBI_E_HIP, "hipStreamCreate (side stream) failed");
+    }
+    for (auto& ev : h->ev_side)
+        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            ev = nullptr;
+            return set_error(DBI_E_HIP, "hipEventCreate (side stream) failed");
+        }
+    return 0;
+}
+
+// big_listed (depth-bin tails): k_depth_chunks listed the chunks above
+// CHUNK_CAP, so the big tier and the giant pass run on the side stream beside
+// the chunk sort and the mid tier (forked after the chunk bounds, joined
+// before the unique counts' scan): the big tier is ~420 blocks of one wave
+// each at SwissProt scale, its time the slowest chunk's, and beside the chunk
+// sort's ~30 k blocks it fills CUs instead of idling most of the chip.
 int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nchunks, uint64_t n,
-                const unsigned long long* d_n, bool est, bool local) {
+                const unsigned long long* d_n, bool est, bool local, bool big_listed) {
     hipStream_t s = h->stream;
     const uint32_t n32 = (uint32_t)n;
     const size_t seg_cap = giant_seg_cap(n);
     // depth bins: the split pairs' second chunks in front blocks (the previous
     // depth build's count + a margin; more, and the pairs' own blocks sort them)
     const uint32_t nfront = local && (est || d_n) && h->tail_local ? std::min(h->grid_split, nchunks) : 0u;
-    STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
-          launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                            h->mid_list.p, h->exact_dups, h->ctr.p, s, local, local ? h->split_list.p : nullptr,
-                            nfront));
+    // (the list grids below, from the previous build, are host values: computed first)
     // one block per listed bin (mid: every bin above the wave sort's reach) or
     // chunk (big: above CHUNK_CAP); the lists are filled on the device.  A device-sized tail
     // launches the previous build's list lengths plus a margin instead (a grid
@@ -273,17 +290,40 @@ int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nc
     // the giant-chunk pass (seven launches) only when the last build had giant
     // chunks: a giant chunk otherwise sets ERR_GRID and the build is redone
     const bool giants = !est || h->giants_seen;
+    int rc;
+    if (big_listed && (rc = ensure_side(h))) return rc;
+    // the big tier (and the giant pass) on stream bs: the side stream, forked here, or the build's own after the mid tier
+    auto big_tiers = [&](hipStream_t bs) -> int {
+        h->stage_stream = bs;
+        struct Reset {
+            dbi_handle* h;
+            ~Reset() { h->stage_stream = nullptr; }
+        } reset{h};
+        STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
+              launch_chunk_sort_big(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
+                                    giants ? h->giant_list.p : nullptr, max_big, h->split_above, h->exact_dups,
+                                    h->ctr.p, bs, h->big_split, local));
+        if (giants)
+            STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
+                  launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,
+                                      h->segs.p, seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, bs));
+        return 0;
+    };
+    if (big_listed) {
+        DBI_HIP(hipEventRecord(h->ev_side[0], s));
+        DBI_HIP(hipStreamWaitEvent(h->side, h->ev_side[0], 0));
+        if ((rc = big_tiers(h->side))) return rc;
+        DBI_HIP(hipEventRecord(h->ev_side[1], h->side));
+    }
+    STAGE(h, "chunk_sort", by(0, 32, 0, 0, 0),
+          launch_chunk_sort(src, dst, bm, h->chunk_lo.p, nchunks, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
+                            h->mid_list.p, h->exact_dups, h->ctr.p, s, local, local ? h->split_list.p : nullptr,
+                            nfront, big_listed));
     STAGE(h, "chunk_sort_mid", by(0, 0, 0, 0, 0),
           launch_chunk_sort_mid(local ? dst : src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p,
                                 h->mid_list.p, max_mid, h->ctr.p, s));
-    STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
-          launch_chunk_sort_big(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
-                                giants ? h->giant_list.p : nullptr, max_big, h->split_above, h->exact_dups, h->ctr.p,
-                                s, h->big_split, local));
-    if (giants)
-        STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
-              launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,
-                                  h->segs.p, seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, s));
+    if (big_listed) DBI_HIP(hipStreamWaitEvent(s, h->ev_side[1], 0));  // join
+    else if ((rc = big_tiers(s))) return rc;
     // unique offsets per chunk
     STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
           launch_scan_u32(h->ucount.p, h->ucount.p, 2 * (uint64_t)nchunks, h->scan_tmp.p, h->scan_tmp.cap,
@@ -598,11 +638,13 @@ int depth_tail(dbi_handle* h, const DepthPlan& pl, const BinMap& sub, uint64_t c
     STAGE(h, "bin_scatter", by(0, 33, 0, 0, 0),
           launch_part_scatter(h->recR.p, h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2,
                               pl.max_chunks, h->hist2.p, h->recA.p, h->ctr.p, s));
+    const bool big_side = h->opt_big_side;  // the big tier beside the chunk sort (sort_chunks)
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
           launch_depth_bounds(h->hist2.p, h->d1c.p, pl.b1, pl.b2, h->bstart.p, T, nchunks, h->chunk_lo.p, h->ctr.p, s,
-                              h->split_list.p));
+                              h->split_list.p, big_side ? h->big_list.p : nullptr));
     int rc;
-    if ((rc = sort_chunks(h, h->recA.p, h->recB.p, sub, nchunks, cap, &h->ctr.p->tail_n, est, true))) return rc;
+    if ((rc = sort_chunks(h, h->recA.p, h->recB.p, sub, nchunks, cap, &h->ctr.p->tail_n, est, true, big_side)))
+        return rc;
     h->stats.n_bins = pl.nbins;
     return 0;
 }
@@ -1540,6 +1582,9 @@ void dbi_close(dbi_handle* h) {
         (void)hipHostUnregister(h->up_host);
         std::free(h->up_host);
     }
+    for (auto& ev : h->ev_side)
+        if (ev) (void)hipEventDestroy(ev);
+    if (h->side) (void)hipStreamDestroy(h->side);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1972,6 +2017,7 @@ int dbi_set_option(dbi_handle* h, const char* name, int64_t value) {
     else if (n == "semi_bounded") h->use_semi_bounded = on;
     else if (n == "depth_bins") h->use_depth = on;
     else if (n == "owner_depth") h->opt_owner_depth = on;
+    else if (n == "big_side") h->opt_big_side = on;
     else if (n == "semi_part") h->use_semi_part = on;
     else if (n == "part_stage") h->use_part_stage = on;
     else if (n == "depth_map_reuse") h->opt_depth_map_reuse = on;

@@ -319,10 +319,13 @@ hipError_t launch_part_scatter(const Rec* d_recs, const uint8_t* d_dig, const ui
 // chunk pairs over the bin-ordered records from the pass-2 offsets: bin
 // starts (bstart: nbins + 1), then chunk_lo[2c] = first bin start at or after
 // c*T, chunk_lo[2c+1] = the last bin's start when the chunk exceeds CHUNK_CAP
-// (those pairs c listed in d_split_list[0, ctr->n_split))
+// (those pairs c listed in d_split_list[0, ctr->n_split)); d_big_list: the
+// chunks above CHUNK_CAP listed too (ctr->n_big), for a big tier launched
+// beside the chunk sort (launch_chunk_sort big_listed)
 hipError_t launch_depth_bounds(const uint32_t* d_offs, const uint32_t* d_d1c, uint32_t b1, uint32_t b2,
                                uint32_t* d_bstart, uint32_t T, uint32_t nchunks, uint32_t* d_chunk_lo,
-                               Counters* d_ctr, hipStream_t s, uint32_t* d_split_list);
+                               Counters* d_ctr, hipStream_t s, uint32_t* d_split_list,
+                               uint32_t* d_big_list = nullptr);
 // semi-specific enzymes (no mandatory residues, no windows): one walk per start
 // into slots bounded by the bit maps (REC_SENTINEL in the unused ones)
 hipError_t launch_digest_semi_bounded(const DevParams& dp, const double* d_mass_tab, const uint8_t* d_flags,
@@ -456,7 +459,8 @@ hipError_t launch_chunk_bounds(const Rec* d_recs, uint32_t n, const BinMap& bm, 
 hipError_t launch_chunk_sort(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                              uint32_t nchunks, const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                              uint32_t* d_big_list, uint32_t* d_mid_list, bool ties, Counters* d_ctr, hipStream_t s,
-                             bool local = false, const uint32_t* d_split_list = nullptr, uint32_t nfront = 0);
+                             bool local = false, const uint32_t* d_split_list = nullptr, uint32_t nfront = 0,
+                             bool big_listed = false);
 hipError_t launch_chunk_sort_mid(const Rec* d_in, Rec* d_out, const BinMap& bm, const uint32_t* d_chunk_lo,
                                  const uint8_t* d_res, const uint32_t* d_poff, uint32_t* d_ucount,
                                  const uint32_t* d_mid_list, uint32_t max_blocks, Counters* d_ctr, hipStream_t s);

@@ -269,7 +269,8 @@ int dbi_device_view(dbi_handle* h, dbi_device_index* out);
  * 1: the big chunk tier's two size classes); "bin_bits_max", "split_above",
  * "chunk_target" (0: by size); "shard_full_path", "shard_dev_digest",
  * "shard_resample" (0 / 1, dbi_build_sharded); "owner_depth" (0 / 1: warm
- * owner merges on depth bins, else the radix tail); "part_stage" (0 / 1: the
+ * owner merges on depth bins, else the radix tail); "big_side" (0 / 1: a
+ * depth-bin tail's big chunk tier on a second stream beside the chunk sort); "part_stage" (0 / 1: the
  * partitioning digest keeps a tile's records in LDS, 1, or writes them
  * through HBM slots, 0).  Test-build library only
  * (libdbindex_hip_hooks.so, -DDBI_TEST_HOOKS; the product library answers

@@ -1,9 +1,11 @@
-# one-off GPU session script (changes per call): TrEMBL bucket-count A/B of hist_advance's lookahead
+# one-off GPU session script (changes per call): the whole GPU suite + A/B of the depth tails' big tier beside the chunk sort
 set -o pipefail
-O=gpurun_out/r06tl; mkdir -p $O
-A="--config trembl --trembl-proteins 10000000 --steps 4 --warmup 1 --no-cold --queries 0"
-for r in 1 2; do
-  timeout -k 10 300 python bench.py $A > $O/cur$r.log 2>&1 || exit 1
-  DBI_LIB_PATH=tools/exp/look2.so timeout -k 10 300 python bench.py $A > $O/look2_$r.log 2>&1 || exit 1
+O=gpurun_out/r06bs3; mkdir -p $O
+PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread"
+timeout -k 10 1000 $PT tests -m gpu > $O/t1.log 2>&1; rc=$?; tail -3 $O/t1.log; [ $rc -eq 0 ] || exit $rc
+A="--steps 20 --warmup 5 --no-cpu-baseline --no-cold --queries 0"
+for r in 1 2 3; do
+  timeout -k 10 300 python bench.py $A --option big_side=0 > $O/off$r.log 2>&1 || exit 1
+  timeout -k 10 300 python bench.py $A > $O/on$r.log 2>&1 || exit 1
 done
-for f in $O/*.log; do echo "$f $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],2), d["cpu_baseline"].get("sample_bucket_parity"))')"; done
+python3 tools/ab_table.py $O off1 on1 off2 on2 off3 on3
