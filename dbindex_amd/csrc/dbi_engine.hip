@@ -638,7 +638,10 @@ int depth_tail(dbi_handle* h, const DepthPlan& pl, const BinMap& sub, uint64_t c
     STAGE(h, "bin_scatter", by(0, 33, 0, 0, 0),
           launch_part_scatter(h->recR.p, h->rdig.p, h->rcur.p, pl.cap, h->desc.p, h->d1c.p, pl.b1, pl.b2,
                               pl.max_chunks, h->hist2.p, h->recA.p, h->ctr.p, s));
-    const bool big_side = h->opt_big_side;  // the big tier beside the chunk sort (sort_chunks)
+    // the big tier beside the chunk sort (sort_chunks); not when every stage is
+    // timed: the per-stage breakdown's event spans would overlap (the big
+    // tier's span then covers the chunk sort's), so such builds serialise
+    const bool big_side = h->opt_big_side && !(h->timing && h->timing_only.empty());
     STAGE(h, "chunk_bounds", by(0, 0, 0, 0, 0),
           launch_depth_bounds(h->hist2.p, h->d1c.p, pl.b1, pl.b2, h->bstart.p, T, nchunks, h->chunk_lo.p, h->ctr.p, s,
                               h->split_list.p, big_side ? h->big_list.p : nullptr));
