@@ -291,7 +291,9 @@ int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nc
     // chunks: a giant chunk otherwise sets ERR_GRID and the build is redone
     const bool giants = !est || h->giants_seen;
     int rc;
-    if (big_listed && (rc = ensure_side(h))) return rc;
+    // (a big tier that is not launched -- its list was empty last build -- needs no fork)
+    const bool fork = big_listed && max_big > 0;
+    if (fork && (rc = ensure_side(h))) return rc;
     // the big tier (and the giant pass) on stream bs: the side stream, forked here, or the build's own after the mid tier
     auto big_tiers = [&](hipStream_t bs) -> int {
         h->stage_stream = bs;
@@ -309,7 +311,7 @@ int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nc
                                       h->segs.p, seg_cap, h->ws_key.p, h->ws_k2.p, h->ctr.p, bs));
         return 0;
     };
-    if (big_listed) {
+    if (fork) {
         DBI_HIP(hipEventRecord(h->ev_side[0], s));
         DBI_HIP(hipStreamWaitEvent(h->side, h->ev_side[0], 0));
         if ((rc = big_tiers(h->side))) return rc;
@@ -322,7 +324,7 @@ int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nc
     STAGE(h, "chunk_sort_mid", by(0, 0, 0, 0, 0),
           launch_chunk_sort_mid(local ? dst : src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p,
                                 h->mid_list.p, max_mid, h->ctr.p, s));
-    if (big_listed) DBI_HIP(hipStreamWaitEvent(s, h->ev_side[1], 0));  // join
+    if (fork) DBI_HIP(hipStreamWaitEvent(s, h->ev_side[1], 0));  // join
     else if ((rc = big_tiers(s))) return rc;
     // unique offsets per chunk
     STAGE(h, "ucount_scan", by(0, 0, 0, 0, 0),
