@@ -294,6 +294,11 @@ int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nc
     // (a big tier that is not launched -- its list was empty last build -- needs no fork)
     const bool fork = big_listed && max_big > 0;
     if (fork && (rc = ensure_side(h))) return rc;
+    // beside the chunk sort the big tier takes its two size classes whatever
+    // the list's length (the 512-thread, half-LDS blocks of the small class
+    // interleave with the chunk sort's: SwissProt 3.40-3.43 -> 3.35-3.36 ms,
+    // `profiles/r06bsp_big_split_ab.txt`); option big_split overrides
+    const int big_split = h->big_split >= 0 ? h->big_split : fork ? 1 : -1;
     // the big tier (and the giant pass) on stream bs: the side stream, forked here, or the build's own after the mid tier
     auto big_tiers = [&](hipStream_t bs) -> int {
         h->stage_stream = bs;
@@ -304,7 +309,7 @@ int sort_chunks(dbi_handle* h, Rec* src, Rec* dst, const BinMap& bm, uint32_t nc
         STAGE(h, "chunk_sort_big", by(0, 0, 0, 0, 0),
               launch_chunk_sort_big(src, dst, bm, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->big_list.p,
                                     giants ? h->giant_list.p : nullptr, max_big, h->split_above, h->exact_dups,
-                                    h->ctr.p, bs, h->big_split, local));
+                                    h->ctr.p, bs, big_split, local));
         if (giants)
             STAGE(h, "chunk_sort_giant", by(0, 0, 0, 0, 0),
                   launch_giant_chunks(src, dst, h->chunk_lo.p, h->d_res, h->d_poff, h->ucount.p, h->giant_list.p,

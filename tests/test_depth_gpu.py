@@ -90,10 +90,14 @@ def test_depth_map_of_another_proteome(Engine):
         assert_queries_equal(eng, oa, m, t, "queries after the map changes")
 
 
-def test_depth_equal_mass_spikes(Engine):
+@pytest.mark.parametrize("opts", [{}, {"big_split": 1}, {"big_side": 0}, {"big_side": 0, "big_split": 1}],
+                         ids=["side", "side_split", "inline", "inline_split"])
+def test_depth_equal_mass_spikes(Engine, opts):
     """Equal-mass spikes (a protein block rewritten as GAAAAAAK repeats) land
     whole in one depth bin: a chunk far above the LDS capacity, through the
-    big / giant tiers from the bin-ordered records, warm and replayed."""
+    big / giant tiers from the bin-ordered records, warm and replayed -- the
+    big tier beside the chunk sort (option big_side, default) or in line,
+    in one size class or two (big_split)."""
     a = fasta.config("human").slice(0, 6000)
     spike = a.residues.copy()
     e = int(a.offsets[400])
@@ -101,11 +105,11 @@ def test_depth_equal_mass_spikes(Engine):
     c = fasta.PackedProteins(spike, a.offsets.copy(), a.defs)
     cp = DBIndexSearchParams.trypsin(2).to_c()
     oc = cref.Index(cp, c.residues, c.offsets)
-    with Engine(cp) as eng:
+    with Engine(cp, options=opts) as eng:
         eng.set_timing(False)
         for k in range(5):
             eng.build(c)
-            assert_index_equal(eng, oc, f"spiked build {k}")
+            assert_index_equal(eng, oc, f"spiked build {k} {opts}")
 
 
 def test_options_and_cold_builds(Engine):
