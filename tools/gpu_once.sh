@@ -1,11 +1,10 @@
-# one-off GPU session script (changes per call): tests + A/B of the side big tier (two size classes) against in line
+# one-off GPU session script (changes per call): A/B of the depth chunk target with the big tier beside the chunk sort
 set -o pipefail
-O=gpurun_out/r06bs5; mkdir -p $O
-PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread"
-timeout -k 10 900 $PT tests/test_depth_gpu.py tests/test_graph_gpu.py tests/test_scale_gpu.py tests/test_gpu_parity.py -k "not trembl and not semi" > $O/t1.log 2>&1; rc=$?; tail -2 $O/t1.log; [ $rc -eq 0 ] || exit $rc
+O=gpurun_out/r06ct; mkdir -p $O
 A="--steps 20 --warmup 5 --no-cpu-baseline --no-cold --queries 0"
-for r in 1 2 3; do
-  timeout -k 10 300 python bench.py $A --option big_side=0 > $O/off$r.log 2>&1 || exit 1
-  timeout -k 10 300 python bench.py $A > $O/on$r.log 2>&1 || exit 1
+for r in 1 2; do
+  timeout -k 10 300 python bench.py $A > $O/d$r.log 2>&1 || exit 1
+  timeout -k 10 300 python bench.py $A --option chunk_target=1536 > $O/t1536_$r.log 2>&1 || exit 1
+  timeout -k 10 300 python bench.py $A --option chunk_target=1664 > $O/t1664_$r.log 2>&1 || exit 1
 done
-python3 tools/ab_table.py $O off1 on1 off2 on2 off3 on3
+python3 tools/ab_table.py $O d1 t1536_1 t1664_1 d2 t1536_2 t1664_2
